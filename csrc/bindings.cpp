@@ -1,0 +1,76 @@
+// Python bindings for the distlearn MI355X native library (pybind11).
+// Module: torch_distlearn_amd._C
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "comm/communicator.h"
+#include "dl_ops.h"
+#include "runtime/loader.h"
+
+namespace py = pybind11;
+using namespace dl;
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "distlearn MI355X (gfx950) native kernels, RCCL communicator and data runtime";
+
+  // ---- flat bucket kernels --------------------------------------------------
+  m.def("sgd_update", &sgd_update, py::arg("p"), py::arg("g"), py::arg("mom"), py::arg("p16"), py::arg("slot"),
+        py::arg("lr"), py::arg("momentum"), py::arg("wd"), py::arg("n"), py::arg("stream"));
+  m.def("scale_by_count", &scale_by_count);
+  m.def("elastic_step", &elastic_step);
+  m.def("add_inplace", &add_inplace);
+  m.def("fill_f32", &fill_f32);
+  m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("multi_copy", &multi_copy);
+  m.def("confusion_update", &confusion_update);
+  m.def("gather_normalize", &gather_normalize);
+
+  // ---- RCCL communicator ------------------------------------------------------
+  m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
+  m.def("rccl_version", &rccl_version);
+  py::class_<RcclCommunicator>(m, "RcclCommunicator")
+      .def(py::init([](py::bytes uid, int rank, int world, int device) {
+             return new RcclCommunicator(std::string(uid), rank, world, device);
+           }),
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("rank", &RcclCommunicator::rank)
+      .def_property_readonly("world", &RcclCommunicator::world)
+      .def_property_readonly("device", &RcclCommunicator::device)
+      .def("all_reduce", &RcclCommunicator::all_reduce)
+      .def("broadcast", &RcclCommunicator::broadcast)
+      .def("reduce", &RcclCommunicator::reduce)
+      .def("reduce_scatter", &RcclCommunicator::reduce_scatter)
+      .def("all_gather", &RcclCommunicator::all_gather)
+      .def("send", &RcclCommunicator::send)
+      .def("recv", &RcclCommunicator::recv)
+      .def("group_start", &RcclCommunicator::group_start)
+      .def("group_end", &RcclCommunicator::group_end)
+      .def("async_error", &RcclCommunicator::async_error)
+      .def("destroy", &RcclCommunicator::destroy)
+      .def("abort", &RcclCommunicator::abort);
+
+  // ---- data runtime -------------------------------------------------------------
+  py::class_<PartitionSampler>(m, "PartitionSampler")
+      .def(py::init<int64_t, std::vector<int64_t>, int, int, int, int, uint64_t>(), py::arg("n"), py::arg("labels"),
+           py::arg("num_classes"), py::arg("partition"), py::arg("partitions"), py::arg("kind"), py::arg("seed"))
+      .def("size", &PartitionSampler::size)
+      .def("num_batches", &PartitionSampler::num_batches)
+      .def("reset_epoch", &PartitionSampler::reset_epoch)
+      .def("next_batch", [](PartitionSampler& s, uintptr_t out, int64_t batch) {
+        return s.next_batch(reinterpret_cast<int64_t*>(out), batch);
+      });
+  py::class_<BatchAssembler>(m, "BatchAssembler")
+      .def(py::init([](uintptr_t images, uintptr_t labels, int64_t n, int64_t sample_bytes, std::vector<int64_t> lbl,
+                       int num_classes, int partition, int partitions, int kind, uint64_t seed, int64_t batch,
+                       int threads, int depth) {
+        auto* s = new PartitionSampler(n, std::move(lbl), num_classes, partition, partitions, kind, seed);
+        return new BatchAssembler(images, labels, n, sample_bytes, s, batch, threads, depth);
+      }))
+      .def("next", &BatchAssembler::next, py::call_guard<py::gil_scoped_release>())
+      .def("release", &BatchAssembler::release)
+      .def("slot_images", &BatchAssembler::slot_images)
+      .def("slot_labels", &BatchAssembler::slot_labels)
+      .def("slot_valid", &BatchAssembler::slot_valid)
+      .def("num_batches", &BatchAssembler::num_batches)
+      .def("reset_epoch", &BatchAssembler::reset_epoch);
+}

@@ -1,0 +1,126 @@
+"""Build the native library ``torch_distlearn_amd/_C*.so`` for gfx950 (MI355X).
+
+Every ``csrc/**/*.hip`` kernel file and the C++ runtime/bindings are compiled
+with ``hipcc --offload-arch=gfx950`` into objects (in parallel, incrementally)
+and linked into one in-tree Python extension that also links RCCL.  Nothing is
+JIT-compiled at import time and nothing is installed into site-packages: the
+built ``.so`` lives next to the Python package so it travels with the repo to
+the GPU box.
+
+Usage:  python csrc/build.py [--force] [-j N] [--verbose]
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+import sysconfig
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+PKG = os.path.join(ROOT, "torch_distlearn_amd")
+BUILD = os.path.join(ROOT, "build", "native")
+ARCH = os.environ.get("DISTLEARN_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.path.join(ROCM, "bin", "hipcc")
+
+
+def ext_path() -> str:
+    return os.path.join(PKG, "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _sources():
+    srcs = []
+    for d, _, files in os.walk(CSRC):
+        for f in sorted(files):
+            if f.endswith((".hip", ".cpp")):
+                srcs.append(os.path.join(d, f))
+    return sorted(srcs)
+
+
+def _headers():
+    hs = []
+    for d, _, files in os.walk(CSRC):
+        for f in files:
+            if f.endswith((".h", ".hpp", ".inc")):
+                hs.append(os.path.join(d, f))
+    return hs
+
+
+def _includes():
+    import pybind11
+
+    return [
+        "-I" + os.path.join(CSRC, "include"),
+        "-I" + CSRC,
+        "-I" + pybind11.get_include(),
+        "-I" + sysconfig.get_paths()["include"],
+    ]
+
+
+COMMON = ["-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", "-Wno-unused-command-line-argument"]
+
+
+def _obj_for(src: str) -> str:
+    rel = os.path.relpath(src, CSRC).replace(os.sep, "__")
+    return os.path.join(BUILD, rel + ".o")
+
+
+def _compile(src: str, force: bool, verbose: bool, newest_header: float):
+    obj = _obj_for(src)
+    if (not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), newest_header)):
+        return obj, 0.0, False
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-c", src, "-o", obj] + COMMON + _includes()
+    if src.endswith(".cpp") and "bindings" in src:
+        cmd += ["-fvisibility=hidden"]
+    t0 = time.time()
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+    return obj, time.time() - t0, True
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    srcs = _sources()
+    hdr = max([os.path.getmtime(h) for h in _headers()] + [0.0])
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    objs = []
+    rebuilt = False
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        futs = {ex.submit(_compile, s, force, verbose, hdr): s for s in srcs}
+        for f in cf.as_completed(futs):
+            obj, dt, did = f.result()
+            objs.append(obj)
+            rebuilt |= did
+            if did:
+                print(f"[distlearn build] {os.path.relpath(futs[f], ROOT)}  {dt:.1f}s", flush=True)
+    out = ext_path()
+    if rebuilt or force or not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + sorted(objs) + [
+            "-L" + os.path.join(ROCM, "lib"), "-lrccl"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        print(f"[distlearn build] linked {os.path.relpath(out, ROOT)}", flush=True)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=None)
+    ap.add_argument("--verbose", action="store_true")
+    a = ap.parse_args()
+    build(a.force, a.j, a.verbose)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

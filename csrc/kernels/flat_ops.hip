@@ -1,0 +1,248 @@
+// Flat-bucket optimizer / elastic-averaging / participation kernels (gfx950).
+//
+// These are the per-step hot path of the reference's algorithms, done over ONE
+// persistent flat fp32 buffer instead of a walkTable loop of per-tensor ops:
+//   * K3  grad:mul(1/n)                      lua/AllReduceSGD.lua:23-27
+//   * K5  params:add(-lr, grads)             examples/cifar10.lua:187-191
+//   * K8  delta=alpha(p-c); p-=delta         lua/AllReduceEA.lua:35-39
+//   * K9  center += sum(delta)               lua/AllReduceEA.lua:43-45
+//   * K10 fused drain step                   lua/AllReduceEA.lua:60-68
+//   * K4/K11 fill / copy                     lua/AllReduceSGD.lua:37,44
+// All kernels are grid-stride streaming kernels with 16-byte (float4) accesses;
+// the participation count `n` is read on the device from the all-reduced slot,
+// so the normalisation needs no host synchronisation (graph-capturable).
+#include "dl_common.h"
+
+namespace dl {
+
+// ---------------------------------------------------------------------------
+// helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float participation_scale(const float* slot) {
+  if (slot == nullptr) return 1.0f;
+  float n = *slot;
+  return n > 1.0f ? 1.0f / n : 1.0f;  // reference: only divide when n > 1
+}
+
+// ---------------------------------------------------------------------------
+// SGD (+ optional momentum / weight decay), fused with 1/n normalisation and
+// the bf16 shadow-weight refresh used by the bf16 compute path.
+// ---------------------------------------------------------------------------
+template <bool kMomentum, bool kShadow>
+__global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                  float* __restrict__ mom, bf16_t* __restrict__ p16,
+                                                  const float* __restrict__ slot, float lr, float momentum,
+                                                  float wd, int64_t n4) {
+  const float s = participation_scale(slot);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pv = reinterpret_cast<float4*>(p)[i];
+    float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float gx = gv.x * s + wd * pv.x, gy = gv.y * s + wd * pv.y;
+    float gz = gv.z * s + wd * pv.z, gw = gv.w * s + wd * pv.w;
+    if constexpr (kMomentum) {
+      float4 mv = reinterpret_cast<float4*>(mom)[i];
+      mv.x = momentum * mv.x + gx; mv.y = momentum * mv.y + gy;
+      mv.z = momentum * mv.z + gz; mv.w = momentum * mv.w + gw;
+      reinterpret_cast<float4*>(mom)[i] = mv;
+      gx = mv.x; gy = mv.y; gz = mv.z; gw = mv.w;
+    }
+    pv.x -= lr * gx; pv.y -= lr * gy; pv.z -= lr * gz; pv.w -= lr * gw;
+    reinterpret_cast<float4*>(p)[i] = pv;
+    if constexpr (kShadow) {
+      uint2 packed;
+      packed.x = pack_bf16x2(pv.x, pv.y);
+      packed.y = pack_bf16x2(pv.z, pv.w);
+      reinterpret_cast<uint2*>(p16)[i] = packed;
+    }
+  }
+}
+
+// x *= 1/n (n read from the all-reduced participation slot)
+__global__ void __launch_bounds__(256) scale_by_count_kernel(float* __restrict__ x, const float* __restrict__ slot,
+                                                             int64_t n4) {
+  const float s = participation_scale(slot);
+  if (s == 1.0f) return;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 v = reinterpret_cast<float4*>(x)[i];
+    v.x *= s; v.y *= s; v.z *= s; v.w *= s;
+    reinterpret_cast<float4*>(x)[i] = v;
+  }
+}
+
+// Elastic step. If `pending` is non-null, first c += pending (the previous
+// round's all-reduced sum of deltas: K9 fused into K8 = K10).
+//   delta = alpha * (p - c);  p -= delta;  out = delta
+template <bool kPending, bool kShadow>
+__global__ void __launch_bounds__(256) elastic_kernel(float* __restrict__ p, float* __restrict__ c,
+                                                      const float* __restrict__ pending, float* __restrict__ out,
+                                                      bf16_t* __restrict__ p16, float alpha, int64_t n4) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pv = reinterpret_cast<float4*>(p)[i];
+    float4 cv = reinterpret_cast<float4*>(c)[i];
+    if constexpr (kPending) {
+      float4 dv = reinterpret_cast<const float4*>(pending)[i];
+      cv.x += dv.x; cv.y += dv.y; cv.z += dv.z; cv.w += dv.w;
+      reinterpret_cast<float4*>(c)[i] = cv;
+    }
+    float4 d;
+    d.x = alpha * (pv.x - cv.x); d.y = alpha * (pv.y - cv.y);
+    d.z = alpha * (pv.z - cv.z); d.w = alpha * (pv.w - cv.w);
+    pv.x -= d.x; pv.y -= d.y; pv.z -= d.z; pv.w -= d.w;
+    reinterpret_cast<float4*>(p)[i] = pv;
+    reinterpret_cast<float4*>(out)[i] = d;
+    if constexpr (kShadow) {
+      uint2 packed;
+      packed.x = pack_bf16x2(pv.x, pv.y);
+      packed.y = pack_bf16x2(pv.z, pv.w);
+      reinterpret_cast<uint2*>(p16)[i] = packed;
+    }
+  }
+}
+
+// y += x
+__global__ void __launch_bounds__(256) add_inplace_kernel(float* __restrict__ y, const float* __restrict__ x, int64_t n4) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 a = reinterpret_cast<float4*>(y)[i];
+    float4 b = reinterpret_cast<const float4*>(x)[i];
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    reinterpret_cast<float4*>(y)[i] = a;
+  }
+}
+
+// x[0:n] = v, and x[slot_index] = slot_value (slot_index < 0: none)
+__global__ void __launch_bounds__(256) fill_kernel(float* __restrict__ x, float v, int64_t n4, int64_t slot_index,
+                                                   float slot_value) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const float4 fv = make_float4(v, v, v, v);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 w = fv;
+    if (slot_index >= 0 && (slot_index >> 2) == i) {
+      switch (slot_index & 3) {
+        case 0: w.x = slot_value; break;
+        case 1: w.y = slot_value; break;
+        case 2: w.z = slot_value; break;
+        default: w.w = slot_value; break;
+      }
+    }
+    reinterpret_cast<float4*>(x)[i] = w;
+  }
+}
+
+__global__ void __launch_bounds__(256) cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
+                                                            int64_t n4) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 v = reinterpret_cast<const float4*>(x)[i];
+    uint2 packed;
+    packed.x = pack_bf16x2(v.x, v.y);
+    packed.y = pack_bf16x2(v.z, v.w);
+    reinterpret_cast<uint2*>(y)[i] = packed;
+  }
+}
+
+// Multi-tensor pack/unpack (K1): copy a list of (src, dst, bytes) segments in
+// one launch. Each segment is split into 16-byte chunks; blockIdx.y = segment.
+struct CopySeg {
+  const char* src;
+  char* dst;
+  int64_t bytes;
+};
+
+__global__ void __launch_bounds__(256) multi_copy_kernel(const CopySeg* __restrict__ segs) {
+  const CopySeg sg = segs[blockIdx.y];
+  const int64_t n16 = sg.bytes >> 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t i = t0; i < n16; i += stride)
+    reinterpret_cast<uint4*>(sg.dst)[i] = reinterpret_cast<const uint4*>(sg.src)[i];
+  // byte tail (segments are normally 16-B multiples; kept for generality)
+  for (int64_t b = (n16 << 4) + t0; b < sg.bytes; b += stride) sg.dst[b] = sg.src[b];
+}
+
+// ---------------------------------------------------------------------------
+// Host launchers (C ABI-ish, raw pointers + stream handle)
+// ---------------------------------------------------------------------------
+static void check_vec4(int64_t n, const char* what) {
+  if (n % 4 != 0) throw std::runtime_error(std::string(what) + ": element count must be a multiple of 4");
+}
+
+void sgd_update(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, uintptr_t slot, float lr, float momentum,
+                float wd, int64_t n, uintptr_t stream) {
+  check_vec4(n, "sgd_update");
+  const int64_t n4 = n / 4;
+  if (n4 == 0) return;
+  dim3 grid(stream_grid(n4)), block(256);
+  auto s = as_stream(stream);
+  float* P = (float*)p; const float* G = (const float*)g; float* M = (float*)mom; bf16_t* P16 = (bf16_t*)p16;
+  const float* S = (const float*)slot;
+  if (mom && p16) sgd_kernel<true, true><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4);
+  else if (mom) sgd_kernel<true, false><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4);
+  else if (p16) sgd_kernel<false, true><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4);
+  else sgd_kernel<false, false><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+void scale_by_count(uintptr_t x, uintptr_t slot, int64_t n, uintptr_t stream) {
+  check_vec4(n, "scale_by_count");
+  const int64_t n4 = n / 4;
+  if (n4 == 0) return;
+  scale_by_count_kernel<<<stream_grid(n4), 256, 0, as_stream(stream)>>>((float*)x, (const float*)slot, n4);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+void elastic_step(uintptr_t p, uintptr_t c, uintptr_t pending, uintptr_t out, uintptr_t p16, float alpha, int64_t n,
+                  uintptr_t stream) {
+  check_vec4(n, "elastic_step");
+  const int64_t n4 = n / 4;
+  if (n4 == 0) return;
+  dim3 grid(stream_grid(n4)), block(256);
+  auto s = as_stream(stream);
+  float* P = (float*)p; float* C = (float*)c; const float* D = (const float*)pending; float* O = (float*)out;
+  bf16_t* P16 = (bf16_t*)p16;
+  if (pending && p16) elastic_kernel<true, true><<<grid, block, 0, s>>>(P, C, D, O, P16, alpha, n4);
+  else if (pending) elastic_kernel<true, false><<<grid, block, 0, s>>>(P, C, D, O, P16, alpha, n4);
+  else if (p16) elastic_kernel<false, true><<<grid, block, 0, s>>>(P, C, D, O, P16, alpha, n4);
+  else elastic_kernel<false, false><<<grid, block, 0, s>>>(P, C, D, O, P16, alpha, n4);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+void add_inplace(uintptr_t y, uintptr_t x, int64_t n, uintptr_t stream) {
+  check_vec4(n, "add_inplace");
+  const int64_t n4 = n / 4;
+  if (n4 == 0) return;
+  add_inplace_kernel<<<stream_grid(n4), 256, 0, as_stream(stream)>>>((float*)y, (const float*)x, n4);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+void fill_f32(uintptr_t x, float v, int64_t n, int64_t slot_index, float slot_value, uintptr_t stream) {
+  check_vec4(n, "fill_f32");
+  const int64_t n4 = n / 4;
+  if (n4 == 0) return;
+  fill_kernel<<<stream_grid(n4), 256, 0, as_stream(stream)>>>((float*)x, v, n4, slot_index, slot_value);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+void cast_f32_bf16(uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream) {
+  check_vec4(n, "cast_f32_bf16");
+  const int64_t n4 = n / 4;
+  if (n4 == 0) return;
+  cast_f32_bf16_kernel<<<stream_grid(n4), 256, 0, as_stream(stream)>>>((const float*)x, (bf16_t*)y, n4);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+// segs: device pointer to `nseg` CopySeg records; max_bytes: largest segment
+void multi_copy(uintptr_t segs, int nseg, int64_t max_bytes, uintptr_t stream) {
+  if (nseg <= 0) return;
+  int64_t n16 = (max_bytes + 15) / 16;
+  int gx = stream_grid(n16);
+  if (gx > 64) gx = 64;  // segments run side by side in blockIdx.y
+  dim3 grid(gx, nseg);
+  multi_copy_kernel<<<grid, 256, 0, as_stream(stream)>>>((const CopySeg*)segs);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dl

@@ -1,0 +1,226 @@
+"""Flat persistent parameter/gradient storage and the fused flat-bucket ops.
+
+``FlatParams`` is the MI355X analogue of torch-autograd's ``stableGradients``
+(examples/mnist.lua:91-94: "Keep the gradient tensors stable so we can use
+CUDA IPC"): every parameter and gradient of a table/module becomes a *view*
+into one contiguous, 256-byte aligned buffer, so
+
+  * a collective over all gradients is one (or a few, bucketed) RCCL calls on
+    the flat buffer -- no per-tensor walkTable serialisation;
+  * the reference's per-tensor update loops (K3/K5/K8/K9/K10) become single
+    fused HIP kernels over the flat buffer (csrc/kernels/flat_ops.hip);
+  * tensor objects never move, which also fixes the reference hazard where
+    AllReduceEA caches tensor objects that the example then replaces
+    (lua/AllReduceEA.lua:19 vs examples/mnist-ea.lua:103-107).
+
+The grad buffer reserves a 64-element header whose element 0 is the
+*participation slot*: each node writes 1 (normal step) or 0 (draining), and
+the all-reduced value is the reference's ``n`` (lua/AllReduceSGD.lua:20-27),
+delivered by the same collective at no extra latency.
+"""
+from __future__ import annotations
+
+from typing import Any, List, Sequence, Tuple
+
+import torch
+
+from .._native import native, stream_handle
+from ..utils.walk import walk_table
+
+ALIGN = 64        # elements; 256 B for fp32 -> every view is 16-B aligned for float4 kernels
+HEADER = 64       # reserved elements at the start of the grad/delta buffers
+SLOT = 0          # participation slot index inside the header
+
+
+def _round_up(x: int, a: int) -> int:
+    return (x + a - 1) // a * a
+
+
+class FlatParams:
+    """Persistent flat storage for a (nested) parameter table or nn.Module.
+
+    Args:
+        params: tensor table or ``nn.Module``; its leaves are re-pointed (``set_``)
+            into the flat buffer, so existing references stay valid.
+        grads: also allocate a flat gradient buffer (with participation header);
+            for ``nn.Parameter`` leaves ``p.grad`` becomes the matching view.
+        shadow_bf16: keep a bf16 copy of the parameters (refreshed by the fused
+            update kernels) for the bf16 compute path.
+    """
+
+    def __init__(self, params: Any, grads: bool = True, shadow_bf16: bool = False, device=None):
+        self.table = params
+        leaves = walk_table(params)
+        if not leaves:
+            raise ValueError("FlatParams: empty parameter table")
+        dtype = leaves[0].dtype
+        if any(t.dtype != dtype for t in leaves):
+            raise ValueError("FlatParams: all leaves must share one dtype")
+        self.dtype = dtype
+        self.device = torch.device(device) if device is not None else leaves[0].device
+        self.shapes = [tuple(t.shape) for t in leaves]
+        self.numels = [t.numel() for t in leaves]
+        offs, o = [], HEADER
+        for n in self.numels:
+            offs.append(o)
+            o = _round_up(o + n, ALIGN)
+        self.offsets = offs
+        self.total = o  # includes header + padding, multiple of ALIGN
+        self.numel = sum(self.numels)
+        self.data = torch.zeros(self.total, dtype=dtype, device=self.device)
+        with torch.no_grad():
+            for t, off, n in zip(leaves, offs, self.numels):
+                self.data[off:off + n].copy_(t.reshape(-1))
+            for t, off, shape in zip(leaves, offs, self.shapes):
+                t.set_(self.data.untyped_storage(), off, shape, _contig_stride(shape))
+        self.leaves = leaves
+        self.grad = None
+        if grads:
+            self.grad = torch.zeros(self.total, dtype=dtype, device=self.device)
+            self.grad_views = self._views(self.grad)
+            for t, g in zip(leaves, self.grad_views):
+                if isinstance(t, torch.nn.Parameter) or t.requires_grad:
+                    t.grad = g
+        self.shadow = None
+        if shadow_bf16:
+            self.shadow = torch.zeros(self.total, dtype=torch.bfloat16, device=self.device)
+            self.refresh_shadow()
+
+    # ----------------------------------------------------------------- views
+    def _views(self, buf: torch.Tensor) -> List[torch.Tensor]:
+        return [buf[o:o + n].view(s) for o, n, s in zip(self.offsets, self.numels, self.shapes)]
+
+    def param_views(self) -> List[torch.Tensor]:
+        return self._views(self.data)
+
+    def like(self, fill: float = 0.0, dtype=None) -> torch.Tensor:
+        """A new flat buffer with the same layout (e.g. EA center/delta)."""
+        return torch.full((self.total,), fill, dtype=dtype or self.dtype, device=self.device)
+
+    def views_of(self, buf: torch.Tensor) -> List[torch.Tensor]:
+        return self._views(buf)
+
+    def shadow_views(self) -> List[torch.Tensor]:
+        assert self.shadow is not None
+        return self._views(self.shadow)
+
+    def tensors(self):  # lets walk_table() visit a FlatParams
+        return self.leaves
+
+    # -------------------------------------------------------------- buckets
+    def buckets(self, bucket_bytes: int) -> List[Tuple[int, int]]:
+        """Contiguous [start, end) ranges of the flat buffer in *reverse*
+        registration order (backward produces the last layers' grads first),
+        each at least ``bucket_bytes`` unless it is the last; boundaries fall
+        on tensor boundaries; the first range issued last includes the header
+        (participation slot) so ``n`` is complete when the last bucket lands."""
+        limit = max(1, bucket_bytes // self.data.element_size())
+        out: List[Tuple[int, int]] = []
+        end = self.total
+        for i in reversed(range(len(self.offsets))):
+            start = self.offsets[i] if i > 0 else 0
+            if end - start >= limit or i == 0:
+                out.append((start, end))
+                end = start
+        return out
+
+    # ---------------------------------------------------------------- misc
+    def refresh_shadow(self) -> None:
+        if self.shadow is None:
+            return
+        if self.data.is_cuda:
+            native().cast_f32_bf16(self.data.data_ptr(), self.shadow.data_ptr(), self.total, stream_handle())
+        else:
+            self.shadow.copy_(self.data)
+
+    def zero_grad(self, participating: bool = True) -> None:
+        fill_(self.grad, 0.0, slot_value=1.0 if participating else 0.0)
+
+    @property
+    def slot(self) -> torch.Tensor:
+        return self.grad[SLOT:SLOT + 1]
+
+
+def _contig_stride(shape: Sequence[int]) -> Tuple[int, ...]:
+    st, acc = [], 1
+    for s in reversed(shape):
+        st.append(acc)
+        acc *= max(1, s)
+    return tuple(reversed(st))
+
+
+# ---------------------------------------------------------------------------
+# fused flat ops: HIP on GPU (native, loud failure if missing), torch on CPU
+# ---------------------------------------------------------------------------
+def _ptr(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def _scale_from_slot(slot):
+    if slot is None:
+        return 1.0
+    n = float(slot.reshape(-1)[0])
+    return 1.0 / n if n > 1 else 1.0
+
+
+def sgd_update_(p: torch.Tensor, g: torch.Tensor, lr: float, slot: torch.Tensor | None = None,
+                mom: torch.Tensor | None = None, momentum: float = 0.0, weight_decay: float = 0.0,
+                shadow: torch.Tensor | None = None) -> None:
+    """p -= lr * (g/n + wd*p) [with momentum buffer]; n from ``slot`` (device)."""
+    if p.is_cuda:
+        native().sgd_update(p.data_ptr(), g.data_ptr(), _ptr(mom), _ptr(shadow), _ptr(slot), float(lr),
+                            float(momentum), float(weight_decay), p.numel(), stream_handle())
+        return
+    with torch.no_grad():
+        d = g * _scale_from_slot(slot)
+        if weight_decay:
+            d = d + weight_decay * p
+        if mom is not None:
+            mom.mul_(momentum).add_(d)
+            d = mom
+        p.sub_(lr * d)
+        if shadow is not None:
+            shadow.copy_(p)
+
+
+def scale_by_count_(x: torch.Tensor, slot: torch.Tensor) -> None:
+    if x.is_cuda:
+        native().scale_by_count(x.data_ptr(), slot.data_ptr(), x.numel(), stream_handle())
+        return
+    s = _scale_from_slot(slot)
+    if s != 1.0:
+        x.mul_(s)
+
+
+def elastic_step_(p: torch.Tensor, c: torch.Tensor, out: torch.Tensor, alpha: float,
+                  pending: torch.Tensor | None = None, shadow: torch.Tensor | None = None) -> None:
+    """[c += pending]; out = alpha*(p - c); p -= out   (K8, fused K10)."""
+    if p.is_cuda:
+        native().elastic_step(p.data_ptr(), c.data_ptr(), _ptr(pending), out.data_ptr(), _ptr(shadow),
+                              float(alpha), p.numel(), stream_handle())
+        return
+    with torch.no_grad():
+        if pending is not None:
+            c.add_(pending)
+        torch.sub(p, c, out=out)
+        out.mul_(alpha)
+        p.sub_(out)
+        if shadow is not None:
+            shadow.copy_(p)
+
+
+def add_(y: torch.Tensor, x: torch.Tensor) -> None:
+    if y.is_cuda:
+        native().add_inplace(y.data_ptr(), x.data_ptr(), y.numel(), stream_handle())
+    else:
+        y.add_(x)
+
+
+def fill_(x: torch.Tensor, value: float, slot_value: float | None = None, slot_index: int = SLOT) -> None:
+    if x.is_cuda and x.dtype == torch.float32 and x.numel() % 4 == 0:
+        native().fill_f32(x.data_ptr(), float(value), x.numel(),
+                          -1 if slot_value is None else int(slot_index), float(slot_value or 0.0), stream_handle())
+        return
+    x.fill_(value)
+    if slot_value is not None:
+        x.view(-1)[slot_index] = slot_value

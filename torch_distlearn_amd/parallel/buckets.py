@@ -1,0 +1,120 @@
+"""Bucketed gradient all-reduce overlapped with backward.
+
+The reference starts communication only after the whole backward finished and
+then ships 18 tensors one by one through a TCP tree (SURVEY §3.2 "No
+overlap").  On MI355X the flat gradient buffer of a :class:`FlatParams` is cut
+into contiguous buckets in reverse registration order (backward produces the
+last layers first).  As soon as every gradient of a bucket has been
+accumulated, the bucket's RCCL all-reduce is issued on a high-priority comm
+stream (event-ordered after the producing kernels), so it runs over xGMI while
+the earlier layers' backward is still computing.  Buckets are always launched
+in index order, so every node issues the identical collective sequence
+(required by RCCL).
+
+Bucket sizing for 7 xGMI links per GPU: a ring all-reduce splits a
+bucket into world x channels chunks; keeping chunks >= ~64-128 KB needs buckets
+of a few MB.  Default 4 MiB.
+
+The participation slot (``n``) lives in the header of the flat buffer, which
+is inside the bucket launched *last*, so ``n`` is complete once all buckets
+have landed; draining nodes replay the same bucket sequence with zeros and
+slot 0 (:meth:`drain`).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+
+from ..ops.flat import SLOT, FlatParams, fill_
+
+
+class GradBucketer:
+    def __init__(self, comm, flat: FlatParams, bucket_bytes: int = 4 << 20, hooks: bool = True,
+                 stream: Optional["torch.cuda.Stream"] = None):
+        self.comm = comm
+        self.flat = flat
+        self.ranges: List[Tuple[int, int]] = flat.buckets(bucket_bytes)
+        self.nb = len(self.ranges)
+        # leaf -> bucket
+        self.leaf_bucket = []
+        for off in flat.offsets:
+            for b, (s, e) in enumerate(self.ranges):
+                if s <= off < e:
+                    self.leaf_bucket.append(b)
+                    break
+        self.need = [0] * self.nb
+        for b in self.leaf_bucket:
+            self.need[b] += 1
+        self.cuda = flat.data.is_cuda
+        self.stream = stream if stream is not None else (
+            torch.cuda.Stream(device=flat.device, priority=-1) if self.cuda else None)
+        self._reset()
+        self._hooks = []
+        if hooks:
+            for i, t in enumerate(flat.leaves):
+                if t.requires_grad and hasattr(t, "register_post_accumulate_grad_hook"):
+                    self._hooks.append(t.register_post_accumulate_grad_hook(self._make_hook(i)))
+
+    def _make_hook(self, i):
+        def hook(_p):
+            self.mark_leaf_ready(i)
+        return hook
+
+    def _reset(self):
+        self.remaining = list(self.need)
+        self.next = 0
+        self.launched = 0
+
+    # ---------------------------------------------------------------- launch
+    def _launch(self, b: int):
+        s, e = self.ranges[b]
+        buf = self.flat.grad[s:e]
+        if self.cuda:
+            cur = torch.cuda.current_stream()
+            self.stream.wait_stream(cur)
+            with torch.cuda.stream(self.stream):
+                self.comm.all_reduce(buf, "sum", stream=self.stream)
+            buf.record_stream(self.stream)
+        else:
+            self.comm.all_reduce(buf, "sum")
+        self.launched += 1
+
+    def _pump(self):
+        while self.next < self.nb and self.remaining[self.next] <= 0:
+            self._launch(self.next)
+            self.next += 1
+
+    def mark_leaf_ready(self, i: int):
+        b = self.leaf_bucket[i]
+        self.remaining[b] -= 1
+        self._pump()
+
+    def mark_bucket_ready(self, b: int):
+        """Explicit-executor path: every gradient of bucket ``b`` is written."""
+        self.remaining[b] = 0
+        self._pump()
+
+    def finish(self):
+        """Launch what is left (params without grads), then order the compute
+        stream after the comm stream.  Resets for the next step."""
+        for b in range(self.nb):
+            self.remaining[b] = 0
+        self._pump()
+        if self.cuda:
+            torch.cuda.current_stream().wait_stream(self.stream)
+        self._reset()
+
+    def drain(self):
+        """Replay zero buckets (slot 0) until no node is active any more."""
+        while True:
+            fill_(self.flat.grad, 0.0, slot_value=0.0)
+            self.finish()
+            n = int(self.flat.grad[SLOT].item())
+            if n == 0:
+                return
+
+    def remove_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

@@ -1,0 +1,240 @@
+"""Communicators: the data plane and control plane under ``Tree``.
+
+Reference transport: ``libipc`` TCP sockets + an unpipelined b-ary tree
+(``ipc.Tree``).  MI355X design:
+
+* **Data plane** -- :class:`RcclCommunicator`: the native C++ RCCL
+  communicator (``csrc/comm/communicator.h``).  Collectives are enqueued on a
+  caller-chosen HIP stream (default: torch's current stream), never block the
+  host, and are legal inside hipGraph capture.  RCCL picks ring/tree channels
+  over the 7 xGMI links per GPU.
+* **Control plane** -- a gloo process group over the c10d TCPStore:
+  rendezvous, the ncclUniqueId exchange, any-source receives (AsyncEA's mutex,
+  which RCCL cannot express), small host-side reductions, and the whole CPU
+  test path.
+* :class:`ProcessGroupCommunicator` implements the same interface on a
+  ``torch.distributed`` group (gloo on CPU -- used by the multi-process tests --
+  or torch's own NCCL/RCCL group when ``backend='nccl'`` is requested).
+"""
+from __future__ import annotations
+
+import contextlib
+import datetime
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .._native import native, stream_handle
+
+DTYPE_CODES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int64: 3,
+               torch.int32: 4, torch.uint8: 5, torch.float64: 6}
+OP_CODES = {"sum": 0, "prod": 1, "max": 2, "min": 3, "avg": 4}
+_DIST_OPS = {"sum": dist.ReduceOp.SUM, "prod": dist.ReduceOp.PRODUCT, "max": dist.ReduceOp.MAX,
+             "min": dist.ReduceOp.MIN}
+
+MSG_LEN = 8  # control-plane message = int64[MSG_LEN]
+
+
+class Communicator:
+    """Interface shared by the RCCL and process-group communicators."""
+
+    rank: int
+    world_size: int
+    ctrl: Optional[dist.ProcessGroup]
+
+    # ---------------- data plane (in-place, stream ordered) ----------------
+    def all_reduce(self, t: torch.Tensor, op: str = "sum", stream=None) -> None:
+        raise NotImplementedError
+
+    def broadcast(self, t: torch.Tensor, root: int = 0, stream=None) -> None:
+        raise NotImplementedError
+
+    def all_gather(self, out: torch.Tensor, t: torch.Tensor, stream=None) -> None:
+        """out = cat over ranks of t (out.numel() == world * t.numel())."""
+        raise NotImplementedError
+
+    def send(self, t: torch.Tensor, peer: int, stream=None) -> None:
+        raise NotImplementedError
+
+    def recv(self, t: torch.Tensor, peer: int, stream=None) -> None:
+        raise NotImplementedError
+
+    @contextlib.contextmanager
+    def group(self):
+        yield
+
+    # ---------------- control plane (host, gloo) ----------------
+    def barrier(self) -> None:
+        if self.world_size > 1:
+            dist.barrier(group=self.ctrl)
+
+    def send_msg(self, msg: Sequence[int], dst: int, tag: int = 0) -> None:
+        buf = torch.zeros(MSG_LEN, dtype=torch.int64)
+        buf[: len(msg)] = torch.tensor(list(msg), dtype=torch.int64)
+        dist.send(buf, dst=dst, group=self.ctrl, tag=tag)
+
+    def recv_msg(self, src: Optional[int] = None, tag: int = 0) -> Tuple[int, List[int]]:
+        """Receive a control message; ``src=None`` = any source (recvAny)."""
+        buf = torch.zeros(MSG_LEN, dtype=torch.int64)
+        sender = dist.recv(buf, src=src, group=self.ctrl, tag=tag)
+        return int(sender), buf.tolist()
+
+    def all_reduce_host(self, t: torch.Tensor, op: str = "sum") -> None:
+        """Small CPU all-reduce on the control plane."""
+        if self.world_size > 1:
+            dist.all_reduce(t, op=_DIST_OPS[op], group=self.ctrl)
+
+    def broadcast_object(self, obj, root: int = 0):
+        lst = [obj]
+        if self.world_size > 1:
+            dist.broadcast_object_list(lst, src=root, group=self.ctrl)
+        return lst[0]
+
+    def health(self) -> str:
+        return ""
+
+    def close(self) -> None:
+        pass
+
+
+class ProcessGroupCommunicator(Communicator):
+    """Communicator over a torch.distributed group (gloo CPU or torch NCCL)."""
+
+    def __init__(self, data_group=None, ctrl_group=None):
+        self.data = data_group
+        self.ctrl = ctrl_group if ctrl_group is not None else data_group
+        self.rank = dist.get_rank(self.data) if dist.is_initialized() else 0
+        self.world_size = dist.get_world_size(self.data) if dist.is_initialized() else 1
+
+    def all_reduce(self, t, op="sum", stream=None):
+        if self.world_size == 1:
+            return
+        if op == "avg":
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.data)
+            t.div_(self.world_size)
+        else:
+            dist.all_reduce(t, op=_DIST_OPS[op], group=self.data)
+
+    def broadcast(self, t, root=0, stream=None):
+        if self.world_size > 1:
+            dist.broadcast(t, src=root, group=self.data)
+
+    def all_gather(self, out, t, stream=None):
+        if self.world_size == 1:
+            out.view(-1).copy_(t.view(-1))
+            return
+        dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1), group=self.data)
+
+    def send(self, t, peer, stream=None):
+        dist.send(t, dst=peer, group=self.data)
+
+    def recv(self, t, peer, stream=None):
+        dist.recv(t, src=peer, group=self.data)
+
+
+class RcclCommunicator(Communicator):
+    """Native RCCL data plane (C++), gloo control plane."""
+
+    def __init__(self, rank: int, world_size: int, device: torch.device, ctrl_group=None):
+        C = native()
+        self.ctrl = ctrl_group
+        self.rank, self.world_size = rank, world_size
+        self.device = torch.device(device)
+        uid = C.rccl_unique_id() if rank == 0 else None
+        if world_size > 1:
+            lst = [uid]
+            dist.broadcast_object_list(lst, src=0, group=ctrl_group)
+            uid = lst[0]
+        self._c = C.RcclCommunicator(uid, rank, world_size, self.device.index or 0)
+        self._in_group = 0
+
+    @staticmethod
+    def _check(t):
+        if not t.is_cuda:
+            raise ValueError("RcclCommunicator: GPU tensors only (use the gloo communicator for CPU)")
+        if not t.is_contiguous():
+            raise ValueError("RcclCommunicator: tensor must be contiguous")
+
+    def all_reduce(self, t, op="sum", stream=None):
+        self._check(t)
+        self._c.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], OP_CODES[op],
+                           stream_handle(stream))
+
+    def broadcast(self, t, root=0, stream=None):
+        self._check(t)
+        self._c.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], root, stream_handle(stream))
+
+    def all_gather(self, out, t, stream=None):
+        self._check(t)
+        self._check(out)
+        self._c.all_gather(t.data_ptr(), out.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], stream_handle(stream))
+
+    def reduce_scatter(self, out, t, op="sum", stream=None):
+        self._check(t)
+        self._c.reduce_scatter(t.data_ptr(), out.data_ptr(), out.numel(), DTYPE_CODES[t.dtype], OP_CODES[op],
+                               stream_handle(stream))
+
+    def send(self, t, peer, stream=None):
+        self._check(t)
+        self._c.send(t.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], peer, stream_handle(stream))
+
+    def recv(self, t, peer, stream=None):
+        self._check(t)
+        self._c.recv(t.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], peer, stream_handle(stream))
+
+    @contextlib.contextmanager
+    def group(self):
+        self._c.group_start()
+        try:
+            yield
+        finally:
+            self._c.group_end()
+
+    def health(self) -> str:
+        return self._c.async_error()
+
+    def close(self):
+        if getattr(self, "_c", None) is not None:
+            self._c.destroy()
+            self._c = None
+
+
+# ---------------------------------------------------------------------------
+# bootstrap
+# ---------------------------------------------------------------------------
+def _env_int(name, default):
+    v = os.environ.get(name)
+    return int(v) if v not in (None, "") else default
+
+
+def init_communicator(rank: Optional[int] = None, world_size: Optional[int] = None, host: Optional[str] = None,
+                      port: Optional[int] = None, device=None, backend: str = "auto",
+                      timeout_s: float = 600.0) -> Communicator:
+    """Rendezvous + communicator construction.
+
+    ``rank``/``world_size`` default to the torchrun env (RANK/WORLD_SIZE).
+    ``host``/``port`` default to MASTER_ADDR/MASTER_PORT (127.0.0.1:29500).
+    ``backend``: ``auto`` (RCCL for CUDA devices, gloo otherwise), ``rccl``,
+    ``nccl`` (torch's process group) or ``gloo``.
+    """
+    rank = _env_int("RANK", 0) if rank is None else rank
+    world_size = _env_int("WORLD_SIZE", 1) if world_size is None else world_size
+    host = host or os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = port or _env_int("MASTER_PORT", 29500)
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    if not dist.is_initialized():
+        dist.init_process_group("gloo", init_method=f"tcp://{host}:{port}", rank=rank, world_size=world_size,
+                                timeout=datetime.timedelta(seconds=timeout_s))
+    ctrl = dist.group.WORLD
+    if backend == "auto":
+        backend = "rccl" if dev.type == "cuda" else "gloo"
+    if backend == "rccl":
+        return RcclCommunicator(rank, world_size, dev, ctrl_group=ctrl)
+    if backend == "nccl":
+        g = dist.new_group(backend="nccl")
+        return ProcessGroupCommunicator(g, ctrl)
+    if backend == "gloo":
+        return ProcessGroupCommunicator(ctrl, ctrl)
+    raise ValueError(f"unknown backend {backend!r}")
