@@ -30,9 +30,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("rccl_version", &rccl_version);
   py::class_<RcclCommunicator>(m, "RcclCommunicator")
       .def(py::init([](py::bytes uid, int rank, int world, int device) {
-             return new RcclCommunicator(std::string(uid), rank, world, device);
-           }),
-           py::call_guard<py::gil_scoped_release>())
+        std::string id(uid);  // copy while holding the GIL
+        py::gil_scoped_release nogil;  // ncclCommInitRank blocks on the other ranks
+        return new RcclCommunicator(id, rank, world, device);
+      }))
       .def_property_readonly("rank", &RcclCommunicator::rank)
       .def_property_readonly("world", &RcclCommunicator::world)
       .def_property_readonly("device", &RcclCommunicator::device)

@@ -1,0 +1,19 @@
+"""Model families of the reference examples (+ ResNet-50 from BASELINE.json).
+
+* :class:`CifarConvNet` -- examples/cifar10.lua:101-143, examples/Model.lua
+* :class:`MnistConvNet` / :class:`MnistMLP` -- examples/mnist.lua:53-66
+* :func:`resnet50` -- BASELINE.json config 5 (bucket / xGMI stress)
+"""
+from .cifar_convnet import CifarConvNet, num_params
+
+
+def make_executor(model, flat, bucketer=None, max_batch=None):
+    """Native (hand-written HIP) executor for ``model`` bound to ``flat``."""
+    if isinstance(model, CifarConvNet):
+        from .cifar_hip import CifarHIPExecutor
+
+        return CifarHIPExecutor(model, flat, bucketer=bucketer, max_batch=max_batch)
+    raise NotImplementedError(f"no native executor for {type(model).__name__}")
+
+
+__all__ = ["CifarConvNet", "num_params", "make_executor"]
