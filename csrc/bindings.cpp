@@ -25,6 +25,24 @@ PYBIND11_MODULE(_C, m) {
   m.def("confusion_update", &confusion_update);
   m.def("gather_normalize", &gather_normalize);
 
+  // ---- convnet kernels (MFMA implicit GEMM, BN/ReLU/pool, classifier head) ------
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd_stat_rows", &conv_fwd_stat_rows);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("slab_reduce", &slab_reduce);
+  m.def("weight_flip_transpose", &weight_flip_transpose);
+  m.def("pack_weight", &pack_weight);
+  m.def("pad_channels", &pad_channels);
+  m.def("prep_step", &prep_step);
+  m.def("bn_finalize", &bn_finalize);
+  m.def("bn_relu_pool_fwd", &bn_relu_pool_fwd);
+  m.def("bn_bwd_blocks", &bn_bwd_blocks);
+  m.def("bn_relu_pool_bwd_reduce", &bn_relu_pool_bwd_reduce);
+  m.def("bn_bwd_finalize", &bn_bwd_finalize);
+  m.def("bn_relu_pool_bwd_apply", &bn_relu_pool_bwd_apply);
+  m.def("head_fwd_bwd", &head_fwd_bwd);
+  m.def("head_wgrad", &head_wgrad);
+
   // ---- RCCL communicator ------------------------------------------------------
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   m.def("rccl_version", &rccl_version);

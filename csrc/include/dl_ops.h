@@ -4,6 +4,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <vector>
+
 namespace dl {
 
 // flat_ops.hip -------------------------------------------------------------
@@ -22,5 +24,39 @@ void confusion_update(uintptr_t pred, int pred_is_bf16, uintptr_t target, uintpt
                       uintptr_t stream);
 void gather_normalize(uintptr_t images, uintptr_t idx, uintptr_t out, int B, int HW, int Cs, int Cd, float m0,
                       float m1, float m2, float s0, float s1, float s2, uintptr_t stream);
+
+// conv_igemm.hip --------------------------------------------------------------
+// NHWC activations, KRSC weights, stride 1, same padding, Cin power of two >= 8.
+int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab, int B, int H, int W, int Cin,
+             int Cout, int KS, int tile, int splits, uintptr_t stream);
+int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile, int splits);
+void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, int Cin, int Cout, int KS, int splits,
+                int ldo, int tile, uintptr_t stream);
+void slab_reduce(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream);
+void weight_flip_transpose(uintptr_t w, uintptr_t wt, int Cout, int Cin, int KS, uintptr_t stream);
+void pack_weight(uintptr_t w, uintptr_t wp, int Cout, int taps, int C, int Cp, uintptr_t stream);
+void pad_channels(uintptr_t x, uintptr_t xp, int64_t P, int C, int Cp, uintptr_t stream);
+void prep_step(uintptr_t x, uintptr_t xp, int64_t P, int C, int Cp, uintptr_t w1, uintptr_t w1p, int w1_cout,
+               int taps, int w1_c, int w1_cp, std::vector<uintptr_t> tw, std::vector<uintptr_t> twt,
+               std::vector<int> tcout, std::vector<int> tcin, uintptr_t stream);
+
+// bn_pool.hip -----------------------------------------------------------------
+void bn_finalize(uintptr_t partial, int T, int C, int64_t M, uintptr_t gamma, uintptr_t beta, uintptr_t bias,
+                 uintptr_t rmean, uintptr_t rvar, float eps, float momentum, int mode, uintptr_t coef,
+                 uintptr_t stream);
+void bn_relu_pool_fwd(uintptr_t y, uintptr_t coef, uintptr_t out, int B, int H, int W, int C, uintptr_t stream);
+int bn_bwd_blocks(int B, int H, int W, int C);
+void bn_relu_pool_bwd_reduce(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t partial, int B, int H, int W, int C,
+                             int blocks, uintptr_t stream);
+void bn_bwd_finalize(uintptr_t partial, int T, int C, int64_t M, uintptr_t gamma, uintptr_t coef, uintptr_t dgamma,
+                     uintptr_t dbeta, uintptr_t acoef, uintptr_t stream);
+void bn_relu_pool_bwd_apply(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t acoef, uintptr_t dy, int B, int H,
+                            int W, int C, uintptr_t stream);
+
+// head.hip --------------------------------------------------------------------
+void head_fwd_bwd(uintptr_t h, uintptr_t w, uintptr_t bias, uintptr_t labels, int F, int B, int NC,
+                  uintptr_t logits_out, uintptr_t dlogits, uintptr_t loss_b, uintptr_t dh, uintptr_t stream);
+void head_wgrad(uintptr_t h, uintptr_t dlogits, uintptr_t loss_b, int F, int B, int NC, uintptr_t dw, uintptr_t db,
+                uintptr_t loss, uintptr_t stream);
 
 }  // namespace dl

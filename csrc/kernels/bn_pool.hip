@@ -1,0 +1,354 @@
+// Train-mode BatchNorm + ReLU + 2x2/2 max-pool, forward and backward, on
+// NHWC bf16 activations (gfx950).
+//
+// Reference ops: nn.SpatialBatchNormalization(C, 1e-3) -> nn.ReLU ->
+// nn.SpatialMaxPooling(2,2,2,2) (examples/cifar10.lua:109-129; SURVEY §2.8
+// K14/K15/K16).  Instead of five separate passes (BN stats, BN apply, ReLU,
+// pool, and their backwards) the block is:
+//
+//   forward : conv epilogue emits per-tile channel sums  (conv_igemm.hip)
+//             bn_finalize      -> mean, invstd, scale, shift (+ running stats)
+//             bn_relu_pool_fwd -> pooled = maxpool(relu(scale*y + shift))   (1 read of y)
+//   backward: bn_relu_pool_bwd_reduce -> per-channel sum(dz), sum(dz*xhat)  (recomputes
+//             the pool argmax / ReLU mask from y: nothing is stored in forward)
+//             bn_bwd_finalize  -> dgamma, dbeta (into the flat grad), apply coefficients
+//             bn_relu_pool_bwd_apply -> dy = a*dz + b*xhat + c           (dense NHWC)
+//
+// Every thread handles 8 channels (one 16-byte vector) of one pooled pixel.
+// All reductions are deterministic (fixed-order partial rows, no atomics).
+// The conv bias is not added in the train forward: BatchNorm in train mode is
+// invariant to a per-channel shift, so the output and every gradient are
+// unchanged and d(bias) is exactly 0; the running mean is updated with
+// mean + bias so eval mode (running statistics) is exact.
+#include "dl_common.h"
+#include "dl_ops.h"
+
+namespace dl {
+
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  f[0] = lo_bf16(v.x); f[1] = hi_bf16(v.x); f[2] = lo_bf16(v.y); f[3] = hi_bf16(v.y);
+  f[4] = lo_bf16(v.z); f[5] = hi_bf16(v.z); f[6] = lo_bf16(v.w); f[7] = hi_bf16(v.w);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]),
+                    pack_bf16x2(f[6], f[7]));
+}
+
+// ---------------------------------------------------------------------------
+// finalize (forward): partial rows [T][2][C] (sum, sumsq) -> coefficients
+// mode 0 = train (batch statistics, update running stats), 1 = eval
+// coef layout [4][C]: mean, invstd, scale, shift
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ partial, int T, int C, int64_t M,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta,
+                                                          const float* __restrict__ bias, float* __restrict__ rmean,
+                                                          float* __restrict__ rvar, float eps, float momentum,
+                                                          int mode, float* __restrict__ coef) {
+  const int c = blockIdx.x;
+  __shared__ float red[2][256];
+  float mean, var;
+  if (mode == 0) {
+    float s1 = 0.f, s2 = 0.f;
+    for (int t = threadIdx.x; t < T; t += 256) {
+      s1 += partial[(int64_t)t * 2 * C + c];
+      s2 += partial[(int64_t)t * 2 * C + C + c];
+    }
+    red[0][threadIdx.x] = s1;
+    red[1][threadIdx.x] = s2;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (threadIdx.x < o) {
+        red[0][threadIdx.x] += red[0][threadIdx.x + o];
+        red[1][threadIdx.x] += red[1][threadIdx.x + o];
+      }
+      __syncthreads();
+    }
+    mean = red[0][0] / (float)M;
+    var = fmaxf(red[1][0] / (float)M - mean * mean, 0.f);
+  } else {
+    mean = rmean[c] - (bias ? bias[c] : 0.f);  // eval: conv output excludes the bias
+    var = rvar[c];
+  }
+  if (threadIdx.x == 0) {
+    const float invstd = rsqrtf(var + eps);
+    const float sc = gamma[c] * invstd;
+    coef[c] = mean;
+    coef[C + c] = invstd;
+    coef[2 * C + c] = sc;
+    coef[3 * C + c] = beta[c] - mean * sc;
+    if (mode == 0 && rmean != nullptr) {
+      const float unbiased = M > 1 ? var * (float)M / (float)(M - 1) : var;
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * (mean + (bias ? bias[c] : 0.f));
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * unbiased;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// forward apply: pooled[b][oh][ow][c] = max_{2x2} relu(scale*y + shift)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) bn_relu_pool_fwd_kernel(const bf16_t* __restrict__ y,
+                                                               const float* __restrict__ coef,
+                                                               bf16_t* __restrict__ out, int B, int H, int W, int C) {
+  const int C8 = C >> 3, Ho = H >> 1, Wo = W >> 1;
+  const int64_t total = (int64_t)B * Ho * Wo * C8;
+  const float* scale = coef + 2 * C;
+  const float* shift = coef + 3 * C;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % C8);
+    const int64_t pix = i / C8;
+    const int ow = (int)(pix % Wo);
+    const int64_t t = pix / Wo;
+    const int oh = (int)(t % Ho);
+    const int64_t b = t / Ho;
+    const int c0 = c8 * 8;
+    float sc[8], sh[8], mx[8];
+    *reinterpret_cast<float4*>(sc) = *reinterpret_cast<const float4*>(scale + c0);
+    *reinterpret_cast<float4*>(sc + 4) = *reinterpret_cast<const float4*>(scale + c0 + 4);
+    *reinterpret_cast<float4*>(sh) = *reinterpret_cast<const float4*>(shift + c0);
+    *reinterpret_cast<float4*>(sh + 4) = *reinterpret_cast<const float4*>(shift + c0 + 4);
+    const bf16_t* base = y + (((b * H + 2 * oh) * W) + 2 * ow) * (int64_t)C + c0;
+    const uint4 v0 = *reinterpret_cast<const uint4*>(base);
+    const uint4 v1 = *reinterpret_cast<const uint4*>(base + C);
+    const uint4 v2 = *reinterpret_cast<const uint4*>(base + (int64_t)W * C);
+    const uint4 v3 = *reinterpret_cast<const uint4*>(base + (int64_t)W * C + C);
+    float f[8];
+    unpack8(v0, f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mx[k] = fmaf(sc[k], f[k], sh[k]);
+    unpack8(v1, f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mx[k] = fmaxf(mx[k], fmaf(sc[k], f[k], sh[k]));
+    unpack8(v2, f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mx[k] = fmaxf(mx[k], fmaf(sc[k], f[k], sh[k]));
+    unpack8(v3, f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mx[k] = fmaxf(fmaxf(mx[k], fmaf(sc[k], f[k], sh[k])), 0.f);
+    *reinterpret_cast<uint4*>(out + pix * C + c0) = pack8(mx);
+  }
+}
+
+// Recompute the backward signal of one pooled pixel x 8 channels:
+// dz[w][k] = dP[k] at the first (row-major) window position holding the max of
+// relu(z) if that z > 0, else 0; xh[w][k] = (y - mean) * invstd.
+struct BwdCtx {
+  float sc[8], sh[8], mu[8], is[8];
+};
+
+__device__ __forceinline__ void load8(float* d, const float* s) {
+  *reinterpret_cast<float4*>(d) = *reinterpret_cast<const float4*>(s);
+  *reinterpret_cast<float4*>(d + 4) = *reinterpret_cast<const float4*>(s + 4);
+}
+
+__device__ __forceinline__ void bwd_window(const bf16_t* __restrict__ y, const bf16_t* __restrict__ dP,
+                                           const BwdCtx& cx, int64_t b, int oh, int ow, int H, int W, int C, int c0,
+                                           float (&yv)[4][8], float (&dz)[4][8]) {
+  const bf16_t* base = y + (((b * H + 2 * oh) * W) + 2 * ow) * (int64_t)C + c0;
+  const int64_t offs[4] = {0, C, (int64_t)W * C, (int64_t)W * C + C};
+#pragma unroll
+  for (int w = 0; w < 4; ++w) unpack8(*reinterpret_cast<const uint4*>(base + offs[w]), yv[w]);
+  float g[8];
+  unpack8(*reinterpret_cast<const uint4*>(dP + (((b * (H >> 1) + oh) * (W >> 1)) + ow) * (int64_t)C + c0), g);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float best = -INFINITY;
+    int arg = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float r = fmaxf(fmaf(cx.sc[k], yv[w][k], cx.sh[k]), 0.f);
+      if (r > best) { best = r; arg = w; }
+    }
+#pragma unroll
+    for (int w = 0; w < 4; ++w) dz[w][k] = (w == arg && best > 0.f) ? g[k] : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward reduce: partial[blk][0][c] = sum dz, partial[blk][1][c] = sum dz*xhat
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) bn_relu_pool_bwd_reduce_kernel(const bf16_t* __restrict__ y,
+                                                                      const bf16_t* __restrict__ dP,
+                                                                      const float* __restrict__ coef,
+                                                                      float* __restrict__ partial, int B, int H,
+                                                                      int W, int C) {
+  const int C8 = C >> 3, Ho = H >> 1, Wo = W >> 1;
+  const int64_t total = (int64_t)B * Ho * Wo * C8;
+  // grid-stride keeps the channel chunk fixed per thread (stride % C8 == 0)
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c8 = (int)(i0 % C8), c0 = c8 * 8;
+  BwdCtx cx;
+  load8(cx.mu, coef + c0);
+  load8(cx.is, coef + C + c0);
+  load8(cx.sc, coef + 2 * C + c0);
+  load8(cx.sh, coef + 3 * C + c0);
+  float s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
+  for (int64_t i = i0; i < total; i += stride) {
+    const int64_t pix = i / C8;
+    const int ow = (int)(pix % Wo);
+    const int64_t t = pix / Wo;
+    const int oh = (int)(t % Ho);
+    const int64_t b = t / Ho;
+    float yv[4][8], dz[4][8];
+    bwd_window(y, dP, cx, b, oh, ow, H, W, C, c0, yv, dz);
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s1[k] += dz[w][k];
+        s2[k] += dz[w][k] * (yv[w][k] - cx.mu[k]) * cx.is[k];
+      }
+  }
+  // block reduction over threads that own the same channel chunk
+  __shared__ float red[256][17];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { red[threadIdx.x][k] = s1[k]; red[threadIdx.x][8 + k] = s2[k]; }
+  __syncthreads();
+  // thread t < C: channel t (chunk t/8, lane k = t%8)
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const int ch = c >> 3, k = c & 7;
+    // threads with (blockIdx.x*256 + tid) % C8 == ch
+    const int first = (int)(((int64_t)ch - ((int64_t)blockIdx.x * blockDim.x) % C8 + C8) % C8);
+    float a = 0.f, bsum = 0.f;
+    for (int t = first; t < (int)blockDim.x; t += C8) { a += red[t][k]; bsum += red[t][8 + k]; }
+    partial[(int64_t)blockIdx.x * 2 * C + c] = a;
+    partial[(int64_t)blockIdx.x * 2 * C + C + c] = bsum;
+  }
+}
+
+// backward finalize: dgamma = sum(dz*xhat), dbeta = sum(dz);
+// apply coefficients [3][C]: dy = a*dz + b*xhat + c
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ partial, int T, int C,
+                                                              int64_t M, const float* __restrict__ gamma,
+                                                              const float* __restrict__ coef,
+                                                              float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                              float* __restrict__ acoef) {
+  const int c = blockIdx.x;
+  __shared__ float red[2][256];
+  float s1 = 0.f, s2 = 0.f;
+  for (int t = threadIdx.x; t < T; t += 256) {
+    s1 += partial[(int64_t)t * 2 * C + c];
+    s2 += partial[(int64_t)t * 2 * C + C + c];
+  }
+  red[0][threadIdx.x] = s1;
+  red[1][threadIdx.x] = s2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + o];
+      red[1][threadIdx.x] += red[1][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float sdz = red[0][0], sdzx = red[1][0];
+    if (dgamma) dgamma[c] = sdzx;
+    if (dbeta) dbeta[c] = sdz;
+    const float a = gamma[c] * coef[C + c];  // gamma * invstd
+    acoef[c] = a;
+    acoef[C + c] = -a * sdzx / (float)M;
+    acoef[2 * C + c] = -a * sdz / (float)M;
+  }
+}
+
+__global__ void __launch_bounds__(256) bn_relu_pool_bwd_apply_kernel(const bf16_t* __restrict__ y,
+                                                                     const bf16_t* __restrict__ dP,
+                                                                     const float* __restrict__ coef,
+                                                                     const float* __restrict__ acoef,
+                                                                     bf16_t* __restrict__ dy, int B, int H, int W,
+                                                                     int C) {
+  const int C8 = C >> 3, Ho = H >> 1, Wo = W >> 1;
+  const int64_t total = (int64_t)B * Ho * Wo * C8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % C8), c0 = c8 * 8;
+    const int64_t pix = i / C8;
+    const int ow = (int)(pix % Wo);
+    const int64_t t = pix / Wo;
+    const int oh = (int)(t % Ho);
+    const int64_t b = t / Ho;
+    BwdCtx cx;
+    load8(cx.mu, coef + c0);
+    load8(cx.is, coef + C + c0);
+    load8(cx.sc, coef + 2 * C + c0);
+    load8(cx.sh, coef + 3 * C + c0);
+    float ka[8], kb[8], kc[8];
+    load8(ka, acoef + c0);
+    load8(kb, acoef + C + c0);
+    load8(kc, acoef + 2 * C + c0);
+    float yv[4][8], dz[4][8];
+    bwd_window(y, dP, cx, b, oh, ow, H, W, C, c0, yv, dz);
+    bf16_t* base = dy + (((b * H + 2 * oh) * W) + 2 * ow) * (int64_t)C + c0;
+    const int64_t offs[4] = {0, C, (int64_t)W * C, (int64_t)W * C + C};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = ka[k] * dz[w][k] + kb[k] * ((yv[w][k] - cx.mu[k]) * cx.is[k]) + kc[k];
+      *reinterpret_cast<uint4*>(base + offs[w]) = pack8(o);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+static void check_c(int C) {
+  if (C % 8 != 0) throw std::runtime_error("bn/pool: C must be a multiple of 8");
+}
+
+void bn_finalize(uintptr_t partial, int T, int C, int64_t M, uintptr_t gamma, uintptr_t beta, uintptr_t bias,
+                 uintptr_t rmean, uintptr_t rvar, float eps, float momentum, int mode, uintptr_t coef,
+                 uintptr_t stream) {
+  bn_finalize_kernel<<<C, 256, 0, as_stream(stream)>>>((const float*)partial, T, C, M, (const float*)gamma,
+                                                       (const float*)beta, (const float*)bias, (float*)rmean,
+                                                       (float*)rvar, eps, momentum, mode, (float*)coef);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+void bn_relu_pool_fwd(uintptr_t y, uintptr_t coef, uintptr_t out, int B, int H, int W, int C, uintptr_t stream) {
+  check_c(C);
+  const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
+  bn_relu_pool_fwd_kernel<<<stream_grid(total), 256, 0, as_stream(stream)>>>(
+      (const bf16_t*)y, (const float*)coef, (bf16_t*)out, B, H, W, C);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+int bn_bwd_blocks(int B, int H, int W, int C) {
+  const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
+  int64_t g = (total + 256 * 4 - 1) / (256 * 4);  // >= 4 pixels per thread
+  if (g > 1024) g = 1024;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+void bn_relu_pool_bwd_reduce(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t partial, int B, int H, int W, int C,
+                             int blocks, uintptr_t stream) {
+  check_c(C);
+  if ((256 % (C / 8)) != 0) throw std::runtime_error("bn_relu_pool_bwd_reduce: C/8 must divide 256");
+  bn_relu_pool_bwd_reduce_kernel<<<blocks, 256, 0, as_stream(stream)>>>(
+      (const bf16_t*)y, (const bf16_t*)dP, (const float*)coef, (float*)partial, B, H, W, C);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+void bn_bwd_finalize(uintptr_t partial, int T, int C, int64_t M, uintptr_t gamma, uintptr_t coef, uintptr_t dgamma,
+                     uintptr_t dbeta, uintptr_t acoef, uintptr_t stream) {
+  bn_bwd_finalize_kernel<<<C, 256, 0, as_stream(stream)>>>((const float*)partial, T, C, M, (const float*)gamma,
+                                                           (const float*)coef, (float*)dgamma, (float*)dbeta,
+                                                           (float*)acoef);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+void bn_relu_pool_bwd_apply(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t acoef, uintptr_t dy, int B, int H,
+                            int W, int C, uintptr_t stream) {
+  check_c(C);
+  const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
+  bn_relu_pool_bwd_apply_kernel<<<stream_grid(total), 256, 0, as_stream(stream)>>>(
+      (const bf16_t*)y, (const bf16_t*)dP, (const float*)coef, (const float*)acoef, (bf16_t*)dy, B, H, W, C);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dl

@@ -27,6 +27,9 @@
 #include "dl_common.h"
 #include "dl_ops.h"
 
+#include <algorithm>
+#include <vector>
+
 namespace dl {
 
 struct ConvGeom {
@@ -102,84 +105,121 @@ __device__ __forceinline__ int xcd_swizzle(int bid, int nwg) {
 }
 
 // --------------------------------------------------------------------------
-// forward / dgrad implicit GEMM
+// LDS-DMA staging (global_load_lds_dwordx4): one wave instruction writes
+// 64 lanes x 16 B = 1 KiB contiguously at a wave-uniform LDS base.  The LDS
+// image stays lane-linear; the swizzle is applied to the per-lane SOURCE chunk
+// (the XORs above are involutions), and zero padding (halo taps, K tails,
+// M/N tails) is read from a 16-byte zero line in global memory.
 // --------------------------------------------------------------------------
-template <int BM, int BN, int BK, bool STATS>
+__device__ uint4 g_zero16[4];
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void block_sync_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// --------------------------------------------------------------------------
+// forward / dgrad implicit GEMM, split-K capable
+//   C[m][n] = sum_{k in split} im2col(x)[m][k] * w[n][k]
+//   splits == 1: bf16 y (+ BN partial sums per M tile)   splits > 1: fp32 slab[split][M][N]
+// 256 threads = 4 waves (2 x 2), wave tile (BM/2) x (BN/2), BK = 64,
+// 3-stage LDS ring filled by LDS-DMA, one barrier per K step.
+// --------------------------------------------------------------------------
+template <int BM, int BN, bool STATS, bool SLAB>
 __global__ void __launch_bounds__(256) conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                        bf16_t* __restrict__ y, float* __restrict__ stats,
-                                                       const ConvGeom g) {
-  constexpr int NT = 256, WM = 2, WN = 2;
-  constexpr int CPR = BK / 8;
-  constexpr int A_PT = BM * CPR / NT, B_PT = BN * CPR / NT;
-  static_assert(BM * CPR % NT == 0 && BN * CPR % NT == 0, "tile/thread mismatch");
+                                                       float* __restrict__ slab, const ConvGeom g, int splits,
+                                                       int kt_per_split) {
+  constexpr int BK = 64, CPR = 8, NT = 256, WM = 2, WN = 2, STAGES = 3;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE_BYTES = A_BYTES + B_BYTES;
+  constexpr int A_INS = A_BYTES / 1024 / 4, B_INS = B_BYTES / 1024 / 4;  // glds per wave per stage
+  constexpr int LPS = A_INS + B_INS;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
-  constexpr int A_CH = BM * CPR, B_CH = BN * CPR;
-  __shared__ __attribute__((aligned(16))) uint4 smem[2 * (A_CH + B_CH)];
+  static_assert(A_INS >= 1 && B_INS >= 1, "tile too small");
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const int ntn = (g.Cout + BN - 1) / BN;
   const int ntm = (g.M + BM - 1) / BM;
-  const int tile = xcd_swizzle(blockIdx.x, ntm * ntn);
-  // n fastest: the ntn tiles sharing one activation panel run back to back
-  const int tm = tile / ntn, tn = tile % ntn;
+  // Panel-major order: the workgroups of one XCD (consecutive ids after the
+  // swizzle) share one (n-tile, K-split) weight panel and sweep the M tiles,
+  // so the panel is fetched into that XCD's L2 once instead of every XCD
+  // streaming the whole weight tensor from the Infinity Cache.
+  const int id = xcd_swizzle(blockIdx.x, ntm * ntn * splits);
+  const int tm = id % ntm;
+  const int panel = id / ntm;
+  const int split = panel % splits, tn = panel / splits;
   const int m0 = tm * BM, n0 = tn * BN;
   const int HW = 1 << g.logHW, Wd = g.W, C8 = 1 << g.logC8;
+  const int nkt_total = (g.Kch + CPR - 1) / CPR;
+  const int kt_beg = split * kt_per_split;
+  const int kt_end = min(nkt_total, kt_beg + kt_per_split);
+  const int nk = max(0, kt_end - kt_beg);
 
-  // per-thread A rows (fixed over the K loop)
-  int a_row[A_PT], a_ch[A_PT], a_oh[A_PT], a_ow[A_PT];
-  int64_t a_base[A_PT];
-  bool a_ok[A_PT];
+  // per-lane source roles (fixed over the K loop)
+  // A: instruction j of this wave covers rows 8*(wid*A_INS + j) .. +7
+  int a_ch[A_INS], a_oh[A_INS], a_ow[A_INS];
+  int64_t a_base[A_INS];
+  bool a_ok[A_INS];
 #pragma unroll
-  for (int i = 0; i < A_PT; ++i) {
-    const int q = tid + i * NT;
-    a_row[i] = q / CPR;
-    a_ch[i] = q % CPR;
-    const int m = m0 + a_row[i];
-    a_ok[i] = m < g.M;
-    const int mm = a_ok[i] ? m : 0;
+  for (int j = 0; j < A_INS; ++j) {
+    const int row = 8 * (wid * A_INS + j) + (lane >> 3);
+    a_ch[j] = (lane & 7) ^ ((row >> 1) & 7);
+    const int m = m0 + row;
+    a_ok[j] = m < g.M;
+    const int mm = a_ok[j] ? m : 0;
     const int b = mm >> g.logHW, rem = mm & (HW - 1);
-    a_oh[i] = rem >> g.logW;
-    a_ow[i] = rem & (Wd - 1);
-    a_base[i] = (int64_t)b * HW * g.Cin;
+    a_oh[j] = rem >> g.logW;
+    a_ow[j] = rem & (Wd - 1);
+    a_base[j] = (int64_t)b * HW * g.Cin;
   }
-  int b_row[B_PT], b_ch[B_PT];
+  int b_ch[B_INS];
+  const bf16_t* b_src[B_INS];
+  bool b_ok[B_INS];
 #pragma unroll
-  for (int i = 0; i < B_PT; ++i) {
-    const int q = tid + i * NT;
-    b_row[i] = q / CPR;
-    b_ch[i] = q % CPR;
+  for (int j = 0; j < B_INS; ++j) {
+    const int row = 8 * (wid * B_INS + j) + (lane >> 3);
+    b_ch[j] = (lane & 7) ^ ((row >> 1) & 7);
+    const int n = n0 + row;
+    b_ok[j] = n < g.Cout;
+    b_src[j] = w + (int64_t)(b_ok[j] ? n : 0) * g.K;
   }
 
-  uint4 ra[A_PT], rb[B_PT];
-  const uint4 zero4 = make_uint4(0, 0, 0, 0);
-  auto load_tiles = [&](int kt) {
+  auto issue = [&](int kt, int slot) {
+    char* sA = smem + slot * STAGE_BYTES;
+    char* sB = sA + A_BYTES;
 #pragma unroll
-    for (int i = 0; i < A_PT; ++i) {
-      const int kc = kt * CPR + a_ch[i];
+    for (int j = 0; j < A_INS; ++j) {
+      const int kc = kt * CPR + a_ch[j];
       const int kpos = kc >> g.logC8;
       const int c0 = (kc & (C8 - 1)) << 3;
       const int kh = kpos / g.KS, kw = kpos - kh * g.KS;
-      const int ih = a_oh[i] + kh - g.pad, iw = a_ow[i] + kw - g.pad;
-      const bool ok = a_ok[i] && kc < g.Kch && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)Wd;
-      ra[i] = ok ? *reinterpret_cast<const uint4*>(x + a_base[i] + (((int64_t)ih << g.logW) + iw) * g.Cin + c0)
-                 : zero4;
+      const int ih = a_oh[j] + kh - g.pad, iw = a_ow[j] + kw - g.pad;
+      const bool ok = a_ok[j] && kc < g.Kch && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)Wd;
+      const void* src = ok ? (const void*)(x + a_base[j] + (((int64_t)ih << g.logW) + iw) * g.Cin + c0)
+                           : (const void*)g_zero16;
+      glds16(src, sA + (wid * A_INS + j) * 1024);
     }
 #pragma unroll
-    for (int i = 0; i < B_PT; ++i) {
-      const int kc = kt * CPR + b_ch[i];
-      const int n = n0 + b_row[i];
-      const bool ok = n < g.Cout && kc < g.Kch;
-      rb[i] = ok ? *reinterpret_cast<const uint4*>(w + (int64_t)n * g.K + (int64_t)kc * 8) : zero4;
+    for (int j = 0; j < B_INS; ++j) {
+      const int kc = kt * CPR + b_ch[j];
+      const bool ok = b_ok[j] && kc < g.Kch;
+      const void* src = ok ? (const void*)(b_src[j] + (int64_t)kc * 8) : (const void*)g_zero16;
+      glds16(src, sB + (wid * B_INS + j) * 1024);
     }
-  };
-  auto store_tiles = [&](int buf) {
-    uint4* As = smem + buf * (A_CH + B_CH);
-    uint4* Bs = As + A_CH;
-#pragma unroll
-    for (int i = 0; i < A_PT; ++i) As[swz_row<CPR>(a_row[i], a_ch[i])] = ra[i];
-#pragma unroll
-    for (int i = 0; i < B_PT; ++i) Bs[swz_row<CPR>(b_row[i], b_ch[i])] = rb[i];
   };
 
   f32x4 acc[FM][FN];
@@ -188,169 +228,235 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const bf16_t* __restrict_
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (g.Kch + CPR - 1) / CPR;
-  load_tiles(0);
-  store_tiles(0);
-  __syncthreads();
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) load_tiles(kt + 1);
-    const uint4* As = smem + cur * (A_CH + B_CH);
-    const uint4* Bs = As + A_CH;
+  if (nk > 0) issue(kt_beg, 0);
+  if (nk > 1) issue(kt_beg + 1, 1);
+  for (int i = 0; i < nk; ++i) {
+    if (i + 1 < nk) wait_vmcnt<LPS>(); else wait_vmcnt<0>();
+    block_sync_lds();  // stage i landed for every wave; slot (i+2)%3 no longer read
+    if (i + 2 < nk) issue(kt_beg + i + 2, (i + 2) % STAGES);
+    const uint4* As = reinterpret_cast<const uint4*>(smem + (i % STAGES) * STAGE_BYTES);
+    const uint4* Bs = reinterpret_cast<const uint4*>(smem + (i % STAGES) * STAGE_BYTES + A_BYTES);
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
       bf16x8 af[FM], bfr[FN];
       const int ch = kk * 4 + (lane >> 4);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        uint4 v = As[swz_row<CPR>(wm * TM + i * 16 + (lane & 15), ch)];
-        af[i] = __builtin_bit_cast(bf16x8, v);
-      }
+      for (int a = 0; a < FM; ++a)
+        af[a] = __builtin_bit_cast(bf16x8, As[swz_row<CPR>(wm * TM + a * 16 + (lane & 15), ch)]);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        uint4 v = Bs[swz_row<CPR>(wn * TN + j * 16 + (lane & 15), ch)];
-        bfr[j] = __builtin_bit_cast(bf16x8, v);
-      }
+      for (int b = 0; b < FN; ++b)
+        bfr[b] = __builtin_bit_cast(bf16x8, Bs[swz_row<CPR>(wn * TN + b * 16 + (lane & 15), ch)]);
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+      for (int a = 0; a < FM; ++a)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+        for (int b = 0; b < FN; ++b) acc[a][b] = mfma16(af[a], bfr[b], acc[a][b]);
     }
-    if (kt + 1 < nk) store_tiles(cur ^ 1);
-    __syncthreads();
-    cur ^= 1;
   }
 
-  // ---- epilogue: bf16 store (+ BN statistics of the stored values)
   const int col_l = lane & 15, rq = lane >> 4;
-  float s1[FN], s2[FN];
+  if constexpr (SLAB) {
+    float* o = slab + (int64_t)split * g.M * g.Cout;
 #pragma unroll
-  for (int j = 0; j < FN; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+    for (int a = 0; a < FM; ++a)
 #pragma unroll
-  for (int i = 0; i < FM; ++i) {
+      for (int b = 0; b < FN; ++b) {
+        const int n = n0 + wn * TN + b * 16 + col_l;
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = n0 + wn * TN + j * 16 + col_l;
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * TM + a * 16 + rq * 4 + r;
+          if (m < g.M && n < g.Cout) o[(int64_t)m * g.Cout + n] = acc[a][b][r];
+        }
+      }
+    return;
+  } else {
+    float s1[FN], s2[FN];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * TM + i * 16 + rq * 4 + r;
-        const bf16_t hv = f32_to_bf16(acc[i][j][r]);
-        if (m < g.M && n < g.Cout) y[(int64_t)m * g.Cout + n] = hv;
-        if constexpr (STATS) {
-          const float v = bf16_to_f32(hv);  // statistics of exactly what is stored (0 for m >= M)
-          s1[j] += v;
-          s2[j] += v * v;
+    for (int b = 0; b < FN; ++b) { s1[b] = 0.f; s2[b] = 0.f; }
+#pragma unroll
+    for (int a = 0; a < FM; ++a) {
+#pragma unroll
+      for (int b = 0; b < FN; ++b) {
+        const int n = n0 + wn * TN + b * 16 + col_l;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * TM + a * 16 + rq * 4 + r;
+          const bf16_t hv = f32_to_bf16(acc[a][b][r]);
+          if (m < g.M && n < g.Cout) y[(int64_t)m * g.Cout + n] = hv;
+          if constexpr (STATS) {
+            const float v = bf16_to_f32(hv);  // statistics of exactly what is stored (0 for m >= M)
+            s1[b] += v;
+            s2[b] += v * v;
+          }
+        }
+      }
+    }
+    if constexpr (STATS) {
+      __syncthreads();  // every wave done with the LDS ring (no DMA in flight: nk loop drained it)
+      float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]
+#pragma unroll
+      for (int b = 0; b < FN; ++b) {
+        s1[b] += __shfl_xor(s1[b], 16, 64);
+        s1[b] += __shfl_xor(s1[b], 32, 64);
+        s2[b] += __shfl_xor(s2[b], 16, 64);
+        s2[b] += __shfl_xor(s2[b], 32, 64);
+        if (rq == 0) {
+          red[(wm * 2 + 0) * BN + wn * TN + b * 16 + col_l] = s1[b];
+          red[(wm * 2 + 1) * BN + wn * TN + b * 16 + col_l] = s2[b];
+        }
+      }
+      __syncthreads();
+      for (int c = tid; c < BN; c += NT) {
+        const int n = n0 + c;
+        if (n < g.Cout) {
+          float sa = 0.f, sb = 0.f;
+#pragma unroll
+          for (int q = 0; q < WM; ++q) { sa += red[(q * 2) * BN + c]; sb += red[(q * 2 + 1) * BN + c]; }
+          stats[(int64_t)tm * 2 * g.Cout + n] = sa;
+          stats[(int64_t)tm * 2 * g.Cout + g.Cout + n] = sb;
         }
       }
     }
   }
-  if constexpr (STATS) {
-    float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]
+}
+
+// split-K combine: y = bf16(sum_s slab[s]) (+ BN partial sums, one row per block)
+template <bool STATS>
+__global__ void __launch_bounds__(256) splitk_combine_kernel(const float* __restrict__ slab, bf16_t* __restrict__ y,
+                                                             float* __restrict__ stats, int splits, int M, int N,
+                                                             int rows_per_block) {
+  const int N8 = N >> 3;
+  const int tpr = N8;                 // threads per row (one 8-column chunk each)
+  const int rpi = 256 / tpr;          // rows per iteration
+  const int c8 = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  float s1[8], s2[8];
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      s1[j] += __shfl_xor(s1[j], 16, 64);
-      s1[j] += __shfl_xor(s1[j], 32, 64);
-      s2[j] += __shfl_xor(s2[j], 16, 64);
-      s2[j] += __shfl_xor(s2[j], 32, 64);
-      if (rq == 0) {
-        red[(wm * 2 + 0) * BN + wn * TN + j * 16 + col_l] = s1[j];
-        red[(wm * 2 + 1) * BN + wn * TN + j * 16 + col_l] = s2[j];
+  for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
+  if (rsub < rpi) {
+    for (int m = r0 + rsub; m < r1; m += rpi) {
+      float v[8];
+      const float* p = slab + (int64_t)m * N + c8 * 8;
+      {
+        const float4 a = *reinterpret_cast<const float4*>(p);
+        const float4 b = *reinterpret_cast<const float4*>(p + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      }
+      for (int s = 1; s < splits; ++s) {
+        const float* q = p + (int64_t)s * M * N;
+        const float4 a = *reinterpret_cast<const float4*>(q);
+        const float4 b = *reinterpret_cast<const float4*>(q + 4);
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+      }
+      uint4 o;
+      o.x = pack_bf16x2(v[0], v[1]); o.y = pack_bf16x2(v[2], v[3]);
+      o.z = pack_bf16x2(v[4], v[5]); o.w = pack_bf16x2(v[6], v[7]);
+      *reinterpret_cast<uint4*>(y + (int64_t)m * N + c8 * 8) = o;
+      if constexpr (STATS) {
+        const float h[8] = {lo_bf16(o.x), hi_bf16(o.x), lo_bf16(o.y), hi_bf16(o.y),
+                            lo_bf16(o.z), hi_bf16(o.z), lo_bf16(o.w), hi_bf16(o.w)};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { s1[k] += h[k]; s2[k] += h[k] * h[k]; }
       }
     }
-    __syncthreads();
-    for (int c = tid; c < BN; c += NT) {
-      const int n = n0 + c;
-      if (n < g.Cout) {
-        float a = 0.f, b = 0.f;
+  }
+  if constexpr (STATS) {
+    __shared__ float red[256][17];
 #pragma unroll
-        for (int q = 0; q < WM; ++q) { a += red[(q * 2) * BN + c]; b += red[(q * 2 + 1) * BN + c]; }
-        stats[(int64_t)tm * 2 * g.Cout + n] = a;
-        stats[(int64_t)tm * 2 * g.Cout + g.Cout + n] = b;
-      }
+    for (int k = 0; k < 8; ++k) { red[threadIdx.x][k] = s1[k]; red[threadIdx.x][8 + k] = s2[k]; }
+    __syncthreads();
+    for (int c = threadIdx.x; c < N; c += 256) {
+      const int ch = c >> 3, k = c & 7;
+      float a = 0.f, b = 0.f;
+      for (int t = ch; t < rpi * tpr; t += tpr) { a += red[t][k]; b += red[t][8 + k]; }
+      stats[(int64_t)blockIdx.x * 2 * N + c] = a;
+      stats[(int64_t)blockIdx.x * 2 * N + N + c] = b;
     }
   }
 }
 
 // --------------------------------------------------------------------------
 // wgrad implicit GEMM: out[split][co][k] = sum_{m in split} dy[m][co] * im2col(x)[m][k]
+// Tiles are staged [m][col] (rows = the reduction index) by LDS-DMA and read
+// as MFMA operands with ds_read_b64_tr_b16.  BK = 64 rows of m per stage.
 // --------------------------------------------------------------------------
-template <int BM, int BN, int BK>
+template <int BM, int BN>
 __global__ void __launch_bounds__(256) conv_wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                          float* __restrict__ out, const ConvGeom g, int m_per_split,
                                                          int ldo) {
-  constexpr int NT = 256, WM = 2, WN = 2;
+  constexpr int BK = 64, NT = 256, WM = 2, WN = 2, STAGES = 3;
   constexpr int ACPR = BM / 8, BCPR = BN / 8;  // chunks per LDS row (row = one m)
-  constexpr int A_CH = BK * ACPR, B_CH = BK * BCPR;
-  constexpr int A_PT = A_CH / NT, B_PT = B_CH / NT;
-  static_assert(A_CH % NT == 0 && B_CH % NT == 0, "tile/thread mismatch");
+  constexpr int A_BYTES = BK * BM * 2, B_BYTES = BK * BN * 2, STAGE_BYTES = A_BYTES + B_BYTES;
+  constexpr int A_INS = A_BYTES / 1024 / 4, B_INS = B_BYTES / 1024 / 4;
+  constexpr int LPS = A_INS + B_INS;
+  constexpr int A_RPI = 64 / ACPR, B_RPI = 64 / BCPR;  // rows per glds instruction
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
-  __shared__ __attribute__((aligned(16))) uint4 smem[2 * (A_CH + B_CH)];
+  static_assert(A_INS >= 1 && B_INS >= 1, "tile too small");
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const int ntm = (g.Cout + BM - 1) / BM, ntn = (g.Kch * 8 + BN - 1) / BN;
+  const int splits = gridDim.y;
   const int tile = xcd_swizzle(blockIdx.x, ntm * ntn);
   const int tm = tile % ntm, tn = tile / ntm;
   const int co0 = tm * BM, k0 = tn * BN;
   const int split = blockIdx.y;
+  (void)splits;
   const int mbeg = split * m_per_split;
   const int mend = min(g.M, mbeg + m_per_split);
   const int HW = 1 << g.logHW, Wd = g.W, C8 = 1 << g.logC8;
 
-  // A (dy) chunks: row r (m), chunk c (8 channels of co)
-  int a_r[A_PT], a_c[A_PT];
+  // A (dy) lanes: row = A_RPI*(wid*A_INS + j) + lane/ACPR, chunk fixed
+  int a_row[A_INS], a_co[A_INS];
+  bool a_cok[A_INS];
 #pragma unroll
-  for (int i = 0; i < A_PT; ++i) {
-    const int q = tid + i * NT;
-    a_r[i] = q / ACPR;
-    a_c[i] = q % ACPR;
+  for (int j = 0; j < A_INS; ++j) {
+    const int row = A_RPI * (wid * A_INS + j) + lane / ACPR;
+    a_row[j] = row;
+    const int ch = swz_tr<ACPR>(row, lane % ACPR) - row * ACPR;  // logical chunk (involution)
+    a_co[j] = co0 + ch * 8;
+    a_cok[j] = a_co[j] < g.Cout;
   }
-  // B (im2col) chunks: row r (m), chunk c -> fixed tap (dh, dw, c0)
-  int b_r[B_PT], b_c[B_PT], b_dh[B_PT], b_dw[B_PT], b_c0[B_PT];
-  bool b_kok[B_PT];
+  // B (im2col) lanes: chunk -> fixed tap (dh, dw, c0)
+  int b_row[B_INS], b_dh[B_INS], b_dw[B_INS], b_c0[B_INS];
+  bool b_kok[B_INS];
 #pragma unroll
-  for (int i = 0; i < B_PT; ++i) {
-    const int q = tid + i * NT;
-    b_r[i] = q / BCPR;
-    b_c[i] = q % BCPR;
-    const int kc = k0 / 8 + b_c[i];
-    b_kok[i] = kc < g.Kch;
+  for (int j = 0; j < B_INS; ++j) {
+    const int row = B_RPI * (wid * B_INS + j) + lane / BCPR;
+    b_row[j] = row;
+    const int ch = swz_tr<BCPR>(row, lane % BCPR) - row * BCPR;
+    const int kc = k0 / 8 + ch;
+    b_kok[j] = kc < g.Kch;
     const int kpos = kc >> g.logC8;
-    b_c0[i] = (kc & (C8 - 1)) << 3;
+    b_c0[j] = (kc & (C8 - 1)) << 3;
     const int kh = kpos / g.KS;
-    b_dh[i] = kh - g.pad;
-    b_dw[i] = kpos - kh * g.KS - g.pad;
+    b_dh[j] = kh - g.pad;
+    b_dw[j] = kpos - kh * g.KS - g.pad;
   }
 
-  uint4 ra[A_PT], rb[B_PT];
-  const uint4 zero4 = make_uint4(0, 0, 0, 0);
-  auto load_tiles = [&](int kt) {
+  auto issue = [&](int kt, int slot) {
+    char* sA = smem + slot * STAGE_BYTES;
+    char* sB = sA + A_BYTES;
     const int mb = mbeg + kt * BK;
 #pragma unroll
-    for (int i = 0; i < A_PT; ++i) {
-      const int m = mb + a_r[i];
-      const int co = co0 + a_c[i] * 8;
-      const bool ok = m < mend && co < g.Cout;
-      ra[i] = ok ? *reinterpret_cast<const uint4*>(dy + (int64_t)m * g.Cout + co) : zero4;
+    for (int j = 0; j < A_INS; ++j) {
+      const int m = mb + a_row[j];
+      const bool ok = m < mend && a_cok[j];
+      const void* src = ok ? (const void*)(dy + (int64_t)m * g.Cout + a_co[j]) : (const void*)g_zero16;
+      glds16(src, sA + (wid * A_INS + j) * 1024);
     }
 #pragma unroll
-    for (int i = 0; i < B_PT; ++i) {
-      const int m = mb + b_r[i];
+    for (int j = 0; j < B_INS; ++j) {
+      const int m = mb + b_row[j];
       const int b = m >> g.logHW, rem = m & (HW - 1);
-      const int ih = (rem >> g.logW) + b_dh[i], iw = (rem & (Wd - 1)) + b_dw[i];
-      const bool ok = m < mend && b_kok[i] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)Wd;
-      rb[i] = ok ? *reinterpret_cast<const uint4*>(x + ((int64_t)b * HW + ((int64_t)ih << g.logW) + iw) * g.Cin +
-                                                   b_c0[i])
-                 : zero4;
+      const int ih = (rem >> g.logW) + b_dh[j], iw = (rem & (Wd - 1)) + b_dw[j];
+      const bool ok = m < mend && b_kok[j] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)Wd;
+      const void* src = ok ? (const void*)(x + ((int64_t)b * HW + ((int64_t)ih << g.logW) + iw) * g.Cin + b_c0[j])
+                           : (const void*)g_zero16;
+      glds16(src, sB + (wid * B_INS + j) * 1024);
     }
-  };
-  auto store_tiles = [&](int buf) {
-    uint4* As = smem + buf * (A_CH + B_CH);
-    uint4* Bs = As + A_CH;
-#pragma unroll
-    for (int i = 0; i < A_PT; ++i) As[swz_tr<ACPR>(a_r[i], a_c[i])] = ra[i];
-#pragma unroll
-    for (int i = 0; i < B_PT; ++i) Bs[swz_tr<BCPR>(b_r[i], b_c[i])] = rb[i];
   };
 
   f32x4 acc[FM][FN];
@@ -359,62 +465,54 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const bf16_t* __restric
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // transposed-read lane roles: group gq = lane>>4 (k rows 8gq..8gq+7),
-  // within the group lane 4q+p -> row q, columns 4p..4p+3
   const int gq = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
-  const int nk = (mend - mbeg + BK - 1) / BK;
-  if (nk > 0) {
-    load_tiles(0);
-    store_tiles(0);
-  }
-  __syncthreads();
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) load_tiles(kt + 1);
-    const char* As = reinterpret_cast<const char*>(smem + cur * (A_CH + B_CH));
-    const char* Bs = As + A_CH * 16;
+  const int nk = max(0, (mend - mbeg + BK - 1) / BK);
+  if (nk > 0) issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  for (int i = 0; i < nk; ++i) {
+    if (i + 1 < nk) wait_vmcnt<LPS>(); else wait_vmcnt<0>();
+    block_sync_lds();
+    if (i + 2 < nk) issue(i + 2, (i + 2) % STAGES);
+    const char* As = smem + (i % STAGES) * STAGE_BYTES;
+    const char* Bs = As + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
       bf16x8 af[FM], bfr[FN];
+      const int r0 = kk * 32 + gq * 8 + q4;
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int col = wm * TM + i * 16 + 4 * p4;  // first of 4 columns (co)
+      for (int a = 0; a < FM; ++a) {
+        const int col = wm * TM + a * 16 + 4 * p4;
         const int ch = col >> 3, sub = (col & 7) * 2;
-        const int r0 = kk * 32 + gq * 8 + q4;
         s16x4 lo = ds_read_tr16(As + swz_tr<ACPR>(r0, ch) * 16 + sub);
         s16x4 hi = ds_read_tr16(As + swz_tr<ACPR>(r0 + 4, ch) * 16 + sub);
-        af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[a] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int col = wn * TN + j * 16 + 4 * p4;
+      for (int b = 0; b < FN; ++b) {
+        const int col = wn * TN + b * 16 + 4 * p4;
         const int ch = col >> 3, sub = (col & 7) * 2;
-        const int r0 = kk * 32 + gq * 8 + q4;
         s16x4 lo = ds_read_tr16(Bs + swz_tr<BCPR>(r0, ch) * 16 + sub);
         s16x4 hi = ds_read_tr16(Bs + swz_tr<BCPR>(r0 + 4, ch) * 16 + sub);
-        bfr[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[b] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+      for (int a = 0; a < FM; ++a)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+        for (int b = 0; b < FN; ++b) acc[a][b] = mfma16(af[a], bfr[b], acc[a][b]);
     }
-    if (kt + 1 < nk) store_tiles(cur ^ 1);
-    __syncthreads();
-    cur ^= 1;
   }
 
   float* o = out + (int64_t)split * g.Cout * ldo;
   const int col_l = lane & 15, rq = lane >> 4;
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+  for (int a = 0; a < FM; ++a)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int k = k0 + wn * TN + j * 16 + col_l;
+    for (int b = 0; b < FN; ++b) {
+      const int k = k0 + wn * TN + b * 16 + col_l;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wm * TM + i * 16 + rq * 4 + r;
-        if (co < g.Cout && k < ldo) o[(int64_t)co * ldo + k] = acc[i][j][r];
+        const int co = co0 + wm * TM + a * 16 + rq * 4 + r;
+        if (co < g.Cout && k < ldo) o[(int64_t)co * ldo + k] = acc[a][b][r];
       }
     }
 }
@@ -479,63 +577,175 @@ __global__ void __launch_bounds__(256) pad_channels_kernel(const bf16_t* __restr
 }
 
 // --------------------------------------------------------------------------
-// host launchers
+// Per-step operand preparation in ONE launch (was 5): zero-pad the input
+// image channels, pack the first layer's fp32 weights to padded bf16, and
+// flip+transpose the bf16 weights of every later layer for its dgrad.
+// Job = blockIdx range; each transpose block moves one 32x32 (co, ci) tile of
+// one tap through LDS.
 // --------------------------------------------------------------------------
-template <int BM, int BN, int BK, bool STATS>
-static void launch_fwd(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, hipStream_t s) {
-  const int ntm = (g.M + BM - 1) / BM, ntn = (g.Cout + BN - 1) / BN;
-  conv_fwd_kernel<BM, BN, BK, STATS><<<ntm * ntn, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y,
-                                                                (float*)stats, g);
-}
+struct PrepArgs {
+  const bf16_t* x; bf16_t* xp; int64_t P; int C, Cp;            // input pad
+  const float* w1; bf16_t* w1p; int w1_cout, taps, w1_c, w1_cp;  // layer-1 pack
+  int nt;                                                        // transposes
+  const bf16_t* tw[4]; bf16_t* twt[4]; int tcout[4], tcin[4];
+  int nb_pad, nb_pack, nb_t[4];
+};
 
-int conv_fwd_mtile(int B, int H, int W, int Cin, int Cout, int KS, int tile) {
-  (void)B; (void)H; (void)W; (void)Cin; (void)Cout; (void)KS;
-  return tile == 1 ? 64 : 128;
-}
-
-// tile: 0 = 128x128, 1 = 64x64, 2 = 128x64   (BK = 64; BK = 32 when K is small)
-void conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int B, int H, int W, int Cin, int Cout, int KS,
-              int tile, uintptr_t stream) {
-  ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
-  hipStream_t s = as_stream(stream);
-  const bool st = stats != 0;
-  const bool smallK = g.K <= 256;
-#define DL_FWD(BM_, BN_, BK_)                                        \
-  do {                                                               \
-    if (st) launch_fwd<BM_, BN_, BK_, true>(g, x, w, y, stats, s);   \
-    else launch_fwd<BM_, BN_, BK_, false>(g, x, w, y, stats, s);     \
-  } while (0)
-  if (tile == 0) {
-    if (smallK) DL_FWD(128, 128, 32); else DL_FWD(128, 128, 64);
-  } else if (tile == 1) {
-    if (smallK) DL_FWD(64, 64, 32); else DL_FWD(64, 64, 64);
-  } else if (tile == 2) {
-    if (smallK) DL_FWD(128, 64, 32); else DL_FWD(128, 64, 64);
-  } else {
-    throw std::runtime_error("conv_fwd: bad tile id");
+__global__ void __launch_bounds__(256) prep_step_kernel(const PrepArgs a) {
+  __shared__ bf16_t t[32][33];
+  int blk = blockIdx.x;
+  if (blk < a.nb_pad) {
+    for (int64_t p = (int64_t)blk * 256 + threadIdx.x; p < a.P; p += (int64_t)a.nb_pad * 256) {
+      bf16_t v[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v[c] = 0;
+      for (int c = 0; c < a.C; ++c) v[c] = a.x[p * a.C + c];
+      for (int c = 0; c < a.Cp; c += 8)
+        *reinterpret_cast<uint4*>(a.xp + p * a.Cp + c) = *reinterpret_cast<const uint4*>(v + c);
+    }
+    return;
   }
-#undef DL_FWD
+  blk -= a.nb_pad;
+  if (blk < a.nb_pack) {
+    const int64_t total = (int64_t)a.w1_cout * a.taps * a.w1_cp;
+    for (int64_t i = (int64_t)blk * 256 + threadIdx.x; i < total; i += (int64_t)a.nb_pack * 256) {
+      const int c = (int)(i % a.w1_cp);
+      a.w1p[i] = c < a.w1_c ? f32_to_bf16(a.w1[(i / a.w1_cp) * a.w1_c + c]) : (bf16_t)0;
+    }
+    return;
+  }
+  blk -= a.nb_pack;
+  for (int j = 0; j < a.nt; ++j) {
+    if (blk >= a.nb_t[j]) { blk -= a.nb_t[j]; continue; }
+    const int Cin = a.tcin[j], Cout = a.tcout[j], taps = a.taps;
+    const int nci = (Cin + 31) / 32, nco = (Cout + 31) / 32;
+    const int tap = blk / (nci * nco);
+    const int r = blk % (nci * nco);
+    const int ci0 = (r % nci) * 32, co0 = (r / nci) * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    for (int q = ty; q < 32; q += 8) {
+      const int co = co0 + q, ci = ci0 + tx;
+      t[q][tx] = (co < Cout && ci < Cin) ? a.tw[j][((int64_t)co * taps + tap) * Cin + ci] : (bf16_t)0;
+    }
+    __syncthreads();
+    const int ftap = taps - 1 - tap;
+    for (int q = ty; q < 32; q += 8) {
+      const int ci = ci0 + q, co = co0 + tx;
+      if (ci < Cin && co < Cout) a.twt[j][((int64_t)ci * taps + ftap) * Cout + co] = t[tx][q];
+    }
+    return;
+  }
+}
+
+void prep_step(uintptr_t x, uintptr_t xp, int64_t P, int C, int Cp, uintptr_t w1, uintptr_t w1p, int w1_cout,
+               int taps, int w1_c, int w1_cp, std::vector<uintptr_t> tw, std::vector<uintptr_t> twt,
+               std::vector<int> tcout, std::vector<int> tcin, uintptr_t stream) {
+  PrepArgs a{};
+  if (C > 16 || Cp > 16 || Cp % 8 != 0) throw std::runtime_error("prep_step: input channels must pad to 8 or 16");
+  a.x = (const bf16_t*)x; a.xp = (bf16_t*)xp; a.P = P; a.C = C; a.Cp = Cp;
+  a.w1 = (const float*)w1; a.w1p = (bf16_t*)w1p; a.w1_cout = w1_cout; a.taps = taps; a.w1_c = w1_c; a.w1_cp = w1_cp;
+  a.nt = (int)tw.size();
+  if (a.nt > 4 || twt.size() != tw.size() || tcout.size() != tw.size() || tcin.size() != tw.size())
+    throw std::runtime_error("prep_step: up to 4 consistent transposes");
+  a.nb_pad = (int)std::min<int64_t>((P + 255) / 256, 1024);
+  a.nb_pack = (int)std::min<int64_t>(((int64_t)w1_cout * taps * w1_cp + 255) / 256, 256);
+  int total = a.nb_pad + a.nb_pack;
+  for (int j = 0; j < a.nt; ++j) {
+    a.tw[j] = (const bf16_t*)tw[j]; a.twt[j] = (bf16_t*)twt[j];
+    a.tcout[j] = tcout[j]; a.tcin[j] = tcin[j];
+    a.nb_t[j] = ((tcin[j] + 31) / 32) * ((tcout[j] + 31) / 32) * taps;
+    total += a.nb_t[j];
+  }
+  prep_step_kernel<<<total, 256, 0, as_stream(stream)>>>(a);
   DL_HIP_CHECK(hipGetLastError());
 }
 
-// out: fp32 [splits][Cout][ldo], ldo >= K (K = KS*KS*Cin)
+// --------------------------------------------------------------------------
+// host launchers
+// --------------------------------------------------------------------------
+static int fwd_bm(int tile) { return tile == 1 ? 64 : 128; }
+static int fwd_bn(int tile) { return tile == 0 ? 128 : 64; }
+
+static int combine_rows_per_block(int M, int N) {
+  const int rpi = 256 / (N / 8);
+  int rpb = (M + 383) / 384;            // ~384 blocks
+  rpb = ((rpb + rpi - 1) / rpi) * rpi;  // whole iterations
+  return rpb < rpi ? rpi : rpb;
+}
+
+// number of BN partial-sum rows conv_fwd writes for this configuration
+int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile, int splits) {
+  ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
+  if (splits <= 1) return (g.M + fwd_bm(tile) - 1) / fwd_bm(tile);
+  const int rpb = combine_rows_per_block(g.M, Cout);
+  return (g.M + rpb - 1) / rpb;
+}
+
+template <int BM, int BN>
+static void launch_fwd(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab,
+                       int splits, hipStream_t s) {
+  const int ntm = (g.M + BM - 1) / BM, ntn = (g.Cout + BN - 1) / BN;
+  const int nkt = (g.Kch + 7) / 8;
+  const int ktps = (nkt + splits - 1) / splits;
+  const int grid = ntm * ntn * splits;
+  if (splits > 1)
+    conv_fwd_kernel<BM, BN, false, true><<<grid, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)w, nullptr, nullptr,
+                                                               (float*)slab, g, splits, ktps);
+  else if (stats)
+    conv_fwd_kernel<BM, BN, true, false><<<grid, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y,
+                                                               (float*)stats, nullptr, g, 1, ktps);
+  else
+    conv_fwd_kernel<BM, BN, false, false><<<grid, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y,
+                                                                nullptr, nullptr, g, 1, ktps);
+}
+
+// tile: 0 = 128x128, 1 = 64x64, 2 = 128x64 (BM x BN, BK = 64).  splits > 1:
+// split-K into `slab` (fp32 [splits][M][Cout]) + combine (bf16 y, BN partials).
+// Returns the number of BN partial rows written to `stats` (if non-null).
+int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab, int B, int H, int W, int Cin,
+             int Cout, int KS, int tile, int splits, uintptr_t stream) {
+  ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
+  hipStream_t s = as_stream(stream);
+  if (splits < 1) splits = 1;
+  if (splits > 1 && !slab) throw std::runtime_error("conv_fwd: split-K needs a slab");
+  if (Cout % 8 != 0) throw std::runtime_error("conv_fwd: Cout % 8 != 0");
+  if (tile == 0) launch_fwd<128, 128>(g, x, w, y, stats, slab, splits, s);
+  else if (tile == 1) launch_fwd<64, 64>(g, x, w, y, stats, slab, splits, s);
+  else if (tile == 2) launch_fwd<128, 64>(g, x, w, y, stats, slab, splits, s);
+  else throw std::runtime_error("conv_fwd: bad tile id");
+  DL_HIP_CHECK(hipGetLastError());
+  if (splits == 1) return (g.M + fwd_bm(tile) - 1) / fwd_bm(tile);
+  if (256 % (Cout / 8) != 0) throw std::runtime_error("conv_fwd split-K combine: Cout/8 must divide 256");
+  const int rpb = combine_rows_per_block(g.M, Cout);
+  const int nb = (g.M + rpb - 1) / rpb;
+  if (stats)
+    splitk_combine_kernel<true><<<nb, 256, 0, s>>>((const float*)slab, (bf16_t*)y, (float*)stats, splits, g.M, Cout,
+                                                   rpb);
+  else
+    splitk_combine_kernel<false><<<nb, 256, 0, s>>>((const float*)slab, (bf16_t*)y, nullptr, splits, g.M, Cout, rpb);
+  DL_HIP_CHECK(hipGetLastError());
+  return nb;
+}
+
+// out: fp32 [splits][Cout][ldo], ldo >= K (K = KS*KS*Cin); tile 0 = 128x64, 1 = 64x64 (co x k)
 void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, int Cin, int Cout, int KS, int splits,
                 int ldo, int tile, uintptr_t stream) {
   ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
   if (ldo < g.K) throw std::runtime_error("conv_wgrad: ldo < K");
+  if (Cout % 8 != 0) throw std::runtime_error("conv_wgrad: Cout % 8 != 0");
   if (splits < 1) splits = 1;
   int mps = (g.M + splits - 1) / splits;
   hipStream_t s = as_stream(stream);
   if (tile == 0) {
-    constexpr int BM = 128, BN = 64, BK = 32;
+    constexpr int BM = 128, BN = 64;
     const int nt = ((g.Cout + BM - 1) / BM) * ((g.K + BN - 1) / BN);
-    conv_wgrad_kernel<BM, BN, BK><<<dim3(nt, splits), 256, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (float*)out,
-                                                                   g, mps, ldo);
+    conv_wgrad_kernel<BM, BN><<<dim3(nt, splits), 256, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (float*)out, g,
+                                                               mps, ldo);
   } else {
-    constexpr int BM = 64, BN = 64, BK = 32;
+    constexpr int BM = 64, BN = 64;
     const int nt = ((g.Cout + BM - 1) / BM) * ((g.K + BN - 1) / BN);
-    conv_wgrad_kernel<BM, BN, BK><<<dim3(nt, splits), 256, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (float*)out,
-                                                                   g, mps, ldo);
+    conv_wgrad_kernel<BM, BN><<<dim3(nt, splits), 256, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (float*)out, g,
+                                                               mps, ldo);
   }
   DL_HIP_CHECK(hipGetLastError());
 }

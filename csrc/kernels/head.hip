@@ -1,0 +1,177 @@
+// Classifier head: Linear(F, C) -> LogSoftMax -> ClassNLLCriterion (mean),
+// forward AND backward fused (gfx950).
+//
+// Reference: grad.nn.Linear(512*2*2, 10) + grad.nn.LogSoftMax +
+// grad.nn.ClassNLLCriterion (examples/cifar10.lua:132-143,159-163),
+// util.logSoftMax + logMultinomialLoss (examples/mnist.lua:79,86); SURVEY §2.8
+// K17/K18.  The head is tiny (B x 10 x 2048), so it is two kernels instead of
+// six library calls:
+//   head_fwd_bwd : one workgroup per sample: logits = W h + b, log-softmax, loss,
+//                  dlogits = (softmax - onehot)/B, dh = W^T dlogits (bf16, feeds
+//                  the last conv block's backward); or logits only (predict)
+//   head_wgrad   : dW[c][j] = sum_b dlogits[b][c] h[b][j], db, mean loss
+//                  (fixed summation order: deterministic)
+#include "dl_common.h"
+#include "dl_ops.h"
+
+namespace dl {
+
+template <int NC>
+__global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restrict__ h, const float* __restrict__ w,
+                                                           const float* __restrict__ bias,
+                                                           const int64_t* __restrict__ labels, int F, int B,
+                                                           float* __restrict__ logits_out, float* __restrict__ dlogits,
+                                                           float* __restrict__ loss_b, bf16_t* __restrict__ dh) {
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ float red[4][NC];
+  __shared__ float dl[NC];
+  const bf16_t* hb = h + (int64_t)b * F;
+  float acc[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) acc[c] = 0.f;
+  for (int j0 = tid * 8; j0 < F; j0 += 256 * 8) {
+    const uint4 hv = *reinterpret_cast<const uint4*>(hb + j0);
+    float hf[8] = {lo_bf16(hv.x), hi_bf16(hv.x), lo_bf16(hv.y), hi_bf16(hv.y),
+                   lo_bf16(hv.z), hi_bf16(hv.z), lo_bf16(hv.w), hi_bf16(hv.w)};
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const float4 w0 = *reinterpret_cast<const float4*>(w + (int64_t)c * F + j0);
+      const float4 w1 = *reinterpret_cast<const float4*>(w + (int64_t)c * F + j0 + 4);
+      acc[c] += hf[0] * w0.x + hf[1] * w0.y + hf[2] * w0.z + hf[3] * w0.w + hf[4] * w1.x + hf[5] * w1.y +
+                hf[6] * w1.z + hf[7] * w1.w;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const float v = wave_sum(acc[c]);
+    if (lane == 0) red[wid][c] = v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float lg[NC], mx = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      lg[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c] + bias[c];
+      mx = fmaxf(mx, lg[c]);
+    }
+    float se = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) se += __expf(lg[c] - mx);
+    const float lse = mx + __logf(se);
+    if (logits_out) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) logits_out[(int64_t)b * NC + c] = lg[c] - lse;  // log-probabilities
+    }
+    if (labels) {
+      const int y = (int)labels[b];
+      float lb = 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const float p = __expf(lg[c] - lse);
+        const float d = (p - (c == y ? 1.f : 0.f)) / (float)B;
+        dl[c] = d;
+        dlogits[(int64_t)b * NC + c] = d;
+        if (c == y) lb = lse - lg[c];
+      }
+      loss_b[b] = lb;
+    }
+  }
+  if (!labels) return;
+  __syncthreads();
+  float d[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) d[c] = dl[c];
+  for (int j0 = tid * 8; j0 < F; j0 += 256 * 8) {
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const float4 w0 = *reinterpret_cast<const float4*>(w + (int64_t)c * F + j0);
+      const float4 w1 = *reinterpret_cast<const float4*>(w + (int64_t)c * F + j0 + 4);
+      o[0] += d[c] * w0.x; o[1] += d[c] * w0.y; o[2] += d[c] * w0.z; o[3] += d[c] * w0.w;
+      o[4] += d[c] * w1.x; o[5] += d[c] * w1.y; o[6] += d[c] * w1.z; o[7] += d[c] * w1.w;
+    }
+    *reinterpret_cast<uint4*>(dh + (int64_t)b * F + j0) =
+        make_uint4(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]), pack_bf16x2(o[6], o[7]));
+  }
+}
+
+// dW[c][j] (fp32, written into the flat grad), db[c], loss = mean(loss_b).
+// Block = 32 columns x 8 row groups; fixed-order reductions (deterministic).
+template <int NC>
+__global__ void __launch_bounds__(256) head_wgrad_kernel(const bf16_t* __restrict__ h,
+                                                         const float* __restrict__ dlogits,
+                                                         const float* __restrict__ loss_b, int F, int B,
+                                                         float* __restrict__ dw, float* __restrict__ db,
+                                                         float* __restrict__ loss) {
+  __shared__ float red[8][NC + 1][33];
+  const int tid = threadIdx.x, col = tid & 31, grp = tid >> 5;
+  const int nblk_cols = (F + 31) / 32;
+  if ((int)blockIdx.x < nblk_cols) {
+    const int j = blockIdx.x * 32 + col;
+    float acc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] = 0.f;
+    if (j < F) {
+      for (int b = grp; b < B; b += 8) {
+        const float hv = bf16_to_f32(h[(int64_t)b * F + j]);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[c] += dlogits[(int64_t)b * NC + c] * hv;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) red[grp][c][col] = acc[c];
+    __syncthreads();
+    for (int o = tid; o < NC * 32; o += 256) {
+      const int c = o / 32, cc = o % 32;
+      float s = 0.f;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) s += red[g][c][cc];
+      const int jj = blockIdx.x * 32 + cc;
+      if (jj < F) dw[(int64_t)c * F + jj] = s;
+    }
+  } else {
+    // bias gradient and mean loss: rows b split over 8 groups x 32 lanes
+    float acc[NC + 1];
+#pragma unroll
+    for (int c = 0; c <= NC; ++c) acc[c] = 0.f;
+    for (int b = tid; b < B; b += 256) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) acc[c] += dlogits[(int64_t)b * NC + c];
+      acc[NC] += loss_b[b];
+    }
+#pragma unroll
+    for (int c = 0; c <= NC; ++c) red[grp][c][col] = acc[c];
+    __syncthreads();
+    if (tid <= NC) {
+      float s = 0.f;
+      for (int g = 0; g < 8; ++g)
+        for (int cc = 0; cc < 32; ++cc) s += red[g][tid][cc];
+      if (tid < NC) {
+        if (db) db[tid] = s;
+      } else if (loss) {
+        *loss = s / (float)B;
+      }
+    }
+  }
+}
+
+void head_fwd_bwd(uintptr_t h, uintptr_t w, uintptr_t bias, uintptr_t labels, int F, int B, int NC,
+                  uintptr_t logits_out, uintptr_t dlogits, uintptr_t loss_b, uintptr_t dh, uintptr_t stream) {
+  if (NC != 10) throw std::runtime_error("head_fwd_bwd: built for 10 classes");
+  if (F % 8 != 0) throw std::runtime_error("head_fwd_bwd: F % 8 != 0");
+  head_fwd_bwd_kernel<10><<<B, 256, 0, as_stream(stream)>>>((const bf16_t*)h, (const float*)w, (const float*)bias,
+                                                            (const int64_t*)labels, F, B, (float*)logits_out,
+                                                            (float*)dlogits, (float*)loss_b, (bf16_t*)dh);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+void head_wgrad(uintptr_t h, uintptr_t dlogits, uintptr_t loss_b, int F, int B, int NC, uintptr_t dw, uintptr_t db,
+                uintptr_t loss, uintptr_t stream) {
+  if (NC != 10) throw std::runtime_error("head_wgrad: built for 10 classes");
+  head_wgrad_kernel<10><<<(F + 31) / 32 + 1, 256, 0, as_stream(stream)>>>((const bf16_t*)h, (const float*)dlogits,
+                                                                        (const float*)loss_b, F, B, (float*)dw,
+                                                                        (float*)db, (float*)loss);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dl

@@ -1,0 +1,265 @@
+"""Numerics of the hand-written convnet kernels (conv_igemm.hip, bn_pool.hip,
+head.hip) against plain PyTorch fp32 references of the same ops, on the
+reference model's real layer shapes plus small odd ones (non-multiple tiles)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def C():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from torch_distlearn_amd import _native
+
+    return _native.native()
+
+
+def _s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
+
+
+# (B, H, Cin, Cout): the four reference layers (batch 8 / 32) + odd sizes
+CONV_SHAPES = [(8, 32, 8, 64), (8, 16, 64, 128), (8, 8, 128, 256), (32, 4, 256, 512), (3, 8, 16, 40), (5, 4, 32, 24)]
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+@pytest.mark.parametrize("tile", [0, 1, 2])
+@pytest.mark.parametrize("splits", [1, 3])
+def test_conv_fwd_and_stats(C, shape, tile, splits):
+    B, H, cin, cout = shape
+    if splits > 1 and 256 % (cout // 8) != 0:
+        pytest.skip("split-K combine needs Cout/8 | 256")
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(B * H + cin)
+    x = torch.randn(B, H, H, cin, device=dev, generator=g).to(torch.bfloat16)
+    w = (torch.randn(cout, 5, 5, cin, device=dev, generator=g) * 0.05).to(torch.bfloat16)
+    y = torch.empty(B, H, H, cout, dtype=torch.bfloat16, device=dev)
+    rows = C.conv_fwd_stat_rows(B, H, H, cin, cout, 5, tile, splits)
+    stats = torch.full((rows, 2, cout), float("nan"), device=dev)
+    slab = torch.empty(splits * B * H * H * cout, device=dev)
+    T = C.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), stats.data_ptr(), slab.data_ptr(), B, H, H, cin, cout,
+                   5, tile, splits, _s())
+    assert T == rows
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=2).permute(0, 2, 3, 1)
+    torch.cuda.synchronize()
+    assert _rel(y, ref) < 8e-3
+    yf = y.float().reshape(-1, cout)
+    torch.testing.assert_close(stats[:, 0].sum(0), yf.sum(0), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(stats[:, 1].sum(0), (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_dgrad_wgrad(C, shape):
+    B, H, cin, cout = shape
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(11 + B * H + cout)
+    x = torch.randn(B, H, H, cin, device=dev, generator=g).to(torch.bfloat16)
+    w = (torch.randn(cout, 5, 5, cin, device=dev, generator=g) * 0.05).to(torch.bfloat16)
+    dy = torch.randn(B, H, H, cout, device=dev, generator=g).to(torch.bfloat16)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.float().permute(0, 3, 1, 2).requires_grad_(True)
+    out = F.conv2d(xr, wr, padding=2)
+    out.backward(dy.float().permute(0, 3, 1, 2))
+    dx_ref = xr.grad.permute(0, 2, 3, 1)
+    dw_ref = wr.grad.permute(0, 2, 3, 1)
+    # dgrad = forward conv of dy with flipped + transposed weights
+    wt = torch.empty(cin, 5, 5, cout, dtype=torch.bfloat16, device=dev)
+    C.weight_flip_transpose(w.data_ptr(), wt.data_ptr(), cout, cin, 5, _s())
+    torch.cuda.synchronize()
+    assert torch.equal(wt, w.permute(3, 1, 2, 0).flip(1, 2).contiguous())
+    if cout & (cout - 1) == 0:  # dgrad input channels (= Cout) must be a power of two
+        for tile, splits in ((1, 1), (0, 2), (2, 4)):
+            dx = torch.empty(B, H, H, cin, dtype=torch.bfloat16, device=dev)
+            slab = torch.empty(splits * B * H * H * cin, device=dev)
+            if splits > 1 and 256 % (cin // 8) != 0:
+                continue
+            C.conv_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, slab.data_ptr(), B, H, H, cout, cin, 5, tile,
+                       splits, _s())
+            torch.cuda.synchronize()
+            assert _rel(dx, dx_ref) < 8e-3, (tile, splits)
+    K = 25 * cin
+    for tile in (0, 1):
+        for splits in (1, 3):
+            slabs = torch.zeros(splits, cout, K, device=dev)
+            C.conv_wgrad(dy.data_ptr(), x.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, splits, K, tile, _s())
+            dw = torch.empty(cout, 5, 5, cin, device=dev)
+            C.slab_reduce(slabs.data_ptr(), dw.data_ptr(), splits, cout, 25, cin, cin, _s())
+            torch.cuda.synchronize()
+            assert _rel(dw, dw_ref) < 1e-4, (tile, splits, _rel(dw, dw_ref))
+
+
+def test_prep_step(C):
+    """Fused per-step prep: input pad, layer-1 pack, dgrad flip-transposes."""
+    dev = torch.device("cuda")
+    B = 3
+    x3 = torch.randn(B, 32, 32, 3, device=dev).to(torch.bfloat16)
+    x8 = torch.full((B, 32, 32, 8), 7.0, dtype=torch.bfloat16, device=dev)
+    w1 = torch.randn(64, 5, 5, 3, device=dev)
+    w1p = torch.full((64, 5, 5, 8), 7.0, dtype=torch.bfloat16, device=dev)
+    ws = [torch.randn(co, 5, 5, ci, device=dev).to(torch.bfloat16) for ci, co in ((64, 128), (128, 256), (256, 512))]
+    wts = [torch.empty(w.shape[3], 5, 5, w.shape[0], dtype=torch.bfloat16, device=dev) for w in ws]
+    C.prep_step(x3.data_ptr(), x8.data_ptr(), B * 1024, 3, 8, w1.data_ptr(), w1p.data_ptr(), 64, 25, 3, 8,
+                [w.data_ptr() for w in ws], [t.data_ptr() for t in wts], [w.shape[0] for w in ws],
+                [w.shape[3] for w in ws], _s())
+    torch.cuda.synchronize()
+    assert torch.equal(x8[..., :3], x3) and not x8[..., 3:].any()
+    assert torch.equal(w1p[..., :3], w1.to(torch.bfloat16)) and not w1p[..., 3:].any()
+    for w, t in zip(ws, wts):
+        assert torch.equal(t, w.permute(3, 1, 2, 0).flip(1, 2).contiguous())
+
+
+def test_padded_input_layer(C):
+    """Layer 1: 3 channels zero-padded to 8 for the kernels; wgrad slab drops the pad."""
+    dev = torch.device("cuda")
+    B, H = 4, 32
+    x3 = torch.randn(B, H, H, 3, device=dev).to(torch.bfloat16)
+    w3 = torch.randn(64, 5, 5, 3, device=dev) * 0.1
+    x8 = torch.empty(B, H, H, 8, dtype=torch.bfloat16, device=dev)
+    C.pad_channels(x3.data_ptr(), x8.data_ptr(), B * H * H, 3, 8, _s())
+    w8 = torch.empty(64, 5, 5, 8, dtype=torch.bfloat16, device=dev)
+    C.pack_weight(w3.data_ptr(), w8.data_ptr(), 64, 25, 3, 8, _s())
+    torch.cuda.synchronize()
+    assert torch.equal(x8[..., :3], x3) and not x8[..., 3:].any()
+    assert torch.equal(w8[..., :3], w3.to(torch.bfloat16)) and not w8[..., 3:].any()
+    dy = torch.randn(B, H, H, 64, device=dev).to(torch.bfloat16)
+    slabs = torch.zeros(4, 64, 200, device=dev)
+    C.conv_wgrad(dy.data_ptr(), x8.data_ptr(), slabs.data_ptr(), B, H, H, 8, 64, 5, 4, 200, 1, _s())
+    dw = torch.empty(64, 5, 5, 3, device=dev)
+    C.slab_reduce(slabs.data_ptr(), dw.data_ptr(), 4, 64, 25, 8, 3, _s())
+    xr = x3.float().permute(0, 3, 1, 2)
+    wr = w3.to(torch.bfloat16).float().permute(0, 3, 1, 2).requires_grad_(True)
+    F.conv2d(xr, wr, padding=2).backward(dy.float().permute(0, 3, 1, 2))
+    torch.cuda.synchronize()
+    assert _rel(dw, wr.grad.permute(0, 2, 3, 1)) < 1e-4
+
+
+@pytest.mark.parametrize("shape", [(8, 32, 64), (8, 16, 128), (16, 4, 512), (3, 8, 32)])
+def test_bn_relu_pool_fwd_bwd(C, shape):
+    B, H, Cc = shape
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(B + H + Cc)
+    y = (torch.randn(B, H, H, Cc, device=dev, generator=g) * 2 + 0.5).to(torch.bfloat16)
+    gamma = torch.rand(Cc, device=dev, generator=g) + 0.5
+    beta = torch.randn(Cc, device=dev, generator=g) * 0.1
+    bias = torch.randn(Cc, device=dev, generator=g) * 0.1
+    rm = torch.zeros(Cc, device=dev)
+    rv = torch.ones(Cc, device=dev)
+    M = B * H * H
+    yf = y.float().reshape(-1, Cc)
+    partial = torch.stack([yf.sum(0), (yf * yf).sum(0)]).unsqueeze(0).contiguous()
+    coef = torch.empty(4, Cc, device=dev)
+    C.bn_finalize(partial.data_ptr(), 1, Cc, M, gamma.data_ptr(), beta.data_ptr(), bias.data_ptr(), rm.data_ptr(),
+                  rv.data_ptr(), 1e-3, 0.1, 0, coef.data_ptr(), _s())
+    out = torch.empty(B, H // 2, H // 2, Cc, dtype=torch.bfloat16, device=dev)
+    C.bn_relu_pool_fwd(y.data_ptr(), coef.data_ptr(), out.data_ptr(), B, H, H, Cc, _s())
+    # reference (fp32 from the same bf16 y)
+    yr = y.float().permute(0, 3, 1, 2).requires_grad_(True)
+    rm_ref, rv_ref = torch.zeros(Cc, device=dev), torch.ones(Cc, device=dev)
+    gr = gamma.clone().requires_grad_(True)
+    br = beta.clone().requires_grad_(True)
+    z = F.batch_norm(yr, rm_ref, rv_ref, gr, br, True, 0.1, 1e-3)
+    o = F.max_pool2d(F.relu(z), 2, 2)
+    torch.cuda.synchronize()
+    assert _rel(out, o.permute(0, 2, 3, 1)) < 5e-3
+    torch.testing.assert_close(rm, rm_ref + 0.1 * bias, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rv, rv_ref, rtol=1e-3, atol=1e-4)
+    # backward
+    dP = torch.randn(B, H // 2, H // 2, Cc, device=dev, generator=g).to(torch.bfloat16)
+    o.backward(dP.float().permute(0, 3, 1, 2))
+    G = C.bn_bwd_blocks(B, H, H, Cc)
+    part = torch.empty(G, 2, Cc, device=dev)
+    C.bn_relu_pool_bwd_reduce(y.data_ptr(), dP.data_ptr(), coef.data_ptr(), part.data_ptr(), B, H, H, Cc, G, _s())
+    dg = torch.empty(Cc, device=dev)
+    db = torch.empty(Cc, device=dev)
+    acoef = torch.empty(3, Cc, device=dev)
+    C.bn_bwd_finalize(part.data_ptr(), G, Cc, M, gamma.data_ptr(), coef.data_ptr(), dg.data_ptr(), db.data_ptr(),
+                      acoef.data_ptr(), _s())
+    dy = torch.empty_like(y)
+    C.bn_relu_pool_bwd_apply(y.data_ptr(), dP.data_ptr(), coef.data_ptr(), acoef.data_ptr(), dy.data_ptr(), B, H, H,
+                             Cc, _s())
+    torch.cuda.synchronize()
+    torch.testing.assert_close(db, br.grad, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(dg, gr.grad, rtol=1e-3, atol=1e-3)
+    assert _rel(dy, yr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+def test_head(C):
+    dev = torch.device("cuda")
+    B, Fd, NC = 37, 2048, 10
+    h = torch.randn(B, Fd, device=dev).to(torch.bfloat16)
+    w = torch.randn(NC, Fd, device=dev) * 0.02
+    b = torch.randn(NC, device=dev) * 0.1
+    lab = torch.randint(0, NC, (B,), device=dev)
+    logp = torch.empty(B, NC, device=dev)
+    dlog = torch.empty(B, NC, device=dev)
+    lb = torch.empty(B, device=dev)
+    dh = torch.empty(B, Fd, dtype=torch.bfloat16, device=dev)
+    dw = torch.empty(NC, Fd, device=dev)
+    db = torch.empty(NC, device=dev)
+    loss = torch.empty(1, device=dev)
+    C.head_fwd_bwd(h.data_ptr(), w.data_ptr(), b.data_ptr(), lab.data_ptr(), Fd, B, NC, logp.data_ptr(),
+                   dlog.data_ptr(), lb.data_ptr(), dh.data_ptr(), _s())
+    C.head_wgrad(h.data_ptr(), dlog.data_ptr(), lb.data_ptr(), Fd, B, NC, dw.data_ptr(), db.data_ptr(),
+                 loss.data_ptr(), _s())
+    hr = h.float().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    lp = F.log_softmax(F.linear(hr, wr, br), 1)
+    L = F.nll_loss(lp, lab)
+    L.backward()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(logp, lp, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(loss[0], L, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(dw, wr.grad, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(db, br.grad, rtol=1e-4, atol=1e-6)
+    assert _rel(dh, hr.grad) < 5e-3
+
+
+def test_executor_matches_torch_model(C):
+    """Whole-model check: HIP executor loss + every gradient vs an fp32 PyTorch
+    reference of the same parameters; the error must be within 2x of what
+    PyTorch's own bf16 path shows against the same fp32 reference."""
+    from torch_distlearn_amd import FlatParams
+    from torch_distlearn_amd.models import CifarConvNet
+    from torch_distlearn_amd.models.cifar_hip import CifarHIPExecutor
+
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    x = torch.randn(16, 32, 32, 3, device=dev).to(torch.bfloat16)
+    y = torch.randint(0, 10, (16,), device=dev)
+    refs = {}
+    for dt in (torch.float32, torch.bfloat16):
+        m = CifarConvNet(seed=3).to(dev)
+        L = m.loss(m(x, compute_dtype=dt), y)
+        L.backward()
+        refs[dt] = (m, float(L))
+    ref, L32 = refs[torch.float32]
+    rbf, Lbf = refs[torch.bfloat16]
+    mdl = CifarConvNet(seed=3).to(dev)
+    flat = FlatParams(mdl, grads=True, shadow_bf16=True)
+    ex = CifarHIPExecutor(mdl, flat, max_batch=16)
+    flat.grad.zero_()
+    loss = ex.forward_backward(x.contiguous(), y)
+    torch.cuda.synchronize()
+    assert abs(float(loss) - L32) < 2e-2 * max(1.0, abs(L32))
+    names = [n for n, _ in ref.named_parameters()]
+    for n, p32, pbf, g in zip(names, ref.parameters(), rbf.parameters(), flat.views_of(flat.grad)):
+        if n.startswith("conv") and n.endswith("_b"):
+            assert float(g.abs().max()) == 0.0  # exact: train-mode BN cancels the conv bias
+            continue
+        r = _rel(g, p32.grad)
+        r_torch = _rel(pbf.grad, p32.grad)
+        assert r < max(5e-2, 2.0 * r_torch), (n, r, r_torch)
+    for i in range(4):
+        torch.testing.assert_close(getattr(mdl, f"bn{i+1}_rm"), getattr(ref, f"bn{i+1}_rm"), rtol=2e-2, atol=2e-3)
+    ref.eval()
+    lp_ref = ref(x, compute_dtype=torch.float32)
+    lp = ex.predict(x)
+    assert _rel(lp, lp_ref) < 2e-2

@@ -1,0 +1,244 @@
+"""Native executor for the CIFAR-10 convnet: every forward/backward op is a
+hand-written gfx950 HIP kernel (csrc/kernels/{conv_igemm,bn_pool,head}.hip),
+launched on the current HIP stream with static workspaces, so the whole step
+is hipGraph-capturable.
+
+Reference computation: examples/cifar10.lua:146-169 (predict / f / df via
+torch-autograd + cunn).  Per block i:
+
+  forward   conv_fwd (MFMA implicit GEMM, epilogue: BN partial sums)
+            bn_finalize (batch mean/invstd, running stats)
+            bn_relu_pool_fwd
+  head      head_fwd_bwd (Linear + LogSoftMax + NLL + dlogits + dh), head_wgrad
+  backward  bn_relu_pool_bwd_reduce -> bn_bwd_finalize (dgamma, dbeta)
+            -> bn_relu_pool_bwd_apply (dy) -> conv_wgrad (-> slab_reduce)
+            -> conv dgrad (= conv_fwd on dy with flipped/transposed weights)
+
+Gradients are written (fp32) straight into the flat gradient buffer; as soon
+as a block's gradients are final its leaves are reported to the
+:class:`~torch_distlearn_amd.parallel.buckets.GradBucketer`, which launches
+that bucket's RCCL all-reduce on the comm stream while the remaining blocks'
+backward runs.  Weights are read as the bf16 shadow that the fused SGD kernel
+refreshes (conv) or as the fp32 master (BN affine, classifier).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+
+from .._native import native, stream_handle
+from .cifar_convnet import BN_EPS, BN_MOMENTUM, KSIZE, CifarConvNet
+
+BF16 = torch.bfloat16
+CIN_PAD = 8  # the 3-channel input layer is zero-padded to 8 channels (one 16-B vector per tap)
+
+# tile ids of conv_fwd: 0 = 128x128, 1 = 64x64, 2 = 128x64 (BK = 64) ; conv_wgrad: 0 = 128x64, 1 = 64x64
+_FWD_TILES = {0: (128, 128), 1: (64, 64), 2: (128, 64)}
+
+
+def _fwd_plan(M: int, N: int, K: int):
+    """(tile, splits) for a forward/dgrad implicit GEMM: the biggest tile the
+    channel count allows, then split-K until the grid covers the 256 CUs
+    (keeping >= 8 K-steps of 64 per split)."""
+    tile = 0 if N % 128 == 0 else 2
+    bm, bn = _FWD_TILES[tile]
+    tiles = ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
+    ksteps = (K + 63) // 64
+    splits = 1
+    while tiles * splits < 256 and ksteps // (splits * 2) >= 8:
+        splits *= 2
+    return tile, splits
+
+
+def _wgrad_plan(cout: int, K: int, M: int):
+    """(tile, splits) for the weight gradient: >= ~256 workgroups, each
+    reducing over >= 2048 rows of m."""
+    tile = 0 if cout % 128 == 0 else 1
+    bm = 128 if tile == 0 else 64
+    tiles = (cout // bm) * ((K + 63) // 64)
+    splits = 1
+    while tiles * splits < 256 and M // (splits * 2) >= 2048:
+        splits *= 2
+    return tile, splits
+
+
+class CifarHIPExecutor:
+    def __init__(self, model: CifarConvNet, flat, bucketer=None, max_batch: Optional[int] = None):
+        if not isinstance(model, CifarConvNet):
+            raise TypeError("CifarHIPExecutor needs a CifarConvNet")
+        if flat.shadow is None:
+            raise ValueError("CifarHIPExecutor needs FlatParams(shadow_bf16=True)")
+        self.C = native()
+        self.model, self.flat, self.bucketer = model, flat, bucketer
+        self.dev = flat.data.device
+        self.B = int(max_batch or 128)
+        ch = model.channels
+        self.nb = model.nblocks
+        self.cins = [CIN_PAD] + list(ch[1:-1])      # kernel-side input channels per block
+        self.cins_real = list(ch[:-1])
+        self.couts = list(ch[1:])
+        self.hs = [model.image >> i for i in range(self.nb)]
+        self.nclass = model.num_classes
+        self.feat = ch[-1] * model.final_hw * model.final_hw
+        # flat views (walk order = registration order)
+        self.p32 = flat.param_views()
+        self.p16 = flat.shadow_views()
+        self.g32 = flat.views_of(flat.grad)
+        self.rm = [getattr(model, f"bn{i + 1}_rm") for i in range(self.nb)]
+        self.rv = [getattr(model, f"bn{i + 1}_rv") for i in range(self.nb)]
+        self._alloc(self.B)
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc(self, B: int):
+        d, C = self.dev, self.C
+        e = lambda *s, dt=BF16: torch.empty(*s, dtype=dt, device=d)  # noqa: E731
+        H0 = self.hs[0]
+        self.x8 = torch.zeros(B, H0, H0, CIN_PAD, dtype=BF16, device=d)
+        self.w1p = torch.zeros(self.couts[0], KSIZE * KSIZE * CIN_PAD, dtype=BF16, device=d)
+        self.wt = [None] + [e(self.cins[i], KSIZE, KSIZE, self.couts[i]) for i in range(1, self.nb)]
+        self.y = [e(B, h, h, c) for h, c in zip(self.hs, self.couts)]
+        self.p = [e(B, h // 2, h // 2, c) for h, c in zip(self.hs, self.couts)]
+        self.dP = [e(B, h // 2, h // 2, c) for h, c in zip(self.hs, self.couts)]
+        self.dY = e(max(B * h * h * c for h, c in zip(self.hs, self.couts)))
+        self.coef = [torch.empty(4, c, device=d) for c in self.couts]
+        self.acoef = [torch.empty(3, c, device=d) for c in self.couts]
+        self.fwd_plan, self.stats = [], []
+        self.dgrad_plan = [None] * self.nb
+        self.bwd_blocks, self.bwd_part = [], []
+        self.wplan, slab_elems = [], 0
+        for i in range(self.nb):
+            h, cin, cout = self.hs[i], self.cins[i], self.couts[i]
+            M = B * h * h
+            K = KSIZE * KSIZE * cin
+            tile, splits = _fwd_plan(M, cout, K)
+            self.fwd_plan.append((tile, splits))
+            if splits > 1:
+                slab_elems = max(slab_elems, splits * M * cout)
+            rows = C.conv_fwd_stat_rows(B, h, h, cin, cout, KSIZE, tile, splits)
+            if splits > 1:
+                rows = max(rows, 400)  # the split-K combine launches <= ~384 blocks for any batch
+            self.stats.append(torch.empty(rows, 2, cout, device=d))
+            g = C.bn_bwd_blocks(B, h, h, cout)
+            self.bwd_blocks.append(g)
+            self.bwd_part.append(torch.empty(g, 2, cout, device=d))
+            tile_w, splits_w = _wgrad_plan(cout, K, M)
+            direct = splits_w == 1 and cin == self.cins_real[i]
+            self.wplan.append((tile_w, splits_w, direct))
+            if not direct:
+                slab_elems = max(slab_elems, splits_w * cout * K)
+            if i > 0:
+                dt, ds = _fwd_plan(M, cin, KSIZE * KSIZE * cout)
+                self.dgrad_plan[i] = (dt, ds)
+                if ds > 1:
+                    slab_elems = max(slab_elems, ds * M * cin)
+        self.slabs = torch.empty(max(slab_elems, 1), device=d)
+        self.logits = torch.empty(B, self.nclass, device=d)
+        self.dlogits = torch.empty(B, self.nclass, device=d)
+        self.loss_b = torch.empty(B, device=d)
+        self.loss = torch.zeros(1, device=d)
+        self.cap = B
+
+    # ------------------------------------------------------------------ helpers
+    def _leaf(self, blk: int, j: int) -> int:
+        return 4 * blk + j  # conv_w, conv_b, bn_w, bn_b
+
+    def _prep(self, x: torch.Tensor, s: int) -> int:
+        """Input channel pad + layer-1 weight pack + dgrad weight transposes (one launch)."""
+        B = x.shape[0]
+        if B > self.cap:
+            raise ValueError(f"batch {B} > executor capacity {self.cap}")
+        if x.dim() != 4 or x.shape[-1] != self.cins_real[0] or x.dtype != BF16 or not x.is_contiguous():
+            raise ValueError("CifarHIPExecutor expects contiguous NHWC bf16 input [B, H, W, 3]")
+        h = self.hs[0]
+        idx = list(range(1, self.nb))
+        self.C.prep_step(x.data_ptr(), self.x8.data_ptr(), B * h * h, self.cins_real[0], CIN_PAD,
+                         self.p32[0].data_ptr(), self.w1p.data_ptr(), self.couts[0], KSIZE * KSIZE,
+                         self.cins_real[0], CIN_PAD, [self.p16[self._leaf(i, 0)].data_ptr() for i in idx],
+                         [self.wt[i].data_ptr() for i in idx], [self.couts[i] for i in idx],
+                         [self.cins[i] for i in idx], s)
+        return B
+
+    def _forward(self, B: int, s: int, train: bool):
+        C = self.C
+        inp = self.x8
+        for i in range(self.nb):
+            h, cin, cout = self.hs[i], self.cins[i], self.couts[i]
+            M = B * h * h
+            w = self.w1p if i == 0 else self.p16[self._leaf(i, 0)]
+            t, sp = self.fwd_plan[i]
+            ntm = C.conv_fwd(inp.data_ptr(), w.data_ptr(), self.y[i].data_ptr(),
+                             self.stats[i].data_ptr() if train else 0, self.slabs.data_ptr(), B, h, h, cin, cout, KSIZE,
+                             t, sp, s)
+            C.bn_finalize(self.stats[i].data_ptr(), ntm, cout, M, self.p32[self._leaf(i, 2)].data_ptr(),
+                          self.p32[self._leaf(i, 3)].data_ptr(), self.p32[self._leaf(i, 1)].data_ptr(),
+                          self.rm[i].data_ptr(), self.rv[i].data_ptr(), BN_EPS, BN_MOMENTUM, 0 if train else 1,
+                          self.coef[i].data_ptr(), s)
+            C.bn_relu_pool_fwd(self.y[i].data_ptr(), self.coef[i].data_ptr(), self.p[i].data_ptr(), B, h, h, cout, s)
+            inp = self.p[i]
+
+    # ------------------------------------------------------------------ API
+    def forward_backward(self, x: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        """One forward + backward on this node's batch; fp32 grads land in the
+        flat gradient buffer.  Returns the mean loss (device tensor)."""
+        C = self.C
+        s = stream_handle()
+        if labels.dtype != torch.int64:
+            raise ValueError("labels must be int64")
+        B = self._prep(x, s)
+        self._forward(B, s, train=True)
+        nfc = 4 * self.nb
+        C.head_fwd_bwd(self.p[-1].data_ptr(), self.p32[nfc].data_ptr(), self.p32[nfc + 1].data_ptr(),
+                       labels.data_ptr(), self.feat, B, self.nclass, self.logits.data_ptr(), self.dlogits.data_ptr(),
+                       self.loss_b.data_ptr(), self.dP[-1].data_ptr(), s)
+        C.head_wgrad(self.p[-1].data_ptr(), self.dlogits.data_ptr(), self.loss_b.data_ptr(), self.feat, B,
+                     self.nclass, self.g32[nfc].data_ptr(), self.g32[nfc + 1].data_ptr(), self.loss.data_ptr(), s)
+        self._ready(nfc)
+        self._ready(nfc + 1)
+        for i in reversed(range(self.nb)):
+            h, cin, cout = self.hs[i], self.cins[i], self.couts[i]
+            M = B * h * h
+            G = self.bwd_blocks[i]
+            C.bn_relu_pool_bwd_reduce(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
+                                      self.bwd_part[i].data_ptr(), B, h, h, cout, G, s)
+            C.bn_bwd_finalize(self.bwd_part[i].data_ptr(), G, cout, M, self.p32[self._leaf(i, 2)].data_ptr(),
+                              self.coef[i].data_ptr(), self.g32[self._leaf(i, 2)].data_ptr(),
+                              self.g32[self._leaf(i, 3)].data_ptr(), self.acoef[i].data_ptr(), s)
+            C.bn_relu_pool_bwd_apply(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
+                                     self.acoef[i].data_ptr(), self.dY.data_ptr(), B, h, h, cout, s)
+            xin = self.x8 if i == 0 else self.p[i - 1]
+            K = KSIZE * KSIZE * cin
+            tile, splits, direct = self.wplan[i]
+            gw = self.g32[self._leaf(i, 0)]
+            if direct:
+                C.conv_wgrad(self.dY.data_ptr(), xin.data_ptr(), gw.data_ptr(), B, h, h, cin, cout, KSIZE, 1, K,
+                             tile, s)
+            else:
+                C.conv_wgrad(self.dY.data_ptr(), xin.data_ptr(), self.slabs.data_ptr(), B, h, h, cin, cout, KSIZE,
+                             splits, K, tile, s)
+                C.slab_reduce(self.slabs.data_ptr(), gw.data_ptr(), splits, cout, KSIZE * KSIZE, cin,
+                              self.cins_real[i], s)
+            # conv bias grad: exactly 0 under train-mode BN (grad buffer was zero-filled)
+            for j in range(4):
+                self._ready(self._leaf(i, j))
+            if i > 0:
+                dt, ds = self.dgrad_plan[i]
+                C.conv_fwd(self.dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), 0,
+                           self.slabs.data_ptr(), B, h, h, cout, cin, KSIZE, dt, ds, s)
+        return self.loss[0]
+
+    def _ready(self, leaf: int):
+        if self.bucketer is not None:
+            self.bucketer.mark_leaf_ready(leaf)
+
+    @torch.no_grad()
+    def predict(self, x: torch.Tensor) -> torch.Tensor:
+        """Eval-mode forward (running BN statistics); returns log-probabilities
+        [B, classes] (fp32)."""
+        s = stream_handle()
+        B = self._prep(x, s)
+        self._forward(B, s, train=False)
+        nfc = 4 * self.nb
+        self.C.head_fwd_bwd(self.p[-1].data_ptr(), self.p32[nfc].data_ptr(), self.p32[nfc + 1].data_ptr(), 0,
+                            self.feat, B, self.nclass, self.logits.data_ptr(), 0, 0, 0, s)
+        return self.logits[:B].clone()

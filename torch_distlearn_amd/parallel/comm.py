@@ -159,11 +159,15 @@ class RcclCommunicator(Communicator):
 
     def all_reduce(self, t, op="sum", stream=None):
         self._check(t)
+        if self.world_size == 1:  # identity (in place); skips RCCL's self-copy
+            return
         self._c.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], OP_CODES[op],
                            stream_handle(stream))
 
     def broadcast(self, t, root=0, stream=None):
         self._check(t)
+        if self.world_size == 1:
+            return
         self._c.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], root, stream_handle(stream))
 
     def all_gather(self, out, t, stream=None):
