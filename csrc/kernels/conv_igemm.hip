@@ -136,7 +136,7 @@ __device__ __forceinline__ void block_sync_lds() {
 // 256 threads = 4 waves (2 x 2), wave tile (BM/2) x (BN/2), BK = 64,
 // 3-stage LDS ring filled by LDS-DMA, one barrier per K step.
 // --------------------------------------------------------------------------
-template <int BM, int BN, bool STATS, bool SLAB>
+template <int BM, int BN, bool STATS, bool SLAB, bool TAPU>
 __global__ void __launch_bounds__(256) conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                        bf16_t* __restrict__ y, float* __restrict__ stats,
                                                        float* __restrict__ slab, const ConvGeom g, int splits,
@@ -169,10 +169,10 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const bf16_t* __restrict_
   const int kt_end = min(nkt_total, kt_beg + kt_per_split);
   const int nk = max(0, kt_end - kt_beg);
 
-  // per-lane source roles (fixed over the K loop)
+  // per-lane source roles (fixed over the K loop); 32-bit element offsets
+  // (host checks that every operand has < 2^31 elements).
   // A: instruction j of this wave covers rows 8*(wid*A_INS + j) .. +7
-  int a_ch[A_INS], a_oh[A_INS], a_ow[A_INS];
-  int64_t a_base[A_INS];
+  int a_ch[A_INS], a_oh[A_INS], a_ow[A_INS], a_pix[A_INS];
   bool a_ok[A_INS];
 #pragma unroll
   for (int j = 0; j < A_INS; ++j) {
@@ -181,44 +181,67 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const bf16_t* __restrict_
     const int m = m0 + row;
     a_ok[j] = m < g.M;
     const int mm = a_ok[j] ? m : 0;
-    const int b = mm >> g.logHW, rem = mm & (HW - 1);
+    const int rem = mm & (HW - 1);
     a_oh[j] = rem >> g.logW;
     a_ow[j] = rem & (Wd - 1);
-    a_base[j] = (int64_t)b * HW * g.Cin;
+    a_pix[j] = mm * g.Cin + a_ch[j] * 8;  // element offset of (pixel m, tap (pad,pad), chunk)
+    if (!a_ok[j]) { a_oh[j] = -(1 << 20); }  // forces the bounds test to fail
   }
-  int b_ch[B_INS];
-  const bf16_t* b_src[B_INS];
+  int b_off[B_INS], b_k[B_INS];
   bool b_ok[B_INS];
 #pragma unroll
   for (int j = 0; j < B_INS; ++j) {
     const int row = 8 * (wid * B_INS + j) + (lane >> 3);
-    b_ch[j] = (lane & 7) ^ ((row >> 1) & 7);
+    const int ch = (lane & 7) ^ ((row >> 1) & 7);
     const int n = n0 + row;
     b_ok[j] = n < g.Cout;
-    b_src[j] = w + (int64_t)(b_ok[j] ? n : 0) * g.K;
+    b_k[j] = ch * 8;
+    b_off[j] = (b_ok[j] ? n : 0) * g.K + ch * 8;
   }
+  const char* zsrc = reinterpret_cast<const char*>(g_zero16);
+  const char* xb = reinterpret_cast<const char*>(x);
+  const char* wb = reinterpret_cast<const char*>(w);
 
   auto issue = [&](int kt, int slot) {
     char* sA = smem + slot * STAGE_BYTES;
     char* sB = sA + A_BYTES;
-#pragma unroll
-    for (int j = 0; j < A_INS; ++j) {
-      const int kc = kt * CPR + a_ch[j];
-      const int kpos = kc >> g.logC8;
-      const int c0 = (kc & (C8 - 1)) << 3;
+    if constexpr (TAPU) {
+      // Cin >= 64: the 8 chunks of a K step are one tap -> tap math is wave-uniform (SALU)
+      const int k0 = kt * BK;
+      const int kpos = k0 >> (g.logC8 + 3);
+      const int cbase = k0 & (g.Cin - 1);
       const int kh = kpos / g.KS, kw = kpos - kh * g.KS;
-      const int ih = a_oh[j] + kh - g.pad, iw = a_ow[j] + kw - g.pad;
-      const bool ok = a_ok[j] && kc < g.Kch && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)Wd;
-      const void* src = ok ? (const void*)(x + a_base[j] + (((int64_t)ih << g.logW) + iw) * g.Cin + c0)
-                           : (const void*)g_zero16;
-      glds16(src, sA + (wid * A_INS + j) * 1024);
+      const int dh = kh - g.pad, dw = kw - g.pad;
+      const int tap_off = (dh * Wd + dw) * g.Cin + cbase;
+      const bool kok = k0 < g.K;
+#pragma unroll
+      for (int j = 0; j < A_INS; ++j) {
+        const int ih = a_oh[j] + dh, iw = a_ow[j] + dw;
+        const bool ok = kok && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)Wd;
+        const uint64_t pa = (uint64_t)xb + (uint64_t)(2u * (unsigned)(a_pix[j] + tap_off));
+        glds16((const void*)(ok ? pa : (uint64_t)zsrc), sA + (wid * A_INS + j) * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < A_INS; ++j) {
+        const int kc = kt * CPR + a_ch[j];
+        const int kpos = kc >> g.logC8;
+        const int c0 = (kc & (C8 - 1)) << 3;
+        const int kh = kpos / g.KS, kw = kpos - kh * g.KS;
+        const int dh = kh - g.pad, dw = kw - g.pad;
+        const int ih = a_oh[j] + dh, iw = a_ow[j] + dw;
+        const bool ok = kc < g.Kch && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)Wd;
+        const char* src = ok ? xb + 2 * (a_pix[j] - a_ch[j] * 8 + (dh * Wd + dw) * g.Cin + c0) : zsrc;
+        glds16(src, sA + (wid * A_INS + j) * 1024);
+      }
     }
+    const int kadd = kt * BK;
 #pragma unroll
     for (int j = 0; j < B_INS; ++j) {
-      const int kc = kt * CPR + b_ch[j];
-      const bool ok = b_ok[j] && kc < g.Kch;
-      const void* src = ok ? (const void*)(b_src[j] + (int64_t)kc * 8) : (const void*)g_zero16;
-      glds16(src, sB + (wid * B_INS + j) * 1024);
+      bool ok = b_ok[j];
+      if constexpr (!TAPU) ok = ok && (kadd + b_k[j]) < g.K;  // K tail (first layer only)
+      const uint64_t pb = (uint64_t)wb + (uint64_t)(2u * (unsigned)(b_off[j] + kadd));
+      glds16((const void*)(ok ? pb : (uint64_t)zsrc), sB + (wid * B_INS + j) * 1024);
     }
   };
 
@@ -409,18 +432,19 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const bf16_t* __restric
   const int HW = 1 << g.logHW, Wd = g.W, C8 = 1 << g.logC8;
 
   // A (dy) lanes: row = A_RPI*(wid*A_INS + j) + lane/ACPR, chunk fixed
-  int a_row[A_INS], a_co[A_INS];
+  int a_row[A_INS], a_off[A_INS];
   bool a_cok[A_INS];
 #pragma unroll
   for (int j = 0; j < A_INS; ++j) {
     const int row = A_RPI * (wid * A_INS + j) + lane / ACPR;
     a_row[j] = row;
     const int ch = swz_tr<ACPR>(row, lane % ACPR) - row * ACPR;  // logical chunk (involution)
-    a_co[j] = co0 + ch * 8;
-    a_cok[j] = a_co[j] < g.Cout;
+    const int co = co0 + ch * 8;
+    a_cok[j] = co < g.Cout;
+    a_off[j] = (mbeg + row) * g.Cout + (a_cok[j] ? co : 0);
   }
   // B (im2col) lanes: chunk -> fixed tap (dh, dw, c0)
-  int b_row[B_INS], b_dh[B_INS], b_dw[B_INS], b_c0[B_INS];
+  int b_row[B_INS], b_dh[B_INS], b_dw[B_INS], b_c0[B_INS], b_dhw[B_INS];
   bool b_kok[B_INS];
 #pragma unroll
   for (int j = 0; j < B_INS; ++j) {
@@ -434,28 +458,32 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const bf16_t* __restric
     const int kh = kpos / g.KS;
     b_dh[j] = kh - g.pad;
     b_dw[j] = kpos - kh * g.KS - g.pad;
+    b_dhw[j] = b_dh[j] * Wd + b_dw[j];
   }
+  const uint64_t zsrc = (uint64_t)g_zero16;
+  const uint64_t dyb = (uint64_t)dy, xb = (uint64_t)x;
+  const int mcount = mend - mbeg;
 
   auto issue = [&](int kt, int slot) {
     char* sA = smem + slot * STAGE_BYTES;
     char* sB = sA + A_BYTES;
-    const int mb = mbeg + kt * BK;
+    const int r0 = kt * BK;
+    const int aadd = r0 * g.Cout;
 #pragma unroll
     for (int j = 0; j < A_INS; ++j) {
-      const int m = mb + a_row[j];
-      const bool ok = m < mend && a_cok[j];
-      const void* src = ok ? (const void*)(dy + (int64_t)m * g.Cout + a_co[j]) : (const void*)g_zero16;
-      glds16(src, sA + (wid * A_INS + j) * 1024);
+      const bool ok = (r0 + a_row[j]) < mcount && a_cok[j];
+      const uint64_t pa = dyb + (uint64_t)(2u * (unsigned)(a_off[j] + aadd));
+      glds16((const void*)(ok ? pa : zsrc), sA + (wid * A_INS + j) * 1024);
     }
 #pragma unroll
     for (int j = 0; j < B_INS; ++j) {
-      const int m = mb + b_row[j];
-      const int b = m >> g.logHW, rem = m & (HW - 1);
+      const int m = mbeg + r0 + b_row[j];
+      const int rem = m & (HW - 1);
       const int ih = (rem >> g.logW) + b_dh[j], iw = (rem & (Wd - 1)) + b_dw[j];
-      const bool ok = m < mend && b_kok[j] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)Wd;
-      const void* src = ok ? (const void*)(x + ((int64_t)b * HW + ((int64_t)ih << g.logW) + iw) * g.Cin + b_c0[j])
-                           : (const void*)g_zero16;
-      glds16(src, sB + (wid * B_INS + j) * 1024);
+      const bool ok = (r0 + b_row[j]) < mcount && b_kok[j] && (unsigned)ih < (unsigned)g.H &&
+                      (unsigned)iw < (unsigned)Wd;
+      const uint64_t pb = xb + (uint64_t)(2u * (unsigned)((m + b_dhw[j]) * g.Cin + b_c0[j]));
+      glds16((const void*)(ok ? pb : zsrc), sB + (wid * B_INS + j) * 1024);
     }
   };
 
@@ -681,22 +709,31 @@ int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile,
   return (g.M + rpb - 1) / rpb;
 }
 
-template <int BM, int BN>
-static void launch_fwd(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab,
-                       int splits, hipStream_t s) {
+template <int BM, int BN, bool TAPU>
+static void launch_fwd_t(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab,
+                         int splits, hipStream_t s) {
   const int ntm = (g.M + BM - 1) / BM, ntn = (g.Cout + BN - 1) / BN;
   const int nkt = (g.Kch + 7) / 8;
   const int ktps = (nkt + splits - 1) / splits;
   const int grid = ntm * ntn * splits;
   if (splits > 1)
-    conv_fwd_kernel<BM, BN, false, true><<<grid, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)w, nullptr, nullptr,
-                                                               (float*)slab, g, splits, ktps);
+    conv_fwd_kernel<BM, BN, false, true, TAPU><<<grid, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)w, nullptr,
+                                                                     nullptr, (float*)slab, g, splits, ktps);
   else if (stats)
-    conv_fwd_kernel<BM, BN, true, false><<<grid, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y,
-                                                               (float*)stats, nullptr, g, 1, ktps);
+    conv_fwd_kernel<BM, BN, true, false, TAPU><<<grid, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y,
+                                                                     (float*)stats, nullptr, g, 1, ktps);
   else
-    conv_fwd_kernel<BM, BN, false, false><<<grid, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y,
-                                                                nullptr, nullptr, g, 1, ktps);
+    conv_fwd_kernel<BM, BN, false, false, TAPU><<<grid, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y,
+                                                                      nullptr, nullptr, g, 1, ktps);
+}
+
+template <int BM, int BN>
+static void launch_fwd(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab,
+                       int splits, hipStream_t s) {
+  if ((int64_t)g.M * g.Cin >= (1ll << 31) || (int64_t)g.Cout * g.K >= (1ll << 31))
+    throw std::runtime_error("conv_fwd: operand too large for 32-bit offsets");
+  if (g.Cin >= 64) launch_fwd_t<BM, BN, true>(g, x, w, y, stats, slab, splits, s);
+  else launch_fwd_t<BM, BN, false>(g, x, w, y, stats, slab, splits, s);
 }
 
 // tile: 0 = 128x128, 1 = 64x64, 2 = 128x64 (BM x BN, BK = 64).  splits > 1:
@@ -732,6 +769,8 @@ void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, i
                 int ldo, int tile, uintptr_t stream) {
   ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
   if (ldo < g.K) throw std::runtime_error("conv_wgrad: ldo < K");
+  if ((int64_t)g.M * g.Cin >= (1ll << 31) || (int64_t)g.M * g.Cout >= (1ll << 31))
+    throw std::runtime_error("conv_wgrad: operand too large for 32-bit offsets");
   if (Cout % 8 != 0) throw std::runtime_error("conv_wgrad: Cout % 8 != 0");
   if (splits < 1) splits = 1;
   int mps = (g.M + splits - 1) / splits;

@@ -1,0 +1,74 @@
+"""Micro-benchmark of the implicit-GEMM conv kernels on the reference model's
+layer shapes (per-GPU batch B): forward, dgrad, wgrad; prints us and TFLOP/s.
+    python scripts/bench_conv.py [--batch 128] [--iters 50] [--only fwd2]"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from torch_distlearn_amd import _native
+from torch_distlearn_amd.models.cifar_hip import _fwd_plan, _wgrad_plan
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--only", default="")
+    ap.add_argument("--tile", type=int, default=-1)
+    ap.add_argument("--splits", type=int, default=-1)
+    a = ap.parse_args()
+    C = _native.native()
+    dev = torch.device("cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    B = a.batch
+    layers = [(32, 8, 64), (16, 64, 128), (8, 128, 256), (4, 256, 512)]
+    slab = torch.empty(64 * 1024 * 1024, device=dev)
+    stats = torch.empty(4096 * 2 * 512, device=dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for li, (H, cin, cout) in enumerate(layers):
+        M, K = B * H * H, 25 * cin
+        x = torch.randn(B, H, H, cin, device=dev).to(torch.bfloat16)
+        w = (torch.randn(cout, 5, 5, cin, device=dev) * 0.05).to(torch.bfloat16)
+        y = torch.empty(B, H, H, cout, dtype=torch.bfloat16, device=dev)
+        dy = torch.randn(B, H, H, cout, device=dev).to(torch.bfloat16)
+        wt = torch.empty(cin, 5, 5, cout, dtype=torch.bfloat16, device=dev)
+        dx = torch.empty(B, H, H, cin, dtype=torch.bfloat16, device=dev)
+        jobs = []
+        t, sp = _fwd_plan(M, cout, K)
+        if a.tile >= 0:
+            t = a.tile
+        if a.splits >= 0:
+            sp = a.splits
+        jobs.append((f"fwd{li+1}", 2 * M * cout * K, lambda t=t, sp=sp: C.conv_fwd(
+            x.data_ptr(), w.data_ptr(), y.data_ptr(), stats.data_ptr(), slab.data_ptr(), B, H, H, cin, cout, 5, t,
+            sp, s), f"tile{t} split{sp}"))
+        if li > 0:
+            dt, ds = _fwd_plan(M, cin, 25 * cout)
+            jobs.append((f"dgrad{li+1}", 2 * M * cout * K, lambda dt=dt, ds=ds: C.conv_fwd(
+                dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, slab.data_ptr(), B, H, H, cout, cin, 5, dt, ds, s),
+                f"tile{dt} split{ds}"))
+        wtile, wsp = _wgrad_plan(cout, K, M)
+        jobs.append((f"wgrad{li+1}", 2 * M * cout * K, lambda wtile=wtile, wsp=wsp: C.conv_wgrad(
+            dy.data_ptr(), x.data_ptr(), slab.data_ptr(), B, H, H, cin, cout, 5, wsp, K, wtile, s),
+            f"tile{wtile} split{wsp}"))
+        for name, flops, fn, desc in jobs:
+            if a.only and a.only not in name:
+                continue
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            ev0.record()
+            for _ in range(a.iters):
+                fn()
+            ev1.record()
+            torch.cuda.synchronize()
+            us = ev0.elapsed_time(ev1) * 1e3 / a.iters
+            print(f"{name:8s} M={M:6d} N={cout if 'dgrad' not in name else cin:4d} K={K:6d} {desc:16s} "
+                  f"{us:8.2f} us  {flops / us / 1e6:7.1f} TFLOP/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
