@@ -28,6 +28,9 @@ PYBIND11_MODULE(_C, m) {
   // ---- convnet kernels (MFMA implicit GEMM, BN/ReLU/pool, classifier head) ------
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_fwd_stat_rows", &conv_fwd_stat_rows);
+  m.def("set_conv_stages", &set_conv_stages);
+  m.def("set_conv_waves", &set_conv_waves);
+  m.def("set_conv_debug", &set_conv_debug);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("slab_reduce", &slab_reduce);
   m.def("weight_flip_transpose", &weight_flip_transpose);

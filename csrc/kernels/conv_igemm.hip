@@ -112,6 +112,13 @@ __device__ __forceinline__ int xcd_swizzle(int bid, int nwg) {
 // M/N tails) is read from a 16-byte zero line in global memory.
 // --------------------------------------------------------------------------
 __device__ uint4 g_zero16[4];
+static unsigned long long* g_conv_dbg = nullptr;  // debug: per-workgroup s_memtime stamps
+
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
 
 __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
@@ -121,6 +128,17 @@ template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until at most `n` stages (of LPS LDS-DMA loads each) are still in flight
+template <int LPS>
+__device__ __forceinline__ void wait_stages(int n) {
+  switch (n) {
+    case 0: wait_vmcnt<0>(); break;
+    case 1: wait_vmcnt<LPS>(); break;
+    case 2: wait_vmcnt<2 * LPS>(); break;
+    default: wait_vmcnt<3 * LPS>(); break;
+  }
 }
 
 __device__ __forceinline__ void block_sync_lds() {
@@ -136,17 +154,20 @@ __device__ __forceinline__ void block_sync_lds() {
 // 256 threads = 4 waves (2 x 2), wave tile (BM/2) x (BN/2), BK = 64,
 // 3-stage LDS ring filled by LDS-DMA, one barrier per K step.
 // --------------------------------------------------------------------------
-template <int BM, int BN, bool STATS, bool SLAB, bool TAPU>
-__global__ void __launch_bounds__(256) conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+template <int BM, int BN, bool STATS, bool SLAB, bool TAPU, int STAGES, int WM = 2, int WN = 2>
+__global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                        bf16_t* __restrict__ y, float* __restrict__ stats,
                                                        float* __restrict__ slab, const ConvGeom g, int splits,
-                                                       int kt_per_split) {
-  constexpr int BK = 64, CPR = 8, NT = 256, WM = 2, WN = 2, STAGES = 3;
+                                                       int kt_per_split, unsigned long long* dbg) {
+  const unsigned long long t_start = dbg ? stamp() : 0ull;
+  constexpr int BK = 64, CPR = 8, NW = WM * WN, NT = 64 * NW, PD = STAGES - 1;
+  static_assert(STAGES >= 2 && STAGES <= 4, "2..4 stages");
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE_BYTES = A_BYTES + B_BYTES;
-  constexpr int A_INS = A_BYTES / 1024 / 4, B_INS = B_BYTES / 1024 / 4;  // glds per wave per stage
+  constexpr int A_INS = A_BYTES / 1024 / NW, B_INS = B_BYTES / 1024 / NW;  // glds per wave per stage
   constexpr int LPS = A_INS + B_INS;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
   static_assert(A_INS >= 1 && B_INS >= 1, "tile too small");
+  static_assert(A_INS * NW * 1024 == A_BYTES && B_INS * NW * 1024 == B_BYTES, "DMA split");
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -202,28 +223,33 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const bf16_t* __restrict_
   const char* xb = reinterpret_cast<const char*>(x);
   const char* wb = reinterpret_cast<const char*>(w);
 
-  auto issue = [&](int kt, int slot) {
-    char* sA = smem + slot * STAGE_BYTES;
-    char* sB = sA + A_BYTES;
+  // One LDS-DMA load (q < A_INS: activation row block, else weight row block)
+  // of K step kt into ring slot `slot`.  The tap math of a TAPU step is
+  // wave-uniform (SALU), computed once per step by tap_of().
+  struct Tap { int dh, dw, off; };
+  auto tap_of = [&](int kt) -> Tap {
+    Tap t{0, 0, 0};
     if constexpr (TAPU) {
-      // Cin >= 64: the 8 chunks of a K step are one tap -> tap math is wave-uniform (SALU)
       const int k0 = kt * BK;
       const int kpos = k0 >> (g.logC8 + 3);
-      const int cbase = k0 & (g.Cin - 1);
       const int kh = kpos / g.KS, kw = kpos - kh * g.KS;
-      const int dh = kh - g.pad, dw = kw - g.pad;
-      const int tap_off = (dh * Wd + dw) * g.Cin + cbase;
-      const bool kok = k0 < g.K;
-#pragma unroll
-      for (int j = 0; j < A_INS; ++j) {
-        const int ih = a_oh[j] + dh, iw = a_ow[j] + dw;
-        const bool ok = kok && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)Wd;
-        const uint64_t pa = (uint64_t)xb + (uint64_t)(2u * (unsigned)(a_pix[j] + tap_off));
+      t.dh = kh - g.pad;
+      t.dw = kw - g.pad;
+      t.off = (t.dh * Wd + t.dw) * g.Cin + (k0 & (g.Cin - 1));
+    }
+    return t;
+  };
+  auto issue_one = [&](int q, int kt, int slot, const Tap& t) {
+    char* sA = smem + slot * STAGE_BYTES;
+    char* sB = sA + A_BYTES;
+    if (q < A_INS) {
+      const int j = q;
+      if constexpr (TAPU) {
+        const int ih = a_oh[j] + t.dh, iw = a_ow[j] + t.dw;
+        const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)Wd;
+        const uint64_t pa = (uint64_t)xb + (uint64_t)(2u * (unsigned)(a_pix[j] + t.off));
         glds16((const void*)(ok ? pa : (uint64_t)zsrc), sA + (wid * A_INS + j) * 1024);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < A_INS; ++j) {
+      } else {
         const int kc = kt * CPR + a_ch[j];
         const int kpos = kc >> g.logC8;
         const int c0 = (kc & (C8 - 1)) << 3;
@@ -234,15 +260,19 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const bf16_t* __restrict_
         const char* src = ok ? xb + 2 * (a_pix[j] - a_ch[j] * 8 + (dh * Wd + dw) * g.Cin + c0) : zsrc;
         glds16(src, sA + (wid * A_INS + j) * 1024);
       }
-    }
-    const int kadd = kt * BK;
-#pragma unroll
-    for (int j = 0; j < B_INS; ++j) {
+    } else {
+      const int j = q - A_INS;
+      const int kadd = kt * BK;
       bool ok = b_ok[j];
       if constexpr (!TAPU) ok = ok && (kadd + b_k[j]) < g.K;  // K tail (first layer only)
       const uint64_t pb = (uint64_t)wb + (uint64_t)(2u * (unsigned)(b_off[j] + kadd));
       glds16((const void*)(ok ? pb : (uint64_t)zsrc), sB + (wid * B_INS + j) * 1024);
     }
+  };
+  auto issue = [&](int kt, int slot) {
+    const Tap t = tap_of(kt);
+#pragma unroll
+    for (int q = 0; q < LPS; ++q) issue_one(q, kt, slot, t);
   };
 
   f32x4 acc[FM][FN];
@@ -251,31 +281,56 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const bf16_t* __restrict_
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) issue(kt_beg, 0);
-  if (nk > 1) issue(kt_beg + 1, 1);
+  const unsigned long long t_setup = dbg ? stamp() : 0ull;
+#pragma unroll
+  for (int p = 0; p < PD; ++p)
+    if (p < nk) issue(kt_beg + p, p);
+  // MFMAs per K step and the spacing of the next stage's DMA issues between them
+  constexpr int NMF = (BK / 32) * FM * FN;
+  constexpr int IL = NMF / LPS > 0 ? NMF / LPS : 1;
   for (int i = 0; i < nk; ++i) {
-    if (i + 1 < nk) wait_vmcnt<LPS>(); else wait_vmcnt<0>();
-    block_sync_lds();  // stage i landed for every wave; slot (i+2)%3 no longer read
-    if (i + 2 < nk) issue(kt_beg + i + 2, (i + 2) % STAGES);
+    wait_stages<LPS>(min(PD - 1, nk - 1 - i));
+    block_sync_lds();  // stage i landed for every wave; slot (i+PD)%STAGES no longer read
+    const bool pf = i + PD < nk;
+    const int kt_n = kt_beg + i + PD, slot_n = (i + PD) % STAGES;
+    const Tap tn = tap_of(kt_n);
     const uint4* As = reinterpret_cast<const uint4*>(smem + (i % STAGES) * STAGE_BYTES);
     const uint4* Bs = reinterpret_cast<const uint4*>(smem + (i % STAGES) * STAGE_BYTES + A_BYTES);
+    bf16x8 af[BK / 32][FM], bfr[BK / 32][FN];
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
-      bf16x8 af[FM], bfr[FN];
       const int ch = kk * 4 + (lane >> 4);
 #pragma unroll
       for (int a = 0; a < FM; ++a)
-        af[a] = __builtin_bit_cast(bf16x8, As[swz_row<CPR>(wm * TM + a * 16 + (lane & 15), ch)]);
+        af[kk][a] = __builtin_bit_cast(bf16x8, As[swz_row<CPR>(wm * TM + a * 16 + (lane & 15), ch)]);
 #pragma unroll
       for (int b = 0; b < FN; ++b)
-        bfr[b] = __builtin_bit_cast(bf16x8, Bs[swz_row<CPR>(wn * TN + b * 16 + (lane & 15), ch)]);
+        bfr[kk][b] = __builtin_bit_cast(bf16x8, Bs[swz_row<CPR>(wn * TN + b * 16 + (lane & 15), ch)]);
+    }
+    // the next stage's LDS-DMA issues ride between the MFMAs (their issue cost
+    // overlaps matrix-core execution instead of serialising in front of it)
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk)
 #pragma unroll
       for (int a = 0; a < FM; ++a)
 #pragma unroll
-        for (int b = 0; b < FN; ++b) acc[a][b] = mfma16(af[a], bfr[b], acc[a][b]);
-    }
+        for (int b = 0; b < FN; ++b) {
+          acc[a][b] = mfma16(af[kk][a], bfr[kk][b], acc[a][b]);
+          const int idx = (kk * FM + a) * FN + b;
+          if (idx % IL == IL - 1 && idx / IL < LPS) {
+            if (pf) issue_one(idx / IL, kt_n, slot_n, tn);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
   }
 
+  const unsigned long long t_loop = dbg ? stamp() : 0ull;
+  auto dbg_out = [&]() {
+    if (dbg && threadIdx.x == 0) {
+      unsigned long long* d = dbg + (size_t)blockIdx.x * 4;
+      d[0] = t_start; d[1] = t_setup; d[2] = t_loop; d[3] = stamp();
+    }
+  };
   const int col_l = lane & 15, rq = lane >> 4;
   if constexpr (SLAB) {
     float* o = slab + (int64_t)split * g.M * g.Cout;
@@ -290,6 +345,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const bf16_t* __restrict_
           if (m < g.M && n < g.Cout) o[(int64_t)m * g.Cout + n] = acc[a][b][r];
         }
       }
+    dbg_out();
     return;
   } else {
     float s1[FN], s2[FN];
@@ -340,6 +396,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const bf16_t* __restrict_
       }
     }
   }
+  dbg_out();
 }
 
 // split-K combine: y = bf16(sum_s slab[s]) (+ BN partial sums, one row per block)
@@ -403,16 +460,18 @@ __global__ void __launch_bounds__(256) splitk_combine_kernel(const float* __rest
 // Tiles are staged [m][col] (rows = the reduction index) by LDS-DMA and read
 // as MFMA operands with ds_read_b64_tr_b16.  BK = 64 rows of m per stage.
 // --------------------------------------------------------------------------
-template <int BM, int BN>
-__global__ void __launch_bounds__(256) conv_wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+template <int BM, int BN, int STAGES, int WM = 2, int WN = 2>
+__global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                          float* __restrict__ out, const ConvGeom g, int m_per_split,
                                                          int ldo) {
-  constexpr int BK = 64, NT = 256, WM = 2, WN = 2, STAGES = 3;
+  constexpr int BK = 64, NW = WM * WN, PD = STAGES - 1;
+  static_assert(STAGES >= 2 && STAGES <= 4, "2..4 stages");
   constexpr int ACPR = BM / 8, BCPR = BN / 8;  // chunks per LDS row (row = one m)
   constexpr int A_BYTES = BK * BM * 2, B_BYTES = BK * BN * 2, STAGE_BYTES = A_BYTES + B_BYTES;
-  constexpr int A_INS = A_BYTES / 1024 / 4, B_INS = B_BYTES / 1024 / 4;
+  constexpr int A_INS = A_BYTES / 1024 / NW, B_INS = B_BYTES / 1024 / NW;
   constexpr int LPS = A_INS + B_INS;
   constexpr int A_RPI = 64 / ACPR, B_RPI = 64 / BCPR;  // rows per glds instruction
+  static_assert(A_INS * NW * 1024 == A_BYTES && B_INS * NW * 1024 == B_BYTES, "DMA split");
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
   static_assert(A_INS >= 1 && B_INS >= 1, "tile too small");
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
@@ -495,12 +554,13 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const bf16_t* __restric
 
   const int gq = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
   const int nk = max(0, (mend - mbeg + BK - 1) / BK);
-  if (nk > 0) issue(0, 0);
-  if (nk > 1) issue(1, 1);
+#pragma unroll
+  for (int p = 0; p < PD; ++p)
+    if (p < nk) issue(p, p);
   for (int i = 0; i < nk; ++i) {
-    if (i + 1 < nk) wait_vmcnt<LPS>(); else wait_vmcnt<0>();
+    wait_stages<LPS>(min(PD - 1, nk - 1 - i));
     block_sync_lds();
-    if (i + 2 < nk) issue(i + 2, (i + 2) % STAGES);
+    if (i + PD < nk) issue(i + PD, (i + PD) % STAGES);
     const char* As = smem + (i % STAGES) * STAGE_BYTES;
     const char* Bs = As + A_BYTES;
 #pragma unroll
@@ -546,18 +606,25 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const bf16_t* __restric
 }
 
 // Sum `splits` fp32 slabs [splits][Cout][Kp] (Kp = taps*Cp) into dst
-// [Cout][taps][C] (C <= Cp: drops zero-padded input channels).
+// [Cout][taps][C] (C <= Cp: drops zero-padded input channels).  TPO lanes
+// share one output (each sums a strided subset of the splits, then a
+// fixed-order shuffle reduction): enough parallelism for 64-way slabs.
+template <int TPO>
 __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slabs, float* __restrict__ dst,
                                                           int splits, int Cout, int taps, int Cp, int C) {
   const int64_t total = (int64_t)Cout * taps * C;
   const int64_t slab = (int64_t)Cout * taps * Cp;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+  const int sub = threadIdx.x % TPO;
+  const int64_t opb = 256 / TPO;  // outputs per block iteration
+  for (int64_t i = (int64_t)blockIdx.x * opb + threadIdx.x / TPO; i < total + 0; i += (int64_t)gridDim.x * opb) {
     const int c = (int)(i % C);
     const int64_t rest = i / C;  // co*taps + tap
     const int64_t src = rest * Cp + c;
     float s = 0.f;
-    for (int sp = 0; sp < splits; ++sp) s += slabs[sp * slab + src];
-    dst[i] = s;
+    for (int sp = sub; sp < splits; sp += TPO) s += slabs[sp * slab + src];
+#pragma unroll
+    for (int o = TPO / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (sub == 0) dst[i] = s;
   }
 }
 
@@ -701,6 +768,7 @@ static int combine_rows_per_block(int M, int N) {
   return rpb < rpi ? rpi : rpb;
 }
 
+
 // number of BN partial-sum rows conv_fwd writes for this configuration
 int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile, int splits) {
   ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
@@ -709,31 +777,67 @@ int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile,
   return (g.M + rpb - 1) / rpb;
 }
 
-template <int BM, int BN, bool TAPU>
-static void launch_fwd_t(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab,
-                         int splits, hipStream_t s) {
+template <int BM, int BN, bool TAPU, int ST, int WM, int WN>
+static void launch_fwd_w(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
+                         uintptr_t slab, int splits, hipStream_t s) {
   const int ntm = (g.M + BM - 1) / BM, ntn = (g.Cout + BN - 1) / BN;
   const int nkt = (g.Kch + 7) / 8;
   const int ktps = (nkt + splits - 1) / splits;
   const int grid = ntm * ntn * splits;
+  constexpr int NT = 64 * WM * WN;
   if (splits > 1)
-    conv_fwd_kernel<BM, BN, false, true, TAPU><<<grid, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)w, nullptr,
-                                                                     nullptr, (float*)slab, g, splits, ktps);
+    conv_fwd_kernel<BM, BN, false, true, TAPU, ST, WM, WN><<<grid, NT, 0, s>>>(
+        (const bf16_t*)x, (const bf16_t*)w, nullptr, nullptr, (float*)slab, g, splits, ktps, g_conv_dbg);
   else if (stats)
-    conv_fwd_kernel<BM, BN, true, false, TAPU><<<grid, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y,
-                                                                     (float*)stats, nullptr, g, 1, ktps);
+    conv_fwd_kernel<BM, BN, true, false, TAPU, ST, WM, WN><<<grid, NT, 0, s>>>(
+        (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)stats, nullptr, g, 1, ktps, g_conv_dbg);
   else
-    conv_fwd_kernel<BM, BN, false, false, TAPU><<<grid, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y,
-                                                                      nullptr, nullptr, g, 1, ktps);
+    conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN><<<grid, NT, 0, s>>>(
+        (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, nullptr, g, 1, ktps, g_conv_dbg);
+}
+
+static int g_fwd_waves = 8;
+
+template <int BM, int BN, bool TAPU, int ST>
+static void launch_fwd_t(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
+                         uintptr_t slab, int splits, hipStream_t s) {
+  if (g_fwd_waves == 8) {
+    if constexpr (BN >= 128) launch_fwd_w<BM, BN, TAPU, ST, 2, 4>(g, x, w, y, stats, slab, splits, s);
+    else if constexpr (BM >= 128) launch_fwd_w<BM, BN, TAPU, ST, 4, 2>(g, x, w, y, stats, slab, splits, s);
+    else launch_fwd_w<BM, BN, TAPU, ST, 2, 4>(g, x, w, y, stats, slab, splits, s);
+  } else {
+    launch_fwd_w<BM, BN, TAPU, ST, 2, 2>(g, x, w, y, stats, slab, splits, s);
+  }
+}
+
+void set_conv_waves(int waves) {
+  if (waves != 4 && waves != 8) throw std::runtime_error("waves must be 4 or 8");
+  g_fwd_waves = waves;
+}
+
+static int g_fwd_stages = 3, g_wgrad_stages = 3;  // tuning knobs (set_conv_stages)
+
+void set_conv_debug(uintptr_t buf) { g_conv_dbg = (unsigned long long*)buf; }
+
+void set_conv_stages(int fwd, int wgrad) {
+  if (fwd < 2 || fwd > 4 || wgrad < 2 || wgrad > 4) throw std::runtime_error("stages must be 2..4");
+  g_fwd_stages = fwd;
+  g_wgrad_stages = wgrad;
 }
 
 template <int BM, int BN>
-static void launch_fwd(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab,
-                       int splits, hipStream_t s) {
+static void launch_fwd(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
+                       uintptr_t slab, int splits, hipStream_t s) {
   if ((int64_t)g.M * g.Cin >= (1ll << 31) || (int64_t)g.Cout * g.K >= (1ll << 31))
     throw std::runtime_error("conv_fwd: operand too large for 32-bit offsets");
-  if (g.Cin >= 64) launch_fwd_t<BM, BN, true>(g, x, w, y, stats, slab, splits, s);
-  else launch_fwd_t<BM, BN, false>(g, x, w, y, stats, slab, splits, s);
+  const int st = (BM * 64 * 2 + BN * 64 * 2) * 4 > 160 * 1024 ? std::min(g_fwd_stages, 3) : g_fwd_stages;
+  if (g.Cin >= 64) {
+    if (st == 2) launch_fwd_t<BM, BN, true, 2>(g, x, w, y, stats, slab, splits, s);
+    else if (st == 3) launch_fwd_t<BM, BN, true, 3>(g, x, w, y, stats, slab, splits, s);
+    else launch_fwd_t<BM, BN, true, 4>(g, x, w, y, stats, slab, splits, s);
+  } else {
+    launch_fwd_t<BM, BN, false, 3>(g, x, w, y, stats, slab, splits, s);
+  }
 }
 
 // tile: 0 = 128x128, 1 = 64x64, 2 = 128x64 (BM x BN, BK = 64).  splits > 1:
@@ -775,24 +879,49 @@ void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, i
   if (splits < 1) splits = 1;
   int mps = (g.M + splits - 1) / splits;
   hipStream_t s = as_stream(stream);
-  if (tile == 0) {
-    constexpr int BM = 128, BN = 64;
-    const int nt = ((g.Cout + BM - 1) / BM) * ((g.K + BN - 1) / BN);
-    conv_wgrad_kernel<BM, BN><<<dim3(nt, splits), 256, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (float*)out, g,
-                                                               mps, ldo);
+#define DL_WG(BM_, BN_, ST_, WM_, WN_)                                                                     \
+  do {                                                                                                     \
+    const int nt = ((g.Cout + BM_ - 1) / BM_) * ((g.K + BN_ - 1) / BN_);                                  \
+    conv_wgrad_kernel<BM_, BN_, ST_, WM_, WN_><<<dim3(nt, splits), 64 * WM_ * WN_, 0, s>>>(                \
+        (const bf16_t*)dy, (const bf16_t*)x, (float*)out, g, mps, ldo);                                    \
+  } while (0)
+  const int st = g_wgrad_stages;
+  if (g_fwd_waves == 8) {
+    if (tile == 0) {
+      if (st == 2) DL_WG(128, 64, 2, 4, 2); else DL_WG(128, 64, 3, 4, 2);
+    } else if (tile == 2) {
+      if (st == 2) DL_WG(128, 128, 2, 2, 4); else DL_WG(128, 128, 3, 2, 4);
+    } else {
+      if (st == 2) DL_WG(64, 64, 2, 2, 4); else DL_WG(64, 64, 3, 2, 4);
+    }
   } else {
-    constexpr int BM = 64, BN = 64;
-    const int nt = ((g.Cout + BM - 1) / BM) * ((g.K + BN - 1) / BN);
-    conv_wgrad_kernel<BM, BN><<<dim3(nt, splits), 256, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (float*)out, g,
-                                                               mps, ldo);
+    if (tile == 0) {
+      if (st == 2) DL_WG(128, 64, 2, 2, 2); else DL_WG(128, 64, 3, 2, 2);
+    } else if (tile == 2) {
+      if (st == 2) DL_WG(128, 128, 2, 2, 2); else DL_WG(128, 128, 3, 2, 2);
+    } else {
+      if (st == 2) DL_WG(64, 64, 2, 2, 2); else DL_WG(64, 64, 3, 2, 2);
+    }
   }
+#undef DL_WG
   DL_HIP_CHECK(hipGetLastError());
 }
 
 void slab_reduce(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream) {
   const int64_t total = (int64_t)Cout * taps * C;
-  slab_reduce_kernel<<<stream_grid(total), 256, 0, as_stream(stream)>>>((const float*)slabs, (float*)dst, splits,
-                                                                        Cout, taps, Cp, C);
+  auto s = as_stream(stream);
+  if (splits >= 32) {
+    int64_t g = (total * 32 + 255) / 256;
+    slab_reduce_kernel<32><<<(int)std::min<int64_t>(g, 4096), 256, 0, s>>>((const float*)slabs, (float*)dst, splits,
+                                                                          Cout, taps, Cp, C);
+  } else if (splits >= 8) {
+    int64_t g = (total * 8 + 255) / 256;
+    slab_reduce_kernel<8><<<(int)std::min<int64_t>(g, 4096), 256, 0, s>>>((const float*)slabs, (float*)dst, splits,
+                                                                         Cout, taps, Cp, C);
+  } else {
+    slab_reduce_kernel<1><<<stream_grid(total), 256, 0, s>>>((const float*)slabs, (float*)dst, splits, Cout, taps,
+                                                             Cp, C);
+  }
   DL_HIP_CHECK(hipGetLastError());
 }
 

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <atomic>
 #include <condition_variable>
 #include <cstring>
@@ -147,8 +148,15 @@ class BatchAssembler {
     if (depth < 1 || threads < 1) throw std::runtime_error("depth/threads must be >= 1");
     slots_.resize(depth);
     for (auto& s : slots_) {
-      DL_HIP_CHECK(hipHostMalloc((void**)&s.images, batch * sample_bytes, hipHostMallocDefault));
-      DL_HIP_CHECK(hipHostMalloc((void**)&s.labels, batch * sizeof(int64_t), hipHostMallocDefault));
+      // pinned (DMA-able) host slots when a HIP device exists; plain memory otherwise (CPU tests)
+      if (hipHostMalloc((void**)&s.images, batch * sample_bytes, hipHostMallocDefault) != hipSuccess ||
+          hipHostMalloc((void**)&s.labels, batch * sizeof(int64_t), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        pinned_ = false;
+        s.images = (uint8_t*)std::malloc(batch * sample_bytes);
+        s.labels = (int64_t*)std::malloc(batch * sizeof(int64_t));
+        if (!s.images || !s.labels) throw std::runtime_error("BatchAssembler: out of host memory");
+      }
       s.indices.resize(batch);
     }
     for (int t = 0; t < threads; ++t) workers_.emplace_back([this] { work(); });
@@ -162,8 +170,13 @@ class BatchAssembler {
     cv_.notify_all();
     for (auto& w : workers_) w.join();
     for (auto& s : slots_) {
-      hipHostFree(s.images);
-      hipHostFree(s.labels);
+      if (pinned_) {
+        (void)hipHostFree(s.images);
+        (void)hipHostFree(s.labels);
+      } else {
+        std::free(s.images);
+        std::free(s.labels);
+      }
     }
     delete sampler_;
   }
@@ -254,6 +267,7 @@ class BatchAssembler {
   std::condition_variable cv_;
   int64_t produce_seq_ = 0, consume_seq_ = 0;
   bool stop_ = false;
+  bool pinned_ = true;
 };
 
 }  // namespace dl

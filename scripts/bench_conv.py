@@ -19,10 +19,18 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--tile", type=int, default=-1)
     ap.add_argument("--splits", type=int, default=-1)
+    ap.add_argument("--stages", default="3,3", help="fwd,wgrad LDS ring depth")
+    ap.add_argument("--wtile", type=int, default=-1, help="override the wgrad tile (0 128x64, 1 64x64, 2 128x128)")
+    ap.add_argument("--waves", type=int, default=8, help="waves per workgroup of the fwd/dgrad kernel (4 or 8)")
     a = ap.parse_args()
     C = _native.native()
+    fs, ws = (int(v) for v in a.stages.split(","))
+    C.set_conv_stages(fs, ws)
+    C.set_conv_waves(a.waves)
+    print(f"# stages fwd={fs} wgrad={ws}")
     dev = torch.device("cuda")
-    s = torch.cuda.current_stream().cuda_stream
+    def cur():  # current-stream handle at call time (graph capture switches streams)
+        return torch.cuda.current_stream().cuda_stream
     B = a.batch
     layers = [(32, 8, 64), (16, 64, 128), (8, 128, 256), (4, 256, 512)]
     slab = torch.empty(64 * 1024 * 1024, device=dev)
@@ -42,17 +50,30 @@ def main():
             t = a.tile
         if a.splits >= 0:
             sp = a.splits
-        jobs.append((f"fwd{li+1}", 2 * M * cout * K, lambda t=t, sp=sp: C.conv_fwd(
-            x.data_ptr(), w.data_ptr(), y.data_ptr(), stats.data_ptr(), slab.data_ptr(), B, H, H, cin, cout, 5, t,
-            sp, s), f"tile{t} split{sp}"))
+        acc = torch.zeros(32, 2, cout, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        gam = torch.ones(cout, device=dev)
+        coef = torch.empty(4, cout, device=dev)
+        jobs.append((f"fwd{li+1}", 2 * M * cout * K, lambda t=t, sp=sp, acc=acc, cnt=cnt, gam=gam, coef=coef:
+                     C.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), slab.data_ptr(), B, H, H, cin, cout, 5, t,
+                                sp, acc.data_ptr(), cnt.data_ptr(), gam.data_ptr(), gam.data_ptr(), 0, 0, 0,
+                                coef.data_ptr(), 1e-3, 0.1, cur()), f"tile{t} split{sp}"))
         if li > 0:
             dt, ds = _fwd_plan(M, cin, 25 * cout)
             jobs.append((f"dgrad{li+1}", 2 * M * cout * K, lambda dt=dt, ds=ds: C.conv_fwd(
-                dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, slab.data_ptr(), B, H, H, cout, cin, 5, dt, ds, s),
+                dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), slab.data_ptr(), B, H, H, cout, cin, 5, dt, ds,
+                0, 0, 0, 0, 0, 0, 0, 0, 0.0, 0.0, cur()),
                 f"tile{dt} split{ds}"))
         wtile, wsp = _wgrad_plan(cout, K, M)
+        if a.wtile >= 0 and cout % 128 == 0:
+            wtile = a.wtile
+            bm, bn = (128, 128) if wtile == 2 else ((128, 64) if wtile == 0 else (64, 64))
+            tiles = (cout // bm) * ((K + bn - 1) // bn)
+            wsp = 1
+            while tiles * wsp < 256 and M // (wsp * 2) >= 2048:
+                wsp *= 2
         jobs.append((f"wgrad{li+1}", 2 * M * cout * K, lambda wtile=wtile, wsp=wsp: C.conv_wgrad(
-            dy.data_ptr(), x.data_ptr(), slab.data_ptr(), B, H, H, cin, cout, 5, wsp, K, wtile, s),
+            dy.data_ptr(), x.data_ptr(), slab.data_ptr(), B, H, H, cin, cout, 5, wsp, K, wtile, cur()),
             f"tile{wtile} split{wsp}"))
         for name, flops, fn, desc in jobs:
             if a.only and a.only not in name:
@@ -60,9 +81,15 @@ def main():
             for _ in range(3):
                 fn()
             torch.cuda.synchronize()
+            # replay a captured graph of `iters` launches: GPU time, not host launch rate
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(a.iters):
+                    fn()
+            g.replay()
+            torch.cuda.synchronize()
             ev0.record()
-            for _ in range(a.iters):
-                fn()
+            g.replay()
             ev1.record()
             torch.cuda.synchronize()
             us = ev0.elapsed_time(ev1) * 1e3 / a.iters

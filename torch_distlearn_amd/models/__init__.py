@@ -5,6 +5,8 @@
 * :func:`resnet50` -- BASELINE.json config 5 (bucket / xGMI stress)
 """
 from .cifar_convnet import CifarConvNet, num_params
+from .mnist import MnistConvNet, MnistMLP
+from .resnet import ResNet50, resnet50
 
 
 def make_executor(model, flat, bucketer=None, max_batch=None):
@@ -16,4 +18,12 @@ def make_executor(model, flat, bucketer=None, max_batch=None):
     raise NotImplementedError(f"no native executor for {type(model).__name__}")
 
 
-__all__ = ["CifarConvNet", "num_params", "make_executor"]
+MODELS = {"cifar10": CifarConvNet, "mnist": MnistConvNet, "mnist_mlp": MnistMLP, "resnet50": ResNet50}
+
+
+def build_model(name: str, **kw):
+    return MODELS[name](**kw)
+
+
+__all__ = ["CifarConvNet", "MnistConvNet", "MnistMLP", "ResNet50", "resnet50", "num_params", "make_executor",
+           "build_model", "MODELS"]

@@ -110,6 +110,34 @@ class CifarConvNet(nn.Module):
     def param_list(self) -> List[torch.Tensor]:
         return list(self.parameters())
 
+    # ---------------------------------------------------- reference layout I/O
+    @torch.no_grad()
+    def reference_state(self) -> List[torch.Tensor]:
+        """Parameters in the reference's layout and walk order (the ``Net``
+        checkpoint): SpatialConvolutionMM weights [Cout, Cin*5*5] in (c, kh, kw)
+        order, the linear weight over the NCHW flatten (c, h, w)."""
+        out = []
+        for i in range(self.nblocks):
+            w, b, g, beta, _, _ = self.block_params(i)
+            out += [w.permute(0, 3, 1, 2).reshape(w.shape[0], -1).clone(), b.clone(), g.clone(), beta.clone()]
+        C, hw = self.channels[-1], self.final_hw
+        fw = self.fc_w.reshape(self.num_classes, hw, hw, C).permute(0, 3, 1, 2).reshape(self.num_classes, -1)
+        return out + [fw.clone(), self.fc_b.clone()]
+
+    @torch.no_grad()
+    def load_reference_state(self, tensors: List[torch.Tensor]) -> None:
+        it = iter(tensors)
+        for i in range(self.nblocks):
+            w, b, g, beta, _, _ = self.block_params(i)
+            cout, k, _, cin = w.shape
+            w.copy_(next(it).reshape(cout, cin, k, k).permute(0, 2, 3, 1))
+            b.copy_(next(it))
+            g.copy_(next(it))
+            beta.copy_(next(it))
+        C, hw = self.channels[-1], self.final_hw
+        self.fc_w.copy_(next(it).reshape(self.num_classes, C, hw, hw).permute(0, 2, 3, 1).reshape(self.num_classes, -1))
+        self.fc_b.copy_(next(it))
+
 
 def num_params(model: nn.Module) -> int:
     return sum(p.numel() for p in model.parameters())
