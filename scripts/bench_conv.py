@@ -50,19 +50,14 @@ def main():
             t = a.tile
         if a.splits >= 0:
             sp = a.splits
-        acc = torch.zeros(32, 2, cout, device=dev)
-        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-        gam = torch.ones(cout, device=dev)
-        coef = torch.empty(4, cout, device=dev)
-        jobs.append((f"fwd{li+1}", 2 * M * cout * K, lambda t=t, sp=sp, acc=acc, cnt=cnt, gam=gam, coef=coef:
-                     C.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), slab.data_ptr(), B, H, H, cin, cout, 5, t,
-                                sp, acc.data_ptr(), cnt.data_ptr(), gam.data_ptr(), gam.data_ptr(), 0, 0, 0,
-                                coef.data_ptr(), 1e-3, 0.1, cur()), f"tile{t} split{sp}"))
+        jobs.append((f"fwd{li+1}", 2 * M * cout * K, lambda t=t, sp=sp: C.conv_fwd(
+            x.data_ptr(), w.data_ptr(), y.data_ptr(), stats.data_ptr(), slab.data_ptr(), B, H, H, cin, cout, 5, t,
+            sp, cur()), f"tile{t} split{sp}"))
         if li > 0:
             dt, ds = _fwd_plan(M, cin, 25 * cout)
             jobs.append((f"dgrad{li+1}", 2 * M * cout * K, lambda dt=dt, ds=ds: C.conv_fwd(
-                dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), slab.data_ptr(), B, H, H, cout, cin, 5, dt, ds,
-                0, 0, 0, 0, 0, 0, 0, 0, 0.0, 0.0, cur()),
+                dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, slab.data_ptr(), B, H, H, cout, cin, 5, dt, ds,
+                cur()),
                 f"tile{dt} split{ds}"))
         wtile, wsp = _wgrad_plan(cout, K, M)
         if a.wtile >= 0 and cout % 128 == 0:
