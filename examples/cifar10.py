@@ -1,0 +1,103 @@
+#!/usr/bin/env python3
+"""CIFAR-10 convnet trained with AllReduceSGD (reference: examples/cifar10.lua).
+
+Same flags as the reference (``--nodeIndex --numNodes --batchSize
+--learningRate --cuda --gpu``); ``--batchSize`` is the GLOBAL batch split
+over the nodes (ceil(B/N) per node, examples/cifar10.lua:36-37).  Each epoch:
+train on this node's partition (label-uniform sampler, :53-71), all-reduce the
+training confusion matrix (:203), ``synchronizeParameters`` (:208), evaluate
+the test partition (:213-231) and all-reduce the test confusion matrix (:234).
+
+MI355X path (``--cuda``): the dataset partition lives in HBM, batches are
+gathered+normalised on the GPU, and the step is the hand-written HIP executor
+(``--backend hip``, default) or PyTorch/MIOpen ops (``--backend torch``),
+captured in a hipGraph.  Without the dataset files (``--data`` directory with
+the CIFAR-10 binary release) synthetic CIFAR-shaped data is used.
+
+    python -m torch_distlearn_amd.launch --nproc 2 examples/cifar10.py --epochs 1
+"""
+import argparse
+import math
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from torch_distlearn_amd import LocalhostTree  # noqa: E402
+from torch_distlearn_amd.data import Dataset  # noqa: E402
+from torch_distlearn_amd.engine import DataParallelTrainer  # noqa: E402
+from torch_distlearn_amd.launch import add_node_flags, device_of, node_opts, quiet_unless_root  # noqa: E402
+from torch_distlearn_amd.models import CifarConvNet  # noqa: E402
+from torch_distlearn_amd.utils.metrics import ConfusionMatrix, JsonlMetrics  # noqa: E402
+
+CLASSES = ["airplane", "automobile", "bird", "cat", "deer", "dog", "frog", "horse", "ship", "truck"]
+
+
+def main():
+    ap = add_node_flags(argparse.ArgumentParser(description=__doc__.split("\n\n")[0]), batch=32, lr=0.1)
+    ap.add_argument("--epochs", type=int, default=100)
+    ap.add_argument("--maxSteps", type=int, default=0, help="stop each epoch after this many steps (0 = all)")
+    ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
+    ap.add_argument("--data", default=None, help="directory with the CIFAR-10 binary release (optional)")
+    ap.add_argument("--trainSize", type=int, default=50000, help="synthetic train set size")
+    ap.add_argument("--testSize", type=int, default=10000, help="synthetic test set size")
+    ap.add_argument("--graph", type=int, default=1)
+    ap.add_argument("--metrics", default=None, help="JSON-lines metrics file (node 1)")
+    opt = ap.parse_args()
+    node_opts(opt)
+    dev = device_of(opt)
+    tree = LocalhostTree(opt.nodeIndex, opt.numNodes, port=opt.port, device=dev)
+    quiet_unless_root(opt.nodeIndex)
+
+    per_node = math.ceil(opt.batchSize / opt.numNodes)  # cifar10.lua:36
+    train = Dataset("cifar10", opt.nodeIndex, opt.numNodes, train=True, root=opt.data, synthetic_size=opt.trainSize,
+                    device=dev)
+    test = Dataset("cifar10", opt.nodeIndex, opt.numNodes, train=False, root=opt.data, synthetic_size=opt.testSize,
+                   device=dev)
+    dt = torch.bfloat16 if dev.type == "cuda" else torch.float32
+    train_b = train.sampledBatcher("label-uniform", per_node, dtype=dt, seed=opt.seed + opt.nodeIndex)
+    test_b = test.sampledBatcher("linear", per_node, dtype=dt)
+
+    torch.manual_seed(0)  # same init on all nodes (cifar10.lua:105)
+    model = CifarConvNet(seed=0).to(dev)
+    backend = opt.backend if dev.type == "cuda" else "torch"
+    trainer = DataParallelTrainer(model, tree, lr=opt.learningRate, backend=backend, compute_dtype=dt,
+                                  graph=bool(opt.graph) and dev.type == "cuda", max_batch=per_node)
+    trainer.synchronize_parameters()  # cifar10.lua:139
+    conf = ConfusionMatrix(CLASSES, device=dev)
+    log = JsonlMetrics(opt.metrics, rank=opt.nodeIndex - 1)
+
+    for epoch in range(1, opt.epochs + 1):
+        conf.zero()
+        nb = train_b.numBatches() if not opt.maxSteps else min(opt.maxSteps, train_b.numBatches())
+        t0 = time.perf_counter()
+        for i in range(nb):
+            x, y = train_b.getBatch()
+            loss = trainer.step(x, y)
+            if i % 50 == 0 or i == nb - 1:
+                conf.add(trainer.last_logits(), y)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        dt_s = time.perf_counter() - t0
+        conf.allReduce(tree)  # cifar10.lua:203
+        print(f"Epoch {epoch}: train loss {float(loss):.4f}  {nb * per_node * opt.numNodes / dt_s:.0f} img/s")
+        print(conf)
+        trainer.synchronize()  # cifar10.lua:208
+        conf.zero()
+        ntb = test_b.numBatches() if not opt.maxSteps else min(opt.maxSteps, test_b.numBatches())
+        test_b.reset()
+        for _ in range(ntb):
+            x, y = test_b.getBatch()
+            conf.add(trainer.predict(x), y)
+        conf.allReduce(tree)  # cifar10.lua:234
+        print(f"Epoch {epoch}: test accuracy {100 * conf.totalValid:.2f}%")
+        log.log(epoch=epoch, loss=float(loss), images_per_s=nb * per_node * opt.numNodes / dt_s,
+                test_acc=conf.totalValid)
+    tree.comm.barrier()
+
+
+if __name__ == "__main__":
+    main()

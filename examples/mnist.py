@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""MNIST convnet trained with AllReduceSGD (reference: examples/mnist.lua).
+
+Per-node batch ``--batchSize`` (reference: 1, :33), lr 0.01 (:113), each node
+trains on its partition with a permutation sampler (:26-40) -- partitions of
+unequal length give nodes different step counts per epoch, which
+``synchronizeParameters`` reconciles with the drain protocol (:129).  The
+confusion matrix is all-reduced and printed every ``--printEvery`` steps
+(:119-125).  ``--model mlp`` trains the 2-layer MLP of BASELINE config 1.
+
+    python -m torch_distlearn_amd.launch --nproc 4 examples/mnist.py --epochs 1
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from torch_distlearn_amd import LocalhostTree  # noqa: E402
+from torch_distlearn_amd.data import Dataset  # noqa: E402
+from torch_distlearn_amd.engine import DataParallelTrainer  # noqa: E402
+from torch_distlearn_amd.launch import add_node_flags, device_of, node_opts, quiet_unless_root  # noqa: E402
+from torch_distlearn_amd.models import MnistConvNet, MnistMLP  # noqa: E402
+from torch_distlearn_amd.utils.metrics import ConfusionMatrix  # noqa: E402
+
+
+def build(opt, algo):
+    node_opts(opt)
+    dev = device_of(opt)
+    tree = LocalhostTree(opt.nodeIndex, opt.numNodes, port=opt.port, device=dev)
+    quiet_unless_root(opt.nodeIndex)
+    ds = Dataset("mnist", opt.nodeIndex, opt.numNodes, train=True, root=opt.data, synthetic_size=opt.trainSize,
+                 device=dev)
+    dt = torch.bfloat16 if dev.type == "cuda" else torch.float32
+    batcher = ds.sampledBatcher("permutation", opt.batchSize, dtype=dt, seed=opt.seed + opt.nodeIndex)
+    torch.manual_seed(0)
+    model = (MnistMLP(seed=0) if opt.model == "mlp" else MnistConvNet(seed=0)).to(dev)
+    trainer = DataParallelTrainer(model, tree, lr=opt.learningRate, algo=algo, tau=getattr(opt, "tau", 10),
+                                  alpha=getattr(opt, "alpha", 0.2), backend="torch", compute_dtype=dt,
+                                  graph=bool(opt.graph) and dev.type == "cuda" and algo == "sgd")
+    return tree, dev, batcher, model, trainer
+
+
+def run(opt, algo="sgd"):
+    tree, dev, batcher, model, trainer = build(opt, algo)
+    trainer.synchronize_parameters()
+    conf = ConfusionMatrix(10, device=dev)
+    step = 0
+    for epoch in range(1, opt.epochs + 1):
+        nb = batcher.numBatches() if not opt.maxSteps else min(opt.maxSteps, batcher.numBatches())
+        # uneven partitions: the last node(s) may run one step less -> drain protocol at sync
+        for _ in range(nb):
+            x, y = batcher.getBatch()
+            loss = trainer.step(x, y)
+            conf.add(trainer.last_logits(), y)
+            step += 1
+        # the reference all-reduces the matrix every 1000 steps (mnist.lua:119-125); a collective
+        # inside the loop requires equal step counts on every node, so it is done per epoch here
+        conf.allReduce(tree)
+        print(f"Epoch {epoch}: loss {float(loss):.4f}")
+        print(conf)
+        conf.zero()
+        trainer.synchronize()
+    tree.comm.barrier()
+    return trainer
+
+
+def parser(desc, lr=0.01, batch=1):
+    ap = add_node_flags(argparse.ArgumentParser(description=desc), batch=batch, lr=lr)
+    ap.add_argument("--epochs", type=int, default=100)
+    ap.add_argument("--maxSteps", type=int, default=0)
+    ap.add_argument("--model", default="convnet", choices=["convnet", "mlp"])
+    ap.add_argument("--data", default=None, help="directory with the MNIST idx files (optional)")
+    ap.add_argument("--trainSize", type=int, default=60000)
+    ap.add_argument("--graph", type=int, default=1)
+    return ap
+
+
+if __name__ == "__main__":
+    run(parser(__doc__.split("\n\n")[0]).parse_args(), "sgd")

@@ -1,0 +1,51 @@
+"""Example smoke tests: the reference's example programs,
+run through the launcher on CPU/gloo with tiny synthetic datasets."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _launch(nproc, script, *args, extra=(), timeout=300, cwd=None):
+    cmd = [sys.executable, "-m", "torch_distlearn_amd.launch", "--nproc", str(nproc), *extra,
+           os.path.join(ROOT, "examples", script), *args]
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=cwd or ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r.stdout
+
+
+def test_mnist_allreduce_sgd_uneven_partitions():
+    # 200 samples over 3 nodes -> partitions of 66/67/67: different step counts per node,
+    # reconciled by the drain protocol of synchronizeParameters
+    out = _launch(3, "mnist.py", "--epochs", "2", "--trainSize", "200", "--batchSize", "4")
+    assert "Epoch 2" in out and "global correct" in out
+
+
+def test_mnist_mlp_baseline_config1():
+    out = _launch(2, "mnist.py", "--model", "mlp", "--epochs", "1", "--trainSize", "256", "--batchSize", "8")
+    assert "Epoch 1" in out
+
+
+def test_mnist_allreduce_ea():
+    out = _launch(2, "mnist_ea.py", "--epochs", "2", "--trainSize", "200", "--batchSize", "4", "--tau", "3")
+    assert "Epoch 2" in out
+
+
+def test_cifar10_two_nodes():
+    out = _launch(2, "cifar10.py", "--epochs", "1", "--maxSteps", "3", "--batchSize", "8", "--trainSize", "256",
+                  "--testSize", "64", "--learningRate", "0.01")
+    assert "test accuracy" in out
+
+
+def test_async_easgd_roles(tmp_path):
+    out = _launch(4, "easgd.py", "--numNodes", "2", "--dataset", "mnist", "--trainSize", "256", "--batchSize", "16",
+                  "--communicationTime", "2", "--testTime", "2", "--numEpochs", "1",
+                  "--resultsRoot", str(tmp_path / "Results"), extra=("--no-node-flags",))
+    assert "server:" in out and "tester:" in out
+    d = tmp_path / "Results" / "log"
+    assert (d / "ErrorRate.log").read_text().splitlines()[0] == "Training Error\tTest Error"
+    assert (d / "Net").exists() and (d / "optState").exists()

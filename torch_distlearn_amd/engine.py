@@ -87,6 +87,7 @@ class DataParallelTrainer:
             return self.executor.forward_backward(x, y)
         self.model.train()
         logp = self.model(x, compute_dtype=self.compute_dtype)
+        self._last_logp = logp.detach()
         loss = self.loss_fn(logp, y)
         loss.backward()
         return loss.detach()
@@ -159,6 +160,14 @@ class DataParallelTrainer:
             self.sgd.synchronizeParameters(self.flat)
         else:
             self.ea.synchronizeParameters(self.flat)
+
+    def last_logits(self) -> torch.Tensor:
+        """Log-probabilities of the last training batch (train-mode forward),
+        what the reference feeds its training confusion matrix
+        (examples/cifar10.lua:194-196)."""
+        if self.executor is not None:
+            return self.executor.last_logits()
+        return self._last_logp
 
     @torch.no_grad()
     def predict(self, x: torch.Tensor) -> torch.Tensor:

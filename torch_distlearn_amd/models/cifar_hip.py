@@ -186,6 +186,7 @@ class CifarHIPExecutor:
         if labels.dtype != torch.int64:
             raise ValueError("labels must be int64")
         B = self._prep(x, s)
+        self._last_b = B
         self._forward(B, s, train=True)
         nfc = 4 * self.nb
         C.head_fwd_bwd(self.p[-1].data_ptr(), self.p32[nfc].data_ptr(), self.p32[nfc + 1].data_ptr(),
@@ -226,6 +227,9 @@ class CifarHIPExecutor:
                 C.conv_fwd(self.dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), 0,
                            self.slabs.data_ptr(), B, h, h, cout, cin, KSIZE, dt, ds, s)
         return self.loss[0]
+
+    def last_logits(self) -> torch.Tensor:
+        return self.logits[:self._last_b]
 
     def _ready(self, leaf: int):
         if self.bucketer is not None:
