@@ -1,0 +1,125 @@
+"""GPU integration: data pipeline kernels, the DataParallelTrainer on one
+MI355X (HIP executor eager vs hipGraph replay vs the PyTorch path), the
+examples with --cuda, and bench.py's JSON contract."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from torch_distlearn_amd import _native
+
+    _native.native()
+    return torch.device("cuda:0")
+
+
+def test_gather_normalize_and_confusion(dev):
+    from torch_distlearn_amd.data import PartitionedDataset, synthetic_cifar10
+    from torch_distlearn_amd.utils.metrics import ConfusionMatrix
+
+    imgs, labels = synthetic_cifar10(256)
+    ds_cpu = PartitionedDataset(imgs, labels, 2, 3)
+    ds_gpu = PartitionedDataset(imgs, labels, 2, 3, device=dev)
+    bc = ds_cpu.sampledBatcher("linear", 16, channels_out=8, dtype=torch.float32)
+    bg = ds_gpu.sampledBatcher("linear", 16, channels_out=8, dtype=torch.bfloat16)
+    for _ in range(3):
+        xc, yc = bc.getBatch()
+        xg, yg = bg.getBatch()
+        torch.cuda.synchronize()
+        torch.testing.assert_close(xg.float().cpu(), xc.to(torch.bfloat16).float(), rtol=0, atol=1e-2)
+        assert torch.equal(yg.cpu(), yc)
+    pred = torch.randn(300, 10, device=dev)
+    tgt = torch.randint(0, 10, (300,), device=dev)
+    cg, cc = ConfusionMatrix(10, device=dev), ConfusionMatrix(10)
+    cg.add(pred, tgt)
+    cg.add(pred.to(torch.bfloat16), tgt)
+    cc.add(pred.cpu(), tgt.cpu())
+    cc.add(pred.to(torch.bfloat16).float().cpu(), tgt.cpu())
+    torch.cuda.synchronize()
+    assert torch.equal(cg.mat.cpu(), cc.mat)
+
+
+def _trainer(dev, backend, graph, port):
+    from torch_distlearn_amd import Tree
+    from torch_distlearn_amd.engine import DataParallelTrainer
+    from torch_distlearn_amd.models import CifarConvNet
+
+    tree = Tree(1, 1, host="127.0.0.1", port=port, device=dev)
+    model = CifarConvNet(seed=7).to(dev)
+    tr = DataParallelTrainer(model, tree, lr=0.02, backend=backend, compute_dtype=torch.bfloat16, graph=graph,
+                             max_batch=32)
+    tr.synchronize_parameters()
+    return tr
+
+
+def test_hip_graph_replay_matches_eager(dev):
+    g = torch.Generator(device=dev).manual_seed(0)
+    xs = torch.randn(4, 32, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)
+    ys = torch.randint(0, 10, (4, 32), device=dev, generator=g)
+    outs = []
+    for graph, port in ((False, 29701), (True, 29701)):
+        tr = _trainer(dev, "hip", graph, port)
+        losses = [float(tr.step(xs[i], ys[i])) for i in range(4)]
+        torch.cuda.synchronize()
+        outs.append((tr.flat.data.clone(), losses, tr.sgd.stepsPerNode.clone()))
+    (p0, l0, s0), (p1, l1, s1) = outs
+    assert torch.equal(s0, s1) and int(s0.sum()) == 4
+    assert max(abs(a - b) for a, b in zip(l0, l1)) < 1e-3
+    assert float((p0 - p1).abs().max()) < 1e-3
+
+
+def test_hip_and_torch_backends_train_alike(dev):
+    g = torch.Generator(device=dev).manual_seed(1)
+    x = torch.randn(32, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)
+    y = torch.randint(0, 10, (32,), device=dev, generator=g)
+    res = {}
+    for backend in ("hip", "torch"):
+        tr = _trainer(dev, backend, False, 29702)
+        losses = [float(tr.step(x, y)) for _ in range(6)]
+        res[backend] = losses
+    assert res["hip"][-1] < res["hip"][0]  # fits the repeated batch
+    for a, b in zip(res["hip"], res["torch"]):
+        assert abs(a - b) < 0.1 * max(1.0, abs(b))
+
+
+def _run(args, timeout=600):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable] + args, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r.stdout
+
+
+def test_cifar10_example_cuda(dev):
+    out = _run(["-m", "torch_distlearn_amd.launch", "--nproc", "1", "--gpus", "examples/cifar10.py", "--epochs", "1",
+                "--maxSteps", "20", "--batchSize", "64", "--trainSize", "2048", "--testSize", "256",
+                "--learningRate", "0.05"])
+    assert "test accuracy" in out
+
+
+def test_mnist_examples_cuda(dev):
+    out = _run(["-m", "torch_distlearn_amd.launch", "--nproc", "1", "--gpus", "examples/mnist.py", "--epochs", "1",
+                "--trainSize", "256", "--batchSize", "8"])
+    assert "Epoch 1" in out
+    out = _run(["-m", "torch_distlearn_amd.launch", "--nproc", "1", "--gpus", "examples/mnist_ea.py", "--epochs",
+                "1", "--trainSize", "256", "--batchSize", "8"])
+    assert "Epoch 1" in out
+
+
+@pytest.mark.parametrize("algo", ["sgd", "ea"])
+def test_bench_json_contract(dev, algo):
+    out = _run(["bench.py", "--steps", "5", "--warmup", "2", "--algo", algo])
+    rec = json.loads(out.strip().splitlines()[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in rec
+    assert rec["n_gpus"] == 1 and rec["steps"] == 5 and rec["value"] > 0 and rec["dtype"] == "bf16"
