@@ -67,3 +67,28 @@ def test_engine_ea_centers_agree():
     res = mp.run(_worker, 2, "ea", True)
     # after synchronizeCenter the centers are broadcast; params differ (elastic), runs must not deadlock
     assert all(torch.isfinite(torch.from_numpy(r["p"])).all() for r in res)
+
+
+def _debug_worker(rank, world, port, perturb):
+    import os
+
+    os.environ["DISTLEARN_DEBUG_SYNC"] = "1"
+    from torch_distlearn_amd import AllReduceSGD, Tree
+    from torch_distlearn_amd.utils.debug import assert_replicas_in_sync
+
+    tree = Tree(rank + 1, world, host="127.0.0.1", port=port)
+    params = [torch.arange(5.0)]
+    sgd = AllReduceSGD(tree)
+    sgd.synchronizeParameters(params)  # runs the checksum check (in sync)
+    if perturb and rank == 1:
+        params[0][2] += 1e-3
+    try:
+        assert_replicas_in_sync(tree, params[0])
+        return "ok"
+    except RuntimeError as e:
+        return "diverged" if "divergence" in str(e) else repr(e)
+
+
+def test_replica_divergence_detection():
+    assert mp.run(_debug_worker, 2, False) == ["ok", "ok"]
+    assert mp.run(_debug_worker, 2, True) == ["diverged", "diverged"]

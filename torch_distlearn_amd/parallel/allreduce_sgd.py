@@ -157,6 +157,11 @@ class AllReduceSGD:
         if isinstance(params, FlatParams):
             params.refresh_shadow()
         self.stepsPerNode.zero_()  # (:49)
+        from ..utils.debug import assert_replicas_in_sync, debug_sync_enabled
+
+        if debug_sync_enabled():
+            assert_replicas_in_sync(self.tree, params.data if isinstance(params, FlatParams)
+                                    else torch.cat([t.reshape(-1) for t in walk_table(params)]))
         return params
 
     # python spellings
