@@ -33,13 +33,35 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=128, help="per-GPU batch (weak scaling)")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (weak scaling; cifar10 128, resnet50 256)")
     ap.add_argument("--backend", default=os.environ.get("DISTLEARN_BENCH_BACKEND", "hip"), choices=["hip", "torch"])
-    ap.add_argument("--algo", default="sgd", choices=["sgd", "ea"])
+    ap.add_argument("--algo", default="sgd", choices=["sgd", "ea", "async"],
+                    help="sgd = AllReduceSGD (headline), ea = AllReduceEA (tau, alpha), "
+                         "async = AsyncEA: rank 0 parameter server + N-1 clients (BASELINE configs 2-4)")
+    ap.add_argument("--model", default="cifar10", choices=["cifar10", "resnet50"],
+                    help="resnet50 = BASELINE config 5 (ImageNet shape 224x224, MIOpen ops)")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu = gloo plumbing check of the same code path (tests only; not a benchmark)")
+    ap.add_argument("--tau", type=int, default=10)
+    ap.add_argument("--alpha", type=float, default=0.2)
     ap.add_argument("--graph", type=int, default=1, help="capture the step in a hipGraph")
     ap.add_argument("--bucket-mb", type=float, default=4.0)
     ap.add_argument("--lr", type=float, default=0.1)
     return ap.parse_args()
+
+
+METRICS = {
+    ("cifar10", "sgd"): "images/sec (whole node) CIFAR-10 AllReduceSGD",
+    ("cifar10", "ea"): "images/sec (whole node) CIFAR-10 AllReduceEA",
+    ("cifar10", "async"): "images/sec (whole node, clients) CIFAR-10 AsyncEA",
+    ("resnet50", "sgd"): "images/sec (whole node) ResNet-50 AllReduceSGD",
+    ("resnet50", "ea"): "images/sec (whole node) ResNet-50 AllReduceEA",
+    ("resnet50", "async"): "images/sec (whole node, clients) ResNet-50 AsyncEA",
+}
+MODEL_DESC = {
+    "cifar10": "cifar10-convnet (examples/cifar10.lua, 4.33M params)",
+    "resnet50": "resnet50 (ImageNet shape 224x224, 25.6M params)",
+}
 
 
 def main():
@@ -50,54 +72,89 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            print(f"bench.py: --gpus {a.gpus} needs torch.distributed.run with {a.gpus} processes", file=sys.stderr)
-            sys.exit(2)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if world != a.gpus and world == 1 and a.gpus > 1:
+        print(f"bench.py: --gpus {a.gpus} needs torch.distributed.run with {a.gpus} processes", file=sys.stderr)
+        sys.exit(2)
+    if a.algo == "async" and world < 2:
+        print("bench.py: --algo async needs >= 2 ranks (1 server + clients)", file=sys.stderr)
+        sys.exit(2)
+    cpu = a.device == "cpu"
+    if cpu:
+        dev = torch.device("cpu")
+        sync = lambda: None  # noqa: E731
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        sync = torch.cuda.synchronize
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29517")
+    batch = a.batch or (128 if a.model == "cifar10" else 256)
+    backend = a.backend if (a.model == "cifar10" and not cpu) else "torch"
+    cdt = torch.float32 if cpu else torch.bfloat16
 
     from torch_distlearn_amd import Tree
     from torch_distlearn_amd.engine import DataParallelTrainer
-    from torch_distlearn_amd.models import CifarConvNet
+    from torch_distlearn_amd.models import CifarConvNet, ResNet50
+    from torch_distlearn_amd.utils.color_print import set_verbose
+
+    set_verbose(False)  # one JSON line on stdout
 
     tree = Tree(rank + 1, world, host=os.environ["MASTER_ADDR"], port=int(os.environ["MASTER_PORT"]), device=dev)
-    model = CifarConvNet(seed=0).to(dev)
-    graph = bool(a.graph) and a.algo == "sgd"
-    tr = DataParallelTrainer(model, tree, lr=a.lr, algo=a.algo, backend=a.backend, compute_dtype=torch.bfloat16,
-                             bucket_bytes=int(a.bucket_mb * (1 << 20)), graph=graph, max_batch=a.batch)
-    tr.synchronize_parameters()
+    model = (CifarConvNet(seed=0) if a.model == "cifar10" else ResNet50(seed=0)).to(dev)
+    is_server = a.algo == "async" and rank == 0
+    # the workers that train: all ranks, or the AsyncEA clients (ranks 1..N-1)
+    workers = list(range(1, world)) if a.algo == "async" else list(range(world))
+    wgroup = dist.new_group(workers, backend="gloo") if a.algo == "async" else None
 
-    # synthetic CIFAR-shaped data: NHWC bf16, normalised; labels uniform over 10 classes
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    nb = 8
-    xs = torch.randn(nb, a.batch, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)
-    ys = torch.randint(0, 10, (nb, a.batch), device=dev, generator=g)
+    def worker_barrier():
+        if wgroup is None:
+            tree.comm.barrier()
+        else:
+            dist.barrier(group=wgroup)
 
-    for i in range(a.warmup):
-        tr.step(xs[i % nb], ys[i % nb])
-    torch.cuda.synchronize()
-    tree.comm.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        loss = tr.step(xs[i % nb], ys[i % nb])
-    torch.cuda.synchronize()
-    tree.comm.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64)
+    dt, loss = 0.0, None
+    if is_server:
+        from torch_distlearn_amd import AsyncEA, FlatParams
+
+        flat = FlatParams(model, grads=False, shadow_bf16=not cpu)
+        server = AsyncEA(tree, None, None, None, None, None, world - 1, 0, a.tau, a.alpha)
+        server.initServer(flat)
+        while server.syncServer(flat):
+            pass
+    else:
+        tr = DataParallelTrainer(model, tree, lr=a.lr, algo=a.algo, tau=a.tau, alpha=a.alpha, backend=backend,
+                                 compute_dtype=cdt, bucket_bytes=int(a.bucket_mb * (1 << 20)),
+                                 graph=bool(a.graph) and not cpu, max_batch=batch)
+        tr.synchronize_parameters()
+        # synthetic data of the named shape: NHWC bf16, normalised; labels uniform
+        g = torch.Generator(device=dev).manual_seed(1234 + rank)
+        nb = 8 if a.model == "cifar10" else 2
+        hw, ncls = (32, 10) if a.model == "cifar10" else (224, 1000)
+        xs = torch.randn(nb, batch, hw, hw, 3, device=dev, generator=g).to(cdt)
+        ys = torch.randint(0, ncls, (nb, batch), device=dev, generator=g)
+        for i in range(a.warmup):
+            tr.step(xs[i % nb], ys[i % nb])
+        sync()
+        worker_barrier()
+        sync()
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            loss = tr.step(xs[i % nb], ys[i % nb])
+        sync()
+        worker_barrier()
+        sync()
+        dt = time.perf_counter() - t0
+        tr.finish()
+    # max over ranks (the AsyncEA server contributes 0); loss from the first worker
+    t = torch.tensor([dt, float(loss.float().item()) if (loss is not None and rank == workers[0]) else -1e30],
+                     dtype=torch.float64)
     tree.comm.all_reduce_host(t, "max")
-    dt = float(t.item())
+    dt, lval = float(t[0]), float(t[1])
     ms = dt / a.steps * 1e3
-    imgs = a.batch * world * a.steps / dt
-    lval = float(loss.float().item())
+    imgs = batch * len(workers) * a.steps / dt
     if rank == 0:
         out = {
-            "metric": "images/sec (whole node) CIFAR-10 AllReduceSGD" if a.algo == "sgd"
-            else "images/sec (whole node) CIFAR-10 AllReduceEA",
+            "metric": METRICS[(a.model, a.algo)],
             "value": round(imgs, 1),
             "unit": "images/s",
             "n_gpus": world,
@@ -107,12 +164,13 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else round(imgs / BASELINE_VALUE, 4),
-            "dtype": "bf16",
-            "data": "synthetic (CIFAR-10 shaped 32x32x3, random-init weights)",
-            "config": {"model": "cifar10-convnet (examples/cifar10.lua, 4.33M params)",
-                       "global_batch": a.batch * world, "per_gpu_batch": a.batch, "seq_len": None,
-                       "parallelism": f"dp{world}", "algo": a.algo, "backend": a.backend, "hipgraph": graph,
-                       "bucket_mb": a.bucket_mb},
+            "dtype": "fp32" if cpu else "bf16",
+            "data": f"synthetic ({a.model} shaped, random-init weights)",
+            "config": {"model": MODEL_DESC[a.model],
+                       "global_batch": batch * len(workers), "per_gpu_batch": batch, "seq_len": None,
+                       "parallelism": f"dp{len(workers)}" + ("+ps1" if a.algo == "async" else ""), "algo": a.algo,
+                       "backend": backend, "hipgraph": bool(a.graph), "bucket_mb": a.bucket_mb,
+                       **({"tau": a.tau, "alpha": a.alpha} if a.algo != "sgd" else {})},
             "final_loss": round(lval, 4),
         }
         print(json.dumps(out), flush=True)

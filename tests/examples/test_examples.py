@@ -49,3 +49,30 @@ def test_async_easgd_roles(tmp_path):
     d = tmp_path / "Results" / "log"
     assert (d / "ErrorRate.log").read_text().splitlines()[0] == "Training Error\tTest Error"
     assert (d / "Net").exists() and (d / "optState").exists()
+
+
+@pytest.mark.parametrize("algo", ["sgd", "ea", "async"])
+def test_bench_contract_cpu(algo):
+    """bench.py under torch.distributed.run (the driver's N>1 launch), run on
+    CPU/gloo: one JSON line from rank 0 with whole-job images/s; AsyncEA = rank 0
+    parameter server + 2 clients (BASELINE configs 2-4 plumbing)."""
+    import json
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "3", "--steps", "3",
+           "--warmup", "1", "--device", "cpu", "--batch", "4", "--algo", algo, "--tau", "2"]
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 3 and out["steps"] == 3 and out["warmup"] == 1 and out["higher_is_better"]
+    workers = 2 if algo == "async" else 3
+    assert out["config"]["global_batch"] == 4 * workers
+    assert abs(out["value"] - 4 * workers * 1000.0 / out["ms_per_step"]) / out["value"] < 1e-3

@@ -44,7 +44,8 @@ class DataParallelTrainer:
                  weight_decay: float = 0.0, algo: str = "sgd", tau: int = 10, alpha: float = 0.2,
                  backend: str = "torch", compute_dtype: torch.dtype = torch.bfloat16,
                  bucket_bytes: int = 4 << 20, overlap: bool = True, graph: bool = False,
-                 loss_fn: Optional[Callable] = None, max_batch: Optional[int] = None):
+                 loss_fn: Optional[Callable] = None, max_batch: Optional[int] = None,
+                 async_ea: Optional[Any] = None):
         self.model = model
         self.tree = tree
         self.lr, self.momentum, self.weight_decay = lr, momentum, weight_decay
@@ -59,7 +60,8 @@ class DataParallelTrainer:
         self.loss_fn = loss_fn or getattr(model, "loss", None) or torch.nn.functional.nll_loss
         hooks = overlap and backend == "torch"
         self.bucketer = GradBucketer(tree.comm, self.flat, bucket_bytes=bucket_bytes, hooks=hooks) \
-            if tree.numNodes > 1 or dev.type == "cuda" else None
+            if (tree.numNodes > 1 or dev.type == "cuda") and algo == "sgd" else None
+        self.aea = None
         if algo == "sgd":
             self.sgd = AllReduceSGD(tree, bucketer=self.bucketer)
             self.ea = None
@@ -67,6 +69,15 @@ class DataParallelTrainer:
             self.sgd = None
             self.ea = AllReduceEA(tree, tau, alpha)
             self.ea._one_time_init(self.flat)
+        elif algo == "async":
+            # AsyncEA client (examples/EASGD_client.lua:97-119): grads, then the
+            # elastic sync every tau steps, then SGD with the pre-move grads
+            from .parallel.async_ea import AsyncEA
+
+            self.sgd = self.ea = None
+            self.aea = async_ea or AsyncEA(tree, None, None, None, None, None, tree.numNodes - 1,
+                                           tree.nodeIndex - 1, tau, alpha)
+            self.aea._one_time_init(self.flat)
         else:
             raise ValueError(f"unknown algo {algo!r}")
         self.executor = None
@@ -93,6 +104,9 @@ class DataParallelTrainer:
         return loss.detach()
 
     def _step_body(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        """The capturable part of a step: zero grads, forward, backward and
+        the update (SGD: bucketed all-reduce + fused 1/n SGD; EA: the local
+        SGD step -- the elastic round every tau steps runs after it)."""
         f = self.flat
         # zero grads, participation slot = 1 (this node contributes this round)
         fill_(f.grad, 0.0, slot_value=1.0)
@@ -100,30 +114,48 @@ class DataParallelTrainer:
         if self.algo == "sgd":
             self.sgd.step(f, self.lr, momentum=self.momentum, weight_decay=self.weight_decay,
                           momentum_buf=self.mom)
-        else:
-            from .ops.flat import sgd_update_
-
-            sgd_update_(f.data, f.grad, self.lr, slot=None, mom=self.mom, momentum=self.momentum,
-                        weight_decay=self.weight_decay, shadow=f.shadow)
-            self.ea.averageParameters(f)
+        elif self.algo == "ea":
+            self._local_update()
         return loss
+
+    def _local_update(self) -> None:
+        from .ops.flat import sgd_update_
+
+        f = self.flat
+        sgd_update_(f.data, f.grad, self.lr, slot=None, mom=self.mom, momentum=self.momentum,
+                    weight_decay=self.weight_decay, shadow=f.shadow)
 
     def step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         """One training step on this node's mini-batch; returns the loss
         (a device tensor; no host synchronisation)."""
         self.steps += 1
-        if not self.graph or self.algo != "sgd":
+        if not self.graph:
             loss = self._step_body(x, y)
-            self.last_loss = loss
-            return loss
-        if self._graph is None:
-            self._capture(x, y)
-        self._static[0].copy_(x, non_blocking=True)
-        self._static[1].copy_(y, non_blocking=True)
-        self._graph.replay()
-        # the captured body counted one step at capture time only
-        self.sgd._count_step()
-        return self._static[2]
+        else:
+            if self._graph is None:
+                self._capture(x, y)
+            if x.data_ptr() != self._static[0].data_ptr():
+                self._static[0].copy_(x, non_blocking=True)
+            if y.data_ptr() != self._static[1].data_ptr():
+                self._static[1].copy_(y, non_blocking=True)
+            self._graph.replay()
+            if self.sgd is not None:
+                # the captured body counted one step at capture time only
+                self.sgd._count_step()
+            loss = self._static[2]
+        if self.ea is not None:
+            # every tau steps: fused elastic kernel + one all-reduce (lua/AllReduceEA.lua:25-47)
+            self.ea.averageParameters(self.flat)
+        elif self.aea is not None:
+            self.aea.syncClient(self.flat)   # EASGD_client.lua:109
+            self._local_update()             # :113-117 (pre-move grads)
+        self.last_loss = loss
+        return loss
+
+    def static_inputs(self):
+        """The graph's input buffers (after the first step): a data loader
+        that writes batches straight into them skips the per-step copy."""
+        return None if self._static is None else self._static[:2]
 
     def _capture(self, x, y):
         sx, sy = x.clone(), y.clone()
@@ -131,6 +163,7 @@ class DataParallelTrainer:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         saved = self.flat.data.clone()
+        saved_mom = None if self.mom is None else self.mom.clone()
         with torch.cuda.stream(s):
             for _ in range(2):
                 self._step_body(sx, sy)
@@ -140,26 +173,38 @@ class DataParallelTrainer:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             loss = self._step_body(sx, sy)
-        # the warm-up + capture bodies counted steps; undo (replay() counts itself)
-        self.sgd.stepsPerNode[self.tree.nodeIndex - 1] -= 3
+        if self.sgd is not None:
+            # the warm-up + capture bodies counted steps; undo (replay() counts itself)
+            self.sgd.stepsPerNode[self.tree.nodeIndex - 1] -= 3
         self.flat.data.copy_(saved)
         self.flat.refresh_shadow()
+        if saved_mom is not None:
+            self.mom.copy_(saved_mom)
         self._graph, self._static = g, (sx, sy, loss)
 
     # ------------------------------------------------------------------ epoch end
     def synchronize(self) -> None:
         """Epoch-end synchronisation (examples/cifar10.lua:208 /
-        examples/mnist-ea.lua:121)."""
+        examples/mnist-ea.lua:121).  AsyncEA clients have none."""
         if self.algo == "sgd":
             self.sgd.synchronizeParameters(self.flat)
-        else:
+        elif self.algo == "ea":
             self.ea.synchronizeCenter(self.flat)
 
     def synchronize_parameters(self) -> None:
+        """Initial synchronisation (AsyncEA: receive the server's center,
+        AsyncEA.lua:64-78)."""
         if self.algo == "sgd":
             self.sgd.synchronizeParameters(self.flat)
-        else:
+        elif self.algo == "ea":
             self.ea.synchronizeParameters(self.flat)
+        else:
+            self.aea.initClient(self.flat)
+
+    def finish(self) -> None:
+        """AsyncEA client: tell the server this client is done."""
+        if self.aea is not None:
+            self.aea.finishClient()
 
     def last_logits(self) -> torch.Tensor:
         """Log-probabilities of the last training batch (train-mode forward),
