@@ -74,6 +74,7 @@ def _compile(src: str, force: bool, verbose: bool, newest_header: float):
     if (not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), newest_header)):
         return obj, 0.0, False
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-c", src, "-o", obj] + COMMON + _includes()
+    cmd += os.environ.get("DISTLEARN_CFLAGS", "").split()  # A/B experiments (e.g. -DDL_FWD_SWAP=0)
     if src.endswith(".cpp") and "bindings" in src:
         cmd += ["-fvisibility=hidden"]
     t0 = time.time()

@@ -102,7 +102,7 @@ __global__ void __launch_bounds__(256) head_wgrad_kernel(const bf16_t* __restric
                                                          const float* __restrict__ dlogits,
                                                          const float* __restrict__ loss_b, int F, int B,
                                                          float* __restrict__ dw, float* __restrict__ db,
-                                                         float* __restrict__ loss) {
+                                                         float* __restrict__ loss, float* __restrict__ slot) {
   __shared__ float red[8][NC + 1][33];
   const int tid = threadIdx.x, col = tid & 31, grp = tid >> 5;
   const int nblk_cols = (F + 31) / 32;
@@ -148,8 +148,12 @@ __global__ void __launch_bounds__(256) head_wgrad_kernel(const bf16_t* __restric
         for (int cc = 0; cc < 32; ++cc) s += red[g][tid][cc];
       if (tid < NC) {
         if (db) db[tid] = s;
-      } else if (loss) {
-        *loss = s / (float)B;
+      } else {
+        if (loss) *loss = s / (float)B;
+        // participation count of this node's gradient (flat-buffer header):
+        // replaces a per-step fill of the whole gradient buffer, every other
+        // gradient element is overwritten by its producing kernel
+        if (slot) *slot = 1.0f;
       }
     }
   }
@@ -166,11 +170,11 @@ void head_fwd_bwd(uintptr_t h, uintptr_t w, uintptr_t bias, uintptr_t labels, in
 }
 
 void head_wgrad(uintptr_t h, uintptr_t dlogits, uintptr_t loss_b, int F, int B, int NC, uintptr_t dw, uintptr_t db,
-                uintptr_t loss, uintptr_t stream) {
+                uintptr_t loss, uintptr_t slot, uintptr_t stream) {
   if (NC != 10) throw std::runtime_error("head_wgrad: built for 10 classes");
   head_wgrad_kernel<10><<<(F + 31) / 32 + 1, 256, 0, as_stream(stream)>>>((const bf16_t*)h, (const float*)dlogits,
                                                                         (const float*)loss_b, F, B, (float*)dw,
-                                                                        (float*)db, (float*)loss);
+                                                                        (float*)db, (float*)loss, (float*)slot);
   DL_HIP_CHECK(hipGetLastError());
 }
 

@@ -206,8 +206,10 @@ def test_head(C):
     loss = torch.empty(1, device=dev)
     C.head_fwd_bwd(h.data_ptr(), w.data_ptr(), b.data_ptr(), lab.data_ptr(), Fd, B, NC, logp.data_ptr(),
                    dlog.data_ptr(), lb.data_ptr(), dh.data_ptr(), _s())
+    slot = torch.zeros(1, device=dev)
     C.head_wgrad(h.data_ptr(), dlog.data_ptr(), lb.data_ptr(), Fd, B, NC, dw.data_ptr(), db.data_ptr(),
-                 loss.data_ptr(), _s())
+                 loss.data_ptr(), slot.data_ptr(), _s())
+    assert float(slot) == 1.0
     hr = h.float().requires_grad_(True)
     wr = w.clone().requires_grad_(True)
     br = b.clone().requires_grad_(True)

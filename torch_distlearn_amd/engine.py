@@ -108,8 +108,10 @@ class DataParallelTrainer:
         the update (SGD: bucketed all-reduce + fused 1/n SGD; EA: the local
         SGD step -- the elastic round every tau steps runs after it)."""
         f = self.flat
-        # zero grads, participation slot = 1 (this node contributes this round)
-        fill_(f.grad, 0.0, slot_value=1.0)
+        # zero grads, participation slot = 1 (this node contributes this round);
+        # a native executor that overwrites every gradient sets the slot itself
+        if not getattr(self.executor, "overwrites_grads", False):
+            fill_(f.grad, 0.0, slot_value=1.0)
         loss = self._forward_backward(x, y)
         if self.algo == "sgd":
             self.sgd.step(f, self.lr, momentum=self.momentum, weight_decay=self.weight_decay,

@@ -14,6 +14,17 @@ torch-autograd + cunn).  Per block i:
             -> bn_relu_pool_bwd_apply (dy) -> conv_wgrad (-> slab_reduce)
             -> conv dgrad (= conv_fwd on dy with flipped/transposed weights)
 
+Optional side stream (measured, off by default): the dgrad weight
+flip-transposes only depend on the previous update and could run during the
+forward (``DISTLEARN_PREP_FORK=1``); the weight gradient of block i only
+needs dy_i and the block's input and could run concurrently with the dgrad of
+block i and the BN/pool backward of block i-1 (``DISTLEARN_WGRAD_STREAM=1``).
+On MI355X both are net LOSSES at batch 128 inside the hipGraph (0.531 and
+0.567 vs 0.480 ms/step): every kernel of the step already spans the 256 CUs,
+concurrent kernels thrash each other's L2, and the cross-queue dependencies
+cost more than the overlap wins.  Forks re-join the main stream before
+forward_backward returns (graph-capturable fork/join).
+
 Gradients are written (fp32) straight into the flat gradient buffer; as soon
 as a block's gradients are final its leaves are reported to the
 :class:`~torch_distlearn_amd.parallel.buckets.GradBucketer`, which launches
@@ -23,6 +34,7 @@ refreshes (conv) or as the fp32 master (BN affine, classifier).
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
@@ -87,6 +99,16 @@ class CifarHIPExecutor:
         self.g32 = flat.views_of(flat.grad)
         self.rm = [getattr(model, f"bn{i + 1}_rm") for i in range(self.nb)]
         self.rv = [getattr(model, f"bn{i + 1}_rv") for i in range(self.nb)]
+        # every gradient element is overwritten each step by its producing kernel
+        # (conv biases: exactly 0 under train-mode BN, zeroed once here) and
+        # head_wgrad sets the participation slot: the engine skips the per-step
+        # fill of the gradient buffer
+        self.overwrites_grads = True
+        for i in range(self.nb):
+            self.g32[self._leaf(i, 1)].zero_()
+        self.side = torch.cuda.Stream(device=self.dev) if self.dev.type == "cuda" else None
+        self.fork_transposes = os.environ.get("DISTLEARN_PREP_FORK", "0") == "1"
+        self.side_wgrad = os.environ.get("DISTLEARN_WGRAD_STREAM", "0") == "1"
         self._alloc(self.B)
 
     # ------------------------------------------------------------------ buffers
@@ -100,13 +122,15 @@ class CifarHIPExecutor:
         self.y = [e(B, h, h, c) for h, c in zip(self.hs, self.couts)]
         self.p = [e(B, h // 2, h // 2, c) for h, c in zip(self.hs, self.couts)]
         self.dP = [e(B, h // 2, h // 2, c) for h, c in zip(self.hs, self.couts)]
-        self.dY = e(max(B * h * h * c for h, c in zip(self.hs, self.couts)))
+        # one dy buffer per block: block i's wgrad (side stream) still reads dy_i
+        # while the main stream writes dy_{i-1}
+        self.dYs = [e(B * h * h * c) for h, c in zip(self.hs, self.couts)]
         self.coef = [torch.empty(4, c, device=d) for c in self.couts]
         self.acoef = [torch.empty(3, c, device=d) for c in self.couts]
         self.fwd_plan, self.stats = [], []
         self.dgrad_plan = [None] * self.nb
         self.bwd_blocks, self.bwd_part = [], []
-        self.wplan, slab_elems = [], 0
+        self.wplan, slab_elems, wslab_elems = [], 0, 0
         for i in range(self.nb):
             h, cin, cout = self.hs[i], self.cins[i], self.couts[i]
             M = B * h * h
@@ -126,13 +150,14 @@ class CifarHIPExecutor:
             direct = splits_w == 1 and cin == self.cins_real[i]
             self.wplan.append((tile_w, splits_w, direct))
             if not direct:
-                slab_elems = max(slab_elems, splits_w * cout * K)
+                wslab_elems = max(wslab_elems, splits_w * cout * K)
             if i > 0:
                 dt, ds = _fwd_plan(M, cin, KSIZE * KSIZE * cout)
                 self.dgrad_plan[i] = (dt, ds)
                 if ds > 1:
                     slab_elems = max(slab_elems, ds * M * cin)
-        self.slabs = torch.empty(max(slab_elems, 1), device=d)
+        self.slabs = torch.empty(max(slab_elems, 1), device=d)    # fwd / dgrad split-K (main stream)
+        self.wslabs = torch.empty(max(wslab_elems, 1), device=d)  # wgrad split-K (side stream)
         self.logits = torch.empty(B, self.nclass, device=d)
         self.dlogits = torch.empty(B, self.nclass, device=d)
         self.loss_b = torch.empty(B, device=d)
@@ -144,20 +169,24 @@ class CifarHIPExecutor:
         return 4 * blk + j  # conv_w, conv_b, bn_w, bn_b
 
     def _prep(self, x: torch.Tensor, s: int) -> int:
-        """Input channel pad + layer-1 weight pack + dgrad weight transposes (one launch)."""
+        """Input channel pad + layer-1 weight pack (one launch)."""
         B = x.shape[0]
         if B > self.cap:
             raise ValueError(f"batch {B} > executor capacity {self.cap}")
         if x.dim() != 4 or x.shape[-1] != self.cins_real[0] or x.dtype != BF16 or not x.is_contiguous():
             raise ValueError("CifarHIPExecutor expects contiguous NHWC bf16 input [B, H, W, 3]")
         h = self.hs[0]
-        idx = list(range(1, self.nb))
         self.C.prep_step(x.data_ptr(), self.x8.data_ptr(), B * h * h, self.cins_real[0], CIN_PAD,
                          self.p32[0].data_ptr(), self.w1p.data_ptr(), self.couts[0], KSIZE * KSIZE,
-                         self.cins_real[0], CIN_PAD, [self.p16[self._leaf(i, 0)].data_ptr() for i in idx],
-                         [self.wt[i].data_ptr() for i in idx], [self.couts[i] for i in idx],
-                         [self.cins[i] for i in idx], s)
+                         self.cins_real[0], CIN_PAD, [], [], [], [], s)
         return B
+
+    def _prep_transposes(self, s: int) -> None:
+        """Flipped/transposed bf16 weights of blocks 2.. for the dgrad (one launch)."""
+        idx = list(range(1, self.nb))
+        self.C.prep_step(0, 0, 0, self.cins_real[0], CIN_PAD, 0, 0, 0, KSIZE * KSIZE, self.cins_real[0], CIN_PAD,
+                         [self.p16[self._leaf(i, 0)].data_ptr() for i in idx], [self.wt[i].data_ptr() for i in idx],
+                         [self.couts[i] for i in idx], [self.cins[i] for i in idx], s)
 
     def _forward(self, B: int, s: int, train: bool):
         C = self.C
@@ -182,50 +211,71 @@ class CifarHIPExecutor:
         """One forward + backward on this node's batch; fp32 grads land in the
         flat gradient buffer.  Returns the mean loss (device tensor)."""
         C = self.C
-        s = stream_handle()
+        main, side = torch.cuda.current_stream(), self.side
+        s, ss = main.cuda_stream, side.cuda_stream
         if labels.dtype != torch.int64:
             raise ValueError("labels must be int64")
         B = self._prep(x, s)
         self._last_b = B
+        # fork: dgrad weight transposes overlap the forward
+        if self.fork_transposes:
+            side.wait_stream(main)
+            self._prep_transposes(ss)
+            wt_ready = torch.cuda.Event()
+            wt_ready.record(side)
+        else:
+            self._prep_transposes(s)
         self._forward(B, s, train=True)
         nfc = 4 * self.nb
         C.head_fwd_bwd(self.p[-1].data_ptr(), self.p32[nfc].data_ptr(), self.p32[nfc + 1].data_ptr(),
                        labels.data_ptr(), self.feat, B, self.nclass, self.logits.data_ptr(), self.dlogits.data_ptr(),
                        self.loss_b.data_ptr(), self.dP[-1].data_ptr(), s)
         C.head_wgrad(self.p[-1].data_ptr(), self.dlogits.data_ptr(), self.loss_b.data_ptr(), self.feat, B,
-                     self.nclass, self.g32[nfc].data_ptr(), self.g32[nfc + 1].data_ptr(), self.loss.data_ptr(), s)
+                     self.nclass, self.g32[nfc].data_ptr(), self.g32[nfc + 1].data_ptr(), self.loss.data_ptr(),
+                     self.flat.slot.data_ptr(), s)
         self._ready(nfc)
         self._ready(nfc + 1)
+        if self.fork_transposes:
+            main.wait_event(wt_ready)
+        ws = side if self.side_wgrad else main
+        wss = ws.cuda_stream
         for i in reversed(range(self.nb)):
             h, cin, cout = self.hs[i], self.cins[i], self.couts[i]
             M = B * h * h
             G = self.bwd_blocks[i]
+            dY = self.dYs[i]
             C.bn_relu_pool_bwd_reduce(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
                                       self.bwd_part[i].data_ptr(), B, h, h, cout, G, s)
             C.bn_bwd_finalize(self.bwd_part[i].data_ptr(), G, cout, M, self.p32[self._leaf(i, 2)].data_ptr(),
                               self.coef[i].data_ptr(), self.g32[self._leaf(i, 2)].data_ptr(),
                               self.g32[self._leaf(i, 3)].data_ptr(), self.acoef[i].data_ptr(), s)
             C.bn_relu_pool_bwd_apply(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
-                                     self.acoef[i].data_ptr(), self.dY.data_ptr(), B, h, h, cout, s)
+                                     self.acoef[i].data_ptr(), dY.data_ptr(), B, h, h, cout, s)
+            # (optional fork) weight gradient of block i on the side stream
+            if self.side_wgrad:
+                side.wait_stream(main)
             xin = self.x8 if i == 0 else self.p[i - 1]
             K = KSIZE * KSIZE * cin
             tile, splits, direct = self.wplan[i]
             gw = self.g32[self._leaf(i, 0)]
             if direct:
-                C.conv_wgrad(self.dY.data_ptr(), xin.data_ptr(), gw.data_ptr(), B, h, h, cin, cout, KSIZE, 1, K,
-                             tile, s)
+                C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), gw.data_ptr(), B, h, h, cin, cout, KSIZE, 1, K, tile, wss)
             else:
-                C.conv_wgrad(self.dY.data_ptr(), xin.data_ptr(), self.slabs.data_ptr(), B, h, h, cin, cout, KSIZE,
-                             splits, K, tile, s)
-                C.slab_reduce(self.slabs.data_ptr(), gw.data_ptr(), splits, cout, KSIZE * KSIZE, cin,
-                              self.cins_real[i], s)
-            # conv bias grad: exactly 0 under train-mode BN (grad buffer was zero-filled)
-            for j in range(4):
-                self._ready(self._leaf(i, j))
+                C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), self.wslabs.data_ptr(), B, h, h, cin, cout, KSIZE,
+                             splits, K, tile, wss)
+                C.slab_reduce(self.wslabs.data_ptr(), gw.data_ptr(), splits, cout, KSIZE * KSIZE, cin,
+                              self.cins_real[i], wss)
+            # conv bias grad: exactly 0 under train-mode BN (grad buffer was zero-filled).
+            # Bucket launches issued here are ordered after the wgrad stream.
+            with torch.cuda.stream(ws):
+                for j in range(4):
+                    self._ready(self._leaf(i, j))
             if i > 0:
                 dt, ds = self.dgrad_plan[i]
-                C.conv_fwd(self.dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), 0,
+                C.conv_fwd(dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), 0,
                            self.slabs.data_ptr(), B, h, h, cout, cin, KSIZE, dt, ds, s)
+        if self.side_wgrad:
+            main.wait_stream(side)  # join
         return self.loss[0]
 
     def last_logits(self) -> torch.Tensor:
