@@ -39,22 +39,23 @@ void slab_reduce(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps,
 void weight_flip_transpose(uintptr_t w, uintptr_t wt, int Cout, int Cin, int KS, uintptr_t stream);
 void pack_weight(uintptr_t w, uintptr_t wp, int Cout, int taps, int C, int Cp, uintptr_t stream);
 void pad_channels(uintptr_t x, uintptr_t xp, int64_t P, int C, int Cp, uintptr_t stream);
-void prep_step(uintptr_t x, uintptr_t xp, int64_t P, int C, int Cp, uintptr_t w1, uintptr_t w1p, int w1_cout,
-               int taps, int w1_c, int w1_cp, std::vector<uintptr_t> tw, std::vector<uintptr_t> twt,
+void prep_step(uintptr_t x, uintptr_t xp, int64_t P, int C, int Cp, int H, int W, int sp, uintptr_t w1, uintptr_t w1p,
+               int w1_cout, int taps, int w1_c, int w1_cp, std::vector<uintptr_t> tw, std::vector<uintptr_t> twt,
                std::vector<int> tcout, std::vector<int> tcin, uintptr_t stream);
 
 // bn_pool.hip -----------------------------------------------------------------
 void bn_finalize(uintptr_t partial, int T, int C, int64_t M, uintptr_t gamma, uintptr_t beta, uintptr_t bias,
                  uintptr_t rmean, uintptr_t rvar, float eps, float momentum, int mode, uintptr_t coef,
                  uintptr_t stream);
-void bn_relu_pool_fwd(uintptr_t y, uintptr_t coef, uintptr_t out, int B, int H, int W, int C, uintptr_t stream);
+void bn_relu_pool_fwd(uintptr_t y, uintptr_t coef, uintptr_t out, int B, int H, int W, int C, int opad,
+                      uintptr_t stream);
 int bn_bwd_blocks(int B, int H, int W, int C);
 void bn_relu_pool_bwd_reduce(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t partial, int B, int H, int W, int C,
                              int blocks, uintptr_t stream);
 void bn_bwd_finalize(uintptr_t partial, int T, int C, int64_t M, uintptr_t gamma, uintptr_t coef, uintptr_t dgamma,
                      uintptr_t dbeta, uintptr_t acoef, uintptr_t stream);
 void bn_relu_pool_bwd_apply(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t acoef, uintptr_t dy, int B, int H,
-                            int W, int C, uintptr_t stream);
+                            int W, int C, int opad, uintptr_t stream);
 
 // head.hip --------------------------------------------------------------------
 void head_fwd_bwd(uintptr_t h, uintptr_t w, uintptr_t bias, uintptr_t labels, int F, int B, int NC,

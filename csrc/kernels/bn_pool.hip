@@ -90,8 +90,12 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) bn_relu_pool_fwd_kernel(const bf16_t* __restrict__ y,
                                                                const float* __restrict__ coef,
-                                                               bf16_t* __restrict__ out, int B, int H, int W, int C) {
+                                                               bf16_t* __restrict__ out, int B, int H, int W, int C,
+                                                               int opad) {
+  // out: pooled [B][Ho+2 opad][Wo+2 opad][C], written in the interior (the
+  // zero border is the next convolution's spatial padding)
   const int C8 = C >> 3, Ho = H >> 1, Wo = W >> 1;
+  const int Hop = Ho + 2 * opad, Wop = Wo + 2 * opad;
   const int64_t total = (int64_t)B * Ho * Wo * C8;
   const float* scale = coef + 2 * C;
   const float* shift = coef + 3 * C;
@@ -126,7 +130,7 @@ __global__ void __launch_bounds__(256) bn_relu_pool_fwd_kernel(const bf16_t* __r
     unpack8(v3, f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) mx[k] = fmaxf(fmaxf(mx[k], fmaf(sc[k], f[k], sh[k])), 0.f);
-    *reinterpret_cast<uint4*>(out + pix * C + c0) = pack8(mx);
+    *reinterpret_cast<uint4*>(out + ((b * Hop + oh + opad) * Wop + ow + opad) * (int64_t)C + c0) = pack8(mx);
   }
 }
 
@@ -260,8 +264,11 @@ __global__ void __launch_bounds__(256) bn_relu_pool_bwd_apply_kernel(const bf16_
                                                                      const float* __restrict__ coef,
                                                                      const float* __restrict__ acoef,
                                                                      bf16_t* __restrict__ dy, int B, int H, int W,
-                                                                     int C) {
+                                                                     int C, int opad) {
+  // dy: [B][H+2 opad][W+2 opad][C], written in the interior (zero border =
+  // the dgrad convolution's spatial padding)
   const int C8 = C >> 3, Ho = H >> 1, Wo = W >> 1;
+  const int Hp = H + 2 * opad, Wp = W + 2 * opad;
   const int64_t total = (int64_t)B * Ho * Wo * C8;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int c8 = (int)(i % C8), c0 = c8 * 8;
@@ -281,8 +288,8 @@ __global__ void __launch_bounds__(256) bn_relu_pool_bwd_apply_kernel(const bf16_
     load8(kc, acoef + 2 * C + c0);
     float yv[4][8], dz[4][8];
     bwd_window(y, dP, cx, b, oh, ow, H, W, C, c0, yv, dz);
-    bf16_t* base = dy + (((b * H + 2 * oh) * W) + 2 * ow) * (int64_t)C + c0;
-    const int64_t offs[4] = {0, C, (int64_t)W * C, (int64_t)W * C + C};
+    bf16_t* base = dy + (((b * Hp + 2 * oh + opad) * Wp) + 2 * ow + opad) * (int64_t)C + c0;
+    const int64_t offs[4] = {0, C, (int64_t)Wp * C, (int64_t)Wp * C + C};
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       float o[8];
@@ -309,11 +316,12 @@ void bn_finalize(uintptr_t partial, int T, int C, int64_t M, uintptr_t gamma, ui
   DL_HIP_CHECK(hipGetLastError());
 }
 
-void bn_relu_pool_fwd(uintptr_t y, uintptr_t coef, uintptr_t out, int B, int H, int W, int C, uintptr_t stream) {
+void bn_relu_pool_fwd(uintptr_t y, uintptr_t coef, uintptr_t out, int B, int H, int W, int C, int opad,
+                      uintptr_t stream) {
   check_c(C);
   const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
   bn_relu_pool_fwd_kernel<<<stream_grid(total), 256, 0, as_stream(stream)>>>(
-      (const bf16_t*)y, (const float*)coef, (bf16_t*)out, B, H, W, C);
+      (const bf16_t*)y, (const float*)coef, (bf16_t*)out, B, H, W, C, opad);
   DL_HIP_CHECK(hipGetLastError());
 }
 
@@ -343,11 +351,11 @@ void bn_bwd_finalize(uintptr_t partial, int T, int C, int64_t M, uintptr_t gamma
 }
 
 void bn_relu_pool_bwd_apply(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t acoef, uintptr_t dy, int B, int H,
-                            int W, int C, uintptr_t stream) {
+                            int W, int C, int opad, uintptr_t stream) {
   check_c(C);
   const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
   bn_relu_pool_bwd_apply_kernel<<<stream_grid(total), 256, 0, as_stream(stream)>>>(
-      (const bf16_t*)y, (const bf16_t*)dP, (const float*)coef, (const float*)acoef, (bf16_t*)dy, B, H, W, C);
+      (const bf16_t*)y, (const bf16_t*)dP, (const float*)coef, (const float*)acoef, (bf16_t*)dy, B, H, W, C, opad);
   DL_HIP_CHECK(hipGetLastError());
 }
 

@@ -34,6 +34,7 @@ namespace dl {
 
 struct ConvGeom {
   int B, H, W;
+  int Hp, Wp;  // spatially zero-padded input dims (H + 2 pad, W + 2 pad)
   int Cin, Cout;
   int KS, pad;
   int logW, logHW, logC8;  // log2(W), log2(H*W), log2(Cin/8)
@@ -50,6 +51,7 @@ static int ilog2_exact(int v, const char* what) {
 static ConvGeom make_geom(int B, int H, int W, int Cin, int Cout, int KS) {
   ConvGeom g;
   g.B = B; g.H = H; g.W = W; g.Cin = Cin; g.Cout = Cout; g.KS = KS; g.pad = KS / 2;
+  g.Hp = H + 2 * g.pad; g.Wp = W + 2 * g.pad;
   if (KS % 2 != 1) throw std::runtime_error("conv: odd kernel size required");
   if (Cin < 8) throw std::runtime_error("conv: Cin must be >= 8 (pad the input channels)");
   g.logW = ilog2_exact(W, "W");
@@ -58,6 +60,8 @@ static ConvGeom make_geom(int B, int H, int W, int Cin, int Cout, int KS) {
   g.M = B * H * W;
   g.K = KS * KS * Cin;
   g.Kch = g.K / 8;
+  if ((int64_t)B * g.Hp * g.Wp * std::max(Cin, Cout) >= (1ll << 31) || (int64_t)Cout * g.K >= (1ll << 31))
+    throw std::runtime_error("conv: operand too large for 32-bit offsets");
   return g;
 }
 
@@ -159,6 +163,11 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
                                                        bf16_t* __restrict__ y, float* __restrict__ stats,
                                                        float* __restrict__ slab, const ConvGeom g, int splits,
                                                        int kt_per_split, unsigned long long* dbg) {
+  // x is the SPATIALLY ZERO-PADDED input [B][Hp][Wp][Cin]: every tap of every
+  // output pixel is in bounds, so an activation load is (per-lane pixel base)
+  // + (wave-uniform tap offset) with no bounds test.  Cout % BN == 0
+  // (host-checked); rows of an M tail load a valid pixel and are masked out
+  // of the stores and BN statistics.
   const unsigned long long t_start = dbg ? stamp() : 0ull;
   constexpr int BK = 64, CPR = 8, NW = WM * WN, NT = 64 * NW, PD = STAGES - 1;
   static_assert(STAGES >= 2 && STAGES <= 4, "2..4 stages");
@@ -173,13 +182,12 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
-  const int ntn = (g.Cout + BN - 1) / BN;
   const int ntm = (g.M + BM - 1) / BM;
   // Panel-major order: the workgroups of one XCD (consecutive ids after the
   // swizzle) share one (n-tile, K-split) weight panel and sweep the M tiles,
   // so the panel is fetched into that XCD's L2 once instead of every XCD
   // streaming the whole weight tensor from the Infinity Cache.
-  const int id = xcd_swizzle(blockIdx.x, ntm * ntn * splits);
+  const int id = xcd_swizzle(blockIdx.x, ntm * (g.Cout / BN) * splits);
   const int tm = id % ntm;
   const int panel = id / ntm;
   const int split = panel % splits, tn = panel / splits;
@@ -190,89 +198,79 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   const int kt_end = min(nkt_total, kt_beg + kt_per_split);
   const int nk = max(0, kt_end - kt_beg);
 
-  // per-lane source roles (fixed over the K loop); 32-bit element offsets
-  // (host checks that every operand has < 2^31 elements).
-  // A: instruction j of this wave covers rows 8*(wid*A_INS + j) .. +7
-  int a_ch[A_INS], a_oh[A_INS], a_ow[A_INS], a_pix[A_INS];
-  bool a_ok[A_INS];
+  // per-lane source roles (fixed over the K loop); 32-bit element offsets.
+  // A: instruction j of this wave covers rows 8*(wid*A_INS + j) .. +7;
+  //    a_base = padded pixel of tap (0,0) of output pixel m (+ chunk for TAPU)
+  int a_base[A_INS], a_ch[A_INS];
 #pragma unroll
   for (int j = 0; j < A_INS; ++j) {
     const int row = 8 * (wid * A_INS + j) + (lane >> 3);
     a_ch[j] = (lane & 7) ^ ((row >> 1) & 7);
-    const int m = m0 + row;
-    a_ok[j] = m < g.M;
-    const int mm = a_ok[j] ? m : 0;
-    const int rem = mm & (HW - 1);
-    a_oh[j] = rem >> g.logW;
-    a_ow[j] = rem & (Wd - 1);
-    a_pix[j] = mm * g.Cin + a_ch[j] * 8;  // element offset of (pixel m, tap (pad,pad), chunk)
-    if (!a_ok[j]) { a_oh[j] = -(1 << 20); }  // forces the bounds test to fail
+    const int m = min(m0 + row, g.M - 1);  // M tail: any valid pixel (masked in the epilogue)
+    const int b = m >> g.logHW, rem = m & (HW - 1);
+    const int pix = (b * g.Hp + (rem >> g.logW)) * g.Wp + (rem & (Wd - 1));
+    a_base[j] = pix * g.Cin + (TAPU ? a_ch[j] * 8 : 0);
   }
   int b_off[B_INS], b_k[B_INS];
-  bool b_ok[B_INS];
 #pragma unroll
   for (int j = 0; j < B_INS; ++j) {
     const int row = 8 * (wid * B_INS + j) + (lane >> 3);
     const int ch = (lane & 7) ^ ((row >> 1) & 7);
-    const int n = n0 + row;
-    b_ok[j] = n < g.Cout;
     b_k[j] = ch * 8;
-    b_off[j] = (b_ok[j] ? n : 0) * g.K + ch * 8;
+    b_off[j] = (n0 + row) * g.K + ch * 8;
   }
   const char* zsrc = reinterpret_cast<const char*>(g_zero16);
   const char* xb = reinterpret_cast<const char*>(x);
   const char* wb = reinterpret_cast<const char*>(w);
 
-  // One LDS-DMA load (q < A_INS: activation row block, else weight row block)
-  // of K step kt into ring slot `slot`.  The tap math of a TAPU step is
-  // wave-uniform (SALU), computed once per step by tap_of().
-  struct Tap { int dh, dw, off; };
-  auto tap_of = [&](int kt) -> Tap {
-    Tap t{0, 0, 0};
+  // Wave-uniform tap state of the next K step to load (TAPU: one step = 64
+  // channels of one tap): off = (kh*Wp + kw)*Cin + c0, advanced incrementally
+  // (no divisions in the loop).
+  struct Tap { int off, c0, kw; };
+  Tap tnext{0, 0, 0};
+  if constexpr (TAPU) {
+    const int k0 = kt_beg * BK;
+    const int kpos = k0 >> (g.logC8 + 3);
+    const int kh = kpos / g.KS, kw = kpos - kh * g.KS;
+    tnext.c0 = k0 & (g.Cin - 1);
+    tnext.kw = kw;
+    tnext.off = (kh * g.Wp + kw) * g.Cin + tnext.c0;
+  }
+  auto tap_advance = [&](Tap& t) {
     if constexpr (TAPU) {
-      const int k0 = kt * BK;
-      const int kpos = k0 >> (g.logC8 + 3);
-      const int kh = kpos / g.KS, kw = kpos - kh * g.KS;
-      t.dh = kh - g.pad;
-      t.dw = kw - g.pad;
-      t.off = (t.dh * Wd + t.dw) * g.Cin + (k0 & (g.Cin - 1));
+      t.off += BK;
+      t.c0 += BK;
+      if (t.c0 == g.Cin) {
+        t.c0 = 0;
+        if (++t.kw == g.KS) { t.kw = 0; t.off += (g.Wp - g.KS) * g.Cin; }
+      }
     }
-    return t;
   };
+  // One LDS-DMA load (q < A_INS: activation row block, else weight row block)
+  // of K step kt into ring slot `slot`.
   auto issue_one = [&](int q, int kt, int slot, const Tap& t) {
     char* sA = smem + slot * STAGE_BYTES;
     char* sB = sA + A_BYTES;
     if (q < A_INS) {
       const int j = q;
       if constexpr (TAPU) {
-        const int ih = a_oh[j] + t.dh, iw = a_ow[j] + t.dw;
-        const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)Wd;
-        const uint64_t pa = (uint64_t)xb + (uint64_t)(2u * (unsigned)(a_pix[j] + t.off));
-        glds16((const void*)(ok ? pa : (uint64_t)zsrc), sA + (wid * A_INS + j) * 1024);
+        glds16(xb + 2 * (a_base[j] + t.off), sA + (wid * A_INS + j) * 1024);
       } else {
+        // first layer (Cin < 64): a 64-wide K step spans several taps, per lane
         const int kc = kt * CPR + a_ch[j];
         const int kpos = kc >> g.logC8;
         const int c0 = (kc & (C8 - 1)) << 3;
         const int kh = kpos / g.KS, kw = kpos - kh * g.KS;
-        const int dh = kh - g.pad, dw = kw - g.pad;
-        const int ih = a_oh[j] + dh, iw = a_ow[j] + dw;
-        const bool ok = kc < g.Kch && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)Wd;
-        const char* src = ok ? xb + 2 * (a_pix[j] - a_ch[j] * 8 + (dh * Wd + dw) * g.Cin + c0) : zsrc;
+        const char* src = kc < g.Kch ? xb + 2 * (a_base[j] + (kh * g.Wp + kw) * g.Cin + c0) : zsrc;
         glds16(src, sA + (wid * A_INS + j) * 1024);
       }
     } else {
       const int j = q - A_INS;
       const int kadd = kt * BK;
-      bool ok = b_ok[j];
-      if constexpr (!TAPU) ok = ok && (kadd + b_k[j]) < g.K;  // K tail (first layer only)
-      const uint64_t pb = (uint64_t)wb + (uint64_t)(2u * (unsigned)(b_off[j] + kadd));
-      glds16((const void*)(ok ? pb : (uint64_t)zsrc), sB + (wid * B_INS + j) * 1024);
+      const char* src = wb + 2 * (b_off[j] + kadd);
+      if constexpr (!TAPU) src = (kadd + b_k[j]) < g.K ? src : zsrc;  // K tail (first layer only)
+      glds16(src, sB + (wid * B_INS + j) * 1024);
     }
-  };
-  auto issue = [&](int kt, int slot) {
-    const Tap t = tap_of(kt);
-#pragma unroll
-    for (int q = 0; q < LPS; ++q) issue_one(q, kt, slot, t);
   };
 
   f32x4 acc[FM][FN];
@@ -284,18 +282,23 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   const unsigned long long t_setup = dbg ? stamp() : 0ull;
 #pragma unroll
   for (int p = 0; p < PD; ++p)
-    if (p < nk) issue(kt_beg + p, p);
+    if (p < nk) {
+#pragma unroll
+      for (int q = 0; q < LPS; ++q) issue_one(q, kt_beg + p, p, tnext);
+      tap_advance(tnext);
+    }
   // MFMAs per K step and the spacing of the next stage's DMA issues between them
   constexpr int NMF = (BK / 32) * FM * FN;
   constexpr int IL = NMF / LPS > 0 ? NMF / LPS : 1;
+  int slot_c = 0, slot_n = PD % STAGES;
   for (int i = 0; i < nk; ++i) {
-    wait_stages<LPS>(min(PD - 1, nk - 1 - i));
+    if (i + PD - 1 < nk) wait_vmcnt<(PD - 1) * LPS>();  // steady state: stage i landed
+    else wait_stages<LPS>(nk - 1 - i);                  // drain
     block_sync_lds();  // stage i landed for every wave; slot (i+PD)%STAGES no longer read
     const bool pf = i + PD < nk;
-    const int kt_n = kt_beg + i + PD, slot_n = (i + PD) % STAGES;
-    const Tap tn = tap_of(kt_n);
-    const uint4* As = reinterpret_cast<const uint4*>(smem + (i % STAGES) * STAGE_BYTES);
-    const uint4* Bs = reinterpret_cast<const uint4*>(smem + (i % STAGES) * STAGE_BYTES + A_BYTES);
+    const int kt_n = kt_beg + i + PD;
+    const uint4* As = reinterpret_cast<const uint4*>(smem + slot_c * STAGE_BYTES);
+    const uint4* Bs = reinterpret_cast<const uint4*>(smem + slot_c * STAGE_BYTES + A_BYTES);
     bf16x8 af[BK / 32][FM], bfr[BK / 32][FN];
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
@@ -318,10 +321,13 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
           acc[a][b] = mfma16(af[kk][a], bfr[kk][b], acc[a][b]);
           const int idx = (kk * FM + a) * FN + b;
           if (idx % IL == IL - 1 && idx / IL < LPS) {
-            if (pf) issue_one(idx / IL, kt_n, slot_n, tn);
+            if (pf) issue_one(idx / IL, kt_n, slot_n, tnext);
             __builtin_amdgcn_sched_barrier(0);
           }
         }
+    if (pf) tap_advance(tnext);
+    slot_c = slot_c + 1 == STAGES ? 0 : slot_c + 1;
+    slot_n = slot_n + 1 == STAGES ? 0 : slot_n + 1;
   }
 
   const unsigned long long t_loop = dbg ? stamp() : 0ull;
@@ -362,7 +368,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
           const bf16_t hv = f32_to_bf16(acc[a][b][r]);
           if (m < g.M && n < g.Cout) y[(int64_t)m * g.Cout + n] = hv;
           if constexpr (STATS) {
-            const float v = bf16_to_f32(hv);  // statistics of exactly what is stored (0 for m >= M)
+            const float v = m < g.M ? bf16_to_f32(hv) : 0.f;  // statistics of exactly what is stored
             s1[b] += v;
             s2[b] += v * v;
           }
@@ -464,6 +470,12 @@ template <int BM, int BN, int STAGES, int WM = 2, int WN = 2>
 __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                          float* __restrict__ out, const ConvGeom g, int m_per_split,
                                                          int ldo) {
+  // dy and x are both spatially zero-padded [B][Hp][Wp][C] (dy: interior at
+  // (pad, pad)).  A 64-row M step starts at a multiple of 64 output pixels;
+  // with W | 64 and (H*W | 64 or 64 | H*W) the padded position of row r of the
+  // step is U(step) + L(r): a wave-uniform part plus a per-lane constant, so
+  // a load is one add, no bounds test (m_per_split % 64 == 0, Cout % BM == 0);
+  // only a partial last step (M % 64 != 0) tests rows (wave-uniform branch).
   constexpr int BK = 64, NW = WM * WN, PD = STAGES - 1;
   static_assert(STAGES >= 2 && STAGES <= 4, "2..4 stages");
   constexpr int ACPR = BM / 8, BCPR = BN / 8;  // chunks per LDS row (row = one m)
@@ -479,31 +491,29 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
-  const int ntm = (g.Cout + BM - 1) / BM, ntn = (g.Kch * 8 + BN - 1) / BN;
-  const int splits = gridDim.y;
+  const int ntm = g.Cout / BM, ntn = (g.Kch * 8 + BN - 1) / BN;
   const int tile = xcd_swizzle(blockIdx.x, ntm * ntn);
   const int tm = tile % ntm, tn = tile / ntm;
   const int co0 = tm * BM, k0 = tn * BN;
   const int split = blockIdx.y;
-  (void)splits;
   const int mbeg = split * m_per_split;
   const int mend = min(g.M, mbeg + m_per_split);
   const int HW = 1 << g.logHW, Wd = g.W, C8 = 1 << g.logC8;
+  const int HpWp = g.Hp * g.Wp;
+  // padded pixel offset of row r inside a 64-aligned step
+  auto lane_pix = [&](int r) { return (r >> g.logHW) * HpWp + ((r & (HW - 1)) >> g.logW) * g.Wp + (r & (Wd - 1)); };
 
   // A (dy) lanes: row = A_RPI*(wid*A_INS + j) + lane/ACPR, chunk fixed
-  int a_row[A_INS], a_off[A_INS];
-  bool a_cok[A_INS];
+  int a_off[A_INS], a_row[A_INS];
 #pragma unroll
   for (int j = 0; j < A_INS; ++j) {
     const int row = A_RPI * (wid * A_INS + j) + lane / ACPR;
     a_row[j] = row;
     const int ch = swz_tr<ACPR>(row, lane % ACPR) - row * ACPR;  // logical chunk (involution)
-    const int co = co0 + ch * 8;
-    a_cok[j] = co < g.Cout;
-    a_off[j] = (mbeg + row) * g.Cout + (a_cok[j] ? co : 0);
+    a_off[j] = (lane_pix(row) + g.pad * g.Wp + g.pad) * g.Cout + co0 + ch * 8;
   }
-  // B (im2col) lanes: chunk -> fixed tap (dh, dw, c0)
-  int b_row[B_INS], b_dh[B_INS], b_dw[B_INS], b_c0[B_INS], b_dhw[B_INS];
+  // B (im2col of x) lanes: chunk -> fixed tap (kh, kw, c0)
+  int b_off[B_INS], b_row[B_INS];
   bool b_kok[B_INS];
 #pragma unroll
   for (int j = 0; j < B_INS; ++j) {
@@ -513,36 +523,38 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
     const int kc = k0 / 8 + ch;
     b_kok[j] = kc < g.Kch;
     const int kpos = kc >> g.logC8;
-    b_c0[j] = (kc & (C8 - 1)) << 3;
-    const int kh = kpos / g.KS;
-    b_dh[j] = kh - g.pad;
-    b_dw[j] = kpos - kh * g.KS - g.pad;
-    b_dhw[j] = b_dh[j] * Wd + b_dw[j];
+    const int kh = kpos / g.KS, kw = kpos - kh * g.KS;
+    b_off[j] = (lane_pix(row) + kh * g.Wp + kw) * g.Cin + ((kc & (C8 - 1)) << 3);
   }
-  const uint64_t zsrc = (uint64_t)g_zero16;
-  const uint64_t dyb = (uint64_t)dy, xb = (uint64_t)x;
-  const int mcount = mend - mbeg;
+  const char* zsrc = reinterpret_cast<const char*>(g_zero16);
+  const char* dyb = reinterpret_cast<const char*>(dy);
+  const char* xb = reinterpret_cast<const char*>(x);
 
   auto issue = [&](int kt, int slot) {
     char* sA = smem + slot * STAGE_BYTES;
     char* sB = sA + A_BYTES;
-    const int r0 = kt * BK;
-    const int aadd = r0 * g.Cout;
+    const int ms = mbeg + kt * BK;  // 64-aligned first row of the step
+    const int u = (ms >> g.logHW) * HpWp + ((ms & (HW - 1)) >> g.logW) * g.Wp;  // wave-uniform
+    const int left = mend - ms;                                                  // rows left (uniform)
+    if (left >= BK) {
 #pragma unroll
-    for (int j = 0; j < A_INS; ++j) {
-      const bool ok = (r0 + a_row[j]) < mcount && a_cok[j];
-      const uint64_t pa = dyb + (uint64_t)(2u * (unsigned)(a_off[j] + aadd));
-      glds16((const void*)(ok ? pa : zsrc), sA + (wid * A_INS + j) * 1024);
-    }
+      for (int j = 0; j < A_INS; ++j) glds16(dyb + 2 * (u * g.Cout + a_off[j]), sA + (wid * A_INS + j) * 1024);
 #pragma unroll
-    for (int j = 0; j < B_INS; ++j) {
-      const int m = mbeg + r0 + b_row[j];
-      const int rem = m & (HW - 1);
-      const int ih = (rem >> g.logW) + b_dh[j], iw = (rem & (Wd - 1)) + b_dw[j];
-      const bool ok = (r0 + b_row[j]) < mcount && b_kok[j] && (unsigned)ih < (unsigned)g.H &&
-                      (unsigned)iw < (unsigned)Wd;
-      const uint64_t pb = xb + (uint64_t)(2u * (unsigned)((m + b_dhw[j]) * g.Cin + b_c0[j]));
-      glds16((const void*)(ok ? pb : zsrc), sB + (wid * B_INS + j) * 1024);
+      for (int j = 0; j < B_INS; ++j) {
+        const char* src = xb + 2 * (u * g.Cin + b_off[j]);
+        glds16(b_kok[j] ? src : zsrc, sB + (wid * B_INS + j) * 1024);
+      }
+    } else {  // partial last step: rows past the end read zeros
+#pragma unroll
+      for (int j = 0; j < A_INS; ++j) {
+        const char* src = dyb + 2 * (u * g.Cout + a_off[j]);
+        glds16(a_row[j] < left ? src : zsrc, sA + (wid * A_INS + j) * 1024);
+      }
+#pragma unroll
+      for (int j = 0; j < B_INS; ++j) {
+        const char* src = xb + 2 * (u * g.Cin + b_off[j]);
+        glds16(b_kok[j] && b_row[j] < left ? src : zsrc, sB + (wid * B_INS + j) * 1024);
+      }
     }
   };
 
@@ -557,11 +569,13 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
 #pragma unroll
   for (int p = 0; p < PD; ++p)
     if (p < nk) issue(p, p);
+  int slot_c = 0, slot_n = PD % STAGES;
   for (int i = 0; i < nk; ++i) {
-    wait_stages<LPS>(min(PD - 1, nk - 1 - i));
+    if (i + PD - 1 < nk) wait_vmcnt<(PD - 1) * LPS>();
+    else wait_stages<LPS>(nk - 1 - i);
     block_sync_lds();
-    if (i + PD < nk) issue(i + PD, (i + PD) % STAGES);
-    const char* As = smem + (i % STAGES) * STAGE_BYTES;
+    if (i + PD < nk) issue(i + PD, slot_n);
+    const char* As = smem + slot_c * STAGE_BYTES;
     const char* Bs = As + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
@@ -588,6 +602,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
 #pragma unroll
         for (int b = 0; b < FN; ++b) acc[a][b] = mfma16(af[a], bfr[b], acc[a][b]);
     }
+    slot_c = slot_c + 1 == STAGES ? 0 : slot_c + 1;
+    slot_n = slot_n + 1 == STAGES ? 0 : slot_n + 1;
   }
 
   float* o = out + (int64_t)split * g.Cout * ldo;
@@ -679,7 +695,8 @@ __global__ void __launch_bounds__(256) pad_channels_kernel(const bf16_t* __restr
 // one tap through LDS.
 // --------------------------------------------------------------------------
 struct PrepArgs {
-  const bf16_t* x; bf16_t* xp; int64_t P; int C, Cp;            // input pad
+  const bf16_t* x; bf16_t* xp; int64_t P; int C, Cp;            // input pad (channels + spatial)
+  int H, W, sp;                                                 // image dims, spatial zero pad
   const float* w1; bf16_t* w1p; int w1_cout, taps, w1_c, w1_cp;  // layer-1 pack
   int nt;                                                        // transposes
   const bf16_t* tw[4]; bf16_t* twt[4]; int tcout[4], tcin[4];
@@ -690,13 +707,17 @@ __global__ void __launch_bounds__(256) prep_step_kernel(const PrepArgs a) {
   __shared__ bf16_t t[32][33];
   int blk = blockIdx.x;
   if (blk < a.nb_pad) {
+    const int HW = a.H * a.W, Hp = a.H + 2 * a.sp, Wp = a.W + 2 * a.sp;
     for (int64_t p = (int64_t)blk * 256 + threadIdx.x; p < a.P; p += (int64_t)a.nb_pad * 256) {
       bf16_t v[16];
 #pragma unroll
       for (int c = 0; c < 16; ++c) v[c] = 0;
       for (int c = 0; c < a.C; ++c) v[c] = a.x[p * a.C + c];
+      const int64_t b = p / HW;
+      const int r = (int)(p - b * HW), h = r / a.W, w = r - h * a.W;
+      const int64_t q = (b * Hp + h + a.sp) * Wp + w + a.sp;  // interior of the zero-bordered buffer
       for (int c = 0; c < a.Cp; c += 8)
-        *reinterpret_cast<uint4*>(a.xp + p * a.Cp + c) = *reinterpret_cast<const uint4*>(v + c);
+        *reinterpret_cast<uint4*>(a.xp + q * a.Cp + c) = *reinterpret_cast<const uint4*>(v + c);
     }
     return;
   }
@@ -732,12 +753,14 @@ __global__ void __launch_bounds__(256) prep_step_kernel(const PrepArgs a) {
   }
 }
 
-void prep_step(uintptr_t x, uintptr_t xp, int64_t P, int C, int Cp, uintptr_t w1, uintptr_t w1p, int w1_cout,
-               int taps, int w1_c, int w1_cp, std::vector<uintptr_t> tw, std::vector<uintptr_t> twt,
+void prep_step(uintptr_t x, uintptr_t xp, int64_t P, int C, int Cp, int H, int W, int sp, uintptr_t w1, uintptr_t w1p,
+               int w1_cout, int taps, int w1_c, int w1_cp, std::vector<uintptr_t> tw, std::vector<uintptr_t> twt,
                std::vector<int> tcout, std::vector<int> tcin, uintptr_t stream) {
   PrepArgs a{};
   if (C > 16 || Cp > 16 || Cp % 8 != 0) throw std::runtime_error("prep_step: input channels must pad to 8 or 16");
+  if (P > 0 && (H <= 0 || W <= 0 || P % ((int64_t)H * W) != 0)) throw std::runtime_error("prep_step: P != B*H*W");
   a.x = (const bf16_t*)x; a.xp = (bf16_t*)xp; a.P = P; a.C = C; a.Cp = Cp;
+  a.H = H; a.W = W; a.sp = sp;
   a.w1 = (const float*)w1; a.w1p = (bf16_t*)w1p; a.w1_cout = w1_cout; a.taps = taps; a.w1_c = w1_c; a.w1_cp = w1_cp;
   a.nt = (int)tw.size();
   if (a.nt > 4 || twt.size() != tw.size() || tcout.size() != tw.size() || tcin.size() != tw.size())
@@ -828,8 +851,6 @@ void set_conv_stages(int fwd, int wgrad) {
 template <int BM, int BN>
 static void launch_fwd(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
                        uintptr_t slab, int splits, hipStream_t s) {
-  if ((int64_t)g.M * g.Cin >= (1ll << 31) || (int64_t)g.Cout * g.K >= (1ll << 31))
-    throw std::runtime_error("conv_fwd: operand too large for 32-bit offsets");
   const int st = (BM * 64 * 2 + BN * 64 * 2) * 4 > 160 * 1024 ? std::min(g_fwd_stages, 3) : g_fwd_stages;
   if (g.Cin >= 64) {
     if (st == 2) launch_fwd_t<BM, BN, true, 2>(g, x, w, y, stats, slab, splits, s);
@@ -850,6 +871,8 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
   if (splits < 1) splits = 1;
   if (splits > 1 && !slab) throw std::runtime_error("conv_fwd: split-K needs a slab");
   if (Cout % 8 != 0) throw std::runtime_error("conv_fwd: Cout % 8 != 0");
+  if (tile < 0 || tile > 2) throw std::runtime_error("conv_fwd: bad tile id");
+  if (Cout % fwd_bn(tile) != 0) throw std::runtime_error("conv_fwd: Cout must be a multiple of the N tile");
   if (tile == 0) launch_fwd<128, 128>(g, x, w, y, stats, slab, splits, s);
   else if (tile == 1) launch_fwd<64, 64>(g, x, w, y, stats, slab, splits, s);
   else if (tile == 2) launch_fwd<128, 64>(g, x, w, y, stats, slab, splits, s);
@@ -873,11 +896,13 @@ void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, i
                 int ldo, int tile, uintptr_t stream) {
   ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
   if (ldo < g.K) throw std::runtime_error("conv_wgrad: ldo < K");
-  if ((int64_t)g.M * g.Cin >= (1ll << 31) || (int64_t)g.M * g.Cout >= (1ll << 31))
-    throw std::runtime_error("conv_wgrad: operand too large for 32-bit offsets");
   if (Cout % 8 != 0) throw std::runtime_error("conv_wgrad: Cout % 8 != 0");
+  const int bm = tile == 1 ? 64 : 128;
+  if (Cout % bm != 0) throw std::runtime_error("conv_wgrad: Cout must be a multiple of the Cout tile");
+  if (W > 64) throw std::runtime_error("conv_wgrad: needs W <= 64");
   if (splits < 1) splits = 1;
   int mps = (g.M + splits - 1) / splits;
+  mps = (mps + 63) / 64 * 64;  // 64-row aligned M steps (padded-layout addressing)
   hipStream_t s = as_stream(stream);
 #define DL_WG(BM_, BN_, ST_, WM_, WN_)                                                                     \
   do {                                                                                                     \

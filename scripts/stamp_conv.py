@@ -12,7 +12,7 @@ C = _native.native()
 ab = int(sys.argv[1]) if len(sys.argv) > 1 else 0
 B, H, cin, cout = 128, 16, 64, 128
 dev = torch.device("cuda")
-x = torch.randn(B, H, H, cin, device=dev).to(torch.bfloat16)
+x = torch.nn.functional.pad(torch.randn(B, H, H, cin, device=dev), (0, 0, 2, 2, 2, 2)).to(torch.bfloat16)  # zero border
 w = (torch.randn(cout, 5, 5, cin, device=dev) * 0.05).to(torch.bfloat16)
 y = torch.empty(B, H, H, cout, dtype=torch.bfloat16, device=dev)
 stats = torch.empty(4096 * 2 * cout, device=dev)

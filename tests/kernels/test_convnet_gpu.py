@@ -25,8 +25,15 @@ def _rel(a, b):
     return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
 
 
-# (B, H, Cin, Cout): the four reference layers (batch 8 / 32) + odd sizes
-CONV_SHAPES = [(8, 32, 8, 64), (8, 16, 64, 128), (8, 8, 128, 256), (32, 4, 256, 512), (3, 8, 16, 40), (5, 4, 32, 24)]
+def _pad(t, p=2):
+    """NHWC -> zero-bordered [B, H+2p, W+2p, C] (the kernels' convolution-input layout)."""
+    return F.pad(t, (0, 0, p, p, p, p)).contiguous()
+
+
+# (B, H, Cin, Cout): the four reference layers (batch 8 / 32) + odd batches (M tails)
+CONV_SHAPES = [(8, 32, 8, 64), (8, 16, 64, 128), (8, 8, 128, 256), (32, 4, 256, 512), (3, 8, 16, 64), (5, 4, 32, 128),
+               (3, 4, 256, 128)]
+_TILE_BN = {0: 128, 1: 64, 2: 64}
 
 
 @pytest.mark.parametrize("shape", CONV_SHAPES)
@@ -36,6 +43,8 @@ def test_conv_fwd_and_stats(C, shape, tile, splits):
     B, H, cin, cout = shape
     if splits > 1 and 256 % (cout // 8) != 0:
         pytest.skip("split-K combine needs Cout/8 | 256")
+    if cout % _TILE_BN[tile] != 0:
+        pytest.skip("Cout must be a multiple of the N tile")
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(B * H + cin)
     x = torch.randn(B, H, H, cin, device=dev, generator=g).to(torch.bfloat16)
@@ -44,7 +53,8 @@ def test_conv_fwd_and_stats(C, shape, tile, splits):
     rows = C.conv_fwd_stat_rows(B, H, H, cin, cout, 5, tile, splits)
     stats = torch.full((rows, 2, cout), float("nan"), device=dev)
     slab = torch.empty(splits * B * H * H * cout, device=dev)
-    T = C.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), stats.data_ptr(), slab.data_ptr(), B, H, H, cin, cout,
+    xp = _pad(x)
+    T = C.conv_fwd(xp.data_ptr(), w.data_ptr(), y.data_ptr(), stats.data_ptr(), slab.data_ptr(), B, H, H, cin, cout,
                    5, tile, splits, _s())
     assert T == rows
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=2).permute(0, 2, 3, 1)
@@ -74,21 +84,26 @@ def test_conv_dgrad_wgrad(C, shape):
     C.weight_flip_transpose(w.data_ptr(), wt.data_ptr(), cout, cin, 5, _s())
     torch.cuda.synchronize()
     assert torch.equal(wt, w.permute(3, 1, 2, 0).flip(1, 2).contiguous())
+    dyp = _pad(dy)
     if cout & (cout - 1) == 0:  # dgrad input channels (= Cout) must be a power of two
         for tile, splits in ((1, 1), (0, 2), (2, 4)):
             dx = torch.empty(B, H, H, cin, dtype=torch.bfloat16, device=dev)
             slab = torch.empty(splits * B * H * H * cin, device=dev)
-            if splits > 1 and 256 % (cin // 8) != 0:
+            if (splits > 1 and 256 % (cin // 8) != 0) or cin % _TILE_BN[tile] != 0:
                 continue
-            C.conv_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, slab.data_ptr(), B, H, H, cout, cin, 5, tile,
+            C.conv_fwd(dyp.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, slab.data_ptr(), B, H, H, cout, cin, 5, tile,
                        splits, _s())
             torch.cuda.synchronize()
             assert _rel(dx, dx_ref) < 8e-3, (tile, splits)
     K = 25 * cin
-    for tile in (0, 1):
+    xp = _pad(x)
+    for tile in (0, 1, 2):
+        if cout % (64 if tile == 1 else 128) != 0:
+            continue
         for splits in (1, 3):
-            slabs = torch.zeros(splits, cout, K, device=dev)
-            C.conv_wgrad(dy.data_ptr(), x.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, splits, K, tile, _s())
+            slabs = torch.full((splits, cout, K), float("nan"), device=dev)
+            C.conv_wgrad(dyp.data_ptr(), xp.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, splits, K, tile,
+                         _s())
             dw = torch.empty(cout, 5, 5, cin, device=dev)
             C.slab_reduce(slabs.data_ptr(), dw.data_ptr(), splits, cout, 25, cin, cin, _s())
             torch.cuda.synchronize()
@@ -100,16 +115,18 @@ def test_prep_step(C):
     dev = torch.device("cuda")
     B = 3
     x3 = torch.randn(B, 32, 32, 3, device=dev).to(torch.bfloat16)
-    x8 = torch.full((B, 32, 32, 8), 7.0, dtype=torch.bfloat16, device=dev)
+    x8 = torch.full((B, 36, 36, 8), 7.0, dtype=torch.bfloat16, device=dev)
     w1 = torch.randn(64, 5, 5, 3, device=dev)
     w1p = torch.full((64, 5, 5, 8), 7.0, dtype=torch.bfloat16, device=dev)
     ws = [torch.randn(co, 5, 5, ci, device=dev).to(torch.bfloat16) for ci, co in ((64, 128), (128, 256), (256, 512))]
     wts = [torch.empty(w.shape[3], 5, 5, w.shape[0], dtype=torch.bfloat16, device=dev) for w in ws]
-    C.prep_step(x3.data_ptr(), x8.data_ptr(), B * 1024, 3, 8, w1.data_ptr(), w1p.data_ptr(), 64, 25, 3, 8,
+    C.prep_step(x3.data_ptr(), x8.data_ptr(), B * 1024, 3, 8, 32, 32, 2, w1.data_ptr(), w1p.data_ptr(), 64, 25, 3, 8,
                 [w.data_ptr() for w in ws], [t.data_ptr() for t in wts], [w.shape[0] for w in ws],
                 [w.shape[3] for w in ws], _s())
     torch.cuda.synchronize()
-    assert torch.equal(x8[..., :3], x3) and not x8[..., 3:].any()
+    inner = x8[:, 2:34, 2:34]
+    assert torch.equal(inner[..., :3], x3) and not inner[..., 3:].any()
+    assert (x8[:, :2] == 7).all() and (x8[:, 34:] == 7).all()  # the border is never written
     assert torch.equal(w1p[..., :3], w1.to(torch.bfloat16)) and not w1p[..., 3:].any()
     for w, t in zip(ws, wts):
         assert torch.equal(t, w.permute(3, 1, 2, 0).flip(1, 2).contiguous())
@@ -130,7 +147,8 @@ def test_padded_input_layer(C):
     assert torch.equal(w8[..., :3], w3.to(torch.bfloat16)) and not w8[..., 3:].any()
     dy = torch.randn(B, H, H, 64, device=dev).to(torch.bfloat16)
     slabs = torch.zeros(4, 64, 200, device=dev)
-    C.conv_wgrad(dy.data_ptr(), x8.data_ptr(), slabs.data_ptr(), B, H, H, 8, 64, 5, 4, 200, 1, _s())
+    dyp, x8p = _pad(dy), _pad(x8)
+    C.conv_wgrad(dyp.data_ptr(), x8p.data_ptr(), slabs.data_ptr(), B, H, H, 8, 64, 5, 4, 200, 1, _s())
     dw = torch.empty(64, 5, 5, 3, device=dev)
     C.slab_reduce(slabs.data_ptr(), dw.data_ptr(), 4, 64, 25, 8, 3, _s())
     xr = x3.float().permute(0, 3, 1, 2)
@@ -158,7 +176,9 @@ def test_bn_relu_pool_fwd_bwd(C, shape):
     C.bn_finalize(partial.data_ptr(), 1, Cc, M, gamma.data_ptr(), beta.data_ptr(), bias.data_ptr(), rm.data_ptr(),
                   rv.data_ptr(), 1e-3, 0.1, 0, coef.data_ptr(), _s())
     out = torch.empty(B, H // 2, H // 2, Cc, dtype=torch.bfloat16, device=dev)
-    C.bn_relu_pool_fwd(y.data_ptr(), coef.data_ptr(), out.data_ptr(), B, H, H, Cc, _s())
+    C.bn_relu_pool_fwd(y.data_ptr(), coef.data_ptr(), out.data_ptr(), B, H, H, Cc, 0, _s())
+    outp = torch.full((B, H // 2 + 4, H // 2 + 4, Cc), 3.0, dtype=torch.bfloat16, device=dev)
+    C.bn_relu_pool_fwd(y.data_ptr(), coef.data_ptr(), outp.data_ptr(), B, H, H, Cc, 2, _s())
     # reference (fp32 from the same bf16 y)
     yr = y.float().permute(0, 3, 1, 2).requires_grad_(True)
     rm_ref, rv_ref = torch.zeros(Cc, device=dev), torch.ones(Cc, device=dev)
@@ -168,6 +188,7 @@ def test_bn_relu_pool_fwd_bwd(C, shape):
     o = F.max_pool2d(F.relu(z), 2, 2)
     torch.cuda.synchronize()
     assert _rel(out, o.permute(0, 2, 3, 1)) < 5e-3
+    assert torch.equal(outp[:, 2:-2, 2:-2], out) and (outp[:, :2] == 3).all() and (outp[:, :, -2:] == 3).all()
     torch.testing.assert_close(rm, rm_ref + 0.1 * bias, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(rv, rv_ref, rtol=1e-3, atol=1e-4)
     # backward
@@ -181,9 +202,10 @@ def test_bn_relu_pool_fwd_bwd(C, shape):
     acoef = torch.empty(3, Cc, device=dev)
     C.bn_bwd_finalize(part.data_ptr(), G, Cc, M, gamma.data_ptr(), coef.data_ptr(), dg.data_ptr(), db.data_ptr(),
                       acoef.data_ptr(), _s())
-    dy = torch.empty_like(y)
-    C.bn_relu_pool_bwd_apply(y.data_ptr(), dP.data_ptr(), coef.data_ptr(), acoef.data_ptr(), dy.data_ptr(), B, H, H,
-                             Cc, _s())
+    dyp = torch.zeros(B, H + 4, H + 4, Cc, dtype=torch.bfloat16, device=dev)
+    C.bn_relu_pool_bwd_apply(y.data_ptr(), dP.data_ptr(), coef.data_ptr(), acoef.data_ptr(), dyp.data_ptr(), B, H, H,
+                             Cc, 2, _s())
+    dy = dyp[:, 2:-2, 2:-2]
     torch.cuda.synchronize()
     torch.testing.assert_close(db, br.grad, rtol=1e-3, atol=1e-3)
     torch.testing.assert_close(dg, gr.grad, rtol=1e-3, atol=1e-3)

@@ -44,6 +44,7 @@ from .cifar_convnet import BN_EPS, BN_MOMENTUM, KSIZE, CifarConvNet
 
 BF16 = torch.bfloat16
 CIN_PAD = 8  # the 3-channel input layer is zero-padded to 8 channels (one 16-B vector per tap)
+SPAD = KSIZE // 2  # spatial zero border of every convolution input (written once, never touched)
 
 # tile ids of conv_fwd: 0 = 128x128, 1 = 64x64, 2 = 128x64 (BK = 64) ; conv_wgrad: 0 = 128x64, 1 = 64x64
 _FWD_TILES = {0: (128, 128), 1: (64, 64), 2: (128, 64)}
@@ -116,15 +117,19 @@ class CifarHIPExecutor:
         d, C = self.dev, self.C
         e = lambda *s, dt=BF16: torch.empty(*s, dtype=dt, device=d)  # noqa: E731
         H0 = self.hs[0]
-        self.x8 = torch.zeros(B, H0, H0, CIN_PAD, dtype=BF16, device=d)
+        # convolution inputs live in zero-bordered buffers [B, H+4, W+4, C]: the
+        # producers write the interior, the kernels never bounds-test a tap
+        P2 = 2 * SPAD
+        self.x8 = torch.zeros(B, H0 + P2, H0 + P2, CIN_PAD, dtype=BF16, device=d)
         self.w1p = torch.zeros(self.couts[0], KSIZE * KSIZE * CIN_PAD, dtype=BF16, device=d)
         self.wt = [None] + [e(self.cins[i], KSIZE, KSIZE, self.couts[i]) for i in range(1, self.nb)]
         self.y = [e(B, h, h, c) for h, c in zip(self.hs, self.couts)]
-        self.p = [e(B, h // 2, h // 2, c) for h, c in zip(self.hs, self.couts)]
+        self.p = [torch.zeros(B, h // 2 + P2, h // 2 + P2, c, dtype=BF16, device=d) if i + 1 < self.nb
+                  else e(B, h // 2, h // 2, c) for i, (h, c) in enumerate(zip(self.hs, self.couts))]
         self.dP = [e(B, h // 2, h // 2, c) for h, c in zip(self.hs, self.couts)]
         # one dy buffer per block: block i's wgrad (side stream) still reads dy_i
         # while the main stream writes dy_{i-1}
-        self.dYs = [e(B * h * h * c) for h, c in zip(self.hs, self.couts)]
+        self.dYs = [torch.zeros(B, h + P2, h + P2, c, dtype=BF16, device=d) for h, c in zip(self.hs, self.couts)]
         self.coef = [torch.empty(4, c, device=d) for c in self.couts]
         self.acoef = [torch.empty(3, c, device=d) for c in self.couts]
         self.fwd_plan, self.stats = [], []
@@ -176,7 +181,7 @@ class CifarHIPExecutor:
         if x.dim() != 4 or x.shape[-1] != self.cins_real[0] or x.dtype != BF16 or not x.is_contiguous():
             raise ValueError("CifarHIPExecutor expects contiguous NHWC bf16 input [B, H, W, 3]")
         h = self.hs[0]
-        self.C.prep_step(x.data_ptr(), self.x8.data_ptr(), B * h * h, self.cins_real[0], CIN_PAD,
+        self.C.prep_step(x.data_ptr(), self.x8.data_ptr(), B * h * h, self.cins_real[0], CIN_PAD, h, h, SPAD,
                          self.p32[0].data_ptr(), self.w1p.data_ptr(), self.couts[0], KSIZE * KSIZE,
                          self.cins_real[0], CIN_PAD, [], [], [], [], s)
         return B
@@ -184,7 +189,8 @@ class CifarHIPExecutor:
     def _prep_transposes(self, s: int) -> None:
         """Flipped/transposed bf16 weights of blocks 2.. for the dgrad (one launch)."""
         idx = list(range(1, self.nb))
-        self.C.prep_step(0, 0, 0, self.cins_real[0], CIN_PAD, 0, 0, 0, KSIZE * KSIZE, self.cins_real[0], CIN_PAD,
+        self.C.prep_step(0, 0, 0, self.cins_real[0], CIN_PAD, 0, 0, 0, 0, 0, 0, KSIZE * KSIZE, self.cins_real[0],
+                         CIN_PAD,
                          [self.p16[self._leaf(i, 0)].data_ptr() for i in idx], [self.wt[i].data_ptr() for i in idx],
                          [self.couts[i] for i in idx], [self.cins[i] for i in idx], s)
 
@@ -203,7 +209,8 @@ class CifarHIPExecutor:
                           self.p32[self._leaf(i, 3)].data_ptr(), self.p32[self._leaf(i, 1)].data_ptr(),
                           self.rm[i].data_ptr(), self.rv[i].data_ptr(), BN_EPS, BN_MOMENTUM, 0 if train else 1,
                           self.coef[i].data_ptr(), s)
-            C.bn_relu_pool_fwd(self.y[i].data_ptr(), self.coef[i].data_ptr(), self.p[i].data_ptr(), B, h, h, cout, s)
+            C.bn_relu_pool_fwd(self.y[i].data_ptr(), self.coef[i].data_ptr(), self.p[i].data_ptr(), B, h, h, cout,
+                               SPAD if i + 1 < self.nb else 0, s)
             inp = self.p[i]
 
     # ------------------------------------------------------------------ API
@@ -250,7 +257,7 @@ class CifarHIPExecutor:
                               self.coef[i].data_ptr(), self.g32[self._leaf(i, 2)].data_ptr(),
                               self.g32[self._leaf(i, 3)].data_ptr(), self.acoef[i].data_ptr(), s)
             C.bn_relu_pool_bwd_apply(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
-                                     self.acoef[i].data_ptr(), dY.data_ptr(), B, h, h, cout, s)
+                                     self.acoef[i].data_ptr(), dY.data_ptr(), B, h, h, cout, SPAD, s)
             # (optional fork) weight gradient of block i on the side stream
             if self.side_wgrad:
                 side.wait_stream(main)
