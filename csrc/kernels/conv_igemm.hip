@@ -128,6 +128,23 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
+// Buffer-descriptor LDS-DMA (buffer_load_dwordx4 ... offen lds): per-lane 32-bit
+// byte offset in a VGPR + wave-uniform byte offset in an SGPR (soffset), so a
+// load whose per-lane part is loop-invariant costs no VALU at all; offsets at
+// or past `bytes` read zeros (hardware range check), which replaces the zero
+// line for K/M tails.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr unsigned kOOB = 0x40000000u;  // a voffset past every operand: loads zeros
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void blds16(rsrc_t r, unsigned voff, unsigned soff, void* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, (int)voff,
+                                           (int)soff, 0, 0);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -219,9 +236,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
     b_k[j] = ch * 8;
     b_off[j] = (n0 + row) * g.K + ch * 8;
   }
-  const char* zsrc = reinterpret_cast<const char*>(g_zero16);
-  const char* xb = reinterpret_cast<const char*>(x);
-  const char* wb = reinterpret_cast<const char*>(w);
+  const rsrc_t xr = make_rsrc(x, (unsigned)((int64_t)g.B * g.Hp * g.Wp * g.Cin * 2));
+  const rsrc_t wr = make_rsrc(w, (unsigned)((int64_t)g.Cout * g.K * 2));
 
   // Wave-uniform tap state of the next K step to load (TAPU: one step = 64
   // channels of one tap): off = (kh*Wp + kw)*Cin + c0, advanced incrementally
@@ -254,22 +270,22 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
     if (q < A_INS) {
       const int j = q;
       if constexpr (TAPU) {
-        glds16(xb + 2 * (a_base[j] + t.off), sA + (wid * A_INS + j) * 1024);
+        blds16(xr, 2u * (unsigned)a_base[j], 2u * (unsigned)t.off, sA + (wid * A_INS + j) * 1024);
       } else {
         // first layer (Cin < 64): a 64-wide K step spans several taps, per lane
         const int kc = kt * CPR + a_ch[j];
         const int kpos = kc >> g.logC8;
         const int c0 = (kc & (C8 - 1)) << 3;
         const int kh = kpos / g.KS, kw = kpos - kh * g.KS;
-        const char* src = kc < g.Kch ? xb + 2 * (a_base[j] + (kh * g.Wp + kw) * g.Cin + c0) : zsrc;
-        glds16(src, sA + (wid * A_INS + j) * 1024);
+        const unsigned off = kc < g.Kch ? 2u * (unsigned)(a_base[j] + (kh * g.Wp + kw) * g.Cin + c0) : kOOB;
+        blds16(xr, off, 0u, sA + (wid * A_INS + j) * 1024);
       }
     } else {
       const int j = q - A_INS;
       const int kadd = kt * BK;
-      const char* src = wb + 2 * (b_off[j] + kadd);
-      if constexpr (!TAPU) src = (kadd + b_k[j]) < g.K ? src : zsrc;  // K tail (first layer only)
-      glds16(src, sB + (wid * B_INS + j) * 1024);
+      unsigned voff = 2u * (unsigned)b_off[j];
+      if constexpr (!TAPU) voff = (kadd + b_k[j]) < g.K ? voff : kOOB;  // K tail (first layer only)
+      blds16(wr, voff, 2u * (unsigned)kadd, sB + (wid * B_INS + j) * 1024);
     }
   };
 
@@ -291,9 +307,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   constexpr int NMF = (BK / 32) * FM * FN;
   constexpr int IL = NMF / LPS > 0 ? NMF / LPS : 1;
   int slot_c = 0, slot_n = PD % STAGES;
-  for (int i = 0; i < nk; ++i) {
-    if (i + PD - 1 < nk) wait_vmcnt<(PD - 1) * LPS>();  // steady state: stage i landed
-    else wait_stages<LPS>(nk - 1 - i);                  // drain
+  auto kstep = [&](int i) {
     block_sync_lds();  // stage i landed for every wave; slot (i+PD)%STAGES no longer read
     const bool pf = i + PD < nk;
     const int kt_n = kt_beg + i + PD;
@@ -328,6 +342,16 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
     if (pf) tap_advance(tnext);
     slot_c = slot_c + 1 == STAGES ? 0 : slot_c + 1;
     slot_n = slot_n + 1 == STAGES ? 0 : slot_n + 1;
+  };
+  // steady state (constant wait: stage i landed, PD-1 younger stages in flight), then the drain
+  int i = 0;
+  for (; i < nk - (PD - 1); ++i) {
+    wait_vmcnt<(PD - 1) * LPS>();
+    kstep(i);
+  }
+  for (; i < nk; ++i) {
+    wait_stages<LPS>(nk - 1 - i);
+    kstep(i);
   }
 
   const unsigned long long t_loop = dbg ? stamp() : 0ull;
@@ -526,9 +550,13 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
     const int kh = kpos / g.KS, kw = kpos - kh * g.KS;
     b_off[j] = (lane_pix(row) + kh * g.Wp + kw) * g.Cin + ((kc & (C8 - 1)) << 3);
   }
-  const char* zsrc = reinterpret_cast<const char*>(g_zero16);
-  const char* dyb = reinterpret_cast<const char*>(dy);
-  const char* xb = reinterpret_cast<const char*>(x);
+  const rsrc_t dyr = make_rsrc(dy, (unsigned)((int64_t)g.B * g.Hp * g.Wp * g.Cout * 2));
+  const rsrc_t xr = make_rsrc(x, (unsigned)((int64_t)g.B * g.Hp * g.Wp * g.Cin * 2));
+  unsigned a_v[A_INS], b_v[B_INS];  // per-lane byte offsets (K-tail lanes: out of range -> zeros)
+#pragma unroll
+  for (int j = 0; j < A_INS; ++j) a_v[j] = 2u * (unsigned)a_off[j];
+#pragma unroll
+  for (int j = 0; j < B_INS; ++j) b_v[j] = b_kok[j] ? 2u * (unsigned)b_off[j] : kOOB;
 
   auto issue = [&](int kt, int slot) {
     char* sA = smem + slot * STAGE_BYTES;
@@ -536,25 +564,17 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
     const int ms = mbeg + kt * BK;  // 64-aligned first row of the step
     const int u = (ms >> g.logHW) * HpWp + ((ms & (HW - 1)) >> g.logW) * g.Wp;  // wave-uniform
     const int left = mend - ms;                                                  // rows left (uniform)
+    const unsigned ua = 2u * (unsigned)(u * g.Cout), ub = 2u * (unsigned)(u * g.Cin);
     if (left >= BK) {
 #pragma unroll
-      for (int j = 0; j < A_INS; ++j) glds16(dyb + 2 * (u * g.Cout + a_off[j]), sA + (wid * A_INS + j) * 1024);
+      for (int j = 0; j < A_INS; ++j) blds16(dyr, a_v[j], ua, sA + (wid * A_INS + j) * 1024);
 #pragma unroll
-      for (int j = 0; j < B_INS; ++j) {
-        const char* src = xb + 2 * (u * g.Cin + b_off[j]);
-        glds16(b_kok[j] ? src : zsrc, sB + (wid * B_INS + j) * 1024);
-      }
+      for (int j = 0; j < B_INS; ++j) blds16(xr, b_v[j], ub, sB + (wid * B_INS + j) * 1024);
     } else {  // partial last step: rows past the end read zeros
 #pragma unroll
-      for (int j = 0; j < A_INS; ++j) {
-        const char* src = dyb + 2 * (u * g.Cout + a_off[j]);
-        glds16(a_row[j] < left ? src : zsrc, sA + (wid * A_INS + j) * 1024);
-      }
+      for (int j = 0; j < A_INS; ++j) blds16(dyr, a_row[j] < left ? a_v[j] : kOOB, ua, sA + (wid * A_INS + j) * 1024);
 #pragma unroll
-      for (int j = 0; j < B_INS; ++j) {
-        const char* src = xb + 2 * (u * g.Cin + b_off[j]);
-        glds16(b_kok[j] && b_row[j] < left ? src : zsrc, sB + (wid * B_INS + j) * 1024);
-      }
+      for (int j = 0; j < B_INS; ++j) blds16(xr, b_row[j] < left ? b_v[j] : kOOB, ub, sB + (wid * B_INS + j) * 1024);
     }
   };
 
@@ -570,9 +590,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
   for (int p = 0; p < PD; ++p)
     if (p < nk) issue(p, p);
   int slot_c = 0, slot_n = PD % STAGES;
-  for (int i = 0; i < nk; ++i) {
-    if (i + PD - 1 < nk) wait_vmcnt<(PD - 1) * LPS>();
-    else wait_stages<LPS>(nk - 1 - i);
+  auto kstep = [&](int i) {
     block_sync_lds();
     if (i + PD < nk) issue(i + PD, slot_n);
     const char* As = smem + slot_c * STAGE_BYTES;
@@ -604,6 +622,15 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
     }
     slot_c = slot_c + 1 == STAGES ? 0 : slot_c + 1;
     slot_n = slot_n + 1 == STAGES ? 0 : slot_n + 1;
+  };
+  int i = 0;
+  for (; i < nk - (PD - 1); ++i) {
+    wait_vmcnt<(PD - 1) * LPS>();
+    kstep(i);
+  }
+  for (; i < nk; ++i) {
+    wait_stages<LPS>(nk - 1 - i);
+    kstep(i);
   }
 
   float* o = out + (int64_t)split * g.Cout * ldo;
