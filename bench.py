@@ -126,20 +126,40 @@ def main():
                                  compute_dtype=cdt, bucket_bytes=int(a.bucket_mb * (1 << 20)),
                                  graph=bool(a.graph) and not cpu, max_batch=batch)
         tr.synchronize_parameters()
-        # synthetic data of the named shape: NHWC bf16, normalised; labels uniform
-        g = torch.Generator(device=dev).manual_seed(1234 + rank)
-        nb = 8 if a.model == "cifar10" else 2
-        hw, ncls = (32, 10) if a.model == "cifar10" else (224, 1000)
-        xs = torch.randn(nb, batch, hw, hw, 3, device=dev, generator=g).to(cdt)
-        ys = torch.randint(0, ncls, (nb, batch), device=dev, generator=g)
-        for i in range(a.warmup):
-            tr.step(xs[i % nb], ys[i % nb])
+        if a.model == "cifar10":
+            # synthetic CIFAR-10-shaped uint8 dataset resident in HBM (this rank's
+            # partition of 50k images); the batch of every step is selected by a
+            # device-side permutation sampler and gathered + normalised + padded
+            # inside the (graph-captured) step -- the real data path, not a
+            # pre-made tensor
+            from torch_distlearn_amd.data import DeviceLoader, PartitionedDataset
+
+            n_local = max(batch, 50000 // len(workers))
+            g = torch.Generator(device=dev).manual_seed(1234 + rank)
+            imgs = torch.randint(0, 256, (n_local, 32, 32, 3), dtype=torch.uint8, device=dev, generator=g)
+            labs = torch.randint(0, 10, (n_local,), device=dev, generator=g)
+            loader = DeviceLoader(PartitionedDataset(imgs, labs, device=dev), "permutation", batch, seed=rank)
+            step_args = None
+        else:
+            g = torch.Generator(device=dev).manual_seed(1234 + rank)
+            nb = 2
+            xs = torch.randn(nb, batch, 224, 224, 3, device=dev, generator=g).to(cdt)
+            ys = torch.randint(0, 1000, (nb, batch), device=dev, generator=g)
+            step_args = lambda i: (xs[i % nb], ys[i % nb])  # noqa: E731
+        if step_args is None:  # device loader: unrolled graph replays of complete steps
+            tr.run(loader, a.warmup)
+        else:
+            for i in range(a.warmup):
+                tr.step(*step_args(i))
         sync()
         worker_barrier()
         sync()
         t0 = time.perf_counter()
-        for i in range(a.steps):
-            loss = tr.step(xs[i % nb], ys[i % nb])
+        if step_args is None:
+            loss = tr.run(loader, a.steps)
+        else:
+            for i in range(a.steps):
+                loss = tr.step(*step_args(i))
         sync()
         worker_barrier()
         sync()
@@ -165,7 +185,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else round(imgs / BASELINE_VALUE, 4),
             "dtype": "fp32" if cpu else "bf16",
-            "data": f"synthetic ({a.model} shaped, random-init weights)",
+            "data": ("synthetic CIFAR-10-shaped uint8 dataset in HBM (50k images split over the workers), "
+                     "device-side permutation sampler, gather+normalise inside the step; random-init weights")
+            if a.model == "cifar10" else "synthetic ImageNet-shaped bf16 batches, random-init weights",
             "config": {"model": MODEL_DESC[a.model],
                        "global_batch": batch * len(workers), "per_gpu_batch": batch, "seq_len": None,
                        "parallelism": f"dp{len(workers)}" + ("+ps1" if a.algo == "async" else ""), "algo": a.algo,

@@ -37,6 +37,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("pack_weight", &pack_weight);
   m.def("pad_channels", &pad_channels);
   m.def("prep_step", &prep_step);
+  m.def("prep_step_gather", &prep_step_gather);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_relu_pool_fwd", &bn_relu_pool_fwd);
   m.def("bn_bwd_blocks", &bn_bwd_blocks);

@@ -42,6 +42,11 @@ void pad_channels(uintptr_t x, uintptr_t xp, int64_t P, int C, int Cp, uintptr_t
 void prep_step(uintptr_t x, uintptr_t xp, int64_t P, int C, int Cp, int H, int W, int sp, uintptr_t w1, uintptr_t w1p,
                int w1_cout, int taps, int w1_c, int w1_cp, std::vector<uintptr_t> tw, std::vector<uintptr_t> twt,
                std::vector<int> tcout, std::vector<int> tcin, uintptr_t stream);
+void prep_step_gather(uintptr_t img, uintptr_t order, uintptr_t lab_all, uintptr_t lab_out, uintptr_t ctr,
+                      int n_order, int B, int C, std::vector<float> mean, std::vector<float> stdv, uintptr_t xp,
+                      int Cp, int H, int W, int sp, uintptr_t w1, uintptr_t w1p, int w1_cout, int taps, int w1_c,
+                      int w1_cp, std::vector<uintptr_t> tw, std::vector<uintptr_t> twt, std::vector<int> tcout,
+                      std::vector<int> tcin, uintptr_t stream);
 
 // bn_pool.hip -----------------------------------------------------------------
 void bn_finalize(uintptr_t partial, int T, int C, int64_t M, uintptr_t gamma, uintptr_t beta, uintptr_t bias,

@@ -722,8 +722,14 @@ __global__ void __launch_bounds__(256) pad_channels_kernel(const bf16_t* __restr
 // one tap through LDS.
 // --------------------------------------------------------------------------
 struct PrepArgs {
-  const bf16_t* x; bf16_t* xp; int64_t P; int C, Cp;            // input pad (channels + spatial)
+  const bf16_t* x; bf16_t* xp; int P; int C, Cp;                // input pad (channels + spatial)
   int H, W, sp;                                                 // image dims, spatial zero pad
+  // device-side data path (img != nullptr): gather + normalise the step's
+  // batch straight from the HBM-resident uint8 dataset
+  const uint8_t* img; const int* order; const int64_t* lab_all; int64_t* lab_out;
+  unsigned long long* ctr;  // [0] = step counter, [1] = arrival ticket
+  int n_order, B;
+  float mean[3], inv_std[3];
   const float* w1; bf16_t* w1p; int w1_cout, taps, w1_c, w1_cp;  // layer-1 pack
   int nt;                                                        // transposes
   const bf16_t* tw[4]; bf16_t* twt[4]; int tcout[4], tcin[4];
@@ -735,24 +741,48 @@ __global__ void __launch_bounds__(256) prep_step_kernel(const PrepArgs a) {
   int blk = blockIdx.x;
   if (blk < a.nb_pad) {
     const int HW = a.H * a.W, Hp = a.H + 2 * a.sp, Wp = a.W + 2 * a.sp;
-    for (int64_t p = (int64_t)blk * 256 + threadIdx.x; p < a.P; p += (int64_t)a.nb_pad * 256) {
+    unsigned long long step = 0;
+    if (a.img) step = __hip_atomic_load(a.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int p = blk * 256 + threadIdx.x; p < a.P; p += a.nb_pad * 256) {
+      const int b = p / HW;
+      const int r = p - b * HW, h = r / a.W, w = r - h * a.W;
       bf16_t v[16];
 #pragma unroll
       for (int c = 0; c < 16; ++c) v[c] = 0;
-      for (int c = 0; c < a.C; ++c) v[c] = a.x[p * a.C + c];
-      const int64_t b = p / HW;
-      const int r = (int)(p - b * HW), h = r / a.W, w = r - h * a.W;
-      const int64_t q = (b * Hp + h + a.sp) * Wp + w + a.sp;  // interior of the zero-bordered buffer
+      if (a.img) {
+        // sample of this step = order[(step * B + b) mod n_order]
+        const int pos = (int)((step * (unsigned long long)a.B + (unsigned long long)b) % (unsigned)a.n_order);
+        const int smp = a.order[pos];
+        const uint8_t* src = a.img + ((int64_t)smp * HW + r) * a.C;
+        for (int c = 0; c < a.C && c < 3; ++c) v[c] = f32_to_bf16((src[c] * (1.0f / 255.0f) - a.mean[c]) * a.inv_std[c]);
+        if (r == 0) a.lab_out[b] = a.lab_all[smp];
+      } else {
+        for (int c = 0; c < a.C; ++c) v[c] = a.x[(int64_t)p * a.C + c];
+      }
+      const int64_t q = ((int64_t)b * Hp + h + a.sp) * Wp + w + a.sp;  // interior of the zero-bordered buffer
       for (int c = 0; c < a.Cp; c += 8)
         *reinterpret_cast<uint4*>(a.xp + q * a.Cp + c) = *reinterpret_cast<const uint4*>(v + c);
+    }
+    if (a.img) {
+      // the last gather block to finish advances the step counter: every
+      // block read it before its arrival (the read's value was consumed
+      // before the barrier), so no block of this step sees the new value
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const unsigned long long n = atomicAdd(a.ctr + 1, 1ull);
+        if (n + 1 == (unsigned long long)a.nb_pad) {
+          a.ctr[1] = 0;
+          atomicAdd(a.ctr, 1ull);
+        }
+      }
     }
     return;
   }
   blk -= a.nb_pad;
   if (blk < a.nb_pack) {
-    const int64_t total = (int64_t)a.w1_cout * a.taps * a.w1_cp;
-    for (int64_t i = (int64_t)blk * 256 + threadIdx.x; i < total; i += (int64_t)a.nb_pack * 256) {
-      const int c = (int)(i % a.w1_cp);
+    const int total = a.w1_cout * a.taps * a.w1_cp;
+    for (int i = blk * 256 + threadIdx.x; i < total; i += a.nb_pack * 256) {
+      const int c = i % a.w1_cp;
       a.w1p[i] = c < a.w1_c ? f32_to_bf16(a.w1[(i / a.w1_cp) * a.w1_c + c]) : (bf16_t)0;
     }
     return;
@@ -780,14 +810,13 @@ __global__ void __launch_bounds__(256) prep_step_kernel(const PrepArgs a) {
   }
 }
 
-void prep_step(uintptr_t x, uintptr_t xp, int64_t P, int C, int Cp, int H, int W, int sp, uintptr_t w1, uintptr_t w1p,
-               int w1_cout, int taps, int w1_c, int w1_cp, std::vector<uintptr_t> tw, std::vector<uintptr_t> twt,
-               std::vector<int> tcout, std::vector<int> tcin, uintptr_t stream) {
-  PrepArgs a{};
-  if (C > 16 || Cp > 16 || Cp % 8 != 0) throw std::runtime_error("prep_step: input channels must pad to 8 or 16");
-  if (P > 0 && (H <= 0 || W <= 0 || P % ((int64_t)H * W) != 0)) throw std::runtime_error("prep_step: P != B*H*W");
-  a.x = (const bf16_t*)x; a.xp = (bf16_t*)xp; a.P = P; a.C = C; a.Cp = Cp;
-  a.H = H; a.W = W; a.sp = sp;
+static void launch_prep(PrepArgs& a, int64_t P, uintptr_t w1, uintptr_t w1p, int w1_cout, int taps, int w1_c,
+                        int w1_cp, const std::vector<uintptr_t>& tw, const std::vector<uintptr_t>& twt,
+                        const std::vector<int>& tcout, const std::vector<int>& tcin, uintptr_t stream) {
+  if (a.C > 16 || a.Cp > 16 || a.Cp % 8 != 0) throw std::runtime_error("prep_step: input channels must pad to 8 or 16");
+  if (P >= (1ll << 31)) throw std::runtime_error("prep_step: too many pixels");
+  if (P > 0 && (a.H <= 0 || a.W <= 0 || P % ((int64_t)a.H * a.W) != 0)) throw std::runtime_error("prep_step: P != B*H*W");
+  a.P = (int)P;
   a.w1 = (const float*)w1; a.w1p = (bf16_t*)w1p; a.w1_cout = w1_cout; a.taps = taps; a.w1_c = w1_c; a.w1_cp = w1_cp;
   a.nt = (int)tw.size();
   if (a.nt > 4 || twt.size() != tw.size() || tcout.size() != tw.size() || tcin.size() != tw.size())
@@ -801,8 +830,41 @@ void prep_step(uintptr_t x, uintptr_t xp, int64_t P, int C, int Cp, int H, int W
     a.nb_t[j] = ((tcin[j] + 31) / 32) * ((tcout[j] + 31) / 32) * taps;
     total += a.nb_t[j];
   }
+  if (total == 0) return;
   prep_step_kernel<<<total, 256, 0, as_stream(stream)>>>(a);
   DL_HIP_CHECK(hipGetLastError());
+}
+
+void prep_step(uintptr_t x, uintptr_t xp, int64_t P, int C, int Cp, int H, int W, int sp, uintptr_t w1, uintptr_t w1p,
+               int w1_cout, int taps, int w1_c, int w1_cp, std::vector<uintptr_t> tw, std::vector<uintptr_t> twt,
+               std::vector<int> tcout, std::vector<int> tcin, uintptr_t stream) {
+  PrepArgs a{};
+  a.x = (const bf16_t*)x; a.xp = (bf16_t*)xp; a.C = C; a.Cp = Cp;
+  a.H = H; a.W = W; a.sp = sp;
+  launch_prep(a, P, w1, w1p, w1_cout, taps, w1_c, w1_cp, tw, twt, tcout, tcin, stream);
+}
+
+// Same launch with the step's input gathered on the device: batch b of step
+// s (= ctr[0]) is sample order[(s*B + b) mod n_order] of the uint8 NHWC
+// dataset `img`, normalised ((v/255 - mean)/std), channel- and spatially
+// padded into xp; its label goes to lab_out[b].  The last gather block
+// advances ctr[0], so a captured graph replays consecutive batches.
+void prep_step_gather(uintptr_t img, uintptr_t order, uintptr_t lab_all, uintptr_t lab_out, uintptr_t ctr,
+                      int n_order, int B, int C, std::vector<float> mean, std::vector<float> stdv, uintptr_t xp,
+                      int Cp, int H, int W, int sp, uintptr_t w1, uintptr_t w1p, int w1_cout, int taps, int w1_c,
+                      int w1_cp, std::vector<uintptr_t> tw, std::vector<uintptr_t> twt, std::vector<int> tcout,
+                      std::vector<int> tcin, uintptr_t stream) {
+  if (C > 3 || mean.size() < (size_t)C || stdv.size() < (size_t)C) throw std::runtime_error("prep_step_gather: C <= 3");
+  if (n_order <= 0 || B <= 0) throw std::runtime_error("prep_step_gather: empty order / batch");
+  PrepArgs a{};
+  a.xp = (bf16_t*)xp; a.C = C; a.Cp = Cp; a.H = H; a.W = W; a.sp = sp;
+  a.img = (const uint8_t*)img; a.order = (const int*)order; a.lab_all = (const int64_t*)lab_all;
+  a.lab_out = (int64_t*)lab_out; a.ctr = (unsigned long long*)ctr; a.n_order = n_order; a.B = B;
+  for (int c = 0; c < 3; ++c) {
+    a.mean[c] = c < C ? mean[c] : 0.f;
+    a.inv_std[c] = c < C ? 1.0f / stdv[c] : 1.f;
+  }
+  launch_prep(a, (int64_t)B * H * W, w1, w1p, w1_cout, taps, w1_c, w1_cp, tw, twt, tcout, tcin, stream);
 }
 
 // --------------------------------------------------------------------------

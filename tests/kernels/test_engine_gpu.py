@@ -92,6 +92,61 @@ def test_hip_and_torch_backends_train_alike(dev):
         assert abs(a - b) < 0.1 * max(1.0, abs(b))
 
 
+def _loader(dev, batch=32, seed=3, kind="permutation"):
+    from torch_distlearn_amd.data import DeviceLoader, PartitionedDataset, synthetic_cifar10
+
+    imgs, labels = synthetic_cifar10(200, seed=5)
+    return DeviceLoader(PartitionedDataset(imgs, labels, device=dev), kind, batch, seed=seed)
+
+
+def test_device_loader_gather_in_prep(dev):
+    """prep_step_gather = the eager gather of the same batch; the device-side
+    step counter advances once per step and wraps into a new epoch."""
+    from torch_distlearn_amd.models import make_executor, CifarConvNet
+    from torch_distlearn_amd.ops.flat import FlatParams
+
+    model = CifarConvNet(seed=1).to(dev)
+    flat = FlatParams(model, grads=True, shadow_bf16=True)
+    ex = make_executor(model, flat, max_batch=32)
+    la, lb = _loader(dev), _loader(dev)  # identical sample streams
+    assert la.steps_per_epoch == 6
+    seen = []
+    for k in range(8):  # crosses the epoch boundary
+        xe, ye = lb.getBatch()
+        ex.forward_backward(la, None)
+        torch.cuda.synchronize()
+        assert int(la.ctr[0]) == k % 6 + 1 and int(la.ctr[1]) == 0
+        inner = ex.x8[:32, 2:34, 2:34]
+        torch.testing.assert_close(inner[..., :3].float(), xe.to(torch.bfloat16).float(), rtol=0, atol=2e-2)
+        assert not inner[..., 3:].any()
+        assert torch.equal(la.labels_out, ye)
+        seen.append(ye)
+        la.step_done()
+        lb.step_done()
+    assert la.epoch == 1
+
+
+def test_device_loader_graph_matches_eager(dev):
+    outs = []
+    for graph, port in ((False, 29703), (True, 29703)):
+        tr = _trainer(dev, "hip", graph, port)
+        ld = _loader(dev)
+        losses = [float(tr.step(ld)) for _ in range(8)]
+        torch.cuda.synchronize()
+        outs.append((tr.flat.data.clone(), losses, int(ld.ctr[0]), ld.epoch))
+    (p0, l0, c0, e0), (p1, l1, c1, e1) = outs
+    assert (c0, e0) == (c1, e1) == (2, 1)
+    assert max(abs(a - b) for a, b in zip(l0, l1)) < 1e-3
+    assert float((p0 - p1).abs().max()) < 1e-3
+    # unrolled multi-step graphs (trainer.run): same 8 steps, same parameters
+    tr = _trainer(dev, "hip", True, 29703)
+    ld = _loader(dev)
+    tr.run(ld, 8, unroll=3)
+    torch.cuda.synchronize()
+    assert (int(ld.ctr[0]), ld.epoch, tr.steps, int(tr.sgd.stepsPerNode.sum())) == (2, 1, 8, 8)
+    assert float((tr.flat.data - p1).abs().max()) < 1e-3
+
+
 def _run(args, timeout=600):
     env = dict(os.environ, PYTHONPATH=ROOT)
     r = subprocess.run([sys.executable] + args, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)

@@ -186,6 +186,85 @@ class Batcher:
     get_batch = getBatch
 
 
+class DeviceLoader:
+    """Device-side batching for graph-captured training steps.
+
+    The epoch's sample order (from the same native sampler as
+    :class:`Batcher`) is uploaded ONCE per epoch as an int32 vector in HBM;
+    a step's batch is then selected by a device-resident step counter and
+    gathered + normalised + padded by the native executor's first kernel
+    (``prep_step_gather``), which also advances the counter.  A captured
+    hipGraph therefore replays consecutive batches with no per-step host
+    work and no host->device copies.  :meth:`step_done` keeps the host's
+    count so that a new epoch's order is uploaded (outside the graph, in
+    place) when the current one is used up.
+
+    Paths without the native executor call :meth:`getBatch` (eager gather of
+    the same batch sequence).
+    """
+
+    def __init__(self, ds: PartitionedDataset, kind: str = "permutation", batch: int = 32, seed: int = 0):
+        self.ds, self.batch = ds, int(batch)
+        self.H, self.W = ds.H, ds.W
+        self.sampler = make_sampler(ds.N, ds.labels_host.tolist() if kind == "label-uniform" else None,
+                                    ds.num_classes, ds.partition, ds.partitions, kind, seed)
+        self.steps_per_epoch = max(1, int(self.sampler.size()) // self.batch)
+        n = self.steps_per_epoch * self.batch
+        self.order = torch.empty(n, dtype=torch.int32, device=ds.device)
+        self.ctr = torch.zeros(2, dtype=torch.int64, device=ds.device)  # [step, arrival ticket]
+        self.labels_out = torch.empty(self.batch, dtype=torch.int64, device=ds.device)
+        self._host_steps = 0
+        self.epoch = 0
+        self._idx = torch.empty(self.batch, dtype=torch.int64)
+        self._fill_epoch()
+
+    def _fill_epoch(self) -> None:
+        self.sampler.reset_epoch()
+        rows = []
+        for _ in range(self.steps_per_epoch):
+            _next_indices(self.sampler, self.batch, self._idx)
+            rows.append(self._idx.clone())
+        self.order.copy_(torch.cat(rows).to(torch.int32))
+        self.ctr.zero_()
+        self._host_steps = 0
+
+    def numBatches(self) -> int:  # noqa: N802
+        return self.steps_per_epoch
+
+    num_batches = numBatches
+
+    def gather_args(self):
+        ds = self.ds
+        return (ds.images.data_ptr(), self.order.data_ptr(), ds.labels.data_ptr(), self.labels_out.data_ptr(),
+                self.ctr.data_ptr(), int(self.order.numel()), ds.C, [float(v) for v in ds.mean[:ds.C]],
+                [float(v) for v in ds.std[:ds.C]])
+
+    def step_done(self) -> None:
+        """Host bookkeeping after a step consumed a batch: start a new epoch
+        (new order, counter reset) once this one is used up."""
+        self._host_steps += 1
+        if self._host_steps >= self.steps_per_epoch:
+            self.epoch += 1
+            self._fill_epoch()
+
+    def getBatch(self) -> Tuple[torch.Tensor, torch.Tensor]:  # noqa: N802
+        """Eager equivalent (the same batch the device path would use):
+        (x NHWC normalised, y int64); advances the counter."""
+        k = int(self.ctr[0].item()) % self.steps_per_epoch
+        idx = self.order[k * self.batch:(k + 1) * self.batch].to(torch.int64)
+        ds = self.ds
+        x = ds.images.index_select(0, idx).float().div_(255.0)
+        mean = torch.tensor(ds.mean[:ds.C], dtype=torch.float32, device=x.device)
+        std = torch.tensor(ds.std[:ds.C], dtype=torch.float32, device=x.device)
+        x = ((x - mean) / std)
+        self.ctr[0] += 1
+        y = ds.labels.index_select(0, idx)
+        self.labels_out.copy_(y)
+        return x, y
+
+    get_batch = getBatch
+
+
 # ---------------------------------------------------------------------------
 # sources
 # ---------------------------------------------------------------------------

@@ -127,19 +127,32 @@ class DataParallelTrainer:
         sgd_update_(f.data, f.grad, self.lr, slot=None, mom=self.mom, momentum=self.momentum,
                     weight_decay=self.weight_decay, shadow=f.shadow)
 
-    def step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    def step(self, x, y: Optional[torch.Tensor] = None) -> torch.Tensor:
         """One training step on this node's mini-batch; returns the loss
-        (a device tensor; no host synchronisation)."""
+        (a device tensor; no host synchronisation).  ``x`` is an NHWC batch
+        with labels ``y``, or a :class:`~torch_distlearn_amd.data.DeviceLoader`
+        (the native executor then gathers the batch on the device inside the
+        step, so a captured graph needs no per-step host work)."""
         self.steps += 1
+        loader = x if hasattr(x, "gather_args") else None
+        if loader is not None and self.executor is None:
+            x, y = loader.getBatch()
+            x = x.to(self.compute_dtype)
+            dev_loader = None
+        else:
+            dev_loader = loader
         if not self.graph:
             loss = self._step_body(x, y)
         else:
             if self._graph is None:
                 self._capture(x, y)
-            if x.data_ptr() != self._static[0].data_ptr():
-                self._static[0].copy_(x, non_blocking=True)
-            if y.data_ptr() != self._static[1].data_ptr():
-                self._static[1].copy_(y, non_blocking=True)
+            if dev_loader is None:
+                if x.data_ptr() != self._static[0].data_ptr():
+                    self._static[0].copy_(x, non_blocking=True)
+                if y.data_ptr() != self._static[1].data_ptr():
+                    self._static[1].copy_(y, non_blocking=True)
+            elif self._static[0] is not dev_loader:
+                raise ValueError("the captured step is bound to another DeviceLoader")
             self._graph.replay()
             if self.sgd is not None:
                 # the captured body counted one step at capture time only
@@ -151,8 +164,57 @@ class DataParallelTrainer:
         elif self.aea is not None:
             self.aea.syncClient(self.flat)   # EASGD_client.lua:109
             self._local_update()             # :113-117 (pre-move grads)
+        if loader is not None:
+            loader.step_done()
         self.last_loss = loss
         return loss
+
+    def run(self, loader, nsteps: int, unroll: int = 8) -> torch.Tensor:
+        """``nsteps`` training steps on a :class:`DeviceLoader`; returns the
+        last step's loss.  With the native executor, hipGraph capture and
+        AllReduceSGD, ``unroll`` consecutive steps (forward, backward, bucketed
+        all-reduce and update each) are captured into ONE graph, so the
+        per-replay launch latency is paid once per ``unroll`` steps; epoch
+        tails and other configurations run step by step.  Every step is
+        still a complete step (the same kernels and collectives as
+        :meth:`step`)."""
+        loss = None
+        fast = self.graph and self.algo == "sgd" and self.executor is not None and unroll > 1
+        while nsteps > 0:
+            left = loader.steps_per_epoch - loader._host_steps
+            if fast and nsteps >= unroll and left >= unroll:
+                if self._graph is None:  # single-step graph first (warm-up, allocations)
+                    loss = self.step(loader)
+                    nsteps -= 1
+                    continue
+                g = self._multi.get(unroll) if hasattr(self, "_multi") else None
+                if g is None:
+                    g = self._capture_multi(loader, unroll)
+                g[0].replay()
+                for _ in range(unroll):
+                    self.sgd._count_step()
+                    loader.step_done()
+                self.steps += unroll
+                loss = g[1]
+                self.last_loss = loss
+                nsteps -= unroll
+            else:
+                loss = self.step(loader)
+                nsteps -= 1
+        return loss
+
+    def _capture_multi(self, loader, k: int):
+        """Capture k consecutive step bodies on ``loader`` into one graph
+        (state the capture touches is restored; replay counts the steps)."""
+        if not hasattr(self, "_multi"):
+            self._multi = {}
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(k):
+                loss = self._step_body(loader, None)
+        self.sgd.stepsPerNode[self.tree.nodeIndex - 1] -= k  # capture counted k (not executed)
+        self._multi[k] = (g, loss)
+        return self._multi[k]
 
     def static_inputs(self):
         """The graph's input buffers (after the first step): a data loader
@@ -160,12 +222,16 @@ class DataParallelTrainer:
         return None if self._static is None else self._static[:2]
 
     def _capture(self, x, y):
-        sx, sy = x.clone(), y.clone()
-        # warm up on a side stream (allocations, autotuning), as torch.cuda.graphs requires
+        dev_loader = hasattr(x, "gather_args")
+        sx, sy = (x, None) if dev_loader else (x.clone(), y.clone())
+        # warm up on a side stream (allocations, autotuning), as torch.cuda.graphs requires;
+        # everything the warm-up steps change is restored afterwards
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         saved = self.flat.data.clone()
         saved_mom = None if self.mom is None else self.mom.clone()
+        saved_bufs = [b.detach().clone() for b in self.model.buffers()]
+        saved_ctr = x.ctr.clone() if dev_loader else None
         with torch.cuda.stream(s):
             for _ in range(2):
                 self._step_body(sx, sy)
@@ -182,6 +248,10 @@ class DataParallelTrainer:
         self.flat.refresh_shadow()
         if saved_mom is not None:
             self.mom.copy_(saved_mom)
+        for b, v in zip(self.model.buffers(), saved_bufs):
+            b.detach().copy_(v)
+        if saved_ctr is not None:
+            x.ctr.copy_(saved_ctr)
         self._graph, self._static = g, (sx, sy, loss)
 
     # ------------------------------------------------------------------ epoch end

@@ -173,26 +173,45 @@ class CifarHIPExecutor:
     def _leaf(self, blk: int, j: int) -> int:
         return 4 * blk + j  # conv_w, conv_b, bn_w, bn_b
 
-    def _prep(self, x: torch.Tensor, s: int) -> int:
-        """Input channel pad + layer-1 weight pack (one launch)."""
+    def _transpose_args(self, with_transposes: bool):
+        if not with_transposes:
+            return [], [], [], []
+        idx = list(range(1, self.nb))
+        return ([self.p16[self._leaf(i, 0)].data_ptr() for i in idx], [self.wt[i].data_ptr() for i in idx],
+                [self.couts[i] for i in idx], [self.cins[i] for i in idx])
+
+    def _prep(self, x, s: int, with_transposes: bool = False) -> int:
+        """ONE launch: the step's input into the zero-bordered, channel-padded
+        layer-1 buffer (from a bf16 NHWC tensor, or gathered + normalised on
+        the device from a :class:`~torch_distlearn_amd.data.DeviceLoader`),
+        the layer-1 weight pack and (optionally) the dgrad weight transposes."""
+        h = self.hs[0]
+        tw = self._transpose_args(with_transposes)
+        if hasattr(x, "gather_args"):  # DeviceLoader: batch selected by the device-side step counter
+            B = x.batch
+            if B > self.cap:
+                raise ValueError(f"batch {B} > executor capacity {self.cap}")
+            img, order, lab_all, lab_out, ctr, n_order, C, mean, std = x.gather_args()
+            if (x.H, x.W, C) != (h, h, self.cins_real[0]):
+                raise ValueError("DeviceLoader images do not match the model input")
+            self.C.prep_step_gather(img, order, lab_all, lab_out, ctr, n_order, B, C, mean, std, self.x8.data_ptr(),
+                                    CIN_PAD, h, h, SPAD, self.p32[0].data_ptr(), self.w1p.data_ptr(), self.couts[0],
+                                    KSIZE * KSIZE, self.cins_real[0], CIN_PAD, *tw, s)
+            return B
         B = x.shape[0]
         if B > self.cap:
             raise ValueError(f"batch {B} > executor capacity {self.cap}")
         if x.dim() != 4 or x.shape[-1] != self.cins_real[0] or x.dtype != BF16 or not x.is_contiguous():
             raise ValueError("CifarHIPExecutor expects contiguous NHWC bf16 input [B, H, W, 3]")
-        h = self.hs[0]
         self.C.prep_step(x.data_ptr(), self.x8.data_ptr(), B * h * h, self.cins_real[0], CIN_PAD, h, h, SPAD,
                          self.p32[0].data_ptr(), self.w1p.data_ptr(), self.couts[0], KSIZE * KSIZE,
-                         self.cins_real[0], CIN_PAD, [], [], [], [], s)
+                         self.cins_real[0], CIN_PAD, *tw, s)
         return B
 
     def _prep_transposes(self, s: int) -> None:
         """Flipped/transposed bf16 weights of blocks 2.. for the dgrad (one launch)."""
-        idx = list(range(1, self.nb))
         self.C.prep_step(0, 0, 0, self.cins_real[0], CIN_PAD, 0, 0, 0, 0, 0, 0, KSIZE * KSIZE, self.cins_real[0],
-                         CIN_PAD,
-                         [self.p16[self._leaf(i, 0)].data_ptr() for i in idx], [self.wt[i].data_ptr() for i in idx],
-                         [self.couts[i] for i in idx], [self.cins[i] for i in idx], s)
+                         CIN_PAD, *self._transpose_args(True), s)
 
     def _forward(self, B: int, s: int, train: bool):
         C = self.C
@@ -214,24 +233,24 @@ class CifarHIPExecutor:
             inp = self.p[i]
 
     # ------------------------------------------------------------------ API
-    def forward_backward(self, x: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
-        """One forward + backward on this node's batch; fp32 grads land in the
-        flat gradient buffer.  Returns the mean loss (device tensor)."""
+    def forward_backward(self, x, labels: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One forward + backward on this node's batch (``x`` NHWC bf16 with
+        int64 ``labels``, or a DeviceLoader); fp32 grads land in the flat
+        gradient buffer.  Returns the mean loss (device tensor)."""
         C = self.C
         main, side = torch.cuda.current_stream(), self.side
         s, ss = main.cuda_stream, side.cuda_stream
+        if hasattr(x, "gather_args"):
+            labels = x.labels_out
         if labels.dtype != torch.int64:
             raise ValueError("labels must be int64")
-        B = self._prep(x, s)
+        B = self._prep(x, s, with_transposes=not self.fork_transposes)
         self._last_b = B
-        # fork: dgrad weight transposes overlap the forward
-        if self.fork_transposes:
+        if self.fork_transposes:  # dgrad weight transposes overlap the forward
             side.wait_stream(main)
             self._prep_transposes(ss)
             wt_ready = torch.cuda.Event()
             wt_ready.record(side)
-        else:
-            self._prep_transposes(s)
         self._forward(B, s, train=True)
         nfc = 4 * self.nb
         C.head_fwd_bwd(self.p[-1].data_ptr(), self.p32[nfc].data_ptr(), self.p32[nfc + 1].data_ptr(),
