@@ -45,7 +45,9 @@ def parse():
     ap.add_argument("--tau", type=int, default=10)
     ap.add_argument("--alpha", type=float, default=0.2)
     ap.add_argument("--graph", type=int, default=1, help="capture the step in a hipGraph")
-    ap.add_argument("--bucket-mb", type=float, default=4.0)
+    ap.add_argument("--bucket-mb", type=float, default=None,
+                    help="gradient all-reduce bucket size (default: cifar10 1 MiB = 3 buckets "
+                         "{conv4+bn4+fc, conv3+bn3, conv1..bn2}; resnet50 16 MiB)")
     ap.add_argument("--lr", type=float, default=0.1)
     return ap.parse_args()
 
@@ -89,6 +91,8 @@ def main():
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29517")
     batch = a.batch or (128 if a.model == "cifar10" else 256)
+    if a.bucket_mb is None:
+        a.bucket_mb = 1.0 if a.model == "cifar10" else 16.0
     backend = a.backend if (a.model == "cifar10" and not cpu) else "torch"
     cdt = torch.float32 if cpu else torch.bfloat16
 

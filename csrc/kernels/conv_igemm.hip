@@ -727,22 +727,63 @@ struct PrepArgs {
   // device-side data path (img != nullptr): gather + normalise the step's
   // batch straight from the HBM-resident uint8 dataset
   const uint8_t* img; const int* order; const int64_t* lab_all; int64_t* lab_out;
-  unsigned long long* ctr;  // [0] = step counter, [1] = arrival ticket
+  const unsigned long long* ctr;  // [0] = step counter (advanced by head_wgrad)
   int n_order, B;
   float mean[3], inv_std[3];
   const float* w1; bf16_t* w1p; int w1_cout, taps, w1_c, w1_cp;  // layer-1 pack
   int nt;                                                        // transposes
   const bf16_t* tw[4]; bf16_t* twt[4]; int tcout[4], tcin[4];
   int nb_pad, nb_pack, nb_t[4];
+  int quad;  // fast gather/pad path: one block per image, 4 pixels per thread
 };
 
 __global__ void __launch_bounds__(256) prep_step_kernel(const PrepArgs a) {
   __shared__ bf16_t t[32][33];
   int blk = blockIdx.x;
+  if (blk < a.nb_pad && a.quad) {
+    // fast path (3 -> 8 channels, W % 4 == 0): block = one image, thread =
+    // 4 consecutive pixels of one row; every load of a thread is issued
+    // before the first use (one dependent round trip for the sample index,
+    // one for the pixels) and the 4 padded pixels go out as 64 contiguous B
+    const int HW = a.H * a.W, Hp = a.H + 2 * a.sp, Wp = a.W + 2 * a.sp;
+    const int b = blk;
+    int smp = 0;
+    if (a.img) {
+      const unsigned long long step = *a.ctr;  // advanced by head_wgrad later in the step
+      const int pos = (int)((step * (unsigned long long)a.B + (unsigned long long)b) % (unsigned)a.n_order);
+      smp = a.order[pos];
+      if (threadIdx.x == 0) a.lab_out[b] = a.lab_all[smp];
+    }
+    for (int q4 = threadIdx.x; q4 < HW / 4; q4 += 256) {
+      const int r = q4 * 4, h = r / a.W, w = r - h * a.W;
+      float f[12];
+      if (a.img) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.img + ((int64_t)smp * HW + r) * 3);
+        const uint32_t d0 = src[0], d1 = src[1], d2 = src[2];
+        const uint32_t d[3] = {d0, d1, d2};
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+          const float u = (float)((d[k >> 2] >> (8 * (k & 3))) & 0xffu);
+          f[k] = (u * (1.0f / 255.0f) - a.mean[k % 3]) * a.inv_std[k % 3];
+        }
+      } else {
+        const uint2* src = reinterpret_cast<const uint2*>(a.x + ((int64_t)b * HW + r) * 3);
+        const uint2 e0 = src[0], e1 = src[1], e2 = src[2];
+        const uint32_t d[6] = {e0.x, e0.y, e1.x, e1.y, e2.x, e2.y};
+#pragma unroll
+        for (int k = 0; k < 12; ++k) f[k] = (k & 1) ? hi_bf16(d[k >> 1]) : lo_bf16(d[k >> 1]);
+      }
+      uint4* dst = reinterpret_cast<uint4*>(a.xp + (((int64_t)b * Hp + h + a.sp) * Wp + w + a.sp) * 8);
+#pragma unroll
+      for (int px = 0; px < 4; ++px)
+        dst[px] = make_uint4(pack_bf16x2(f[3 * px], f[3 * px + 1]), pack_bf16x2(f[3 * px + 2], 0.f), 0u, 0u);
+    }
+    return;
+  }
   if (blk < a.nb_pad) {
     const int HW = a.H * a.W, Hp = a.H + 2 * a.sp, Wp = a.W + 2 * a.sp;
-    unsigned long long step = 0;
-    if (a.img) step = __hip_atomic_load(a.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // step counter: advanced by head_wgrad later in the same step (stream order)
+    const unsigned long long step = a.img ? *a.ctr : 0ull;
     for (int p = blk * 256 + threadIdx.x; p < a.P; p += a.nb_pad * 256) {
       const int b = p / HW;
       const int r = p - b * HW, h = r / a.W, w = r - h * a.W;
@@ -763,19 +804,6 @@ __global__ void __launch_bounds__(256) prep_step_kernel(const PrepArgs a) {
       for (int c = 0; c < a.Cp; c += 8)
         *reinterpret_cast<uint4*>(a.xp + q * a.Cp + c) = *reinterpret_cast<const uint4*>(v + c);
     }
-    if (a.img) {
-      // the last gather block to finish advances the step counter: every
-      // block read it before its arrival (the read's value was consumed
-      // before the barrier), so no block of this step sees the new value
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        const unsigned long long n = atomicAdd(a.ctr + 1, 1ull);
-        if (n + 1 == (unsigned long long)a.nb_pad) {
-          a.ctr[1] = 0;
-          atomicAdd(a.ctr, 1ull);
-        }
-      }
-    }
     return;
   }
   blk -= a.nb_pad;
@@ -791,6 +819,37 @@ __global__ void __launch_bounds__(256) prep_step_kernel(const PrepArgs a) {
   for (int j = 0; j < a.nt; ++j) {
     if (blk >= a.nb_t[j]) { blk -= a.nb_t[j]; continue; }
     const int Cin = a.tcin[j], Cout = a.tcout[j], taps = a.taps;
+    if (Cin % 64 == 0 && Cout % 64 == 0) {
+      // 64 (co) x 64 (ci) tile of one tap through LDS, 16-byte loads and
+      // stores: in, 8 lanes sweep one 128-B weight row; out, the 64 lanes of
+      // a wave own 64 consecutive ci and each gathers 8 consecutive co
+      // (row stride 72 elements: the column reads are conflict-free).
+      __shared__ __attribute__((aligned(16))) bf16_t tt[64][72];
+      const int nci = Cin / 64, nco = Cout / 64;
+      const int tap = blk / (nci * nco);
+      const int r = blk % (nci * nco);
+      const int ci0 = (r % nci) * 64, co0 = (r / nci) * 64;
+      const bf16_t* src = a.tw[j];
+#pragma unroll
+      for (int q = threadIdx.x; q < 512; q += 256) {
+        const int row = q >> 3, ch = q & 7;
+        *reinterpret_cast<uint4*>(&tt[row][ch * 8]) =
+            *reinterpret_cast<const uint4*>(src + ((int64_t)(co0 + row) * taps + tap) * Cin + ci0 + ch * 8);
+      }
+      __syncthreads();
+      const int ftap = taps - 1 - tap;
+#pragma unroll
+      for (int q = threadIdx.x; q < 512; q += 256) {
+        const int ci = q & 63, ch = q >> 6;
+        uint32_t w4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          w4[e] = (uint32_t)tt[ch * 8 + 2 * e][ci] | ((uint32_t)tt[ch * 8 + 2 * e + 1][ci] << 16);
+        *reinterpret_cast<uint4*>(a.twt[j] + ((int64_t)(ci0 + ci) * taps + ftap) * Cout + co0 + ch * 8) =
+            make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      }
+      return;
+    }
     const int nci = (Cin + 31) / 32, nco = (Cout + 31) / 32;
     const int tap = blk / (nci * nco);
     const int r = blk % (nci * nco);
@@ -821,13 +880,15 @@ static void launch_prep(PrepArgs& a, int64_t P, uintptr_t w1, uintptr_t w1p, int
   a.nt = (int)tw.size();
   if (a.nt > 4 || twt.size() != tw.size() || tcout.size() != tw.size() || tcin.size() != tw.size())
     throw std::runtime_error("prep_step: up to 4 consistent transposes");
-  a.nb_pad = (int)std::min<int64_t>((P + 255) / 256, 1024);
+  a.quad = (a.C == 3 && a.Cp == 8 && P > 0 && a.W % 4 == 0) ? 1 : 0;
+  a.nb_pad = a.quad ? (int)(P / ((int64_t)a.H * a.W)) : (int)std::min<int64_t>((P + 255) / 256, 1024);
   a.nb_pack = (int)std::min<int64_t>(((int64_t)w1_cout * taps * w1_cp + 255) / 256, 256);
   int total = a.nb_pad + a.nb_pack;
   for (int j = 0; j < a.nt; ++j) {
     a.tw[j] = (const bf16_t*)tw[j]; a.twt[j] = (bf16_t*)twt[j];
     a.tcout[j] = tcout[j]; a.tcin[j] = tcin[j];
-    a.nb_t[j] = ((tcin[j] + 31) / 32) * ((tcout[j] + 31) / 32) * taps;
+    a.nb_t[j] = (tcin[j] % 64 == 0 && tcout[j] % 64 == 0) ? (tcin[j] / 64) * (tcout[j] / 64) * taps
+                                                          : ((tcin[j] + 31) / 32) * ((tcout[j] + 31) / 32) * taps;
     total += a.nb_t[j];
   }
   if (total == 0) return;
@@ -847,8 +908,8 @@ void prep_step(uintptr_t x, uintptr_t xp, int64_t P, int C, int Cp, int H, int W
 // Same launch with the step's input gathered on the device: batch b of step
 // s (= ctr[0]) is sample order[(s*B + b) mod n_order] of the uint8 NHWC
 // dataset `img`, normalised ((v/255 - mean)/std), channel- and spatially
-// padded into xp; its label goes to lab_out[b].  The last gather block
-// advances ctr[0], so a captured graph replays consecutive batches.
+// padded into xp; its label goes to lab_out[b].  head_wgrad advances ctr[0]
+// later in the step, so a captured graph replays consecutive batches.
 void prep_step_gather(uintptr_t img, uintptr_t order, uintptr_t lab_all, uintptr_t lab_out, uintptr_t ctr,
                       int n_order, int B, int C, std::vector<float> mean, std::vector<float> stdv, uintptr_t xp,
                       int Cp, int H, int W, int sp, uintptr_t w1, uintptr_t w1p, int w1_cout, int taps, int w1_c,
@@ -859,7 +920,7 @@ void prep_step_gather(uintptr_t img, uintptr_t order, uintptr_t lab_all, uintptr
   PrepArgs a{};
   a.xp = (bf16_t*)xp; a.C = C; a.Cp = Cp; a.H = H; a.W = W; a.sp = sp;
   a.img = (const uint8_t*)img; a.order = (const int*)order; a.lab_all = (const int64_t*)lab_all;
-  a.lab_out = (int64_t*)lab_out; a.ctr = (unsigned long long*)ctr; a.n_order = n_order; a.B = B;
+  a.lab_out = (int64_t*)lab_out; a.ctr = (const unsigned long long*)ctr; a.n_order = n_order; a.B = B;
   for (int c = 0; c < 3; ++c) {
     a.mean[c] = c < C ? mean[c] : 0.f;
     a.inv_std[c] = c < C ? 1.0f / stdv[c] : 1.f;

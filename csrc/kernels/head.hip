@@ -102,7 +102,8 @@ __global__ void __launch_bounds__(256) head_wgrad_kernel(const bf16_t* __restric
                                                          const float* __restrict__ dlogits,
                                                          const float* __restrict__ loss_b, int F, int B,
                                                          float* __restrict__ dw, float* __restrict__ db,
-                                                         float* __restrict__ loss, float* __restrict__ slot) {
+                                                         float* __restrict__ loss, float* __restrict__ slot,
+                                                         unsigned long long* __restrict__ step_ctr) {
   __shared__ float red[8][NC + 1][33];
   const int tid = threadIdx.x, col = tid & 31, grp = tid >> 5;
   const int nblk_cols = (F + 31) / 32;
@@ -154,6 +155,10 @@ __global__ void __launch_bounds__(256) head_wgrad_kernel(const bf16_t* __restric
         // replaces a per-step fill of the whole gradient buffer, every other
         // gradient element is overwritten by its producing kernel
         if (slot) *slot = 1.0f;
+        // device-side data path: the step's gather kernel (prep_step_gather)
+        // read the step counter; advance it here, one kernel boundary later
+        // (a plain read-modify-write by one lane, no arrival ticket)
+        if (step_ctr) *step_ctr += 1ull;
       }
     }
   }
@@ -170,11 +175,12 @@ void head_fwd_bwd(uintptr_t h, uintptr_t w, uintptr_t bias, uintptr_t labels, in
 }
 
 void head_wgrad(uintptr_t h, uintptr_t dlogits, uintptr_t loss_b, int F, int B, int NC, uintptr_t dw, uintptr_t db,
-                uintptr_t loss, uintptr_t slot, uintptr_t stream) {
+                uintptr_t loss, uintptr_t slot, uintptr_t step_ctr, uintptr_t stream) {
   if (NC != 10) throw std::runtime_error("head_wgrad: built for 10 classes");
   head_wgrad_kernel<10><<<(F + 31) / 32 + 1, 256, 0, as_stream(stream)>>>((const bf16_t*)h, (const float*)dlogits,
                                                                         (const float*)loss_b, F, B, (float*)dw,
-                                                                        (float*)db, (float*)loss, (float*)slot);
+                                                                        (float*)db, (float*)loss, (float*)slot,
+                                                                        (unsigned long long*)step_ctr);
   DL_HIP_CHECK(hipGetLastError());
 }
 

@@ -230,7 +230,7 @@ def test_head(C):
                    dlog.data_ptr(), lb.data_ptr(), dh.data_ptr(), _s())
     slot = torch.zeros(1, device=dev)
     C.head_wgrad(h.data_ptr(), dlog.data_ptr(), lb.data_ptr(), Fd, B, NC, dw.data_ptr(), db.data_ptr(),
-                 loss.data_ptr(), slot.data_ptr(), _s())
+                 loss.data_ptr(), slot.data_ptr(), 0, _s())
     assert float(slot) == 1.0
     hr = h.float().requires_grad_(True)
     wr = w.clone().requires_grad_(True)

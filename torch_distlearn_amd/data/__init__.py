@@ -193,7 +193,8 @@ class DeviceLoader:
     :class:`Batcher`) is uploaded ONCE per epoch as an int32 vector in HBM;
     a step's batch is then selected by a device-resident step counter and
     gathered + normalised + padded by the native executor's first kernel
-    (``prep_step_gather``), which also advances the counter.  A captured
+    (``prep_step_gather``); a later kernel of the same step advances the
+    counter.  A captured
     hipGraph therefore replays consecutive batches with no per-step host
     work and no host->device copies.  :meth:`step_done` keeps the host's
     count so that a new epoch's order is uploaded (outside the graph, in
@@ -211,7 +212,7 @@ class DeviceLoader:
         self.steps_per_epoch = max(1, int(self.sampler.size()) // self.batch)
         n = self.steps_per_epoch * self.batch
         self.order = torch.empty(n, dtype=torch.int32, device=ds.device)
-        self.ctr = torch.zeros(2, dtype=torch.int64, device=ds.device)  # [step, arrival ticket]
+        self.ctr = torch.zeros(2, dtype=torch.int64, device=ds.device)  # [step, reserved]
         self.labels_out = torch.empty(self.batch, dtype=torch.int64, device=ds.device)
         self._host_steps = 0
         self.epoch = 0

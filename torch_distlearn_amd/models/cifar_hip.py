@@ -240,8 +240,10 @@ class CifarHIPExecutor:
         C = self.C
         main, side = torch.cuda.current_stream(), self.side
         s, ss = main.cuda_stream, side.cuda_stream
+        ctr = 0
         if hasattr(x, "gather_args"):
             labels = x.labels_out
+            ctr = x.ctr.data_ptr()  # advanced by head_wgrad after the gather read it
         if labels.dtype != torch.int64:
             raise ValueError("labels must be int64")
         B = self._prep(x, s, with_transposes=not self.fork_transposes)
@@ -258,7 +260,7 @@ class CifarHIPExecutor:
                        self.loss_b.data_ptr(), self.dP[-1].data_ptr(), s)
         C.head_wgrad(self.p[-1].data_ptr(), self.dlogits.data_ptr(), self.loss_b.data_ptr(), self.feat, B,
                      self.nclass, self.g32[nfc].data_ptr(), self.g32[nfc + 1].data_ptr(), self.loss.data_ptr(),
-                     self.flat.slot.data_ptr(), s)
+                     self.flat.slot.data_ptr(), ctr, s)
         self._ready(nfc)
         self._ready(nfc + 1)
         if self.fork_transposes:
