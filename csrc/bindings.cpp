@@ -28,6 +28,10 @@ PYBIND11_MODULE(_C, m) {
   // ---- convnet kernels (MFMA implicit GEMM, BN/ReLU/pool, classifier head) ------
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_fwd_stat_rows", &conv_fwd_stat_rows);
+  m.def("set_conv_region", &set_conv_region);
+  m.def("set_conv_region_stages", &set_conv_region_stages);
+  m.def("set_conv_region_ablate", &set_conv_region_ablate);
+  m.def("set_conv_region_waves", &set_conv_region_waves);
   m.def("set_conv_stages", &set_conv_stages);
   m.def("set_conv_waves", &set_conv_waves);
   m.def("set_conv_debug", &set_conv_debug);

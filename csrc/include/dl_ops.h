@@ -30,6 +30,10 @@ void gather_normalize(uintptr_t images, uintptr_t idx, uintptr_t out, int B, int
 int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab, int B, int H, int W, int Cin,
              int Cout, int KS, int tile, int splits, uintptr_t stream);
 int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile, int splits);
+void set_conv_region(int on);
+void set_conv_region_stages(int st);
+void set_conv_region_ablate(int a);
+void set_conv_region_waves(int w);
 void set_conv_stages(int fwd, int wgrad);
 void set_conv_waves(int waves);
 void set_conv_debug(uintptr_t buf);

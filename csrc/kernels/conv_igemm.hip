@@ -158,7 +158,10 @@ __device__ __forceinline__ void wait_stages(int n) {
     case 0: wait_vmcnt<0>(); break;
     case 1: wait_vmcnt<LPS>(); break;
     case 2: wait_vmcnt<2 * LPS>(); break;
-    default: wait_vmcnt<3 * LPS>(); break;
+    case 3: wait_vmcnt<3 * LPS>(); break;
+    case 4: wait_vmcnt<(4 * LPS < 63 ? 4 * LPS : 63)>(); break;
+    case 5: wait_vmcnt<(5 * LPS < 63 ? 5 * LPS : 63)>(); break;
+    default: wait_vmcnt<(6 * LPS < 63 ? 6 * LPS : 63)>(); break;
   }
 }
 
@@ -166,6 +169,83 @@ __device__ __forceinline__ void block_sync_lds() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
+}
+
+// Forward / dgrad epilogue shared by the implicit-GEMM kernels: SLAB = fp32
+// split-K partials; else bf16 y (+ STATS: per-M-tile channel sum / sum of
+// squares of exactly the stored bf16 values, one deterministic partial row
+// per M tile, reduced through `smem`, which the caller no longer uses).
+template <int BM, int BN, bool STATS, bool SLAB, int WM, int WN>
+__device__ __forceinline__ void conv_fwd_epilogue(const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], const ConvGeom& g,
+                                                  bf16_t* __restrict__ y, float* __restrict__ stats,
+                                                  float* __restrict__ slab, int split, int tm, int m0, int n0,
+                                                  char* smem) {
+  constexpr int NT = 64 * WM * WN, TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = tid >> 6, wm = wid / WN, wn = wid % WN;
+  const int col_l = lane & 15, rq = lane >> 4;
+  if constexpr (SLAB) {
+    float* o = slab + (int64_t)split * g.M * g.Cout;
+#pragma unroll
+    for (int a = 0; a < FM; ++a)
+#pragma unroll
+      for (int b = 0; b < FN; ++b) {
+        const int n = n0 + wn * TN + b * 16 + col_l;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * TM + a * 16 + rq * 4 + r;
+          if (m < g.M && n < g.Cout) o[(int64_t)m * g.Cout + n] = acc[a][b][r];
+        }
+      }
+  } else {
+    float s1[FN], s2[FN];
+#pragma unroll
+    for (int b = 0; b < FN; ++b) { s1[b] = 0.f; s2[b] = 0.f; }
+#pragma unroll
+    for (int a = 0; a < FM; ++a) {
+#pragma unroll
+      for (int b = 0; b < FN; ++b) {
+        const int n = n0 + wn * TN + b * 16 + col_l;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * TM + a * 16 + rq * 4 + r;
+          const bf16_t hv = f32_to_bf16(acc[a][b][r]);
+          if (m < g.M && n < g.Cout) y[(int64_t)m * g.Cout + n] = hv;
+          if constexpr (STATS) {
+            const float v = m < g.M ? bf16_to_f32(hv) : 0.f;  // statistics of exactly what is stored
+            s1[b] += v;
+            s2[b] += v * v;
+          }
+        }
+      }
+    }
+    if constexpr (STATS) {
+      __syncthreads();  // every wave done with the LDS ring (no DMA in flight: the K loop drained it)
+      float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]
+#pragma unroll
+      for (int b = 0; b < FN; ++b) {
+        s1[b] += __shfl_xor(s1[b], 16, 64);
+        s1[b] += __shfl_xor(s1[b], 32, 64);
+        s2[b] += __shfl_xor(s2[b], 16, 64);
+        s2[b] += __shfl_xor(s2[b], 32, 64);
+        if (rq == 0) {
+          red[(wm * 2 + 0) * BN + wn * TN + b * 16 + col_l] = s1[b];
+          red[(wm * 2 + 1) * BN + wn * TN + b * 16 + col_l] = s2[b];
+        }
+      }
+      __syncthreads();
+      for (int c = tid; c < BN; c += NT) {
+        const int n = n0 + c;
+        if (n < g.Cout) {
+          float sa = 0.f, sb = 0.f;
+#pragma unroll
+          for (int q = 0; q < WM; ++q) { sa += red[(q * 2) * BN + c]; sb += red[(q * 2 + 1) * BN + c]; }
+          stats[(int64_t)tm * 2 * g.Cout + n] = sa;
+          stats[(int64_t)tm * 2 * g.Cout + g.Cout + n] = sb;
+        }
+      }
+    }
+  }
 }
 
 // --------------------------------------------------------------------------
@@ -361,72 +441,343 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
       d[0] = t_start; d[1] = t_setup; d[2] = t_loop; d[3] = stamp();
     }
   };
-  const int col_l = lane & 15, rq = lane >> 4;
-  if constexpr (SLAB) {
-    float* o = slab + (int64_t)split * g.M * g.Cout;
+  conv_fwd_epilogue<BM, BN, STATS, SLAB, WM, WN>(acc, g, y, stats, slab, split, tm, m0, n0, smem);
+  dbg_out();
+}
+
+// --------------------------------------------------------------------------
+// forward / dgrad implicit GEMM with the activation REGION resident in LDS
+// (tap reuse).  The generic kernel above streams the A operand tap by tap:
+// each of the KS*KS k-steps of a 64-channel chunk re-reads an almost
+// identical shifted window of the input through the L2 -> LDS path, which is
+// what bounds it (~25 B/clk/CU of LDS-DMA fill).  Here a workgroup's M tile
+// (BM = 128 output pixels = whole output rows of one image, or whole images)
+// loads the padded input pixels it touches ONCE per 64-channel chunk, and
+// every tap reads its A fragments from that region at a wave-uniform offset;
+// only the weight tile (B) is streamed per k-step (3-stage LDS-DMA ring).
+// Fill bytes per FLOP drop ~1.8-2.6x.
+//
+// Region image: pixel-major, S = 10 16-byte slots per pixel (8 data + 2 pad),
+// row stride RS = RW*S + RP slots, image stride IS = RH*RS (host-chosen, see
+// region_geom): with these paddings the ds_read_b128 fragment reads of 16
+// output pixels are bank-conflict free for W = 4, 8, 16, 32 at every tap,
+// and a tap is a plain address offset (no per-tap swizzle arithmetic).
+// Pad slots are loaded from an out-of-range offset (zeros, no traffic).
+// --------------------------------------------------------------------------
+struct RegionGeom {
+  int S, RS, IS;    // slots per pixel / region row / region image
+  int RW, RH;       // region row width (= Wp) and rows per region image
+  int nimg;         // images per region (rows mode: 1)
+  int rows_mode;    // 1: M tile = BM/W output rows of one image; 0: BM/HW whole images
+  int nslot;        // slots per region (multiple of 64)
+  int cpw;          // 64-channel chunks per workgroup (1 or 2)
+  float inv_S, inv_RS, inv_IS;  // exact slot -> (img,row,col,chunk) decomposition (slots < 2^16)
+};
+
+// Inclusive sum over the 16 lanes of each DPP row: lane 15 of the row ends
+// with the row total (row_shr 1, 2, 4, 8 with zero fill; fixed order).
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x112, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x114, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x118, 0xf, 0xf, true));
+  return v;
+}
+
+// Epilogue of the region kernel.  Its MFMAs compute C^T (weights as the A
+// operand), so lane l holds, per 16-pixel M fragment a and N-fragment pair
+// p, the 8 CONSECUTIVE channels n0 + wn*TN + 32p + 8*(l>>4) + 0..7 of pixel
+// m0 + wm*TM + 16a + (l&15) (fragments 2p / 2p+1 hold channel quads 0..3 /
+// 4..7, see the B row map): one 16-byte bf16 store (or two 16-byte fp32
+// slab stores) per (a, p) instead of 8 scattered 2-byte stores.  BN
+// statistics: DPP row sums over the 16 pixels of a lane group, then a
+// fixed-order sum over the WM wave rows through LDS (deterministic).
+template <int BN, bool STATS, bool SLAB, int WM, int WN, int FM, int FN>
+__device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], const ConvGeom& g,
+                                                    bf16_t* __restrict__ y, float* __restrict__ stats,
+                                                    float* __restrict__ slab, int split, int tm, int m0, int n0,
+                                                    char* smem) {
+  constexpr int NT = 64 * WM * WN, TM = 128 / WM, TN = BN / WN, NP = FN / 2;
+  static_assert(FN % 2 == 0, "N fragments pair up");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = tid >> 6, wm = wid / WN, wn = wid % WN;
+  const int nl = wn * TN + 8 * (lane >> 4);  // + 32p: local channel of the lane's 8-run
+  float s1[NP][8], s2[NP][8];
 #pragma unroll
-    for (int a = 0; a < FM; ++a)
+  for (int q = 0; q < NP; ++q)
 #pragma unroll
-      for (int b = 0; b < FN; ++b) {
-        const int n = n0 + wn * TN + b * 16 + col_l;
+    for (int k = 0; k < 8; ++k) { s1[q][k] = 0.f; s2[q][k] = 0.f; }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm * TM + a * 16 + rq * 4 + r;
-          if (m < g.M && n < g.Cout) o[(int64_t)m * g.Cout + n] = acc[a][b][r];
+  for (int a = 0; a < FM; ++a) {
+    const int m = m0 + wm * TM + a * 16 + (lane & 15);
+    const bool ok = m < g.M;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const int n = n0 + nl + 32 * q;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[j] = acc[a][2 * q][j]; v[4 + j] = acc[a][2 * q + 1][j]; }
+      if constexpr (SLAB) {
+        float* o = slab + ((int64_t)split * g.M + m) * g.Cout + n;
+        if (ok) {
+          *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
         }
-      }
-    dbg_out();
-    return;
-  } else {
-    float s1[FN], s2[FN];
+      } else {
+        const uint4 pk = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                                    pack_bf16x2(v[6], v[7]));
+        if (ok) *reinterpret_cast<uint4*>(y + (int64_t)m * g.Cout + n) = pk;
+        if constexpr (STATS) {
+          const float h[8] = {lo_bf16(pk.x), hi_bf16(pk.x), lo_bf16(pk.y), hi_bf16(pk.y),
+                              lo_bf16(pk.z), hi_bf16(pk.z), lo_bf16(pk.w), hi_bf16(pk.w)};
 #pragma unroll
-    for (int b = 0; b < FN; ++b) { s1[b] = 0.f; s2[b] = 0.f; }
-#pragma unroll
-    for (int a = 0; a < FM; ++a) {
-#pragma unroll
-      for (int b = 0; b < FN; ++b) {
-        const int n = n0 + wn * TN + b * 16 + col_l;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm * TM + a * 16 + rq * 4 + r;
-          const bf16_t hv = f32_to_bf16(acc[a][b][r]);
-          if (m < g.M && n < g.Cout) y[(int64_t)m * g.Cout + n] = hv;
-          if constexpr (STATS) {
-            const float v = m < g.M ? bf16_to_f32(hv) : 0.f;  // statistics of exactly what is stored
-            s1[b] += v;
-            s2[b] += v * v;
+          for (int k = 0; k < 8; ++k) {  // statistics of exactly what is stored
+            const float hv = ok ? h[k] : 0.f;
+            s1[q][k] += hv;
+            s2[q][k] += hv * hv;
           }
         }
       }
     }
-    if constexpr (STATS) {
-      __syncthreads();  // every wave done with the LDS ring (no DMA in flight: nk loop drained it)
-      float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]
+  }
+  if constexpr (STATS && !SLAB) {
 #pragma unroll
-      for (int b = 0; b < FN; ++b) {
-        s1[b] += __shfl_xor(s1[b], 16, 64);
-        s1[b] += __shfl_xor(s1[b], 32, 64);
-        s2[b] += __shfl_xor(s2[b], 16, 64);
-        s2[b] += __shfl_xor(s2[b], 32, 64);
-        if (rq == 0) {
-          red[(wm * 2 + 0) * BN + wn * TN + b * 16 + col_l] = s1[b];
-          red[(wm * 2 + 1) * BN + wn * TN + b * 16 + col_l] = s2[b];
-        }
-      }
-      __syncthreads();
-      for (int c = tid; c < BN; c += NT) {
-        const int n = n0 + c;
-        if (n < g.Cout) {
-          float sa = 0.f, sb = 0.f;
+    for (int q = 0; q < NP; ++q)
 #pragma unroll
-          for (int q = 0; q < WM; ++q) { sa += red[(q * 2) * BN + c]; sb += red[(q * 2 + 1) * BN + c]; }
-          stats[(int64_t)tm * 2 * g.Cout + n] = sa;
-          stats[(int64_t)tm * 2 * g.Cout + g.Cout + n] = sb;
+      for (int k = 0; k < 8; ++k) { s1[q][k] = row16_sum(s1[q][k]); s2[q][k] = row16_sum(s2[q][k]); }
+    __syncthreads();  // every wave done with the LDS ring and region
+    float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]
+    if ((lane & 15) == 15) {
+#pragma unroll
+      for (int q = 0; q < NP; ++q)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          red[(wm * 2 + 0) * BN + nl + 32 * q + k] = s1[q][k];
+          red[(wm * 2 + 1) * BN + nl + 32 * q + k] = s2[q][k];
         }
-      }
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      float sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int q = 0; q < WM; ++q) { sa += red[(q * 2) * BN + c]; sb += red[(q * 2 + 1) * BN + c]; }
+      stats[(int64_t)tm * 2 * g.Cout + n0 + c] = sa;
+      stats[(int64_t)tm * 2 * g.Cout + g.Cout + n0 + c] = sb;
     }
   }
-  dbg_out();
+}
+
+// B-tile chunk swizzle of the region kernel: conflict-free ds_read_b128 for
+// its permuted fragment rows 8(i>>2) + 4b + (i&3) (and for identity rows)
+__device__ __forceinline__ int swz_b(int row) { return ((row >> 1) ^ (row >> 3)) & 7; }
+
+template <int BN, bool STATS, bool SLAB, int STAGES, int WM, int WN>
+__global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf16_t* __restrict__ x,
+                                                              const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
+                                                              float* __restrict__ stats, float* __restrict__ slab,
+                                                              const ConvGeom g, const RegionGeom rg, int splits,
+                                                              unsigned long long* dbg, int ablate) {
+  const unsigned long long t_start = dbg ? stamp() : 0ull;
+  constexpr int BM = 128, BK = 64, CPR = 8, NW = WM * WN, PD = STAGES - 1;
+  constexpr int B_BYTES = BN * BK * 2, B_INS = B_BYTES / 1024 / NW, LPS = B_INS;
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  static_assert(B_INS >= 1 && B_INS * NW * 1024 == B_BYTES, "B DMA split");
+  static_assert(FN % 2 == 0, "the 16-byte epilogue pairs N fragments");
+  static_assert(STAGES >= 3, "fragment prefetch needs >= 3 ring slots");
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int region_bytes = rg.nslot * 16;
+  char* sR = smem;                          // cpw region images
+  char* sB = smem + rg.cpw * region_bytes;  // B ring
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int ntm = (g.M + BM - 1) / BM;
+  const int id = xcd_swizzle(blockIdx.x, ntm * (g.Cout / BN) * splits);
+  const int tm = id % ntm;
+  const int panel = id / ntm;
+  const int split = panel % splits, tn = panel / splits;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int HW = 1 << g.logHW, Wd = g.W;
+  const int HpWp = g.Hp * g.Wp;
+  const int taps = g.KS * g.KS;
+  const int nk = rg.cpw * taps;
+  const int img0 = m0 >> g.logHW, oh0 = (m0 & (HW - 1)) >> g.logW;  // oh0 = 0 in images mode
+  const int start_pix = img0 * HpWp + oh0 * g.Wp;
+  const rsrc_t xr = make_rsrc(x, (unsigned)((int64_t)g.B * HpWp * g.Cin * 2));
+  const rsrc_t wr = make_rsrc(w, (unsigned)((int64_t)g.Cout * g.K * 2));
+  const int cbase = split * rg.cpw;  // first 64-channel chunk of this workgroup
+
+  // ---- region loads (once per chunk): lane-linear slots -> source pixel/chunk
+  {
+    const int nq = rg.nslot >> 6;
+    // slot -> (region row R, pixel in row, chunk): the region's image rows
+    // are consecutive padded rows (rows mode: RH rows of one image; images
+    // mode: RH = Hp, whole images), so the source pixel is start + R*Wp + col
+    const int nrows = rg.nimg * rg.RH;
+    for (int q = wid; q < nq; q += NW) {
+      const int sl = q * 64 + lane;
+      const int R = (int)(((float)sl + 0.5f) * rg.inv_RS);
+      const int r2 = sl - R * rg.RS;
+      const int col = (r2 * 6554) >> 16;  // r2 / 10 (exact for r2 < 16384; S == 10)
+      const int ch = r2 - col * 10;
+      const bool ok = R < nrows && col < rg.RW && ch < 8;
+      const int pix = start_pix + R * g.Wp + col;
+      const unsigned voff = ok ? 2u * (unsigned)(pix * g.Cin + ch * 8) : kOOB;
+      for (int c = 0; c < rg.cpw; ++c)
+        blds16(xr, voff, 2u * (unsigned)((cbase + c) * 64), sR + c * region_bytes + q * 1024);
+    }
+  }
+  // ---- B (weight) stream: k-step ks = (chunk c, tap t): k offset t*Cin + (cbase+c)*64
+  int b_v[B_INS];
+#pragma unroll
+  for (int j = 0; j < B_INS; ++j) {
+    const int row = 8 * (wid * B_INS + j) + (lane >> 3);
+    const int ch = (lane & 7) ^ swz_b(row);
+    b_v[j] = 2 * ((n0 + row) * g.K + ch * 8);
+  }
+  int ld_c = 0, ld_t = 0, ld_slot = 0;  // next k-step to load (wave-uniform)
+  // Every step issues its DMA unconditionally (k-steps past the end load
+  // zeros from an out-of-range offset into a slot nobody reads again), so the
+  // number of loads in flight is the same at every wait and the loop body is
+  // one basic block the scheduler can interleave.
+  auto issue_b = [&](int q, bool live) {
+    const unsigned soff = 2u * (unsigned)(ld_t * g.Cin + (cbase + ld_c) * 64);
+    blds16(wr, live ? (unsigned)b_v[q] : kOOB, soff, sB + ld_slot * B_BYTES + (wid * B_INS + q) * 1024);
+  };
+  int ld_k = 0;
+  auto advance_ld = [&]() {  // branch-free (keeps the step one basic block)
+    ++ld_k;
+    ++ld_t;
+    const int wrap = ld_t == taps;
+    ld_t -= wrap * taps;
+    ld_c = min(ld_c + wrap, rg.cpw - 1);
+    ++ld_slot;
+    ld_slot -= (ld_slot == STAGES) * STAGES;
+  };
+
+  // ---- per-lane A fragment bases (slot of the tap-(0,0) pixel + lane's chunk)
+  int a_base[FM];
+#pragma unroll
+  for (int a = 0; a < FM; ++a) {
+    const int m = min(m0 + wm * TM + a * 16 + (lane & 15), g.M - 1);
+    const int im = (m >> g.logHW) - img0;
+    const int oh = ((m & (HW - 1)) >> g.logW) - oh0;
+    const int ow = m & (Wd - 1);
+    a_base[a] = (im * rg.IS + oh * rg.RS + ow * rg.S + (lane >> 4)) * 16;
+  }
+  // B fragment rows: N fragment b, MFMA row i -> channel
+  // 32*(b>>1) + 8*(i>>2) + 4*(b&1) + (i&3) of the wave's TN channels (so a
+  // lane's fragments 2p, 2p+1 cover 8 consecutive channels of the
+  // transposed accumulator)
+  int b_row[FN];
+#pragma unroll
+  for (int b = 0; b < FN; ++b) {
+    const int i = lane & 15;
+    b_row[b] = wn * TN + 32 * (b >> 1) + 8 * (i >> 2) + 4 * (b & 1) + (i & 3);
+  }
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: region + PD B stages in flight
+#pragma unroll
+  for (int p = 0; p < PD; ++p) {
+#pragma unroll
+    for (int q = 0; q < LPS; ++q) issue_b(q, ld_k < nk);
+    advance_ld();
+  }
+  const unsigned long long t_issued = dbg ? stamp() : 0ull;
+
+  // fragment reads of k-step (rc, rkh, rkw) from ring slot rslot
+  int rc = 0, rkh = 0, rkw = 0, rslot = 0;
+  auto read_frags = [&](bf16x8 (&fa)[BK / 32][FM], bf16x8 (&fb)[BK / 32][FN]) {
+    const char* As = sR + rc * region_bytes + (rkh * rg.RS + rkw * rg.S) * 16;  // wave-uniform tap offset
+    const uint4* Bs = reinterpret_cast<const uint4*>(sB + rslot * B_BYTES);
+    {  // advance the read state, branch-free
+      ++rkw;
+      const int ww = rkw == g.KS;
+      rkw -= ww * g.KS;
+      rkh += ww;
+      const int wh = rkh == g.KS;
+      rkh -= wh * g.KS;
+      rc = min(rc + wh, rg.cpw - 1);
+      ++rslot;
+      rslot -= (rslot == STAGES) * STAGES;
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int ch = kk * 4 + (lane >> 4);
+#pragma unroll
+      for (int b = 0; b < FN; ++b) fb[kk][b] = __builtin_bit_cast(bf16x8, Bs[b_row[b] * CPR + (ch ^ swz_b(b_row[b]))]);
+#pragma unroll
+      for (int a = 0; a < FM; ++a) fa[kk][a] = *reinterpret_cast<const bf16x8*>(As + a_base[a] + kk * 64);
+    }
+  };
+  // Step i: [wait stage i+1, barrier] -> prefetch fragments of step i+1 ->
+  // MFMAs of step i (C^T += W * X^T) with the DMA of stage i+PD (into the
+  // slot read two steps ago), reads and MFMAs interleaved 1:1 so that a
+  // read stalled on a full LDS queue never holds back more than one MFMA.
+  constexpr int NRD = (BK / 32) * (FM + FN);  // fragment reads per step
+  constexpr int NMF = (BK / 32) * FM * FN;    // MFMAs per step
+  bf16x8 fa0[BK / 32][FM], fb0[BK / 32][FN], fa1[BK / 32][FM], fb1[BK / 32][FN];
+  wait_vmcnt<(PD - 1) * LPS>();  // region + stage 0 landed
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned long long t_first = dbg ? stamp() : 0ull;
+  read_frags(fa0, fb0);
+  auto step = [&](bf16x8 (&fca)[BK / 32][FM], bf16x8 (&fcb)[BK / 32][FN], bf16x8 (&fna)[BK / 32][FM],
+                  bf16x8 (&fnb)[BK / 32][FN]) {
+    wait_vmcnt<(PD - 2) * LPS>();  // stage i+1 landed (stages i+2 .. i+PD-1 may fly)
+    // The fragments of step i must be in registers: the builtin wait is seen
+    // by the compiler's waitcnt pass (an inline-asm one is not, and it would
+    // then wait lgkmcnt(0) at the first MFMA, i.e. also for the prefetch).
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();        // stage i+1 visible to all waves; slot of step i-1 fully read
+    __builtin_amdgcn_sched_barrier(0);
+    const bool live = ld_k < nk;
+    read_frags(fna, fnb);
+#pragma unroll
+    for (int q = 0; q < LPS; ++q) issue_b(q, live);
+    advance_ld();
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk)
+#pragma unroll
+      for (int a = 0; a < FM; ++a)
+#pragma unroll
+        for (int b = 0; b < FN; ++b) acc[a][b] = mfma16(fcb[kk][b], fca[kk][a], acc[a][b]);
+    // issue order: (MFMA, read) pairs, leftover reads, (MFMA, DMA) pairs, the rest
+    constexpr int P1 = NRD < NMF ? NRD : NMF;
+    constexpr int P2 = LPS < NMF - P1 ? LPS : NMF - P1;
+#pragma unroll
+    for (int q = 0; q < P1; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    if constexpr (NRD > P1) __builtin_amdgcn_sched_group_barrier(0x100, NRD - P1, 0);
+#pragma unroll
+    for (int q = 0; q < LPS; ++q) {
+      if (q < P2) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    }
+    if constexpr (NMF - P1 - P2 > 0) __builtin_amdgcn_sched_group_barrier(0x008, NMF - P1 - P2, 0);
+  };
+  int i = 0;
+  for (; i + 1 < nk; i += 2) {
+    step(fa0, fb0, fa1, fb1);
+    step(fa1, fb1, fa0, fb0);
+  }
+  if (i < nk) step(fa0, fb0, fa1, fb1);
+  const unsigned long long t_loop = dbg ? stamp() : 0ull;
+  conv_fwd_epilogue_t<BN, STATS, SLAB, WM, WN, FM, FN>(acc, g, y, stats, slab, split, tm, m0, n0, smem);
+  if (dbg && threadIdx.x == 0) {
+    unsigned long long* d = dbg + (size_t)blockIdx.x * 5;
+    d[0] = t_start; d[1] = t_issued; d[2] = t_first; d[3] = t_loop; d[4] = stamp();
+  }
 }
 
 // split-K combine: y = bf16(sum_s slab[s]) (+ BN partial sums, one row per block)
@@ -1011,6 +1362,104 @@ static void launch_fwd(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y,
   }
 }
 
+// ---- tap-reuse (LDS-resident region) forward path --------------------------
+// set_conv_region(0) forces the streaming kernel (A/B); 1 = region kernel
+// for row tiles (H*W % 128 == 0), 2 = also for whole-image tiles.  Measured
+// (MI355X, batch 128, rocprofv3): rows mode wins (conv2 fwd 19.3 -> 17.7 us,
+// dgrad 22.8 -> 20.5 us); images mode loses (conv3/conv4 21-25 vs 19.7 us:
+// the 4x4/8x8 outputs need 8x8/12x12 padded inputs, the region fill does not
+// amortise over 25 k-steps), so it is off by default.
+static int g_region = 1, g_region_images = 0;
+void set_conv_region(int on) {
+  g_region = on ? 1 : 0;
+  g_region_images = on >= 2 ? 1 : 0;
+}
+
+// Region geometry for a BM = 128 tile, or false if the shape does not fit the
+// region kernel (then the streaming kernel runs).
+static bool region_geom(const ConvGeom& g, int BN, int splits, RegionGeom& rg) {
+  constexpr int BM = 128, STAGES = 3;
+  if (!g_region || g.Cin % 64 != 0 || g.W > BM || BM % g.W != 0) return false;
+  const int HW = g.H * g.W;
+  const int chunks = g.Cin / 64;
+  if (chunks % splits != 0) return false;
+  rg.cpw = chunks / splits;
+  if (rg.cpw > 2) return false;
+  rg.S = 10;  // the kernel's region loader divides by 10 with a multiply
+  rg.RW = g.Wp;
+  if (HW % BM == 0) {  // M tile = BM / W whole output rows of one image
+    rg.rows_mode = 1;
+    rg.nimg = 1;
+    rg.RH = BM / g.W + g.KS - 1;
+    rg.RS = rg.RW * rg.S;
+  } else if (BM % HW == 0 && g_region_images) {  // M tile = BM / HW whole images
+    rg.rows_mode = 0;
+    rg.nimg = BM / HW;
+    rg.RH = g.Hp;
+    rg.RS = rg.RW * rg.S + 8;  // + 8 slots per region row: conflict-free fragment reads across rows
+  } else {
+    return false;
+  }
+  rg.IS = rg.RH * rg.RS;
+  rg.nslot = (rg.nimg * rg.IS + 63) / 64 * 64;
+  if (rg.RS >= 16384) return false;
+  if (rg.nslot >= (1 << 16)) return false;
+  rg.inv_S = 1.0f / rg.S;
+  rg.inv_RS = 1.0f / rg.RS;
+  rg.inv_IS = 1.0f / rg.IS;
+  const int lds = rg.cpw * rg.nslot * 16 + STAGES * BN * 64 * 2;  // at least a 3-stage B ring
+  return lds <= 160 * 1024;
+}
+
+static int g_region_waves = 8;  // 8: 2 waves per SIMD; 4: one wave per SIMD with 2x wider wave tiles
+void set_conv_region_waves(int w) {
+  if (w != 4 && w != 8) throw std::runtime_error("region waves must be 4 or 8");
+  g_region_waves = w;
+}
+static int g_region_ablate = 0;  // debug: bit 0 = no in-loop weight DMA, bit 1 = no MFMAs
+void set_conv_region_ablate(int a) { g_region_ablate = a; }
+static int g_region_stages = 0;  // 0 = as many B stages as the LDS holds (max 8)
+void set_conv_region_stages(int st) { g_region_stages = st; }
+
+template <int BN, int WM, int WN, int ST>
+static void launch_fwd_region_st(const ConvGeom& g, const RegionGeom& rg, uintptr_t x, uintptr_t w, uintptr_t y,
+                                 uintptr_t stats, uintptr_t slab, int splits, hipStream_t s) {
+  const int ntm = (g.M + 127) / 128;
+  const int grid = ntm * (g.Cout / BN) * splits;
+  const size_t lds = (size_t)rg.cpw * rg.nslot * 16 + ST * BN * 64 * 2;
+  auto go = [&](auto kern, bf16_t* yy, float* st, float* sl) {
+    static bool attr = false;  // per instantiation: allow > 64 KiB of dynamic LDS
+    if (!attr) {
+      DL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      attr = true;
+    }
+    kern<<<grid, 64 * WM * WN, lds, s>>>((const bf16_t*)x, (const bf16_t*)w, yy, st, sl, g, rg, splits, g_conv_dbg,
+                                         g_region_ablate);
+  };
+  if (splits > 1)
+    go(conv_fwd_region_kernel<BN, false, true, ST, WM, WN>, nullptr, nullptr, (float*)slab);
+  else if (stats)
+    go(conv_fwd_region_kernel<BN, true, false, ST, WM, WN>, (bf16_t*)y, (float*)stats, nullptr);
+  else
+    go(conv_fwd_region_kernel<BN, false, false, ST, WM, WN>, (bf16_t*)y, nullptr, nullptr);
+}
+
+// The LDS-DMA issue -> landed latency is ~1.1 us while a k-step computes in
+// ~0.2 us: the B ring must keep ~5 k-steps in flight, so it takes every
+// stage the LDS has left after the region.
+template <int BN, int WM, int WN>
+static void launch_fwd_region(const ConvGeom& g, const RegionGeom& rg, uintptr_t x, uintptr_t w, uintptr_t y,
+                              uintptr_t stats, uintptr_t slab, int splits, hipStream_t s) {
+  const int free_b = 160 * 1024 - rg.cpw * rg.nslot * 16;
+  int st = std::min(8, free_b / (BN * 64 * 2));
+  if (g_region_stages > 0) st = std::min(st, g_region_stages);
+  if (st >= 8) launch_fwd_region_st<BN, WM, WN, 8>(g, rg, x, w, y, stats, slab, splits, s);
+  else if (st >= 6) launch_fwd_region_st<BN, WM, WN, 6>(g, rg, x, w, y, stats, slab, splits, s);
+  else if (st >= 5) launch_fwd_region_st<BN, WM, WN, 5>(g, rg, x, w, y, stats, slab, splits, s);
+  else if (st >= 4) launch_fwd_region_st<BN, WM, WN, 4>(g, rg, x, w, y, stats, slab, splits, s);
+  else launch_fwd_region_st<BN, WM, WN, 3>(g, rg, x, w, y, stats, slab, splits, s);
+}
+
 // tile: 0 = 128x128, 1 = 64x64, 2 = 128x64 (BM x BN, BK = 64).  splits > 1:
 // split-K into `slab` (fp32 [splits][M][Cout]) + combine (bf16 y, BN partials).
 // Returns the number of BN partial rows written to `stats` (if non-null).
@@ -1023,7 +1472,15 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
   if (Cout % 8 != 0) throw std::runtime_error("conv_fwd: Cout % 8 != 0");
   if (tile < 0 || tile > 2) throw std::runtime_error("conv_fwd: bad tile id");
   if (Cout % fwd_bn(tile) != 0) throw std::runtime_error("conv_fwd: Cout must be a multiple of the N tile");
-  if (tile == 0) launch_fwd<128, 128>(g, x, w, y, stats, slab, splits, s);
+  RegionGeom rg;
+  if (tile == 0 && region_geom(g, 128, splits, rg)) {
+    if (g_region_waves == 4) launch_fwd_region<128, 2, 2>(g, rg, x, w, y, stats, slab, splits, s);
+    else launch_fwd_region<128, 2, 4>(g, rg, x, w, y, stats, slab, splits, s);
+  } else if (tile == 2 && region_geom(g, 64, splits, rg)) {
+    if (g_region_waves == 4) launch_fwd_region<64, 2, 2>(g, rg, x, w, y, stats, slab, splits, s);
+    else launch_fwd_region<64, 4, 2>(g, rg, x, w, y, stats, slab, splits, s);
+  }
+  else if (tile == 0) launch_fwd<128, 128>(g, x, w, y, stats, slab, splits, s);
   else if (tile == 1) launch_fwd<64, 64>(g, x, w, y, stats, slab, splits, s);
   else if (tile == 2) launch_fwd<128, 64>(g, x, w, y, stats, slab, splits, s);
   else throw std::runtime_error("conv_fwd: bad tile id");

@@ -22,12 +22,18 @@ def main():
     ap.add_argument("--stages", default="3,3", help="fwd,wgrad LDS ring depth")
     ap.add_argument("--wtile", type=int, default=-1, help="override the wgrad tile (0 128x64, 1 64x64, 2 128x128)")
     ap.add_argument("--waves", type=int, default=8, help="waves per workgroup of the fwd/dgrad kernel (4 or 8)")
+    ap.add_argument("--region", type=int, default=1, help="1: tap-reuse (LDS-resident region) fwd/dgrad kernel")
+    ap.add_argument("--rstages", type=int, default=0, help="region kernel B-ring stages (0 = max that fits)")
+    ap.add_argument("--rwaves", type=int, default=8, help="region kernel waves per workgroup (4 or 8)")
     a = ap.parse_args()
     C = _native.native()
     fs, ws = (int(v) for v in a.stages.split(","))
     C.set_conv_stages(fs, ws)
     C.set_conv_waves(a.waves)
-    print(f"# stages fwd={fs} wgrad={ws}")
+    C.set_conv_region(a.region)
+    C.set_conv_region_stages(a.rstages)
+    C.set_conv_region_waves(a.rwaves)
+    print(f"# stages fwd={fs} wgrad={ws} region={a.region}")
     dev = torch.device("cuda")
     def cur():  # current-stream handle at call time (graph capture switches streams)
         return torch.cuda.current_stream().cuda_stream

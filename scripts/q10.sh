@@ -1,0 +1,7 @@
+set -o pipefail
+C=tests/kernels/test_convnet_gpu.py
+timeout -k 5 300 python -u -m pytest $C -x -q --timeout 120 --timeout-method thread -k "fwd or dgrad" > gpurun_out/t_conv.log 2>&1; rc=$?; tail -2 gpurun_out/t_conv.log
+[ $rc -ne 0 ] && exit 1
+rm -f gpurun_out/stamps.txt
+for wv in 8 4; do for L in 2 4; do timeout -k 5 60 python scripts/stamp_region.py $L fwd 0 0 $wv >> gpurun_out/stamps.txt 2>&1 || exit 1; done; done
+for wv in 8 4; do timeout -k 5 120 python scripts/bench_conv.py --iters 100 --region 1 --rwaves $wv > gpurun_out/bc_w$wv.txt 2>&1 || exit 1; done

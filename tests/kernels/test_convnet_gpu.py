@@ -38,8 +38,12 @@ _TILE_BN = {0: 128, 1: 64, 2: 64}
 
 @pytest.mark.parametrize("shape", CONV_SHAPES)
 @pytest.mark.parametrize("tile", [0, 1, 2])
-@pytest.mark.parametrize("splits", [1, 3])
-def test_conv_fwd_and_stats(C, shape, tile, splits):
+@pytest.mark.parametrize("splits", [1, 2, 3, 4])
+@pytest.mark.parametrize("region", [2, 1, 0])
+def test_conv_fwd_and_stats(C, shape, tile, splits, region):
+    """region=1/2: the tap-reuse kernel where the shape allows it (row tiles /
+    also whole-image tiles; else the streaming kernel runs anyway); region=0
+    forces the streaming kernel."""
     B, H, cin, cout = shape
     if splits > 1 and 256 % (cout // 8) != 0:
         pytest.skip("split-K combine needs Cout/8 | 256")
@@ -54,8 +58,12 @@ def test_conv_fwd_and_stats(C, shape, tile, splits):
     stats = torch.full((rows, 2, cout), float("nan"), device=dev)
     slab = torch.empty(splits * B * H * H * cout, device=dev)
     xp = _pad(x)
-    T = C.conv_fwd(xp.data_ptr(), w.data_ptr(), y.data_ptr(), stats.data_ptr(), slab.data_ptr(), B, H, H, cin, cout,
-                   5, tile, splits, _s())
+    C.set_conv_region(region)
+    try:
+        T = C.conv_fwd(xp.data_ptr(), w.data_ptr(), y.data_ptr(), stats.data_ptr(), slab.data_ptr(), B, H, H, cin,
+                       cout, 5, tile, splits, _s())
+    finally:
+        C.set_conv_region(1)
     assert T == rows
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=2).permute(0, 2, 3, 1)
     torch.cuda.synchronize()
@@ -86,15 +94,20 @@ def test_conv_dgrad_wgrad(C, shape):
     assert torch.equal(wt, w.permute(3, 1, 2, 0).flip(1, 2).contiguous())
     dyp = _pad(dy)
     if cout & (cout - 1) == 0:  # dgrad input channels (= Cout) must be a power of two
-        for tile, splits in ((1, 1), (0, 2), (2, 4)):
+        for tile, splits in ((1, 1), (0, 2), (2, 4), (0, 1), (2, 1), (0, 4), (0, 8)):
             dx = torch.empty(B, H, H, cin, dtype=torch.bfloat16, device=dev)
             slab = torch.empty(splits * B * H * H * cin, device=dev)
             if (splits > 1 and 256 % (cin // 8) != 0) or cin % _TILE_BN[tile] != 0:
                 continue
-            C.conv_fwd(dyp.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, slab.data_ptr(), B, H, H, cout, cin, 5, tile,
-                       splits, _s())
-            torch.cuda.synchronize()
-            assert _rel(dx, dx_ref) < 8e-3, (tile, splits)
+            for region in (2, 0):
+                C.set_conv_region(region)
+                try:
+                    C.conv_fwd(dyp.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, slab.data_ptr(), B, H, H, cout, cin,
+                               5, tile, splits, _s())
+                finally:
+                    C.set_conv_region(1)
+                torch.cuda.synchronize()
+                assert _rel(dx, dx_ref) < 8e-3, (tile, splits, region)
     K = 25 * cin
     xp = _pad(x)
     for tile in (0, 1, 2):
