@@ -841,7 +841,7 @@ __global__ void __launch_bounds__(256) splitk_combine_kernel(const float* __rest
 // Tiles are staged [m][col] (rows = the reduction index) by LDS-DMA and read
 // as MFMA operands with ds_read_b64_tr_b16.  BK = 64 rows of m per stage.
 // --------------------------------------------------------------------------
-template <int BM, int BN, int STAGES, int WM = 2, int WN = 2>
+template <int BM, int BN, int STAGES, int WM = 2, int WN = 2, bool PF = true>
 __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                          float* __restrict__ out, const ConvGeom g, int m_per_split,
                                                          int ldo) {
@@ -909,6 +909,9 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
 #pragma unroll
   for (int j = 0; j < B_INS; ++j) b_v[j] = b_kok[j] ? 2u * (unsigned)b_off[j] : kOOB;
 
+  // One stage's LDS-DMA (branch-free: rows past the end -- a partial last
+  // step, or a k-step past nk issued by the unconditional pipeline -- read
+  // zeros from an out-of-range offset).
   auto issue = [&](int kt, int slot) {
     char* sA = smem + slot * STAGE_BYTES;
     char* sB = sA + A_BYTES;
@@ -916,17 +919,10 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
     const int u = (ms >> g.logHW) * HpWp + ((ms & (HW - 1)) >> g.logW) * g.Wp;  // wave-uniform
     const int left = mend - ms;                                                  // rows left (uniform)
     const unsigned ua = 2u * (unsigned)(u * g.Cout), ub = 2u * (unsigned)(u * g.Cin);
-    if (left >= BK) {
 #pragma unroll
-      for (int j = 0; j < A_INS; ++j) blds16(dyr, a_v[j], ua, sA + (wid * A_INS + j) * 1024);
+    for (int j = 0; j < A_INS; ++j) blds16(dyr, a_row[j] < left ? a_v[j] : kOOB, ua, sA + (wid * A_INS + j) * 1024);
 #pragma unroll
-      for (int j = 0; j < B_INS; ++j) blds16(xr, b_v[j], ub, sB + (wid * B_INS + j) * 1024);
-    } else {  // partial last step: rows past the end read zeros
-#pragma unroll
-      for (int j = 0; j < A_INS; ++j) blds16(dyr, a_row[j] < left ? a_v[j] : kOOB, ua, sA + (wid * A_INS + j) * 1024);
-#pragma unroll
-      for (int j = 0; j < B_INS; ++j) blds16(xr, b_row[j] < left ? b_v[j] : kOOB, ub, sB + (wid * B_INS + j) * 1024);
-    }
+    for (int j = 0; j < B_INS; ++j) blds16(xr, b_row[j] < left ? b_v[j] : kOOB, ub, sB + (wid * B_INS + j) * 1024);
   };
 
   f32x4 acc[FM][FN];
@@ -937,18 +933,20 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
 
   const int gq = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
   const int nk = max(0, (mend - mbeg + BK - 1) / BK);
+  // PF: (as conv_fwd_region_kernel) every step issues one stage
+  // unconditionally, fragments of step i+1 are read (transposed LDS reads)
+  // while the MFMAs of step i run, interleaved 1:1 -- needs >= 4 stages to
+  // keep DMA lookahead.  !PF: read-then-compute per step, PD-1 stages in
+  // flight beyond the one being read (better at 3 stages / 2 WGs per CU).
+  static_assert(!PF || STAGES >= 3, "fragment prefetch needs >= 3 ring slots");
 #pragma unroll
-  for (int p = 0; p < PD; ++p)
-    if (p < nk) issue(p, p);
-  int slot_c = 0, slot_n = PD % STAGES;
-  auto kstep = [&](int i) {
-    block_sync_lds();
-    if (i + PD < nk) issue(i + PD, slot_n);
-    const char* As = smem + slot_c * STAGE_BYTES;
+  for (int p = 0; p < PD; ++p) issue(p, p);
+  int rslot = 0, dslot = PD % STAGES;
+  auto read_frags = [&](bf16x8 (&af)[BK / 32][FM], bf16x8 (&bf)[BK / 32][FN]) {
+    const char* As = smem + rslot * STAGE_BYTES;
     const char* Bs = As + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
-      bf16x8 af[FM], bfr[FN];
       const int r0 = kk * 32 + gq * 8 + q4;
 #pragma unroll
       for (int a = 0; a < FM; ++a) {
@@ -956,7 +954,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
         const int ch = col >> 3, sub = (col & 7) * 2;
         s16x4 lo = ds_read_tr16(As + swz_tr<ACPR>(r0, ch) * 16 + sub);
         s16x4 hi = ds_read_tr16(As + swz_tr<ACPR>(r0 + 4, ch) * 16 + sub);
-        af[a] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[kk][a] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
       for (int b = 0; b < FN; ++b) {
@@ -964,24 +962,76 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
         const int ch = col >> 3, sub = (col & 7) * 2;
         s16x4 lo = ds_read_tr16(Bs + swz_tr<BCPR>(r0, ch) * 16 + sub);
         s16x4 hi = ds_read_tr16(Bs + swz_tr<BCPR>(r0 + 4, ch) * 16 + sub);
-        bfr[b] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bf[kk][b] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
+    }
+    ++rslot;
+    rslot -= (rslot == STAGES) * STAGES;
+  };
+  constexpr int NRD = (BK / 32) * (FM + FN) * 2;  // ds_read_b64_tr_b16 per step
+  constexpr int NMF = (BK / 32) * FM * FN;
+  bf16x8 fa0[BK / 32][FM], fb0[BK / 32][FN], fa1[BK / 32][FM], fb1[BK / 32][FN];
+  if constexpr (!PF) {
+    for (int i = 0; i < nk; ++i) {
+      wait_vmcnt<(PD - 1) * LPS>();  // stage i landed (loads past nk are zero-fill dummies)
+      block_sync_lds();
+      issue(i + PD, dslot);
+      ++dslot;
+      dslot -= (dslot == STAGES) * STAGES;
+      read_frags(fa0, fb0);
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk)
+#pragma unroll
+        for (int a = 0; a < FM; ++a)
+#pragma unroll
+          for (int b = 0; b < FN; ++b) acc[a][b] = mfma16(fb0[kk][b], fa0[kk][a], acc[a][b]);
+    }
+  } else {
+  wait_vmcnt<(PD - 1) * LPS>();  // stage 0 landed
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  read_frags(fa0, fb0);
+  int kt_next = PD;
+  auto step = [&](bf16x8 (&fca)[BK / 32][FM], bf16x8 (&fcb)[BK / 32][FN], bf16x8 (&fna)[BK / 32][FM],
+                  bf16x8 (&fnb)[BK / 32][FN]) {
+    wait_vmcnt<(PD - 2) * LPS>();        // stage i+1 landed
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // step i's fragments in registers (compiler-visible wait)
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    read_frags(fna, fnb);
+    issue(kt_next, dslot);  // into the slot read two steps ago
+    ++kt_next;
+    ++dslot;
+    dslot -= (dslot == STAGES) * STAGES;
+    // C^T (k x co): lane holds 4 consecutive k of one co -> 16-byte stores
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk)
 #pragma unroll
       for (int a = 0; a < FM; ++a)
 #pragma unroll
-        for (int b = 0; b < FN; ++b) acc[a][b] = mfma16(af[a], bfr[b], acc[a][b]);
+        for (int b = 0; b < FN; ++b) acc[a][b] = mfma16(fcb[kk][b], fca[kk][a], acc[a][b]);
+    constexpr int P1 = NRD / 2 < NMF ? NRD / 2 : NMF;  // (MFMA, 2 reads) pairs
+#pragma unroll
+    for (int q = 0; q < P1; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
     }
-    slot_c = slot_c + 1 == STAGES ? 0 : slot_c + 1;
-    slot_n = slot_n + 1 == STAGES ? 0 : slot_n + 1;
+    if constexpr (NRD > 2 * P1) __builtin_amdgcn_sched_group_barrier(0x100, NRD - 2 * P1, 0);
+    if constexpr (NMF > P1) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, LPS, 0);
+      if constexpr (NMF > P1 + 1) __builtin_amdgcn_sched_group_barrier(0x008, NMF - P1 - 1, 0);
+    } else {
+      __builtin_amdgcn_sched_group_barrier(0x020, LPS, 0);
+    }
   };
   int i = 0;
-  for (; i < nk - (PD - 1); ++i) {
-    wait_vmcnt<(PD - 1) * LPS>();
-    kstep(i);
+  for (; i + 1 < nk; i += 2) {
+    step(fa0, fb0, fa1, fb1);
+    step(fa1, fb1, fa0, fb0);
   }
-  for (; i < nk; ++i) {
-    wait_stages<LPS>(nk - 1 - i);
-    kstep(i);
+  if (i < nk) step(fa0, fb0, fa1, fb1);
   }
 
   float* o = out + (int64_t)split * g.Cout * ldo;
@@ -990,12 +1040,11 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
   for (int a = 0; a < FM; ++a)
 #pragma unroll
     for (int b = 0; b < FN; ++b) {
-      const int k = k0 + wn * TN + b * 16 + col_l;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wm * TM + a * 16 + rq * 4 + r;
-        if (co < g.Cout && k < ldo) o[(int64_t)co * ldo + k] = acc[a][b][r];
-      }
+      const int k = k0 + wn * TN + b * 16 + rq * 4;
+      const int co = co0 + wm * TM + a * 16 + col_l;
+      if (co < g.Cout && k < ldo)  // ldo % 4 == 0 and k % 4 == 0: the 4-run is in bounds
+        *reinterpret_cast<float4*>(o + (int64_t)co * ldo + k) =
+            make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
     }
 }
 
@@ -1339,12 +1388,12 @@ void set_conv_waves(int waves) {
   g_fwd_waves = waves;
 }
 
-static int g_fwd_stages = 3, g_wgrad_stages = 3;  // tuning knobs (set_conv_stages)
+static int g_fwd_stages = 3, g_wgrad_stages = 0;  // tuning knobs (set_conv_stages); wgrad 0 = per-tile default
 
 void set_conv_debug(uintptr_t buf) { g_conv_dbg = (unsigned long long*)buf; }
 
 void set_conv_stages(int fwd, int wgrad) {
-  if (fwd < 2 || fwd > 4 || wgrad < 2 || wgrad > 4) throw std::runtime_error("stages must be 2..4");
+  if (fwd < 2 || fwd > 4 || wgrad < 0 || wgrad > 4) throw std::runtime_error("stages must be 2..4 (wgrad 0 = default)");
   g_fwd_stages = fwd;
   g_wgrad_stages = wgrad;
 }
@@ -1503,6 +1552,7 @@ void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, i
                 int ldo, int tile, uintptr_t stream) {
   ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
   if (ldo < g.K) throw std::runtime_error("conv_wgrad: ldo < K");
+  if (ldo % 4 != 0) throw std::runtime_error("conv_wgrad: ldo % 4 != 0 (16-byte slab stores)");
   if (Cout % 8 != 0) throw std::runtime_error("conv_wgrad: Cout % 8 != 0");
   const int bm = tile == 1 ? 64 : 128;
   if (Cout % bm != 0) throw std::runtime_error("conv_wgrad: Cout must be a multiple of the Cout tile");
@@ -1517,25 +1567,35 @@ void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, i
     conv_wgrad_kernel<BM_, BN_, ST_, WM_, WN_><<<dim3(nt, splits), 64 * WM_ * WN_, 0, s>>>(                \
         (const bf16_t*)dy, (const bf16_t*)x, (float*)out, g, mps, ldo);                                    \
   } while (0)
-  const int st = g_wgrad_stages;
+#define DL_WGN(BM_, BN_, ST_, WM_, WN_)                                                                     \
+  do {                                                                                                     \
+    const int nt = ((g.Cout + BM_ - 1) / BM_) * ((g.K + BN_ - 1) / BN_);                                  \
+    conv_wgrad_kernel<BM_, BN_, ST_, WM_, WN_, false><<<dim3(nt, splits), 64 * WM_ * WN_, 0, s>>>(                \
+        (const bf16_t*)dy, (const bf16_t*)x, (float*)out, g, mps, ldo);                                    \
+  } while (0)
+  // the wgrad pipeline keeps >= 2 stages in flight beyond the one being read.
+  // Measured (batch 128): 64x64 tiles want 4 stages (2 WGs/CU still fit:
+  // wgrad1 22.1 -> 16.8 us), 128x64 tiles 3 (4 would drop to 1 WG/CU: +20%)
+  const int st = g_wgrad_stages > 0 ? std::max(3, g_wgrad_stages) : (tile == 1 ? 4 : 3);
   if (g_fwd_waves == 8) {
     if (tile == 0) {
-      if (st == 2) DL_WG(128, 64, 2, 4, 2); else DL_WG(128, 64, 3, 4, 2);
+      if (st >= 4) DL_WG(128, 64, 4, 4, 2); else DL_WGN(128, 64, 3, 4, 2);
     } else if (tile == 2) {
-      if (st == 2) DL_WG(128, 128, 2, 2, 4); else DL_WG(128, 128, 3, 2, 4);
+      DL_WG(128, 128, 3, 2, 4);
     } else {
-      if (st == 2) DL_WG(64, 64, 2, 2, 4); else DL_WG(64, 64, 3, 2, 4);
+      if (st >= 4) DL_WG(64, 64, 4, 2, 4); else DL_WG(64, 64, 3, 2, 4);
     }
   } else {
     if (tile == 0) {
-      if (st == 2) DL_WG(128, 64, 2, 2, 2); else DL_WG(128, 64, 3, 2, 2);
+      DL_WG(128, 64, 3, 2, 2);
     } else if (tile == 2) {
-      if (st == 2) DL_WG(128, 128, 2, 2, 2); else DL_WG(128, 128, 3, 2, 2);
+      DL_WG(128, 128, 3, 2, 2);
     } else {
-      if (st == 2) DL_WG(64, 64, 2, 2, 2); else DL_WG(64, 64, 3, 2, 2);
+      DL_WG(64, 64, 3, 2, 2);
     }
   }
 #undef DL_WG
+#undef DL_WGN
   DL_HIP_CHECK(hipGetLastError());
 }
 

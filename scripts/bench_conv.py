@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--tile", type=int, default=-1)
     ap.add_argument("--splits", type=int, default=-1)
-    ap.add_argument("--stages", default="3,3", help="fwd,wgrad LDS ring depth")
+    ap.add_argument("--stages", default="3,0", help="fwd,wgrad LDS ring depth (wgrad 0 = per-tile default)")
     ap.add_argument("--wtile", type=int, default=-1, help="override the wgrad tile (0 128x64, 1 64x64, 2 128x128)")
     ap.add_argument("--waves", type=int, default=8, help="waves per workgroup of the fwd/dgrad kernel (4 or 8)")
     ap.add_argument("--region", type=int, default=1, help="1: tap-reuse (LDS-resident region) fwd/dgrad kernel")
