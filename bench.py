@@ -85,6 +85,13 @@ def main():
         dev = torch.device("cpu")
         sync = lambda: None  # noqa: E731
     else:
+        ndev = torch.cuda.device_count()
+        if local >= ndev:
+            # more ranks than GPUs (a functional rehearsal of the multi-rank
+            # path on a small box; not a benchmark configuration)
+            print(f"bench.py: rank {rank}: LOCAL_RANK {local} >= {ndev} GPUs, sharing GPU {local % ndev}",
+                  file=sys.stderr)
+            local = local % ndev
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         sync = torch.cuda.synchronize

@@ -78,6 +78,25 @@ def test_hip_graph_replay_matches_eager(dev):
     assert float((p0 - p1).abs().max()) < 1e-3
 
 
+def test_rccl_collectives_inside_hipgraph(dev, monkeypatch):
+    """World-1 collectives are normally skipped (identity); forcing them
+    through RCCL puts ncclAllReduce (3 bucket all-reduces per step, on the
+    comm stream) inside the captured hipGraph: replay must match eager."""
+    monkeypatch.setenv("DISTLEARN_RCCL_WORLD1", "1")
+    g = torch.Generator(device=dev).manual_seed(3)
+    xs = torch.randn(3, 32, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)
+    ys = torch.randint(0, 10, (3, 32), device=dev, generator=g)
+    outs = []
+    for graph, port in ((False, 29703), (True, 29703)):
+        tr = _trainer(dev, "hip", graph, port)
+        assert not tr.tree.comm._skip1 and len(tr.bucketer.ranges) >= 2
+        for i in range(3):
+            tr.step(xs[i], ys[i])
+        torch.cuda.synchronize()
+        outs.append(tr.flat.data.clone())
+    assert float((outs[0] - outs[1]).abs().max()) < 1e-3
+
+
 def test_hip_and_torch_backends_train_alike(dev):
     g = torch.Generator(device=dev).manual_seed(1)
     x = torch.randn(32, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)

@@ -149,6 +149,9 @@ class RcclCommunicator(Communicator):
             uid = lst[0]
         self._c = C.RcclCommunicator(uid, rank, world_size, self.device.index or 0)
         self._in_group = 0
+        # world 1 collectives are the identity and skipped; DISTLEARN_RCCL_WORLD1=1
+        # issues them anyway (exercises RCCL inside hipGraph capture on one GPU)
+        self._skip1 = world_size == 1 and os.environ.get("DISTLEARN_RCCL_WORLD1", "0") != "1"
 
     @staticmethod
     def _check(t):
@@ -159,14 +162,14 @@ class RcclCommunicator(Communicator):
 
     def all_reduce(self, t, op="sum", stream=None):
         self._check(t)
-        if self.world_size == 1:  # identity (in place); skips RCCL's self-copy
+        if self._skip1:  # identity (in place); skips RCCL's self-copy
             return
         self._c.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], OP_CODES[op],
                            stream_handle(stream))
 
     def broadcast(self, t, root=0, stream=None):
         self._check(t)
-        if self.world_size == 1:
+        if self._skip1:
             return
         self._c.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], root, stream_handle(stream))
 
