@@ -44,11 +44,17 @@ def parse():
                     help="cpu = gloo plumbing check of the same code path (tests only; not a benchmark)")
     ap.add_argument("--tau", type=int, default=10)
     ap.add_argument("--alpha", type=float, default=0.2)
-    ap.add_argument("--graph", type=int, default=1, help="capture the step in a hipGraph")
+    ap.add_argument("--graph", type=int, default=None,
+                    help="capture the step in a hipGraph (default: cifar10 1; resnet50 0 -- the MIOpen path "
+                         "replayed back to back without host syncs produced NaN losses from the 2nd replay "
+                         "after a device sync, while eager and per-step-synced replays train normally; "
+                         "eager costs <2%% there: 62 vs 63 ms/step)")
     ap.add_argument("--bucket-mb", type=float, default=None,
                     help="gradient all-reduce bucket size (default: cifar10 1 MiB = 3 buckets "
                          "{conv4+bn4+fc, conv3+bn3, conv1..bn2}; resnet50 16 MiB)")
-    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--lr", type=float, default=None,
+                    help="SGD learning rate (default: cifar10 0.1 = examples/cifar10.lua:7; resnet50 0.02)")
+    ap.add_argument("--overlap", type=int, default=1, help="bucketed all-reduce overlapped with backward")
     return ap.parse_args()
 
 
@@ -98,6 +104,10 @@ def main():
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29517")
     batch = a.batch or (128 if a.model == "cifar10" else 256)
+    if a.graph is None:
+        a.graph = 1 if a.model == "cifar10" else 0
+    if a.lr is None:
+        a.lr = 0.1 if a.model == "cifar10" else 0.02
     if a.bucket_mb is None:
         a.bucket_mb = 1.0 if a.model == "cifar10" else 16.0
     backend = a.backend if (a.model == "cifar10" and not cpu) else "torch"
@@ -134,7 +144,7 @@ def main():
             pass
     else:
         tr = DataParallelTrainer(model, tree, lr=a.lr, algo=a.algo, tau=a.tau, alpha=a.alpha, backend=backend,
-                                 compute_dtype=cdt, bucket_bytes=int(a.bucket_mb * (1 << 20)),
+                                 compute_dtype=cdt, bucket_bytes=int(a.bucket_mb * (1 << 20)), overlap=bool(a.overlap),
                                  graph=bool(a.graph) and not cpu, max_batch=batch)
         tr.synchronize_parameters()
         if a.model == "cifar10":
@@ -161,7 +171,10 @@ def main():
             tr.run(loader, a.warmup)
         else:
             for i in range(a.warmup):
-                tr.step(*step_args(i))
+                wl = tr.step(*step_args(i))
+                if os.environ.get("DISTLEARN_BENCH_TRACE", "") == "sync":
+                    print(f"warmup {i} loss {float(wl):.4f} |p| {float(tr.flat.data.norm()):.4e} "
+                          f"|g| {float(tr.flat.grad.norm()):.4e}", file=sys.stderr, flush=True)
         sync()
         worker_barrier()
         sync()
@@ -169,8 +182,16 @@ def main():
         if step_args is None:
             loss = tr.run(loader, a.steps)
         else:
+            trace = os.environ.get("DISTLEARN_BENCH_TRACE", "")  # debug: per-step losses (stderr)
+            hist = []
             for i in range(a.steps):
                 loss = tr.step(*step_args(i))
+                if trace == "sync":
+                    print(f"step {i} loss {float(loss):.4f}", file=sys.stderr, flush=True)
+                elif trace:
+                    hist.append(loss.detach().clone())
+            for i, l in enumerate(hist):
+                print(f"step {i} loss {float(l):.4f}", file=sys.stderr, flush=True)
         sync()
         worker_barrier()
         sync()

@@ -29,7 +29,26 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
   float acc[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) acc[c] = 0.f;
-  for (int j0 = tid * 8; j0 < F; j0 += 256 * 8) {
+  // F == 2048 (the reference net): one 8-feature chunk per thread; its 8 x NC
+  // weights stay in registers for the dh pass (W is read once per sample)
+  const bool one = F == 256 * 8;
+  float4 wc[NC][2];
+  if (one) {
+    const int j0 = tid * 8;
+    const uint4 hv = *reinterpret_cast<const uint4*>(hb + j0);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      wc[c][0] = *reinterpret_cast<const float4*>(w + (int64_t)c * F + j0);
+      wc[c][1] = *reinterpret_cast<const float4*>(w + (int64_t)c * F + j0 + 4);
+    }
+    const float hf[8] = {lo_bf16(hv.x), hi_bf16(hv.x), lo_bf16(hv.y), hi_bf16(hv.y),
+                         lo_bf16(hv.z), hi_bf16(hv.z), lo_bf16(hv.w), hi_bf16(hv.w)};
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      acc[c] = hf[0] * wc[c][0].x + hf[1] * wc[c][0].y + hf[2] * wc[c][0].z + hf[3] * wc[c][0].w +
+               hf[4] * wc[c][1].x + hf[5] * wc[c][1].y + hf[6] * wc[c][1].z + hf[7] * wc[c][1].w;
+  }
+  for (int j0 = tid * 8; !one && j0 < F; j0 += 256 * 8) {
     const uint4 hv = *reinterpret_cast<const uint4*>(hb + j0);
     float hf[8] = {lo_bf16(hv.x), hi_bf16(hv.x), lo_bf16(hv.y), hi_bf16(hv.y),
                    lo_bf16(hv.z), hi_bf16(hv.z), lo_bf16(hv.w), hi_bf16(hv.w)};
@@ -81,6 +100,18 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
   float d[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) d[c] = dl[c];
+  if (one) {
+    const int j0 = tid * 8;
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      o[0] += d[c] * wc[c][0].x; o[1] += d[c] * wc[c][0].y; o[2] += d[c] * wc[c][0].z; o[3] += d[c] * wc[c][0].w;
+      o[4] += d[c] * wc[c][1].x; o[5] += d[c] * wc[c][1].y; o[6] += d[c] * wc[c][1].z; o[7] += d[c] * wc[c][1].w;
+    }
+    *reinterpret_cast<uint4*>(dh + (int64_t)b * F + j0) =
+        make_uint4(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]), pack_bf16x2(o[6], o[7]));
+    return;
+  }
   for (int j0 = tid * 8; j0 < F; j0 += 256 * 8) {
     float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -113,7 +144,19 @@ __global__ void __launch_bounds__(256) head_wgrad_kernel(const bf16_t* __restric
 #pragma unroll
     for (int c = 0; c < NC; ++c) acc[c] = 0.f;
     if (j < F) {
-      for (int b = grp; b < B; b += 8) {
+      // rows in batches of 4 with every load issued before the FMAs (the
+      // serial load->use chain was latency-bound)
+      int b = grp;
+      for (; b + 24 < B; b += 32) {
+        float hv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) hv[u] = bf16_to_f32(h[(int64_t)(b + 8 * u) * F + j]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int c = 0; c < NC; ++c) acc[c] += dlogits[(int64_t)(b + 8 * u) * NC + c] * hv[u];
+      }
+      for (; b < B; b += 8) {
         const float hv = bf16_to_f32(h[(int64_t)b * F + j]);
 #pragma unroll
         for (int c = 0; c < NC; ++c) acc[c] += dlogits[(int64_t)b * NC + c] * hv;

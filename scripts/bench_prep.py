@@ -51,5 +51,27 @@ def main():
     print(f"transposes only          {timeit(lambda: ex._prep_transposes(s())):7.2f} us")
 
 
+def small_kernels():
+    """Isolated small per-step kernels of the executor (graph-replayed)."""
+    dev = torch.device("cuda")
+    C = _native.native()
+    s = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
+    for T, Cc, M in ((1024, 64, 131072), (256, 128, 32768), (384, 256, 8192), (400, 512, 2048)):
+        part = torch.randn(T, 2, Cc, device=dev).abs()
+        gam = torch.ones(Cc, device=dev)
+        bet = torch.zeros(Cc, device=dev)
+        rm = torch.zeros(Cc, device=dev)
+        rv = torch.ones(Cc, device=dev)
+        coef = torch.empty(4, Cc, device=dev)
+        acoef = torch.empty(3, Cc, device=dev)
+        dg = torch.empty(Cc, device=dev)
+        t1 = timeit(lambda: C.bn_finalize(part.data_ptr(), T, Cc, M, gam.data_ptr(), bet.data_ptr(), 0, rm.data_ptr(),
+                                          rv.data_ptr(), 1e-3, 0.1, 0, coef.data_ptr(), s()))
+        t2 = timeit(lambda: C.bn_bwd_finalize(part.data_ptr(), T, Cc, M, gam.data_ptr(), coef.data_ptr(), dg.data_ptr(),
+                                              dg.data_ptr(), acoef.data_ptr(), s()))
+        print(f"bn_finalize T={T:5d} C={Cc:4d}: {t1:6.2f} us   bn_bwd_finalize: {t2:6.2f} us")
+
+
 if __name__ == "__main__":
     main()
+    small_kernels()
