@@ -191,21 +191,57 @@ __global__ void __launch_bounds__(256) bn_relu_pool_bwd_reduce_kernel(const bf16
   float s1[8], s2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
-  for (int64_t i = i0; i < total; i += stride) {
+  // items in batches of U: every load of the batch is issued before the
+  // first use (the per-item load->use chain was latency-bound); the
+  // accumulation order is the same item order as a plain loop
+  constexpr int U = 4;
+  auto item_loads = [&](int64_t i, uint4 (&yw)[4], uint4& gv) {
     const int64_t pix = i / C8;
     const int ow = (int)(pix % Wo);
     const int64_t t = pix / Wo;
     const int oh = (int)(t % Ho);
     const int64_t b = t / Ho;
-    float yv[4][8], dz[4][8];
-    bwd_window(y, dP, cx, b, oh, ow, H, W, C, c0, yv, dz);
+    const bf16_t* base = y + (((b * H + 2 * oh) * W) + 2 * ow) * (int64_t)C + c0;
+    yw[0] = *reinterpret_cast<const uint4*>(base);
+    yw[1] = *reinterpret_cast<const uint4*>(base + C);
+    yw[2] = *reinterpret_cast<const uint4*>(base + (int64_t)W * C);
+    yw[3] = *reinterpret_cast<const uint4*>(base + (int64_t)W * C + C);
+    gv = *reinterpret_cast<const uint4*>(dP + (((b * Ho + oh) * Wo) + ow) * (int64_t)C + c0);
+  };
+  auto item_acc = [&](const uint4 (&yw)[4], const uint4& gv) {
+    float yv[4][8], g[8];
 #pragma unroll
-    for (int w = 0; w < 4; ++w)
+    for (int w = 0; w < 4; ++w) unpack8(yw[w], yv[w]);
+    unpack8(gv, g);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        s1[k] += dz[w][k];
-        s2[k] += dz[w][k] * (yv[w][k] - cx.mu[k]) * cx.is[k];
+    for (int k = 0; k < 8; ++k) {
+      float best = -INFINITY;
+      int arg = 0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float r = fmaxf(fmaf(cx.sc[k], yv[w][k], cx.sh[k]), 0.f);
+        if (r > best) { best = r; arg = w; }
       }
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float dz = (w == arg && best > 0.f) ? g[k] : 0.f;
+        s1[k] += dz;
+        s2[k] += dz * (yv[w][k] - cx.mu[k]) * cx.is[k];
+      }
+    }
+  };
+  int64_t i = i0;
+  for (; i + (U - 1) * stride < total; i += U * stride) {
+    uint4 yw[U][4], gv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) item_loads(i + u * stride, yw[u], gv[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) item_acc(yw[u], gv[u]);
+  }
+  for (; i < total; i += stride) {
+    uint4 yw[4], gv;
+    item_loads(i, yw, gv);
+    item_acc(yw, gv);
   }
   // block reduction over threads that own the same channel chunk
   __shared__ float red[256][17];

@@ -780,6 +780,90 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf1
   }
 }
 
+// --------------------------------------------------------------------------
+// First layer (Cin = 8 after the 3 -> 8 channel pad; K = KS*KS*8 = 200): the
+// whole problem of a workgroup fits in LDS at once -- its 128 output pixels'
+// padded input rows (16 B per pixel) and the 64 x K weight panel -- so it is
+// one DMA burst, one barrier and ceil(K/32) MFMA steps; a 32-deep k-step
+// covers 4 taps (lane group q = l>>4 reads tap 4s+q at its own pixel offset).
+// The streaming kernel spent most of its time on per-lane tap arithmetic and
+// on re-reading each input pixel through the L2 for 25 taps.
+// Output: transposed accumulator -> conv_fwd_epilogue_t (16-byte stores, BN
+// statistics per M tile).
+// --------------------------------------------------------------------------
+template <bool STATS>
+__global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                          bf16_t* __restrict__ y, float* __restrict__ stats,
+                                                          const ConvGeom g, int region_rows) {
+  constexpr int BM = 128, BN = 64, WM = 4, WN = 2, NW = 8, TM = 32, TN = 32, FM = 2, FN = 2;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int taps = g.KS * g.KS;                      // K = taps * 8
+  const int nsteps = (taps + 3) / 4;                 // 32-deep k-steps (4 taps each)
+  const int rslots = region_rows * g.Wp;             // region pixels (16 B each)
+  const int rslots_p = (rslots + 1 + 63) / 64 * 64;  // + >= 1 zero slot, whole DMA pieces
+  const int wslots = BN * taps;                      // weight panel: BN rows x taps 16-B chunks
+  const int wslots_p = (wslots + 63) / 64 * 64;
+  char* sR = smem;
+  char* sW = smem + rslots_p * 16;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int ntm = (g.M + BM - 1) / BM;
+  const int id = xcd_swizzle(blockIdx.x, ntm * (g.Cout / BN));
+  const int tm = id % ntm, tn = id / ntm;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int HW = 1 << g.logHW;
+  const int img0 = m0 >> g.logHW, oh0 = (m0 & (HW - 1)) >> g.logW;
+  const int start_pix = (img0 * g.Hp + oh0) * g.Wp;
+  const rsrc_t xr = make_rsrc(x, (unsigned)((int64_t)g.B * g.Hp * g.Wp * 16));
+  const rsrc_t wr = make_rsrc(w, (unsigned)((int64_t)g.Cout * taps * 16));
+  // one DMA burst: region pixels (contiguous padded rows) then the weight panel
+  for (int q = wid; q < rslots_p / 64; q += NW) {
+    const int sl = q * 64 + lane;
+    blds16(xr, sl < rslots ? 16u * (unsigned)(start_pix + sl) : kOOB, 0u, sR + q * 1024);
+  }
+  for (int q = wid; q < wslots_p / 64; q += NW) {
+    const int sl = q * 64 + lane;
+    blds16(wr, sl < wslots ? 16u * (unsigned)(n0 * taps + sl) : kOOB, 0u, sW + q * 1024);
+  }
+  const int i = lane & 15, qg = lane >> 4;
+  int a_pix[FM];
+#pragma unroll
+  for (int a = 0; a < FM; ++a) {
+    const int m = min(m0 + wm * TM + a * 16 + i, g.M - 1) - m0;  // tile-local output pixel
+    a_pix[a] = (m >> g.logW) * g.Wp + (m & (g.W - 1));
+  }
+  int b_row[FN];
+#pragma unroll
+  for (int b = 0; b < FN; ++b) b_row[b] = wn * TN + 8 * (i >> 2) + 4 * b + (i & 3);
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int a = 0; a < FM; ++a)
+#pragma unroll
+    for (int b = 0; b < FN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  wait_vmcnt<0>();
+  block_sync_lds();
+  const int zero_slot = rslots;  // loaded from an out-of-range offset: zeros
+  for (int st = 0; st < nsteps; ++st) {
+    const int t = 4 * st + qg;  // this lane group's tap
+    const int kh = t / g.KS, kw = t - (t / g.KS) * g.KS;
+    const int toff = kh * g.Wp + kw;
+    bf16x8 fa[FM], fb[FN];
+#pragma unroll
+    for (int a = 0; a < FM; ++a)
+      fa[a] = *reinterpret_cast<const bf16x8*>(sR + (t < taps ? a_pix[a] + toff : zero_slot) * 16);
+#pragma unroll
+    for (int b = 0; b < FN; ++b)
+      fb[b] = *reinterpret_cast<const bf16x8*>(sW + (b_row[b] * taps + min(t, taps - 1)) * 16);
+#pragma unroll
+    for (int a = 0; a < FM; ++a)
+#pragma unroll
+      for (int b = 0; b < FN; ++b) acc[a][b] = mfma16(fb[b], fa[a], acc[a][b]);
+  }
+  conv_fwd_epilogue_t<BN, STATS, false, WM, WN, FM, FN>(acc, g, y, stats, nullptr, 0, tm, m0, n0, smem);
+}
+
 // split-K combine: y = bf16(sum_s slab[s]) (+ BN partial sums, one row per block)
 template <bool STATS>
 __global__ void __launch_bounds__(256) splitk_combine_kernel(const float* __restrict__ slab, bf16_t* __restrict__ y,
@@ -1522,7 +1606,22 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
   if (tile < 0 || tile > 2) throw std::runtime_error("conv_fwd: bad tile id");
   if (Cout % fwd_bn(tile) != 0) throw std::runtime_error("conv_fwd: Cout must be a multiple of the N tile");
   RegionGeom rg;
-  if (tile == 0 && region_geom(g, 128, splits, rg)) {
+  const int c8_rows = 128 / std::max(1, W) + KS - 1;
+  const size_t c8_lds = (size_t)((c8_rows * g.Wp + 1 + 63) / 64 * 64 + (64 * KS * KS + 63) / 64 * 64) * 16;
+  if (tile == 2 && splits == 1 && g_region && Cin == 8 && W <= 128 && 128 % W == 0 && (H * W) % 128 == 0 &&
+      Cout % 64 == 0 && c8_lds <= 160 * 1024) {
+    const int grid = (g.M / 128) * (Cout / 64);
+    auto go = [&](auto kern) {
+      static bool attr = false;
+      if (!attr) {
+        DL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr = true;
+      }
+      kern<<<grid, 512, c8_lds, s>>>((const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)stats, g, c8_rows);
+    };
+    if (stats) go(conv_fwd_c8_kernel<true>);
+    else go(conv_fwd_c8_kernel<false>);
+  } else if (tile == 0 && region_geom(g, 128, splits, rg)) {
     if (g_region_waves == 4) launch_fwd_region<128, 2, 2>(g, rg, x, w, y, stats, slab, splits, s);
     else launch_fwd_region<128, 2, 4>(g, rg, x, w, y, stats, slab, splits, s);
   } else if (tile == 2 && region_geom(g, 64, splits, rg)) {
