@@ -110,6 +110,12 @@ class CifarHIPExecutor:
         self.side = torch.cuda.Stream(device=self.dev) if self.dev.type == "cuda" else None
         self.fork_transposes = os.environ.get("DISTLEARN_PREP_FORK", "0") == "1"
         self.side_wgrad = os.environ.get("DISTLEARN_WGRAD_STREAM", "0") == "1"
+        # (optional) split-K slab reduce of a layer's weight gradient on the side
+        # stream, concurrent with that layer's dgrad; every layer has its own
+        # slab buffer.  Measured inside the hipGraph: 0.459 vs 0.400 ms/step
+        # (the cross-queue edges leave ~150 us of idle gaps per step), so off.
+        self.side_reduce = (not self.side_wgrad and self.side is not None
+                            and os.environ.get("DISTLEARN_REDUCE_STREAM", "0") == "1")
         self._alloc(self.B)
 
     # ------------------------------------------------------------------ buffers
@@ -136,6 +142,7 @@ class CifarHIPExecutor:
         self.dgrad_plan = [None] * self.nb
         self.bwd_blocks, self.bwd_part = [], []
         self.wplan, slab_elems, wslab_elems = [], 0, 0
+        self.wslab_l = []
         for i in range(self.nb):
             h, cin, cout = self.hs[i], self.cins[i], self.couts[i]
             M = B * h * h
@@ -156,13 +163,13 @@ class CifarHIPExecutor:
             self.wplan.append((tile_w, splits_w, direct))
             if not direct:
                 wslab_elems = max(wslab_elems, splits_w * cout * K)
+            self.wslab_l.append(None if direct else torch.empty(splits_w * cout * K, device=d))
             if i > 0:
                 dt, ds = _fwd_plan(M, cin, KSIZE * KSIZE * cout)
                 self.dgrad_plan[i] = (dt, ds)
                 if ds > 1:
                     slab_elems = max(slab_elems, ds * M * cin)
         self.slabs = torch.empty(max(slab_elems, 1), device=d)    # fwd / dgrad split-K (main stream)
-        self.wslabs = torch.empty(max(wslab_elems, 1), device=d)  # wgrad split-K (side stream)
         self.logits = torch.empty(B, self.nclass, device=d)
         self.dlogits = torch.empty(B, self.nclass, device=d)
         self.loss_b = torch.empty(B, device=d)
@@ -267,6 +274,7 @@ class CifarHIPExecutor:
             main.wait_event(wt_ready)
         ws = side if self.side_wgrad else main
         wss = ws.cuda_stream
+        side_pending = False
         for i in reversed(range(self.nb)):
             h, cin, cout = self.hs[i], self.cins[i], self.couts[i]
             M = B * h * h
@@ -288,21 +296,32 @@ class CifarHIPExecutor:
             gw = self.g32[self._leaf(i, 0)]
             if direct:
                 C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), gw.data_ptr(), B, h, h, cin, cout, KSIZE, 1, K, tile, wss)
-            else:
-                C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), self.wslabs.data_ptr(), B, h, h, cin, cout, KSIZE,
+            rs = ws  # the stream that writes this block's weight gradient last
+            if not direct:
+                slab = self.wslab_l[i]
+                C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), slab.data_ptr(), B, h, h, cin, cout, KSIZE,
                              splits, K, tile, wss)
-                C.slab_reduce(self.wslabs.data_ptr(), gw.data_ptr(), splits, cout, KSIZE * KSIZE, cin,
-                              self.cins_real[i], wss)
+                if self.side_reduce and i > 0:  # overlaps this block's dgrad (block 1 has none)
+                    side.wait_stream(main)
+                    rs = side
+                C.slab_reduce(slab.data_ptr(), gw.data_ptr(), splits, cout, KSIZE * KSIZE, cin,
+                              self.cins_real[i], rs.cuda_stream)
             # conv bias grad: exactly 0 under train-mode BN (grad buffer was zero-filled).
-            # Bucket launches issued here are ordered after the wgrad stream.
-            with torch.cuda.stream(ws):
+            # Bucket launches issued here are ordered after the stream that wrote the grads;
+            # a bucket readied on the main stream may also hold leaves reduced on the side
+            # stream earlier, so main joins the side stream first.
+            if rs is main and side_pending:
+                main.wait_stream(side)
+                side_pending = False
+            side_pending |= rs is side
+            with torch.cuda.stream(rs):
                 for j in range(4):
                     self._ready(self._leaf(i, j))
             if i > 0:
                 dt, ds = self.dgrad_plan[i]
                 C.conv_fwd(dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), 0,
                            self.slabs.data_ptr(), B, h, h, cout, cin, KSIZE, dt, ds, s)
-        if self.side_wgrad:
+        if self.side_wgrad or self.side_reduce:
             main.wait_stream(side)  # join
         return self.loss[0]
 
