@@ -107,7 +107,8 @@ class CifarHIPExecutor:
         self.overwrites_grads = True
         for i in range(self.nb):
             self.g32[self._leaf(i, 1)].zero_()
-        self.side = torch.cuda.Stream(device=self.dev) if self.dev.type == "cuda" else None
+        self.side = torch.cuda.Stream(device=self.dev, priority=int(os.environ.get("DISTLEARN_SIDE_PRIORITY", "0"))) \
+            if self.dev.type == "cuda" else None
         self.fork_transposes = os.environ.get("DISTLEARN_PREP_FORK", "0") == "1"
         self.side_wgrad = os.environ.get("DISTLEARN_WGRAD_STREAM", "0") == "1"
         # (optional) split-K slab reduce of a layer's weight gradient on the side
