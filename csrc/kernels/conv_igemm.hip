@@ -1508,6 +1508,17 @@ void set_conv_region(int on) {
   g_region_images = on >= 2 ? 1 : 0;
 }
 
+// LDS budget of one region-kernel workgroup: the CU's 160 KiB minus room for
+// one co-resident RCCL collective workgroup (rcclGenericKernel: 19,744 B of
+// LDS, 256 threads, <= 280 VGPRs -- read from librccl's gfx950 code object),
+// so the bucket all-reduce that overlaps the backward at N > 1 never evicts
+// a conv workgroup from a CU (a 1-workgroup-per-CU grid would otherwise need
+// a second round for the CUs RCCL holds).  The dgrad instance (BN = 64, the
+// one that runs beside the all-reduce) also stays at <= 112 VGPRs, so two
+// of its waves fit a SIMD next to a 288-VGPR RCCL wave; the BN = 128
+// instance (127 VGPRs) only runs in the forward, before any collective.
+constexpr int kRegionLdsCap = 160 * 1024 - 20 * 1024;
+
 // Region geometry for a BM = 128 tile, or false if the shape does not fit the
 // region kernel (then the streaming kernel runs).
 static bool region_geom(const ConvGeom& g, int BN, int splits, RegionGeom& rg) {
@@ -1541,7 +1552,7 @@ static bool region_geom(const ConvGeom& g, int BN, int splits, RegionGeom& rg) {
   rg.inv_RS = 1.0f / rg.RS;
   rg.inv_IS = 1.0f / rg.IS;
   const int lds = rg.cpw * rg.nslot * 16 + STAGES * BN * 64 * 2;  // at least a 3-stage B ring
-  return lds <= 160 * 1024;
+  return lds <= kRegionLdsCap;
 }
 
 static int g_region_waves = 8;  // 8: 2 waves per SIMD; 4: one wave per SIMD with 2x wider wave tiles
@@ -1583,7 +1594,7 @@ static void launch_fwd_region_st(const ConvGeom& g, const RegionGeom& rg, uintpt
 template <int BN, int WM, int WN>
 static void launch_fwd_region(const ConvGeom& g, const RegionGeom& rg, uintptr_t x, uintptr_t w, uintptr_t y,
                               uintptr_t stats, uintptr_t slab, int splits, hipStream_t s) {
-  const int free_b = 160 * 1024 - rg.cpw * rg.nslot * 16;
+  const int free_b = kRegionLdsCap - rg.cpw * rg.nslot * 16;
   int st = std::min(8, free_b / (BN * 64 * 2));
   if (g_region_stages > 0) st = std::min(st, g_region_stages);
   if (st >= 8) launch_fwd_region_st<BN, WM, WN, 8>(g, rg, x, w, y, stats, slab, splits, s);
