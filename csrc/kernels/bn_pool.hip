@@ -34,6 +34,40 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
                     pack_bf16x2(f[6], f[7]));
 }
 
+// Per-channel column sums of partial rows [T][2][C] (stat 0 at +0, stat 1 at
+// +C), one block per channel: every thread issues the loads of 4 rows before
+// their first use (the rows were just written by other CUs: each round trip
+// is a cross-XCD miss), then a fixed-order wave butterfly and a 4-wave
+// combine (one barrier instead of an 8-level LDS tree).  Deterministic.
+// Thread 0 returns the totals.
+__device__ __forceinline__ void column_sums(const float* __restrict__ partial, int T, int C, int c, float& tot1,
+                                            float& tot2) {
+  __shared__ float red[2][4];
+  float s1 = 0.f, s2 = 0.f;
+  int t = threadIdx.x;
+  for (; t + 768 < T; t += 1024) {
+    float a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a[u] = partial[(int64_t)(t + 256 * u) * 2 * C + c];
+      b[u] = partial[(int64_t)(t + 256 * u) * 2 * C + C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { s1 += a[u]; s2 += b[u]; }
+  }
+  for (; t < T; t += 256) {
+    s1 += partial[(int64_t)t * 2 * C + c];
+    s2 += partial[(int64_t)t * 2 * C + C + c];
+  }
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { red[0][wid] = s1; red[1][wid] = s2; }
+  __syncthreads();
+  tot1 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+  tot2 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+}
+
 // ---------------------------------------------------------------------------
 // finalize (forward): partial rows [T][2][C] (sum, sumsq) -> coefficients
 // mode 0 = train (batch statistics, update running stats), 1 = eval
@@ -46,26 +80,12 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
                                                           float* __restrict__ rvar, float eps, float momentum,
                                                           int mode, float* __restrict__ coef) {
   const int c = blockIdx.x;
-  __shared__ float red[2][256];
   float mean, var;
   if (mode == 0) {
-    float s1 = 0.f, s2 = 0.f;
-    for (int t = threadIdx.x; t < T; t += 256) {
-      s1 += partial[(int64_t)t * 2 * C + c];
-      s2 += partial[(int64_t)t * 2 * C + C + c];
-    }
-    red[0][threadIdx.x] = s1;
-    red[1][threadIdx.x] = s2;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (threadIdx.x < o) {
-        red[0][threadIdx.x] += red[0][threadIdx.x + o];
-        red[1][threadIdx.x] += red[1][threadIdx.x + o];
-      }
-      __syncthreads();
-    }
-    mean = red[0][0] / (float)M;
-    var = fmaxf(red[1][0] / (float)M - mean * mean, 0.f);
+    float t1, t2;
+    column_sums(partial, T, C, c, t1, t2);
+    mean = t1 / (float)M;
+    var = fmaxf(t2 / (float)M - mean * mean, 0.f);
   } else {
     mean = rmean[c] - (bias ? bias[c] : 0.f);  // eval: conv output excludes the bias
     var = rvar[c];
@@ -268,24 +288,9 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                               float* __restrict__ acoef) {
   const int c = blockIdx.x;
-  __shared__ float red[2][256];
-  float s1 = 0.f, s2 = 0.f;
-  for (int t = threadIdx.x; t < T; t += 256) {
-    s1 += partial[(int64_t)t * 2 * C + c];
-    s2 += partial[(int64_t)t * 2 * C + C + c];
-  }
-  red[0][threadIdx.x] = s1;
-  red[1][threadIdx.x] = s2;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + o];
-      red[1][threadIdx.x] += red[1][threadIdx.x + o];
-    }
-    __syncthreads();
-  }
+  float sdz, sdzx;
+  column_sums(partial, T, C, c, sdz, sdzx);
   if (threadIdx.x == 0) {
-    const float sdz = red[0][0], sdzx = red[1][0];
     if (dgamma) dgamma[c] = sdzx;
     if (dbeta) dbeta[c] = sdz;
     const float a = gamma[c] * coef[C + c];  // gamma * invstd
