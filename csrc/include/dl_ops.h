@@ -32,6 +32,7 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
 int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile, int splits);
 void set_conv_region(int on);
 void set_conv_region_stages(int st);
+void set_conv_wgrad_pf(int pf);
 void set_conv_region_ablate(int a);
 void set_conv_region_waves(int w);
 void set_conv_stages(int fwd, int wgrad);

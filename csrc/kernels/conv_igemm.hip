@@ -1472,6 +1472,8 @@ void set_conv_waves(int waves) {
   g_fwd_waves = waves;
 }
 
+static int g_wgrad_pf = -1;  // wgrad fragment prefetch: -1 = by stage count, 0 off, 1 on
+void set_conv_wgrad_pf(int pf) { g_wgrad_pf = pf; }
 static int g_fwd_stages = 3, g_wgrad_stages = 0;  // tuning knobs (set_conv_stages); wgrad 0 = per-tile default
 
 void set_conv_debug(uintptr_t buf) { g_conv_dbg = (unsigned long long*)buf; }
@@ -1685,13 +1687,26 @@ void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, i
   } while (0)
   // the wgrad pipeline keeps >= 2 stages in flight beyond the one being read.
   // Measured (batch 128): 64x64 tiles want 4 stages (2 WGs/CU still fit:
-  // wgrad1 22.1 -> 16.8 us), 128x64 tiles 3 (4 would drop to 1 WG/CU: +20%)
-  const int st = g_wgrad_stages > 0 ? std::max(3, g_wgrad_stages) : (tile == 1 ? 4 : 3);
+  // wgrad1 22.1 -> 16.8 us), 128x64 tiles 3 (4 would drop to 1 WG/CU: +20%),
+  // 128x128 tiles 4 with fragment prefetch (1 WG/CU, 128 KiB LDS, 141 VGPRs:
+  // wgrad2/3/4 31.7/29.7/28.4 us as 128x64 -> 24.7/23.0/21.8 us; the waves
+  // wait on the LDS-DMA ring, so the deeper ring wins over occupancy)
+  const int st = g_wgrad_stages > 0 ? std::max(3, g_wgrad_stages) : (tile == 0 ? 3 : 4);
+  // fragment prefetch (PF): default on for 4 stages, off for 3 (set_conv_wgrad_pf overrides)
+  const bool pf = g_wgrad_pf >= 0 ? g_wgrad_pf != 0 : st >= 4;
   if (g_fwd_waves == 8) {
     if (tile == 0) {
-      if (st >= 4) DL_WG(128, 64, 4, 4, 2); else DL_WGN(128, 64, 3, 4, 2);
+      if (st >= 4) {
+        if (pf) DL_WG(128, 64, 4, 4, 2); else DL_WGN(128, 64, 4, 4, 2);
+      } else {
+        if (pf) DL_WG(128, 64, 3, 4, 2); else DL_WGN(128, 64, 3, 4, 2);
+      }
     } else if (tile == 2) {
-      DL_WG(128, 128, 3, 2, 4);
+      if (st >= 4) {
+        if (pf) DL_WG(128, 128, 4, 2, 4); else DL_WGN(128, 128, 4, 2, 4);
+      } else {
+        if (pf) DL_WG(128, 128, 3, 2, 4); else DL_WGN(128, 128, 3, 2, 4);
+      }
     } else {
       if (st >= 4) DL_WG(64, 64, 4, 2, 4); else DL_WG(64, 64, 3, 2, 4);
     }

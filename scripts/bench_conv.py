@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--splits", type=int, default=-1)
     ap.add_argument("--stages", default="3,0", help="fwd,wgrad LDS ring depth (wgrad 0 = per-tile default)")
     ap.add_argument("--wtile", type=int, default=-1, help="override the wgrad tile (0 128x64, 1 64x64, 2 128x128)")
+    ap.add_argument("--wpf", type=int, default=-1, help="wgrad fragment prefetch: -1 by stages, 0 off, 1 on")
     ap.add_argument("--waves", type=int, default=8, help="waves per workgroup of the fwd/dgrad kernel (4 or 8)")
     ap.add_argument("--region", type=int, default=1, help="1: tap-reuse (LDS-resident region) fwd/dgrad kernel")
     ap.add_argument("--rstages", type=int, default=0, help="region kernel B-ring stages (0 = max that fits)")
@@ -30,6 +31,7 @@ def main():
     fs, ws = (int(v) for v in a.stages.split(","))
     C.set_conv_stages(fs, ws)
     C.set_conv_waves(a.waves)
+    C.set_conv_wgrad_pf(a.wpf)
     C.set_conv_region(a.region)
     C.set_conv_region_stages(a.rstages)
     C.set_conv_region_waves(a.rwaves)

@@ -121,6 +121,24 @@ def test_conv_dgrad_wgrad(C, shape):
             C.slab_reduce(slabs.data_ptr(), dw.data_ptr(), splits, cout, 25, cin, cin, _s())
             torch.cuda.synchronize()
             assert _rel(dw, dw_ref) < 1e-4, (tile, splits, _rel(dw, dw_ref))
+    # non-default DMA ring depths / fragment-prefetch modes of the wgrad kernel
+    for tile in (0, 2):
+        if cout % 128 != 0:
+            continue
+        for st, pf in ((3, 1), (3, 0), (4, 0), (4, 1)):
+            C.set_conv_stages(3, st)
+            C.set_conv_wgrad_pf(pf)
+            try:
+                slabs = torch.full((2, cout, K), float("nan"), device=dev)
+                C.conv_wgrad(dyp.data_ptr(), xp.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, 2, K, tile,
+                             _s())
+            finally:
+                C.set_conv_stages(3, 0)
+                C.set_conv_wgrad_pf(-1)
+            dw = torch.empty(cout, 5, 5, cin, device=dev)
+            C.slab_reduce(slabs.data_ptr(), dw.data_ptr(), 2, cout, 25, cin, cin, _s())
+            torch.cuda.synchronize()
+            assert _rel(dw, dw_ref) < 1e-4, (tile, st, pf, _rel(dw, dw_ref))
 
 
 def test_prep_step(C):

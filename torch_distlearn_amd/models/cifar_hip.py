@@ -46,7 +46,7 @@ BF16 = torch.bfloat16
 CIN_PAD = 8  # the 3-channel input layer is zero-padded to 8 channels (one 16-B vector per tap)
 SPAD = KSIZE // 2  # spatial zero border of every convolution input (written once, never touched)
 
-# tile ids of conv_fwd: 0 = 128x128, 1 = 64x64, 2 = 128x64 (BK = 64) ; conv_wgrad: 0 = 128x64, 1 = 64x64
+# tile ids of conv_fwd: 0 = 128x128, 1 = 64x64, 2 = 128x64 (BK = 64) ; conv_wgrad: 0 = 128x64, 1 = 64x64, 2 = 128x128
 _FWD_TILES = {0: (128, 128), 1: (64, 64), 2: (128, 64)}
 
 
@@ -66,10 +66,11 @@ def _fwd_plan(M: int, N: int, K: int):
 
 def _wgrad_plan(cout: int, K: int, M: int):
     """(tile, splits) for the weight gradient: >= ~256 workgroups, each
-    reducing over >= 2048 rows of m."""
-    tile = 0 if cout % 128 == 0 else 1
-    bm = 128 if tile == 0 else 64
-    tiles = (cout // bm) * ((K + 63) // 64)
+    reducing over >= 2048 rows of m.  128x128 tiles (tile 2: 4-stage DMA ring,
+    fragment prefetch) whenever Cout allows, else 64x64."""
+    tile = 2 if cout % 128 == 0 else 1
+    bm, bn = (128, 128) if tile == 2 else (64, 64)
+    tiles = (cout // bm) * ((K + bn - 1) // bn)
     splits = 1
     while tiles * splits < 256 and M // (splits * 2) >= 2048:
         splits *= 2
