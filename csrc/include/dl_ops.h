@@ -33,6 +33,7 @@ int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile,
 void set_conv_region(int on);
 void set_conv_region_stages(int st);
 void set_conv_wgrad_pf(int pf);
+void set_bn_bwd_items(int n);
 void set_conv_region_ablate(int a);
 void set_conv_region_waves(int w);
 void set_conv_stages(int fwd, int wgrad);

@@ -108,6 +108,8 @@ class CifarHIPExecutor:
         self.overwrites_grads = True
         for i in range(self.nb):
             self.g32[self._leaf(i, 1)].zero_()
+        if "DISTLEARN_BN_BWD_ITEMS" in os.environ:  # tuning: pooled pixels per thread of the BN backward reduce
+            self.C.set_bn_bwd_items(int(os.environ["DISTLEARN_BN_BWD_ITEMS"]))
         self.side = torch.cuda.Stream(device=self.dev, priority=int(os.environ.get("DISTLEARN_SIDE_PRIORITY", "0"))) \
             if self.dev.type == "cuda" else None
         self.fork_transposes = os.environ.get("DISTLEARN_PREP_FORK", "0") == "1"
