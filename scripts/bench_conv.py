@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--tile", type=int, default=-1)
     ap.add_argument("--splits", type=int, default=-1)
+    ap.add_argument("--dtile", type=int, default=-1, help="override the dgrad tile")
+    ap.add_argument("--dsplits", type=int, default=-1, help="override the dgrad split count")
     ap.add_argument("--stages", default="3,0", help="fwd,wgrad LDS ring depth (wgrad 0 = per-tile default)")
     ap.add_argument("--wtile", type=int, default=-1, help="override the wgrad tile (0 128x64, 1 64x64, 2 128x128)")
     ap.add_argument("--wpf", type=int, default=-1, help="wgrad fragment prefetch: -1 by stages, 0 off, 1 on")
@@ -64,6 +66,10 @@ def main():
             sp, cur()), f"tile{t} split{sp}"))
         if li > 0:
             dt, ds = _fwd_plan(M, cin, 25 * cout)
+            if a.dtile >= 0:
+                dt = a.dtile
+            if a.dsplits >= 0:
+                ds = a.dsplits
             jobs.append((f"dgrad{li+1}", 2 * M * cout * K, lambda dt=dt, ds=ds: C.conv_fwd(
                 dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, slab.data_ptr(), B, H, H, cout, cin, 5, dt, ds,
                 cur()),
