@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--tile", type=int, default=-1)
     ap.add_argument("--splits", type=int, default=-1)
+    ap.add_argument("--wsplits", type=int, default=-1, help="override the wgrad split count")
     ap.add_argument("--dtile", type=int, default=-1, help="override the dgrad tile")
     ap.add_argument("--dsplits", type=int, default=-1, help="override the dgrad split count")
     ap.add_argument("--stages", default="3,0", help="fwd,wgrad LDS ring depth (wgrad 0 = per-tile default)")
@@ -82,6 +83,8 @@ def main():
             wsp = 1
             while tiles * wsp < 256 and M // (wsp * 2) >= 2048:
                 wsp *= 2
+        if a.wsplits > 0:
+            wsp = a.wsplits
         jobs.append((f"wgrad{li+1}", 2 * M * cout * K, lambda wtile=wtile, wsp=wsp: C.conv_wgrad(
             dy.data_ptr(), x.data_ptr(), slab.data_ptr(), B, H, H, cin, cout, 5, wsp, K, wtile, cur()),
             f"tile{wtile} split{wsp}"))

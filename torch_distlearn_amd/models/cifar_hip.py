@@ -70,15 +70,21 @@ def _fwd_plan(M: int, N: int, K: int):
 
 
 def _wgrad_plan(cout: int, K: int, M: int):
-    """(tile, splits) for the weight gradient: >= ~256 workgroups, each
-    reducing over >= 2048 rows of m.  128x128 tiles (tile 2: 4-stage DMA ring,
-    fragment prefetch) whenever Cout allows, else 64x64."""
+    """(tile, splits) for the weight gradient.  128x128 tiles (tile 2: 4-stage
+    DMA ring, fragment prefetch, one workgroup per CU) whenever Cout allows,
+    else 64x64 (two per CU).  Every workgroup is one ~20 us "round", so the
+    split count fills the resident slots exactly (not the next power of two:
+    conv3 50 tiles x 5 splits = 250 workgroups, 26 k-steps each, beats 4 splits
+    = 200 workgroups of 32 k-steps by 1.7 us), keeping >= 512 rows per split."""
     tile = 2 if cout % 128 == 0 else 1
     bm, bn = (128, 128) if tile == 2 else (64, 64)
+    slots = 256 if tile == 2 else 512
     tiles = (cout // bm) * ((K + bn - 1) // bn)
-    splits = 1
-    while tiles * splits < 256 and M // (splits * 2) >= 2048:
-        splits *= 2
+    splits = max(1, min(slots // tiles, M // 512))
+    if os.environ.get("DISTLEARN_WGRAD_POW2", "0") == "1":  # A/B: the earlier power-of-two rule
+        splits = 1
+        while tiles * splits < 256 and M // (splits * 2) >= 2048:
+            splits *= 2
     return tile, splits
 
 
