@@ -1,0 +1,49 @@
+// Diagnostics: emulate the CU footprint of a concurrently running RCCL
+// collective on one GPU.
+//
+// RCCL's gfx950 all-reduce workgroup (rcclGenericKernel in librccl's code
+// object: 256 threads, 261-280 arch VGPRs + 17-32 AGPRs, 19,744 B LDS) shares
+// a CU only with compute workgroups that fit beside it.  On a multi-GPU run
+// the bucketed all-reduce overlaps the backward convolutions; this kernel
+// reproduces that footprint (same workgroup size, register and LDS budget)
+// so the effect of R occupied CUs on the training step can be measured on a
+// one-GPU box (scripts/emulate_rccl.py).  Each workgroup spins on the 100 MHz
+// constant clock for `us` microseconds and exits: every wave reaches the end.
+#include "dl_common.h"
+#include "dl_ops.h"
+
+namespace dl {
+
+__global__ void __launch_bounds__(256) occupy_kernel(int us, float* __restrict__ sink) {
+  __shared__ float lds[19744 / 4];
+  // claim the register budget of an RCCL wave: arch VGPRs up to v255, 32 AGPRs
+  asm volatile("" ::: "v255", "a31");
+  lds[threadIdx.x] = (float)threadIdx.x;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long ticks = (unsigned long long)us * 100ull;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+  __syncthreads();
+  if (threadIdx.x == 0 && sink) sink[blockIdx.x] = lds[(blockIdx.x + 1) & 255];
+}
+
+// Control: one wave, no LDS, few registers -- fits beside any workgroup, so
+// whatever it costs the step is the price of a second active queue, not of
+// occupied CU resources.
+__global__ void __launch_bounds__(64) occupy_light_kernel(int us, float* __restrict__ sink) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long ticks = (unsigned long long)us * 100ull;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+  if (threadIdx.x == 0 && sink) sink[blockIdx.x] = 1.f;
+}
+
+void occupy_cus(int blocks, int us, uintptr_t sink, uintptr_t stream) {
+  if (blocks == 0) return;
+  if (us > 2000000) throw std::runtime_error("occupy_cus: at most 2 s");
+  if (blocks < 0)  // light control variant
+    occupy_light_kernel<<<-blocks, 64, 0, as_stream(stream)>>>(us, (float*)sink);
+  else
+    occupy_kernel<<<blocks, 256, 0, as_stream(stream)>>>(us, (float*)sink);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dl

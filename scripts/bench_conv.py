@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--tile", type=int, default=-1)
     ap.add_argument("--splits", type=int, default=-1)
     ap.add_argument("--wsplits", type=int, default=-1, help="override the wgrad split count")
+    ap.add_argument("--occupy", type=int, default=0,
+                    help="hold R CUs with RCCL-sized workgroups on a side stream while timing (diag.hip)")
     ap.add_argument("--dtile", type=int, default=-1, help="override the dgrad tile")
     ap.add_argument("--dsplits", type=int, default=-1, help="override the dgrad split count")
     ap.add_argument("--stages", default="3,0", help="fwd,wgrad LDS ring depth (wgrad 0 = per-tile default)")
@@ -88,6 +90,7 @@ def main():
         jobs.append((f"wgrad{li+1}", 2 * M * cout * K, lambda wtile=wtile, wsp=wsp: C.conv_wgrad(
             dy.data_ptr(), x.data_ptr(), slab.data_ptr(), B, H, H, cin, cout, 5, wsp, K, wtile, cur()),
             f"tile{wtile} split{wsp}"))
+        occ_stream = torch.cuda.Stream()
         for name, flops, fn, desc in jobs:
             if a.only and a.only not in name:
                 continue
@@ -101,6 +104,9 @@ def main():
                     fn()
             g.replay()
             torch.cuda.synchronize()
+            if a.occupy:
+                C.occupy_cus(a.occupy, 300000, 0, occ_stream.cuda_stream)
+                torch.cuda._sleep(2_000_000)
             ev0.record()
             g.replay()
             ev1.record()

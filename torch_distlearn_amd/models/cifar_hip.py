@@ -69,16 +69,20 @@ def _fwd_plan(M: int, N: int, K: int):
     return tile, splits
 
 
-def _wgrad_plan(cout: int, K: int, M: int):
+def _wgrad_plan(cout: int, K: int, M: int, reserve: int = 0):
     """(tile, splits) for the weight gradient.  128x128 tiles (tile 2: 4-stage
     DMA ring, fragment prefetch, one workgroup per CU) whenever Cout allows,
     else 64x64 (two per CU).  Every workgroup is one ~20 us "round", so the
     split count fills the resident slots exactly (not the next power of two:
     conv3 50 tiles x 5 splits = 250 workgroups, 26 k-steps each, beats 4 splits
-    = 200 workgroups of 32 k-steps by 1.7 us), keeping >= 512 rows per split."""
+    = 200 workgroups of 32 k-steps by 1.7 us), keeping >= 512 rows per split.
+    ``reserve`` CUs are left to a concurrent RCCL collective (its workgroups do
+    not fit beside these: parallel/comm.py)."""
     tile = 2 if cout % 128 == 0 else 1
-    bm, bn = (128, 128) if tile == 2 else (64, 64)
-    slots = 256 if tile == 2 else 512
+    if tile == 2 and "DISTLEARN_WGRAD_TILE" in os.environ:  # tuning: 0 = 128x64 tiles
+        tile = int(os.environ["DISTLEARN_WGRAD_TILE"])
+    bm, bn = {2: (128, 128), 1: (64, 64), 0: (128, 64)}[tile]
+    slots = 2 * (256 - reserve) if tile == 1 else 256 - reserve
     tiles = (cout // bm) * ((K + bn - 1) // bn)
     splits = max(1, min(slots // tiles, M // 512))
     if os.environ.get("DISTLEARN_WGRAD_POW2", "0") == "1":  # A/B: the earlier power-of-two rule
@@ -119,6 +123,26 @@ class CifarHIPExecutor:
         self.overwrites_grads = True
         for i in range(self.nb):
             self.g32[self._leaf(i, 1)].zero_()
+        self._wgrad_stages = int(os.environ.get("DISTLEARN_WGRAD_STAGES", "0"))  # tuning (3/4, 0 = per tile)
+        self.C.set_conv_stages(3, self._wgrad_stages)
+        # The dgrad convolutions run while the bucketed all-reduce is in flight
+        # (the first bucket is launched after the last layer's wgrad).  An
+        # RCCL workgroup (19.7 KiB LDS, ~280 registers/wave) shares a CU only
+        # with workgroups of <= ~72 KiB LDS here (measured with
+        # scripts/emulate_rccl.py / bench_conv.py --occupy: the 96 KiB 3-stage
+        # ring does not fit beside it, so a 256-workgroup dgrad needs a second
+        # round, +14 us; the 64 KiB 2-stage ring does, +1 us).  With a real
+        # all-reduce (world > 1) the dgrads therefore use the 2-stage ring.
+        comm = getattr(bucketer, "comm", None)
+        overlapped = comm is not None and getattr(comm, "world_size", 1) > 1
+        self.dgrad_stages = int(os.environ.get("DISTLEARN_DGRAD_STAGES", "2" if overlapped else "3"))
+        # CUs held by the concurrent collective's workgroups (wgrad grids leave them free)
+        self.cu_reserve = int(os.environ.get("DISTLEARN_CU_RESERVE",
+                                             getattr(comm, "cu_reserve", 0) if overlapped else 0))
+        if "DISTLEARN_WGRAD_PF" in os.environ:  # tuning: wgrad fragment prefetch (-1 auto, 0, 1)
+            self.C.set_conv_wgrad_pf(int(os.environ["DISTLEARN_WGRAD_PF"]))
+        if "DISTLEARN_REGION" in os.environ:  # tuning: tap-reuse region conv kernel (0 off, 1 rows, 2 + images)
+            self.C.set_conv_region(int(os.environ["DISTLEARN_REGION"]))
         if "DISTLEARN_BN_BWD_ITEMS" in os.environ:  # tuning: pooled pixels per thread of the BN backward reduce
             self.C.set_bn_bwd_items(int(os.environ["DISTLEARN_BN_BWD_ITEMS"]))
         self.side = torch.cuda.Stream(device=self.dev, priority=int(os.environ.get("DISTLEARN_SIDE_PRIORITY", "0"))) \
@@ -173,7 +197,7 @@ class CifarHIPExecutor:
             g = C.bn_bwd_blocks(B, h, h, cout)
             self.bwd_blocks.append(g)
             self.bwd_part.append(torch.empty(g, 2, cout, device=d))
-            tile_w, splits_w = _wgrad_plan(cout, K, M)
+            tile_w, splits_w = _wgrad_plan(cout, K, M, self.cu_reserve)
             direct = splits_w == 1 and cin == self.cins_real[i]
             self.wplan.append((tile_w, splits_w, direct))
             if not direct:
@@ -334,8 +358,12 @@ class CifarHIPExecutor:
                     self._ready(self._leaf(i, j))
             if i > 0:
                 dt, ds = self.dgrad_plan[i]
+                if self.dgrad_stages != 3:
+                    C.set_conv_stages(self.dgrad_stages, self._wgrad_stages)
                 C.conv_fwd(dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), 0,
                            self.slabs.data_ptr(), B, h, h, cout, cin, KSIZE, dt, ds, s)
+                if self.dgrad_stages != 3:
+                    C.set_conv_stages(3, self._wgrad_stages)
         if self.side_wgrad or self.side_reduce:
             main.wait_stream(side)  # join
         return self.loss[0]

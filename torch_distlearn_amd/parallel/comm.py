@@ -134,11 +134,29 @@ class ProcessGroupCommunicator(Communicator):
         dist.recv(t, src=peer, group=self.data)
 
 
+# CU footprint of RCCL's collectives: one workgroup per channel (rcclGenericKernel:
+# 256 threads, ~280 registers/wave, 19.7 KiB LDS).  A compute workgroup shares a CU
+# with it only if it needs <= ~72 KiB LDS and <= 112 registers/wave (8-wave
+# workgroups); otherwise that CU is lost to the compute grid for the collective's
+# lifetime, and a grid sized to the whole chip needs a second round
+# (scripts/emulate_rccl.py, bench_conv.py --occupy).  The channel count is therefore
+# capped (NCCL_MAX_NCHANNELS, unless the user set it) and the executor sizes the
+# grids of the kernels that overlap the bucketed all-reduce to leave that many CUs.
+DEFAULT_RCCL_CHANNELS = 32
+
+
+def rccl_channel_cap() -> int:
+    return int(os.environ.get("NCCL_MAX_NCHANNELS", DEFAULT_RCCL_CHANNELS))
+
+
 class RcclCommunicator(Communicator):
     """Native RCCL data plane (C++), gloo control plane."""
 
     def __init__(self, rank: int, world_size: int, device: torch.device, ctrl_group=None):
         C = native()
+        if world_size > 1:
+            os.environ.setdefault("NCCL_MAX_NCHANNELS", str(DEFAULT_RCCL_CHANNELS))  # read at comm init
+        self.cu_reserve = rccl_channel_cap() if world_size > 1 else 0
         self.ctrl = ctrl_group
         self.rank, self.world_size = rank, world_size
         self.device = torch.device(device)
