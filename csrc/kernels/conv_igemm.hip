@@ -1519,6 +1519,10 @@ void set_conv_region(int on) {
 // one that runs beside the all-reduce) also stays at <= 112 VGPRs, so two
 // of its waves fit a SIMD next to a 288-VGPR RCCL wave; the BN = 128
 // instance (127 VGPRs) only runs in the forward, before any collective.
+// Measured with one CU held by a workgroup of RCCL's footprint
+// (bench_conv.py --occupy 1): the dgrad instance (~126 KiB) +1 us, while the
+// streaming kernel's 3-stage ring (96 KiB, 90 VGPRs) loses 14 us -- the executor
+// switches the overlapped dgrads to its 2-stage ring (models/cifar_hip.py).
 constexpr int kRegionLdsCap = 160 * 1024 - 20 * 1024;
 
 // Region geometry for a BM = 128 tile, or false if the shape does not fit the

@@ -126,13 +126,13 @@ class CifarHIPExecutor:
         self._wgrad_stages = int(os.environ.get("DISTLEARN_WGRAD_STAGES", "0"))  # tuning (3/4, 0 = per tile)
         self.C.set_conv_stages(3, self._wgrad_stages)
         # The dgrad convolutions run while the bucketed all-reduce is in flight
-        # (the first bucket is launched after the last layer's wgrad).  An
-        # RCCL workgroup (19.7 KiB LDS, ~280 registers/wave) shares a CU only
-        # with workgroups of <= ~72 KiB LDS here (measured with
-        # scripts/emulate_rccl.py / bench_conv.py --occupy: the 96 KiB 3-stage
-        # ring does not fit beside it, so a 256-workgroup dgrad needs a second
-        # round, +14 us; the 64 KiB 2-stage ring does, +1 us).  With a real
-        # all-reduce (world > 1) the dgrads therefore use the 2-stage ring.
+        # (the first bucket is launched after the last layer's wgrad).  With one
+        # CU held by a workgroup of RCCL's footprint (19.7 KiB LDS, ~280
+        # registers/wave; scripts/emulate_rccl.py, bench_conv.py --occupy 1) the
+        # 256-workgroup streaming dgrad with the 3-stage ring (96 KiB LDS) slows
+        # by 14 us (dgrad3/dgrad4 23 -> 37 us), with the 2-stage ring (64 KiB,
+        # two workgroups fit a CU) by 1 us; the region dgrad (layer 2) by 1 us.
+        # With a real all-reduce (world > 1) the dgrads use the 2-stage ring.
         comm = getattr(bucketer, "comm", None)
         overlapped = comm is not None and getattr(comm, "world_size", 1) > 1
         self.dgrad_stages = int(os.environ.get("DISTLEARN_DGRAD_STAGES", "2" if overlapped else "3"))

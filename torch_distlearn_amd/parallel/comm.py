@@ -135,11 +135,11 @@ class ProcessGroupCommunicator(Communicator):
 
 
 # CU footprint of RCCL's collectives: one workgroup per channel (rcclGenericKernel:
-# 256 threads, ~280 registers/wave, 19.7 KiB LDS).  A compute workgroup shares a CU
-# with it only if it needs <= ~72 KiB LDS and <= 112 registers/wave (8-wave
-# workgroups); otherwise that CU is lost to the compute grid for the collective's
-# lifetime, and a grid sized to the whole chip needs a second round
-# (scripts/emulate_rccl.py, bench_conv.py --occupy).  The channel count is therefore
+# 256 threads, ~280 registers/wave, 19.7 KiB LDS).  Compute kernels that do not fit
+# beside it (here: the 128x128 wgrad, 141 registers/wave, and the 3-stage streaming
+# conv) lose that CU for the collective's lifetime, and a grid sized to the whole chip
+# then needs a second round (measured per kernel with scripts/emulate_rccl.py and
+# bench_conv.py --occupy).  The channel count is therefore
 # capped (NCCL_MAX_NCHANNELS, unless the user set it) and the executor sizes the
 # grids of the kernels that overlap the bucketed all-reduce to leave that many CUs.
 DEFAULT_RCCL_CHANNELS = 32
