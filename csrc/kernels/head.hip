@@ -16,12 +16,26 @@
 
 namespace dl {
 
-template <int NC>
+// POOL: the head's input h is not read but computed here from the last conv
+// block's pre-BN output y [B][yH][yW][yC] (bf16) and its BN coefficients
+// (coef [4][yC]: scale at 2*yC, shift at 3*yC) -- the work of
+// bn_relu_pool_fwd for that block, with the identical operation order and
+// bf16 rounding -- and written to h_out for head_wgrad (one launch and one
+// pass over h fewer per step).  Needs F == 2048 (one 8-feature chunk per thread).
+struct HeadPool {
+  const bf16_t* y;
+  const float* coef;
+  bf16_t* h_out;
+  int yH, yW, yC;
+};
+
+template <int NC, bool POOL = false>
 __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restrict__ h, const float* __restrict__ w,
                                                            const float* __restrict__ bias,
                                                            const int64_t* __restrict__ labels, int F, int B,
                                                            float* __restrict__ logits_out, float* __restrict__ dlogits,
-                                                           float* __restrict__ loss_b, bf16_t* __restrict__ dh) {
+                                                           float* __restrict__ loss_b, bf16_t* __restrict__ dh,
+                                                           const HeadPool hp = HeadPool{}) {
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   __shared__ float red[4][NC];
   __shared__ float dl[NC];
@@ -35,7 +49,41 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
   float4 wc[NC][2];
   if (one) {
     const int j0 = tid * 8;
-    const uint4 hv = *reinterpret_cast<const uint4*>(hb + j0);
+    uint4 hv;
+    if constexpr (POOL) {
+      // feature j0 = (oh * Wo + ow) * yC + c0 of the pooled NHWC map
+      const int Wo = hp.yW >> 1;
+      const int pix = j0 / hp.yC, c0 = j0 - pix * hp.yC;
+      const int oh = pix / Wo, ow = pix - oh * Wo;
+      const bf16_t* base = hp.y + (((int64_t)b * hp.yH + 2 * oh) * hp.yW + 2 * ow) * hp.yC + c0;
+      const uint4 v[4] = {*reinterpret_cast<const uint4*>(base), *reinterpret_cast<const uint4*>(base + hp.yC),
+                          *reinterpret_cast<const uint4*>(base + (int64_t)hp.yW * hp.yC),
+                          *reinterpret_cast<const uint4*>(base + (int64_t)hp.yW * hp.yC + hp.yC)};
+      const float4 sc0 = *reinterpret_cast<const float4*>(hp.coef + 2 * hp.yC + c0);
+      const float4 sc1 = *reinterpret_cast<const float4*>(hp.coef + 2 * hp.yC + c0 + 4);
+      const float4 sh0 = *reinterpret_cast<const float4*>(hp.coef + 3 * hp.yC + c0);
+      const float4 sh1 = *reinterpret_cast<const float4*>(hp.coef + 3 * hp.yC + c0 + 4);
+      const float sc[8] = {sc0.x, sc0.y, sc0.z, sc0.w, sc1.x, sc1.y, sc1.z, sc1.w};
+      const float sh[8] = {sh0.x, sh0.y, sh0.z, sh0.w, sh1.x, sh1.y, sh1.z, sh1.w};
+      float mx[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float f[8] = {lo_bf16(v[q].x), hi_bf16(v[q].x), lo_bf16(v[q].y), hi_bf16(v[q].y),
+                            lo_bf16(v[q].z), hi_bf16(v[q].z), lo_bf16(v[q].w), hi_bf16(v[q].w)};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float z = fmaf(sc[k], f[k], sh[k]);
+          mx[k] = q == 0 ? z : fmaxf(mx[k], z);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) mx[k] = fmaxf(mx[k], 0.f);
+      hv = make_uint4(pack_bf16x2(mx[0], mx[1]), pack_bf16x2(mx[2], mx[3]), pack_bf16x2(mx[4], mx[5]),
+                      pack_bf16x2(mx[6], mx[7]));
+      *reinterpret_cast<uint4*>(hp.h_out + (int64_t)b * F + j0) = hv;
+    } else {
+      hv = *reinterpret_cast<const uint4*>(hb + j0);
+    }
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       wc[c][0] = *reinterpret_cast<const float4*>(w + (int64_t)c * F + j0);
@@ -214,6 +262,20 @@ void head_fwd_bwd(uintptr_t h, uintptr_t w, uintptr_t bias, uintptr_t labels, in
   head_fwd_bwd_kernel<10><<<B, 256, 0, as_stream(stream)>>>((const bf16_t*)h, (const float*)w, (const float*)bias,
                                                             (const int64_t*)labels, F, B, (float*)logits_out,
                                                             (float*)dlogits, (float*)loss_b, (bf16_t*)dh);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+void head_fwd_bwd_pool(uintptr_t y, uintptr_t coef, int yH, int yW, int yC, uintptr_t h_out, uintptr_t w,
+                       uintptr_t bias, uintptr_t labels, int B, int NC, uintptr_t logits_out, uintptr_t dlogits,
+                       uintptr_t loss_b, uintptr_t dh, uintptr_t stream) {
+  if (NC != 10) throw std::runtime_error("head_fwd_bwd_pool: built for 10 classes");
+  const int F = (yH / 2) * (yW / 2) * yC;
+  if (F != 2048 || yC % 8 != 0 || yH % 2 != 0 || yW % 2 != 0)
+    throw std::runtime_error("head_fwd_bwd_pool: needs a 2048-feature pooled map, C % 8 == 0");
+  const HeadPool hp{(const bf16_t*)y, (const float*)coef, (bf16_t*)h_out, yH, yW, yC};
+  head_fwd_bwd_kernel<10, true><<<B, 256, 0, as_stream(stream)>>>(
+      nullptr, (const float*)w, (const float*)bias, (const int64_t*)labels, F, B, (float*)logits_out,
+      (float*)dlogits, (float*)loss_b, (bf16_t*)dh, hp);
   DL_HIP_CHECK(hipGetLastError());
 }
 

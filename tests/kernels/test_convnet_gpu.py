@@ -277,6 +277,37 @@ def test_head(C):
     assert _rel(dh, hr.grad) < 5e-3
 
 
+def test_head_with_fused_pool(C):
+    """head_fwd_bwd_pool (last block's BN/ReLU/pool inside the head kernel) is
+    bitwise identical to bn_relu_pool_fwd followed by head_fwd_bwd."""
+    dev = torch.device("cuda")
+    B, H, Cc, NC = 29, 4, 512, 10
+    Fd = (H // 2) ** 2 * Cc
+    g = torch.Generator(device=dev).manual_seed(5)
+    y = torch.randn(B, H, H, Cc, device=dev, generator=g).to(torch.bfloat16)
+    coef = torch.randn(4, Cc, device=dev, generator=g)
+    w = torch.randn(NC, Fd, device=dev, generator=g) * 0.02
+    b = torch.randn(NC, device=dev, generator=g) * 0.1
+    lab = torch.randint(0, NC, (B,), device=dev, generator=g)
+    outs = []
+    for fused in (False, True):
+        h = torch.full((B, Fd), 7.0, dtype=torch.bfloat16, device=dev)
+        logp, dlog = torch.empty(B, NC, device=dev), torch.empty(B, NC, device=dev)
+        lb, dh = torch.empty(B, device=dev), torch.empty(B, Fd, dtype=torch.bfloat16, device=dev)
+        if fused:
+            C.head_fwd_bwd_pool(y.data_ptr(), coef.data_ptr(), H, H, Cc, h.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                lab.data_ptr(), B, NC, logp.data_ptr(), dlog.data_ptr(), lb.data_ptr(),
+                                dh.data_ptr(), _s())
+        else:
+            C.bn_relu_pool_fwd(y.data_ptr(), coef.data_ptr(), h.data_ptr(), B, H, H, Cc, 0, _s())
+            C.head_fwd_bwd(h.data_ptr(), w.data_ptr(), b.data_ptr(), lab.data_ptr(), Fd, B, NC, logp.data_ptr(),
+                           dlog.data_ptr(), lb.data_ptr(), dh.data_ptr(), _s())
+        torch.cuda.synchronize()
+        outs.append((h, logp, dlog, lb, dh))
+    for a, b_ in zip(*outs):
+        assert torch.equal(a, b_)
+
+
 def test_executor_matches_torch_model(C):
     """Whole-model check: HIP executor loss + every gradient vs an fp32 PyTorch
     reference of the same parameters; the error must be within 2x of what

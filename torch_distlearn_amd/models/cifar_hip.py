@@ -141,6 +141,9 @@ class CifarHIPExecutor:
                                              getattr(comm, "cu_reserve", 0) if overlapped else 0))
         if "DISTLEARN_WGRAD_PF" in os.environ:  # tuning: wgrad fragment prefetch (-1 auto, 0, 1)
             self.C.set_conv_wgrad_pf(int(os.environ["DISTLEARN_WGRAD_PF"]))
+        # fuse the last block's BN/ReLU/pool into the head kernel (2048 pooled features)
+        self.head_pool = (os.environ.get("DISTLEARN_HEAD_POOL", "1") == "1"
+                          and (self.hs[-1] // 2) ** 2 * self.couts[-1] == 2048 and self.nclass == 10)
         if "DISTLEARN_REGION" in os.environ:  # tuning: tap-reuse region conv kernel (0 off, 1 rows, 2 + images)
             self.C.set_conv_region(int(os.environ["DISTLEARN_REGION"]))
         if "DISTLEARN_BN_BWD_ITEMS" in os.environ:  # tuning: pooled pixels per thread of the BN backward reduce
@@ -259,7 +262,9 @@ class CifarHIPExecutor:
         self.C.prep_step(0, 0, 0, self.cins_real[0], CIN_PAD, 0, 0, 0, 0, 0, 0, KSIZE * KSIZE, self.cins_real[0],
                          CIN_PAD, *self._transpose_args(True), s)
 
-    def _forward(self, B: int, s: int, train: bool):
+    def _forward(self, B: int, s: int, train: bool, pool_last: bool = True):
+        """Conv -> BN finalize -> BN/ReLU/pool per block.  ``pool_last=False``
+        leaves the last block's pool to the head kernel (head_fwd_bwd_pool)."""
         C = self.C
         inp = self.x8
         for i in range(self.nb):
@@ -274,8 +279,9 @@ class CifarHIPExecutor:
                           self.p32[self._leaf(i, 3)].data_ptr(), self.p32[self._leaf(i, 1)].data_ptr(),
                           self.rm[i].data_ptr(), self.rv[i].data_ptr(), BN_EPS, BN_MOMENTUM, 0 if train else 1,
                           self.coef[i].data_ptr(), s)
-            C.bn_relu_pool_fwd(self.y[i].data_ptr(), self.coef[i].data_ptr(), self.p[i].data_ptr(), B, h, h, cout,
-                               SPAD if i + 1 < self.nb else 0, s)
+            if pool_last or i + 1 < self.nb:
+                C.bn_relu_pool_fwd(self.y[i].data_ptr(), self.coef[i].data_ptr(), self.p[i].data_ptr(), B, h, h,
+                                   cout, SPAD if i + 1 < self.nb else 0, s)
             inp = self.p[i]
 
     # ------------------------------------------------------------------ API
@@ -299,11 +305,18 @@ class CifarHIPExecutor:
             self._prep_transposes(ss)
             wt_ready = torch.cuda.Event()
             wt_ready.record(side)
-        self._forward(B, s, train=True)
+        self._forward(B, s, train=True, pool_last=not self.head_pool)
         nfc = 4 * self.nb
-        C.head_fwd_bwd(self.p[-1].data_ptr(), self.p32[nfc].data_ptr(), self.p32[nfc + 1].data_ptr(),
-                       labels.data_ptr(), self.feat, B, self.nclass, self.logits.data_ptr(), self.dlogits.data_ptr(),
-                       self.loss_b.data_ptr(), self.dP[-1].data_ptr(), s)
+        if self.head_pool:  # the last block's BN/ReLU/pool runs inside the head kernel (writes p[-1])
+            hl = self.hs[-1]
+            C.head_fwd_bwd_pool(self.y[-1].data_ptr(), self.coef[-1].data_ptr(), hl, hl, self.couts[-1],
+                                self.p[-1].data_ptr(), self.p32[nfc].data_ptr(), self.p32[nfc + 1].data_ptr(),
+                                labels.data_ptr(), B, self.nclass, self.logits.data_ptr(), self.dlogits.data_ptr(),
+                                self.loss_b.data_ptr(), self.dP[-1].data_ptr(), s)
+        else:
+            C.head_fwd_bwd(self.p[-1].data_ptr(), self.p32[nfc].data_ptr(), self.p32[nfc + 1].data_ptr(),
+                           labels.data_ptr(), self.feat, B, self.nclass, self.logits.data_ptr(),
+                           self.dlogits.data_ptr(), self.loss_b.data_ptr(), self.dP[-1].data_ptr(), s)
         C.head_wgrad(self.p[-1].data_ptr(), self.dlogits.data_ptr(), self.loss_b.data_ptr(), self.feat, B,
                      self.nclass, self.g32[nfc].data_ptr(), self.g32[nfc + 1].data_ptr(), self.loss.data_ptr(),
                      self.flat.slot.data_ptr(), ctr, s)
