@@ -53,6 +53,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_relu_pool_bwd_apply", &bn_relu_pool_bwd_apply);
   m.def("head_fwd_bwd", &head_fwd_bwd);
   m.def("head_fwd_bwd_pool", &head_fwd_bwd_pool);
+  m.def("bn_bwd_reduce_head", &bn_bwd_reduce_head);
   m.def("head_wgrad", &head_wgrad);
 
   // ---- RCCL communicator ------------------------------------------------------

@@ -22,6 +22,7 @@
 // mean + bias so eval mode (running statistics) is exact.
 #include "dl_common.h"
 #include "dl_ops.h"
+#include "head_wgrad_dev.h"
 
 namespace dl {
 
@@ -192,16 +193,15 @@ __device__ __forceinline__ void bwd_window(const bf16_t* __restrict__ y, const b
 // ---------------------------------------------------------------------------
 // backward reduce: partial[blk][0][c] = sum dz, partial[blk][1][c] = sum dz*xhat
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) bn_relu_pool_bwd_reduce_kernel(const bf16_t* __restrict__ y,
-                                                                      const bf16_t* __restrict__ dP,
-                                                                      const float* __restrict__ coef,
-                                                                      float* __restrict__ partial, int B, int H,
-                                                                      int W, int C) {
+// Body of the reduce for block `bid` of `nblk` (the reduce part of the grid).
+__device__ __forceinline__ void bwd_reduce_body(const bf16_t* __restrict__ y, const bf16_t* __restrict__ dP,
+                                                const float* __restrict__ coef, float* __restrict__ partial, int B,
+                                                int H, int W, int C, int bid, int nblk) {
   const int C8 = C >> 3, Ho = H >> 1, Wo = W >> 1;
   const int64_t total = (int64_t)B * Ho * Wo * C8;
   // grid-stride keeps the channel chunk fixed per thread (stride % C8 == 0)
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)nblk * blockDim.x;
+  const int64_t i0 = (int64_t)bid * blockDim.x + threadIdx.x;
   const int c8 = (int)(i0 % C8), c0 = c8 * 8;
   BwdCtx cx;
   load8(cx.mu, coef + c0);
@@ -272,12 +272,45 @@ __global__ void __launch_bounds__(256) bn_relu_pool_bwd_reduce_kernel(const bf16
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     const int ch = c >> 3, k = c & 7;
     // threads with (blockIdx.x*256 + tid) % C8 == ch
-    const int first = (int)(((int64_t)ch - ((int64_t)blockIdx.x * blockDim.x) % C8 + C8) % C8);
+    const int first = (int)(((int64_t)ch - ((int64_t)bid * blockDim.x) % C8 + C8) % C8);
     float a = 0.f, bsum = 0.f;
     for (int t = first; t < (int)blockDim.x; t += C8) { a += red[t][k]; bsum += red[t][8 + k]; }
-    partial[(int64_t)blockIdx.x * 2 * C + c] = a;
-    partial[(int64_t)blockIdx.x * 2 * C + C + c] = bsum;
+    partial[(int64_t)bid * 2 * C + c] = a;
+    partial[(int64_t)bid * 2 * C + C + c] = bsum;
   }
+}
+
+__global__ void __launch_bounds__(256) bn_relu_pool_bwd_reduce_kernel(const bf16_t* __restrict__ y,
+                                                                      const bf16_t* __restrict__ dP,
+                                                                      const float* __restrict__ coef,
+                                                                      float* __restrict__ partial, int B, int H,
+                                                                      int W, int C) {
+  bwd_reduce_body(y, dP, coef, partial, B, H, W, C, (int)blockIdx.x, (int)gridDim.x);
+}
+
+// One launch for two independent jobs that both wait only for the head:
+// blocks [0, G) = the last conv block's BN backward reduce, blocks [G, ...) =
+// the classifier weight gradient (head_wgrad_body).  Saves a kernel boundary
+// and runs the small head job beside the reduce instead of after it.
+struct HeadWgradArgs {
+  const bf16_t* h;
+  const float* dlogits;
+  const float* loss_b;
+  int F, B;
+  float *dw, *db, *loss, *slot;
+  unsigned long long* step_ctr;
+};
+
+__global__ void __launch_bounds__(256) bwd_reduce_head_kernel(const bf16_t* __restrict__ y,
+                                                              const bf16_t* __restrict__ dP,
+                                                              const float* __restrict__ coef,
+                                                              float* __restrict__ partial, int B, int H, int W, int C,
+                                                              int G, const HeadWgradArgs ha) {
+  if ((int)blockIdx.x < G)
+    bwd_reduce_body(y, dP, coef, partial, B, H, W, C, (int)blockIdx.x, G);
+  else
+    head_wgrad_body<10>(ha.h, ha.dlogits, ha.loss_b, ha.F, ha.B, ha.dw, ha.db, ha.loss, ha.slot, ha.step_ctr,
+                        (int)blockIdx.x - G);
 }
 
 // backward finalize: dgamma = sum(dz*xhat), dbeta = sum(dz);
@@ -393,6 +426,20 @@ void bn_relu_pool_bwd_reduce(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_
   if ((256 % (C / 8)) != 0) throw std::runtime_error("bn_relu_pool_bwd_reduce: C/8 must divide 256");
   bn_relu_pool_bwd_reduce_kernel<<<blocks, 256, 0, as_stream(stream)>>>(
       (const bf16_t*)y, (const bf16_t*)dP, (const float*)coef, (float*)partial, B, H, W, C);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+void bn_bwd_reduce_head(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t partial, int B, int H, int W, int C,
+                        int blocks, uintptr_t h, uintptr_t dlogits, uintptr_t loss_b, int F, int NC, uintptr_t dw,
+                        uintptr_t db, uintptr_t loss, uintptr_t slot, uintptr_t step_ctr, uintptr_t stream) {
+  check_c(C);
+  if ((256 % (C / 8)) != 0) throw std::runtime_error("bn_bwd_reduce_head: C/8 must divide 256");
+  if (NC != 10) throw std::runtime_error("bn_bwd_reduce_head: built for 10 classes");
+  const HeadWgradArgs ha{(const bf16_t*)h, (const float*)dlogits, (const float*)loss_b, F, B, (float*)dw,
+                         (float*)db, (float*)loss, (float*)slot, (unsigned long long*)step_ctr};
+  const int head_blocks = (F + 31) / 32 + 1;
+  bwd_reduce_head_kernel<<<blocks + head_blocks, 256, 0, as_stream(stream)>>>(
+      (const bf16_t*)y, (const bf16_t*)dP, (const float*)coef, (float*)partial, B, H, W, C, blocks, ha);
   DL_HIP_CHECK(hipGetLastError());
 }
 

@@ -308,6 +308,41 @@ def test_head_with_fused_pool(C):
         assert torch.equal(a, b_)
 
 
+def test_bwd_reduce_head_fused(C):
+    """bn_bwd_reduce_head (one launch) == bn_relu_pool_bwd_reduce + head_wgrad, bitwise."""
+    dev = torch.device("cuda")
+    B, H, Cc, NC = 32, 4, 512, 10
+    Fd = (H // 2) ** 2 * Cc
+    g = torch.Generator(device=dev).manual_seed(9)
+    y = torch.randn(B, H, H, Cc, device=dev, generator=g).to(torch.bfloat16)
+    dP = torch.randn(B, H // 2, H // 2, Cc, device=dev, generator=g).to(torch.bfloat16)
+    coef = torch.randn(4, Cc, device=dev, generator=g)
+    h = torch.randn(B, Fd, device=dev, generator=g).to(torch.bfloat16)
+    dlog = torch.randn(B, NC, device=dev, generator=g)
+    lb = torch.rand(B, device=dev, generator=g)
+    G = C.bn_bwd_blocks(B, H, H, Cc)
+    res = []
+    for fused in (False, True):
+        part = torch.full((G, 2 * Cc), float("nan"), device=dev)
+        dw, db = torch.full((NC, Fd), float("nan"), device=dev), torch.full((NC,), float("nan"), device=dev)
+        loss, slot = torch.zeros(1, device=dev), torch.zeros(1, device=dev)
+        ctr = torch.zeros(2, dtype=torch.int64, device=dev)
+        if fused:
+            C.bn_bwd_reduce_head(y.data_ptr(), dP.data_ptr(), coef.data_ptr(), part.data_ptr(), B, H, H, Cc, G,
+                                 h.data_ptr(), dlog.data_ptr(), lb.data_ptr(), Fd, NC, dw.data_ptr(), db.data_ptr(),
+                                 loss.data_ptr(), slot.data_ptr(), ctr.data_ptr(), _s())
+        else:
+            C.bn_relu_pool_bwd_reduce(y.data_ptr(), dP.data_ptr(), coef.data_ptr(), part.data_ptr(), B, H, H, Cc, G,
+                                      _s())
+            C.head_wgrad(h.data_ptr(), dlog.data_ptr(), lb.data_ptr(), Fd, B, NC, dw.data_ptr(), db.data_ptr(),
+                         loss.data_ptr(), slot.data_ptr(), ctr.data_ptr(), _s())
+        torch.cuda.synchronize()
+        res.append((part, dw, db, loss, slot, ctr))
+    for a, b_ in zip(*res):
+        assert torch.equal(a, b_)
+    assert int(res[1][5][0]) == 1 and float(res[1][4]) == 1.0
+
+
 def test_executor_matches_torch_model(C):
     """Whole-model check: HIP executor loss + every gradient vs an fp32 PyTorch
     reference of the same parameters; the error must be within 2x of what

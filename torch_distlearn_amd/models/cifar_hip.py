@@ -144,6 +144,7 @@ class CifarHIPExecutor:
         # fuse the last block's BN/ReLU/pool into the head kernel (2048 pooled features)
         self.head_pool = (os.environ.get("DISTLEARN_HEAD_POOL", "1") == "1"
                           and (self.hs[-1] // 2) ** 2 * self.couts[-1] == 2048 and self.nclass == 10)
+        self.head_wgrad_fused = os.environ.get("DISTLEARN_HEAD_WGRAD_FUSED", "1") == "1" and self.nclass == 10
         if "DISTLEARN_REGION" in os.environ:  # tuning: tap-reuse region conv kernel (0 off, 1 rows, 2 + images)
             self.C.set_conv_region(int(os.environ["DISTLEARN_REGION"]))
         if "DISTLEARN_BN_BWD_ITEMS" in os.environ:  # tuning: pooled pixels per thread of the BN backward reduce
@@ -317,11 +318,14 @@ class CifarHIPExecutor:
             C.head_fwd_bwd(self.p[-1].data_ptr(), self.p32[nfc].data_ptr(), self.p32[nfc + 1].data_ptr(),
                            labels.data_ptr(), self.feat, B, self.nclass, self.logits.data_ptr(),
                            self.dlogits.data_ptr(), self.loss_b.data_ptr(), self.dP[-1].data_ptr(), s)
-        C.head_wgrad(self.p[-1].data_ptr(), self.dlogits.data_ptr(), self.loss_b.data_ptr(), self.feat, B,
+        head_args = (self.p[-1].data_ptr(), self.dlogits.data_ptr(), self.loss_b.data_ptr(), self.feat,
                      self.nclass, self.g32[nfc].data_ptr(), self.g32[nfc + 1].data_ptr(), self.loss.data_ptr(),
-                     self.flat.slot.data_ptr(), ctr, s)
-        self._ready(nfc)
-        self._ready(nfc + 1)
+                     self.flat.slot.data_ptr(), ctr)
+        if not self.head_wgrad_fused:
+            h_, dl_, lb_, F_, nc_, dw_, db_, loss_, slot_, ctr_ = head_args
+            C.head_wgrad(h_, dl_, lb_, F_, B, nc_, dw_, db_, loss_, slot_, ctr_, s)
+            self._ready(nfc)
+            self._ready(nfc + 1)
         if self.fork_transposes:
             main.wait_event(wt_ready)
         ws = side if self.side_wgrad else main
@@ -332,8 +336,15 @@ class CifarHIPExecutor:
             M = B * h * h
             G = self.bwd_blocks[i]
             dY = self.dYs[i]
-            C.bn_relu_pool_bwd_reduce(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
-                                      self.bwd_part[i].data_ptr(), B, h, h, cout, G, s)
+            if i == self.nb - 1 and self.head_wgrad_fused:
+                # one launch: this block's BN backward reduce + the classifier weight gradient
+                C.bn_bwd_reduce_head(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
+                                     self.bwd_part[i].data_ptr(), B, h, h, cout, G, *head_args, s)
+                self._ready(nfc)
+                self._ready(nfc + 1)
+            else:
+                C.bn_relu_pool_bwd_reduce(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
+                                          self.bwd_part[i].data_ptr(), B, h, h, cout, G, s)
             C.bn_bwd_finalize(self.bwd_part[i].data_ptr(), G, cout, M, self.p32[self._leaf(i, 2)].data_ptr(),
                               self.coef[i].data_ptr(), self.g32[self._leaf(i, 2)].data_ptr(),
                               self.g32[self._leaf(i, 3)].data_ptr(), self.acoef[i].data_ptr(), s)
