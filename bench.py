@@ -111,6 +111,8 @@ def main():
     if a.bucket_mb is None:
         a.bucket_mb = 1.0 if a.model == "cifar10" else 16.0
     backend = a.backend if (a.model == "cifar10" and not cpu) else "torch"
+    if backend == "torch" and not cpu and os.environ.get("DISTLEARN_MIOPEN_FIND", "0") == "1":
+        torch.backends.cudnn.benchmark = True  # MIOpen exhaustive find per conv shape (warmup pays it)
     cdt = torch.float32 if cpu else torch.bfloat16
 
     from torch_distlearn_amd import Tree

@@ -76,3 +76,18 @@ def test_bench_contract_cpu(algo):
     workers = 2 if algo == "async" else 3
     assert out["config"]["global_batch"] == 4 * workers
     assert abs(out["value"] - 4 * workers * 1000.0 / out["ms_per_step"]) / out["value"] < 1e-3
+
+
+def test_allreduce_bw_script_gloo():
+    # scripts/allreduce_bw.py (data-plane bandwidth sweep) on 2 gloo ranks
+    import json
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", "29563", os.path.join(ROOT, "scripts", "allreduce_bw.py"), "--device", "cpu",
+           "--max-mb", "1", "--iters", "2", "--warmup", "1"]
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rows = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert [x["bytes"] for x in rows] == [65536, 262144, 1048576]
+    assert all(x["n_ranks"] == 2 and x["busbw_GBps"] > 0 for x in rows)

@@ -13,9 +13,17 @@ from __future__ import annotations
 
 from typing import List, Optional
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+# BatchNorm precision: "mixed" (default) feeds the bf16 activation straight to
+# the BN kernel, which keeps fp32 statistics / affine parameters internally;
+# "fp32" materialises an fp32 copy of every activation first (one extra full
+# read + write of each BN input and output in HBM).
+_BN_MODE = os.environ.get("DISTLEARN_RESNET_BN", "mixed")
 
 
 class _BN(nn.Module):
@@ -27,6 +35,9 @@ class _BN(nn.Module):
         self.register_buffer("running_var", torch.ones(c))
 
     def forward(self, x):
+        if _BN_MODE == "mixed" and x.is_cuda:
+            return F.batch_norm(x, self.running_mean, self.running_var, self.weight, self.bias, self.training, 0.1,
+                                1e-5)
         y = F.batch_norm(x.float(), self.running_mean, self.running_var, self.weight, self.bias, self.training, 0.1,
                          1e-5)
         return y.to(x.dtype)
