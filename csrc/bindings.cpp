@@ -23,6 +23,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("multi_copy", &multi_copy);
   m.def("confusion_update", &confusion_update);
+  m.def("bn_nhwc_fwd", &bn_nhwc_fwd);
+  m.def("bn_nhwc_bwd", &bn_nhwc_bwd);
   m.def("gather_normalize", &gather_normalize);
 
   // ---- convnet kernels (MFMA implicit GEMM, BN/ReLU/pool, classifier head) ------

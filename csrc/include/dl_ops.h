@@ -20,6 +20,12 @@ void cast_f32_bf16(uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream);
 void multi_copy(uintptr_t segs, int nseg, int64_t max_bytes, uintptr_t stream);
 
 // metrics.hip ---------------------------------------------------------------
+// channels-last training BatchNorm (+ReLU, +residual) for the ResNet-50 path
+void bn_nhwc_fwd(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b, uintptr_t save,
+                 uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps, double momentum, int relu,
+                 uintptr_t stream);
+void bn_nhwc_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t acc, uintptr_t dx,
+                 uintptr_t dres, uintptr_t dw, uintptr_t db, int64_t M, int C, int relu, uintptr_t stream);
 void confusion_update(uintptr_t pred, int pred_is_bf16, uintptr_t target, uintptr_t mat, int B, int C,
                       uintptr_t stream);
 void gather_normalize(uintptr_t images, uintptr_t idx, uintptr_t out, int B, int HW, int Cs, int Cd, float m0,

@@ -1,0 +1,296 @@
+// Channels-last (NHWC) training BatchNorm for the ResNet-50 path, fused with
+// the activation and the residual add of a bottleneck:
+//
+//   forward   y  = act(x * scale + shift [+ res])        scale = w * invstd
+//   backward  g  = dy * (y > 0)            (relu; dres = g when fused with +res)
+//             dx = w * invstd * (g - mean(g) - xhat * mean(g * xhat))
+//
+// bf16 activations, fp32 statistics.  Replaces MIOpen's BN (+ torch's separate
+// ReLU / add / ReLU-backward passes, each a full HBM round trip of the
+// activation): measured in the ResNet-50 profile at 34 % (BN) + 19 %
+// (elementwise) of the step (profiles/r1_resnet50_kernels.txt).
+//
+// Layout: x is [M, C] (M = N*H*W rows), each thread owns 8 consecutive
+// channels (one 16-byte load per row).  A block covers CVB channel vectors
+// (<= 256 channels) and RPI = 256 / CVB rows per iteration; the grid is
+// (row blocks, channel groups).  Per-channel sums are reduced in LDS inside a
+// block and across blocks with one fp32 global atomic per channel per block
+// (vector-memory atomics; acc is zeroed by the host before each reduce).
+// The apply kernels recompute mean / invstd from the sums; block (0, g) writes
+// the saved statistics (and running stats / weight gradients) of its channels.
+#include "dl_common.h"
+
+namespace dl {
+
+namespace {
+
+constexpr int kThreads = 256;
+
+struct BnGeom {
+  int64_t M;
+  int C;
+  int CVB;             // channel vectors (of 8) per block
+  int RPI;             // rows per block iteration (= 256 / CVB)
+  int64_t rows_per_block;
+};
+
+__device__ __forceinline__ void unpack8(u32x4 v, float* f) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    f[2 * k] = __uint_as_float(v[k] << 16);
+    f[2 * k + 1] = __uint_as_float(v[k] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ u32x4 pack8(const float* f) {
+  u32x4 v;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    v[k] = (uint32_t)f32_to_bf16(f[2 * k]) | ((uint32_t)f32_to_bf16(f[2 * k + 1]) << 16);
+  return v;
+}
+
+// Sum a[8] and b[8] of every thread over the RPI row lanes of the block; add
+// the block totals of its channels to acc[c] / acc[C + c].
+__device__ __forceinline__ void block_reduce_atomic(const float* a, const float* b, const BnGeom& g, int c0,
+                                                    float* __restrict__ acc) {
+  __shared__ float red[kThreads * 16];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[t * 16 + k] = a[k];
+    red[t * 16 + 8 + k] = b[k];
+  }
+  __syncthreads();
+  const int nch = g.CVB * 8;
+  for (int j = t; j < 2 * nch; j += kThreads) {
+    const int which = j / nch, ch = j - which * nch;
+    const int cv = ch >> 3, k = ch & 7;
+    float s = 0.f;
+    for (int r = 0; r < g.RPI; ++r) s += red[(r * g.CVB + cv) * 16 + which * 8 + k];
+    atomicAdd(&acc[which * g.C + c0 + ch], s);
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) bn_nhwc_stats_kernel(const bf16_t* __restrict__ x, BnGeom g,
+                                                                   float* __restrict__ acc) {
+  const int t = threadIdx.x, cv = t % g.CVB, r = t / g.CVB;
+  const int c0 = blockIdx.y * g.CVB * 8;
+  const int c = c0 + cv * 8;
+  const int64_t row0 = (int64_t)blockIdx.x * g.rows_per_block;
+  const int64_t row1 = min(g.M, row0 + g.rows_per_block);
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t row = row0 + r; row < row1; row += g.RPI) {
+    float f[8];
+    unpack8(*(const u32x4*)(x + row * g.C + c), f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s[k] += f[k];
+      q[k] = fmaf(f[k], f[k], q[k]);
+    }
+  }
+  block_reduce_atomic(s, q, g, c0, acc);
+}
+
+__device__ __forceinline__ void stats8(const float* __restrict__ acc, int C, int c, float invM, float eps,
+                                       float* mean, float* invstd) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float m = acc[c + k] * invM;
+    const float var = fmaxf(acc[C + c + k] * invM - m * m, 0.f);
+    mean[k] = m;
+    invstd[k] = rsqrtf(var + eps);
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) bn_nhwc_fwd_apply_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
+    const float* __restrict__ acc, const float* __restrict__ w, const float* __restrict__ b, BnGeom g, float eps,
+    int relu, float* __restrict__ save, float* __restrict__ run_mean, float* __restrict__ run_var, float momentum) {
+  const int t = threadIdx.x, cv = t % g.CVB, r = t / g.CVB;
+  const int c0 = blockIdx.y * g.CVB * 8;
+  const int c = c0 + cv * 8;
+  const float invM = 1.f / (float)g.M;
+  float mean[8], invstd[8], sc[8], sh[8];
+  stats8(acc, g.C, c, invM, eps, mean, invstd);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sc[k] = w[c + k] * invstd[k];
+    sh[k] = fmaf(-mean[k], sc[k], b[c + k]);
+  }
+  if (blockIdx.x == 0 && r == 0) {
+    const float unbias = g.M > 1 ? (float)g.M / (float)(g.M - 1) : 1.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      save[c + k] = mean[k];
+      save[g.C + c + k] = invstd[k];
+      if (run_mean != nullptr) {
+        const float var = fmaxf(acc[g.C + c + k] * invM - mean[k] * mean[k], 0.f);
+        run_mean[c + k] = (1.f - momentum) * run_mean[c + k] + momentum * mean[k];
+        run_var[c + k] = (1.f - momentum) * run_var[c + k] + momentum * var * unbias;
+      }
+    }
+  }
+  const int64_t row0 = (int64_t)blockIdx.x * g.rows_per_block;
+  const int64_t row1 = min(g.M, row0 + g.rows_per_block);
+  for (int64_t row = row0 + r; row < row1; row += g.RPI) {
+    const int64_t off = row * g.C + c;
+    float f[8];
+    unpack8(*(const u32x4*)(x + off), f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] = fmaf(f[k], sc[k], sh[k]);
+    if (res != nullptr) {
+      float rr[8];
+      unpack8(*(const u32x4*)(res + off), rr);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] += rr[k];
+    }
+    if (relu) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = fmaxf(f[k], 0.f);
+    }
+    *(u32x4*)(y + off) = pack8(f);
+  }
+}
+
+// g = dy * (y > 0 if relu)
+__device__ __forceinline__ void load_g(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, int64_t off,
+                                       int relu, float* gv) {
+  unpack8(*(const u32x4*)(dy + off), gv);
+  if (relu) {
+    float yy[8];
+    unpack8(*(const u32x4*)(y + off), yy);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gv[k] = yy[k] > 0.f ? gv[k] : 0.f;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_reduce_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
+    const float* __restrict__ save, BnGeom g, int relu, float* __restrict__ acc) {
+  const int t = threadIdx.x, cv = t % g.CVB, r = t / g.CVB;
+  const int c0 = blockIdx.y * g.CVB * 8;
+  const int c = c0 + cv * 8;
+  float mean[8], invstd[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    mean[k] = save[c + k];
+    invstd[k] = save[g.C + c + k];
+  }
+  float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int64_t row0 = (int64_t)blockIdx.x * g.rows_per_block;
+  const int64_t row1 = min(g.M, row0 + g.rows_per_block);
+  for (int64_t row = row0 + r; row < row1; row += g.RPI) {
+    const int64_t off = row * g.C + c;
+    float gv[8], xv[8];
+    load_g(dy, y, off, relu, gv);
+    unpack8(*(const u32x4*)(x + off), xv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sg[k] += gv[k];
+      sgx[k] = fmaf(gv[k], (xv[k] - mean[k]) * invstd[k], sgx[k]);
+    }
+  }
+  block_reduce_atomic(sg, sgx, g, c0, acc);
+}
+
+__global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
+    const float* __restrict__ save, const float* __restrict__ w, const float* __restrict__ acc, BnGeom g, int relu,
+    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, float* __restrict__ dw, float* __restrict__ db) {
+  const int t = threadIdx.x, cv = t % g.CVB, r = t / g.CVB;
+  const int c0 = blockIdx.y * g.CVB * 8;
+  const int c = c0 + cv * 8;
+  const float invM = 1.f / (float)g.M;
+  float mean[8], invstd[8], a[8], mg[8], mgx[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    mean[k] = save[c + k];
+    invstd[k] = save[g.C + c + k];
+    a[k] = w[c + k] * invstd[k];
+    mg[k] = acc[c + k] * invM;
+    mgx[k] = acc[g.C + c + k] * invM;
+  }
+  if (blockIdx.x == 0 && r == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      db[c + k] = acc[c + k];
+      dw[c + k] = acc[g.C + c + k];
+    }
+  }
+  const int64_t row0 = (int64_t)blockIdx.x * g.rows_per_block;
+  const int64_t row1 = min(g.M, row0 + g.rows_per_block);
+  for (int64_t row = row0 + r; row < row1; row += g.RPI) {
+    const int64_t off = row * g.C + c;
+    float gv[8], xv[8], o[8];
+    load_g(dy, y, off, relu, gv);
+    unpack8(*(const u32x4*)(x + off), xv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float xh = (xv[k] - mean[k]) * invstd[k];
+      o[k] = a[k] * (gv[k] - mg[k] - xh * mgx[k]);
+    }
+    *(u32x4*)(dx + off) = pack8(o);
+    if (dres != nullptr) *(u32x4*)(dres + off) = pack8(gv);
+  }
+}
+
+BnGeom make_geom(int64_t M, int C, dim3* grid) {
+  if (M <= 0 || C <= 0 || C % 8 != 0 || (kThreads % (C / 8 < 32 ? C / 8 : 32)) != 0 ||
+      (C / 8 > 32 && (C / 8) % 32 != 0))
+    throw std::runtime_error("bn_nhwc: C must be a multiple of 8 dividing 256*8 or a multiple of 256 (got " +
+                             std::to_string(C) + ")");
+  BnGeom g;
+  g.M = M;
+  g.C = C;
+  g.CVB = C / 8 < 32 ? C / 8 : 32;
+  g.RPI = kThreads / g.CVB;
+  const int groups = (C / 8) / g.CVB;
+  int64_t cap = 262144 / C;
+  if (cap < 64) cap = 64;
+  if (cap > 2048) cap = 2048;
+  int64_t rb = (M + (int64_t)g.RPI * 16 - 1) / ((int64_t)g.RPI * 16);
+  if (rb > cap) rb = cap;
+  if (rb < 1) rb = 1;
+  int64_t rpb = (M + rb - 1) / rb;
+  rpb = (rpb + g.RPI - 1) / g.RPI * g.RPI;
+  rb = (M + rpb - 1) / rpb;
+  g.rows_per_block = rpb;
+  *grid = dim3((unsigned)rb, (unsigned)groups);
+  return g;
+}
+
+}  // namespace
+
+// acc: fp32 [2C], zeroed by the caller.
+void bn_nhwc_fwd(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b, uintptr_t save,
+                 uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps, double momentum, int relu,
+                 uintptr_t stream) {
+  dim3 grid;
+  const BnGeom g = make_geom(M, C, &grid);
+  hipStream_t s = as_stream(stream);
+  bn_nhwc_stats_kernel<<<grid, kThreads, 0, s>>>((const bf16_t*)x, g, (float*)acc);
+  DL_HIP_CHECK(hipGetLastError());
+  bn_nhwc_fwd_apply_kernel<<<grid, kThreads, 0, s>>>((const bf16_t*)x, (const bf16_t*)res, (bf16_t*)y,
+                                                      (const float*)acc, (const float*)w, (const float*)b, g,
+                                                      (float)eps, relu, (float*)save, (float*)run_mean,
+                                                      (float*)run_var, (float)momentum);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+// acc: fp32 [2C], zeroed by the caller; dres may be 0 (no fused residual).
+void bn_nhwc_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t acc, uintptr_t dx,
+                 uintptr_t dres, uintptr_t dw, uintptr_t db, int64_t M, int C, int relu, uintptr_t stream) {
+  dim3 grid;
+  const BnGeom g = make_geom(M, C, &grid);
+  hipStream_t s = as_stream(stream);
+  bn_nhwc_bwd_reduce_kernel<<<grid, kThreads, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x,
+                                                       (const float*)save, g, relu, (float*)acc);
+  DL_HIP_CHECK(hipGetLastError());
+  bn_nhwc_bwd_apply_kernel<<<grid, kThreads, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x,
+                                                      (const float*)save, (const float*)w, (const float*)acc, g, relu,
+                                                      (bf16_t*)dx, (bf16_t*)dres, (float*)dw, (float*)db);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dl

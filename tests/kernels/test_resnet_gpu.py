@@ -51,3 +51,50 @@ def test_resnet50_train_step():
     assert all(torch.isfinite(torch.tensor(losses))), losses
     assert float((tr.flat.data - before).abs().max()) > 0
     tr.finish()
+
+
+@pytest.mark.parametrize("c,hw,relu,res", [(64, 28, True, False), (256, 14, True, True), (128, 7, False, False),
+                                           (2048, 7, True, True), (512, 7, False, True)])
+def test_bn_act_hip_matches_fp32(c, hw, relu, res):
+    """ops.bn_nhwc.bn_act (HIP) vs an fp32 PyTorch reference of
+    act(BN(x) [+ r]): output, dx, dweight, dbias, dres, running stats."""
+    from torch_distlearn_amd import _native
+    from torch_distlearn_amd.ops.bn_nhwc import bn_act
+
+    _native.native()
+    torch.manual_seed(c + hw)
+    dev = "cuda"
+    n = 16
+    cl = torch.channels_last
+    xb = (torch.randn(n, c, hw, hw, device=dev) * 2 + 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
+    rb = torch.randn(n, c, hw, hw, device=dev).to(torch.bfloat16).contiguous(memory_format=cl) if res else None
+    w, b = torch.rand(c, device=dev) + 0.5, torch.randn(c, device=dev) * 0.2
+    go = torch.randn(n, c, hw, hw, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+
+    def run(hip):
+        x = (xb if hip else xb.float()).detach().requires_grad_(True)
+        r = None if rb is None else (rb if hip else rb.float()).detach().requires_grad_(True)
+        wi, bi = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        rm, rv = torch.zeros(c, device=dev), torch.ones(c, device=dev)
+        if hip:
+            y = bn_act(x, wi, bi, rm, rv, r, relu)
+        else:
+            y = F.batch_norm(x, rm, rv, wi, bi, True, 0.1, 1e-5)
+            y = y + r if r is not None else y
+            y = F.relu(y) if relu else y
+        y.backward(go.to(y.dtype))
+        outs = [y, x.grad, wi.grad, bi.grad, rm, rv] + ([r.grad] if r is not None else [])
+        return [o.float() for o in outs]
+
+    got, ref = run(True), run(False)
+    names = ["y", "dx", "dw", "db", "running_mean", "running_var", "dres"]
+    for name, a, r in zip(names, got, ref):
+        rel = float((a - r).norm() / (r.norm() + 1e-12))
+        assert rel < 2e-2, (name, rel)
+
+
+def test_resnet50_hip_bn_train_step(monkeypatch):
+    from torch_distlearn_amd.models import resnet
+
+    monkeypatch.setattr(resnet, "_BN_MODE", "hip")
+    test_resnet50_train_step()

@@ -22,7 +22,9 @@ import torch.nn.functional as F
 # BatchNorm precision: "mixed" (default) feeds the bf16 activation straight to
 # the BN kernel, which keeps fp32 statistics / affine parameters internally;
 # "fp32" materialises an fp32 copy of every activation first (one extra full
-# read + write of each BN input and output in HBM).
+# read + write of each BN input and output in HBM); "hip" runs training BN
+# fused with its ReLU / residual add on the channels-last HIP kernels
+# (ops/bn_nhwc.py, csrc/kernels/bn_nhwc.hip).
 _BN_MODE = os.environ.get("DISTLEARN_RESNET_BN", "mixed")
 
 
@@ -41,6 +43,17 @@ class _BN(nn.Module):
         y = F.batch_norm(x.float(), self.running_mean, self.running_var, self.weight, self.bias, self.training, 0.1,
                          1e-5)
         return y.to(x.dtype)
+
+    def act(self, x, relu: bool = True, residual=None):
+        """act(BN(x) [+ residual]); one fused HIP kernel pair in "hip" mode."""
+        if _BN_MODE == "hip" and self.training and x.is_cuda:
+            from ..ops.bn_nhwc import bn_act
+
+            return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual, relu)
+        y = self(x)
+        if residual is not None:
+            y = y + residual
+        return F.relu(y) if relu else y
 
 
 class _Conv(nn.Module):
@@ -66,11 +79,10 @@ class _Bottleneck(nn.Module):
             self.down = nn.ModuleList([_Conv(cin, cout, 1, stride, g), _BN(cout)])
 
     def forward(self, x):
-        y = F.relu(self.b1(self.c1(x)))
-        y = F.relu(self.b2(self.c2(y)))
-        y = self.b3(self.c3(y))
-        s = x if self.down is None else self.down[1](self.down[0](x))
-        return F.relu(y + s)
+        y = self.b1.act(self.c1(x))
+        y = self.b2.act(self.c2(y))
+        s = x if self.down is None else self.down[1].act(self.down[0](x), relu=False)
+        return self.b3.act(self.c3(y), residual=s)
 
 
 class ResNet50(nn.Module):
@@ -96,7 +108,7 @@ class ResNet50(nn.Module):
         h = x.to(cd)
         if h.is_cuda:
             h = h.contiguous(memory_format=torch.channels_last)
-        h = F.max_pool2d(F.relu(self.stem_bn(self.stem(h))), 3, 2, 1)
+        h = F.max_pool2d(self.stem_bn.act(self.stem(h)), 3, 2, 1)
         for b in self.blocks:
             h = b(h)
         # classifier in fp32 (2048 x 1000: negligible cost): bf16 logits of a

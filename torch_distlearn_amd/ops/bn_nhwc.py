@@ -1,0 +1,79 @@
+"""Fused channels-last training BatchNorm (+ReLU, +residual add) on the HIP
+kernels of ``csrc/kernels/bn_nhwc.hip`` -- the ResNet-50 path's BN.
+
+``bn_act(x, weight, bias, running_mean, running_var, residual=None, relu=True)``
+computes ``act(BN(x) [+ residual])`` for a channels-last bf16 ``x`` [N, C, H, W]
+with fp32 statistics / affine parameters, updating the running statistics like
+``F.batch_norm(training=True)``.  Backward fuses the ReLU mask, the BN input
+gradient and the residual gradient into two kernels.  Reference parity: the
+reference's cunn ``SpatialBatchNormalization`` + ``ReLU`` layers
+(examples/cifar10.lua:108-133); numerics are tested against the fp32 PyTorch
+op (tests/kernels/test_resnet_gpu.py).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .._native import native, stream_handle
+
+
+def _geom(x: torch.Tensor):
+    n, c, h, w = x.shape
+    return n * h * w, c
+
+
+def supported(x: torch.Tensor) -> bool:
+    c = x.shape[1]
+    ok_c = c % 8 == 0 and ((c < 256 and 256 % (c // 8) == 0) or c % 256 == 0)
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and ok_c
+            and x.is_contiguous(memory_format=torch.channels_last))
+
+
+class _BnAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, relu, eps, momentum):
+        M, C = _geom(x)
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        acc = torch.zeros(2 * C, device=x.device, dtype=torch.float32)
+        save = torch.empty(2 * C, device=x.device, dtype=torch.float32)
+        res = residual.contiguous(memory_format=torch.channels_last) if residual is not None else None
+        native().bn_nhwc_fwd(x.data_ptr(), res.data_ptr() if res is not None else 0, y.data_ptr(), acc.data_ptr(),
+                             weight.data_ptr(), bias.data_ptr(), save.data_ptr(),
+                             running_mean.data_ptr() if running_mean is not None else 0,
+                             running_var.data_ptr() if running_var is not None else 0, M, C, float(eps),
+                             float(momentum), int(relu), stream_handle())
+        ctx.save_for_backward(x, y, weight, save)
+        ctx.relu = bool(relu)
+        ctx.has_res = residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, weight, save = ctx.saved_tensors
+        M, C = _geom(x)
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
+        acc = torch.zeros(2 * C, device=x.device, dtype=torch.float32)
+        dw = torch.empty(C, device=x.device, dtype=torch.float32)
+        db = torch.empty(C, device=x.device, dtype=torch.float32)
+        native().bn_nhwc_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), save.data_ptr(), weight.data_ptr(),
+                             acc.data_ptr(), dx.data_ptr(), dres.data_ptr() if dres is not None else 0, dw.data_ptr(),
+                             db.data_ptr(), M, C, int(ctx.relu), stream_handle())
+        return dx, dw.to(weight.dtype), db.to(weight.dtype), None, None, dres, None, None, None
+
+
+def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_mean: Optional[torch.Tensor],
+           running_var: Optional[torch.Tensor], residual: Optional[torch.Tensor] = None, relu: bool = True,
+           eps: float = 1e-5, momentum: float = 0.1) -> torch.Tensor:
+    if not supported(x):
+        raise ValueError(f"bn_act: needs a channels-last bf16 CUDA tensor with a supported channel count, got "
+                         f"{tuple(x.shape)} {x.dtype} {x.device}")
+    if residual is not None and (residual.shape != x.shape or residual.dtype != x.dtype):
+        raise ValueError("bn_act: residual must match x in shape and dtype")
+    if weight.dtype != torch.float32 or bias.dtype != torch.float32:
+        raise ValueError("bn_act: weight / bias must be fp32")
+    return _BnAct.apply(x, weight.contiguous(), bias.contiguous(), running_mean, running_var, residual, relu, eps,
+                        momentum)
