@@ -5,5 +5,4 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 S=scripts/gpu_step.sh
 $S 300 gpurun_out/rocprof_r50.log rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r50 -o run -- python bench.py --model resnet50 --steps 10 --warmup 3 || exit 1
-python scripts/prof_summary.py gpurun_out/prof_r50 --steps 13 --top 40 > gpurun_out/kernels_r50.txt 2>&1
 echo ALLDONE

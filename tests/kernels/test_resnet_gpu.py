@@ -93,8 +93,9 @@ def test_bn_act_hip_matches_fp32(c, hw, relu, res):
         assert rel < 2e-2, (name, rel)
 
 
-def test_resnet50_hip_bn_train_step(monkeypatch):
+def test_resnet50_mixed_bn_train_step(monkeypatch):
+    # the MIOpen BN path (DISTLEARN_RESNET_BN=mixed); the default is the HIP BN
     from torch_distlearn_amd.models import resnet
 
-    monkeypatch.setattr(resnet, "_BN_MODE", "hip")
+    monkeypatch.setattr(resnet, "_BN_MODE", "mixed")
     test_resnet50_train_step()

