@@ -80,7 +80,21 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_stats_kernel(const bf16_t* _
   const int64_t row0 = (int64_t)blockIdx.x * g.rows_per_block;
   const int64_t row1 = min(g.M, row0 + g.rows_per_block);
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int64_t row = row0 + r; row < row1; row += g.RPI) {
+  int64_t row = row0 + r;
+  // two rows per iteration: two independent 16-byte loads in flight per thread
+  for (; row + g.RPI < row1; row += 2 * g.RPI) {
+    const u32x4 v0 = *(const u32x4*)(x + row * g.C + c);
+    const u32x4 v1 = *(const u32x4*)(x + (row + g.RPI) * g.C + c);
+    float f[8], h[8];
+    unpack8(v0, f);
+    unpack8(v1, h);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s[k] += f[k] + h[k];
+      q[k] = fmaf(f[k], f[k], fmaf(h[k], h[k], q[k]));
+    }
+  }
+  if (row < row1) {
     float f[8];
     unpack8(*(const u32x4*)(x + row * g.C + c), f);
 #pragma unroll

@@ -36,7 +36,8 @@ class _BnAct(torch.autograd.Function):
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, relu, eps, momentum):
         M, C = _geom(x)
         y = torch.empty_like(x, memory_format=torch.channels_last)
-        acc = torch.zeros(2 * C, device=x.device, dtype=torch.float32)
+        # forward and backward per-channel sums in one zeroed buffer (one fill)
+        acc = torch.zeros(4 * C, device=x.device, dtype=torch.float32)
         save = torch.empty(2 * C, device=x.device, dtype=torch.float32)
         res = residual.contiguous(memory_format=torch.channels_last) if residual is not None else None
         native().bn_nhwc_fwd(x.data_ptr(), res.data_ptr() if res is not None else 0, y.data_ptr(), acc.data_ptr(),
@@ -44,19 +45,19 @@ class _BnAct(torch.autograd.Function):
                              running_mean.data_ptr() if running_mean is not None else 0,
                              running_var.data_ptr() if running_var is not None else 0, M, C, float(eps),
                              float(momentum), int(relu), stream_handle())
-        ctx.save_for_backward(x, y, weight, save)
+        ctx.save_for_backward(x, y, weight, save, acc)
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, weight, save = ctx.saved_tensors
+        x, y, weight, save, acc4 = ctx.saved_tensors
         M, C = _geom(x)
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
-        acc = torch.zeros(2 * C, device=x.device, dtype=torch.float32)
+        acc = acc4[2 * C:]
         dw = torch.empty(C, device=x.device, dtype=torch.float32)
         db = torch.empty(C, device=x.device, dtype=torch.float32)
         native().bn_nhwc_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), save.data_ptr(), weight.data_ptr(),
