@@ -24,7 +24,8 @@ void multi_copy(uintptr_t segs, int nseg, int64_t max_bytes, uintptr_t stream);
 void bn_nhwc_fwd(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b, uintptr_t save,
                  uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps, double momentum, int relu,
                  uintptr_t stream);
-void bn_nhwc_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t acc, uintptr_t dx,
+void bn_nhwc_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, uintptr_t acc,
+                 uintptr_t dx,
                  uintptr_t dres, uintptr_t dw, uintptr_t db, int64_t M, int C, int relu, uintptr_t stream);
 void confusion_update(uintptr_t pred, int pred_is_bf16, uintptr_t target, uintptr_t mat, int B, int C,
                       uintptr_t stream);

@@ -167,11 +167,17 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_fwd_apply_kernel(
   }
 }
 
-// g = dy * (y > 0 if relu)
+// g = dy * relu'(.): relu 0 = identity, 1 = mask from the saved output y (BN
+// fused with a residual add), 2 = mask recomputed from x (x * sc + sh > 0,
+// bitwise the forward's pre-activation: same fp32 operands and fma), which
+// saves reading y in both backward passes.
 __device__ __forceinline__ void load_g(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, int64_t off,
-                                       int relu, float* gv) {
+                                       int relu, const float* xv, const float* sc, const float* sh, float* gv) {
   unpack8(*(const u32x4*)(dy + off), gv);
-  if (relu) {
+  if (relu == 2) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gv[k] = fmaf(xv[k], sc[k], sh[k]) > 0.f ? gv[k] : 0.f;
+  } else if (relu) {
     float yy[8];
     unpack8(*(const u32x4*)(y + off), yy);
 #pragma unroll
@@ -181,15 +187,18 @@ __device__ __forceinline__ void load_g(const bf16_t* __restrict__ dy, const bf16
 
 __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
-    const float* __restrict__ save, BnGeom g, int relu, float* __restrict__ acc) {
+    const float* __restrict__ save, const float* __restrict__ w, const float* __restrict__ b, BnGeom g, int relu,
+    float* __restrict__ acc) {
   const int t = threadIdx.x, cv = t % g.CVB, r = t / g.CVB;
   const int c0 = blockIdx.y * g.CVB * 8;
   const int c = c0 + cv * 8;
-  float mean[8], invstd[8];
+  float mean[8], invstd[8], sc[8], sh[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     mean[k] = save[c + k];
     invstd[k] = save[g.C + c + k];
+    sc[k] = w[c + k] * invstd[k];
+    sh[k] = fmaf(-mean[k], sc[k], b[c + k]);
   }
   float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int64_t row0 = (int64_t)blockIdx.x * g.rows_per_block;
@@ -197,8 +206,8 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_reduce_kernel(
   for (int64_t row = row0 + r; row < row1; row += g.RPI) {
     const int64_t off = row * g.C + c;
     float gv[8], xv[8];
-    load_g(dy, y, off, relu, gv);
     unpack8(*(const u32x4*)(x + off), xv);
+    load_g(dy, y, off, relu, xv, sc, sh, gv);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       sg[k] += gv[k];
@@ -210,18 +219,19 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_reduce_kernel(
 
 __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
-    const float* __restrict__ save, const float* __restrict__ w, const float* __restrict__ acc, BnGeom g, int relu,
-    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, float* __restrict__ dw, float* __restrict__ db) {
+    const float* __restrict__ save, const float* __restrict__ w, const float* __restrict__ b,
+    const float* __restrict__ acc, BnGeom g, int relu, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, float* __restrict__ dw, float* __restrict__ db) {
   const int t = threadIdx.x, cv = t % g.CVB, r = t / g.CVB;
   const int c0 = blockIdx.y * g.CVB * 8;
   const int c = c0 + cv * 8;
   const float invM = 1.f / (float)g.M;
-  float mean[8], invstd[8], a[8], mg[8], mgx[8];
+  float mean[8], invstd[8], a[8], sh[8], mg[8], mgx[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     mean[k] = save[c + k];
     invstd[k] = save[g.C + c + k];
     a[k] = w[c + k] * invstd[k];
+    sh[k] = fmaf(-mean[k], a[k], b[c + k]);
     mg[k] = acc[c + k] * invM;
     mgx[k] = acc[g.C + c + k] * invM;
   }
@@ -237,8 +247,8 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
   for (int64_t row = row0 + r; row < row1; row += g.RPI) {
     const int64_t off = row * g.C + c;
     float gv[8], xv[8], o[8];
-    load_g(dy, y, off, relu, gv);
     unpack8(*(const u32x4*)(x + off), xv);
+    load_g(dy, y, off, relu, xv, a, sh, gv);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float xh = (xv[k] - mean[k]) * invstd[k];
@@ -292,17 +302,21 @@ void bn_nhwc_fwd(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr
   DL_HIP_CHECK(hipGetLastError());
 }
 
-// acc: fp32 [2C], zeroed by the caller; dres may be 0 (no fused residual).
-void bn_nhwc_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t acc, uintptr_t dx,
+// acc: fp32 [2C], zeroed by the caller; dres may be 0 (no fused residual);
+// relu: 0 none, 1 mask from y, 2 mask recomputed from x (y may be 0).
+void bn_nhwc_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, uintptr_t acc,
+                 uintptr_t dx,
                  uintptr_t dres, uintptr_t dw, uintptr_t db, int64_t M, int C, int relu, uintptr_t stream) {
   dim3 grid;
   const BnGeom g = make_geom(M, C, &grid);
   hipStream_t s = as_stream(stream);
   bn_nhwc_bwd_reduce_kernel<<<grid, kThreads, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x,
-                                                       (const float*)save, g, relu, (float*)acc);
+                                                       (const float*)save, (const float*)w, (const float*)b, g, relu,
+                                                       (float*)acc);
   DL_HIP_CHECK(hipGetLastError());
   bn_nhwc_bwd_apply_kernel<<<grid, kThreads, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x,
-                                                      (const float*)save, (const float*)w, (const float*)acc, g, relu,
+                                                      (const float*)save, (const float*)w, (const float*)b,
+                                                      (const float*)acc, g, relu,
                                                       (bf16_t*)dx, (bf16_t*)dres, (float*)dw, (float*)db);
   DL_HIP_CHECK(hipGetLastError());
 }

@@ -24,7 +24,7 @@ import torch.nn.functional as F
 # "fp32" materialises an fp32 copy of every activation first (one extra full
 # read + write of each BN input and output in HBM); "hip" runs training BN
 # fused with its ReLU / residual add on the channels-last HIP kernels
-# (ops/bn_nhwc.py, csrc/kernels/bn_nhwc.hip; default: 43.5 -> 36.2 ms/step).
+# (ops/bn_nhwc.py, csrc/kernels/bn_nhwc.hip; default: 43.7 -> 35.5 ms/step).
 _BN_MODE = os.environ.get("DISTLEARN_RESNET_BN", "hip")
 
 

@@ -45,14 +45,17 @@ class _BnAct(torch.autograd.Function):
                              running_mean.data_ptr() if running_mean is not None else 0,
                              running_var.data_ptr() if running_var is not None else 0, M, C, float(eps),
                              float(momentum), int(relu), stream_handle())
-        ctx.save_for_backward(x, y, weight, save, acc)
-        ctx.relu = bool(relu)
         ctx.has_res = residual is not None
+        # relu mask: from the output when a residual was added (mode 1),
+        # otherwise recomputed from x in the backward kernels (mode 2: y is
+        # neither saved nor read)
+        ctx.relu = (1 if ctx.has_res else 2) if relu else 0
+        ctx.save_for_backward(x, y if ctx.relu == 1 else None, weight, bias, save, acc)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, weight, save, acc4 = ctx.saved_tensors
+        x, y, weight, bias, save, acc4 = ctx.saved_tensors
         M, C = _geom(x)
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = torch.empty_like(x, memory_format=torch.channels_last)
@@ -60,9 +63,9 @@ class _BnAct(torch.autograd.Function):
         acc = acc4[2 * C:]
         dw = torch.empty(C, device=x.device, dtype=torch.float32)
         db = torch.empty(C, device=x.device, dtype=torch.float32)
-        native().bn_nhwc_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), save.data_ptr(), weight.data_ptr(),
-                             acc.data_ptr(), dx.data_ptr(), dres.data_ptr() if dres is not None else 0, dw.data_ptr(),
-                             db.data_ptr(), M, C, int(ctx.relu), stream_handle())
+        native().bn_nhwc_bwd(dy.data_ptr(), y.data_ptr() if y is not None else 0, x.data_ptr(), save.data_ptr(),
+                             weight.data_ptr(), bias.data_ptr(), acc.data_ptr(), dx.data_ptr(), dres.data_ptr() if dres is not None else 0, dw.data_ptr(),
+                             db.data_ptr(), M, C, ctx.relu, stream_handle())
         return dx, dw.to(weight.dtype), db.to(weight.dtype), None, None, dres, None, None, None
 
 
