@@ -82,8 +82,10 @@ def test_allreduce_bw_script_gloo():
     # scripts/allreduce_bw.py (data-plane bandwidth sweep) on 2 gloo ranks
     import json
 
+    from torch_distlearn_amd.launch import free_port
+
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-           "--master-port", "29563", os.path.join(ROOT, "scripts", "allreduce_bw.py"), "--device", "cpu",
+           "--master-port", str(free_port()), os.path.join(ROOT, "scripts", "allreduce_bw.py"), "--device", "cpu",
            "--max-mb", "1", "--iters", "2", "--warmup", "1"]
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
