@@ -178,6 +178,9 @@ def main():
                 if os.environ.get("DISTLEARN_BENCH_TRACE", "") == "sync":
                     print(f"warmup {i} loss {float(wl):.4f} |p| {float(tr.flat.data.norm()):.4e} "
                           f"|g| {float(tr.flat.grad.norm()):.4e}", file=sys.stderr, flush=True)
+        if step_args is None:
+            tr.prepare(loader)  # (run() already did; explicit: no capture may fall in the timed region)
+        captures0 = tr.captures
         sync()
         worker_barrier()
         sync()
@@ -199,6 +202,8 @@ def main():
         worker_barrier()
         sync()
         dt = time.perf_counter() - t0
+        if tr.captures != captures0:
+            raise RuntimeError(f"bench.py: {tr.captures - captures0} hipGraph capture(s) inside the timed region")
         tr.finish()
     # max over ranks (the AsyncEA server contributes 0); loss from the first worker
     t = torch.tensor([dt, float(loss.float().item()) if (loss is not None and rank == workers[0]) else -1e30],

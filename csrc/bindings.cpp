@@ -62,11 +62,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   m.def("rccl_version", &rccl_version);
   py::class_<RcclCommunicator>(m, "RcclCommunicator")
-      .def(py::init([](py::bytes uid, int rank, int world, int device) {
-        std::string id(uid);  // copy while holding the GIL
-        py::gil_scoped_release nogil;  // ncclCommInitRank blocks on the other ranks
-        return new RcclCommunicator(id, rank, world, device);
-      }))
+      .def(py::init([](py::bytes uid, int rank, int world, int device, double timeout_s) {
+             std::string id(uid);  // copy while holding the GIL
+             py::gil_scoped_release nogil;  // ncclCommInitRank blocks on the other ranks
+             return new RcclCommunicator(id, rank, world, device, timeout_s);
+           }),
+           py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("timeout_s") = 0.0)
       .def_property_readonly("rank", &RcclCommunicator::rank)
       .def_property_readonly("world", &RcclCommunicator::world)
       .def_property_readonly("device", &RcclCommunicator::device)
@@ -79,9 +80,14 @@ PYBIND11_MODULE(_C, m) {
       .def("recv", &RcclCommunicator::recv)
       .def("group_start", &RcclCommunicator::group_start)
       .def("group_end", &RcclCommunicator::group_end)
+      .def("track", &RcclCommunicator::track)
+      .def("set_timeout", &RcclCommunicator::set_timeout)
+      .def("timeout", &RcclCommunicator::timeout)
+      .def("pending", &RcclCommunicator::pending)
+      .def("error", &RcclCommunicator::error)
       .def("async_error", &RcclCommunicator::async_error)
-      .def("destroy", &RcclCommunicator::destroy)
-      .def("abort", &RcclCommunicator::abort);
+      .def("destroy", &RcclCommunicator::destroy, py::call_guard<py::gil_scoped_release>())
+      .def("abort", &RcclCommunicator::abort, py::call_guard<py::gil_scoped_release>());
 
   // ---- data runtime -------------------------------------------------------------
   py::class_<PartitionSampler>(m, "PartitionSampler")

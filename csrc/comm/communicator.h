@@ -15,7 +15,13 @@
 #pragma once
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -72,28 +78,47 @@ inline int rccl_version() {
   return v;
 }
 
+// Failure detection.  RCCL collectives never return to the host:
+// a dead or stuck peer leaves every later stream synchronisation blocked
+// forever.  Each communicator therefore owns a watchdog thread (the ProcessGroup
+// watchdog pattern, re-done natively):
+//   * every collective / p2p call enqueued outside hipGraph capture records a
+//     completion event on its stream; track(stream) does the same for work the
+//     communicator cannot see (a replayed hipGraph holding captured collectives);
+//   * the thread polls the oldest pending event and ncclCommGetAsyncError every
+//     poll interval; an event older than the timeout, or an async error, aborts
+//     the communicator (ncclCommAbort makes the in-flight RCCL kernels exit, so
+//     the blocked host synchronisation returns) and records the reason;
+//   * every later call (and check()) raises with that reason instead of hanging.
+// The thread switches itself to relaxed stream-capture mode, so its event
+// queries never invalidate a capture running on the main thread.
 class RcclCommunicator {
  public:
-  RcclCommunicator(const std::string& uid, int rank, int world, int device) : rank_(rank), world_(world), dev_(device) {
+  RcclCommunicator(const std::string& uid, int rank, int world, int device, double timeout_s)
+      : rank_(rank), world_(world), dev_(device), timeout_s_(timeout_s) {
     if ((int)uid.size() != (int)sizeof(ncclUniqueId)) throw std::runtime_error("bad ncclUniqueId size");
     ncclUniqueId id;
     std::memcpy(&id, uid.data(), sizeof(id));
     DL_HIP_CHECK(hipSetDevice(device));
     DL_NCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
+    if (timeout_s_ > 0) watcher_ = std::thread([this] { watch_loop(); });
   }
   ~RcclCommunicator() { destroy(); }
 
   void destroy() {
+    stop_watchdog();
+    std::lock_guard<std::mutex> g(mu_);
     if (comm_) {
       ncclCommDestroy(comm_);
       comm_ = nullptr;
     }
+    release_events_locked();
   }
   void abort() {
-    if (comm_) {
-      ncclCommAbort(comm_);
-      comm_ = nullptr;
-    }
+    stop_watchdog();
+    std::lock_guard<std::mutex> g(mu_);
+    abort_locked("aborted by the caller");
+    release_events_locked();
   }
 
   int rank() const { return rank_; }
@@ -101,45 +126,94 @@ class RcclCommunicator {
   int device() const { return dev_; }
 
   void all_reduce(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int op, uintptr_t stream) {
+    std::lock_guard<std::mutex> g(mu_);
     live();
     DL_NCCL_CHECK(ncclAllReduce((const void*)send, (void*)recv, (size_t)count, to_nccl(dtype), to_nccl_op(op), comm_,
                                 as_stream(stream)));
+    track_locked(stream);
   }
   void broadcast(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int root, uintptr_t stream) {
+    std::lock_guard<std::mutex> g(mu_);
     live();
     DL_NCCL_CHECK(
         ncclBroadcast((const void*)send, (void*)recv, (size_t)count, to_nccl(dtype), root, comm_, as_stream(stream)));
+    track_locked(stream);
   }
   void reduce(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int op, int root, uintptr_t stream) {
+    std::lock_guard<std::mutex> g(mu_);
     live();
     DL_NCCL_CHECK(ncclReduce((const void*)send, (void*)recv, (size_t)count, to_nccl(dtype), to_nccl_op(op), root,
                              comm_, as_stream(stream)));
+    track_locked(stream);
   }
   // recvcount elements per rank
   void reduce_scatter(uintptr_t send, uintptr_t recv, int64_t recvcount, int dtype, int op, uintptr_t stream) {
+    std::lock_guard<std::mutex> g(mu_);
     live();
     DL_NCCL_CHECK(ncclReduceScatter((const void*)send, (void*)recv, (size_t)recvcount, to_nccl(dtype),
                                     to_nccl_op(op), comm_, as_stream(stream)));
+    track_locked(stream);
   }
   void all_gather(uintptr_t send, uintptr_t recv, int64_t sendcount, int dtype, uintptr_t stream) {
+    std::lock_guard<std::mutex> g(mu_);
     live();
     DL_NCCL_CHECK(
         ncclAllGather((const void*)send, (void*)recv, (size_t)sendcount, to_nccl(dtype), comm_, as_stream(stream)));
+    track_locked(stream);
   }
   void send(uintptr_t buf, int64_t count, int dtype, int peer, uintptr_t stream) {
+    std::lock_guard<std::mutex> g(mu_);
     live();
     DL_NCCL_CHECK(ncclSend((const void*)buf, (size_t)count, to_nccl(dtype), peer, comm_, as_stream(stream)));
+    if (group_depth_ == 0) track_locked(stream);
+    else grouped_streams_.push_back(stream);
   }
   void recv(uintptr_t buf, int64_t count, int dtype, int peer, uintptr_t stream) {
+    std::lock_guard<std::mutex> g(mu_);
     live();
     DL_NCCL_CHECK(ncclRecv((void*)buf, (size_t)count, to_nccl(dtype), peer, comm_, as_stream(stream)));
+    if (group_depth_ == 0) track_locked(stream);
+    else grouped_streams_.push_back(stream);
   }
-  void group_start() { DL_NCCL_CHECK(ncclGroupStart()); }
-  void group_end() { DL_NCCL_CHECK(ncclGroupEnd()); }
+  void group_start() {
+    std::lock_guard<std::mutex> g(mu_);
+    live();
+    DL_NCCL_CHECK(ncclGroupStart());
+    ++group_depth_;
+  }
+  void group_end() {
+    std::lock_guard<std::mutex> g(mu_);
+    DL_NCCL_CHECK(ncclGroupEnd());
+    if (--group_depth_ == 0) {
+      // grouped p2p is only launched at the outermost group end: time it from here
+      for (uintptr_t s : grouped_streams_) track_locked(s);
+      grouped_streams_.clear();
+    }
+  }
 
-  // Non-blocking health check (failure detection). Returns the
-  // RCCL async error string or "" when healthy.
+  // Time the work enqueued so far on `stream` (no-op while it is being captured).
+  void track(uintptr_t stream) {
+    std::lock_guard<std::mutex> g(mu_);
+    live();
+    track_locked(stream);
+  }
+  void set_timeout(double s) { timeout_s_.store(s); }
+  double timeout() const { return timeout_s_.load(); }
+  int pending() {
+    std::lock_guard<std::mutex> g(mu_);
+    return (int)pending_.size();
+  }
+  // "" while healthy, else why the communicator was aborted
+  std::string error() {
+    std::lock_guard<std::mutex> g(mu_);
+    return reason_;
+  }
+
+  // Non-blocking health check: RCCL async error string, the watchdog's abort
+  // reason, or "" when healthy.
   std::string async_error() {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!reason_.empty()) return reason_;
     if (!comm_) return "communicator destroyed";
     ncclResult_t r;
     DL_NCCL_CHECK(ncclCommGetAsyncError(comm_, &r));
@@ -148,11 +222,106 @@ class RcclCommunicator {
   }
 
  private:
+  struct Pending {
+    hipEvent_t ev;
+    std::chrono::steady_clock::time_point t;
+  };
+
   void live() const {
-    if (!comm_) throw std::runtime_error("RCCL communicator used after destroy/abort");
+    if (!reason_.empty()) throw std::runtime_error("RCCL communicator failed: " + reason_);
+    if (!comm_) throw std::runtime_error("RCCL communicator used after destroy");
   }
+
+  void track_locked(uintptr_t stream) {
+    if (timeout_s_.load() <= 0 || !watcher_.joinable()) return;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    DL_HIP_CHECK(hipStreamIsCapturing(as_stream(stream), &st));
+    if (st != hipStreamCaptureStatusNone) return;  // captured work is tracked at replay (track())
+    hipEvent_t ev;
+    if (free_.empty()) {
+      DL_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    } else {
+      ev = free_.back();
+      free_.pop_back();
+    }
+    DL_HIP_CHECK(hipEventRecord(ev, as_stream(stream)));
+    pending_.push_back({ev, std::chrono::steady_clock::now()});
+  }
+
+  void abort_locked(const std::string& why) {
+    if (reason_.empty()) reason_ = why;
+    if (comm_) {
+      ncclCommAbort(comm_);
+      comm_ = nullptr;
+    }
+  }
+
+  void release_events_locked() {
+    for (auto& p : pending_) hipEventDestroy(p.ev);
+    pending_.clear();
+    for (auto ev : free_) hipEventDestroy(ev);
+    free_.clear();
+  }
+
+  void stop_watchdog() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    if (watcher_.joinable() && watcher_.get_id() != std::this_thread::get_id()) watcher_.join();
+  }
+
+  void watch_loop() {
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+    (void)hipSetDevice(dev_);
+    std::unique_lock<std::mutex> lk(mu_);
+    while (!stop_) {
+      cv_.wait_for(lk, std::chrono::milliseconds(poll_ms_));
+      if (stop_ || !comm_) continue;
+      // retire completed work (in order: events of one stream complete in order;
+      // across streams an old unfinished event simply keeps the queue from draining)
+      while (!pending_.empty()) {
+        hipError_t q = hipEventQuery(pending_.front().ev);
+        if (q == hipErrorNotReady) break;
+        if (q != hipSuccess) {
+          abort_locked(std::string("HIP error while waiting for a collective: ") + hipGetErrorString(q));
+          break;
+        }
+        free_.push_back(pending_.front().ev);
+        pending_.pop_front();
+      }
+      if (!comm_) continue;
+      ncclResult_t r = ncclSuccess;
+      if (ncclCommGetAsyncError(comm_, &r) == ncclSuccess && r != ncclSuccess && r != ncclInProgress) {
+        abort_locked(std::string("RCCL async error: ") + ncclGetErrorString(r));
+        continue;
+      }
+      const double limit = timeout_s_.load();
+      if (!pending_.empty() && limit > 0) {
+        double age = std::chrono::duration<double>(std::chrono::steady_clock::now() - pending_.front().t).count();
+        if (age > limit) {
+          abort_locked("collective on rank " + std::to_string(rank_) + " did not complete within " +
+                       std::to_string(limit) + " s (dead or stuck peer?)");
+        }
+      }
+    }
+  }
+
   ncclComm_t comm_ = nullptr;
   int rank_, world_, dev_;
+  std::atomic<double> timeout_s_;
+  int poll_ms_ = 50;
+  int group_depth_ = 0;
+  std::vector<uintptr_t> grouped_streams_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool stop_ = false;
+  std::string reason_;
+  std::deque<Pending> pending_;
+  std::vector<hipEvent_t> free_;
+  std::thread watcher_;
 };
 
 }  // namespace dl

@@ -28,7 +28,7 @@ from torch_distlearn_amd import AllReduceEA, FlatParams, Tree  # noqa: E402
 from torch_distlearn_amd.data import Dataset  # noqa: E402
 from torch_distlearn_amd.launch import add_node_flags, device_of, node_opts  # noqa: E402
 from torch_distlearn_amd.models import CifarConvNet  # noqa: E402
-from torch_distlearn_amd.ops.flat import sgd_update_  # noqa: E402
+from torch_distlearn_amd.ops.flat import flat_sgd_  # noqa: E402
 
 
 def main():
@@ -59,7 +59,7 @@ def main():
             flat.grad.zero_()
             loss = model.loss(model(x, compute_dtype=cd), y)
             loss.backward()
-            sgd_update_(flat.data, flat.grad, opt.learningRate)
+            flat_sgd_(flat, opt.learningRate)
             ea.averageParameters(flat)
         ea.synchronizeCenter(flat)
         if opt.nodeIndex == 1:

@@ -32,7 +32,7 @@ from torch_distlearn_amd.checkpoint import results_dir, save_checkpoint  # noqa:
 from torch_distlearn_amd.data import Dataset  # noqa: E402
 from torch_distlearn_amd.launch import device_of  # noqa: E402
 from torch_distlearn_amd.models import CifarConvNet, MnistConvNet  # noqa: E402
-from torch_distlearn_amd.ops.flat import sgd_update_  # noqa: E402
+from torch_distlearn_amd.ops.flat import flat_sgd_  # noqa: E402
 from torch_distlearn_amd.utils.color_print import set_verbose  # noqa: E402
 from torch_distlearn_amd.utils.metrics import ConfusionMatrix, Logger  # noqa: E402
 
@@ -114,7 +114,7 @@ def main():
                 loss = model.loss(model(x, compute_dtype=cd), y)
                 loss.backward()
                 ea.syncClient(flat)                                  # EASGD_client.lua:109
-                sgd_update_(flat.data, flat.grad, opt.learningRate)  # :113-117 (pre-move grads)
+                flat_sgd_(flat, opt.learningRate)  # :113-117 (pre-move grads)
         ea.finishClient()
         print(f"client {rank}: {ea.syncs} syncs, last loss {float(loss.detach()):.4f}")
     else:

@@ -45,8 +45,8 @@ def _ea_worker(rank, world, port, trials, replace_out_of_place):
 
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_allreduce_ea_converges(world):
-    res = mp.run(_ea_worker, world, 2, False)
-    for trial in range(2):
+    res = mp.run(_ea_worker, world, 10, False)  # 10 trials: test/test_AllReduceEA.lua:23
+    for trial in range(10):
         p0, c0, _ = res[0][trial]
         for r in range(1, world):
             p, c, _ = res[r][trial]
@@ -60,3 +60,31 @@ def test_allreduce_ea_out_of_place_params():
     p1, _, _ = res[1][0]
     assert n0 > 0
     assert abs(p0 - p1).max() < 1e-6
+
+
+def _idle_worker(rank, world, port, active):
+    from torch_distlearn_amd import AllReduceEA, Tree
+
+    tree = Tree(rank + 1, world, host="127.0.0.1", port=port)
+    ea = AllReduceEA(tree, 2, 0.3)
+    torch.manual_seed(5 + rank)
+    params = [torch.randn(9)]
+    ea.synchronizeParameters(params)
+    for _ in range(active[rank]):
+        params[0].add_(torch.randn(9))
+        ea.averageParameters(params)
+    ea.synchronizeCenter(params)
+    first = params[0].clone()
+    ea.synchronizeCenter(params)  # every node idle: the drain must not move anything (AllReduceEA.lua:52)
+    return first, params[0].clone(), ea.center[64:73].clone()
+
+
+@pytest.mark.parametrize("active", [(0, 0), (3, 5), (0, 4)])
+def test_allreduce_ea_idle_drain_leaves_params(active):
+    """A second synchronizeCenter in a row (every node at step 0) leaves the
+    params untouched, like the reference's ``if step > 0`` guard; a mix of
+    idle and active nodes (a deadlock in the reference) completes."""
+    res = mp.run(_idle_worker, 2, list(active))
+    for first, second, _ in res:
+        assert first.tobytes() == second.tobytes()
+    assert res[0][2].tobytes() == res[1][2].tobytes()

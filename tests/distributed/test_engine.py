@@ -26,7 +26,8 @@ def _worker(rank, world, port, algo, uneven):
         y = torch.randint(0, 10, (4,), generator=g)
         tr.step(x, y)
     tr.synchronize()
-    return {"p": tr.flat.data.clone(), "nb": len(tr.bucketer.ranges) if tr.bucketer else 0}
+    return {"p": tr.flat.data.clone(), "nb": len(tr.bucketer.ranges) if tr.bucketer else 0,
+            "c": tr.ea.center.clone() if tr.ea is not None else None}
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -65,8 +66,13 @@ def test_engine_sgd_matches_single_process_mean_gradient():
 
 def test_engine_ea_centers_agree():
     res = mp.run(_worker, 2, "ea", True)
-    # after synchronizeCenter the centers are broadcast; params differ (elastic), runs must not deadlock
+    # after synchronizeCenter the centers are broadcast from node 1: bit-identical
+    # (lua/AllReduceEA.lua:74-83); params stay elastic (they differ) but finite
+    assert res[0]["c"].tobytes() == res[1]["c"].tobytes()
     assert all(torch.isfinite(torch.from_numpy(r["p"])).all() for r in res)
+    assert (res[0]["p"] != res[1]["p"]).any(), "uneven elastic runs should leave distinct local params"
+    # the center header (participation count) never leaks into the body
+    assert (res[0]["c"][:64] == res[0]["p"][:64]).all()
 
 
 def _debug_worker(rank, world, port, perturb):

@@ -197,3 +197,16 @@ def test_bench_json_contract(dev, algo):
               "vs_baseline", "dtype", "data", "config"):
         assert k in rec
     assert rec["n_gpus"] == 1 and rec["steps"] == 5 and rec["value"] > 0 and rec["dtype"] == "bf16"
+
+
+def test_run_captures_only_before_timed_steps(dev):
+    """trainer.run captures the single-step and the unrolled graph before the
+    first step, whatever nsteps is (the driver's --warmup 5 < unroll 8 case):
+    later calls replay only (bench.py asserts the same on its timed region)."""
+    tr = _trainer(dev, "hip", True, 29704)
+    ld = _loader(dev, batch=16)
+    tr.run(ld, 2, unroll=8)
+    assert tr.captures == 4  # 1-, 2-, 4- and 8-step graphs
+    tr.run(ld, 9, unroll=8)
+    torch.cuda.synchronize()
+    assert tr.captures == 4 and tr.steps == 11

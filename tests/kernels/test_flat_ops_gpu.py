@@ -113,3 +113,24 @@ def test_rccl_world1_identity(dev):
     tree.scatter([t])
     torch.cuda.synchronize()
     assert torch.equal(t, t0)
+
+
+def test_sum_and_normalize_slot_in_buffer(dev):
+    """sumAndNormalizeGradients on a FlatParams whose all-reduced slot says
+    n = 4, with a buffer spanning thousands of workgroups: every element is
+    divided (the slot itself lives in the buffer's header and is read, never
+    scaled).  Regression for the slot/scale race."""
+    from torch_distlearn_amd import FlatParams
+    from torch_distlearn_amd.ops.flat import HEADER, scale_by_count_
+
+    m = torch.nn.Sequential(torch.nn.Linear(1024, 2048), torch.nn.Linear(2048, 1000)).to(dev)
+    f = FlatParams(m)
+    f.grad.normal_()
+    f.grad[0] = 4.0
+    ref = f.grad.clone()
+    scale_by_count_(f.grad[HEADER:], f.slot)
+    torch.cuda.synchronize()
+    assert float(f.grad[0]) == 4.0
+    torch.testing.assert_close(f.grad[HEADER:], ref[HEADER:] / 4.0, rtol=1e-6, atol=0)
+    with pytest.raises(ValueError):
+        scale_by_count_(f.grad, f.slot)

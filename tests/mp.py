@@ -42,9 +42,11 @@ def _entry(rank, world, port, fn, args, q):
         q.put((rank, "err", traceback.format_exc()))
 
 
-def run(fn, world: int, *args, timeout: float = 240.0):
+def run(fn, world: int, *args, timeout: float = 240.0, dead=()):
     """Run ``fn(rank, world, port, *args)`` in ``world`` processes; return the
-    per-rank results (raises on any worker failure or timeout)."""
+    per-rank results (raises on any worker failure or timeout).  Ranks in
+    ``dead`` are expected to die without reporting (fault-injection tests):
+    their result is None."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
@@ -53,7 +55,7 @@ def run(fn, world: int, *args, timeout: float = 240.0):
         p.start()
     results = {}
     try:
-        for _ in range(world):
+        for _ in range(world - len(dead)):
             rank, status, payload = q.get(timeout=timeout)
             if status != "ok":
                 raise RuntimeError(f"rank {rank} failed:\n{payload}")
@@ -63,4 +65,4 @@ def run(fn, world: int, *args, timeout: float = 240.0):
             p.join(timeout=5)
             if p.is_alive():
                 p.kill()
-    return [results[r] for r in range(world)]
+    return [results.get(r) for r in range(world)]

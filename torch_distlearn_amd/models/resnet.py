@@ -47,9 +47,11 @@ class _BN(nn.Module):
     def act(self, x, relu: bool = True, residual=None):
         """act(BN(x) [+ residual]); one fused HIP kernel pair in "hip" mode."""
         if _BN_MODE == "hip" and self.training and x.is_cuda:
-            from ..ops.bn_nhwc import bn_act
+            from ..ops.bn_nhwc import bn_act, supported
 
-            return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual, relu)
+            if supported(x) and self.weight.dtype == torch.float32 and (
+                    residual is None or (residual.dtype == x.dtype and residual.shape == x.shape)):
+                return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual, relu)
         y = self(x)
         if residual is not None:
             y = y + residual

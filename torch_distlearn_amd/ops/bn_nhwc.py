@@ -61,6 +61,7 @@ class _BnAct(torch.autograd.Function):
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
         acc = acc4[2 * C:]
+        acc.zero_()  # the kernels accumulate atomically: a second backward (retain_graph) starts from 0 too
         dw = torch.empty(C, device=x.device, dtype=torch.float32)
         db = torch.empty(C, device=x.device, dtype=torch.float32)
         native().bn_nhwc_bwd(dy.data_ptr(), y.data_ptr() if y is not None else 0, x.data_ptr(), save.data_ptr(),

@@ -183,7 +183,30 @@ def sgd_update_(p: torch.Tensor, g: torch.Tensor, lr: float, slot: torch.Tensor 
             shadow.copy_(p)
 
 
+def _overlaps(x: torch.Tensor, y: torch.Tensor) -> bool:
+    if x.untyped_storage().data_ptr() != y.untyped_storage().data_ptr():
+        return False
+    xs, ys = x.data_ptr(), y.data_ptr()
+    return xs < ys + y.numel() * y.element_size() and ys < xs + x.numel() * x.element_size()
+
+
+def flat_sgd_(flat: "FlatParams", lr: float, slot: torch.Tensor | None = None, mom: torch.Tensor | None = None,
+              momentum: float = 0.0, weight_decay: float = 0.0) -> None:
+    """The fused update over a FlatParams' parameter body: the 64-element
+    header (whose gradient element is the participation count) is left out,
+    so ``n`` never flows into the parameter buffer."""
+    H = HEADER
+    sgd_update_(flat.data[H:], flat.grad[H:], lr, slot=slot, mom=None if mom is None else mom[H:],
+                momentum=momentum, weight_decay=weight_decay,
+                shadow=None if flat.shadow is None else flat.shadow[H:])
+
+
 def scale_by_count_(x: torch.Tensor, slot: torch.Tensor) -> None:
+    """x *= 1/n with n read from ``slot`` on the device.  ``slot`` must not lie
+    inside ``x`` (every workgroup reads n; one that ran after the slot's own
+    element was scaled would read 1): scale ``grad[HEADER:]``."""
+    if _overlaps(x, slot):
+        raise ValueError("scale_by_count_: the slot lies inside the scaled buffer (pass grad[HEADER:])")
     if x.is_cuda:
         native().scale_by_count(x.data_ptr(), slot.data_ptr(), x.numel(), stream_handle())
         return

@@ -31,7 +31,7 @@ from typing import Any, Optional
 
 import torch
 
-from ..ops.flat import FlatParams, add_, elastic_step_
+from ..ops.flat import HEADER, FlatParams, add_, elastic_step_
 from ..utils.walk import walk_table
 from .tree import FlatBuffer, Tree
 
@@ -94,20 +94,38 @@ class AllReduceEA:
         self.step += 1
         if self.step % self.tau != 0:
             return False
-        f = self.flat
+        p, c, d, s = self._body()
         # delta = alpha (p - c); p -= delta   (K8, writes the comm buffer)
-        elastic_step_(f.data, self.center, self.delta, self.alpha, shadow=f.shadow)
+        elastic_step_(p, c, d, self.alpha, shadow=s)
         self.tree.allReduce(FlatBuffer(self.delta))  # (:41)
-        add_(self.center, self.delta)               # c += sum(delta)  (:43-45)
+        add_(c, d)                                   # c += sum(delta)  (:43-45)
         return True
 
-    def _handle_uneven_steps(self) -> None:  # (:50-72)
+    def _body(self):
+        """(params, center, delta, shadow) without the 64-element header: the
+        delta buffer's header carries the all-reduced participation count,
+        which must never flow into the center or the parameters."""
         f = self.flat
-        self.delta.zero_()
+        return (f.data[HEADER:], self.center[HEADER:], self.delta[HEADER:],
+                None if f.shadow is None else f.shadow[HEADER:])
 
-        def drain_step(d, i):
+    def _handle_uneven_steps(self) -> None:  # (:50-72)
+        p, c, d, s = self._body()
+        self.delta.zero_()
+        rounds = [0]
+        idle = self.step == 0
+
+        def drain_step(_t, _i):
+            rounds[0] += 1
+            if rounds[0] == 1 and idle:
+                # reference guard ``if step > 0`` (:52): a node with no pending
+                # steps contributes zeros and does not move in the first round;
+                # if every node is idle that round ends the drain (n == 0) and
+                # params are untouched.  It still joins the rounds, so a mix of
+                # idle and active nodes cannot deadlock (the reference did).
+                return self.delta
             # c += previous round's sum(delta); delta = alpha (p - c); p -= delta   (K10)
-            elastic_step_(f.data, self.center, self.delta, self.alpha, pending=self.delta, shadow=f.shadow)
+            elastic_step_(p, c, d, self.alpha, pending=d, shadow=s)
             return self.delta
 
         self.tree.allReduce(FlatBuffer(self.delta), "sum", drain_step)

@@ -38,7 +38,7 @@ from typing import Any, Optional
 
 import torch
 
-from ..ops.flat import FlatParams, scale_by_count_, sgd_update_
+from ..ops.flat import HEADER, FlatParams, flat_sgd_, scale_by_count_
 from ..utils.walk import walk_table
 from .tree import FlatBuffer, Tree
 
@@ -79,10 +79,10 @@ class AllReduceSGD:
         f = _flat_of(grads)
         if self.bucketer is not None and f is self.bucketer.flat:
             self.bucketer.finish()
-            scale_by_count_(f.grad, f.slot)
+            scale_by_count_(f.grad[HEADER:], f.slot)  # the header (slot) itself is never scaled
         elif f is not None:
             self.tree.allReduce(FlatBuffer(f.grad))
-            scale_by_count_(f.grad, f.slot)
+            scale_by_count_(f.grad[HEADER:], f.slot)
         else:
             _, n = self.tree.allReduce(grads)
             leaves = walk_table(grads)
@@ -109,8 +109,7 @@ class AllReduceSGD:
                 self.tree.allReduce(FlatBuffer(flat.grad))
             self._count_step()
             self._remember(flat)
-        sgd_update_(flat.data, flat.grad, lr, slot=flat.slot, mom=momentum_buf, momentum=momentum,
-                    weight_decay=weight_decay, shadow=flat.shadow)
+        flat_sgd_(flat, lr, slot=flat.slot, mom=momentum_buf, momentum=momentum, weight_decay=weight_decay)
 
     def _remember(self, grads):
         if self._drain_template is None:

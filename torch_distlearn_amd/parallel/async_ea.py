@@ -21,8 +21,16 @@ MI355X mapping:
   express ``recvAny``), GRANT, TEST/STOP, ACK.  Every message carries a sequence
   number that is checked (replaces the reference's string asserts, :89,169,186);
 * **data plane**: the center / delta payloads are point-to-point
-  ``ncclSend/ncclRecv`` of the persistent flat buffers (C14/C15) on the GPU,
-  gloo send/recv on CPU;
+  ``ncclSend/ncclRecv`` of the persistent flat buffers (C14/C15) on a
+  dedicated **payload stream** (gloo send/recv on CPU).  Ordering: a payload
+  is only posted after the host has received the GRANT (the RCCL send/recv
+  pair is then matched on both sides); the payload stream waits for the
+  compute stream before reading/overwriting a buffer, and the compute stream
+  waits for the payload stream only right before it consumes a received
+  buffer.  The client's delta push therefore overlaps its next training
+  steps, and the server's host loop serves the next ENTER while the GPU is
+  still absorbing the previous delta (reference: lua/AsyncEA.lua:95-132,
+  180-228, all blocking on the host);
 * **non-blocking tester** (reference defect: the server blocked on "Ack" for
   the tester's whole evaluation, :251-252): ``testNet`` only sends a new
   snapshot when the previous one has been acknowledged, and otherwise returns
@@ -30,19 +38,26 @@ MI355X mapping:
 * **explicit shutdown** (reference had none, numEpochs=inf loops forever):
   clients send BYE (:meth:`finishClient`), the server's :meth:`syncServer`
   returns False once every client said BYE, and :meth:`shutdown` stops the
-  tester.
+  tester;
+* **failure detection** (the reference waited forever): every
+  control-plane wait is bounded by ``timeout`` (default: the communicator's
+  timeout, ``--commTimeout``).  A client that dies or stops syncing makes the
+  server raise :class:`~torch_distlearn_amd.parallel.comm.CommError` naming
+  the clients that never finished; the tester stops the same way when the
+  server disappears.
 """
 from __future__ import annotations
 
+import datetime
 from typing import Any, Optional
 
 import torch
 import torch.distributed as dist
 
-from ..ops.flat import FlatParams, add_, elastic_step_
+from ..ops.flat import HEADER, FlatParams, add_, elastic_step_
 from ..utils.color_print import printClient, printServer
 from .allreduce_ea import _FlatState
-from .comm import MSG_LEN, Communicator
+from .comm import MSG_LEN, CommError, Communicator, comm_timeout
 from .tree import Tree
 
 # message types
@@ -64,7 +79,7 @@ class AsyncEA:
 
     def __init__(self, server=None, serverBroadcast=None, client=None, clientBroadcast=None,  # noqa: N803
                  serverTest=None, clientTest=None, numNodes: int = 1, node: int = 0, tau: int = 10,  # noqa: N803
-                 alpha: float = 0.2, comm: Optional[Communicator] = None):
+                 alpha: float = 0.2, comm: Optional[Communicator] = None, timeout: Optional[float] = None):
         if comm is None:
             for c in (server, serverBroadcast, client, clientBroadcast, serverTest, clientTest):
                 if isinstance(c, Tree):
@@ -91,6 +106,9 @@ class AsyncEA:
         self._ack_work = None
         self._ack_buf = torch.zeros(MSG_LEN, dtype=torch.int64)
         self.syncs = 0
+        self.timeout = float(timeout) if timeout is not None else float(getattr(comm, "timeout_s", comm_timeout()))
+        self._ps = None        # payload stream (GPU)
+        self._done = set()     # clients that said BYE (server)
 
     # ------------------------------------------------------------- helpers
     def _one_time_init(self, params: Any):  # (:18-29)
@@ -105,18 +123,43 @@ class AsyncEA:
     def flat(self) -> FlatParams:
         return self.state.flat
 
+    def _payload_stream(self):
+        if self._ps is None and self.flat.data.is_cuda:
+            self._ps = torch.cuda.Stream(device=self.flat.data.device)
+        return self._ps
+
     def _send_payload(self, buf: torch.Tensor, peer: int):
-        self.comm.send(buf, peer)
+        ps = self._payload_stream()
+        if ps is None:
+            self.comm.send(buf, peer)
+            return
+        ps.wait_stream(torch.cuda.current_stream())  # buf is final on the compute stream
+        self.comm.send(buf, peer, stream=ps)
+        buf.record_stream(ps)
 
     def _recv_payload(self, buf: torch.Tensor, peer: int):
-        self.comm.recv(buf, peer)
+        ps = self._payload_stream()
+        if ps is None:
+            self.comm.recv(buf, peer)
+            return
+        ps.wait_stream(torch.cuda.current_stream())  # nothing still reads the old contents
+        self.comm.recv(buf, peer, stream=ps)
+        torch.cuda.current_stream().wait_stream(ps)  # consumers of buf run after it landed
+
+    def _drain_payloads(self):
+        if self._ps is not None:
+            torch.cuda.current_stream().wait_stream(self._ps)
+            self._ps.synchronize()
 
     def _msg(self, typ: int, dst: int, tag: int, *extra):
         self._seq += 1
         self.comm.send_msg([typ, self.comm.rank, self._seq, *extra], dst, tag)
 
-    def _expect(self, src, tag, *types):
-        sender, m = self.comm.recv_msg(src, tag)
+    def _expect(self, src, tag, *types, what: str = ""):
+        try:
+            sender, m = self.comm.recv_msg(src, tag, timeout=self.timeout)
+        except CommError as e:
+            raise CommError(f"AsyncEA {what or 'wait'}: {e}") from e
         if m[0] not in types:
             raise RuntimeError(f"AsyncEA protocol error: expected {types} on tag {tag}, got {m} from {sender}")
         if m[1] != sender:
@@ -140,18 +183,21 @@ class AsyncEA:
             return False
         printClient(self.node, "Waiting to sync")
         self._msg(ENTER, SERVER_RANK, TAG_ENTER)                 # clientEnterSync (:82-92)
-        self._expect(SERVER_RANK, TAG_GRANT, GRANT)
+        self._expect(SERVER_RANK, TAG_GRANT, GRANT, what=f"client #{self.node} waiting for the server's grant")
         printClient(self.node, "Entered Sync")
         self._recv_payload(self.center, SERVER_RANK)             # clientGetCenter (:95-106)
         printClient(self.node, "Received center")
         f = self.flat                                            # calculateUpdateDiff (:109-119)
-        elastic_step_(f.data, self.center, self.delta, self.alpha, shadow=f.shadow)
+        H = HEADER  # (the header stays out of the elastic math, like AllReduceEA)
+        elastic_step_(f.data[H:], self.center[H:], self.delta[H:], self.alpha,
+                      shadow=None if f.shadow is None else f.shadow[H:])
         self._send_payload(self.delta, SERVER_RANK)              # clientSendDiff (:122-132)
         self.syncs += 1
         return True
 
     def finishClient(self) -> None:  # noqa: N802
         """Tell the server this client is done (no reference equivalent)."""
+        self._drain_payloads()
         self._msg(BYE, SERVER_RANK, TAG_ENTER)
 
     # --------------------------------------------------------------- server
@@ -166,10 +212,14 @@ class AsyncEA:
         self._one_time_init(params)
         while True:
             printServer("Server waiting to sync")
-            sender, m = self._expect(None, TAG_ENTER, ENTER, BYE)  # serverEnterSync: recvAny (:163-177)
+            missing = sorted(set(range(1, self.numNodes + 1)) - self._done)
+            sender, m = self._expect(None, TAG_ENTER, ENTER, BYE,  # serverEnterSync: recvAny (:163-177)
+                                     what=f"server waiting for clients {missing} (dead or stuck client?)")
             if m[0] == BYE:
                 self._byes += 1
+                self._done.add(sender)
                 if self._byes >= self.numNodes:
+                    self._drain_payloads()
                     return False
                 continue
             break
@@ -177,7 +227,7 @@ class AsyncEA:
         self._msg(GRANT, sender, TAG_GRANT)
         self._send_payload(self.center, sender)                   # serverSendCenter (:180-196)
         self._recv_payload(self.delta, sender)                    # serverGetUpdateDiff (:198-228)
-        add_(self.center, self.delta)
+        add_(self.center, self.delta)                            # (compute stream, after the delta landed)
         self.flat.data.copy_(self.center)
         self.flat.refresh_shadow()
         printServer(f"Received delta from client #{sender}")
@@ -190,7 +240,10 @@ class AsyncEA:
         if self._ack_work is None:
             self._ack_work = dist.irecv(self._ack_buf, src=self.tester_rank, group=self.comm.ctrl, tag=TAG_ACK)
         if block:
-            self._ack_work.wait()
+            try:
+                self._ack_work.wait(datetime.timedelta(seconds=self.timeout))
+            except RuntimeError as e:
+                raise CommError(f"AsyncEA server waiting for the tester's ACK: {e}") from e
         elif not self._ack_work.is_completed():
             return
         if int(self._ack_buf[0]) != ACK:
@@ -224,7 +277,7 @@ class AsyncEA:
     def startTest(self, params: Any) -> bool:  # noqa: N802  (:268-285)
         """Receive the next snapshot into params; False when the server stops."""
         self._one_time_init(params)
-        _, m = self._expect(SERVER_RANK, TAG_TEST, TEST, STOP)
+        _, m = self._expect(SERVER_RANK, TAG_TEST, TEST, STOP, what="tester waiting for the server")
         if m[0] == STOP:
             return False
         self._recv_payload(self.center, SERVER_RANK)

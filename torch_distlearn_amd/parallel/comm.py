@@ -36,6 +36,23 @@ _DIST_OPS = {"sum": dist.ReduceOp.SUM, "prod": dist.ReduceOp.PRODUCT, "max": dis
 
 MSG_LEN = 8  # control-plane message = int64[MSG_LEN]
 
+DEFAULT_TIMEOUT_S = 600.0
+
+
+def comm_timeout(default: float = DEFAULT_TIMEOUT_S) -> float:
+    """Communication timeout in seconds (``DISTLEARN_COMM_TIMEOUT``; the
+    examples' ``--commTimeout`` flag sets it): control-plane (gloo) operations
+    and the RCCL watchdog give up after this long instead of hanging on a dead
+    or stuck peer."""
+    v = os.environ.get("DISTLEARN_COMM_TIMEOUT")
+    return float(v) if v not in (None, "") else default
+
+
+class CommError(RuntimeError):
+    """A collective or control-plane message could not complete: a peer died,
+    hung past the timeout, or the transport failed.  The communicator is no
+    longer usable."""
+
 
 class Communicator:
     """Interface shared by the RCCL and process-group communicators."""
@@ -68,23 +85,37 @@ class Communicator:
     # ---------------- control plane (host, gloo) ----------------
     def barrier(self) -> None:
         if self.world_size > 1:
-            dist.barrier(group=self.ctrl)
+            with _ctrl_errors("barrier"):
+                dist.barrier(group=self.ctrl)
 
     def send_msg(self, msg: Sequence[int], dst: int, tag: int = 0) -> None:
         buf = torch.zeros(MSG_LEN, dtype=torch.int64)
         buf[: len(msg)] = torch.tensor(list(msg), dtype=torch.int64)
-        dist.send(buf, dst=dst, group=self.ctrl, tag=tag)
+        with _ctrl_errors(f"send to rank {dst}"):
+            dist.send(buf, dst=dst, group=self.ctrl, tag=tag)
 
-    def recv_msg(self, src: Optional[int] = None, tag: int = 0) -> Tuple[int, List[int]]:
-        """Receive a control message; ``src=None`` = any source (recvAny)."""
+    def recv_msg(self, src: Optional[int] = None, tag: int = 0,
+                 timeout: Optional[float] = None) -> Tuple[int, List[int]]:
+        """Receive a control message; ``src=None`` = any source (recvAny).
+        ``timeout`` (seconds) bounds the wait; default: the group's timeout."""
         buf = torch.zeros(MSG_LEN, dtype=torch.int64)
-        sender = dist.recv(buf, src=src, group=self.ctrl, tag=tag)
+        what = "receive from " + ("any rank" if src is None else f"rank {src}")
+        with _ctrl_errors(what):
+            if timeout is None:
+                sender = dist.recv(buf, src=src, group=self.ctrl, tag=tag)
+            else:
+                work = (dist.irecv(buf, src=src, group=self.ctrl, tag=tag) if src is not None
+                        else self.ctrl.recv_anysource([buf], tag))
+                if not work.wait(datetime.timedelta(seconds=timeout)):
+                    raise CommError(f"{what}: nothing within {timeout:.1f} s")
+                sender = src if src is not None else work._source_rank()
         return int(sender), buf.tolist()
 
     def all_reduce_host(self, t: torch.Tensor, op: str = "sum") -> None:
         """Small CPU all-reduce on the control plane."""
         if self.world_size > 1:
-            dist.all_reduce(t, op=_DIST_OPS[op], group=self.ctrl)
+            with _ctrl_errors("host all-reduce"):
+                dist.all_reduce(t, op=_DIST_OPS[op], group=self.ctrl)
 
     def broadcast_object(self, obj, root: int = 0):
         lst = [obj]
@@ -95,8 +126,25 @@ class Communicator:
     def health(self) -> str:
         return ""
 
+    def check(self) -> None:
+        """Raise :class:`CommError` if the communicator has failed."""
+        h = self.health()
+        if h:
+            raise CommError(h)
+
     def close(self) -> None:
         pass
+
+
+@contextlib.contextmanager
+def _ctrl_errors(what: str):
+    """gloo failures (peer closed the connection, op timed out) -> CommError."""
+    try:
+        yield
+    except CommError:
+        raise
+    except RuntimeError as e:
+        raise CommError(f"control plane: {what} failed: {e}") from e
 
 
 class ProcessGroupCommunicator(Communicator):
@@ -111,27 +159,32 @@ class ProcessGroupCommunicator(Communicator):
     def all_reduce(self, t, op="sum", stream=None):
         if self.world_size == 1:
             return
-        if op == "avg":
-            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.data)
-            t.div_(self.world_size)
-        else:
-            dist.all_reduce(t, op=_DIST_OPS[op], group=self.data)
+        with _ctrl_errors("all-reduce"):
+            if op == "avg":
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.data)
+                t.div_(self.world_size)
+            else:
+                dist.all_reduce(t, op=_DIST_OPS[op], group=self.data)
 
     def broadcast(self, t, root=0, stream=None):
         if self.world_size > 1:
-            dist.broadcast(t, src=root, group=self.data)
+            with _ctrl_errors("broadcast"):
+                dist.broadcast(t, src=root, group=self.data)
 
     def all_gather(self, out, t, stream=None):
         if self.world_size == 1:
             out.view(-1).copy_(t.view(-1))
             return
-        dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1), group=self.data)
+        with _ctrl_errors("all-gather"):
+            dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1), group=self.data)
 
     def send(self, t, peer, stream=None):
-        dist.send(t, dst=peer, group=self.data)
+        with _ctrl_errors(f"send to rank {peer}"):
+            dist.send(t, dst=peer, group=self.data)
 
     def recv(self, t, peer, stream=None):
-        dist.recv(t, src=peer, group=self.data)
+        with _ctrl_errors(f"receive from rank {peer}"):
+            dist.recv(t, src=peer, group=self.data)
 
 
 # CU footprint of RCCL's collectives: one workgroup per channel (rcclGenericKernel:
@@ -152,7 +205,8 @@ def rccl_channel_cap() -> int:
 class RcclCommunicator(Communicator):
     """Native RCCL data plane (C++), gloo control plane."""
 
-    def __init__(self, rank: int, world_size: int, device: torch.device, ctrl_group=None):
+    def __init__(self, rank: int, world_size: int, device: torch.device, ctrl_group=None,
+                 timeout_s: Optional[float] = None):
         C = native()
         if world_size > 1:
             os.environ.setdefault("NCCL_MAX_NCHANNELS", str(DEFAULT_RCCL_CHANNELS))  # read at comm init
@@ -165,7 +219,10 @@ class RcclCommunicator(Communicator):
             lst = [uid]
             dist.broadcast_object_list(lst, src=0, group=ctrl_group)
             uid = lst[0]
-        self._c = C.RcclCommunicator(uid, rank, world_size, self.device.index or 0)
+        # watchdog (csrc/comm/communicator.h): a collective older than timeout_s,
+        # or an RCCL async error, aborts the communicator instead of hanging
+        self.timeout_s = comm_timeout() if timeout_s is None else float(timeout_s)
+        self._c = C.RcclCommunicator(uid, rank, world_size, self.device.index or 0, self.timeout_s)
         self._in_group = 0
         # world 1 collectives are the identity and skipped; DISTLEARN_RCCL_WORLD1=1
         # issues them anyway (exercises RCCL inside hipGraph capture on one GPU)
@@ -182,32 +239,32 @@ class RcclCommunicator(Communicator):
         self._check(t)
         if self._skip1:  # identity (in place); skips RCCL's self-copy
             return
-        self._c.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], OP_CODES[op],
+        self._call(self._c.all_reduce, t.data_ptr(), t.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], OP_CODES[op],
                            stream_handle(stream))
 
     def broadcast(self, t, root=0, stream=None):
         self._check(t)
         if self._skip1:
             return
-        self._c.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], root, stream_handle(stream))
+        self._call(self._c.broadcast, t.data_ptr(), t.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], root, stream_handle(stream))
 
     def all_gather(self, out, t, stream=None):
         self._check(t)
         self._check(out)
-        self._c.all_gather(t.data_ptr(), out.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], stream_handle(stream))
+        self._call(self._c.all_gather, t.data_ptr(), out.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], stream_handle(stream))
 
     def reduce_scatter(self, out, t, op="sum", stream=None):
         self._check(t)
-        self._c.reduce_scatter(t.data_ptr(), out.data_ptr(), out.numel(), DTYPE_CODES[t.dtype], OP_CODES[op],
+        self._call(self._c.reduce_scatter, t.data_ptr(), out.data_ptr(), out.numel(), DTYPE_CODES[t.dtype], OP_CODES[op],
                                stream_handle(stream))
 
     def send(self, t, peer, stream=None):
         self._check(t)
-        self._c.send(t.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], peer, stream_handle(stream))
+        self._call(self._c.send, t.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], peer, stream_handle(stream))
 
     def recv(self, t, peer, stream=None):
         self._check(t)
-        self._c.recv(t.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], peer, stream_handle(stream))
+        self._call(self._c.recv, t.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], peer, stream_handle(stream))
 
     @contextlib.contextmanager
     def group(self):
@@ -218,7 +275,25 @@ class RcclCommunicator(Communicator):
             self._c.group_end()
 
     def health(self) -> str:
-        return self._c.async_error()
+        return "communicator closed" if self._c is None else self._c.async_error()
+
+    def track(self, stream=None) -> None:
+        """Hand the work enqueued so far on ``stream`` to the watchdog (used
+        after replaying a hipGraph that contains captured collectives)."""
+        if self.world_size > 1 or not self._skip1:
+            self._call(self._c.track, stream_handle(stream))
+
+    def set_timeout(self, seconds: float) -> None:
+        self.timeout_s = float(seconds)
+        self._c.set_timeout(self.timeout_s)
+
+    def _call(self, fn, *args):
+        try:
+            return fn(*args)
+        except RuntimeError as e:
+            if "RCCL communicator failed" in str(e):
+                raise CommError(str(e)) from e
+            raise
 
     def close(self):
         if getattr(self, "_c", None) is not None:
@@ -236,14 +311,17 @@ def _env_int(name, default):
 
 def init_communicator(rank: Optional[int] = None, world_size: Optional[int] = None, host: Optional[str] = None,
                       port: Optional[int] = None, device=None, backend: str = "auto",
-                      timeout_s: float = 600.0) -> Communicator:
+                      timeout_s: Optional[float] = None) -> Communicator:
     """Rendezvous + communicator construction.
 
     ``rank``/``world_size`` default to the torchrun env (RANK/WORLD_SIZE).
     ``host``/``port`` default to MASTER_ADDR/MASTER_PORT (127.0.0.1:29500).
     ``backend``: ``auto`` (RCCL for CUDA devices, gloo otherwise), ``rccl``,
-    ``nccl`` (torch's process group) or ``gloo``.
+    ``nccl`` (torch's process group) or ``gloo``.  ``timeout_s`` (default
+    :func:`comm_timeout`) bounds every control-plane operation and arms the
+    RCCL watchdog.
     """
+    timeout_s = comm_timeout() if timeout_s is None else float(timeout_s)
     rank = _env_int("RANK", 0) if rank is None else rank
     world_size = _env_int("WORLD_SIZE", 1) if world_size is None else world_size
     host = host or os.environ.get("MASTER_ADDR", "127.0.0.1")
@@ -256,10 +334,13 @@ def init_communicator(rank: Optional[int] = None, world_size: Optional[int] = No
     if backend == "auto":
         backend = "rccl" if dev.type == "cuda" else "gloo"
     if backend == "rccl":
-        return RcclCommunicator(rank, world_size, dev, ctrl_group=ctrl)
+        return RcclCommunicator(rank, world_size, dev, ctrl_group=ctrl, timeout_s=timeout_s)
     if backend == "nccl":
-        g = dist.new_group(backend="nccl")
-        return ProcessGroupCommunicator(g, ctrl)
-    if backend == "gloo":
-        return ProcessGroupCommunicator(ctrl, ctrl)
+        comm = ProcessGroupCommunicator(dist.new_group(backend="nccl"), ctrl)
+    elif backend == "gloo":
+        comm = ProcessGroupCommunicator(ctrl, ctrl)
+    else:
+        raise ValueError(f"unknown backend {backend!r}")
+    comm.timeout_s = timeout_s
+    return comm
     raise ValueError(f"unknown backend {backend!r}")
