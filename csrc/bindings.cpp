@@ -21,7 +21,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("add_inplace", &add_inplace);
   m.def("fill_f32", &fill_f32);
   m.def("cast_f32_bf16", &cast_f32_bf16);
-  m.def("multi_copy", &multi_copy);
   m.def("confusion_update", &confusion_update);
   m.def("bn_nhwc_fwd", &bn_nhwc_fwd);
   m.def("bn_nhwc_bwd", &bn_nhwc_bwd);
@@ -99,18 +98,4 @@ PYBIND11_MODULE(_C, m) {
       .def("next_batch", [](PartitionSampler& s, uintptr_t out, int64_t batch) {
         return s.next_batch(reinterpret_cast<int64_t*>(out), batch);
       });
-  py::class_<BatchAssembler>(m, "BatchAssembler")
-      .def(py::init([](uintptr_t images, uintptr_t labels, int64_t n, int64_t sample_bytes, std::vector<int64_t> lbl,
-                       int num_classes, int partition, int partitions, int kind, uint64_t seed, int64_t batch,
-                       int threads, int depth) {
-        auto* s = new PartitionSampler(n, std::move(lbl), num_classes, partition, partitions, kind, seed);
-        return new BatchAssembler(images, labels, n, sample_bytes, s, batch, threads, depth);
-      }))
-      .def("next", &BatchAssembler::next, py::call_guard<py::gil_scoped_release>())
-      .def("release", &BatchAssembler::release)
-      .def("slot_images", &BatchAssembler::slot_images)
-      .def("slot_labels", &BatchAssembler::slot_labels)
-      .def("slot_valid", &BatchAssembler::slot_valid)
-      .def("num_batches", &BatchAssembler::num_batches)
-      .def("reset_epoch", &BatchAssembler::reset_epoch);
 }

@@ -116,9 +116,13 @@ class RcclCommunicator {
   }
   void abort() {
     stop_watchdog();
-    std::lock_guard<std::mutex> g(mu_);
-    abort_locked("aborted by the caller");
-    release_events_locked();
+    ncclComm_t c;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      c = detach_locked("aborted by the caller");
+      release_events_locked();
+    }
+    if (c) ncclCommAbort(c);
   }
 
   int rank() const { return rank_; }
@@ -248,12 +252,14 @@ class RcclCommunicator {
     pending_.push_back({ev, std::chrono::steady_clock::now()});
   }
 
-  void abort_locked(const std::string& why) {
+  // Record why the communicator failed and take it out of service; the caller
+  // aborts the returned handle WITHOUT holding mu_ (ncclCommAbort can wait for
+  // the device), so health()/error() answer immediately.
+  ncclComm_t detach_locked(const std::string& why) {
     if (reason_.empty()) reason_ = why;
-    if (comm_) {
-      ncclCommAbort(comm_);
-      comm_ = nullptr;
-    }
+    ncclComm_t c = comm_;
+    comm_ = nullptr;
+    return c;
   }
 
   void release_events_locked() {
@@ -280,31 +286,33 @@ class RcclCommunicator {
     while (!stop_) {
       cv_.wait_for(lk, std::chrono::milliseconds(poll_ms_));
       if (stop_ || !comm_) continue;
+      ncclComm_t dead = nullptr;
       // retire completed work (in order: events of one stream complete in order;
       // across streams an old unfinished event simply keeps the queue from draining)
       while (!pending_.empty()) {
         hipError_t q = hipEventQuery(pending_.front().ev);
         if (q == hipErrorNotReady) break;
         if (q != hipSuccess) {
-          abort_locked(std::string("HIP error while waiting for a collective: ") + hipGetErrorString(q));
+          dead = detach_locked(std::string("HIP error while waiting for a collective: ") + hipGetErrorString(q));
           break;
         }
         free_.push_back(pending_.front().ev);
         pending_.pop_front();
       }
-      if (!comm_) continue;
       ncclResult_t r = ncclSuccess;
-      if (ncclCommGetAsyncError(comm_, &r) == ncclSuccess && r != ncclSuccess && r != ncclInProgress) {
-        abort_locked(std::string("RCCL async error: ") + ncclGetErrorString(r));
-        continue;
-      }
+      if (!dead && ncclCommGetAsyncError(comm_, &r) == ncclSuccess && r != ncclSuccess && r != ncclInProgress)
+        dead = detach_locked(std::string("RCCL async error: ") + ncclGetErrorString(r));
       const double limit = timeout_s_.load();
-      if (!pending_.empty() && limit > 0) {
+      if (!dead && !pending_.empty() && limit > 0) {
         double age = std::chrono::duration<double>(std::chrono::steady_clock::now() - pending_.front().t).count();
-        if (age > limit) {
-          abort_locked("collective on rank " + std::to_string(rank_) + " did not complete within " +
-                       std::to_string(limit) + " s (dead or stuck peer?)");
-        }
+        if (age > limit)
+          dead = detach_locked("collective on rank " + std::to_string(rank_) + " did not complete within " +
+                               std::to_string(limit) + " s (dead or stuck peer?)");
+      }
+      if (dead) {  // abort outside the lock: the in-flight RCCL kernels see the abort flag and exit
+        lk.unlock();
+        ncclCommAbort(dead);
+        lk.lock();
       }
     }
   }

@@ -17,7 +17,6 @@ void elastic_step(uintptr_t p, uintptr_t c, uintptr_t pending, uintptr_t out, ui
 void add_inplace(uintptr_t y, uintptr_t x, int64_t n, uintptr_t stream);
 void fill_f32(uintptr_t x, float v, int64_t n, int64_t slot_index, float slot_value, uintptr_t stream);
 void cast_f32_bf16(uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream);
-void multi_copy(uintptr_t segs, int nseg, int64_t max_bytes, uintptr_t stream);
 
 // metrics.hip ---------------------------------------------------------------
 // channels-last training BatchNorm (+ReLU, +residual) for the ResNet-50 path

@@ -144,25 +144,6 @@ __global__ void __launch_bounds__(256) cast_f32_bf16_kernel(const float* __restr
   }
 }
 
-// Multi-tensor pack/unpack (K1): copy a list of (src, dst, bytes) segments in
-// one launch. Each segment is split into 16-byte chunks; blockIdx.y = segment.
-struct CopySeg {
-  const char* src;
-  char* dst;
-  int64_t bytes;
-};
-
-__global__ void __launch_bounds__(256) multi_copy_kernel(const CopySeg* __restrict__ segs) {
-  const CopySeg sg = segs[blockIdx.y];
-  const int64_t n16 = sg.bytes >> 4;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (int64_t i = t0; i < n16; i += stride)
-    reinterpret_cast<uint4*>(sg.dst)[i] = reinterpret_cast<const uint4*>(sg.src)[i];
-  // byte tail (segments are normally 16-B multiples; kept for generality)
-  for (int64_t b = (n16 << 4) + t0; b < sg.bytes; b += stride) sg.dst[b] = sg.src[b];
-}
-
 // ---------------------------------------------------------------------------
 // Host launchers (C ABI-ish, raw pointers + stream handle)
 // ---------------------------------------------------------------------------
@@ -231,17 +212,6 @@ void cast_f32_bf16(uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream) {
   const int64_t n4 = n / 4;
   if (n4 == 0) return;
   cast_f32_bf16_kernel<<<stream_grid(n4), 256, 0, as_stream(stream)>>>((const float*)x, (bf16_t*)y, n4);
-  DL_HIP_CHECK(hipGetLastError());
-}
-
-// segs: device pointer to `nseg` CopySeg records; max_bytes: largest segment
-void multi_copy(uintptr_t segs, int nseg, int64_t max_bytes, uintptr_t stream) {
-  if (nseg <= 0) return;
-  int64_t n16 = (max_bytes + 15) / 16;
-  int gx = stream_grid(n16);
-  if (gx > 64) gx = 64;  // segments run side by side in blockIdx.y
-  dim3 grid(gx, nseg);
-  multi_copy_kernel<<<grid, 256, 0, as_stream(stream)>>>((const CopySeg*)segs);
   DL_HIP_CHECK(hipGetLastError());
 }
 

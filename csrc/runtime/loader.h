@@ -1,5 +1,4 @@
-// Native data-loading runtime: partitioned samplers + a multi-threaded,
-// pinned-memory batch assembler.
+// Native data-loading runtime: partitioned samplers.
 //
 // Replaces torch-dataset's Dataset(url, {partition, partitions}) +
 // sampledBatcher{samplerKind, batchSize, processor} worker threads
@@ -13,11 +12,9 @@
 //                      (cifar10.lua:53-71)
 //      uniform       - i.i.d. uniform over the slice
 //    Deterministic given (seed, partition): xoshiro256** streams.
-//  * BatchAssembler: `threads` workers gather uint8 samples into `depth`
-//    pinned host slots (hipHostMalloc) in sequence order, so the H2D copy of
-//    slot k overlaps the gather of slot k+1..k+depth-1 and GPU compute.
-//    Normalisation/cast happens on the GPU (metrics.hip gather_normalize), so
-//    only uint8 crosses PCIe (4x less than fp32).
+//  The dataset partition itself lives in HBM (data/__init__.py): a step
+//  uploads only indices (or nothing: DeviceLoader), and the gather +
+//  normalisation is a GPU kernel (metrics.hip gather_normalize, prep_step_gather).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -137,137 +134,5 @@ class PartitionSampler {
   std::vector<int64_t> nonempty_;
 };
 
-class BatchAssembler {
- public:
-  // images: host uint8 [n, sample_bytes], labels: host int64 [n] (both must
-  // stay alive), sampler owned by the assembler.
-  BatchAssembler(uintptr_t images, uintptr_t labels, int64_t n, int64_t sample_bytes, PartitionSampler* sampler,
-                 int64_t batch, int threads, int depth)
-      : img_((const uint8_t*)images), lab_((const int64_t*)labels), n_(n), sb_(sample_bytes), sampler_(sampler),
-        batch_(batch), depth_(depth) {
-    if (depth < 1 || threads < 1) throw std::runtime_error("depth/threads must be >= 1");
-    slots_.resize(depth);
-    for (auto& s : slots_) {
-      // pinned (DMA-able) host slots when a HIP device exists; plain memory otherwise (CPU tests)
-      if (hipHostMalloc((void**)&s.images, batch * sample_bytes, hipHostMallocDefault) != hipSuccess ||
-          hipHostMalloc((void**)&s.labels, batch * sizeof(int64_t), hipHostMallocDefault) != hipSuccess) {
-        (void)hipGetLastError();
-        pinned_ = false;
-        s.images = (uint8_t*)std::malloc(batch * sample_bytes);
-        s.labels = (int64_t*)std::malloc(batch * sizeof(int64_t));
-        if (!s.images || !s.labels) throw std::runtime_error("BatchAssembler: out of host memory");
-      }
-      s.indices.resize(batch);
-    }
-    for (int t = 0; t < threads; ++t) workers_.emplace_back([this] { work(); });
-  }
-
-  ~BatchAssembler() {
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& w : workers_) w.join();
-    for (auto& s : slots_) {
-      if (pinned_) {
-        (void)hipHostFree(s.images);
-        (void)hipHostFree(s.labels);
-      } else {
-        std::free(s.images);
-        std::free(s.labels);
-      }
-    }
-    delete sampler_;
-  }
-
-  // Blocks until the next batch in sequence order is ready; returns its slot.
-  int next() {
-    std::unique_lock<std::mutex> lk(mu_);
-    const int64_t seq = consume_seq_++;
-    const int slot = (int)(seq % depth_);
-    cv_.wait(lk, [&] { return slots_[slot].ready_seq == seq || stop_; });
-    if (stop_) throw std::runtime_error("assembler stopped");
-    slots_[slot].in_use = true;
-    return slot;
-  }
-
-  void release(int slot) {
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      slots_[slot].in_use = false;
-      slots_[slot].ready_seq = -1;
-    }
-    cv_.notify_all();
-  }
-
-  uintptr_t slot_images(int s) const { return (uintptr_t)slots_[s].images; }
-  uintptr_t slot_labels(int s) const { return (uintptr_t)slots_[s].labels; }
-  int64_t slot_valid(int s) const { return slots_[s].valid; }
-  int64_t num_batches() const { return sampler_->num_batches(batch_); }
-  void reset_epoch() {
-    std::lock_guard<std::mutex> g(mu_);
-    sampler_->reset_epoch();
-  }
-
- private:
-  struct Slot {
-    uint8_t* images = nullptr;
-    int64_t* labels = nullptr;
-    std::vector<int64_t> indices;
-    int64_t valid = 0;
-    int64_t ready_seq = -1;
-    bool in_use = false;
-    bool filling = false;
-  };
-
-  void work() {
-    for (;;) {
-      int slot;
-      int64_t seq;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        // the next sequence number may be produced once its slot is free
-        cv_.wait(lk, [&] {
-          if (stop_) return true;
-          const Slot& s = slots_[produce_seq_ % depth_];
-          return produce_seq_ < consume_seq_ + depth_ && !s.in_use && !s.filling && s.ready_seq < 0;
-        });
-        if (stop_) return;
-        seq = produce_seq_++;
-        slot = (int)(seq % depth_);
-        Slot& s = slots_[slot];
-        s.filling = true;
-        s.valid = sampler_->next_batch(s.indices.data(), batch_);  // sequence-ordered draw
-      }
-      Slot& s = slots_[slot];
-      for (int64_t b = 0; b < batch_; ++b) {
-        const int64_t i = s.indices[b];
-        std::memcpy(s.images + b * sb_, img_ + i * sb_, sb_);
-        s.labels[b] = lab_ ? lab_[i] : 0;
-      }
-      {
-        std::lock_guard<std::mutex> g(mu_);
-        s.filling = false;
-        s.ready_seq = seq;
-      }
-      cv_.notify_all();
-    }
-  }
-
-  const uint8_t* img_;
-  const int64_t* lab_;
-  int64_t n_, sb_;
-  PartitionSampler* sampler_;
-  int64_t batch_;
-  int depth_;
-  std::vector<Slot> slots_;
-  std::vector<std::thread> workers_;
-  std::mutex mu_;
-  std::condition_variable cv_;
-  int64_t produce_seq_ = 0, consume_seq_ = 0;
-  bool stop_ = false;
-  bool pinned_ = true;
-};
 
 }  // namespace dl

@@ -19,9 +19,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from torch_distlearn_amd import LocalhostTree  # noqa: E402
+from torch_distlearn_amd.checkpoint import results_dir, resume_trainer, save_trainer  # noqa: E402
 from torch_distlearn_amd.data import Dataset  # noqa: E402
 from torch_distlearn_amd.engine import DataParallelTrainer  # noqa: E402
-from torch_distlearn_amd.launch import add_node_flags, device_of, node_opts, quiet_unless_root  # noqa: E402
+from torch_distlearn_amd.launch import (add_checkpoint_flags, add_node_flags, device_of, node_opts,  # noqa: E402
+                                        quiet_unless_root)
 from torch_distlearn_amd.models import MnistConvNet, MnistMLP  # noqa: E402
 from torch_distlearn_amd.utils.metrics import ConfusionMatrix  # noqa: E402
 
@@ -45,10 +47,18 @@ def build(opt, algo):
 
 def run(opt, algo="sgd"):
     tree, dev, batcher, model, trainer = build(opt, algo)
-    trainer.synchronize_parameters()
+    first = 1
+    if opt.resume:
+        # Results/<save>/{Net, optState}: params, algorithm state, this node's sample stream
+        st = resume_trainer(results_dir(opt.save, opt.resultsRoot), trainer)
+        batcher.skip(int(st["node/drawn"][opt.nodeIndex - 1]))
+        first = int(st["epoch"]) + 1
+        print(f"resumed from {opt.resultsRoot}/{opt.save} after epoch {first - 1}")
+    else:
+        trainer.synchronize_parameters()
     conf = ConfusionMatrix(10, device=dev)
     step = 0
-    for epoch in range(1, opt.epochs + 1):
+    for epoch in range(first, opt.epochs + 1):
         nb = batcher.numBatches() if not opt.maxSteps else min(opt.maxSteps, batcher.numBatches())
         # uneven partitions: the last node(s) may run one step less -> drain protocol at sync
         for _ in range(nb):
@@ -63,6 +73,8 @@ def run(opt, algo="sgd"):
         print(conf)
         conf.zero()
         trainer.synchronize()
+        if opt.save:
+            save_trainer(results_dir(opt.save, opt.resultsRoot), trainer, epoch, per_node={"drawn": batcher.drawn})
     tree.comm.barrier()
     return trainer
 
@@ -75,6 +87,7 @@ def parser(desc, lr=0.01, batch=1):
     ap.add_argument("--data", default=None, help="directory with the MNIST idx files (optional)")
     ap.add_argument("--trainSize", type=int, default=60000)
     ap.add_argument("--graph", type=int, default=1)
+    add_checkpoint_flags(ap)
     return ap
 
 

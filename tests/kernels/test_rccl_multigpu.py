@@ -1,0 +1,241 @@
+"""N-rank RCCL data plane, one rank per GPU (the reference ran every
+collective across real nodes: lua/AllReduceSGD.lua:20, lua/AllReduceEA.lua:41,
+58-68, lua/AsyncEA.lua:87-130,155-159,183-228).
+
+Every test is parameterised over the world size and skips cleanly when the box
+has fewer GPUs (``torch.cuda.device_count() < N``); on a 1-GPU box only the
+``gloo``-on-one-GPU rehearsal rows run (same worker code, data plane = gloo on
+device tensors, hipGraph off: gloo is not capturable).  Oracles mirror the
+reference's tests: bitwise-identical parameters after the uneven-step drain
+(test/test_AllReduceSGD.lua:23-39), bit-identical EA centers
+(test/test_AllReduceEA.lua:23-41), and the AsyncEA center == initial center +
+every pushed delta.
+"""
+import os
+
+import pytest
+import torch
+
+from tests import mp
+
+pytestmark = pytest.mark.gpu
+
+CASES = [("gloo", 2), ("rccl", 2), ("rccl", 4), ("rccl", 8)]
+
+
+def _need(backend, world):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    if backend == "rccl" and torch.cuda.device_count() < world:
+        pytest.skip(f"needs {world} GPUs (one rank per GPU), box has {torch.cuda.device_count()}")
+
+
+def _setup(rank, world, port, backend):
+    os.environ.setdefault("DISTLEARN_COMM_TIMEOUT", "120")
+    import torch
+
+    from torch_distlearn_amd import Tree
+
+    dev = torch.device("cuda", rank if backend == "rccl" else 0)
+    torch.cuda.set_device(dev)
+    tree = Tree(rank + 1, world, host="127.0.0.1", port=port, device=dev, backend=backend)
+    return dev, tree
+
+
+# ---------------------------------------------------------------------------
+def _collectives_worker(rank, world, port, backend):
+    dev, tree = _setup(rank, world, port, backend)
+    c = tree.comm
+    out = {}
+    x = torch.full((1 << 20,), float(rank + 1), device=dev)
+    c.all_reduce(x)
+    out["sum"] = float(x[0]), float(x[-1])
+    b = torch.full((4099,), float(rank), device=dev, dtype=torch.bfloat16)
+    c.broadcast(b, root=world - 1)
+    out["bcast"] = float(b.float().min()), float(b.float().max())
+    g = torch.empty(world * 5, device=dev)
+    c.all_gather(g, torch.full((5,), float(rank), device=dev))
+    out["gather"] = g.view(world, 5)[:, 0].tolist()
+    if hasattr(c, "reduce_scatter"):
+        rs = torch.empty(3, device=dev)
+        c.reduce_scatter(rs, torch.arange(3 * world, device=dev, dtype=torch.float32))
+        out["rs"] = rs.tolist()
+    # ring p2p in one group (no deadlock: sends and receives are fused)
+    s = torch.full((777,), float(rank), device=dev)
+    r = torch.empty(777, device=dev)
+    with c.group():
+        c.send(s, (rank + 1) % world)
+        c.recv(r, (rank - 1) % world)
+    torch.cuda.synchronize()
+    out["ring"] = float(r[0])
+    c.check()
+    return out
+
+
+@pytest.mark.parametrize("backend,world", CASES)
+def test_collectives(backend, world):
+    _need(backend, world)
+    res = mp.run(_collectives_worker, world, backend, timeout=300)
+    tot = world * (world + 1) / 2
+    for rank, o in enumerate(res):
+        assert o["sum"] == (tot, tot)
+        assert o["bcast"] == (world - 1, world - 1)
+        assert o["gather"] == [float(r) for r in range(world)]
+        if "rs" in o:
+            assert o["rs"] == [float(world * (3 * rank + j)) for j in range(3)]
+        assert o["ring"] == float((rank - 1) % world)
+
+
+# ---------------------------------------------------------------------------
+def _sgd_worker(rank, world, port, backend):
+    dev, tree = _setup(rank, world, port, backend)
+    from torch_distlearn_amd.data import DeviceLoader, PartitionedDataset
+    from torch_distlearn_amd.engine import DataParallelTrainer
+    from torch_distlearn_amd.models import CifarConvNet
+
+    graph = backend == "rccl"
+    model = CifarConvNet(seed=0).to(dev)
+    tr = DataParallelTrainer(model, tree, lr=0.05, backend="hip", compute_dtype=torch.bfloat16,
+                             bucket_bytes=1 << 20, graph=graph, max_batch=16)
+    tr.synchronize_parameters()
+    g = torch.Generator(device=dev).manual_seed(7 + rank)
+    n_local = 16 * (6 + 3 * rank)  # uneven partitions -> uneven epochs -> drain
+    imgs = torch.randint(0, 256, (n_local, 32, 32, 3), dtype=torch.uint8, device=dev, generator=g)
+    labs = torch.randint(0, 10, (n_local,), device=dev, generator=g)
+    loader = DeviceLoader(PartitionedDataset(imgs, labs, device=dev), "permutation", 16, seed=rank)
+    steps = []
+    for _epoch in range(2):
+        nsteps = loader.steps_per_epoch
+        if graph:
+            tr.run(loader, nsteps)   # unrolled hipGraphs with captured RCCL bucket all-reduces
+        else:
+            for _ in range(nsteps):
+                tr.step(loader)
+        steps.append(int(tr.sgd.stepsPerNode.sum()))
+        tr.synchronize()  # drain (zero buckets) + winner broadcast
+    torch.cuda.synchronize()
+    tree.comm.check()
+    return {"p": tr.flat.data.cpu(), "steps": steps, "nb": len(tr.bucketer.ranges),
+            "finite": bool(torch.isfinite(tr.flat.data).all()), "captures": tr.captures}
+
+
+@pytest.mark.parametrize("backend,world", CASES)
+def test_sgd_hip_executor_buckets_graph_uneven(backend, world):
+    _need(backend, world)
+    res = mp.run(_sgd_worker, world, backend, timeout=600)
+    assert all(r["finite"] for r in res)
+    assert res[0]["nb"] == 3
+    for rank, r in enumerate(res):
+        assert r["steps"] == [6 + 3 * rank] * 2
+        assert r["p"].tobytes() == res[0]["p"].tobytes(), f"rank {rank} params differ"
+
+
+# ---------------------------------------------------------------------------
+def _ea_worker(rank, world, port, backend):
+    dev, tree = _setup(rank, world, port, backend)
+    from torch_distlearn_amd.engine import DataParallelTrainer
+    from torch_distlearn_amd.models import CifarConvNet
+
+    model = CifarConvNet(seed=0).to(dev)
+    tr = DataParallelTrainer(model, tree, lr=0.05, algo="ea", tau=3, alpha=0.3, backend="hip",
+                             compute_dtype=torch.bfloat16, graph=backend == "rccl", max_batch=16)
+    tr.synchronize_parameters()
+    g = torch.Generator(device=dev).manual_seed(11 + rank)
+    for _ in range(7 + 2 * rank):
+        x = torch.randn(16, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)
+        y = torch.randint(0, 10, (16,), device=dev, generator=g)
+        tr.step(x, y)
+    tr.synchronize()  # synchronizeCenter: drain + center scatter
+    torch.cuda.synchronize()
+    return {"c": tr.ea.center.cpu(), "p": tr.flat.data.cpu()}
+
+
+@pytest.mark.parametrize("backend,world", CASES)
+def test_ea_centers_bit_identical(backend, world):
+    _need(backend, world)
+    res = mp.run(_ea_worker, world, backend, timeout=600)
+    for r in res:
+        assert r["c"].tobytes() == res[0]["c"].tobytes()
+        assert torch.isfinite(torch.from_numpy(r["p"])).all()
+
+
+# ---------------------------------------------------------------------------
+def _async_worker(rank, world, port, backend):
+    dev, tree = _setup(rank, world, port, backend)
+    from torch_distlearn_amd import AsyncEA, FlatParams
+    from torch_distlearn_amd.utils.color_print import set_verbose
+
+    set_verbose(False)
+    torch.manual_seed(100 + rank)
+    m = torch.nn.Sequential(torch.nn.Linear(300, 200), torch.nn.Linear(200, 10)).to(dev)
+    flat = FlatParams(m, grads=False)
+    nclients = world - 1
+    ea = AsyncEA(tree, None, None, None, None, None, nclients, rank, 2, 0.25)
+    if rank == 0:
+        ea.initServer(flat)
+        init = ea.center.clone()
+        while ea.syncServer(flat):
+            pass
+        ea.shutdown()
+        torch.cuda.synchronize()
+        return {"init": init.cpu(), "center": ea.center.cpu(), "syncs": ea.syncs}
+    ea.initClient(flat)
+    sent = torch.zeros_like(ea.delta)
+    g = torch.Generator(device=dev).manual_seed(rank)
+    for _ in range(6 + rank):
+        flat.data.add_(torch.randn(flat.data.shape, device=dev, generator=g) * 0.01)
+        if ea.syncClient(flat):
+            torch.cuda.current_stream().wait_stream(ea._ps)  # (test only) read delta after the push
+            sent += ea.delta
+    ea.finishClient()
+    torch.cuda.synchronize()
+    return {"sent": sent.cpu(), "syncs": ea.syncs}
+
+
+@pytest.mark.parametrize("backend,world", CASES)
+def test_async_ea_payload_stream(backend, world):
+    _need(backend, world)
+    res = mp.run(_async_worker, world, backend, timeout=600)
+    server, clients = res[0], res[1:]
+    assert server["syncs"] == sum(c["syncs"] for c in clients) > 0
+    want = server["init"] + sum(c["sent"] for c in clients)
+    got = server["center"]
+    assert abs(got[64:] - want[64:]).max() < 1e-4
+
+
+# ---------------------------------------------------------------------------
+def test_watchdog_aborts_stuck_work(monkeypatch):
+    """World-1 RCCL communicator with a 0.5 s timeout; a 2 s spin kernel
+    (csrc/kernels/diag.hip occupy_cus, light variant: every wave exits by
+    itself) is handed to the watchdog: it must abort the communicator and
+    every later call must raise CommError instead of hanging."""
+    _need("gloo", 1)
+    import time
+
+    from torch_distlearn_amd import _native
+    from torch_distlearn_amd.parallel.comm import CommError, RcclCommunicator
+
+    monkeypatch.setenv("DISTLEARN_RCCL_WORLD1", "1")
+    dev = torch.device("cuda", 0)
+    C = _native.native()
+    comm = RcclCommunicator(0, 1, dev, ctrl_group=None, timeout_s=30.0)
+    x = torch.ones(1024, device=dev)
+    comm.all_reduce(x)
+    torch.cuda.synchronize()
+    time.sleep(0.3)
+    assert comm.health() == "" and comm._c.pending() == 0  # healthy work retires
+    comm.set_timeout(0.5)
+    s = torch.cuda.Stream(device=dev)
+    C.occupy_cus(-1, 2_000_000, 0, s.cuda_stream)
+    comm.track(s)
+    t0 = time.time()
+    while comm.health() == "" and time.time() - t0 < 5:
+        time.sleep(0.05)
+    assert "did not complete within" in comm.health()
+    assert time.time() - t0 < 1.5  # reported long before the 2 s kernel ends
+    with pytest.raises(CommError):
+        comm.all_reduce(x)
+    with pytest.raises(CommError):
+        comm.check()
+    s.synchronize()  # the spin ends by itself
+    comm.close()

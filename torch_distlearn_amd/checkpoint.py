@@ -14,8 +14,21 @@ block commented out, examples/EASGD_server.lua:37-48) but never writes
   momentum buffer, learning rate, epoch and the BatchNorm running statistics.
 * ``Log.txt`` / ``ErrorRate.log`` -- text logs (:class:`~torch_distlearn_amd.utils.metrics.Logger`).
 
-Resume = :func:`load_checkpoint` on every node, then
-``synchronizeParameters`` (root's values win, exactly like a fresh start).
+Training resume (SURVEY §5.4 "resume = load + synchronizeParameters"):
+:func:`save_trainer` is called by every node at an epoch boundary (after the
+epoch-end synchronisation) and :func:`resume_trainer` on every node of the
+restarted job.  optState then also carries ``stepsPerNode``, the EA ``center``
+and ``ea_step``, the momentum buffer, lr, epoch and per-node counters (e.g.
+batches drawn, so each node's sampler continues its stream); for AllReduceEA
+every node's own parameters (and momentum) are gathered into optState too,
+because elastic replicas differ between nodes.  Loading refreshes the bf16
+shadow the HIP executor computes with, and the algorithm's resynchronisation
+keeps what was restored: AllReduceSGD broadcasts node 1's (identical)
+parameters, AllReduceEA runs ``synchronizeCenter`` (an idle drain + center
+scatter), which leaves both the restored center and the local parameters in
+place.  Result: a run resumed from epoch k is bitwise the run that never
+stopped (tests/distributed/test_resume.py).
+
 Files are written by node 1 only, atomically (write to a temp name, rename).
 """
 from __future__ import annotations
@@ -84,6 +97,12 @@ def load_checkpoint(directory: str, model_or_params: Any) -> Dict[str, Any]:
 
 
 def trainer_state(trainer) -> Dict[str, Any]:
+    """The algorithm state of a DataParallelTrainer for ``optState`` (node-local
+    view; :func:`save_trainer` adds the per-node parts)."""
+    return _trainer_state(trainer)
+
+
+def _trainer_state(trainer) -> Dict[str, Any]:
     """Collect the algorithm state of a DataParallelTrainer for ``optState``."""
     st: Dict[str, Any] = {"lr": trainer.lr, "steps": trainer.steps}
     if trainer.sgd is not None:
@@ -97,7 +116,9 @@ def trainer_state(trainer) -> Dict[str, Any]:
 
 
 def restore_trainer_state(trainer, st: Dict[str, Any]) -> None:
+    """Inverse of :func:`trainer_state` (node-local parts)."""
     trainer.steps = int(st.get("steps", 0))
+    trainer.lr = float(st.get("lr", trainer.lr))
     if trainer.sgd is not None and "stepsPerNode" in st:
         trainer.sgd.stepsPerNode.copy_(st["stepsPerNode"])
     if trainer.ea is not None and "center" in st:
@@ -105,3 +126,59 @@ def restore_trainer_state(trainer, st: Dict[str, Any]) -> None:
         trainer.ea.step = int(st.get("ea_step", 0))
     if trainer.mom is not None and "momentum" in st:
         trainer.mom.copy_(st["momentum"].to(trainer.mom.device))
+
+
+def _gather_rows(comm, t: torch.Tensor) -> torch.Tensor:
+    """[world, numel] copy of every node's ``t`` (collective)."""
+    out = torch.empty(comm.world_size * t.numel(), dtype=t.dtype, device=t.device)
+    comm.all_gather(out, t.contiguous().view(-1))
+    return out.view(comm.world_size, -1)
+
+
+def save_trainer(directory: str, trainer, epoch: int, per_node: Optional[Dict[str, int]] = None,
+                 extra: Optional[Dict[str, Any]] = None) -> None:
+    """Checkpoint a :class:`~torch_distlearn_amd.engine.DataParallelTrainer`
+    into ``directory`` (``Results/<save>``).  Collective: every node calls it
+    at the same point (after the epoch-end synchronisation); node 1 writes
+    ``Net`` and ``optState``.  ``per_node`` integers (e.g. batches drawn) are
+    gathered into ``optState['node/<key>']`` = int64[numNodes]."""
+    tree, flat = trainer.tree, trainer.flat
+    comm = tree.comm
+    st = _trainer_state(trainer)
+    st["epoch"] = int(epoch)
+    st["algo"] = trainer.algo
+    for k, v in (per_node or {}).items():
+        row = torch.zeros(tree.numNodes, dtype=torch.int64)
+        row[tree.nodeIndex - 1] = int(v)
+        comm.all_reduce_host(row, "sum")
+        st["node/" + k] = row
+    if trainer.algo == "ea":
+        # elastic replicas differ between nodes: keep every node's own params (+ momentum)
+        st["params_per_node"] = _gather_rows(comm, flat.data)
+        if trainer.mom is not None:
+            st["momentum_per_node"] = _gather_rows(comm, trainer.mom)
+    st.update(extra or {})
+    if tree.nodeIndex == 1:
+        save_checkpoint(directory, trainer.model, st)
+    comm.barrier()
+
+
+def resume_trainer(directory: str, trainer) -> Dict[str, Any]:
+    """Restore a trainer from :func:`save_trainer`'s files (every node), then
+    resynchronise the way the algorithm needs (see the module docstring).
+    Returns optState (``epoch``, ``node/<key>`` counters, ...)."""
+    flat = trainer.flat
+    st = load_checkpoint(directory, trainer.model)
+    restore_trainer_state(trainer, st)
+    me = trainer.tree.nodeIndex - 1
+    with torch.no_grad():  # per-node parts override node 1's
+        if "params_per_node" in st:
+            flat.data.copy_(st["params_per_node"][me].to(flat.data.device))
+        if "momentum_per_node" in st and trainer.mom is not None:
+            trainer.mom.copy_(st["momentum_per_node"][me].to(trainer.mom.device))
+    flat.refresh_shadow()  # the HIP executor computes with the bf16 shadow
+    if trainer.algo == "sgd":
+        trainer.sgd.synchronizeParameters(flat)
+    elif trainer.algo == "ea":
+        trainer.ea.synchronizeCenter(flat)  # step 0 everywhere: idle drain + center scatter
+    return st

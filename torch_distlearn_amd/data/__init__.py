@@ -152,6 +152,7 @@ class Batcher:
         self.idx_dev = torch.empty(self.batch, dtype=torch.int64, device=ds.device)
         self.out = torch.empty(self.batch, ds.H, ds.W, self.cout, dtype=dtype, device=ds.device)
         self.valid = self.batch
+        self.drawn = 0  # batches drawn so far (checkpointed so a resumed run continues the stream)
 
     def numBatches(self) -> int:  # noqa: N802
         return int(self.sampler.num_batches(self.batch))
@@ -161,7 +162,15 @@ class Batcher:
     def reset(self) -> None:
         self.sampler.reset_epoch()
 
+    def skip(self, nbatches: int) -> None:
+        """Advance the sample stream by ``nbatches`` batches without gathering
+        them (resume: continue exactly where the checkpointed run was)."""
+        for _ in range(int(nbatches)):
+            _next_indices(self.sampler, self.batch, self.idx_host)
+        self.drawn += int(nbatches)
+
     def getBatch(self) -> Tuple[torch.Tensor, torch.Tensor]:  # noqa: N802
+        self.drawn += 1
         self.valid = _next_indices(self.sampler, self.batch, self.idx_host)
         ds = self.ds
         if ds.device.type == "cuda":

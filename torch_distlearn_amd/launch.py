@@ -45,11 +45,25 @@ def add_node_flags(ap: argparse.ArgumentParser, batch: int = 32, lr: float = 0.1
     ap.add_argument("--base", type=int, default=2, help="tree arity (accepted for parity; RCCL picks rings/trees)")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--commTimeout", type=float, default=None,
+                    help="seconds before a dead/stuck peer turns into an error (default 600; DISTLEARN_COMM_TIMEOUT)")
+    return ap
+
+
+def add_checkpoint_flags(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
+    """``--save NAME`` writes Results/NAME/{Net, optState} after every epoch;
+    ``--resume`` continues from them."""
+    ap.add_argument("--save", default=None, help="checkpoint directory name under --resultsRoot")
+    ap.add_argument("--resultsRoot", default="Results")
+    ap.add_argument("--resume", action="store_true", help="resume from Results/<save>")
     return ap
 
 
 def node_opts(opt) -> None:
-    """Fill nodeIndex/numNodes/gpu from torchrun-style env when not given."""
+    """Fill nodeIndex/numNodes/gpu from torchrun-style env when not given;
+    export ``--commTimeout`` for the communicators."""
+    if getattr(opt, "commTimeout", None) is not None:
+        os.environ["DISTLEARN_COMM_TIMEOUT"] = str(opt.commTimeout)
     if opt.nodeIndex is None:
         opt.nodeIndex = int(os.environ.get("RANK", "0")) + 1
     if opt.numNodes is None:

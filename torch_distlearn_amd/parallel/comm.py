@@ -155,6 +155,8 @@ class ProcessGroupCommunicator(Communicator):
         self.ctrl = ctrl_group if ctrl_group is not None else data_group
         self.rank = dist.get_rank(self.data) if dist.is_initialized() else 0
         self.world_size = dist.get_world_size(self.data) if dist.is_initialized() else 1
+        self._ops = None  # pending p2p ops inside group()
+        self._unstage = []
 
     def all_reduce(self, t, op="sum", stream=None):
         if self.world_size == 1:
@@ -176,15 +178,56 @@ class ProcessGroupCommunicator(Communicator):
             out.view(-1).copy_(t.view(-1))
             return
         with _ctrl_errors("all-gather"):
-            dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1), group=self.data)
+            if self._stage(t):  # gloo: host-staged for device tensors
+                o = torch.empty(out.numel(), dtype=out.dtype)
+                dist.all_gather_into_tensor(o, t.detach().reshape(-1).cpu(), group=self.data)
+                out.view(-1).copy_(o)
+            else:
+                dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1), group=self.data)
+
+    def _stage(self, t) -> bool:
+        return t.is_cuda and dist.get_backend(self.data) == "gloo"
 
     def send(self, t, peer, stream=None):
+        src = t.detach().cpu() if self._stage(t) else t
+        if self._ops is not None:
+            self._ops.append(dist.P2POp(dist.isend, src, peer, group=self.data))
+            return
         with _ctrl_errors(f"send to rank {peer}"):
-            dist.send(t, dst=peer, group=self.data)
+            dist.send(src, dst=peer, group=self.data)
 
     def recv(self, t, peer, stream=None):
+        dst = torch.empty(t.shape, dtype=t.dtype) if self._stage(t) else t
+        if self._ops is not None:
+            self._ops.append(dist.P2POp(dist.irecv, dst, peer, group=self.data))
+            if dst is not t:
+                self._unstage.append((t, dst))
+            return
         with _ctrl_errors(f"receive from rank {peer}"):
-            dist.recv(t, src=peer, group=self.data)
+            dist.recv(dst, src=peer, group=self.data)
+        if dst is not t:
+            t.copy_(dst)
+
+    @contextlib.contextmanager
+    def group(self):
+        """Point-to-point calls inside the block are issued together
+        (``batch_isend_irecv``), so a ring of sends and receives cannot
+        deadlock -- the gloo analogue of ncclGroupStart/End."""
+        if self._ops is not None:  # nested: the outermost group issues
+            yield
+            return
+        self._ops, self._unstage = [], []
+        try:
+            yield
+            ops, unstage = self._ops, self._unstage
+        finally:
+            self._ops = None
+        if ops:
+            with _ctrl_errors("grouped send/recv"):
+                for w in dist.batch_isend_irecv(ops):
+                    w.wait()
+        for t, h in unstage:
+            t.copy_(h)
 
 
 # CU footprint of RCCL's collectives: one workgroup per channel (rcclGenericKernel:
