@@ -27,9 +27,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from torch_distlearn_amd import LocalhostTree  # noqa: E402
+from torch_distlearn_amd.checkpoint import results_dir, resume_trainer, save_trainer  # noqa: E402
 from torch_distlearn_amd.data import Dataset  # noqa: E402
 from torch_distlearn_amd.engine import DataParallelTrainer  # noqa: E402
-from torch_distlearn_amd.launch import add_node_flags, device_of, node_opts, quiet_unless_root  # noqa: E402
+from torch_distlearn_amd.launch import (add_checkpoint_flags, add_node_flags, device_of, node_opts,  # noqa: E402
+                                        quiet_unless_root)
 from torch_distlearn_amd.models import CifarConvNet  # noqa: E402
 from torch_distlearn_amd.utils.metrics import ConfusionMatrix, JsonlMetrics  # noqa: E402
 
@@ -46,6 +48,7 @@ def main():
     ap.add_argument("--testSize", type=int, default=10000, help="synthetic test set size")
     ap.add_argument("--graph", type=int, default=1)
     ap.add_argument("--metrics", default=None, help="JSON-lines metrics file (node 1)")
+    add_checkpoint_flags(ap)
     opt = ap.parse_args()
     node_opts(opt)
     dev = device_of(opt)
@@ -66,19 +69,27 @@ def main():
     backend = opt.backend if dev.type == "cuda" else "torch"
     trainer = DataParallelTrainer(model, tree, lr=opt.learningRate, backend=backend, compute_dtype=dt,
                                   graph=bool(opt.graph) and dev.type == "cuda", max_batch=per_node)
-    trainer.synchronize_parameters()  # cifar10.lua:139
+    first = 1
+    if opt.resume:
+        st = resume_trainer(results_dir(opt.save, opt.resultsRoot), trainer)
+        train_b.skip(int(st["node/drawn"][opt.nodeIndex - 1]))
+        first = int(st["epoch"]) + 1
+        print(f"resumed from {opt.resultsRoot}/{opt.save} after epoch {first - 1}")
+    else:
+        trainer.synchronize_parameters()  # cifar10.lua:139
     conf = ConfusionMatrix(CLASSES, device=dev)
     log = JsonlMetrics(opt.metrics, rank=opt.nodeIndex - 1)
 
-    for epoch in range(1, opt.epochs + 1):
+    for epoch in range(first, opt.epochs + 1):
         conf.zero()
         nb = train_b.numBatches() if not opt.maxSteps else min(opt.maxSteps, train_b.numBatches())
         t0 = time.perf_counter()
         for i in range(nb):
             x, y = train_b.getBatch()
             loss = trainer.step(x, y)
-            if i % 50 == 0 or i == nb - 1:
-                conf.add(trainer.last_logits(), y)
+            # every training sample enters the matrix (cifar10.lua:194-196); on the GPU
+            # this is one argmax+histogram kernel per step, no host sync
+            conf.add(trainer.last_logits(), y)
         if dev.type == "cuda":
             torch.cuda.synchronize()
         dt_s = time.perf_counter() - t0
@@ -96,6 +107,8 @@ def main():
         print(f"Epoch {epoch}: test accuracy {100 * conf.totalValid:.2f}%")
         log.log(epoch=epoch, loss=float(loss), images_per_s=nb * per_node * opt.numNodes / dt_s,
                 test_acc=conf.totalValid)
+        if opt.save:
+            save_trainer(results_dir(opt.save, opt.resultsRoot), trainer, epoch, per_node={"drawn": train_b.drawn})
     tree.comm.barrier()
 
 

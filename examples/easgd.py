@@ -28,11 +28,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from torch_distlearn_amd import AsyncEA, FlatParams, Tree  # noqa: E402
-from torch_distlearn_amd.checkpoint import results_dir, save_checkpoint  # noqa: E402
+from torch_distlearn_amd.checkpoint import load_checkpoint, results_dir, save_checkpoint  # noqa: E402
 from torch_distlearn_amd.data import Dataset  # noqa: E402
 from torch_distlearn_amd.launch import device_of  # noqa: E402
 from torch_distlearn_amd.models import CifarConvNet, MnistConvNet  # noqa: E402
 from torch_distlearn_amd.ops.flat import flat_sgd_  # noqa: E402
+from torch_distlearn_amd.parallel.comm import CommError  # noqa: E402
 from torch_distlearn_amd.utils.color_print import set_verbose  # noqa: E402
 from torch_distlearn_amd.utils.metrics import ConfusionMatrix, Logger  # noqa: E402
 
@@ -62,11 +63,27 @@ def parse():
     ap.add_argument("--host", default=os.environ.get("MASTER_ADDR", "127.0.0.1"))
     ap.add_argument("--port", type=int, default=int(os.environ.get("MASTER_PORT", "8080")))
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--resume", action="store_true",
+                    help="server: start from the center in Results/<save> (written by the tester)")
+    ap.add_argument("--dieAfter", default=None, help=argparse.SUPPRESS)  # "client:syncs" fault injection (tests)
+    ap.add_argument("--commTimeout", type=float, default=None,
+                    help="seconds before a dead/stuck peer stops the run (default 600)")
     return ap.parse_args()
 
 
 def main():
     opt = parse()
+    if opt.commTimeout is not None:
+        os.environ["DISTLEARN_COMM_TIMEOUT"] = str(opt.commTimeout)
+    try:
+        run(opt)
+    except CommError as e:
+        # a dead or stuck peer (reference: every role waited forever)
+        print(f"easgd: communication failure: {e}", file=sys.stderr, flush=True)
+        sys.exit(2)
+
+
+def run(opt):
     N = opt.numNodes
     world = N + (1 if opt.noTester else 2)
     if opt.server:
@@ -95,6 +112,10 @@ def main():
     cd = torch.bfloat16 if dev.type == "cuda" else torch.float32
 
     if role == "server":
+        if opt.resume:
+            st = load_checkpoint(results_dir(opt.save, opt.resultsRoot), model)  # Net = the last tested center
+            ea.syncs = int(st.get("server_syncs", 0))
+            print(f"server: resumed center of snapshot {st.get('snapshot')} ({ea.syncs} syncs)")
         ea.initServer(flat)
         while ea.syncServer(flat):
             if ea.syncs % opt.testTime == 0:
@@ -114,6 +135,8 @@ def main():
                 loss = model.loss(model(x, compute_dtype=cd), y)
                 loss.backward()
                 ea.syncClient(flat)                                  # EASGD_client.lua:109
+                if opt.dieAfter and [rank, ea.syncs] == [int(v) for v in opt.dieAfter.split(":")]:
+                    os._exit(3)  # fault injection: this client dies without saying BYE
                 flat_sgd_(flat, opt.learningRate)  # :113-117 (pre-move grads)
         ea.finishClient()
         print(f"client {rank}: {ea.syncs} syncs, last loss {float(loss.detach()):.4f}")
@@ -141,7 +164,10 @@ def main():
             txt.write(f"snapshot {n}: train error {errs[0]:.4f} test error {errs[1]:.4f}\n")
             txt.flush()
             n += 1
-            save_checkpoint(out, model, {"snapshot": n})
+            # Net = the evaluated center (reference layout); optState = its counters
+            save_checkpoint(out, model, {"center": ea.center, "snapshot": n, "server_syncs": ea.server_syncs,
+                                         "lr": opt.learningRate, "tau": opt.communicationTime, "alpha": opt.alpha,
+                                         "train_error": errs[0], "test_error": errs[1]})
             ea.finishTest()
         print(f"tester: {n} snapshots")
     tree.comm.barrier()

@@ -49,6 +49,32 @@ def test_async_easgd_roles(tmp_path):
     d = tmp_path / "Results" / "log"
     assert (d / "ErrorRate.log").read_text().splitlines()[0] == "Training Error\tTest Error"
     assert (d / "Net").exists() and (d / "optState").exists()
+    import torch
+
+    st = torch.load(d / "optState", weights_only=True)
+    net = torch.load(d / "Net", weights_only=True)
+    # the tester's checkpoint is the evaluated center (Net, reference layout) plus its counters
+    assert st["snapshot"] >= 1 and st["server_syncs"] >= 2 and st["tau"] == 2
+    flat_center = st["center"]
+    assert torch.equal(flat_center[64:64 + net[0].numel()], net[0].reshape(-1))
+    # the server restarts from that center (--resume)
+    out = _launch(4, "easgd.py", "--numNodes", "2", "--dataset", "mnist", "--trainSize", "64", "--batchSize", "16",
+                  "--communicationTime", "2", "--testTime", "2", "--numEpochs", "1", "--resume",
+                  "--resultsRoot", str(tmp_path / "Results"), extra=("--no-node-flags",))
+    assert f"resumed center of snapshot {st['snapshot']}" in out
+
+
+def test_async_easgd_dead_client_exits_nonzero(tmp_path):
+    """examples/easgd.py with a client that dies: the server and tester exit
+    non-zero with a communication error within --commTimeout (no hang)."""
+    cmd = [sys.executable, "-m", "torch_distlearn_amd.launch", "--nproc", "4", "--no-node-flags",
+           os.path.join(ROOT, "examples", "easgd.py"), "--numNodes", "2", "--dataset", "mnist", "--trainSize", "4096",
+           "--batchSize", "16", "--communicationTime", "2", "--testTime", "2", "--numEpochs", "50",
+           "--commTimeout", "5", "--dieAfter", "2:3", "--resultsRoot", str(tmp_path / "Results")]
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "communication failure" in r.stderr and "clients [2]" in r.stderr, r.stderr[-2000:]
 
 
 @pytest.mark.parametrize("algo", ["sgd", "ea", "async"])

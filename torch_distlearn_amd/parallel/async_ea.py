@@ -106,6 +106,7 @@ class AsyncEA:
         self._ack_work = None
         self._ack_buf = torch.zeros(MSG_LEN, dtype=torch.int64)
         self.syncs = 0
+        self.server_syncs = 0  # tester: sync count of the last snapshot
         self.timeout = float(timeout) if timeout is not None else float(getattr(comm, "timeout_s", comm_timeout()))
         self._ps = None        # payload stream (GPU)
         self._done = set()     # clients that said BYE (server)
@@ -259,7 +260,7 @@ class AsyncEA:
         self._poll_ack(block=False)
         if self._test_inflight:
             return False
-        self._msg(TEST, self.tester_rank, TAG_TEST)
+        self._msg(TEST, self.tester_rank, TAG_TEST, self.syncs)
         self._send_payload(self.center, self.tester_rank)
         self._test_inflight = True
         return True
@@ -280,6 +281,7 @@ class AsyncEA:
         _, m = self._expect(SERVER_RANK, TAG_TEST, TEST, STOP, what="tester waiting for the server")
         if m[0] == STOP:
             return False
+        self.server_syncs = int(m[3])  # the server's sync count when it took this snapshot
         self._recv_payload(self.center, SERVER_RANK)
         self.flat.data.copy_(self.center)
         self.flat.refresh_shadow()
