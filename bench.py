@@ -136,7 +136,7 @@ def main():
         else:
             dist.barrier(group=wgroup)
 
-    dt, loss = 0.0, None
+    dt, loss, comm = 0.0, None, {}
     if is_server:
         from torch_distlearn_amd import AsyncEA, FlatParams
 
@@ -180,6 +180,11 @@ def main():
                           f"|g| {float(tr.flat.grad.norm()):.4e}", file=sys.stderr, flush=True)
         if step_args is None:
             tr.prepare(loader)  # (run() already did; explicit: no capture may fall in the timed region)
+        comm = {}
+        if len(workers) > 1 and a.algo == "sgd" and not cpu:
+            # communication profile: eager calibration steps with HIP events around every
+            # bucket all-reduce, OUTSIDE the timed region; training state is restored after
+            comm = tr.comm_profile(loader if step_args is None else step_args, steps=6)
         captures0 = tr.captures
         sync()
         worker_barrier()
@@ -235,6 +240,8 @@ def main():
                        **({"tau": a.tau, "alpha": a.alpha} if a.algo != "sgd" else {})},
             "final_loss": round(lval, 4),
         }
+        if comm:
+            out["comm"] = {**comm, "method": "rank-0 HIP events, 6 eager calibration steps outside the timed region"}
         print(json.dumps(out), flush=True)
     tree.comm.barrier()
 

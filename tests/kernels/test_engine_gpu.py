@@ -210,3 +210,25 @@ def test_run_captures_only_before_timed_steps(dev):
     tr.run(ld, 9, unroll=8)
     torch.cuda.synchronize()
     assert tr.captures == 4 and tr.steps == 11
+
+
+def test_comm_profile_is_side_effect_free(dev, monkeypatch):
+    """comm_profile runs eager calibration steps with HIP events around the
+    bucket all-reduces (world-1 collectives forced through RCCL) and restores
+    the training state: the next steps match a run that never profiled."""
+    monkeypatch.setenv("DISTLEARN_RCCL_WORLD1", "1")
+    outs = []
+    for prof in (False, True):
+        tr = _trainer(dev, "hip", True, 29705)
+        ld = _loader(dev, batch=16)
+        tr.run(ld, 3)
+        if prof:
+            st = tr.comm_profile(ld, steps=3)
+            assert st["steps"] == 3 and st["buckets"] == len(tr.bucketer.ranges)
+            assert st["comm_ms"] > 0 and 0.0 <= st["overlap_fraction"] <= 1.0
+            assert st["bytes_per_step"] == tr.flat.total * 4
+        tr.run(ld, 5)
+        torch.cuda.synchronize()
+        outs.append((tr.flat.data.clone(), int(ld.ctr[0]), int(tr.sgd.stepsPerNode.sum())))
+    assert outs[0][1:] == outs[1][1:]
+    assert torch.equal(outs[0][0], outs[1][0])

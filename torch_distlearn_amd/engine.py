@@ -276,6 +276,34 @@ class DataParallelTrainer:
         self._multi[k] = (g, loss)
         return self._multi[k]
 
+    def comm_profile(self, batch, steps: int = 6) -> dict:
+        """Measure the bucketed all-reduce of ``steps`` eager training steps
+        (``batch``: a DeviceLoader, or a callable i -> (x, y)) with HIP events:
+        communication time, the part of it exposed after the backward, and
+        the overlap fraction (utils/profiling.comm_summary).  Collective:
+        every rank calls it at the same point.  The steps run outside any
+        hipGraph and the training state is restored afterwards, so the
+        measured run continues exactly as if this had not been called."""
+        from .utils.profiling import comm_summary
+
+        if self.bucketer is None or self.device.type != "cuda" or self.algo != "sgd":
+            return {}
+        loader = batch if hasattr(batch, "gather_args") else None
+        saved = self._snapshot(loader)
+        self.bucketer.profile = []
+        try:
+            for i in range(steps + 1):  # the first step is a warm-up
+                x, y = (loader, None) if loader is not None else batch(i)
+                self._step_body(x, y)
+                if i == 0:
+                    self.bucketer.profile.clear()
+            out = comm_summary(self.bucketer.profile)
+        finally:
+            self.bucketer.profile = None
+        self.sgd.stepsPerNode[self.tree.nodeIndex - 1] -= steps + 1
+        self._restore(saved, loader)
+        return out
+
     def static_inputs(self):
         """The graph's input buffers (after the first step): a data loader
         that writes batches straight into them skips the per-step copy."""

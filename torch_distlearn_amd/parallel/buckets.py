@@ -47,6 +47,10 @@ class GradBucketer:
         for b in self.leaf_bucket:
             self.need[b] += 1
         self.cuda = flat.data.is_cuda
+        # communication profile (utils/profiling.py): a list while enabled; eager
+        # steps only -- nothing is recorded while a hipGraph is being captured
+        self.profile = None
+        self._rec = None
         self.stream = stream if stream is not None else (
             torch.cuda.Stream(device=flat.device, priority=-1) if self.cuda else None)
         self._reset()
@@ -67,14 +71,29 @@ class GradBucketer:
         self.launched = 0
 
     # ---------------------------------------------------------------- launch
+    def _profiling(self) -> bool:
+        return self.profile is not None and self.cuda and not torch.cuda.is_current_stream_capturing()
+
+    def _event(self, stream):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(stream)
+        return ev
+
     def _launch(self, b: int):
         s, e = self.ranges[b]
         buf = self.flat.grad[s:e]
         if self.cuda:
             cur = torch.cuda.current_stream()
             self.stream.wait_stream(cur)
+            prof = self._profiling()
+            if prof:
+                if self._rec is None:
+                    self._rec = {"buckets": []}
+                t0 = self._event(self.stream)
             with torch.cuda.stream(self.stream):
                 self.comm.all_reduce(buf, "sum", stream=self.stream)
+            if prof:
+                self._rec["buckets"].append((t0, self._event(self.stream), (e - s) * buf.element_size()))
             buf.record_stream(self.stream)
         else:
             self.comm.all_reduce(buf, "sum")
@@ -102,7 +121,15 @@ class GradBucketer:
             self.remaining[b] = 0
         self._pump()
         if self.cuda:
-            torch.cuda.current_stream().wait_stream(self.stream)
+            cur = torch.cuda.current_stream()
+            prof = self._profiling() and self._rec is not None
+            if prof:
+                self._rec["compute_done"] = self._event(cur)   # backward finished on the compute stream
+            cur.wait_stream(self.stream)
+            if prof:
+                self._rec["comm_joined"] = self._event(cur)    # the update may start
+                self.profile.append(self._rec)
+        self._rec = None
         self._reset()
 
     def drain(self):

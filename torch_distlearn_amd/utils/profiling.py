@@ -2,10 +2,10 @@
 
 * :class:`StepTimer` -- wall-clock per step with device synchronisation,
   images/s.
-* :class:`CommTimer` -- HIP events recorded on the comm stream around every
-  bucket all-reduce (no host synchronisation on the hot path); ``summary()``
-  reports total communication time and how much of it overlapped compute
-  (events on the compute stream bracket the backward).
+* :func:`comm_summary` -- communication time / exposed time / overlap
+  fraction from the events the gradient bucketer records while profiling
+  (``DataParallelTrainer.comm_profile``: eager calibration steps outside any
+  captured hipGraph, training state restored afterwards).
 * :func:`torch_profile` -- a ``torch.profiler`` context that exports a Chrome
   trace; for per-kernel counters use ``rocprofv3 --kernel-trace --stats``
   (scripts/prof_summary.py summarises its database).
@@ -42,60 +42,33 @@ class StepTimer:
         return items_per_step * len(self.times) / max(sum(self.times), 1e-12)
 
 
-class CommTimer:
-    """Attach to a GradBucketer: ``CommTimer(bucketer)``; call ``begin_step()``
-    before forward and ``end_step()`` after the optimizer step."""
+def comm_summary(records) -> dict:
+    """Summarise :class:`~torch_distlearn_amd.parallel.buckets.GradBucketer`
+    profile records (HIP events on the comm stream around every bucket
+    all-reduce, and on the compute stream where the backward ends and where
+    the update may start):
 
-    def __init__(self, bucketer):
-        self.b = bucketer
-        self.enabled = bucketer is not None and bucketer.cuda
-        self.records = []
-        self._cur = None
-        if self.enabled:
-            orig = bucketer._launch
-
-            def timed_launch(i, _orig=orig):
-                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                s.record(self.b.stream)
-                _orig(i)
-                e.record(self.b.stream)
-                if self._cur is not None:
-                    self._cur["buckets"].append((s, e))
-
-            bucketer._launch = timed_launch
-
-    def begin_step(self):
-        if not self.enabled:
-            return
-        s = torch.cuda.Event(enable_timing=True)
-        s.record()
-        self._cur = {"start": s, "buckets": []}
-
-    def end_step(self):
-        if not self.enabled or self._cur is None:
-            return
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()
-        self._cur["end"] = e
-        self.records.append(self._cur)
-        self._cur = None
-
-    def summary(self) -> dict:
-        if not self.records:
-            return {}
-        torch.cuda.synchronize()
-        step_ms = comm_ms = exposed_ms = 0.0
-        for r in self.records:
-            step_ms += r["start"].elapsed_time(r["end"])
-            for s, e in r["buckets"]:
-                comm_ms += s.elapsed_time(e)
-            if r["buckets"]:
-                # communication still running after the last compute event is exposed
-                last = r["buckets"][-1][1]
-                exposed_ms += max(0.0, r["end"].elapsed_time(last))
-        n = len(self.records)
-        return {"steps": n, "step_ms": step_ms / n, "comm_ms": comm_ms / n, "exposed_comm_ms": exposed_ms / n,
-                "overlap_fraction": 1.0 - (exposed_ms / comm_ms if comm_ms > 0 else 0.0)}
+    * ``comm_ms``          -- summed all-reduce time per step (comm stream busy);
+    * ``exposed_comm_ms``  -- time the compute stream waits for communication
+      after its backward is done (the part NOT hidden behind backward);
+    * ``overlap_fraction`` -- 1 - exposed / comm;
+    * ``busbw_GBps``       -- ring bus bandwidth of the bucket all-reduces,
+      2 (n-1)/n * bytes / time (set by the caller's world size).
+    """
+    recs = [r for r in records if r.get("buckets") and "comm_joined" in r]
+    if not recs:
+        return {}
+    torch.cuda.synchronize()
+    comm = exposed = 0.0
+    nbytes = 0
+    for r in recs:
+        comm += sum(s.elapsed_time(e) for s, e, _ in r["buckets"])
+        nbytes += sum(b for _, _, b in r["buckets"])
+        exposed += max(0.0, r["compute_done"].elapsed_time(r["comm_joined"]))
+    n = len(recs)
+    return {"steps": n, "comm_ms": round(comm / n, 4), "exposed_comm_ms": round(exposed / n, 4),
+            "overlap_fraction": round(1.0 - (exposed / comm if comm > 0 else 0.0), 4),
+            "bytes_per_step": nbytes // n, "buckets": len(recs[0]["buckets"])}
 
 
 @contextlib.contextmanager
