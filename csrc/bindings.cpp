@@ -24,6 +24,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("confusion_update", &confusion_update);
   m.def("bn_nhwc_fwd", &bn_nhwc_fwd);
   m.def("bn_nhwc_bwd", &bn_nhwc_bwd);
+  m.def("bn_rows_reduce", &bn_rows_reduce);
   m.def("gather_normalize", &gather_normalize);
 
   // ---- convnet kernels (MFMA implicit GEMM, BN/ReLU/pool, classifier head) ------
@@ -52,10 +53,22 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_relu_pool_bwd_reduce", &bn_relu_pool_bwd_reduce);
   m.def("bn_bwd_finalize", &bn_bwd_finalize);
   m.def("bn_relu_pool_bwd_apply", &bn_relu_pool_bwd_apply);
+  m.def("bn_relu_pool_bwd_apply_sums", &bn_relu_pool_bwd_apply_sums);
+  m.def("bn_relu_pool_fwd_fin", &bn_relu_pool_fwd_fin);
+  // reduction mode of the BN statistics / gradients (0: deterministic partial
+  // rows + finalize kernels, 1: atomic per-channel totals, no finalize launches)
+  static int g_host_red_atomic = 0;  // mirrors the device flags (default 0 = partial rows)
+  m.def("set_reduce_atomic", [](int on) {
+    set_reduce_atomic_conv(on);
+    set_reduce_atomic_bn(on);
+    g_host_red_atomic = on ? 1 : 0;
+  });
+  m.def("reduce_atomic", []() { return g_host_red_atomic; });
   m.def("head_fwd_bwd", &head_fwd_bwd);
   m.def("head_fwd_bwd_pool", &head_fwd_bwd_pool);
   m.def("bn_bwd_reduce_head", &bn_bwd_reduce_head);
   m.def("head_wgrad", &head_wgrad);
+  m.def("mnist_step", &mnist_step);
 
   // ---- RCCL communicator ------------------------------------------------------
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });

@@ -21,8 +21,9 @@ void cast_f32_bf16(uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream);
 // metrics.hip ---------------------------------------------------------------
 // channels-last training BatchNorm (+ReLU, +residual) for the ResNet-50 path
 void bn_nhwc_fwd(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b, uintptr_t save,
-                 uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps, double momentum, int relu,
+                 uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps, double momentum, int relu, int have_stats,
                  uintptr_t stream);
+void bn_rows_reduce(uintptr_t rows, int T, int C, uintptr_t acc, uintptr_t stream);
 void bn_nhwc_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, uintptr_t acc,
                  uintptr_t dx,
                  uintptr_t dres, uintptr_t dw, uintptr_t db, int64_t M, int C, int relu, uintptr_t stream);
@@ -47,19 +48,21 @@ void set_conv_stages(int fwd, int wgrad);
 void set_conv_waves(int waves);
 void set_conv_debug(uintptr_t buf);
 void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, int Cin, int Cout, int KS, int splits,
-                int ldo, int tile, uintptr_t stream);
+                int ldo, int tile, int atomic_creal, uintptr_t stream);
+void set_reduce_atomic_conv(int on);
 void slab_reduce(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream);
 void weight_flip_transpose(uintptr_t w, uintptr_t wt, int Cout, int Cin, int KS, uintptr_t stream);
 void pack_weight(uintptr_t w, uintptr_t wp, int Cout, int taps, int C, int Cp, uintptr_t stream);
 void pad_channels(uintptr_t x, uintptr_t xp, int64_t P, int C, int Cp, uintptr_t stream);
 void prep_step(uintptr_t x, uintptr_t xp, int64_t P, int C, int Cp, int H, int W, int sp, uintptr_t w1, uintptr_t w1p,
                int w1_cout, int taps, int w1_c, int w1_cp, std::vector<uintptr_t> tw, std::vector<uintptr_t> twt,
-               std::vector<int> tcout, std::vector<int> tcin, uintptr_t stream);
+               std::vector<int> tcout, std::vector<int> tcin, std::vector<uintptr_t> zp, std::vector<int64_t> zn,
+               uintptr_t stream);
 void prep_step_gather(uintptr_t img, uintptr_t order, uintptr_t lab_all, uintptr_t lab_out, uintptr_t ctr,
                       int n_order, int B, int C, std::vector<float> mean, std::vector<float> stdv, uintptr_t xp,
                       int Cp, int H, int W, int sp, uintptr_t w1, uintptr_t w1p, int w1_cout, int taps, int w1_c,
                       int w1_cp, std::vector<uintptr_t> tw, std::vector<uintptr_t> twt, std::vector<int> tcout,
-                      std::vector<int> tcin, uintptr_t stream);
+                      std::vector<int> tcin, std::vector<uintptr_t> zp, std::vector<int64_t> zn, uintptr_t stream);
 
 // bn_pool.hip -----------------------------------------------------------------
 void bn_finalize(uintptr_t partial, int T, int C, int64_t M, uintptr_t gamma, uintptr_t beta, uintptr_t bias,
@@ -74,6 +77,12 @@ void bn_bwd_finalize(uintptr_t partial, int T, int C, int64_t M, uintptr_t gamma
                      uintptr_t dbeta, uintptr_t acoef, uintptr_t stream);
 void bn_relu_pool_bwd_apply(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t acoef, uintptr_t dy, int B, int H,
                             int W, int C, int opad, uintptr_t stream);
+void bn_relu_pool_bwd_apply_sums(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t dgb, uintptr_t gamma, int64_t M,
+                                 uintptr_t dy, int B, int H, int W, int C, int opad, uintptr_t stream);
+void bn_relu_pool_fwd_fin(uintptr_t y, uintptr_t sums, int64_t M, uintptr_t gamma, uintptr_t beta, uintptr_t bias,
+                          uintptr_t rmean, uintptr_t rvar, float eps, float momentum, uintptr_t coef, uintptr_t out,
+                          int B, int H, int W, int C, int opad, uintptr_t stream);
+void set_reduce_atomic_bn(int on);
 
 // head.hip --------------------------------------------------------------------
 void head_fwd_bwd(uintptr_t h, uintptr_t w, uintptr_t bias, uintptr_t labels, int F, int B, int NC,
@@ -83,8 +92,15 @@ void bn_bwd_reduce_head(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t par
                         uintptr_t db, uintptr_t loss, uintptr_t slot, uintptr_t step_ctr, uintptr_t stream);
 void head_fwd_bwd_pool(uintptr_t y, uintptr_t coef, int yH, int yW, int yC, uintptr_t h_out, uintptr_t w,
                        uintptr_t bias, uintptr_t labels, int B, int NC, uintptr_t logits_out, uintptr_t dlogits,
-                       uintptr_t loss_b, uintptr_t dh, uintptr_t stream);
+                       uintptr_t loss_b, uintptr_t dh, uintptr_t fin_sums, int64_t fin_m, uintptr_t gamma,
+                       uintptr_t beta, uintptr_t conv_bias, uintptr_t rmean, uintptr_t rvar, float eps, float momentum,
+                       uintptr_t stream);
 void head_wgrad(uintptr_t h, uintptr_t dlogits, uintptr_t loss_b, int F, int B, int NC, uintptr_t dw, uintptr_t db,
                 uintptr_t loss, uintptr_t slot, uintptr_t step_ctr, uintptr_t stream);
+
+// mnist.hip -------------------------------------------------------------------
+void mnist_step(uintptr_t x, int x_bf16, uintptr_t labels, uintptr_t w1, uintptr_t b1, uintptr_t w2, uintptr_t b2,
+                uintptr_t wf, uintptr_t bf, uintptr_t gw1, uintptr_t gb1, uintptr_t gw2, uintptr_t gb2, uintptr_t gwf,
+                uintptr_t gbf, uintptr_t logp, uintptr_t loss_b, int B, uintptr_t stream);
 
 }  // namespace dl

@@ -286,15 +286,51 @@ BnGeom make_geom(int64_t M, int C, dim3* grid) {
 
 }  // namespace
 
-// acc: fp32 [2C], zeroed by the caller.
+// Column sums of a convolution epilogue's deterministic per-M-tile partial
+// rows [T][2][C] (sum, sum of squares) into acc [2C] (one block per channel,
+// fixed order): the BatchNorm statistics of a 1x1 conv output for T*2C reads
+// instead of a pass over the M*C activation (ops/conv.py).
+__global__ void __launch_bounds__(kThreads) bn_rows_reduce_kernel(const float* __restrict__ rows, int T, int C,
+                                                                  float* __restrict__ acc) {
+  const int c = blockIdx.x;
+  float s1 = 0.f, s2 = 0.f;
+  for (int t = threadIdx.x; t < T; t += kThreads) {
+    s1 += rows[(int64_t)t * 2 * C + c];
+    s2 += rows[(int64_t)t * 2 * C + C + c];
+  }
+  __shared__ float red[2][kThreads / 64];
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { red[0][wid] = s1; red[1][wid] = s2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.f, b = 0.f;
+    for (int w = 0; w < kThreads / 64; ++w) { a += red[0][w]; b += red[1][w]; }
+    acc[c] = a;
+    acc[C + c] = b;
+  }
+}
+
+void bn_rows_reduce(uintptr_t rows, int T, int C, uintptr_t acc, uintptr_t stream) {
+  if (T <= 0 || C <= 0) throw std::runtime_error("bn_rows_reduce: empty");
+  bn_rows_reduce_kernel<<<C, kThreads, 0, as_stream(stream)>>>((const float*)rows, T, C, (float*)acc);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+// acc: fp32 [2C], zeroed by the caller.  have_stats: acc already holds the
+// per-channel sum / sum of squares of x (emitted by the producing 1x1
+// convolution's epilogue, ops/conv.py): the statistics pass is skipped.
 void bn_nhwc_fwd(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b, uintptr_t save,
                  uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps, double momentum, int relu,
-                 uintptr_t stream) {
+                 int have_stats, uintptr_t stream) {
   dim3 grid;
   const BnGeom g = make_geom(M, C, &grid);
   hipStream_t s = as_stream(stream);
-  bn_nhwc_stats_kernel<<<grid, kThreads, 0, s>>>((const bf16_t*)x, g, (float*)acc);
-  DL_HIP_CHECK(hipGetLastError());
+  if (!have_stats) {
+    bn_nhwc_stats_kernel<<<grid, kThreads, 0, s>>>((const bf16_t*)x, g, (float*)acc);
+    DL_HIP_CHECK(hipGetLastError());
+  }
   bn_nhwc_fwd_apply_kernel<<<grid, kThreads, 0, s>>>((const bf16_t*)x, (const bf16_t*)res, (bf16_t*)y,
                                                       (const float*)acc, (const float*)w, (const float*)b, g,
                                                       (float)eps, relu, (float*)save, (float*)run_mean,

@@ -23,8 +23,15 @@
 #include "dl_common.h"
 #include "dl_ops.h"
 #include "head_wgrad_dev.h"
+#include "bn_fin_dev.h"
 
 namespace dl {
+
+// reduction mode (conv_igemm.hip g_red_atomic; set together by set_reduce_atomic):
+// 1 = the backward reduce atomically adds its per-block totals into the BN
+// parameter gradients [dgamma (C) ; dbeta (C)] (zeroed by the step's prep
+// kernel), and the apply kernel derives its coefficients from them.
+__device__ int g_red_atomic_bn = 0;
 
 __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
   f[0] = lo_bf16(v.x); f[1] = hi_bf16(v.x); f[2] = lo_bf16(v.y); f[3] = hi_bf16(v.y);
@@ -139,6 +146,53 @@ __global__ void __launch_bounds__(256) bn_relu_pool_fwd_kernel(const bf16_t* __r
     const uint4 v2 = *reinterpret_cast<const uint4*>(base + (int64_t)W * C);
     const uint4 v3 = *reinterpret_cast<const uint4*>(base + (int64_t)W * C + C);
     float f[8];
+    unpack8(v0, f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mx[k] = fmaf(sc[k], f[k], sh[k]);
+    unpack8(v1, f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mx[k] = fmaxf(mx[k], fmaf(sc[k], f[k], sh[k]));
+    unpack8(v2, f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mx[k] = fmaxf(mx[k], fmaf(sc[k], f[k], sh[k]));
+    unpack8(v3, f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mx[k] = fmaxf(fmaxf(mx[k], fmaf(sc[k], f[k], sh[k])), 0.f);
+    *reinterpret_cast<uint4*>(out + ((b * Hop + oh + opad) * Wop + ow + opad) * (int64_t)C + c0) = pack8(mx);
+  }
+}
+
+// Same, with the BN coefficients derived from the atomically accumulated
+// statistics (bn_fin_dev.h); block 0 publishes coef + running statistics.
+__global__ void __launch_bounds__(256) bn_relu_pool_fwd_fin_kernel(const bf16_t* __restrict__ y, const BnFin fin,
+                                                                   bf16_t* __restrict__ out, int B, int H, int W, int C,
+                                                                   int opad) {
+  bn_fin_publish(fin, C);
+  const int C8 = C >> 3, Ho = H >> 1, Wo = W >> 1;
+  const int Hop = Ho + 2 * opad, Wop = Wo + 2 * opad;
+  const int64_t total = (int64_t)B * Ho * Wo * C8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int cur = -1;
+  float sc[8], sh[8];
+  for (; i < total; i += stride) {
+    const int c8 = (int)(i % C8);
+    const int64_t pix = i / C8;
+    const int ow = (int)(pix % Wo);
+    const int64_t t = pix / Wo;
+    const int oh = (int)(t % Ho);
+    const int64_t b = t / Ho;
+    const int c0 = c8 * 8;
+    if (c8 != cur) {  // the chunk is fixed per thread whenever C8 divides the stride
+      bn_fin_coef8(fin, C, c0, sc, sh);
+      cur = c8;
+    }
+    const bf16_t* base = y + (((b * H + 2 * oh) * W) + 2 * ow) * (int64_t)C + c0;
+    const uint4 v0 = *reinterpret_cast<const uint4*>(base);
+    const uint4 v1 = *reinterpret_cast<const uint4*>(base + C);
+    const uint4 v2 = *reinterpret_cast<const uint4*>(base + (int64_t)W * C);
+    const uint4 v3 = *reinterpret_cast<const uint4*>(base + (int64_t)W * C + C);
+    float f[8], mx[8];
     unpack8(v0, f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) mx[k] = fmaf(sc[k], f[k], sh[k]);
@@ -275,8 +329,13 @@ __device__ __forceinline__ void bwd_reduce_body(const bf16_t* __restrict__ y, co
     const int first = (int)(((int64_t)ch - ((int64_t)bid * blockDim.x) % C8 + C8) % C8);
     float a = 0.f, bsum = 0.f;
     for (int t = first; t < (int)blockDim.x; t += C8) { a += red[t][k]; bsum += red[t][8 + k]; }
-    partial[(int64_t)bid * 2 * C + c] = a;
-    partial[(int64_t)bid * 2 * C + C + c] = bsum;
+    if (g_red_atomic_bn) {  // partial = [dgamma ; dbeta] = [sum dz*xhat ; sum dz]
+      unsafeAtomicAdd(partial + c, bsum);
+      unsafeAtomicAdd(partial + C + c, a);
+    } else {
+      partial[(int64_t)bid * 2 * C + c] = a;
+      partial[(int64_t)bid * 2 * C + C + c] = bsum;
+    }
   }
 }
 
@@ -333,12 +392,16 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
   }
 }
 
+// SUMS: acoef is the accumulated [dgamma ; dbeta] (mode 1) and the apply
+// coefficients are derived here: a = gamma*invstd, b = -a*dgamma/M, c = -a*dbeta/M.
+template <bool SUMS>
 __global__ void __launch_bounds__(256) bn_relu_pool_bwd_apply_kernel(const bf16_t* __restrict__ y,
                                                                      const bf16_t* __restrict__ dP,
                                                                      const float* __restrict__ coef,
                                                                      const float* __restrict__ acoef,
                                                                      bf16_t* __restrict__ dy, int B, int H, int W,
-                                                                     int C, int opad) {
+                                                                     int C, int opad, const float* __restrict__ gamma,
+                                                                     float inv_m) {
   // dy: [B][H+2 opad][W+2 opad][C], written in the interior (zero border =
   // the dgrad convolution's spatial padding)
   const int C8 = C >> 3, Ho = H >> 1, Wo = W >> 1;
@@ -357,9 +420,22 @@ __global__ void __launch_bounds__(256) bn_relu_pool_bwd_apply_kernel(const bf16_
     load8(cx.sc, coef + 2 * C + c0);
     load8(cx.sh, coef + 3 * C + c0);
     float ka[8], kb[8], kc[8];
-    load8(ka, acoef + c0);
-    load8(kb, acoef + C + c0);
-    load8(kc, acoef + 2 * C + c0);
+    if constexpr (SUMS) {
+      float gm[8], dg[8], db[8];
+      load8(gm, gamma + c0);
+      load8(dg, acoef + c0);
+      load8(db, acoef + C + c0);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        ka[k] = gm[k] * cx.is[k];
+        kb[k] = -ka[k] * dg[k] * inv_m;
+        kc[k] = -ka[k] * db[k] * inv_m;
+      }
+    } else {
+      load8(ka, acoef + c0);
+      load8(kb, acoef + C + c0);
+      load8(kc, acoef + 2 * C + c0);
+    }
     float yv[4][8], dz[4][8];
     bwd_window(y, dP, cx, b, oh, ow, H, W, C, c0, yv, dz);
     bf16_t* base = dy + (((b * Hp + 2 * oh + opad) * Wp) + 2 * ow + opad) * (int64_t)C + c0;
@@ -455,9 +531,38 @@ void bn_relu_pool_bwd_apply(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t
                             int W, int C, int opad, uintptr_t stream) {
   check_c(C);
   const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
-  bn_relu_pool_bwd_apply_kernel<<<stream_grid(total), 256, 0, as_stream(stream)>>>(
-      (const bf16_t*)y, (const bf16_t*)dP, (const float*)coef, (const float*)acoef, (bf16_t*)dy, B, H, W, C, opad);
+  bn_relu_pool_bwd_apply_kernel<false><<<stream_grid(total), 256, 0, as_stream(stream)>>>(
+      (const bf16_t*)y, (const bf16_t*)dP, (const float*)coef, (const float*)acoef, (bf16_t*)dy, B, H, W, C, opad,
+      nullptr, 0.f);
   DL_HIP_CHECK(hipGetLastError());
+}
+
+// mode 1: dgb = [dgamma ; dbeta] accumulated by the reduce (no bn_bwd_finalize launch)
+void bn_relu_pool_bwd_apply_sums(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t dgb, uintptr_t gamma, int64_t M,
+                                 uintptr_t dy, int B, int H, int W, int C, int opad, uintptr_t stream) {
+  check_c(C);
+  const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
+  bn_relu_pool_bwd_apply_kernel<true><<<stream_grid(total), 256, 0, as_stream(stream)>>>(
+      (const bf16_t*)y, (const bf16_t*)dP, (const float*)coef, (const float*)dgb, (bf16_t*)dy, B, H, W, C, opad,
+      (const float*)gamma, 1.0f / (float)M);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+// mode 1 forward apply: coefficients from the accumulated statistics `sums` [2][C]
+void bn_relu_pool_fwd_fin(uintptr_t y, uintptr_t sums, int64_t M, uintptr_t gamma, uintptr_t beta, uintptr_t bias,
+                          uintptr_t rmean, uintptr_t rvar, float eps, float momentum, uintptr_t coef, uintptr_t out,
+                          int B, int H, int W, int C, int opad, uintptr_t stream) {
+  check_c(C);
+  const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
+  const BnFin fin = make_bn_fin(sums, M, gamma, beta, bias, rmean, rvar, eps, momentum, coef);
+  bn_relu_pool_fwd_fin_kernel<<<stream_grid(total), 256, 0, as_stream(stream)>>>((const bf16_t*)y, fin,
+                                                                                   (bf16_t*)out, B, H, W, C, opad);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+void set_reduce_atomic_bn(int on) {
+  const int v = on ? 1 : 0;
+  DL_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_red_atomic_bn), &v, sizeof(int)));
 }
 
 }  // namespace dl

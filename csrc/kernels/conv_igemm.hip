@@ -32,6 +32,24 @@
 
 namespace dl {
 
+// Reduction mode of the train-mode BatchNorm statistics (set_reduce_atomic):
+// 0 = one deterministic partial row per M tile (reduced by bn_finalize),
+// 1 = every workgroup atomically adds its per-channel totals into ONE
+// zero-initialised [2][C] row (the consumer -- bn_relu_pool_fwd_fin / the
+// head -- derives the BN coefficients itself: no finalize launch).  Read once
+// per workgroup epilogue (a wave-uniform load).
+__device__ int g_red_atomic = 0;
+
+__device__ __forceinline__ void put_stats(float* __restrict__ stats, int64_t row, int C, int n, float sa, float sb) {
+  if (g_red_atomic) {
+    unsafeAtomicAdd(stats + n, sa);
+    unsafeAtomicAdd(stats + C + n, sb);
+  } else {
+    stats[row * 2 * C + n] = sa;
+    stats[row * 2 * C + C + n] = sb;
+  }
+}
+
 struct ConvGeom {
   int B, H, W;
   int Hp, Wp;  // spatially zero-padded input dims (H + 2 pad, W + 2 pad)
@@ -240,8 +258,7 @@ __device__ __forceinline__ void conv_fwd_epilogue(const f32x4 (&acc)[BM / WM / 1
           float sa = 0.f, sb = 0.f;
 #pragma unroll
           for (int q = 0; q < WM; ++q) { sa += red[(q * 2) * BN + c]; sb += red[(q * 2 + 1) * BN + c]; }
-          stats[(int64_t)tm * 2 * g.Cout + n] = sa;
-          stats[(int64_t)tm * 2 * g.Cout + g.Cout + n] = sb;
+          put_stats(stats, tm, g.Cout, n, sa, sb);
         }
       }
     }
@@ -561,8 +578,7 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
       float sa = 0.f, sb = 0.f;
 #pragma unroll
       for (int q = 0; q < WM; ++q) { sa += red[(q * 2) * BN + c]; sb += red[(q * 2 + 1) * BN + c]; }
-      stats[(int64_t)tm * 2 * g.Cout + n0 + c] = sa;
-      stats[(int64_t)tm * 2 * g.Cout + g.Cout + n0 + c] = sb;
+      put_stats(stats, tm, g.Cout, n0 + c, sa, sb);
     }
   }
 }
@@ -914,8 +930,7 @@ __global__ void __launch_bounds__(256) splitk_combine_kernel(const float* __rest
       const int ch = c >> 3, k = c & 7;
       float a = 0.f, b = 0.f;
       for (int t = ch; t < rpi * tpr; t += tpr) { a += red[t][k]; b += red[t][8 + k]; }
-      stats[(int64_t)blockIdx.x * 2 * N + c] = a;
-      stats[(int64_t)blockIdx.x * 2 * N + N + c] = b;
+      put_stats(stats, blockIdx.x, N, c, a, b);
     }
   }
 }
@@ -925,10 +940,13 @@ __global__ void __launch_bounds__(256) splitk_combine_kernel(const float* __rest
 // Tiles are staged [m][col] (rows = the reduction index) by LDS-DMA and read
 // as MFMA operands with ds_read_b64_tr_b16.  BK = 64 rows of m per stage.
 // --------------------------------------------------------------------------
-template <int BM, int BN, int STAGES, int WM = 2, int WN = 2, bool PF = true>
+// ATOM: split-K partials are atomically added straight into the zeroed fp32
+// weight gradient [Cout][taps][creal] (creal <= Cin drops zero-padded input
+// channels) -- no slab round trip and no slab_reduce launch.
+template <int BM, int BN, int STAGES, int WM = 2, int WN = 2, bool PF = true, bool ATOM = false>
 __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                          float* __restrict__ out, const ConvGeom g, int m_per_split,
-                                                         int ldo) {
+                                                         int ldo, int creal) {
   // dy and x are both spatially zero-padded [B][Hp][Wp][C] (dy: interior at
   // (pad, pad)).  A 64-row M step starts at a multiple of 64 output pixels;
   // with W | 64 and (H*W | 64 or 64 | H*W) the padded position of row r of the
@@ -1118,8 +1136,25 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
   if (i < nk) step(fa0, fb0, fa1, fb1);
   }
 
-  float* o = out + (int64_t)split * g.Cout * ldo;
   const int col_l = lane & 15, rq = lane >> 4;
+  if constexpr (ATOM) {
+    const int logCin = g.logC8 + 3, taps = g.KS * g.KS;
+#pragma unroll
+    for (int a = 0; a < FM; ++a)
+#pragma unroll
+      for (int b = 0; b < FN; ++b) {
+        const int co = co0 + wm * TM + a * 16 + col_l;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = k0 + wn * TN + b * 16 + rq * 4 + r;
+          const int tap = k >> logCin, c = k & ((1 << logCin) - 1);
+          if (co < g.Cout && k < g.K && c < creal)
+            unsafeAtomicAdd(out + ((int64_t)co * taps + tap) * creal + c, acc[a][b][r]);
+        }
+      }
+    return;
+  }
+  float* o = out + (int64_t)split * g.Cout * ldo;
 #pragma unroll
   for (int a = 0; a < FM; ++a)
 #pragma unroll
@@ -1219,6 +1254,11 @@ struct PrepArgs {
   const bf16_t* tw[4]; bf16_t* twt[4]; int tcout[4], tcin[4];
   int nb_pad, nb_pack, nb_t[4];
   int quad;  // fast gather/pad path: one block per image, 4 pixels per thread
+  // zero job: the step's atomic accumulators (BN statistics, BN parameter
+  // gradients, split-K weight gradients) -- float4 granularity
+  int nz, nb_zero;
+  float* zp[8];
+  int zn4[8];
 };
 
 __global__ void __launch_bounds__(256) prep_step_kernel(const PrepArgs a) {
@@ -1300,6 +1340,18 @@ __global__ void __launch_bounds__(256) prep_step_kernel(const PrepArgs a) {
     return;
   }
   blk -= a.nb_pack;
+  if (blk < a.nb_zero) {
+    int64_t total = 0;
+    for (int j = 0; j < a.nz; ++j) total += a.zn4[j];
+    for (int64_t i = (int64_t)blk * 256 + threadIdx.x; i < total; i += (int64_t)a.nb_zero * 256) {
+      int64_t r = i;
+      int j = 0;
+      while (r >= a.zn4[j]) { r -= a.zn4[j]; ++j; }
+      reinterpret_cast<float4*>(a.zp[j])[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    return;
+  }
+  blk -= a.nb_zero;
   for (int j = 0; j < a.nt; ++j) {
     if (blk >= a.nb_t[j]) { blk -= a.nb_t[j]; continue; }
     const int Cin = a.tcin[j], Cout = a.tcout[j], taps = a.taps;
@@ -1355,7 +1407,19 @@ __global__ void __launch_bounds__(256) prep_step_kernel(const PrepArgs a) {
 
 static void launch_prep(PrepArgs& a, int64_t P, uintptr_t w1, uintptr_t w1p, int w1_cout, int taps, int w1_c,
                         int w1_cp, const std::vector<uintptr_t>& tw, const std::vector<uintptr_t>& twt,
-                        const std::vector<int>& tcout, const std::vector<int>& tcin, uintptr_t stream) {
+                        const std::vector<int>& tcout, const std::vector<int>& tcin,
+                        const std::vector<uintptr_t>& zp, const std::vector<int64_t>& zn, uintptr_t stream) {
+  if (zp.size() != zn.size() || zp.size() > 8) throw std::runtime_error("prep_step: up to 8 zero ranges");
+  a.nz = (int)zp.size();
+  int64_t z4 = 0;
+  for (int j = 0; j < a.nz; ++j) {
+    if (zn[j] % 4 != 0 || zp[j] % 16 != 0 || zn[j] <= 0 || zn[j] / 4 >= (1ll << 31))
+      throw std::runtime_error("prep_step: zero ranges must be 16-byte aligned multiples of 4 floats");
+    a.zp[j] = (float*)zp[j];
+    a.zn4[j] = (int)(zn[j] / 4);
+    z4 += zn[j] / 4;
+  }
+  a.nb_zero = (int)std::min<int64_t>((z4 + 1023) / 1024, 256);
   if (a.C > 16 || a.Cp > 16 || a.Cp % 8 != 0) throw std::runtime_error("prep_step: input channels must pad to 8 or 16");
   if (P >= (1ll << 31)) throw std::runtime_error("prep_step: too many pixels");
   if (P > 0 && (a.H <= 0 || a.W <= 0 || P % ((int64_t)a.H * a.W) != 0)) throw std::runtime_error("prep_step: P != B*H*W");
@@ -1367,7 +1431,7 @@ static void launch_prep(PrepArgs& a, int64_t P, uintptr_t w1, uintptr_t w1p, int
   a.quad = (a.C == 3 && a.Cp == 8 && P > 0 && a.W % 4 == 0) ? 1 : 0;
   a.nb_pad = a.quad ? (int)(P / ((int64_t)a.H * a.W)) : (int)std::min<int64_t>((P + 255) / 256, 1024);
   a.nb_pack = (int)std::min<int64_t>(((int64_t)w1_cout * taps * w1_cp + 255) / 256, 256);
-  int total = a.nb_pad + a.nb_pack;
+  int total = a.nb_pad + a.nb_pack + a.nb_zero;
   for (int j = 0; j < a.nt; ++j) {
     a.tw[j] = (const bf16_t*)tw[j]; a.twt[j] = (bf16_t*)twt[j];
     a.tcout[j] = tcout[j]; a.tcin[j] = tcin[j];
@@ -1382,11 +1446,12 @@ static void launch_prep(PrepArgs& a, int64_t P, uintptr_t w1, uintptr_t w1p, int
 
 void prep_step(uintptr_t x, uintptr_t xp, int64_t P, int C, int Cp, int H, int W, int sp, uintptr_t w1, uintptr_t w1p,
                int w1_cout, int taps, int w1_c, int w1_cp, std::vector<uintptr_t> tw, std::vector<uintptr_t> twt,
-               std::vector<int> tcout, std::vector<int> tcin, uintptr_t stream) {
+               std::vector<int> tcout, std::vector<int> tcin, std::vector<uintptr_t> zp, std::vector<int64_t> zn,
+               uintptr_t stream) {
   PrepArgs a{};
   a.x = (const bf16_t*)x; a.xp = (bf16_t*)xp; a.C = C; a.Cp = Cp;
   a.H = H; a.W = W; a.sp = sp;
-  launch_prep(a, P, w1, w1p, w1_cout, taps, w1_c, w1_cp, tw, twt, tcout, tcin, stream);
+  launch_prep(a, P, w1, w1p, w1_cout, taps, w1_c, w1_cp, tw, twt, tcout, tcin, zp, zn, stream);
 }
 
 // Same launch with the step's input gathered on the device: batch b of step
@@ -1398,7 +1463,7 @@ void prep_step_gather(uintptr_t img, uintptr_t order, uintptr_t lab_all, uintptr
                       int n_order, int B, int C, std::vector<float> mean, std::vector<float> stdv, uintptr_t xp,
                       int Cp, int H, int W, int sp, uintptr_t w1, uintptr_t w1p, int w1_cout, int taps, int w1_c,
                       int w1_cp, std::vector<uintptr_t> tw, std::vector<uintptr_t> twt, std::vector<int> tcout,
-                      std::vector<int> tcin, uintptr_t stream) {
+                      std::vector<int> tcin, std::vector<uintptr_t> zp, std::vector<int64_t> zn, uintptr_t stream) {
   if (C > 3 || mean.size() < (size_t)C || stdv.size() < (size_t)C) throw std::runtime_error("prep_step_gather: C <= 3");
   if (n_order <= 0 || B <= 0) throw std::runtime_error("prep_step_gather: empty order / batch");
   PrepArgs a{};
@@ -1409,7 +1474,7 @@ void prep_step_gather(uintptr_t img, uintptr_t order, uintptr_t lab_all, uintptr
     a.mean[c] = c < C ? mean[c] : 0.f;
     a.inv_std[c] = c < C ? 1.0f / stdv[c] : 1.f;
   }
-  launch_prep(a, (int64_t)B * H * W, w1, w1p, w1_cout, taps, w1_c, w1_cp, tw, twt, tcout, tcin, stream);
+  launch_prep(a, (int64_t)B * H * W, w1, w1p, w1_cout, taps, w1_c, w1_cp, tw, twt, tcout, tcin, zp, zn, stream);
 }
 
 // --------------------------------------------------------------------------
@@ -1664,8 +1729,10 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
 }
 
 // out: fp32 [splits][Cout][ldo], ldo >= K (K = KS*KS*Cin); tile 0 = 128x64, 1 = 64x64 (co x k)
+// atomic_creal > 0: every split atomically adds into the ZEROED fp32 gradient
+// out = [Cout][KS*KS][atomic_creal] (no slabs, no slab_reduce).
 void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, int Cin, int Cout, int KS, int splits,
-                int ldo, int tile, uintptr_t stream) {
+                int ldo, int tile, int atomic_creal, uintptr_t stream) {
   ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
   if (ldo < g.K) throw std::runtime_error("conv_wgrad: ldo < K");
   if (ldo % 4 != 0) throw std::runtime_error("conv_wgrad: ldo % 4 != 0 (16-byte slab stores)");
@@ -1674,21 +1741,23 @@ void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, i
   if (Cout % bm != 0) throw std::runtime_error("conv_wgrad: Cout must be a multiple of the Cout tile");
   if (W > 64) throw std::runtime_error("conv_wgrad: needs W <= 64");
   if (splits < 1) splits = 1;
+  if (atomic_creal > Cin) throw std::runtime_error("conv_wgrad: atomic_creal > Cin");
   int mps = (g.M + splits - 1) / splits;
   mps = (mps + 63) / 64 * 64;  // 64-row aligned M steps (padded-layout addressing)
   hipStream_t s = as_stream(stream);
-#define DL_WG(BM_, BN_, ST_, WM_, WN_)                                                                     \
+  const bool atom = atomic_creal > 0;
+#define DL_WGX(BM_, BN_, ST_, WM_, WN_, PF_)                                                                \
   do {                                                                                                     \
     const int nt = ((g.Cout + BM_ - 1) / BM_) * ((g.K + BN_ - 1) / BN_);                                  \
-    conv_wgrad_kernel<BM_, BN_, ST_, WM_, WN_><<<dim3(nt, splits), 64 * WM_ * WN_, 0, s>>>(                \
-        (const bf16_t*)dy, (const bf16_t*)x, (float*)out, g, mps, ldo);                                    \
+    if (atom)                                                                                              \
+      conv_wgrad_kernel<BM_, BN_, ST_, WM_, WN_, PF_, true><<<dim3(nt, splits), 64 * WM_ * WN_, 0, s>>>(   \
+          (const bf16_t*)dy, (const bf16_t*)x, (float*)out, g, mps, ldo, atomic_creal);                     \
+    else                                                                                                   \
+      conv_wgrad_kernel<BM_, BN_, ST_, WM_, WN_, PF_, false><<<dim3(nt, splits), 64 * WM_ * WN_, 0, s>>>(  \
+          (const bf16_t*)dy, (const bf16_t*)x, (float*)out, g, mps, ldo, Cin);                              \
   } while (0)
-#define DL_WGN(BM_, BN_, ST_, WM_, WN_)                                                                     \
-  do {                                                                                                     \
-    const int nt = ((g.Cout + BM_ - 1) / BM_) * ((g.K + BN_ - 1) / BN_);                                  \
-    conv_wgrad_kernel<BM_, BN_, ST_, WM_, WN_, false><<<dim3(nt, splits), 64 * WM_ * WN_, 0, s>>>(                \
-        (const bf16_t*)dy, (const bf16_t*)x, (float*)out, g, mps, ldo);                                    \
-  } while (0)
+#define DL_WG(BM_, BN_, ST_, WM_, WN_) DL_WGX(BM_, BN_, ST_, WM_, WN_, true)
+#define DL_WGN(BM_, BN_, ST_, WM_, WN_) DL_WGX(BM_, BN_, ST_, WM_, WN_, false)
   // the wgrad pipeline keeps >= 2 stages in flight beyond the one being read.
   // Measured (batch 128): 64x64 tiles want 4 stages (2 WGs/CU still fit:
   // wgrad1 22.1 -> 16.8 us), 128x64 tiles 3 (4 would drop to 1 WG/CU: +20%),
@@ -1725,7 +1794,13 @@ void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, i
   }
 #undef DL_WG
 #undef DL_WGN
+#undef DL_WGX
   DL_HIP_CHECK(hipGetLastError());
+}
+
+void set_reduce_atomic_conv(int on) {
+  const int v = on ? 1 : 0;
+  DL_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_red_atomic), &v, sizeof(int)));
 }
 
 void slab_reduce(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream) {

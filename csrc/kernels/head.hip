@@ -14,6 +14,7 @@
 #include "dl_common.h"
 #include "dl_ops.h"
 #include "head_wgrad_dev.h"
+#include "bn_fin_dev.h"
 
 namespace dl {
 
@@ -28,6 +29,7 @@ struct HeadPool {
   const float* coef;
   bf16_t* h_out;
   int yH, yW, yC;
+  BnFin fin;  // fin.sums != nullptr: derive the coefficients from the accumulated statistics (mode 1)
 };
 
 template <int NC, bool POOL = false>
@@ -60,12 +62,20 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
       const uint4 v[4] = {*reinterpret_cast<const uint4*>(base), *reinterpret_cast<const uint4*>(base + hp.yC),
                           *reinterpret_cast<const uint4*>(base + (int64_t)hp.yW * hp.yC),
                           *reinterpret_cast<const uint4*>(base + (int64_t)hp.yW * hp.yC + hp.yC)};
-      const float4 sc0 = *reinterpret_cast<const float4*>(hp.coef + 2 * hp.yC + c0);
-      const float4 sc1 = *reinterpret_cast<const float4*>(hp.coef + 2 * hp.yC + c0 + 4);
-      const float4 sh0 = *reinterpret_cast<const float4*>(hp.coef + 3 * hp.yC + c0);
-      const float4 sh1 = *reinterpret_cast<const float4*>(hp.coef + 3 * hp.yC + c0 + 4);
-      const float sc[8] = {sc0.x, sc0.y, sc0.z, sc0.w, sc1.x, sc1.y, sc1.z, sc1.w};
-      const float sh[8] = {sh0.x, sh0.y, sh0.z, sh0.w, sh1.x, sh1.y, sh1.z, sh1.w};
+      float sc[8], sh[8];
+      if (hp.fin.sums != nullptr) {
+        bn_fin_publish(hp.fin, hp.yC);
+        bn_fin_coef8(hp.fin, hp.yC, c0, sc, sh);
+      } else {
+        const float4 sc0 = *reinterpret_cast<const float4*>(hp.coef + 2 * hp.yC + c0);
+        const float4 sc1 = *reinterpret_cast<const float4*>(hp.coef + 2 * hp.yC + c0 + 4);
+        const float4 sh0 = *reinterpret_cast<const float4*>(hp.coef + 3 * hp.yC + c0);
+        const float4 sh1 = *reinterpret_cast<const float4*>(hp.coef + 3 * hp.yC + c0 + 4);
+        sc[0] = sc0.x; sc[1] = sc0.y; sc[2] = sc0.z; sc[3] = sc0.w; sc[4] = sc1.x; sc[5] = sc1.y; sc[6] = sc1.z;
+        sc[7] = sc1.w;
+        sh[0] = sh0.x; sh[1] = sh0.y; sh[2] = sh0.z; sh[3] = sh0.w; sh[4] = sh1.x; sh[5] = sh1.y; sh[6] = sh1.z;
+        sh[7] = sh1.w;
+      }
       float mx[8];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -197,14 +207,19 @@ void head_fwd_bwd(uintptr_t h, uintptr_t w, uintptr_t bias, uintptr_t labels, in
   DL_HIP_CHECK(hipGetLastError());
 }
 
+// fin_sums != 0 (mode 1): the last block's BN coefficients are derived from
+// the accumulated statistics (block 0 also publishes coef + running stats)
 void head_fwd_bwd_pool(uintptr_t y, uintptr_t coef, int yH, int yW, int yC, uintptr_t h_out, uintptr_t w,
                        uintptr_t bias, uintptr_t labels, int B, int NC, uintptr_t logits_out, uintptr_t dlogits,
-                       uintptr_t loss_b, uintptr_t dh, uintptr_t stream) {
+                       uintptr_t loss_b, uintptr_t dh, uintptr_t fin_sums, int64_t fin_m, uintptr_t gamma,
+                       uintptr_t beta, uintptr_t conv_bias, uintptr_t rmean, uintptr_t rvar, float eps, float momentum,
+                       uintptr_t stream) {
   if (NC != 10) throw std::runtime_error("head_fwd_bwd_pool: built for 10 classes");
   const int F = (yH / 2) * (yW / 2) * yC;
   if (F != 2048 || yC % 8 != 0 || yH % 2 != 0 || yW % 2 != 0)
     throw std::runtime_error("head_fwd_bwd_pool: needs a 2048-feature pooled map, C % 8 == 0");
-  const HeadPool hp{(const bf16_t*)y, (const float*)coef, (bf16_t*)h_out, yH, yW, yC};
+  const HeadPool hp{(const bf16_t*)y, (const float*)coef, (bf16_t*)h_out, yH, yW, yC,
+                    make_bn_fin(fin_sums, fin_m, gamma, beta, conv_bias, rmean, rvar, eps, momentum, coef)};
   head_fwd_bwd_kernel<10, true><<<B, 256, 0, as_stream(stream)>>>(
       nullptr, (const float*)w, (const float*)bias, (const int64_t*)labels, F, B, (float*)logits_out,
       (float*)dlogits, (float*)loss_b, (bf16_t*)dh, hp);

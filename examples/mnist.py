@@ -39,9 +39,12 @@ def build(opt, algo):
     batcher = ds.sampledBatcher("permutation", opt.batchSize, dtype=dt, seed=opt.seed + opt.nodeIndex)
     torch.manual_seed(0)
     model = (MnistMLP(seed=0) if opt.model == "mlp" else MnistConvNet(seed=0)).to(dev)
+    # --cuda: the convnet's whole step is one hand-written kernel (models/mnist_hip.py)
+    backend = opt.backend if (dev.type == "cuda" and opt.model == "convnet") else "torch"
     trainer = DataParallelTrainer(model, tree, lr=opt.learningRate, algo=algo, tau=getattr(opt, "tau", 10),
-                                  alpha=getattr(opt, "alpha", 0.2), backend="torch", compute_dtype=dt,
-                                  graph=bool(opt.graph) and dev.type == "cuda" and algo == "sgd")
+                                  alpha=getattr(opt, "alpha", 0.2), backend=backend, compute_dtype=dt,
+                                  graph=bool(opt.graph) and dev.type == "cuda" and algo == "sgd",
+                                  max_batch=opt.batchSize)
     return tree, dev, batcher, model, trainer
 
 
@@ -87,6 +90,8 @@ def parser(desc, lr=0.01, batch=1):
     ap.add_argument("--data", default=None, help="directory with the MNIST idx files (optional)")
     ap.add_argument("--trainSize", type=int, default=60000)
     ap.add_argument("--graph", type=int, default=1)
+    ap.add_argument("--backend", default="hip", choices=["hip", "torch"],
+                    help="--cuda convnet: fused HIP step kernel (hip) or PyTorch ops (torch)")
     add_checkpoint_flags(ap)
     return ap
 

@@ -88,7 +88,7 @@ def main():
         if a.wsplits > 0:
             wsp = a.wsplits
         jobs.append((f"wgrad{li+1}", 2 * M * cout * K, lambda wtile=wtile, wsp=wsp: C.conv_wgrad(
-            dy.data_ptr(), x.data_ptr(), slab.data_ptr(), B, H, H, cin, cout, 5, wsp, K, wtile, cur()),
+            dy.data_ptr(), x.data_ptr(), slab.data_ptr(), B, H, H, cin, cout, 5, wsp, K, wtile, 0, cur()),
             f"tile{wtile} split{wsp}"))
         occ_stream = torch.cuda.Stream()
         for name, flops, fn, desc in jobs:

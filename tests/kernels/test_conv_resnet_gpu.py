@@ -1,0 +1,136 @@
+"""ResNet-50 convolutions on the shadow weights (ops/conv.py) against fp32
+PyTorch references of the same ops: the stride-1 1x1 convolutions on the
+hand-written MFMA kernels (forward, dgrad, fp32 wgrad written into the flat
+gradient, with and without split-K atomics), the MIOpen path for the rest,
+and a whole ResNet-50 step with the convolutions bound to the flat buffers
+against the unbound model."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from torch_distlearn_amd import _native
+
+    _native.native()
+    return torch.device("cuda", 0)
+
+
+# (N, Cin, H, Cout): ResNet-50 bottleneck 1x1 shapes at small batch + M tails
+SHAPES = [(4, 64, 56, 64), (4, 64, 56, 256), (4, 256, 56, 64), (2, 512, 28, 128), (2, 1024, 14, 256),
+          (2, 2048, 7, 512), (3, 512, 7, 2048), (1, 128, 9, 512)]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv1x1_matches_fp32(dev, shape):
+    from torch_distlearn_amd.ops.conv import Conv1x1, ShadowBinding, conv1x1_supported
+
+    N, cin, H, cout = shape
+    g = torch.Generator(device=dev).manual_seed(cin * cout + H)
+    cl = torch.channels_last
+    x = torch.randn(N, cin, H, H, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = torch.randn(cout, cin, 1, 1, device=dev, generator=g) * cin ** -0.5
+    w16 = w.to(torch.bfloat16)
+    go = torch.randn(N, cout, H, H, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    assert conv1x1_supported(x, cout)
+    g32 = torch.full((cout, cin), float("nan"), device=dev)
+    g32.zero_()  # the trainer zeroes the flat gradient at step start
+    ready = []
+    bind = ShadowBinding(w16.view(cout, cin), g32, lambda: ready.append(1))
+    xi = x.detach().requires_grad_(True)
+    wp = torch.nn.Parameter(w.clone())
+    y = Conv1x1.apply(xi, wp, bind, None)
+    y.backward(go)
+    xr = x.float().detach().requires_grad_(True)
+    wr = w16.float().detach().requires_grad_(True)
+    yr = F.conv2d(xr, wr)
+    yr.backward(go.float())
+    torch.cuda.synchronize()
+    assert y.is_contiguous(memory_format=cl) and y.dtype == torch.bfloat16
+    assert _rel(y, yr) < 1e-2
+    assert _rel(xi.grad, xr.grad) < 1e-2
+    assert _rel(g32, wr.grad.view(cout, cin)) < 1e-3
+    assert wp.grad is None and ready == [1]
+
+
+@pytest.mark.parametrize("N,cin,H,cout", [(4, 256, 28, 128), (2, 64, 56, 256), (3, 512, 7, 2048)])
+def test_conv1x1_bn_stats_epilogue(dev, N, cin, H, cout):
+    """The forward epilogue's per-channel sum / sum of squares (deterministic
+    partial rows + bn_rows_reduce: the input of the following BatchNorm)
+    equal those of the stored bf16 output."""
+    from torch_distlearn_amd import _native
+    from torch_distlearn_amd.ops.conv import Conv1x1, ShadowBinding
+
+    C = _native.native()
+    C.set_reduce_atomic(0)
+    x = torch.randn(N, cin, H, H, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w16 = (torch.randn(cout, cin, device=dev) * 0.05).to(torch.bfloat16)
+    stats = torch.zeros(2 * cout, device=dev)
+    bind = ShadowBinding(w16, torch.zeros(cout, cin, device=dev), lambda: None)
+    with torch.no_grad():
+        y = Conv1x1.apply(x, torch.nn.Parameter(w16.float().view(cout, cin, 1, 1)), bind, stats)
+    torch.cuda.synchronize()
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, cout)
+    torch.testing.assert_close(stats[:cout], yf.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(stats[cout:], (yf * yf).sum(0), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("k,stride,cin,cout,hw", [(3, 1, 64, 64, 28), (3, 2, 128, 128, 28), (1, 2, 256, 512, 28),
+                                                  (7, 2, 3, 64, 64)])
+def test_shadow_conv_matches_fp32(dev, k, stride, cin, cout, hw):
+    from torch_distlearn_amd.ops.conv import ShadowBinding, ShadowConv
+
+    g = torch.Generator(device=dev).manual_seed(k * 100 + cin)
+    cl = torch.channels_last
+    x = torch.randn(2, cin, hw, hw, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    w16 = (torch.randn(cout, cin, k, k, device=dev, generator=g) * (cin * k * k) ** -0.5).to(torch.bfloat16)
+    g32 = torch.zeros(cout, cin, k, k, device=dev)
+    bind = ShadowBinding(w16.view(-1), g32.view(-1), lambda: None)
+    xi = x.detach().requires_grad_(True)
+    y = ShadowConv.apply(xi, torch.nn.Parameter(w16.float()), bind, stride, k // 2)
+    go = torch.randn_like(y)
+    y.backward(go)
+    xr, wr = x.float().detach().requires_grad_(True), w16.float().detach().requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, stride, k // 2)
+    yr.backward(go.float())
+    torch.cuda.synchronize()
+    assert _rel(y, yr) < 1e-2 and _rel(xi.grad, xr.grad) < 2e-2 and _rel(g32, wr.grad) < 2e-2
+
+
+def test_resnet50_bound_convs_match_unbound(dev, monkeypatch):
+    """One ResNet-50 training step (64x64 inputs, batch 8) with every
+    convolution bound to the flat buffers (HIP 1x1 GEMMs + shadow MIOpen)
+    against the same step with plain F.conv2d on cast weights: loss and the
+    updated parameters agree to bf16 accuracy."""
+    from torch_distlearn_amd import Tree
+    from torch_distlearn_amd.engine import DataParallelTrainer
+    from torch_distlearn_amd.models import ResNet50, resnet
+
+    tree = Tree(1, 1, host="127.0.0.1", port=29573, device=dev)
+    x = torch.randn(8, 64, 64, 3, device=dev).to(torch.bfloat16)
+    y = torch.randint(0, 100, (8,), device=dev)
+    out = {}
+    for bound in (True, False):
+        model = ResNet50(num_classes=100, seed=0).to(dev)
+        if not bound:
+            model.attach_flat = None  # the trainer then leaves the convolutions unbound
+        tr = DataParallelTrainer(model, tree, lr=0.05, backend="torch", compute_dtype=torch.bfloat16, max_batch=8)
+        assert any(getattr(m, "bind", None) is not None for m in model.modules()) == bound
+        tr.synchronize_parameters()
+        before = tr.flat.data.clone()
+        loss = float(tr.step(x, y))
+        torch.cuda.synchronize()
+        out[bound] = (loss, tr.flat.data - before)
+    (lb, db), (lu, du) = out[True], out[False]
+    assert abs(lb - lu) < 2e-2 * max(1.0, abs(lu))
+    cos = float(F.cosine_similarity(db, du, dim=0))
+    assert cos > 0.98, cos

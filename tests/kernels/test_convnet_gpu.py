@@ -14,7 +14,16 @@ def C():
         pytest.skip("no GPU")
     from torch_distlearn_amd import _native
 
-    return _native.native()
+    C = _native.native()
+    C.set_reduce_atomic(0)  # these tests check the deterministic partial-row mode; mode 1 below
+    return C
+
+
+@pytest.fixture()
+def atomic_mode(C):
+    C.set_reduce_atomic(1)
+    yield C
+    C.set_reduce_atomic(0)
 
 
 def _s():
@@ -115,7 +124,7 @@ def test_conv_dgrad_wgrad(C, shape):
             continue
         for splits in (1, 3):
             slabs = torch.full((splits, cout, K), float("nan"), device=dev)
-            C.conv_wgrad(dyp.data_ptr(), xp.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, splits, K, tile,
+            C.conv_wgrad(dyp.data_ptr(), xp.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, splits, K, tile, 0,
                          _s())
             dw = torch.empty(cout, 5, 5, cin, device=dev)
             C.slab_reduce(slabs.data_ptr(), dw.data_ptr(), splits, cout, 25, cin, cin, _s())
@@ -130,7 +139,7 @@ def test_conv_dgrad_wgrad(C, shape):
             C.set_conv_wgrad_pf(pf)
             try:
                 slabs = torch.full((2, cout, K), float("nan"), device=dev)
-                C.conv_wgrad(dyp.data_ptr(), xp.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, 2, K, tile,
+                C.conv_wgrad(dyp.data_ptr(), xp.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, 2, K, tile, 0,
                              _s())
             finally:
                 C.set_conv_stages(3, 0)
@@ -153,7 +162,7 @@ def test_prep_step(C):
     wts = [torch.empty(w.shape[3], 5, 5, w.shape[0], dtype=torch.bfloat16, device=dev) for w in ws]
     C.prep_step(x3.data_ptr(), x8.data_ptr(), B * 1024, 3, 8, 32, 32, 2, w1.data_ptr(), w1p.data_ptr(), 64, 25, 3, 8,
                 [w.data_ptr() for w in ws], [t.data_ptr() for t in wts], [w.shape[0] for w in ws],
-                [w.shape[3] for w in ws], _s())
+                [w.shape[3] for w in ws], [], [], _s())
     torch.cuda.synchronize()
     inner = x8[:, 2:34, 2:34]
     assert torch.equal(inner[..., :3], x3) and not inner[..., 3:].any()
@@ -179,7 +188,7 @@ def test_padded_input_layer(C):
     dy = torch.randn(B, H, H, 64, device=dev).to(torch.bfloat16)
     slabs = torch.zeros(4, 64, 200, device=dev)
     dyp, x8p = _pad(dy), _pad(x8)
-    C.conv_wgrad(dyp.data_ptr(), x8p.data_ptr(), slabs.data_ptr(), B, H, H, 8, 64, 5, 4, 200, 1, _s())
+    C.conv_wgrad(dyp.data_ptr(), x8p.data_ptr(), slabs.data_ptr(), B, H, H, 8, 64, 5, 4, 200, 1, 0, _s())
     dw = torch.empty(64, 5, 5, 3, device=dev)
     C.slab_reduce(slabs.data_ptr(), dw.data_ptr(), 4, 64, 25, 8, 3, _s())
     xr = x3.float().permute(0, 3, 1, 2)
@@ -297,7 +306,7 @@ def test_head_with_fused_pool(C):
         if fused:
             C.head_fwd_bwd_pool(y.data_ptr(), coef.data_ptr(), H, H, Cc, h.data_ptr(), w.data_ptr(), b.data_ptr(),
                                 lab.data_ptr(), B, NC, logp.data_ptr(), dlog.data_ptr(), lb.data_ptr(),
-                                dh.data_ptr(), _s())
+                                dh.data_ptr(), 0, 0, 0, 0, 0, 0, 0, 0.0, 0.0, _s())
         else:
             C.bn_relu_pool_fwd(y.data_ptr(), coef.data_ptr(), h.data_ptr(), B, H, H, Cc, 0, _s())
             C.head_fwd_bwd(h.data_ptr(), w.data_ptr(), b.data_ptr(), lab.data_ptr(), Fd, B, NC, logp.data_ptr(),
@@ -343,10 +352,14 @@ def test_bwd_reduce_head_fused(C):
     assert int(res[1][5][0]) == 1 and float(res[1][4]) == 1.0
 
 
-def test_executor_matches_torch_model(C):
+@pytest.mark.parametrize("atomic", ["1", "0"])
+def test_executor_matches_torch_model(C, atomic, monkeypatch):
     """Whole-model check: HIP executor loss + every gradient vs an fp32 PyTorch
     reference of the same parameters; the error must be within 2x of what
-    PyTorch's own bf16 path shows against the same fp32 reference."""
+    PyTorch's own bf16 path shows against the same fp32 reference.  Both
+    reduction modes (1 = atomic accumulation, no finalize / slab-reduce
+    launches; 0 = deterministic partial rows)."""
+    monkeypatch.setenv("DISTLEARN_REDUCE_ATOMIC", atomic)
     from torch_distlearn_amd import FlatParams
     from torch_distlearn_amd.models import CifarConvNet
     from torch_distlearn_amd.models.cifar_hip import CifarHIPExecutor
@@ -384,3 +397,170 @@ def test_executor_matches_torch_model(C):
     lp_ref = ref(x, compute_dtype=torch.float32)
     lp = ex.predict(x)
     assert _rel(lp, lp_ref) < 2e-2
+
+
+
+# ---------------------------------------------------------------------------
+# reduction mode 1 (atomic per-channel totals, finalize fused into consumers)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("shape", [(8, 32, 8, 64, 2, 1), (8, 16, 64, 128, 0, 1), (32, 4, 256, 512, 0, 4),
+                                   (8, 8, 128, 256, 2, 1)])
+def test_conv_fwd_stats_atomic(C, atomic_mode, shape):
+    """conv_fwd statistics in mode 1 = the column sums of mode 0's partial rows."""
+    B, H, cin, cout, tile, splits = shape
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(cin + cout)
+    x = _pad(torch.randn(B, H, H, cin, device=dev, generator=g).to(torch.bfloat16))
+    w = (torch.randn(cout, 5, 5, cin, device=dev, generator=g) * 0.05).to(torch.bfloat16)
+    slab = torch.empty(max(splits, 1) * B * H * H * cout, device=dev)
+    res = []
+    for mode in (0, 1):
+        C.set_reduce_atomic(mode)
+        y = torch.empty(B, H, H, cout, dtype=torch.bfloat16, device=dev)
+        stats = torch.zeros(512, 2, cout, device=dev)
+        T = C.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), stats.data_ptr(), slab.data_ptr(), B, H, H, cin,
+                       cout, 5, tile, splits, _s())
+        torch.cuda.synchronize()
+        res.append((y.clone(), stats[:T].sum(0) if mode == 0 else stats[0].clone()))
+    assert torch.equal(res[0][0], res[1][0])
+    torch.testing.assert_close(res[1][1], res[0][1], rtol=1e-5, atol=1e-2)
+
+
+@pytest.mark.parametrize("shape", [(8, 32, 64), (8, 16, 128), (16, 4, 512), (3, 8, 32)])
+def test_bn_relu_pool_fused_finalize(C, atomic_mode, shape):
+    """bn_relu_pool_fwd_fin (coefficients from the totals) == bn_finalize +
+    bn_relu_pool_fwd, bitwise (same arithmetic); the backward reduce in mode 1
+    accumulates [dgamma; dbeta] and bn_relu_pool_bwd_apply_sums matches
+    bn_bwd_finalize + bn_relu_pool_bwd_apply."""
+    B, H, Cc = shape
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(B * H + Cc)
+    y = (torch.randn(B, H, H, Cc, device=dev, generator=g) * 2 + 0.5).to(torch.bfloat16)
+    gamma = torch.rand(Cc, device=dev, generator=g) + 0.5
+    beta = torch.randn(Cc, device=dev, generator=g) * 0.1
+    bias = torch.randn(Cc, device=dev, generator=g) * 0.1
+    M = B * H * H
+    yf = y.float().reshape(-1, Cc)
+    sums = torch.stack([yf.sum(0), (yf * yf).sum(0)]).contiguous()
+    outs = []
+    for fused in (False, True):
+        rm, rv = torch.zeros(Cc, device=dev), torch.ones(Cc, device=dev)
+        coef = torch.full((4, Cc), float("nan"), device=dev)
+        out = torch.empty(B, H // 2 + 4, H // 2 + 4, Cc, dtype=torch.bfloat16, device=dev)
+        if fused:
+            C.bn_relu_pool_fwd_fin(y.data_ptr(), sums.data_ptr(), M, gamma.data_ptr(), beta.data_ptr(),
+                                   bias.data_ptr(), rm.data_ptr(), rv.data_ptr(), 1e-3, 0.1, coef.data_ptr(),
+                                   out.data_ptr(), B, H, H, Cc, 2, _s())
+        else:
+            C.bn_finalize(sums.data_ptr(), 1, Cc, M, gamma.data_ptr(), beta.data_ptr(), bias.data_ptr(),
+                          rm.data_ptr(), rv.data_ptr(), 1e-3, 0.1, 0, coef.data_ptr(), _s())
+            C.bn_relu_pool_fwd(y.data_ptr(), coef.data_ptr(), out.data_ptr(), B, H, H, Cc, 2, _s())
+        torch.cuda.synchronize()
+        outs.append((out[:, 2:-2, 2:-2].clone(), coef, rm, rv))
+    for a, b_ in zip(*outs):
+        assert torch.equal(a, b_)
+    coef = outs[0][1]
+    dP = torch.randn(B, H // 2, H // 2, Cc, device=dev, generator=g).to(torch.bfloat16)
+    G = C.bn_bwd_blocks(B, H, H, Cc)
+    # mode 0
+    C.set_reduce_atomic(0)
+    part = torch.empty(G, 2, Cc, device=dev)
+    C.bn_relu_pool_bwd_reduce(y.data_ptr(), dP.data_ptr(), coef.data_ptr(), part.data_ptr(), B, H, H, Cc, G, _s())
+    dg, db, acoef = torch.empty(Cc, device=dev), torch.empty(Cc, device=dev), torch.empty(3, Cc, device=dev)
+    C.bn_bwd_finalize(part.data_ptr(), G, Cc, M, gamma.data_ptr(), coef.data_ptr(), dg.data_ptr(), db.data_ptr(),
+                      acoef.data_ptr(), _s())
+    dy0 = torch.zeros(B, H + 4, H + 4, Cc, dtype=torch.bfloat16, device=dev)
+    C.bn_relu_pool_bwd_apply(y.data_ptr(), dP.data_ptr(), coef.data_ptr(), acoef.data_ptr(), dy0.data_ptr(), B, H, H,
+                             Cc, 2, _s())
+    # mode 1
+    C.set_reduce_atomic(1)
+    dgb = torch.zeros(2, Cc, device=dev)
+    C.bn_relu_pool_bwd_reduce(y.data_ptr(), dP.data_ptr(), coef.data_ptr(), dgb.data_ptr(), B, H, H, Cc, G, _s())
+    dy1 = torch.zeros(B, H + 4, H + 4, Cc, dtype=torch.bfloat16, device=dev)
+    C.bn_relu_pool_bwd_apply_sums(y.data_ptr(), dP.data_ptr(), coef.data_ptr(), dgb.data_ptr(), gamma.data_ptr(), M,
+                                  dy1.data_ptr(), B, H, H, Cc, 2, _s())
+    torch.cuda.synchronize()
+    torch.testing.assert_close(dgb[0], dg, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dgb[1], db, rtol=1e-4, atol=1e-4)
+    assert _rel(dy1, dy0) < 2e-3
+
+
+def test_head_pool_fused_finalize(C, atomic_mode):
+    """head_fwd_bwd_pool deriving the BN coefficients from the totals == the
+    same kernel fed bn_finalize's coefficients (bitwise); block 0 publishes
+    coef and the running statistics."""
+    dev = torch.device("cuda")
+    B, H, Cc, NC = 29, 4, 512, 10
+    Fd = (H // 2) ** 2 * Cc
+    g = torch.Generator(device=dev).manual_seed(15)
+    y = torch.randn(B, H, H, Cc, device=dev, generator=g).to(torch.bfloat16)
+    yf = y.float().reshape(-1, Cc)
+    sums = torch.stack([yf.sum(0), (yf * yf).sum(0)]).contiguous()
+    gamma = torch.rand(Cc, device=dev, generator=g) + 0.5
+    beta = torch.randn(Cc, device=dev, generator=g) * 0.1
+    cb = torch.randn(Cc, device=dev, generator=g) * 0.1
+    w = torch.randn(NC, Fd, device=dev, generator=g) * 0.02
+    b = torch.randn(NC, device=dev, generator=g) * 0.1
+    lab = torch.randint(0, NC, (B,), device=dev, generator=g)
+    M = B * H * H
+    outs = []
+    for fused in (False, True):
+        rm, rv = torch.zeros(Cc, device=dev), torch.ones(Cc, device=dev)
+        coef = torch.full((4, Cc), float("nan"), device=dev)
+        h = torch.empty(B, Fd, dtype=torch.bfloat16, device=dev)
+        logp, dlog = torch.empty(B, NC, device=dev), torch.empty(B, NC, device=dev)
+        lb, dh = torch.empty(B, device=dev), torch.empty(B, Fd, dtype=torch.bfloat16, device=dev)
+        if fused:
+            fin = (sums.data_ptr(), M, gamma.data_ptr(), beta.data_ptr(), cb.data_ptr(), rm.data_ptr(), rv.data_ptr(),
+                   1e-3, 0.1)
+        else:
+            C.bn_finalize(sums.data_ptr(), 1, Cc, M, gamma.data_ptr(), beta.data_ptr(), cb.data_ptr(), rm.data_ptr(),
+                          rv.data_ptr(), 1e-3, 0.1, 0, coef.data_ptr(), _s())
+            fin = (0, 0, 0, 0, 0, 0, 0, 0.0, 0.0)
+        C.head_fwd_bwd_pool(y.data_ptr(), coef.data_ptr(), H, H, Cc, h.data_ptr(), w.data_ptr(), b.data_ptr(),
+                            lab.data_ptr(), B, NC, logp.data_ptr(), dlog.data_ptr(), lb.data_ptr(), dh.data_ptr(),
+                            *fin, _s())
+        torch.cuda.synchronize()
+        outs.append((h, logp, dlog, lb, dh, coef, rm, rv))
+    for a, b_ in zip(*outs):
+        assert torch.equal(a, b_)
+
+
+@pytest.mark.parametrize("shape", [(8, 32, 8, 64, 3, 1, 128), (8, 16, 64, 128, 64, 2, 8), (8, 8, 128, 256, 128, 2, 5),
+                                   (4, 16, 32, 64, 32, 1, 3)])
+def test_wgrad_atomic_split_k(C, shape):
+    """conv_wgrad with atomic split-K straight into the zeroed gradient
+    (dropping zero-padded input channels) == slabs + slab_reduce."""
+    B, H, cin, cout, creal, tile, splits = shape
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(cin * cout + splits)
+    x = torch.randn(B, H, H, cin, device=dev, generator=g)
+    x[..., creal:] = 0
+    xp = _pad(x.to(torch.bfloat16))
+    dyp = _pad(torch.randn(B, H, H, cout, device=dev, generator=g).to(torch.bfloat16))
+    K = 25 * cin
+    slabs = torch.full((splits, cout, K), float("nan"), device=dev)
+    C.conv_wgrad(dyp.data_ptr(), xp.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, splits, K, tile, 0, _s())
+    ref = torch.empty(cout, 5, 5, creal, device=dev)
+    C.slab_reduce(slabs.data_ptr(), ref.data_ptr(), splits, cout, 25, cin, creal, _s())
+    dw = torch.zeros(cout, 5, 5, creal, device=dev)
+    C.conv_wgrad(dyp.data_ptr(), xp.data_ptr(), dw.data_ptr(), B, H, H, cin, cout, 5, splits, K, tile, creal, _s())
+    torch.cuda.synchronize()
+    assert _rel(dw, ref) < 1e-5
+
+
+def test_prep_zero_ranges(C):
+    """The step's prep kernel zeroes the listed accumulator ranges (mode 1)."""
+    dev = torch.device("cuda")
+    B = 4
+    x3 = torch.randn(B, 32, 32, 3, device=dev).to(torch.bfloat16)
+    x8 = torch.zeros(B, 36, 36, 8, dtype=torch.bfloat16, device=dev)
+    w1 = torch.randn(64, 5, 5, 3, device=dev)
+    w1p = torch.empty(64, 5, 5, 8, dtype=torch.bfloat16, device=dev)
+    bufs = [torch.randn(n, device=dev) for n in (1920, 256, 819200, 4800)]
+    keep = torch.randn(64, device=dev)
+    ref = keep.clone()
+    C.prep_step(x3.data_ptr(), x8.data_ptr(), B * 1024, 3, 8, 32, 32, 2, w1.data_ptr(), w1p.data_ptr(), 64, 25, 3, 8,
+                [], [], [], [], [b.data_ptr() for b in bufs], [b.numel() for b in bufs], _s())
+    torch.cuda.synchronize()
+    assert all(not b.any() for b in bufs) and torch.equal(keep, ref)

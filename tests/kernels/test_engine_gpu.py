@@ -13,6 +13,15 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+@pytest.fixture(autouse=True)
+def deterministic(monkeypatch):
+    """Graph-vs-eager and side-effect checks compare runs bitwise / to 1e-3:
+    they use the deterministic reduction mode (partial rows + finalize
+    kernels).  Mode 1 (atomic accumulation, the bench default) is covered by
+    test_mode1_trains_and_graph_tracks_eager and tests/kernels/test_convnet_gpu.py."""
+    monkeypatch.setenv("DISTLEARN_REDUCE_ATOMIC", "0")
+
+
 @pytest.fixture(scope="module")
 def dev():
     if not torch.cuda.is_available():
@@ -232,3 +241,21 @@ def test_comm_profile_is_side_effect_free(dev, monkeypatch):
         outs.append((tr.flat.data.clone(), int(ld.ctr[0]), int(tr.sgd.stepsPerNode.sum())))
     assert outs[0][1:] == outs[1][1:]
     assert torch.equal(outs[0][0], outs[1][0])
+
+
+def test_mode1_trains_and_graph_tracks_eager(dev, monkeypatch):
+    """Reduction mode 1 (fp32 atomics: not bitwise reproducible run to run):
+    the model fits a repeated batch, and graph replay tracks eager within the
+    run-to-run noise of the atomics (measured: scripts/diag_mode1.py)."""
+    monkeypatch.setenv("DISTLEARN_REDUCE_ATOMIC", "1")
+    g = torch.Generator(device=dev).manual_seed(1)
+    x = torch.randn(32, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)
+    y = torch.randint(0, 10, (32,), device=dev, generator=g)
+    res = []
+    for graph in (False, True):
+        tr = _trainer(dev, "hip", graph, 29706)
+        assert tr.executor.atomic
+        res.append([float(tr.step(x, y)) for _ in range(8)])
+    for losses in res:
+        assert losses[-1] < 0.5 * losses[0]
+    assert max(abs(a - b) for a, b in zip(*res)) < 0.05 * res[0][0]

@@ -80,6 +80,9 @@ class DataParallelTrainer:
             self.aea._one_time_init(self.flat)
         else:
             raise ValueError(f"unknown algo {algo!r}")
+        if backend == "torch" and bf16_shadow and callable(getattr(model, "attach_flat", None)):
+            # convolutions read the bf16 shadow and write fp32 grads into the flat buffer
+            model.attach_flat(self.flat, self.bucketer.mark_leaf_ready if self.bucketer is not None else None)
         self.executor = None
         if backend == "hip":
             from .models import make_executor
@@ -136,7 +139,7 @@ class DataParallelTrainer:
         step, so a captured graph needs no per-step host work)."""
         self.steps += 1
         loader = x if hasattr(x, "gather_args") else None
-        if loader is not None and self.executor is None:
+        if loader is not None and not getattr(self.executor, "takes_loader", False):
             x, y = loader.getBatch()
             x = x.to(self.compute_dtype)
             dev_loader = None
@@ -182,7 +185,7 @@ class DataParallelTrainer:
         covers the rest.  Every step is still a complete step (the same
         kernels and collectives as :meth:`step`)."""
         loss = None
-        fast = self._unrolled(unroll)
+        fast = self._unrolled(unroll) and getattr(self.executor, "takes_loader", False)
         if fast:
             # every graph this loop can replay is captured (and replayed once,
             # state restored) before the first step runs, whatever nsteps is: a

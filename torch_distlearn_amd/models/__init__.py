@@ -15,6 +15,10 @@ def make_executor(model, flat, bucketer=None, max_batch=None):
         from .cifar_hip import CifarHIPExecutor
 
         return CifarHIPExecutor(model, flat, bucketer=bucketer, max_batch=max_batch)
+    if isinstance(model, MnistConvNet):
+        from .mnist_hip import MnistHIPExecutor
+
+        return MnistHIPExecutor(model, flat, bucketer=bucketer, max_batch=max_batch)
     raise NotImplementedError(f"no native executor for {type(model).__name__}")
 
 

@@ -93,6 +93,8 @@ def _wgrad_plan(cout: int, K: int, M: int, reserve: int = 0):
 
 
 class CifarHIPExecutor:
+    takes_loader = True  # gathers DeviceLoader batches on the device inside the step
+
     def __init__(self, model: CifarConvNet, flat, bucketer=None, max_batch: Optional[int] = None):
         if not isinstance(model, CifarConvNet):
             raise TypeError("CifarHIPExecutor needs a CifarConvNet")
@@ -159,6 +161,17 @@ class CifarHIPExecutor:
         # (the cross-queue edges leave ~150 us of idle gaps per step), so off.
         self.side_reduce = (not self.side_wgrad and self.side is not None
                             and os.environ.get("DISTLEARN_REDUCE_STREAM", "0") == "1")
+        # Reduction mode (csrc/kernels/bn_fin_dev.h).  0 (default) = deterministic
+        # partial rows + finalize kernels (bitwise run-to-run reproducible).  1 =
+        # BN statistics, BN parameter gradients and split-K weight gradients are
+        # accumulated with fp32 atomics into buffers the step's prep kernel zeroes
+        # and the consumers derive the BN coefficients themselves: 11 fewer kernel
+        # boundaries per step, but MEASURED SLOWER on MI355X (0.495 vs 0.358 ms/step
+        # at batch 128): same-address fp32 atomics serialise in the L2 -- the layer-1
+        # forward with 1024 workgroups adding into 128 addresses takes 31 us instead
+        # of 11, the 128-way split-K wgrad 56 us instead of 15 + 5 (slab reduce)
+        # (profiles/r2_mode1_timeline.txt).
+        self.atomic = os.environ.get("DISTLEARN_REDUCE_ATOMIC", "0") == "1"
         self._alloc(self.B)
 
     # ------------------------------------------------------------------ buffers
@@ -182,6 +195,9 @@ class CifarHIPExecutor:
         self.coef = [torch.empty(4, c, device=d) for c in self.couts]
         self.acoef = [torch.empty(3, c, device=d) for c in self.couts]
         self.fwd_plan, self.stats = [], []
+        # mode 1: one zeroed [2][C] (sum, sumsq) row per layer in one arena
+        arena = torch.zeros(sum(2 * c for c in self.couts), device=d) if self.atomic else None
+        arena_off = 0
         self.dgrad_plan = [None] * self.nb
         self.bwd_blocks, self.bwd_part = [], []
         self.wplan, slab_elems, wslab_elems = [], 0, 0
@@ -194,25 +210,43 @@ class CifarHIPExecutor:
             self.fwd_plan.append((tile, splits))
             if splits > 1:
                 slab_elems = max(slab_elems, splits * M * cout)
-            rows = C.conv_fwd_stat_rows(B, h, h, cin, cout, KSIZE, tile, splits)
-            if splits > 1:
-                rows = max(rows, 400)  # the split-K combine launches <= ~384 blocks for any batch
-            self.stats.append(torch.empty(rows, 2, cout, device=d))
+            if self.atomic:
+                self.stats.append(arena[arena_off:arena_off + 2 * cout].view(2, cout))
+                arena_off += 2 * cout
+            else:
+                rows = C.conv_fwd_stat_rows(B, h, h, cin, cout, KSIZE, tile, splits)
+                if splits > 1:
+                    rows = max(rows, 400)  # the split-K combine launches <= ~384 blocks for any batch
+                self.stats.append(torch.empty(rows, 2, cout, device=d))
             g = C.bn_bwd_blocks(B, h, h, cout)
             self.bwd_blocks.append(g)
-            self.bwd_part.append(torch.empty(g, 2, cout, device=d))
+            self.bwd_part.append(None if self.atomic else torch.empty(g, 2, cout, device=d))
             tile_w, splits_w = _wgrad_plan(cout, K, M, self.cu_reserve)
             direct = splits_w == 1 and cin == self.cins_real[i]
             self.wplan.append((tile_w, splits_w, direct))
-            if not direct:
+            if not direct and not self.atomic:
                 wslab_elems = max(wslab_elems, splits_w * cout * K)
-            self.wslab_l.append(None if direct else torch.empty(splits_w * cout * K, device=d))
+            self.wslab_l.append(None if (direct or self.atomic) else torch.empty(splits_w * cout * K, device=d))
             if i > 0:
                 dt, ds = _fwd_plan(M, cin, KSIZE * KSIZE * cout)
                 self.dgrad_plan[i] = (dt, ds)
                 if ds > 1:
                     slab_elems = max(slab_elems, ds * M * cin)
         self.slabs = torch.empty(max(slab_elems, 1), device=d)    # fwd / dgrad split-K (main stream)
+        # what the step's prep kernel zeroes in mode 1: the statistics arena, every
+        # layer's [dgamma; dbeta] and the atomically accumulated weight gradients
+        self.zero_ranges = []
+        if self.atomic:
+            self.zero_ranges.append((arena.data_ptr(), arena.numel()))
+            for i in range(self.nb):
+                gw_, gb_ = self.g32[self._leaf(i, 2)], self.g32[self._leaf(i, 3)]
+                if gb_.data_ptr() != gw_.data_ptr() + 4 * gw_.numel():
+                    raise RuntimeError("BN weight/bias gradients must be adjacent in the flat buffer")
+                self.zero_ranges.append((gw_.data_ptr(), 2 * gw_.numel()))
+                if not self.wplan[i][2]:
+                    gw = self.g32[self._leaf(i, 0)]
+                    self.zero_ranges.append((gw.data_ptr(), gw.numel()))
+            self._arena = arena
         self.logits = torch.empty(B, self.nclass, device=d)
         self.dlogits = torch.empty(B, self.nclass, device=d)
         self.loss_b = torch.empty(B, device=d)
@@ -230,7 +264,12 @@ class CifarHIPExecutor:
         return ([self.p16[self._leaf(i, 0)].data_ptr() for i in idx], [self.wt[i].data_ptr() for i in idx],
                 [self.couts[i] for i in idx], [self.cins[i] for i in idx])
 
-    def _prep(self, x, s: int, with_transposes: bool = False) -> int:
+    def _zero_args(self, train: bool):
+        if not (train and self.atomic):
+            return [], []
+        return [p for p, _ in self.zero_ranges], [n for _, n in self.zero_ranges]
+
+    def _prep(self, x, s: int, with_transposes: bool = False, train: bool = True) -> int:
         """ONE launch: the step's input into the zero-bordered, channel-padded
         layer-1 buffer (from a bf16 NHWC tensor, or gathered + normalised on
         the device from a :class:`~torch_distlearn_amd.data.DeviceLoader`),
@@ -246,7 +285,7 @@ class CifarHIPExecutor:
                 raise ValueError("DeviceLoader images do not match the model input")
             self.C.prep_step_gather(img, order, lab_all, lab_out, ctr, n_order, B, C, mean, std, self.x8.data_ptr(),
                                     CIN_PAD, h, h, SPAD, self.p32[0].data_ptr(), self.w1p.data_ptr(), self.couts[0],
-                                    KSIZE * KSIZE, self.cins_real[0], CIN_PAD, *tw, s)
+                                    KSIZE * KSIZE, self.cins_real[0], CIN_PAD, *tw, *self._zero_args(train), s)
             return B
         B = x.shape[0]
         if B > self.cap:
@@ -255,13 +294,13 @@ class CifarHIPExecutor:
             raise ValueError("CifarHIPExecutor expects contiguous NHWC bf16 input [B, H, W, 3]")
         self.C.prep_step(x.data_ptr(), self.x8.data_ptr(), B * h * h, self.cins_real[0], CIN_PAD, h, h, SPAD,
                          self.p32[0].data_ptr(), self.w1p.data_ptr(), self.couts[0], KSIZE * KSIZE,
-                         self.cins_real[0], CIN_PAD, *tw, s)
+                         self.cins_real[0], CIN_PAD, *tw, *self._zero_args(train), s)
         return B
 
     def _prep_transposes(self, s: int) -> None:
         """Flipped/transposed bf16 weights of blocks 2.. for the dgrad (one launch)."""
         self.C.prep_step(0, 0, 0, self.cins_real[0], CIN_PAD, 0, 0, 0, 0, 0, 0, KSIZE * KSIZE, self.cins_real[0],
-                         CIN_PAD, *self._transpose_args(True), s)
+                         CIN_PAD, *self._transpose_args(True), [], [], s)
 
     def _forward(self, B: int, s: int, train: bool, pool_last: bool = True):
         """Conv -> BN finalize -> BN/ReLU/pool per block.  ``pool_last=False``
@@ -276,14 +315,29 @@ class CifarHIPExecutor:
             ntm = C.conv_fwd(inp.data_ptr(), w.data_ptr(), self.y[i].data_ptr(),
                              self.stats[i].data_ptr() if train else 0, self.slabs.data_ptr(), B, h, h, cin, cout, KSIZE,
                              t, sp, s)
-            C.bn_finalize(self.stats[i].data_ptr(), ntm, cout, M, self.p32[self._leaf(i, 2)].data_ptr(),
-                          self.p32[self._leaf(i, 3)].data_ptr(), self.p32[self._leaf(i, 1)].data_ptr(),
-                          self.rm[i].data_ptr(), self.rv[i].data_ptr(), BN_EPS, BN_MOMENTUM, 0 if train else 1,
-                          self.coef[i].data_ptr(), s)
+            fused = train and self.atomic  # coefficients derived by the consumer kernel
+            if not fused:
+                C.bn_finalize(self.stats[i].data_ptr(), ntm, cout, M, self.p32[self._leaf(i, 2)].data_ptr(),
+                              self.p32[self._leaf(i, 3)].data_ptr(), self.p32[self._leaf(i, 1)].data_ptr(),
+                              self.rm[i].data_ptr(), self.rv[i].data_ptr(), BN_EPS, BN_MOMENTUM, 0 if train else 1,
+                              self.coef[i].data_ptr(), s)
             if pool_last or i + 1 < self.nb:
-                C.bn_relu_pool_fwd(self.y[i].data_ptr(), self.coef[i].data_ptr(), self.p[i].data_ptr(), B, h, h,
-                                   cout, SPAD if i + 1 < self.nb else 0, s)
+                opad = SPAD if i + 1 < self.nb else 0
+                if fused:
+                    C.bn_relu_pool_fwd_fin(self.y[i].data_ptr(), *self._fin_args(i, M), self.p[i].data_ptr(), B, h,
+                                           h, cout, opad, s)
+                else:
+                    C.bn_relu_pool_fwd(self.y[i].data_ptr(), self.coef[i].data_ptr(), self.p[i].data_ptr(), B, h, h,
+                                       cout, opad, s)
             inp = self.p[i]
+
+    def _fin_args(self, i: int, M: int):
+        """(sums, M, gamma, beta, conv bias, running mean, running var, eps,
+        momentum, coef) of block i for the kernels that finalize the BN
+        statistics themselves (mode 1)."""
+        return (self.stats[i].data_ptr(), M, self.p32[self._leaf(i, 2)].data_ptr(),
+                self.p32[self._leaf(i, 3)].data_ptr(), self.p32[self._leaf(i, 1)].data_ptr(), self.rm[i].data_ptr(),
+                self.rv[i].data_ptr(), BN_EPS, BN_MOMENTUM, self.coef[i].data_ptr())
 
     # ------------------------------------------------------------------ API
     def forward_backward(self, x, labels: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -291,6 +345,7 @@ class CifarHIPExecutor:
         int64 ``labels``, or a DeviceLoader); fp32 grads land in the flat
         gradient buffer.  Returns the mean loss (device tensor)."""
         C = self.C
+        self._set_mode()
         main, side = torch.cuda.current_stream(), self.side
         s, ss = main.cuda_stream, side.cuda_stream
         ctr = 0
@@ -310,10 +365,16 @@ class CifarHIPExecutor:
         nfc = 4 * self.nb
         if self.head_pool:  # the last block's BN/ReLU/pool runs inside the head kernel (writes p[-1])
             hl = self.hs[-1]
+            last = self.nb - 1
+            if self.atomic:
+                sums, Ml, gam, bet, cb, rm, rv, eps, mom, _ = self._fin_args(last, B * hl * hl)
+                fin = (sums, Ml, gam, bet, cb, rm, rv, eps, mom)
+            else:
+                fin = (0, 0, 0, 0, 0, 0, 0, 0.0, 0.0)
             C.head_fwd_bwd_pool(self.y[-1].data_ptr(), self.coef[-1].data_ptr(), hl, hl, self.couts[-1],
                                 self.p[-1].data_ptr(), self.p32[nfc].data_ptr(), self.p32[nfc + 1].data_ptr(),
                                 labels.data_ptr(), B, self.nclass, self.logits.data_ptr(), self.dlogits.data_ptr(),
-                                self.loss_b.data_ptr(), self.dP[-1].data_ptr(), s)
+                                self.loss_b.data_ptr(), self.dP[-1].data_ptr(), *fin, s)
         else:
             C.head_fwd_bwd(self.p[-1].data_ptr(), self.p32[nfc].data_ptr(), self.p32[nfc + 1].data_ptr(),
                            labels.data_ptr(), self.feat, B, self.nclass, self.logits.data_ptr(),
@@ -336,20 +397,27 @@ class CifarHIPExecutor:
             M = B * h * h
             G = self.bwd_blocks[i]
             dY = self.dYs[i]
+            # mode 1: the reduce accumulates straight into [dgamma; dbeta] of the flat gradient
+            part = self.g32[self._leaf(i, 2)] if self.atomic else self.bwd_part[i]
             if i == self.nb - 1 and self.head_wgrad_fused:
                 # one launch: this block's BN backward reduce + the classifier weight gradient
                 C.bn_bwd_reduce_head(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
-                                     self.bwd_part[i].data_ptr(), B, h, h, cout, G, *head_args, s)
+                                     part.data_ptr(), B, h, h, cout, G, *head_args, s)
                 self._ready(nfc)
                 self._ready(nfc + 1)
             else:
                 C.bn_relu_pool_bwd_reduce(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
-                                          self.bwd_part[i].data_ptr(), B, h, h, cout, G, s)
-            C.bn_bwd_finalize(self.bwd_part[i].data_ptr(), G, cout, M, self.p32[self._leaf(i, 2)].data_ptr(),
-                              self.coef[i].data_ptr(), self.g32[self._leaf(i, 2)].data_ptr(),
-                              self.g32[self._leaf(i, 3)].data_ptr(), self.acoef[i].data_ptr(), s)
-            C.bn_relu_pool_bwd_apply(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
-                                     self.acoef[i].data_ptr(), dY.data_ptr(), B, h, h, cout, SPAD, s)
+                                          part.data_ptr(), B, h, h, cout, G, s)
+            if self.atomic:
+                C.bn_relu_pool_bwd_apply_sums(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
+                                              part.data_ptr(), self.p32[self._leaf(i, 2)].data_ptr(), M,
+                                              dY.data_ptr(), B, h, h, cout, SPAD, s)
+            else:
+                C.bn_bwd_finalize(self.bwd_part[i].data_ptr(), G, cout, M, self.p32[self._leaf(i, 2)].data_ptr(),
+                                  self.coef[i].data_ptr(), self.g32[self._leaf(i, 2)].data_ptr(),
+                                  self.g32[self._leaf(i, 3)].data_ptr(), self.acoef[i].data_ptr(), s)
+                C.bn_relu_pool_bwd_apply(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
+                                         self.acoef[i].data_ptr(), dY.data_ptr(), B, h, h, cout, SPAD, s)
             # (optional fork) weight gradient of block i on the side stream
             if self.side_wgrad:
                 side.wait_stream(main)
@@ -358,12 +426,16 @@ class CifarHIPExecutor:
             tile, splits, direct = self.wplan[i]
             gw = self.g32[self._leaf(i, 0)]
             if direct:
-                C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), gw.data_ptr(), B, h, h, cin, cout, KSIZE, 1, K, tile, wss)
+                C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), gw.data_ptr(), B, h, h, cin, cout, KSIZE, 1, K, tile, 0,
+                             wss)
+            elif self.atomic:  # split-K partials atomically added into the zeroed gradient
+                C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), gw.data_ptr(), B, h, h, cin, cout, KSIZE, splits, K, tile,
+                             self.cins_real[i], wss)
             rs = ws  # the stream that writes this block's weight gradient last
-            if not direct:
+            if not direct and not self.atomic:
                 slab = self.wslab_l[i]
                 C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), slab.data_ptr(), B, h, h, cin, cout, KSIZE,
-                             splits, K, tile, wss)
+                             splits, K, tile, 0, wss)
                 if self.side_reduce and i > 0:  # overlaps this block's dgrad (block 1 has none)
                     side.wait_stream(main)
                     rs = side
@@ -392,6 +464,14 @@ class CifarHIPExecutor:
             main.wait_stream(side)  # join
         return self.loss[0]
 
+    def _set_mode(self) -> None:
+        """The reduction mode lives in device globals shared by every executor
+        of the process: (re)select this executor's (a blocking symbol copy --
+        never issued while a hipGraph is being captured; a captured step
+        replays with the mode that was active at capture)."""
+        if self.C.reduce_atomic() != int(self.atomic) and not torch.cuda.is_current_stream_capturing():
+            self.C.set_reduce_atomic(int(self.atomic))
+
     def last_logits(self) -> torch.Tensor:
         return self.logits[:self._last_b]
 
@@ -404,7 +484,7 @@ class CifarHIPExecutor:
         """Eval-mode forward (running BN statistics); returns log-probabilities
         [B, classes] (fp32)."""
         s = stream_handle()
-        B = self._prep(x, s)
+        B = self._prep(x, s, train=False)
         self._forward(B, s, train=False)
         nfc = 4 * self.nb
         self.C.head_fwd_bwd(self.p[-1].data_ptr(), self.p32[nfc].data_ptr(), self.p32[nfc + 1].data_ptr(), 0,

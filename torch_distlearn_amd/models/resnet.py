@@ -35,6 +35,7 @@ class _BN(nn.Module):
         self.bias = nn.Parameter(torch.zeros(c))
         self.register_buffer("running_mean", torch.zeros(c))
         self.register_buffer("running_var", torch.ones(c))
+        self.bind = None  # (weight grad view, bias grad view, ready) -- ResNet50.attach_flat
 
     def forward(self, x):
         if _BN_MODE == "mixed" and x.is_cuda:
@@ -44,18 +45,35 @@ class _BN(nn.Module):
                          1e-5)
         return y.to(x.dtype)
 
-    def act(self, x, relu: bool = True, residual=None):
-        """act(BN(x) [+ residual]); one fused HIP kernel pair in "hip" mode."""
-        if _BN_MODE == "hip" and self.training and x.is_cuda:
-            from ..ops.bn_nhwc import bn_act, supported
+    def hip_ok(self, x, residual=None) -> bool:
+        if not (_BN_MODE == "hip" and self.training and x.is_cuda):
+            return False
+        from ..ops.bn_nhwc import supported
 
-            if supported(x) and self.weight.dtype == torch.float32 and (
-                    residual is None or (residual.dtype == x.dtype and residual.shape == x.shape)):
-                return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual, relu)
+        return supported(x) and self.weight.dtype == torch.float32 and (
+            residual is None or (residual.dtype == x.dtype and residual.shape == x.shape))
+
+    def act(self, x, relu: bool = True, residual=None, acc=None):
+        """act(BN(x) [+ residual]); one fused HIP kernel pair in "hip" mode
+        (``acc``: statistics already accumulated by the producing conv)."""
+        if self.hip_ok(x, residual):
+            from ..ops.bn_nhwc import bn_act
+
+            return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual, relu, acc=acc,
+                          grads=self.bind)
         y = self(x)
         if residual is not None:
             y = y + residual
         return F.relu(y) if relu else y
+
+
+# Convolution path once the trainer has bound the flat buffers (attach_flat):
+# "hip" = stride-1 1x1 convolutions on the hand-written MFMA GEMM kernels,
+# the rest on MIOpen, all reading the bf16 shadow weights (ops/conv.py);
+# "miopen" = every convolution on MIOpen (shadow weights still used).
+_CONV_MODE = os.environ.get("DISTLEARN_RESNET_CONV", "hip")
+# BatchNorm statistics from the 1x1 GEMM epilogue (skips the BN statistics pass)
+_FUSE_STATS = os.environ.get("DISTLEARN_RESNET_FUSE_STATS", "1") == "1"
 
 
 class _Conv(nn.Module):
@@ -63,10 +81,47 @@ class _Conv(nn.Module):
         super().__init__()
         fan = cin * k * k
         self.weight = nn.Parameter(torch.randn(cout, cin, k, k, generator=g) * (2.0 / fan) ** 0.5)
-        self.stride, self.pad = stride, k // 2
+        self.stride, self.pad, self.k = stride, k // 2, k
+        self.bind = None  # ops.conv.ShadowBinding (set by ResNet50.attach_flat)
 
-    def forward(self, x):
-        return F.conv2d(x, self.weight.to(x.dtype), None, self.stride, self.pad)
+    def hip_gemm(self, x) -> bool:
+        """Stride-1 1x1 convolution on the hand-written MFMA GEMM kernels."""
+        if self.bind is None or not x.is_cuda or x.dtype != torch.bfloat16 or not torch.is_grad_enabled():
+            return False
+        from ..ops.conv import conv1x1_supported
+
+        return _CONV_MODE == "hip" and self.k == 1 and self.stride == 1 and conv1x1_supported(x, self.weight.shape[0])
+
+    def forward(self, x, stats=None):
+        """``stats``: optional zeroed fp32 [2*Cout] that receives the output's
+        per-channel sum / sum of squares (HIP GEMM path only)."""
+        b = self.bind
+        if b is None or not x.is_cuda or x.dtype != torch.bfloat16:
+            return F.conv2d(x, self.weight.to(x.dtype), None, self.stride, self.pad)
+        from ..ops.conv import Conv1x1, ShadowConv
+
+        if not torch.is_grad_enabled():
+            return F.conv2d(x, b.w16.view(self.weight.shape), None, self.stride, self.pad)
+        if self.hip_gemm(x):
+            return Conv1x1.apply(x, self.weight, b, stats)
+        return ShadowConv.apply(x, self.weight, b, self.stride, self.pad)
+
+
+def _conv_bn(conv: _Conv, bn: "_BN", x, relu: bool = True, residual=None):
+    """bn.act(conv(x)) with the BatchNorm statistics produced by the conv's
+    epilogue when both run on the HIP kernels (one full read of the conv
+    output fewer per BatchNorm)."""
+    if _FUSE_STATS and conv.hip_gemm(x) and _BN_MODE == "hip" and bn.training:
+        from .._native import native
+
+        if native().reduce_atomic() == 0:  # partial-row statistics (deterministic)
+            cout = conv.weight.shape[0]
+            acc = torch.zeros(4 * cout, device=x.device)
+            y = conv(x, stats=acc[:2 * cout])
+            if bn.hip_ok(y, residual):
+                return bn.act(y, relu, residual, acc=acc)
+            return bn.act(y, relu, residual)
+    return bn.act(conv(x), relu, residual)
 
 
 class _Bottleneck(nn.Module):
@@ -81,10 +136,10 @@ class _Bottleneck(nn.Module):
             self.down = nn.ModuleList([_Conv(cin, cout, 1, stride, g), _BN(cout)])
 
     def forward(self, x):
-        y = self.b1.act(self.c1(x))
+        y = _conv_bn(self.c1, self.b1, x)
         y = self.b2.act(self.c2(y))
-        s = x if self.down is None else self.down[1].act(self.down[0](x), relu=False)
-        return self.b3.act(self.c3(y), residual=s)
+        s = x if self.down is None else _conv_bn(self.down[0], self.down[1], x, relu=False)
+        return _conv_bn(self.c3, self.b3, y, residual=s)
 
 
 class ResNet50(nn.Module):
@@ -121,6 +176,26 @@ class ResNet50(nn.Module):
     @staticmethod
     def loss(logp, target):
         return F.nll_loss(logp, target)
+
+    def attach_flat(self, flat, ready=None) -> None:
+        """Bind every convolution to the trainer's flat buffers: it then reads
+        its bf16 shadow weight and writes its fp32 gradient into the flat
+        gradient directly, reporting it with ``ready(leaf_index)`` (the
+        bucketed all-reduce) -- ops/conv.py."""
+        from ..ops.conv import ShadowBinding
+
+        if flat.shadow is None or flat.grad is None:
+            return
+        index = {id(t): i for i, t in enumerate(flat.leaves)}
+        w16, g32 = flat.shadow_views(), flat.views_of(flat.grad)
+        for m in self.modules():
+            if isinstance(m, _Conv):
+                i = index[id(m.weight)]
+                m.bind = ShadowBinding(w16[i], g32[i], (lambda i=i: ready(i)) if ready else (lambda: None))
+            elif isinstance(m, _BN):
+                # the HIP BatchNorm backward writes dgamma / dbeta straight into the flat gradient
+                iw, ib = index[id(m.weight)], index[id(m.bias)]
+                m.bind = (g32[iw], g32[ib], (lambda iw=iw, ib=ib: (ready(iw), ready(ib))) if ready else (lambda: None))
 
 
 def resnet50(num_classes: int = 1000, seed: Optional[int] = 0) -> ResNet50:

@@ -33,19 +33,24 @@ def supported(x: torch.Tensor) -> bool:
 
 class _BnAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, residual, relu, eps, momentum):
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, relu, eps, momentum, acc, grads):
         M, C = _geom(x)
         y = torch.empty_like(x, memory_format=torch.channels_last)
-        # forward and backward per-channel sums in one zeroed buffer (one fill)
-        acc = torch.zeros(4 * C, device=x.device, dtype=torch.float32)
+        # forward and backward per-channel sums in one zeroed buffer (one fill);
+        # a caller-provided acc already holds the forward statistics (emitted by the
+        # producing convolution's epilogue): the statistics pass is skipped
+        have_stats = acc is not None
+        if acc is None:
+            acc = torch.zeros(4 * C, device=x.device, dtype=torch.float32)
         save = torch.empty(2 * C, device=x.device, dtype=torch.float32)
         res = residual.contiguous(memory_format=torch.channels_last) if residual is not None else None
         native().bn_nhwc_fwd(x.data_ptr(), res.data_ptr() if res is not None else 0, y.data_ptr(), acc.data_ptr(),
                              weight.data_ptr(), bias.data_ptr(), save.data_ptr(),
                              running_mean.data_ptr() if running_mean is not None else 0,
                              running_var.data_ptr() if running_var is not None else 0, M, C, float(eps),
-                             float(momentum), int(relu), stream_handle())
+                             float(momentum), int(relu), int(have_stats), stream_handle())
         ctx.has_res = residual is not None
+        ctx.grads = grads
         # relu mask: from the output when a residual was added (mode 1),
         # otherwise recomputed from x in the backward kernels (mode 2: y is
         # neither saved nor read)
@@ -62,17 +67,29 @@ class _BnAct(torch.autograd.Function):
         dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
         acc = acc4[2 * C:]
         acc.zero_()  # the kernels accumulate atomically: a second backward (retain_graph) starts from 0 too
-        dw = torch.empty(C, device=x.device, dtype=torch.float32)
-        db = torch.empty(C, device=x.device, dtype=torch.float32)
+        if ctx.grads is not None:  # dgamma / dbeta straight into the flat gradient (overwritten)
+            dw, db, ready = ctx.grads
+        else:
+            dw = torch.empty(C, device=x.device, dtype=torch.float32)
+            db = torch.empty(C, device=x.device, dtype=torch.float32)
         native().bn_nhwc_bwd(dy.data_ptr(), y.data_ptr() if y is not None else 0, x.data_ptr(), save.data_ptr(),
                              weight.data_ptr(), bias.data_ptr(), acc.data_ptr(), dx.data_ptr(), dres.data_ptr() if dres is not None else 0, dw.data_ptr(),
                              db.data_ptr(), M, C, ctx.relu, stream_handle())
-        return dx, dw.to(weight.dtype), db.to(weight.dtype), None, None, dres, None, None, None
+        if ctx.grads is not None:
+            ready()
+            return dx, None, None, None, None, dres, None, None, None, None, None
+        return dx, dw.to(weight.dtype), db.to(weight.dtype), None, None, dres, None, None, None, None, None
 
 
 def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_mean: Optional[torch.Tensor],
            running_var: Optional[torch.Tensor], residual: Optional[torch.Tensor] = None, relu: bool = True,
-           eps: float = 1e-5, momentum: float = 0.1) -> torch.Tensor:
+           eps: float = 1e-5, momentum: float = 0.1, acc: Optional[torch.Tensor] = None,
+           grads=None) -> torch.Tensor:
+    """``acc``: optional zeroed fp32 [4C] whose first 2C already hold the
+    per-channel sum / sum of squares of x (see ops/conv.py Conv1x1).
+    ``grads``: optional (dweight view, dbias view, ready callback): the
+    backward writes the parameter gradients there (e.g. into the flat
+    gradient buffer) instead of returning them to autograd."""
     if not supported(x):
         raise ValueError(f"bn_act: needs a channels-last bf16 CUDA tensor with a supported channel count, got "
                          f"{tuple(x.shape)} {x.dtype} {x.device}")
@@ -80,5 +97,7 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
         raise ValueError("bn_act: residual must match x in shape and dtype")
     if weight.dtype != torch.float32 or bias.dtype != torch.float32:
         raise ValueError("bn_act: weight / bias must be fp32")
+    if acc is not None and (acc.numel() != 4 * x.shape[1] or acc.dtype != torch.float32):
+        raise ValueError("bn_act: acc must be fp32 [4C]")
     return _BnAct.apply(x, weight.contiguous(), bias.contiguous(), running_mean, running_var, residual, relu, eps,
-                        momentum)
+                        momentum, acc, grads)

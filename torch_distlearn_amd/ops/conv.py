@@ -1,0 +1,149 @@
+"""Convolutions of the ResNet-50 path that read the FlatParams bf16 shadow and
+write fp32 weight gradients straight into the flat gradient buffer.
+
+Without this, every step casts every fp32 master weight to bf16 in the
+forward (``weight.to(bf16)``) and casts + accumulates the bf16 weight gradient
+back into the fp32 ``.grad`` in the backward: 376 elementwise kernels,
+3.3 ms of a 35.5 ms ResNet-50 step (profiles/r1_resnet50_kernels.txt).  The
+fused SGD kernel already keeps a bf16 shadow of every parameter
+(csrc/kernels/flat_ops.hip ``sgd_kernel<.., kShadow>``), so:
+
+* :class:`Conv1x1` -- stride-1 1x1 convolutions (2 of the 3 convolutions of
+  every bottleneck) are plain NHWC GEMMs and run on the hand-written MFMA
+  kernels of ``csrc/kernels/conv_igemm.hip`` (``M = N*H*W`` pixels as a batch
+  of 1x1 images): forward ``y = x W^T`` (optionally emitting the following
+  BatchNorm's per-channel sum / sum of squares: deterministic partial rows
+  from its epilogue + a T x 2C column reduce, instead of the BatchNorm's own
+  pass over the M x C output), dgrad
+  ``dx = dy W`` (same kernel on the transposed shadow) and wgrad
+  ``dW = dy^T x`` written in fp32 into the flat gradient (split-K partials
+  atomically added when the weight is too small to fill the chip).
+* :class:`ShadowConv` -- every other convolution (3x3, strided, the 7x7 stem)
+  stays on MIOpen but reads the shadow and adds its weight gradient into the
+  flat buffer (one cast-add instead of three elementwise kernels).
+
+Both mark their weight's gradient ready for the bucketed all-reduce
+themselves (the autograd graph gets no weight gradient, so the
+post-accumulate-grad hook would never fire).
+
+Reference parity: these are the ResNet-50 stress config of BASELINE.json
+(config 5); the reference's own convolutions are cunn SpatialConvolutionMM
+(examples/cifar10.lua:108-126).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .._native import native, stream_handle
+
+BF16 = torch.bfloat16
+
+
+class ShadowBinding:
+    """What a conv module needs from the trainer: its bf16 shadow weight view,
+    its fp32 gradient view, and a callback that reports the gradient ready."""
+
+    __slots__ = ("w16", "g32", "ready")
+
+    def __init__(self, w16: torch.Tensor, g32: torch.Tensor, ready):
+        self.w16, self.g32, self.ready = w16, g32, ready
+
+
+def _fwd_plan(M: int, N: int, K: int):
+    from ..models.cifar_hip import _fwd_plan as plan
+
+    return plan(M, N, K)
+
+
+def _wgrad_plan(cout: int, K: int, M: int):
+    from ..models.cifar_hip import _wgrad_plan as plan
+
+    return plan(cout, K, M, 0)
+
+
+def conv1x1_supported(x: torch.Tensor, cout: int) -> bool:
+    cin = x.shape[1]
+    pow2 = lambda v: v >= 8 and (v & (v - 1)) == 0  # noqa: E731
+    M = x.shape[0] * x.shape[2] * x.shape[3]
+    return (x.is_cuda and x.dtype == BF16 and pow2(cin) and pow2(cout) and cout % 64 == 0 and cin % 64 == 0
+            and M * max(cin, cout) < (1 << 31))
+
+
+class Conv1x1(torch.autograd.Function):
+    """y = conv1x1(x, W) on the MFMA kernels; x channels-last bf16 [N, Cin, H, W]."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bind: ShadowBinding, stats):
+        C = native()
+        x = x.contiguous(memory_format=torch.channels_last)
+        N, cin, H, W = x.shape
+        cout = weight.shape[0]
+        M = N * H * W
+        y = torch.empty((N, cout, H, W), dtype=BF16, device=x.device, memory_format=torch.channels_last)
+        tile, splits = _fwd_plan(M, cout, cin)
+        slab = torch.empty(splits * M * cout, device=x.device) if splits > 1 else None
+        s = stream_handle()
+        rows = None
+        if stats is not None:
+            # the epilogue's deterministic per-M-tile partial sums (reduction mode 0) ...
+            if C.reduce_atomic() != 0:
+                raise RuntimeError("Conv1x1 statistics need reduction mode 0 (partial rows)")
+            nrows = C.conv_fwd_stat_rows(M, 1, 1, cin, cout, 1, tile, splits)
+            rows = torch.empty(max(nrows, 400 if splits > 1 else 1), 2, cout, device=x.device)
+        T = C.conv_fwd(x.data_ptr(), bind.w16.data_ptr(), y.data_ptr(), 0 if rows is None else rows.data_ptr(),
+                       0 if slab is None else slab.data_ptr(), M, 1, 1, cin, cout, 1, tile, splits, s)
+        if rows is not None:  # ... -> sum / sum of squares per channel for the BatchNorm
+            C.bn_rows_reduce(rows.data_ptr(), T, cout, stats.data_ptr(), s)
+        ctx.save_for_backward(x)
+        ctx.bind = bind
+        ctx.geom = (M, cin, cout)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        (x,) = ctx.saved_tensors
+        bind = ctx.bind
+        M, cin, cout = ctx.geom
+        s = stream_handle()
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wt = torch.empty(cin, cout, dtype=BF16, device=x.device)
+            C.weight_flip_transpose(bind.w16.data_ptr(), wt.data_ptr(), cout, cin, 1, s)
+            dx = torch.empty_like(x, memory_format=torch.channels_last)
+            tile, splits = _fwd_plan(M, cin, cout)
+            slab = torch.empty(splits * M * cin, device=x.device) if splits > 1 else None
+            C.conv_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, 0 if slab is None else slab.data_ptr(), M, 1,
+                       1, cout, cin, 1, tile, splits, s)
+        # fp32 weight gradient straight into the flat buffer (zeroed at step start)
+        tile, splits = _wgrad_plan(cout, cin, M)
+        C.conv_wgrad(dy.data_ptr(), x.data_ptr(), bind.g32.data_ptr(), M, 1, 1, cin, cout, 1, splits, cin, tile,
+                     cin if splits > 1 else 0, s)
+        bind.ready()
+        return dx, None, None, None
+
+
+class ShadowConv(torch.autograd.Function):
+    """MIOpen convolution on the bf16 shadow weight; fp32 weight gradient
+    added into the flat buffer."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bind: ShadowBinding, stride: int, pad: int):
+        w16 = bind.w16.view(weight.shape)
+        ctx.save_for_backward(x)
+        ctx.bind, ctx.stride, ctx.pad, ctx.wshape = bind, stride, pad, weight.shape
+        return F.conv2d(x, w16, None, stride, pad)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        bind = ctx.bind
+        w16 = bind.w16.view(ctx.wshape)
+        dx, dw, _ = torch.ops.aten.convolution_backward(
+            dy, x, w16, None, (ctx.stride, ctx.stride), (ctx.pad, ctx.pad), (1, 1), False, (0, 0), 1,
+            (ctx.needs_input_grad[0], True, False))
+        bind.g32.view(ctx.wshape).add_(dw)
+        bind.ready()
+        return dx, None, None, None, None

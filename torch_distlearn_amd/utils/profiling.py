@@ -51,7 +51,8 @@ def comm_summary(records) -> dict:
     * ``comm_ms``          -- summed all-reduce time per step (comm stream busy);
     * ``exposed_comm_ms``  -- time the compute stream waits for communication
       after its backward is done (the part NOT hidden behind backward);
-    * ``overlap_fraction`` -- 1 - exposed / comm;
+    * ``overlap_fraction`` -- 1 - exposed / comm, clamped to [0, 1] (the
+      exposed wait also holds the event / queue latency of the last bucket);
     * ``busbw_GBps``       -- ring bus bandwidth of the bucket all-reduces,
       2 (n-1)/n * bytes / time (set by the caller's world size).
     """
@@ -67,7 +68,8 @@ def comm_summary(records) -> dict:
         exposed += max(0.0, r["compute_done"].elapsed_time(r["comm_joined"]))
     n = len(recs)
     return {"steps": n, "comm_ms": round(comm / n, 4), "exposed_comm_ms": round(exposed / n, 4),
-            "overlap_fraction": round(1.0 - (exposed / comm if comm > 0 else 0.0), 4),
+            # exposed can exceed comm when issue latency dominates tiny collectives: clamp
+            "overlap_fraction": round(min(1.0, max(0.0, 1.0 - (exposed / comm if comm > 0 else 0.0))), 4),
             "bytes_per_step": nbytes // n, "buckets": len(recs[0]["buckets"])}
 
 
