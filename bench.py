@@ -39,17 +39,18 @@ def parse():
                     help="sgd = AllReduceSGD (headline), ea = AllReduceEA (tau, alpha), "
                          "async = AsyncEA: rank 0 parameter server + N-1 clients (BASELINE configs 2-4)")
     ap.add_argument("--model", default="cifar10", choices=["cifar10", "resnet50"],
-                    help="resnet50 = BASELINE config 5 (ImageNet shape 224x224, MIOpen ops)")
+                    help="resnet50 = BASELINE config 5 (ImageNet shape 224x224; 1x1 convs on the HIP MFMA kernels, "
+                         "3x3/strided convs on MIOpen, HIP BatchNorm)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = gloo plumbing check of the same code path (tests only; not a benchmark)")
     ap.add_argument("--tau", type=int, default=10)
     ap.add_argument("--alpha", type=float, default=0.2)
-    ap.add_argument("--graph", type=int, default=None,
-                    help="capture the step in a hipGraph (default: cifar10 1; resnet50 0 -- with MIOpen BN the "
-                         "replayed graph produced NaN losses; with the HIP BN it trains without NaN and is 3%% "
-                         "faster (35.1 vs 36.2 ms/step) but its loss after 45 steps is systematically off the "
-                         "eager run's (6.557 / 6.558 vs 6.509; eager reruns agree to 0.002), so it stays off "
-                         "until that is understood; scripts/r50_graph_check.sh)")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="capture the step in a hipGraph (default 1).  ResNet-50: one step from the same state "
+                         "differs between graph and eager by 2.0e-3 (relative, all gradients) while two eager runs "
+                         "differ by 2.4e-3 and eager vs fp32 by 3.5e-2 (scripts/diag_r50_graph.py, "
+                         "profiles/r2_resnet50_graph_diag.txt): the round-1 loss drift after 45 steps was bf16 "
+                         "run-to-run noise amplified by a memorising synthetic run, not a graph bug")
     ap.add_argument("--bucket-mb", type=float, default=None,
                     help="gradient all-reduce bucket size (default: cifar10 1 MiB = 3 buckets "
                          "{conv4+bn4+fc, conv3+bn3, conv1..bn2}; resnet50 16 MiB)")
@@ -105,8 +106,6 @@ def main():
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29517")
     batch = a.batch or (128 if a.model == "cifar10" else 256)
-    if a.graph is None:
-        a.graph = 1 if a.model == "cifar10" else 0
     if a.lr is None:
         a.lr = 0.1 if a.model == "cifar10" else 0.02
     if a.bucket_mb is None:

@@ -29,6 +29,7 @@ PYBIND11_MODULE(_C, m) {
 
   // ---- convnet kernels (MFMA implicit GEMM, BN/ReLU/pool, classifier head) ------
   m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd_add", &conv_fwd_add);
   m.def("conv_fwd_stat_rows", &conv_fwd_stat_rows);
   m.def("set_conv_region", &set_conv_region);
   m.def("set_conv_region_stages", &set_conv_region_stages);
@@ -69,6 +70,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_reduce_head", &bn_bwd_reduce_head);
   m.def("head_wgrad", &head_wgrad);
   m.def("mnist_step", &mnist_step);
+  m.def("maxpool_nhwc_fwd", &maxpool_nhwc_fwd);
+  m.def("maxpool_nhwc_bwd", &maxpool_nhwc_bwd);
 
   // ---- RCCL communicator ------------------------------------------------------
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });

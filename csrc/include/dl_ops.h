@@ -50,6 +50,8 @@ void set_conv_debug(uintptr_t buf);
 void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, int Cin, int Cout, int KS, int splits,
                 int ldo, int tile, int atomic_creal, uintptr_t stream);
 void set_reduce_atomic_conv(int on);
+void conv_fwd_add(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t addend, int B, int H, int W, int Cin, int Cout,
+                  int KS, int tile, uintptr_t stream);
 void slab_reduce(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream);
 void weight_flip_transpose(uintptr_t w, uintptr_t wt, int Cout, int Cin, int KS, uintptr_t stream);
 void pack_weight(uintptr_t w, uintptr_t wp, int Cout, int taps, int C, int Cp, uintptr_t stream);
@@ -97,6 +99,12 @@ void head_fwd_bwd_pool(uintptr_t y, uintptr_t coef, int yH, int yW, int yC, uint
                        uintptr_t stream);
 void head_wgrad(uintptr_t h, uintptr_t dlogits, uintptr_t loss_b, int F, int B, int NC, uintptr_t dw, uintptr_t db,
                 uintptr_t loss, uintptr_t slot, uintptr_t step_ctr, uintptr_t stream);
+
+// pool_nhwc.hip ----------------------------------------------------------------
+void maxpool_nhwc_fwd(uintptr_t x, uintptr_t y, uintptr_t idx, int N, int H, int W, int C, int K, int S, int P,
+                      uintptr_t stream);
+void maxpool_nhwc_bwd(uintptr_t dy, uintptr_t idx, uintptr_t dx, int N, int H, int W, int C, int K, int S, int P,
+                      uintptr_t stream);
 
 // mnist.hip -------------------------------------------------------------------
 void mnist_step(uintptr_t x, int x_bf16, uintptr_t labels, uintptr_t w1, uintptr_t b1, uintptr_t w2, uintptr_t b2,

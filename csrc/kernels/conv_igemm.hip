@@ -193,7 +193,11 @@ __device__ __forceinline__ void block_sync_lds() {
 // split-K partials; else bf16 y (+ STATS: per-M-tile channel sum / sum of
 // squares of exactly the stored bf16 values, one deterministic partial row
 // per M tile, reduced through `smem`, which the caller no longer uses).
-template <int BM, int BN, bool STATS, bool SLAB, int WM, int WN>
+// ADD (!SLAB): y = bf16(acc + addend) with addend a bf16 [M][Cout] tensor passed
+// through the (otherwise unused) slab pointer -- the dgrad of a 1x1 conv whose
+// input also feeds a residual branch adds that branch's gradient in place of a
+// separate elementwise pass (ops/conv.py).
+template <int BM, int BN, bool STATS, bool SLAB, int WM, int WN, bool ADD = false>
 __device__ __forceinline__ void conv_fwd_epilogue(const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], const ConvGeom& g,
                                                   bf16_t* __restrict__ y, float* __restrict__ stats,
                                                   float* __restrict__ slab, int split, int tm, int m0, int n0,
@@ -227,7 +231,11 @@ __device__ __forceinline__ void conv_fwd_epilogue(const f32x4 (&acc)[BM / WM / 1
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = m0 + wm * TM + a * 16 + rq * 4 + r;
-          const bf16_t hv = f32_to_bf16(acc[a][b][r]);
+          float v0 = acc[a][b][r];
+          if constexpr (ADD) {
+            if (m < g.M && n < g.Cout) v0 += bf16_to_f32(reinterpret_cast<const bf16_t*>(slab)[(int64_t)m * g.Cout + n]);
+          }
+          const bf16_t hv = f32_to_bf16(v0);
           if (m < g.M && n < g.Cout) y[(int64_t)m * g.Cout + n] = hv;
           if constexpr (STATS) {
             const float v = m < g.M ? bf16_to_f32(hv) : 0.f;  // statistics of exactly what is stored
@@ -272,7 +280,7 @@ __device__ __forceinline__ void conv_fwd_epilogue(const f32x4 (&acc)[BM / WM / 1
 // 256 threads = 4 waves (2 x 2), wave tile (BM/2) x (BN/2), BK = 64,
 // 3-stage LDS ring filled by LDS-DMA, one barrier per K step.
 // --------------------------------------------------------------------------
-template <int BM, int BN, bool STATS, bool SLAB, bool TAPU, int STAGES, int WM = 2, int WN = 2>
+template <int BM, int BN, bool STATS, bool SLAB, bool TAPU, int STAGES, int WM = 2, int WN = 2, bool ADD = false>
 __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                        bf16_t* __restrict__ y, float* __restrict__ stats,
                                                        float* __restrict__ slab, const ConvGeom g, int splits,
@@ -458,7 +466,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
       d[0] = t_start; d[1] = t_setup; d[2] = t_loop; d[3] = stamp();
     }
   };
-  conv_fwd_epilogue<BM, BN, STATS, SLAB, WM, WN>(acc, g, y, stats, slab, split, tm, m0, n0, smem);
+  conv_fwd_epilogue<BM, BN, STATS, SLAB, WM, WN, ADD>(acc, g, y, stats, slab, split, tm, m0, n0, smem);
   dbg_out();
 }
 
@@ -1499,6 +1507,8 @@ int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile,
   return (g.M + rpb - 1) / rpb;
 }
 
+static uintptr_t g_fwd_addend = 0;  // conv_fwd_add: bf16 [M][Cout] added in the epilogue
+
 template <int BM, int BN, bool TAPU, int ST, int WM, int WN>
 static void launch_fwd_w(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
                          uintptr_t slab, int splits, hipStream_t s) {
@@ -1507,7 +1517,11 @@ static void launch_fwd_w(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t 
   const int ktps = (nkt + splits - 1) / splits;
   const int grid = ntm * ntn * splits;
   constexpr int NT = 64 * WM * WN;
-  if (splits > 1)
+  if (g_fwd_addend && (splits > 1 || stats)) throw std::runtime_error("conv_fwd_add: no split-K / statistics");
+  if (g_fwd_addend)
+    conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, true><<<grid, NT, 0, s>>>(
+        (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, (float*)g_fwd_addend, g, 1, ktps, g_conv_dbg);
+  else if (splits > 1)
     conv_fwd_kernel<BM, BN, false, true, TAPU, ST, WM, WN><<<grid, NT, 0, s>>>(
         (const bf16_t*)x, (const bf16_t*)w, nullptr, nullptr, (float*)slab, g, splits, ktps, g_conv_dbg);
   else if (stats)
@@ -1726,6 +1740,29 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
     splitk_combine_kernel<false><<<nb, 256, 0, s>>>((const float*)slab, (bf16_t*)y, nullptr, splits, g.M, Cout, rpb);
   DL_HIP_CHECK(hipGetLastError());
   return nb;
+}
+
+// y = conv(x, w) + addend (bf16, same layout as y), streaming kernel only
+// (KS = 1 or the region kernels disabled for the shape), no split-K / stats.
+void conv_fwd_add(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t addend, int B, int H, int W, int Cin, int Cout,
+                  int KS, int tile, uintptr_t stream) {
+  ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
+  hipStream_t s = as_stream(stream);
+  if (!addend) throw std::runtime_error("conv_fwd_add: null addend");
+  if (Cout % fwd_bn(tile) != 0) throw std::runtime_error("conv_fwd_add: Cout must be a multiple of the N tile");
+  if (KS != 1 && g_region) throw std::runtime_error("conv_fwd_add: only the streaming kernel (KS = 1)");
+  g_fwd_addend = addend;
+  try {
+    if (tile == 0) launch_fwd<128, 128>(g, x, w, y, 0, 0, 1, s);
+    else if (tile == 1) launch_fwd<64, 64>(g, x, w, y, 0, 0, 1, s);
+    else if (tile == 2) launch_fwd<128, 64>(g, x, w, y, 0, 0, 1, s);
+    else throw std::runtime_error("conv_fwd_add: bad tile id");
+  } catch (...) {
+    g_fwd_addend = 0;
+    throw;
+  }
+  g_fwd_addend = 0;
+  DL_HIP_CHECK(hipGetLastError());
 }
 
 // out: fp32 [splits][Cout][ldo], ldo >= K (K = KS*KS*Cin); tile 0 = 128x64, 1 = 64x64 (co x k)

@@ -25,7 +25,8 @@ namespace dl {
 
 namespace {
 
-constexpr int kT = 256;  // threads per workgroup (4 waves)
+constexpr int kT = 1024;  // threads per workgroup (16 waves: 4 per SIMD hide the LDS latency)
+constexpr int kNW = kT / 64;
 constexpr int IMG = 32, K5 = 5, C1 = 16, H1 = 28, P1 = 14, C2 = 16, H2 = 10, P2 = 5;
 constexpr int NF = C2 * P2 * P2;  // 400 features
 constexpr int NC = 10;
@@ -45,15 +46,17 @@ constexpr int L_A2 = L_DP1 + C1 * P1 * P1;     // 1600 tanh(conv2), later dz2
 constexpr int L_P2 = L_A2 + C2 * H2 * H2;      // 400 pooled 2 (features)
 constexpr int L_DP2 = L_P2 + NF;               // 400 d features
 constexpr int L_LG = L_DP2 + NF;               // 16 logits / dlogits
-constexpr int L_RED = L_LG + 16;               // 4 x 16 wave partials
-constexpr int L_END = L_RED + 64;
+constexpr int L_RED = L_LG + 16;               // kNW x 16 wave partials
+constexpr int L_END = L_RED + kNW * 16;
 constexpr int L_IDX1 = L_END;                  // 3136 bytes of argmax (as floats: 784)
 constexpr int L_IDX2 = L_IDX1 + C1 * P1 * P1 / 4;  // 400 bytes (100 floats)
 constexpr int L_TOTAL = L_IDX2 + NF / 4;
 constexpr size_t kLdsBytes = (size_t)L_TOTAL * 4;
 static_assert(kLdsBytes <= 160 * 1024, "MNIST step does not fit in LDS");
 
-__device__ __forceinline__ float tanh_f(float v) { return tanhf(v); }
+// tanh(v) = 1 - 2 / (exp(2v) + 1): exact limits at +-inf, ~1 ulp-level error
+// on the hardware exp (the reference's Tanh is fp32 too)
+__device__ __forceinline__ float tanh_f(float v) { return 1.f - 2.f / (__expf(2.f * v) + 1.f); }
 
 }  // namespace
 
@@ -169,7 +172,9 @@ __global__ void __launch_bounds__(kT) mnist_step_kernel(const void* __restrict__
     float z[NC], mx = -INFINITY;
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
-      z[k] = red[k] + red[16 + k] + red[32 + k] + red[48 + k] + sbf[k];
+      float t = sbf[k];
+      for (int w = 0; w < kNW; ++w) t += red[w * 16 + k];
+      z[k] = t;
       mx = fmaxf(mx, z[k]);
     }
     float se = 0.f;

@@ -18,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--only", default=None, help="e.g. hip-graph / torch-graph (profiling)")
     a = ap.parse_args()
     from torch_distlearn_amd import Tree
     from torch_distlearn_amd.engine import DataParallelTrainer
@@ -29,6 +30,8 @@ def main():
     xs = torch.randn(64, a.batch, 1024, device=dev, generator=g)
     ys = torch.randint(0, 10, (64, a.batch), device=dev, generator=g)
     for backend, graph in (("hip", True), ("hip", False), ("torch", True), ("torch", False)):
+        if a.only and a.only != f"{backend}-{'graph' if graph else 'eager'}":
+            continue
         m = MnistConvNet(seed=0).to(dev)
         tr = DataParallelTrainer(m, tree, lr=0.01, backend=backend, compute_dtype=torch.float32, graph=graph,
                                  max_batch=a.batch)

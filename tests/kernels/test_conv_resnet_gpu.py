@@ -134,3 +134,27 @@ def test_resnet50_bound_convs_match_unbound(dev, monkeypatch):
     assert abs(lb - lu) < 2e-2 * max(1.0, abs(lu))
     cos = float(F.cosine_similarity(db, du, dim=0))
     assert cos > 0.98, cos
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (2, 16, 9, 13), (3, 8, 7, 7)])
+def test_maxpool_nhwc_matches_torch(dev, shape):
+    """HIP channels-last 3x3/2 max pool (argmax bytes, gather backward) ==
+    torch.nn.functional.max_pool2d forward and backward (same bf16 values,
+    first-max tie rule)."""
+    from torch_distlearn_amd.ops.pool import max_pool2d_nhwc
+
+    N, C, H, W = shape
+    g = torch.Generator(device=dev).manual_seed(C + H)
+    # quantised values: plenty of ties inside the windows
+    x = (torch.randn(N, C, H, W, device=dev, generator=g) * 2).round().div(2).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    xa = x.detach().requires_grad_(True)
+    xb = x.detach().requires_grad_(True)
+    ya = max_pool2d_nhwc(xa, 3, 2, 1)
+    yb = F.max_pool2d(xb, 3, 2, 1)
+    go = torch.randn_like(yb)
+    ya.backward(go)
+    yb.backward(go)
+    torch.cuda.synchronize()
+    assert torch.equal(ya, yb)
+    torch.testing.assert_close(xa.grad.float(), xb.grad.float(), rtol=1e-2, atol=1e-2)

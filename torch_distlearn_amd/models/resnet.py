@@ -53,14 +53,14 @@ class _BN(nn.Module):
         return supported(x) and self.weight.dtype == torch.float32 and (
             residual is None or (residual.dtype == x.dtype and residual.shape == x.shape))
 
-    def act(self, x, relu: bool = True, residual=None, acc=None):
+    def act(self, x, relu: bool = True, residual=None, acc=None, res_sink=None):
         """act(BN(x) [+ residual]); one fused HIP kernel pair in "hip" mode
         (``acc``: statistics already accumulated by the producing conv)."""
         if self.hip_ok(x, residual):
             from ..ops.bn_nhwc import bn_act
 
             return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual, relu, acc=acc,
-                          grads=self.bind)
+                          grads=self.bind, res_sink=res_sink)
         y = self(x)
         if residual is not None:
             y = y + residual
@@ -74,6 +74,10 @@ class _BN(nn.Module):
 _CONV_MODE = os.environ.get("DISTLEARN_RESNET_CONV", "hip")
 # BatchNorm statistics from the 1x1 GEMM epilogue (skips the BN statistics pass)
 _FUSE_STATS = os.environ.get("DISTLEARN_RESNET_FUSE_STATS", "1") == "1"
+# residual gradient added in the c1 dgrad epilogue (ops/conv.py conv_fwd_add)
+_FUSE_RES = os.environ.get("DISTLEARN_RESNET_FUSE_RES", "1") == "1"
+# stem max-pool on the HIP gather-backward kernels (ops/pool.py)
+_POOL_HIP = os.environ.get("DISTLEARN_RESNET_POOL", "hip") == "hip"
 
 
 class _Conv(nn.Module):
@@ -92,9 +96,11 @@ class _Conv(nn.Module):
 
         return _CONV_MODE == "hip" and self.k == 1 and self.stride == 1 and conv1x1_supported(x, self.weight.shape[0])
 
-    def forward(self, x, stats=None):
+    def forward(self, x, stats=None, res_link=None):
         """``stats``: optional zeroed fp32 [2*Cout] that receives the output's
-        per-channel sum / sum of squares (HIP GEMM path only)."""
+        per-channel sum / sum of squares (HIP GEMM path only); ``res_link``:
+        a dict through which a residual BatchNorm hands over the gradient of
+        the same input (added in the dgrad epilogue)."""
         b = self.bind
         if b is None or not x.is_cuda or x.dtype != torch.bfloat16:
             return F.conv2d(x, self.weight.to(x.dtype), None, self.stride, self.pad)
@@ -103,11 +109,11 @@ class _Conv(nn.Module):
         if not torch.is_grad_enabled():
             return F.conv2d(x, b.w16.view(self.weight.shape), None, self.stride, self.pad)
         if self.hip_gemm(x):
-            return Conv1x1.apply(x, self.weight, b, stats)
+            return Conv1x1.apply(x, self.weight, b, stats, res_link)
         return ShadowConv.apply(x, self.weight, b, self.stride, self.pad)
 
 
-def _conv_bn(conv: _Conv, bn: "_BN", x, relu: bool = True, residual=None):
+def _conv_bn(conv: _Conv, bn: "_BN", x, relu: bool = True, residual=None, link=None, res_sink=None):
     """bn.act(conv(x)) with the BatchNorm statistics produced by the conv's
     epilogue when both run on the HIP kernels (one full read of the conv
     output fewer per BatchNorm)."""
@@ -117,11 +123,11 @@ def _conv_bn(conv: _Conv, bn: "_BN", x, relu: bool = True, residual=None):
         if native().reduce_atomic() == 0:  # partial-row statistics (deterministic)
             cout = conv.weight.shape[0]
             acc = torch.zeros(4 * cout, device=x.device)
-            y = conv(x, stats=acc[:2 * cout])
+            y = conv(x, stats=acc[:2 * cout], res_link=link)
             if bn.hip_ok(y, residual):
-                return bn.act(y, relu, residual, acc=acc)
+                return bn.act(y, relu, residual, acc=acc, res_sink=res_sink)
             return bn.act(y, relu, residual)
-    return bn.act(conv(x), relu, residual)
+    return bn.act(conv(x, res_link=link) if conv.bind is not None else conv(x), relu, residual, res_sink=res_sink)
 
 
 class _Bottleneck(nn.Module):
@@ -136,10 +142,13 @@ class _Bottleneck(nn.Module):
             self.down = nn.ModuleList([_Conv(cin, cout, 1, stride, g), _BN(cout)])
 
     def forward(self, x):
-        y = _conv_bn(self.c1, self.b1, x)
+        # identity residual + c1 on the HIP GEMM: the residual BatchNorm (b3) hands the
+        # gradient of x to c1, whose dgrad epilogue adds it (no separate x-gradient sum)
+        link = {} if (self.down is None and _FUSE_RES and torch.is_grad_enabled() and self.c1.hip_gemm(x)) else None
+        y = _conv_bn(self.c1, self.b1, x, link=link)
         y = self.b2.act(self.c2(y))
         s = x if self.down is None else _conv_bn(self.down[0], self.down[1], x, relu=False)
-        return _conv_bn(self.c3, self.b3, y, residual=s)
+        return _conv_bn(self.c3, self.b3, y, residual=s, res_sink=link)
 
 
 class ResNet50(nn.Module):
@@ -165,7 +174,10 @@ class ResNet50(nn.Module):
         h = x.to(cd)
         if h.is_cuda:
             h = h.contiguous(memory_format=torch.channels_last)
-        h = F.max_pool2d(self.stem_bn.act(self.stem(h)), 3, 2, 1)
+        h = self.stem_bn.act(self.stem(h))
+        from ..ops.pool import max_pool2d_nhwc, supported
+
+        h = max_pool2d_nhwc(h, 3, 2, 1) if (_POOL_HIP and supported(h)) else F.max_pool2d(h, 3, 2, 1)
         for b in self.blocks:
             h = b(h)
         # classifier in fp32 (2048 x 1000: negligible cost): bf16 logits of a

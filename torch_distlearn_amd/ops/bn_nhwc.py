@@ -33,7 +33,7 @@ def supported(x: torch.Tensor) -> bool:
 
 class _BnAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, residual, relu, eps, momentum, acc, grads):
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, relu, eps, momentum, acc, grads, res_sink):
         M, C = _geom(x)
         y = torch.empty_like(x, memory_format=torch.channels_last)
         # forward and backward per-channel sums in one zeroed buffer (one fill);
@@ -51,6 +51,9 @@ class _BnAct(torch.autograd.Function):
                              float(momentum), int(relu), int(have_stats), stream_handle())
         ctx.has_res = residual is not None
         ctx.grads = grads
+        ctx.res_sink = res_sink
+        if res_sink is not None and residual is not None:
+            res_sink["expect"] = True  # the residual's gradient goes to the sink, not to autograd
         # relu mask: from the output when a residual was added (mode 1),
         # otherwise recomputed from x in the backward kernels (mode 2: y is
         # neither saved nor read)
@@ -75,21 +78,27 @@ class _BnAct(torch.autograd.Function):
         native().bn_nhwc_bwd(dy.data_ptr(), y.data_ptr() if y is not None else 0, x.data_ptr(), save.data_ptr(),
                              weight.data_ptr(), bias.data_ptr(), acc.data_ptr(), dx.data_ptr(), dres.data_ptr() if dres is not None else 0, dw.data_ptr(),
                              db.data_ptr(), M, C, ctx.relu, stream_handle())
+        if ctx.res_sink is not None and dres is not None:
+            ctx.res_sink["g"] = dres  # consumed by the conv whose input is the residual (ops/conv.py)
+            dres = None
         if ctx.grads is not None:
             ready()
-            return dx, None, None, None, None, dres, None, None, None, None, None
-        return dx, dw.to(weight.dtype), db.to(weight.dtype), None, None, dres, None, None, None, None, None
+            return dx, None, None, None, None, dres, None, None, None, None, None, None
+        return dx, dw.to(weight.dtype), db.to(weight.dtype), None, None, dres, None, None, None, None, None, None
 
 
 def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_mean: Optional[torch.Tensor],
            running_var: Optional[torch.Tensor], residual: Optional[torch.Tensor] = None, relu: bool = True,
            eps: float = 1e-5, momentum: float = 0.1, acc: Optional[torch.Tensor] = None,
-           grads=None) -> torch.Tensor:
+           grads=None, res_sink: Optional[dict] = None) -> torch.Tensor:
     """``acc``: optional zeroed fp32 [4C] whose first 2C already hold the
     per-channel sum / sum of squares of x (see ops/conv.py Conv1x1).
     ``grads``: optional (dweight view, dbias view, ready callback): the
     backward writes the parameter gradients there (e.g. into the flat
-    gradient buffer) instead of returning them to autograd."""
+    gradient buffer) instead of returning them to autograd.
+    ``res_sink``: a dict that receives the residual's gradient (key ``"g"``)
+    instead of autograd, for a consumer that adds it itself (Conv1x1's dgrad
+    epilogue): saves the separate gradient-sum pass of a tensor used twice."""
     if not supported(x):
         raise ValueError(f"bn_act: needs a channels-last bf16 CUDA tensor with a supported channel count, got "
                          f"{tuple(x.shape)} {x.dtype} {x.device}")
@@ -100,4 +109,4 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
     if acc is not None and (acc.numel() != 4 * x.shape[1] or acc.dtype != torch.float32):
         raise ValueError("bn_act: acc must be fp32 [4C]")
     return _BnAct.apply(x, weight.contiguous(), bias.contiguous(), running_mean, running_var, residual, relu, eps,
-                        momentum, acc, grads)
+                        momentum, acc, grads, res_sink)

@@ -74,8 +74,9 @@ class Conv1x1(torch.autograd.Function):
     """y = conv1x1(x, W) on the MFMA kernels; x channels-last bf16 [N, Cin, H, W]."""
 
     @staticmethod
-    def forward(ctx, x, weight, bind: ShadowBinding, stats):
+    def forward(ctx, x, weight, bind: ShadowBinding, stats, res_link=None):
         C = native()
+        ctx.res_link = res_link
         x = x.contiguous(memory_format=torch.channels_last)
         N, cin, H, W = x.shape
         cout = weight.shape[0]
@@ -109,20 +110,38 @@ class Conv1x1(torch.autograd.Function):
         s = stream_handle()
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = None
+        add = None
+        link = ctx.res_link
+        if link is not None and link.get("expect"):
+            # the same input also fed a residual branch whose BatchNorm parked its
+            # gradient here (ops/bn_nhwc.py res_sink): dx = dy W + that gradient
+            add = link.pop("g", None)
+            if add is None:
+                raise RuntimeError("Conv1x1: the residual branch's gradient did not arrive before the dgrad")
+            add = add.contiguous(memory_format=torch.channels_last)
         if ctx.needs_input_grad[0]:
             wt = torch.empty(cin, cout, dtype=BF16, device=x.device)
             C.weight_flip_transpose(bind.w16.data_ptr(), wt.data_ptr(), cout, cin, 1, s)
             dx = torch.empty_like(x, memory_format=torch.channels_last)
             tile, splits = _fwd_plan(M, cin, cout)
-            slab = torch.empty(splits * M * cin, device=x.device) if splits > 1 else None
-            C.conv_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, 0 if slab is None else slab.data_ptr(), M, 1,
-                       1, cout, cin, 1, tile, splits, s)
+            if add is not None and splits == 1:
+                C.conv_fwd_add(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), add.data_ptr(), M, 1, 1, cout, cin, 1,
+                               tile, s)
+                add = None
+            else:
+                slab = torch.empty(splits * M * cin, device=x.device) if splits > 1 else None
+                C.conv_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, 0 if slab is None else slab.data_ptr(),
+                           M, 1, 1, cout, cin, 1, tile, splits, s)
+            if add is not None:
+                dx.add_(add)
+        elif add is not None:
+            dx = add
         # fp32 weight gradient straight into the flat buffer (zeroed at step start)
         tile, splits = _wgrad_plan(cout, cin, M)
         C.conv_wgrad(dy.data_ptr(), x.data_ptr(), bind.g32.data_ptr(), M, 1, 1, cin, cout, 1, splits, cin, tile,
                      cin if splits > 1 else 0, s)
         bind.ready()
-        return dx, None, None, None
+        return dx, None, None, None, None
 
 
 class ShadowConv(torch.autograd.Function):
