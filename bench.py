@@ -111,8 +111,11 @@ def main():
     if a.bucket_mb is None:
         a.bucket_mb = 1.0 if a.model == "cifar10" else 16.0
     backend = a.backend if (a.model == "cifar10" and not cpu) else "torch"
-    if backend == "torch" and not cpu and os.environ.get("DISTLEARN_MIOPEN_FIND", "0") == "1":
-        torch.backends.cudnn.benchmark = True  # MIOpen exhaustive find per conv shape (warmup pays it)
+    if backend == "torch" and not cpu and os.environ.get("DISTLEARN_MIOPEN_FIND", "1") == "1":
+        # MIOpen solver search per conv shape (the remaining 3x3 / strided / stem convs of
+        # ResNet-50); runs in the graph-capture warm-up steps, before the timed region.
+        # Measured 32.69 vs 33.93 ms/step at batch 256 (profiles/r2_bench_resnet50.txt)
+        torch.backends.cudnn.benchmark = True
     cdt = torch.float32 if cpu else torch.bfloat16
 
     from torch_distlearn_amd import Tree
