@@ -70,6 +70,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_reduce_head", &bn_bwd_reduce_head);
   m.def("head_wgrad", &head_wgrad);
   m.def("mnist_step", &mnist_step);
+  m.def("mnist_scratch_bytes", &mnist_scratch_bytes);
   m.def("maxpool_nhwc_fwd", &maxpool_nhwc_fwd);
   m.def("maxpool_nhwc_bwd", &maxpool_nhwc_bwd);
 

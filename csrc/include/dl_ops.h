@@ -109,6 +109,7 @@ void maxpool_nhwc_bwd(uintptr_t dy, uintptr_t idx, uintptr_t dx, int N, int H, i
 // mnist.hip -------------------------------------------------------------------
 void mnist_step(uintptr_t x, int x_bf16, uintptr_t labels, uintptr_t w1, uintptr_t b1, uintptr_t w2, uintptr_t b2,
                 uintptr_t wf, uintptr_t bf, uintptr_t gw1, uintptr_t gb1, uintptr_t gw2, uintptr_t gb2, uintptr_t gwf,
-                uintptr_t gbf, uintptr_t logp, uintptr_t loss_b, int B, uintptr_t stream);
+                uintptr_t gbf, uintptr_t logp, uintptr_t loss_b, uintptr_t scratch, int B, uintptr_t stream);
+int64_t mnist_scratch_bytes(int B);
 
 }  // namespace dl

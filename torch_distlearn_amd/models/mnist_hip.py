@@ -1,10 +1,10 @@
 """Native executor for the reference MNIST convnet: the whole forward +
-backward of a training step is ONE hand-written gfx950 kernel
-(csrc/kernels/mnist.hip, one workgroup per sample, everything in LDS).
+backward of a training step is four small hand-written gfx950 kernels
+(csrc/kernels/mnist.hip), each parallel over (channel x sample) workgroups.
 
 Reference: examples/mnist.lua:53-130 (batch 1 per node, lr 0.01).  The
 reference's step is ~35 library kernels for ~6 MFLOP of work, i.e. pure launch
-latency; here it is this kernel + the engine's zero-fill
+latency; here it is these kernels + the engine's zero-fill
 of the gradient buffer + the fused SGD update, all captured in one hipGraph
 (``DataParallelTrainer(graph=True)``), with the whole 43 KB gradient in one
 all-reduce bucket.
@@ -36,6 +36,8 @@ class MnistHIPExecutor:
         self.cap = int(max_batch or 1)
         self.logp = torch.empty(self.cap, 10, device=dev)
         self.loss_b = torch.empty(self.cap, device=dev)
+        # per-sample activations / argmax bytes / conv2 output gradient (kernel scratch)
+        self.scratch = torch.empty(self.C.mnist_scratch_bytes(self.cap) // 4, device=dev)
         self._last_b = 0
 
     def _input(self, x: torch.Tensor) -> torch.Tensor:
@@ -55,7 +57,7 @@ class MnistHIPExecutor:
         train = labels is not None
         self.C.mnist_step(x.data_ptr(), int(x.dtype == torch.bfloat16), labels.data_ptr() if train else 0,
                           *[t.data_ptr() for t in p], *[t.data_ptr() for t in g], self.logp.data_ptr(),
-                          self.loss_b.data_ptr() if train else 0, B, stream_handle())
+                          self.loss_b.data_ptr() if train else 0, self.scratch.data_ptr(), B, stream_handle())
         self._last_b = B
         return B
 
