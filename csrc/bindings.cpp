@@ -43,6 +43,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_conv_debug", &set_conv_debug);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("slab_reduce", &slab_reduce);
+  m.def("slab_reduce_add", &slab_reduce_add);
   m.def("weight_flip_transpose", &weight_flip_transpose);
   m.def("pack_weight", &pack_weight);
   m.def("pad_channels", &pad_channels);

@@ -273,6 +273,121 @@ __device__ __forceinline__ void conv_fwd_epilogue(const f32x4 (&acc)[BM / WM / 1
   }
 }
 
+// Inclusive sum over the 16 lanes of each DPP row: lane 15 of the row ends
+// with the row total (row_shr 1, 2, 4, 8 with zero fill; fixed order).
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x112, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x114, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x118, 0xf, 0xf, true));
+  return v;
+}
+
+// Transposed epilogue (region kernel, and the streaming kernel whenever its
+// wave tile has an even number of N fragments).  The MFMAs compute C^T
+// (weights as the A operand), so lane l holds, per 16-pixel M fragment a and
+// N-fragment pair p, the 8 CONSECUTIVE channels n0 + wn*TN + 32p + 8*(l>>4) +
+// 0..7 of pixel m0 + wm*TM + 16a + (l&15) (fragments 2p / 2p+1 hold channel
+// quads 0..3 / 4..7, see the B row map b_frag_row): one 16-byte bf16 store (or
+// two 16-byte fp32 slab stores) per (a, p) instead of 8 scattered 2-byte
+// stores.  Measured on the ResNet-50 1x1 shapes (scripts/bench_gemm1x1.py):
+// the write-heavy GEMMs (Cout = 4 Cin) ran at ~2.6 TB/s with the scattered
+// stores vs ~5 TB/s for the read-heavy ones.  BN statistics: DPP row sums
+// over the 16 pixels of a lane group, then a fixed-order sum over the WM wave
+// rows through LDS (deterministic).  ADD: + a bf16 [M][Cout] addend (16-byte
+// loads), passed through the slab pointer.
+template <int BM, int BN, bool STATS, bool SLAB, int WM, int WN, int FM, int FN, bool ADD = false>
+__device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], const ConvGeom& g,
+                                                    bf16_t* __restrict__ y, float* __restrict__ stats,
+                                                    float* __restrict__ slab, int split, int tm, int m0, int n0,
+                                                    char* smem) {
+  constexpr int NT = 64 * WM * WN, TM = BM / WM, TN = BN / WN, NP = FN / 2;
+  static_assert(!(ADD && (SLAB || STATS)), "ADD: plain bf16 output only");
+  static_assert(FN % 2 == 0, "N fragments pair up");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = tid >> 6, wm = wid / WN, wn = wid % WN;
+  const int nl = wn * TN + 8 * (lane >> 4);  // + 32p: local channel of the lane's 8-run
+  float s1[NP][8], s2[NP][8];
+#pragma unroll
+  for (int q = 0; q < NP; ++q)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { s1[q][k] = 0.f; s2[q][k] = 0.f; }
+#pragma unroll
+  for (int a = 0; a < FM; ++a) {
+    const int m = m0 + wm * TM + a * 16 + (lane & 15);
+    const bool ok = m < g.M;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const int n = n0 + nl + 32 * q;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[j] = acc[a][2 * q][j]; v[4 + j] = acc[a][2 * q + 1][j]; }
+      if constexpr (ADD) {
+        if (ok) {
+          const uint4 ad = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(slab) + (int64_t)m * g.Cout + n);
+          v[0] += lo_bf16(ad.x); v[1] += hi_bf16(ad.x); v[2] += lo_bf16(ad.y); v[3] += hi_bf16(ad.y);
+          v[4] += lo_bf16(ad.z); v[5] += hi_bf16(ad.z); v[6] += lo_bf16(ad.w); v[7] += hi_bf16(ad.w);
+        }
+      }
+      if constexpr (SLAB) {
+        float* o = slab + ((int64_t)split * g.M + m) * g.Cout + n;
+        if (ok) {
+          *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+      } else {
+        const uint4 pk = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                                    pack_bf16x2(v[6], v[7]));
+        if (ok) *reinterpret_cast<uint4*>(y + (int64_t)m * g.Cout + n) = pk;
+        if constexpr (STATS) {
+          const float h[8] = {lo_bf16(pk.x), hi_bf16(pk.x), lo_bf16(pk.y), hi_bf16(pk.y),
+                              lo_bf16(pk.z), hi_bf16(pk.z), lo_bf16(pk.w), hi_bf16(pk.w)};
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {  // statistics of exactly what is stored
+            const float hv = ok ? h[k] : 0.f;
+            s1[q][k] += hv;
+            s2[q][k] += hv * hv;
+          }
+        }
+      }
+    }
+  }
+  if constexpr (STATS && !SLAB) {
+#pragma unroll
+    for (int q = 0; q < NP; ++q)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { s1[q][k] = row16_sum(s1[q][k]); s2[q][k] = row16_sum(s2[q][k]); }
+    __syncthreads();  // every wave done with the LDS ring and region
+    float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]
+    if ((lane & 15) == 15) {
+#pragma unroll
+      for (int q = 0; q < NP; ++q)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          red[(wm * 2 + 0) * BN + nl + 32 * q + k] = s1[q][k];
+          red[(wm * 2 + 1) * BN + nl + 32 * q + k] = s2[q][k];
+        }
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      float sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int q = 0; q < WM; ++q) { sa += red[(q * 2) * BN + c]; sb += red[(q * 2 + 1) * BN + c]; }
+      put_stats(stats, tm, g.Cout, n0 + c, sa, sb);
+    }
+  }
+}
+
+// B-tile chunk swizzle of the region kernel: conflict-free ds_read_b128 for
+// its permuted fragment rows 8(i>>2) + 4b + (i&3) (and for identity rows)
+__device__ __forceinline__ int swz_b(int row) { return ((row >> 1) ^ (row >> 3)) & 7; }
+
+// B fragment row of lane group i (0..15) for N fragment b of a transposed
+// (C^T) wave tile: fragment pair p = b/2 covers 32 channels, and lane group
+// i>>2 reads channels 8(i>>2) + 4(b&1) + (i&3), so the accumulator lane of
+// output row 4(l>>4)+r holds channel 32p + 8(l>>4) + 4(b&1) + r.
+__device__ __forceinline__ int b_frag_row(int b, int i) { return 32 * (b >> 1) + 8 * (i >> 2) + 4 * (b & 1) + (i & 3); }
+
 // --------------------------------------------------------------------------
 // forward / dgrad implicit GEMM, split-K capable
 //   C[m][n] = sum_{k in split} im2col(x)[m][k] * w[n][k]
@@ -280,7 +395,8 @@ __device__ __forceinline__ void conv_fwd_epilogue(const f32x4 (&acc)[BM / WM / 1
 // 256 threads = 4 waves (2 x 2), wave tile (BM/2) x (BN/2), BK = 64,
 // 3-stage LDS ring filled by LDS-DMA, one barrier per K step.
 // --------------------------------------------------------------------------
-template <int BM, int BN, bool STATS, bool SLAB, bool TAPU, int STAGES, int WM = 2, int WN = 2, bool ADD = false>
+template <int BM, int BN, bool STATS, bool SLAB, bool TAPU, int STAGES, int WM = 2, int WN = 2, bool ADD = false,
+          bool TRP = true>
 __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                        bf16_t* __restrict__ y, float* __restrict__ stats,
                                                        float* __restrict__ slab, const ConvGeom g, int splits,
@@ -297,6 +413,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   constexpr int A_INS = A_BYTES / 1024 / NW, B_INS = B_BYTES / 1024 / NW;  // glds per wave per stage
   constexpr int LPS = A_INS + B_INS;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  // transposed accumulators (16-byte epilogue stores) unless FN is odd (TRP = false: the old layout)
+  constexpr bool TR = TRP && FN % 2 == 0;
   static_assert(A_INS >= 1 && B_INS >= 1, "tile too small");
   static_assert(A_INS * NW * 1024 == A_BYTES && B_INS * NW * 1024 == B_BYTES, "DMA split");
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
@@ -337,7 +455,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
 #pragma unroll
   for (int j = 0; j < B_INS; ++j) {
     const int row = 8 * (wid * B_INS + j) + (lane >> 3);
-    const int ch = (lane & 7) ^ ((row >> 1) & 7);
+    const int ch = (lane & 7) ^ swz_b(row);
     b_k[j] = ch * 8;
     b_off[j] = (n0 + row) * g.K + ch * 8;
   }
@@ -426,8 +544,10 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
       for (int a = 0; a < FM; ++a)
         af[kk][a] = __builtin_bit_cast(bf16x8, As[swz_row<CPR>(wm * TM + a * 16 + (lane & 15), ch)]);
 #pragma unroll
-      for (int b = 0; b < FN; ++b)
-        bfr[kk][b] = __builtin_bit_cast(bf16x8, Bs[swz_row<CPR>(wn * TN + b * 16 + (lane & 15), ch)]);
+      for (int b = 0; b < FN; ++b) {
+        const int row = wn * TN + (TR ? b_frag_row(b, lane & 15) : b * 16 + (lane & 15));
+        bfr[kk][b] = __builtin_bit_cast(bf16x8, Bs[row * CPR + (ch ^ swz_b(row))]);
+      }
     }
     // the next stage's LDS-DMA issues ride between the MFMAs (their issue cost
     // overlaps matrix-core execution instead of serialising in front of it)
@@ -437,7 +557,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
       for (int a = 0; a < FM; ++a)
 #pragma unroll
         for (int b = 0; b < FN; ++b) {
-          acc[a][b] = mfma16(af[kk][a], bfr[kk][b], acc[a][b]);
+          acc[a][b] = TR ? mfma16(bfr[kk][b], af[kk][a], acc[a][b]) : mfma16(af[kk][a], bfr[kk][b], acc[a][b]);
           const int idx = (kk * FM + a) * FN + b;
           if (idx % IL == IL - 1 && idx / IL < LPS) {
             if (pf) issue_one(idx / IL, kt_n, slot_n, tnext);
@@ -466,7 +586,10 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
       d[0] = t_start; d[1] = t_setup; d[2] = t_loop; d[3] = stamp();
     }
   };
-  conv_fwd_epilogue<BM, BN, STATS, SLAB, WM, WN, ADD>(acc, g, y, stats, slab, split, tm, m0, n0, smem);
+  if constexpr (TR)
+    conv_fwd_epilogue_t<BM, BN, STATS, SLAB, WM, WN, FM, FN, ADD>(acc, g, y, stats, slab, split, tm, m0, n0, smem);
+  else
+    conv_fwd_epilogue<BM, BN, STATS, SLAB, WM, WN, ADD>(acc, g, y, stats, slab, split, tm, m0, n0, smem);
   dbg_out();
 }
 
@@ -499,101 +622,6 @@ struct RegionGeom {
   float inv_S, inv_RS, inv_IS;  // exact slot -> (img,row,col,chunk) decomposition (slots < 2^16)
 };
 
-// Inclusive sum over the 16 lanes of each DPP row: lane 15 of the row ends
-// with the row total (row_shr 1, 2, 4, 8 with zero fill; fixed order).
-__device__ __forceinline__ float row16_sum(float v) {
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x112, 0xf, 0xf, true));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x114, 0xf, 0xf, true));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x118, 0xf, 0xf, true));
-  return v;
-}
-
-// Epilogue of the region kernel.  Its MFMAs compute C^T (weights as the A
-// operand), so lane l holds, per 16-pixel M fragment a and N-fragment pair
-// p, the 8 CONSECUTIVE channels n0 + wn*TN + 32p + 8*(l>>4) + 0..7 of pixel
-// m0 + wm*TM + 16a + (l&15) (fragments 2p / 2p+1 hold channel quads 0..3 /
-// 4..7, see the B row map): one 16-byte bf16 store (or two 16-byte fp32
-// slab stores) per (a, p) instead of 8 scattered 2-byte stores.  BN
-// statistics: DPP row sums over the 16 pixels of a lane group, then a
-// fixed-order sum over the WM wave rows through LDS (deterministic).
-template <int BN, bool STATS, bool SLAB, int WM, int WN, int FM, int FN>
-__device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], const ConvGeom& g,
-                                                    bf16_t* __restrict__ y, float* __restrict__ stats,
-                                                    float* __restrict__ slab, int split, int tm, int m0, int n0,
-                                                    char* smem) {
-  constexpr int NT = 64 * WM * WN, TM = 128 / WM, TN = BN / WN, NP = FN / 2;
-  static_assert(FN % 2 == 0, "N fragments pair up");
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = tid >> 6, wm = wid / WN, wn = wid % WN;
-  const int nl = wn * TN + 8 * (lane >> 4);  // + 32p: local channel of the lane's 8-run
-  float s1[NP][8], s2[NP][8];
-#pragma unroll
-  for (int q = 0; q < NP; ++q)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { s1[q][k] = 0.f; s2[q][k] = 0.f; }
-#pragma unroll
-  for (int a = 0; a < FM; ++a) {
-    const int m = m0 + wm * TM + a * 16 + (lane & 15);
-    const bool ok = m < g.M;
-#pragma unroll
-    for (int q = 0; q < NP; ++q) {
-      const int n = n0 + nl + 32 * q;
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { v[j] = acc[a][2 * q][j]; v[4 + j] = acc[a][2 * q + 1][j]; }
-      if constexpr (SLAB) {
-        float* o = slab + ((int64_t)split * g.M + m) * g.Cout + n;
-        if (ok) {
-          *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
-          *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
-        }
-      } else {
-        const uint4 pk = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
-                                    pack_bf16x2(v[6], v[7]));
-        if (ok) *reinterpret_cast<uint4*>(y + (int64_t)m * g.Cout + n) = pk;
-        if constexpr (STATS) {
-          const float h[8] = {lo_bf16(pk.x), hi_bf16(pk.x), lo_bf16(pk.y), hi_bf16(pk.y),
-                              lo_bf16(pk.z), hi_bf16(pk.z), lo_bf16(pk.w), hi_bf16(pk.w)};
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {  // statistics of exactly what is stored
-            const float hv = ok ? h[k] : 0.f;
-            s1[q][k] += hv;
-            s2[q][k] += hv * hv;
-          }
-        }
-      }
-    }
-  }
-  if constexpr (STATS && !SLAB) {
-#pragma unroll
-    for (int q = 0; q < NP; ++q)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) { s1[q][k] = row16_sum(s1[q][k]); s2[q][k] = row16_sum(s2[q][k]); }
-    __syncthreads();  // every wave done with the LDS ring and region
-    float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]
-    if ((lane & 15) == 15) {
-#pragma unroll
-      for (int q = 0; q < NP; ++q)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          red[(wm * 2 + 0) * BN + nl + 32 * q + k] = s1[q][k];
-          red[(wm * 2 + 1) * BN + nl + 32 * q + k] = s2[q][k];
-        }
-    }
-    __syncthreads();
-    for (int c = tid; c < BN; c += NT) {
-      float sa = 0.f, sb = 0.f;
-#pragma unroll
-      for (int q = 0; q < WM; ++q) { sa += red[(q * 2) * BN + c]; sb += red[(q * 2 + 1) * BN + c]; }
-      put_stats(stats, tm, g.Cout, n0 + c, sa, sb);
-    }
-  }
-}
-
-// B-tile chunk swizzle of the region kernel: conflict-free ds_read_b128 for
-// its permuted fragment rows 8(i>>2) + 4b + (i&3) (and for identity rows)
-__device__ __forceinline__ int swz_b(int row) { return ((row >> 1) ^ (row >> 3)) & 7; }
 
 template <int BN, bool STATS, bool SLAB, int STAGES, int WM, int WN>
 __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf16_t* __restrict__ x,
@@ -797,7 +825,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf1
   }
   if (i < nk) step(fa0, fb0, fa1, fb1);
   const unsigned long long t_loop = dbg ? stamp() : 0ull;
-  conv_fwd_epilogue_t<BN, STATS, SLAB, WM, WN, FM, FN>(acc, g, y, stats, slab, split, tm, m0, n0, smem);
+  conv_fwd_epilogue_t<128, BN, STATS, SLAB, WM, WN, FM, FN>(acc, g, y, stats, slab, split, tm, m0, n0, smem);
   if (dbg && threadIdx.x == 0) {
     unsigned long long* d = dbg + (size_t)blockIdx.x * 5;
     d[0] = t_start; d[1] = t_issued; d[2] = t_first; d[3] = t_loop; d[4] = stamp();
@@ -885,7 +913,7 @@ __global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restri
 #pragma unroll
       for (int b = 0; b < FN; ++b) acc[a][b] = mfma16(fb[b], fa[a], acc[a][b]);
   }
-  conv_fwd_epilogue_t<BN, STATS, false, WM, WN, FM, FN>(acc, g, y, stats, nullptr, 0, tm, m0, n0, smem);
+  conv_fwd_epilogue_t<128, BN, STATS, false, WM, WN, FM, FN>(acc, g, y, stats, nullptr, 0, tm, m0, n0, smem);
 }
 
 // split-K combine: y = bf16(sum_s slab[s]) (+ BN partial sums, one row per block)
@@ -1179,7 +1207,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
 // [Cout][taps][C] (C <= Cp: drops zero-padded input channels).  TPO lanes
 // share one output (each sums a strided subset of the splits, then a
 // fixed-order shuffle reduction): enough parallelism for 64-way slabs.
-template <int TPO>
+// ACC: dst += sum (gradient accumulation semantics) instead of dst = sum.
+template <int TPO, bool ACC = false>
 __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slabs, float* __restrict__ dst,
                                                           int splits, int Cout, int taps, int Cp, int C) {
   const int64_t total = (int64_t)Cout * taps * C;
@@ -1194,7 +1223,7 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restric
     for (int sp = sub; sp < splits; sp += TPO) s += slabs[sp * slab + src];
 #pragma unroll
     for (int o = TPO / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (sub == 0) dst[i] = s;
+    if (sub == 0) dst[i] = ACC ? dst[i] + s : s;
   }
 }
 
@@ -1501,6 +1530,7 @@ static int combine_rows_per_block(int M, int N) {
 
 // number of BN partial-sum rows conv_fwd writes for this configuration
 int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile, int splits) {
+  tile &= 15;
   ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
   if (splits <= 1) return (g.M + fwd_bm(tile) - 1) / fwd_bm(tile);
   const int rpb = combine_rows_per_block(g.M, Cout);
@@ -1533,6 +1563,26 @@ static void launch_fwd_w(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t 
 }
 
 static int g_fwd_waves = 8;
+static int g_fwd_stages = 3, g_wgrad_stages = 0;  // tuning knobs (set_conv_stages); wgrad 0 = per-tile default
+
+// Per-call streaming-kernel configuration packed into the tile id:
+// bits 0-3 tile, bits 4-7 LDS ring stages (0 = the global default), bits 8-11
+// waves per workgroup (0 = default).  The ResNet-50 1x1 GEMMs pick 2 stages
+// (96 -> 64 KiB of LDS: two workgroups per CU, which is what the short-K
+// GEMMs need -- scripts/bench_gemm1x1.py SWEEP=1, ops/conv.py _plan_1x1),
+// while the CIFAR layers keep the tuned global default.
+struct FwdCfg {
+  int saved_st, saved_wv;
+  explicit FwdCfg(int& tile) : saved_st(g_fwd_stages), saved_wv(g_fwd_waves) {
+    const int st = (tile >> 4) & 15, wv = (tile >> 8) & 15;
+    tile &= 15;
+    if (st && (st < 2 || st > 4)) throw std::runtime_error("conv_fwd: packed stages must be 2..4");
+    if (wv && wv != 4 && wv != 8) throw std::runtime_error("conv_fwd: packed waves must be 4 or 8");
+    if (st) g_fwd_stages = st;
+    if (wv) g_fwd_waves = wv;
+  }
+  ~FwdCfg() { g_fwd_stages = saved_st; g_fwd_waves = saved_wv; }
+};
 
 template <int BM, int BN, bool TAPU, int ST>
 static void launch_fwd_t(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
@@ -1553,8 +1603,6 @@ void set_conv_waves(int waves) {
 
 static int g_wgrad_pf = -1;  // wgrad fragment prefetch: -1 = by stage count, 0 off, 1 on
 void set_conv_wgrad_pf(int pf) { g_wgrad_pf = pf; }
-static int g_fwd_stages = 3, g_wgrad_stages = 0;  // tuning knobs (set_conv_stages); wgrad 0 = per-tile default
-
 void set_conv_debug(uintptr_t buf) { g_conv_dbg = (unsigned long long*)buf; }
 
 void set_conv_stages(int fwd, int wgrad) {
@@ -1694,6 +1742,7 @@ static void launch_fwd_region(const ConvGeom& g, const RegionGeom& rg, uintptr_t
 // Returns the number of BN partial rows written to `stats` (if non-null).
 int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab, int B, int H, int W, int Cin,
              int Cout, int KS, int tile, int splits, uintptr_t stream) {
+  const FwdCfg cfg(tile);
   ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
   hipStream_t s = as_stream(stream);
   if (splits < 1) splits = 1;
@@ -1746,6 +1795,7 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
 // (KS = 1 or the region kernels disabled for the shape), no split-K / stats.
 void conv_fwd_add(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t addend, int B, int H, int W, int Cin, int Cout,
                   int KS, int tile, uintptr_t stream) {
+  const FwdCfg cfg(tile);
   ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
   hipStream_t s = as_stream(stream);
   if (!addend) throw std::runtime_error("conv_fwd_add: null addend");
@@ -1840,22 +1890,34 @@ void set_reduce_atomic_conv(int on) {
   DL_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_red_atomic), &v, sizeof(int)));
 }
 
-void slab_reduce(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream) {
+template <bool ACC>
+static void slab_reduce_t(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C,
+                          uintptr_t stream) {
   const int64_t total = (int64_t)Cout * taps * C;
   auto s = as_stream(stream);
   if (splits >= 32) {
     int64_t g = (total * 32 + 255) / 256;
-    slab_reduce_kernel<32><<<(int)std::min<int64_t>(g, 4096), 256, 0, s>>>((const float*)slabs, (float*)dst, splits,
-                                                                          Cout, taps, Cp, C);
+    slab_reduce_kernel<32, ACC><<<(int)std::min<int64_t>(g, 4096), 256, 0, s>>>((const float*)slabs, (float*)dst,
+                                                                               splits, Cout, taps, Cp, C);
   } else if (splits >= 8) {
     int64_t g = (total * 8 + 255) / 256;
-    slab_reduce_kernel<8><<<(int)std::min<int64_t>(g, 4096), 256, 0, s>>>((const float*)slabs, (float*)dst, splits,
-                                                                         Cout, taps, Cp, C);
+    slab_reduce_kernel<8, ACC><<<(int)std::min<int64_t>(g, 4096), 256, 0, s>>>((const float*)slabs, (float*)dst,
+                                                                              splits, Cout, taps, Cp, C);
   } else {
-    slab_reduce_kernel<1><<<stream_grid(total), 256, 0, s>>>((const float*)slabs, (float*)dst, splits, Cout, taps,
-                                                             Cp, C);
+    slab_reduce_kernel<1, ACC><<<stream_grid(total), 256, 0, s>>>((const float*)slabs, (float*)dst, splits, Cout,
+                                                                  taps, Cp, C);
   }
   DL_HIP_CHECK(hipGetLastError());
+}
+
+void slab_reduce(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream) {
+  slab_reduce_t<false>(slabs, dst, splits, Cout, taps, Cp, C, stream);
+}
+
+// dst += sum of the slabs (the ResNet-50 1x1 weight gradients: plain slab
+// stores + this reduce beat the atomic split-K 1.3-2.3x, profiles/r2_gemm1x1_wgrad_slab.jsonl)
+void slab_reduce_add(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream) {
+  slab_reduce_t<true>(slabs, dst, splits, Cout, taps, Cp, C, stream);
 }
 
 void weight_flip_transpose(uintptr_t w, uintptr_t wt, int Cout, int Cin, int KS, uintptr_t stream) {

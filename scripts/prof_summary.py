@@ -1,6 +1,8 @@
 """Summarise a rocprofv3 kernel-trace database (.db) or kernel_stats csv:
 per-kernel calls / total / mean time, sorted by total.  Usage:
-    python scripts/prof_summary.py <dir-or-db> [--steps N] [--top K]"""
+    python scripts/prof_summary.py <dir-or-db> [--steps N] [--top K] [--last-ms T]
+--last-ms keeps only the kernels that started in the last T ms of the trace
+(e.g. the timed steps after a warm-up that ran MIOpen's solver search)."""
 import glob
 import os
 import sqlite3
@@ -11,11 +13,16 @@ def main():
     path = sys.argv[1]
     steps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else None
     top = int(sys.argv[sys.argv.index("--top") + 1]) if "--top" in sys.argv else 40
+    last = float(sys.argv[sys.argv.index("--last-ms") + 1]) if "--last-ms" in sys.argv else None
     dbs = [path] if path.endswith(".db") else glob.glob(os.path.join(path, "**", "*.db"), recursive=True)
     rows = {}
     for db in dbs:
         c = sqlite3.connect(db)
-        for name, dur in c.execute("select name, duration from kernels"):
+        q = "select name, duration from kernels"
+        if last is not None:
+            end = c.execute("select max(end) from kernels").fetchone()[0]
+            q += f" where start >= {int(end - last * 1e6)}"
+        for name, dur in c.execute(q):
             r = rows.setdefault(name, [0, 0])
             r[0] += 1
             r[1] += dur

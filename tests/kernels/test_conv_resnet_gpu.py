@@ -1,7 +1,7 @@
 """ResNet-50 convolutions on the shadow weights (ops/conv.py) against fp32
 PyTorch references of the same ops: the stride-1 1x1 convolutions on the
 hand-written MFMA kernels (forward, dgrad, fp32 wgrad written into the flat
-gradient, with and without split-K atomics), the MIOpen path for the rest,
+gradient: split-K slabs reduce-added onto it), the MIOpen path for the rest,
 and a whole ResNet-50 step with the convolutions bound to the flat buffers
 against the unbound model."""
 import pytest
@@ -42,8 +42,8 @@ def test_conv1x1_matches_fp32(dev, shape):
     w16 = w.to(torch.bfloat16)
     go = torch.randn(N, cout, H, H, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
     assert conv1x1_supported(x, cout)
-    g32 = torch.full((cout, cin), float("nan"), device=dev)
-    g32.zero_()  # the trainer zeroes the flat gradient at step start
+    prior = torch.randn(cout, cin, device=dev, generator=g)
+    g32 = prior.clone()  # the weight gradient is ADDED to what the flat gradient holds
     ready = []
     bind = ShadowBinding(w16.view(cout, cin), g32, lambda: ready.append(1))
     xi = x.detach().requires_grad_(True)
@@ -58,7 +58,7 @@ def test_conv1x1_matches_fp32(dev, shape):
     assert y.is_contiguous(memory_format=cl) and y.dtype == torch.bfloat16
     assert _rel(y, yr) < 1e-2
     assert _rel(xi.grad, xr.grad) < 1e-2
-    assert _rel(g32, wr.grad.view(cout, cin)) < 1e-3
+    assert _rel(g32 - prior, wr.grad.view(cout, cin)) < 1e-3
     assert wp.grad is None and ready == [1]
 
 

@@ -74,11 +74,11 @@ class _BN(nn.Module):
 _CONV_MODE = os.environ.get("DISTLEARN_RESNET_CONV", "hip")
 # BatchNorm statistics from the 1x1 GEMM epilogue (skips the BN statistics pass)
 _FUSE_STATS = os.environ.get("DISTLEARN_RESNET_FUSE_STATS", "1") == "1"
-# residual gradient added in the c1 dgrad epilogue (ops/conv.py conv_fwd_add).  Off:
-# measured slower -- the epilogue's per-element 2-byte addend loads made the dgrad
-# 308 us instead of 74 us (12 calls/step, +2.7 ms) while the separate bf16 add it
-# replaces costs 94 us (profiles/r2_resnet50_kernels_fuse_res.txt)
-_FUSE_RES = os.environ.get("DISTLEARN_RESNET_FUSE_RES", "0") == "1"
+# residual gradient added in the c1 dgrad epilogue (ops/conv.py conv_fwd_add).  With
+# the first epilogue (per-element 2-byte addend loads) the dgrad took 308 us instead
+# of 74 us (profiles/r2_resnet50_kernels_fuse_res.txt); the transposed epilogue loads
+# the addend 16 bytes at a time and the fusion now wins: 30.33 -> 29.68 ms/step.
+_FUSE_RES = os.environ.get("DISTLEARN_RESNET_FUSE_RES", "1") == "1"
 # stem max-pool on the HIP gather-backward kernels (ops/pool.py)
 _POOL_HIP = os.environ.get("DISTLEARN_RESNET_POOL", "hip") == "hip"
 

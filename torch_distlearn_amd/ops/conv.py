@@ -16,8 +16,8 @@ fused SGD kernel already keeps a bf16 shadow of every parameter
   from its epilogue + a T x 2C column reduce, instead of the BatchNorm's own
   pass over the M x C output), dgrad
   ``dx = dy W`` (same kernel on the transposed shadow) and wgrad
-  ``dW = dy^T x`` written in fp32 into the flat gradient (split-K partials
-  atomically added when the weight is too small to fill the chip).
+  ``dW = dy^T x`` in fp32 (split-K partial slabs, reduced and added into the
+  flat gradient by one kernel).
 * :class:`ShadowConv` -- every other convolution (3x3, strided, the 7x7 stem)
   stays on MIOpen but reads the shadow and adds its weight gradient into the
   flat buffer (one cast-add instead of three elementwise kernels).
@@ -56,6 +56,21 @@ def _fwd_plan(M: int, N: int, K: int):
     return plan(M, N, K)
 
 
+def _plan_1x1(M: int, N: int, K: int):
+    """(packed tile id, splits) of an M x K x N 1x1-conv GEMM.  Measured on the
+    ResNet-50 shapes (profiles/r2_gemm1x1_sweep.jsonl, scripts/bench_gemm1x1.py
+    SWEEP=1): a 2-stage LDS ring (two workgroups per CU) beats the 3-stage
+    default by up to 1.5x on the short-K GEMMs, and 4-wave workgroups win when
+    K <= 128; only the N = 64, K >= 256 GEMMs keep 3 stages."""
+    tile, splits = _fwd_plan(M, N, K)
+    if splits > 1:
+        return tile, splits
+    tile = 0 if N % 128 == 0 else 2
+    stages = 3 if (N == 64 and K >= 256) else 2
+    waves = 4 if K <= 128 else 8
+    return tile | (stages << 4) | (waves << 8), 1
+
+
 def _wgrad_plan(cout: int, K: int, M: int):
     from ..models.cifar_hip import _wgrad_plan as plan
 
@@ -82,7 +97,7 @@ class Conv1x1(torch.autograd.Function):
         cout = weight.shape[0]
         M = N * H * W
         y = torch.empty((N, cout, H, W), dtype=BF16, device=x.device, memory_format=torch.channels_last)
-        tile, splits = _fwd_plan(M, cout, cin)
+        tile, splits = _plan_1x1(M, cout, cin)
         slab = torch.empty(splits * M * cout, device=x.device) if splits > 1 else None
         s = stream_handle()
         rows = None
@@ -123,7 +138,7 @@ class Conv1x1(torch.autograd.Function):
             wt = torch.empty(cin, cout, dtype=BF16, device=x.device)
             C.weight_flip_transpose(bind.w16.data_ptr(), wt.data_ptr(), cout, cin, 1, s)
             dx = torch.empty_like(x, memory_format=torch.channels_last)
-            tile, splits = _fwd_plan(M, cin, cout)
+            tile, splits = _plan_1x1(M, cin, cout)
             if add is not None and splits == 1:
                 C.conv_fwd_add(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), add.data_ptr(), M, 1, 1, cout, cin, 1,
                                tile, s)
@@ -136,10 +151,14 @@ class Conv1x1(torch.autograd.Function):
                 dx.add_(add)
         elif add is not None:
             dx = add
-        # fp32 weight gradient straight into the flat buffer (zeroed at step start)
+        # fp32 weight gradient added into the flat buffer: split-K partials in plain
+        # slabs + one reduce-add (atomic split-K adds were 1.3-2.3x slower on every
+        # ResNet-50 shape: device-scope fp32 atomics from all 8 XCDs contend,
+        # profiles/r2_gemm1x1_wgrad_slab.jsonl)
         tile, splits = _wgrad_plan(cout, cin, M)
-        C.conv_wgrad(dy.data_ptr(), x.data_ptr(), bind.g32.data_ptr(), M, 1, 1, cin, cout, 1, splits, cin, tile,
-                     cin if splits > 1 else 0, s)
+        ws = torch.empty(splits * cout * cin, device=x.device)
+        C.conv_wgrad(dy.data_ptr(), x.data_ptr(), ws.data_ptr(), M, 1, 1, cin, cout, 1, splits, cin, tile, 0, s)
+        C.slab_reduce_add(ws.data_ptr(), bind.g32.data_ptr(), splits, cout, 1, cin, cin, s)
         bind.ready()
         return dx, None, None, None, None
 
