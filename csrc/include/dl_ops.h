@@ -52,6 +52,7 @@ void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, i
 void set_reduce_atomic_conv(int on);
 void conv_fwd_add(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t addend, int B, int H, int W, int Cin, int Cout,
                   int KS, int tile, uintptr_t stream);
+void set_conv_fwd_tr(int on);
 void slab_reduce(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream);
 void slab_reduce_add(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream);
 void weight_flip_transpose(uintptr_t w, uintptr_t wt, int Cout, int Cin, int KS, uintptr_t stream);

@@ -1538,6 +1538,10 @@ int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile,
 }
 
 static uintptr_t g_fwd_addend = 0;  // conv_fwd_add: bf16 [M][Cout] added in the epilogue
+// A/B knob: 0 = the untransposed accumulator layout for the split-K and BN-statistics
+// instances of the streaming kernel (set_conv_fwd_tr)
+static int g_fwd_tr = 1;
+void set_conv_fwd_tr(int on) { g_fwd_tr = on ? 1 : 0; }
 
 template <int BM, int BN, bool TAPU, int ST, int WM, int WN>
 static void launch_fwd_w(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
@@ -1551,9 +1555,15 @@ static void launch_fwd_w(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t 
   if (g_fwd_addend)
     conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, true><<<grid, NT, 0, s>>>(
         (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, (float*)g_fwd_addend, g, 1, ktps, g_conv_dbg);
+  else if (splits > 1 && !g_fwd_tr)
+    conv_fwd_kernel<BM, BN, false, true, TAPU, ST, WM, WN, false, false><<<grid, NT, 0, s>>>(
+        (const bf16_t*)x, (const bf16_t*)w, nullptr, nullptr, (float*)slab, g, splits, ktps, g_conv_dbg);
   else if (splits > 1)
     conv_fwd_kernel<BM, BN, false, true, TAPU, ST, WM, WN><<<grid, NT, 0, s>>>(
         (const bf16_t*)x, (const bf16_t*)w, nullptr, nullptr, (float*)slab, g, splits, ktps, g_conv_dbg);
+  else if (stats && !g_fwd_tr)
+    conv_fwd_kernel<BM, BN, true, false, TAPU, ST, WM, WN, false, false><<<grid, NT, 0, s>>>(
+        (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)stats, nullptr, g, 1, ktps, g_conv_dbg);
   else if (stats)
     conv_fwd_kernel<BM, BN, true, false, TAPU, ST, WM, WN><<<grid, NT, 0, s>>>(
         (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)stats, nullptr, g, 1, ktps, g_conv_dbg);

@@ -53,6 +53,58 @@ def test_resnet50_train_step():
     tr.finish()
 
 
+def test_resnet50_graph_matches_eager():
+    """VERDICT r1 item 3b as a test (scripts/diag_r50_graph.py at test size):
+    from the same state and batch, one step eager and one replayed from a
+    captured hipGraph agree on the loss, and their gradients are as close to
+    an fp32 autograd reference as each other (the only graph-vs-eager
+    difference allowed is bf16 algorithm-selection noise)."""
+    import os
+
+    from torch_distlearn_amd import FlatParams, Tree
+    from torch_distlearn_amd.engine import DataParallelTrainer
+    from torch_distlearn_amd.models import ResNet50
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dev = torch.device("cuda", 0)
+    tree = Tree(1, 1, host="127.0.0.1", port=29573, device=dev)
+    B = 8
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(B, 64, 64, 3, device=dev, generator=g).to(torch.bfloat16)
+    y = torch.randint(0, 100, (B,), device=dev, generator=g)
+    out = {}
+    for mode in ("eager", "graph"):
+        model = ResNet50(num_classes=100, seed=0).to(dev)
+        tr = DataParallelTrainer(model, tree, lr=0.02, backend="torch", compute_dtype=torch.bfloat16,
+                                 graph=mode == "graph", max_batch=B)
+        tr.synchronize_parameters()
+        p0 = tr.flat.data.clone()
+        loss = float(tr.step(x, y))
+        torch.cuda.synchronize()
+        out[mode] = (loss, tr.flat.grad.clone(), tr.flat.data - p0)
+        if mode == "graph":
+            assert tr.captures >= 1
+        tr.finish()
+    ref = ResNet50(num_classes=100, seed=0).to(dev)
+    L = ref.loss(ref(x.float(), compute_dtype=torch.float32), y)
+    L.backward()
+    fr = FlatParams(ref, grads=False)
+    gref = torch.zeros_like(out["eager"][1])
+    for t, o, n in zip(fr.leaves, fr.offsets, fr.numels):
+        gref[o:o + n] = t.grad.reshape(-1)
+    H = 64
+    (le, ge, de), (lg, gg, dg) = out["eager"], out["graph"]
+
+    def rel(a, b):
+        return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
+
+    lr32 = float(L.detach())
+    assert abs(lg - le) < 1e-2 * abs(le) and abs(le - lr32) < 2e-2 * abs(lr32), (le, lg, lr32)
+    e_ref, g_ref = rel(ge[H:], gref[H:]), rel(gg[H:], gref[H:])
+    assert e_ref < 0.1 and g_ref < 1.5 * e_ref + 1e-3, (e_ref, g_ref)
+    assert rel(dg, de) < 0.1
+
+
 @pytest.mark.parametrize("c,hw,relu,res", [(64, 28, True, False), (256, 14, True, True), (128, 7, False, False),
                                            (2048, 7, True, True), (512, 7, False, True)])
 def test_bn_act_hip_matches_fp32(c, hw, relu, res):

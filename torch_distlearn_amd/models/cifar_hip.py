@@ -138,9 +138,15 @@ class CifarHIPExecutor:
         comm = getattr(bucketer, "comm", None)
         overlapped = comm is not None and getattr(comm, "world_size", 1) > 1
         self.dgrad_stages = int(os.environ.get("DISTLEARN_DGRAD_STAGES", "2" if overlapped else "3"))
+        # streaming-kernel forward configuration packed into the tile id (csrc conv_fwd
+        # FwdCfg: bits 4-7 ring stages, 8-11 waves; 0 = the global default)
+        self.fwd_cfg = (int(os.environ.get("DISTLEARN_FWD_STAGES", "0")) << 4) | (
+            int(os.environ.get("DISTLEARN_FWD_WAVES", "0")) << 8)
         # CUs held by the concurrent collective's workgroups (wgrad grids leave them free)
         self.cu_reserve = int(os.environ.get("DISTLEARN_CU_RESERVE",
                                              getattr(comm, "cu_reserve", 0) if overlapped else 0))
+        if "DISTLEARN_FWD_TR" in os.environ:  # A/B: transposed-accumulator streaming kernel (1) or not (0)
+            self.C.set_conv_fwd_tr(int(os.environ["DISTLEARN_FWD_TR"]))
         if "DISTLEARN_WGRAD_PF" in os.environ:  # tuning: wgrad fragment prefetch (-1 auto, 0, 1)
             self.C.set_conv_wgrad_pf(int(os.environ["DISTLEARN_WGRAD_PF"]))
         # fuse the last block's BN/ReLU/pool into the head kernel (2048 pooled features)
@@ -314,7 +320,7 @@ class CifarHIPExecutor:
             t, sp = self.fwd_plan[i]
             ntm = C.conv_fwd(inp.data_ptr(), w.data_ptr(), self.y[i].data_ptr(),
                              self.stats[i].data_ptr() if train else 0, self.slabs.data_ptr(), B, h, h, cin, cout, KSIZE,
-                             t, sp, s)
+                             t | self.fwd_cfg, sp, s)
             fused = train and self.atomic  # coefficients derived by the consumer kernel
             if not fused:
                 C.bn_finalize(self.stats[i].data_ptr(), ntm, cout, M, self.p32[self._leaf(i, 2)].data_ptr(),
