@@ -46,6 +46,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("slab_reduce", &slab_reduce);
   m.def("slab_reduce_add", &slab_reduce_add);
   m.def("weight_flip_transpose", &weight_flip_transpose);
+  m.def("transpose_many", &transpose_many);
+  m.def("transpose_entry_bytes", &transpose_entry_bytes);
+  m.def("weights_to_cl", &weights_to_cl);
+  m.def("cl_entry_bytes", &cl_entry_bytes);
   m.def("pack_weight", &pack_weight);
   m.def("pad_channels", &pad_channels);
   m.def("prep_step", &prep_step);

@@ -1252,6 +1252,58 @@ __global__ void __launch_bounds__(256) weight_flip_transpose_kernel(const bf16_t
 }
 
 // fp32 [Cout][taps][C] -> bf16 [Cout][taps][Cp] (zero channels C..Cp-1)
+// Many [rows][cols] bf16 matrices transposed in ONE launch (the ResNet-50 1x1
+// weights for their dgrads, once per step: 33 weight_flip_transpose launches
+// of ~5 us each before).  Entries sorted by tile0; 64x64 tiles.
+struct TrEntry {
+  int64_t src, dst;
+  int rows, cols, tile0, tiles_c;
+};
+
+__global__ void __launch_bounds__(256) transpose_many_kernel(const TrEntry* __restrict__ tab, int n) {
+  __shared__ bf16_t t[64][65];
+  const int b = blockIdx.x;
+  int e = 0;
+  for (int i = 1; i < n; ++i)
+    if (tab[i].tile0 <= b) e = i;
+  const TrEntry en = tab[e];
+  const bf16_t* __restrict__ src = reinterpret_cast<const bf16_t*>(en.src);
+  bf16_t* __restrict__ dst = reinterpret_cast<bf16_t*>(en.dst);
+  const int local = b - en.tile0;
+  const int r0 = (local / en.tiles_c) * 64, c0 = (local % en.tiles_c) * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4)
+    t[r][tx] = (r0 + r < en.rows && c0 + tx < en.cols) ? src[(int64_t)(r0 + r) * en.cols + c0 + tx] : (bf16_t)0;
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int c = c0 + r, rr = r0 + tx;
+    if (c < en.cols && rr < en.rows) dst[(int64_t)c * en.rows + rr] = t[tx][r];
+  }
+}
+
+// Many conv weights [Cout][Cin][KK] -> channels-last [Cout][KK][Cin] in ONE
+// launch (the ResNet-50 MIOpen convolutions read channels-last weights: torch
+// converted each one on every call, 34 copy kernels per step).
+// blockIdx.y = entry, grid-stride over that entry's elements in dst order.
+struct ClEntry {
+  int64_t src, dst;
+  int cout, cin, kk, pad;
+};
+
+__global__ void __launch_bounds__(256) weights_to_cl_kernel(const ClEntry* __restrict__ tab) {
+  const ClEntry en = tab[blockIdx.y];
+  const bf16_t* __restrict__ src = reinterpret_cast<const bf16_t*>(en.src);
+  bf16_t* __restrict__ dst = reinterpret_cast<bf16_t*>(en.dst);
+  const int64_t total = (int64_t)en.cout * en.kk * en.cin;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < total; j += (int64_t)gridDim.x * blockDim.x) {
+    const int ci = (int)(j % en.cin);
+    const int64_t r = j / en.cin;  // co * kk + t
+    const int t = (int)(r % en.kk);
+    const int64_t co = r / en.kk;
+    dst[j] = src[(co * en.cin + ci) * en.kk + t];
+  }
+}
+
 __global__ void __launch_bounds__(256) pack_weight_kernel(const float* __restrict__ w, bf16_t* __restrict__ wp,
                                                           int Cout, int taps, int C, int Cp) {
   const int64_t total = (int64_t)Cout * taps * Cp;
@@ -1935,6 +1987,25 @@ void weight_flip_transpose(uintptr_t w, uintptr_t wt, int Cout, int Cin, int KS,
   weight_flip_transpose_kernel<<<grid, 256, 0, as_stream(stream)>>>((const bf16_t*)w, (bf16_t*)wt, Cout, Cin, KS);
   DL_HIP_CHECK(hipGetLastError());
 }
+
+// table_dev: n TrEntry on the device (32 bytes each; built once by the caller,
+// ops/conv.py WeightTransposes, and reused by every step / graph replay).
+void transpose_many(uintptr_t table_dev, int n, int total_tiles, uintptr_t stream) {
+  if (n <= 0) return;
+  if (total_tiles <= 0) throw std::runtime_error("transpose_many: no tiles");
+  transpose_many_kernel<<<total_tiles, 256, 0, as_stream(stream)>>>((const TrEntry*)table_dev, n);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+int transpose_entry_bytes() { return (int)sizeof(TrEntry); }
+
+void weights_to_cl(uintptr_t table_dev, int n, uintptr_t stream) {
+  if (n <= 0) return;
+  weights_to_cl_kernel<<<dim3(256, n), 256, 0, as_stream(stream)>>>((const ClEntry*)table_dev);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+int cl_entry_bytes() { return (int)sizeof(ClEntry); }
 
 void pack_weight(uintptr_t w, uintptr_t wp, int Cout, int taps, int C, int Cp, uintptr_t stream) {
   const int64_t total = (int64_t)Cout * taps * Cp;

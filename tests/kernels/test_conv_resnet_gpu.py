@@ -158,3 +158,38 @@ def test_maxpool_nhwc_matches_torch(dev, shape):
     torch.cuda.synchronize()
     assert torch.equal(ya, yb)
     torch.testing.assert_close(xa.grad.float(), xb.grad.float(), rtol=1e-2, atol=1e-2)
+
+
+def test_weight_transposes_one_launch(dev):
+    """ops.conv.WeightTransposes: many [Cout][Cin] shadows transposed by one
+    transpose_many launch (ragged shapes, tails of the 64x64 tiles)."""
+    from torch_distlearn_amd.ops.conv import ShadowBinding, WeightTransposes
+
+    shapes = [(64, 64), (256, 64), (64, 256), (2048, 512), (96, 40), (8, 200)]
+    ws = [torch.randn(co, ci, 1, 1, device=dev).to(torch.bfloat16) for co, ci in shapes]
+    binds = [ShadowBinding(w, torch.zeros(w.shape, device=dev), lambda: None) for w in ws]
+    wt = WeightTransposes(binds)
+    wt.refresh()
+    torch.cuda.synchronize()
+    for w, b in zip(ws, binds):
+        assert torch.equal(b.wt, w.view(w.shape[0], -1).t())
+    ws[3].mul_(2)  # the shadow changes (optimizer step): the next refresh follows
+    wt.refresh()
+    torch.cuda.synchronize()
+    assert torch.equal(binds[3].wt, ws[3].view(2048, 512).t())
+
+
+def test_channels_last_weights_one_launch(dev):
+    """ops.conv.ChannelsLastWeights: KxK shadows copied to channels-last by one
+    weights_to_cl launch equal torch's own channels-last conversion."""
+    from torch_distlearn_amd.ops.conv import ChannelsLastWeights, ShadowBinding
+
+    shapes = [(64, 3, 7, 7), (64, 64, 3, 3), (512, 512, 3, 3), (24, 40, 3, 3)]
+    ws = [torch.randn(s, device=dev).to(torch.bfloat16) for s in shapes]
+    binds = [ShadowBinding(w, torch.zeros(w.shape, device=dev), lambda: None) for w in ws]
+    cl = ChannelsLastWeights(binds, shapes)
+    cl.refresh()
+    torch.cuda.synchronize()
+    for w, b in zip(ws, binds):
+        assert b.wcl.is_contiguous(memory_format=torch.channels_last)
+        assert torch.equal(b.wcl, w)

@@ -36,6 +36,7 @@ class _BN(nn.Module):
         self.register_buffer("running_mean", torch.zeros(c))
         self.register_buffer("running_var", torch.ones(c))
         self.bind = None  # (weight grad view, bias grad view, ready) -- ResNet50.attach_flat
+        self.acc = None  # this step's zeroed fp32 [4C] slice of the model's statistics arena
 
     def forward(self, x):
         if _BN_MODE == "mixed" and x.is_cuda:
@@ -53,14 +54,17 @@ class _BN(nn.Module):
         return supported(x) and self.weight.dtype == torch.float32 and (
             residual is None or (residual.dtype == x.dtype and residual.shape == x.shape))
 
-    def act(self, x, relu: bool = True, residual=None, acc=None, res_sink=None):
+    def act(self, x, relu: bool = True, residual=None, acc=None, res_sink=None, have_stats: bool = False):
         """act(BN(x) [+ residual]); one fused HIP kernel pair in "hip" mode
-        (``acc``: statistics already accumulated by the producing conv)."""
+        (``acc`` with ``have_stats``: statistics already accumulated by the
+        producing conv; else the step's zeroed arena slice, if any)."""
         if self.hip_ok(x, residual):
             from ..ops.bn_nhwc import bn_act
 
+            if acc is None:
+                acc, have_stats = self.acc, False
             return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual, relu, acc=acc,
-                          grads=self.bind, res_sink=res_sink)
+                          grads=self.bind, res_sink=res_sink, have_stats=have_stats if acc is not None else None)
         y = self(x)
         if residual is not None:
             y = y + residual
@@ -79,6 +83,8 @@ _FUSE_STATS = os.environ.get("DISTLEARN_RESNET_FUSE_STATS", "1") == "1"
 # of 74 us (profiles/r2_resnet50_kernels_fuse_res.txt); the transposed epilogue loads
 # the addend 16 bytes at a time and the fusion now wins: 30.33 -> 29.68 ms/step.
 _FUSE_RES = os.environ.get("DISTLEARN_RESNET_FUSE_RES", "1") == "1"
+# channels-last copies of the KxK shadows for MIOpen, one launch per step (ops/conv.py)
+_CL_WEIGHTS = os.environ.get("DISTLEARN_RESNET_CL_WEIGHTS", "1") == "1"
 # stem max-pool on the HIP gather-backward kernels (ops/pool.py)
 _POOL_HIP = os.environ.get("DISTLEARN_RESNET_POOL", "hip") == "hip"
 
@@ -99,38 +105,41 @@ class _Conv(nn.Module):
 
         return _CONV_MODE == "hip" and self.k == 1 and self.stride == 1 and conv1x1_supported(x, self.weight.shape[0])
 
-    def forward(self, x, stats=None, res_link=None):
-        """``stats``: optional zeroed fp32 [2*Cout] that receives the output's
+    def forward(self, x, stats=None, res_link=None, dx_sink=None):
+        """``stats``: optional fp32 [2*Cout] that receives the output's
         per-channel sum / sum of squares (HIP GEMM path only); ``res_link``:
-        a dict through which a residual BatchNorm hands over the gradient of
-        the same input (added in the dgrad epilogue)."""
+        a dict through which another branch hands over its gradient of the
+        same input (added in the dgrad epilogue); ``dx_sink``: the dict that
+        receives THIS conv's input gradient instead of autograd."""
         b = self.bind
         if b is None or not x.is_cuda or x.dtype != torch.bfloat16:
             return F.conv2d(x, self.weight.to(x.dtype), None, self.stride, self.pad)
         from ..ops.conv import Conv1x1, ShadowConv
 
         if not torch.is_grad_enabled():
-            return F.conv2d(x, b.w16.view(self.weight.shape), None, self.stride, self.pad)
+            w = b.wcl if b.wcl is not None else b.w16.view(self.weight.shape)
+            return F.conv2d(x, w, None, self.stride, self.pad)
         if self.hip_gemm(x):
-            return Conv1x1.apply(x, self.weight, b, stats, res_link)
-        return ShadowConv.apply(x, self.weight, b, self.stride, self.pad)
+            return Conv1x1.apply(x, self.weight, b, stats, res_link, dx_sink)
+        return ShadowConv.apply(x, self.weight, b, self.stride, self.pad, dx_sink)
 
 
-def _conv_bn(conv: _Conv, bn: "_BN", x, relu: bool = True, residual=None, link=None, res_sink=None):
+def _conv_bn(conv: _Conv, bn: "_BN", x, relu: bool = True, residual=None, link=None, res_sink=None, dx_sink=None):
     """bn.act(conv(x)) with the BatchNorm statistics produced by the conv's
     epilogue when both run on the HIP kernels (one full read of the conv
     output fewer per BatchNorm)."""
+    kw = {"res_link": link, "dx_sink": dx_sink} if conv.bind is not None else {}
     if _FUSE_STATS and conv.hip_gemm(x) and _BN_MODE == "hip" and bn.training:
         from .._native import native
 
         if native().reduce_atomic() == 0:  # partial-row statistics (deterministic)
             cout = conv.weight.shape[0]
-            acc = torch.zeros(4 * cout, device=x.device)
-            y = conv(x, stats=acc[:2 * cout], res_link=link)
+            acc = bn.acc if bn.acc is not None else torch.zeros(4 * cout, device=x.device)
+            y = conv(x, stats=acc[:2 * cout], **kw)
             if bn.hip_ok(y, residual):
-                return bn.act(y, relu, residual, acc=acc, res_sink=res_sink)
+                return bn.act(y, relu, residual, acc=acc, res_sink=res_sink, have_stats=True)
             return bn.act(y, relu, residual)
-    return bn.act(conv(x, res_link=link) if conv.bind is not None else conv(x), relu, residual, res_sink=res_sink)
+    return bn.act(conv(x, **kw), relu, residual, res_sink=res_sink)
 
 
 class _Bottleneck(nn.Module):
@@ -145,13 +154,19 @@ class _Bottleneck(nn.Module):
             self.down = nn.ModuleList([_Conv(cin, cout, 1, stride, g), _BN(cout)])
 
     def forward(self, x):
-        # identity residual + c1 on the HIP GEMM: the residual BatchNorm (b3) hands the
-        # gradient of x to c1, whose dgrad epilogue adds it (no separate x-gradient sum)
-        link = {} if (self.down is None and _FUSE_RES and torch.is_grad_enabled() and self.c1.hip_gemm(x)) else None
+        # x feeds c1 (HIP GEMM) and a second branch: the identity residual (its
+        # BatchNorm b3 hands the gradient of x over) or the downsample conv (hands
+        # its dgrad over); c1's dgrad epilogue adds it -- no separate gradient sum.
+        # Autograd runs the second branch's backward first (its nodes are younger),
+        # and Conv1x1 raises if the hand-over is missing.
+        link = {} if (_FUSE_RES and torch.is_grad_enabled() and self.c1.hip_gemm(x)
+                      and (self.down is None or self.down[0].bind is not None)) else None
         y = _conv_bn(self.c1, self.b1, x, link=link)
         y = self.b2.act(self.c2(y))
-        s = x if self.down is None else _conv_bn(self.down[0], self.down[1], x, relu=False)
-        return _conv_bn(self.c3, self.b3, y, residual=s, res_sink=link)
+        if self.down is None:
+            return _conv_bn(self.c3, self.b3, y, residual=x, res_sink=link)
+        s = _conv_bn(self.down[0], self.down[1], x, relu=False, dx_sink=link)
+        return _conv_bn(self.c3, self.b3, y, residual=s)
 
 
 class ResNet50(nn.Module):
@@ -177,6 +192,7 @@ class ResNet50(nn.Module):
         h = x.to(cd)
         if h.is_cuda:
             h = h.contiguous(memory_format=torch.channels_last)
+        self._begin_step(h)
         h = self.stem_bn.act(self.stem(h))
         from ..ops.pool import max_pool2d_nhwc, supported
 
@@ -187,6 +203,27 @@ class ResNet50(nn.Module):
         # memorising synthetic run overflowed into NaN at lr 0.1
         h = h.float().mean((2, 3))
         return F.log_softmax(F.linear(h, self.fc_w, self.fc_b), dim=1)
+
+    def _begin_step(self, h) -> None:
+        """Per training step: ONE zero fill for every BatchNorm's forward and
+        backward statistics (53 x 2 fills of ~5 us before), and ONE launch that
+        refreshes the transposed 1x1 shadows for the dgrads."""
+        train = torch.is_grad_enabled() and h.is_cuda and self.training
+        bns = self._bns if hasattr(self, "_bns") else [m for m in self.modules() if isinstance(m, _BN)]
+        self._bns = bns
+        if train and _BN_MODE == "hip" and h.dtype == torch.bfloat16:
+            arena = torch.zeros(sum(4 * m.weight.numel() for m in bns), device=h.device)
+            o = 0
+            for m in bns:
+                m.acc = arena[o:o + 4 * m.weight.numel()]
+                o += 4 * m.weight.numel()
+        else:
+            for m in bns:
+                m.acc = None
+        if train and getattr(self, "_wt", None) is not None:
+            self._wt.refresh()
+        if getattr(self, "_wcl", None) is not None and h.is_cuda:
+            self._wcl.refresh()  # also read by the no-grad (predict) path
 
     @staticmethod
     def loss(logp, target):
@@ -203,14 +240,27 @@ class ResNet50(nn.Module):
             return
         index = {id(t): i for i, t in enumerate(flat.leaves)}
         w16, g32 = flat.shadow_views(), flat.views_of(flat.grad)
+        gemm, spatial = [], []
         for m in self.modules():
             if isinstance(m, _Conv):
                 i = index[id(m.weight)]
                 m.bind = ShadowBinding(w16[i], g32[i], (lambda i=i: ready(i)) if ready else (lambda: None))
+                if m.k == 1 and m.stride == 1 and w16[i].is_cuda:
+                    gemm.append(m.bind)
+                elif m.k > 1 and w16[i].is_cuda:
+                    spatial.append((m.bind, tuple(m.weight.shape)))
             elif isinstance(m, _BN):
                 # the HIP BatchNorm backward writes dgamma / dbeta straight into the flat gradient
                 iw, ib = index[id(m.weight)], index[id(m.bias)]
                 m.bind = (g32[iw], g32[ib], (lambda iw=iw, ib=ib: (ready(iw), ready(ib))) if ready else (lambda: None))
+        if gemm and _CONV_MODE == "hip":
+            from ..ops.conv import WeightTransposes
+
+            self._wt = WeightTransposes(gemm)
+        if spatial and _CL_WEIGHTS:
+            from ..ops.conv import ChannelsLastWeights
+
+            self._wcl = ChannelsLastWeights([b for b, _ in spatial], [s for _, s in spatial])
 
 
 def resnet50(num_classes: int = 1000, seed: Optional[int] = 0) -> ResNet50:

@@ -33,15 +33,18 @@ def supported(x: torch.Tensor) -> bool:
 
 class _BnAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, residual, relu, eps, momentum, acc, grads, res_sink):
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, relu, eps, momentum, acc, grads, res_sink,
+                have_stats):
         M, C = _geom(x)
         y = torch.empty_like(x, memory_format=torch.channels_last)
-        # forward and backward per-channel sums in one zeroed buffer (one fill);
-        # a caller-provided acc already holds the forward statistics (emitted by the
-        # producing convolution's epilogue): the statistics pass is skipped
-        have_stats = acc is not None
+        # forward and backward per-channel sums in one zeroed buffer (one fill, or a
+        # slice of the caller's per-step zeroed arena); with have_stats the first 2C
+        # already hold the forward statistics (emitted by the producing convolution's
+        # epilogue): the statistics pass is skipped
         if acc is None:
             acc = torch.zeros(4 * C, device=x.device, dtype=torch.float32)
+            have_stats = False
+        ctx.backwards = 0
         save = torch.empty(2 * C, device=x.device, dtype=torch.float32)
         res = residual.contiguous(memory_format=torch.channels_last) if residual is not None else None
         native().bn_nhwc_fwd(x.data_ptr(), res.data_ptr() if res is not None else 0, y.data_ptr(), acc.data_ptr(),
@@ -69,7 +72,9 @@ class _BnAct(torch.autograd.Function):
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
         acc = acc4[2 * C:]
-        acc.zero_()  # the kernels accumulate atomically: a second backward (retain_graph) starts from 0 too
+        if ctx.backwards:  # the kernels accumulate atomically into the zeroed half: a second
+            acc.zero_()    # backward (retain_graph) must start from 0 again
+        ctx.backwards += 1
         if ctx.grads is not None:  # dgamma / dbeta straight into the flat gradient (overwritten)
             dw, db, ready = ctx.grads
         else:
@@ -83,16 +88,18 @@ class _BnAct(torch.autograd.Function):
             dres = None
         if ctx.grads is not None:
             ready()
-            return dx, None, None, None, None, dres, None, None, None, None, None, None
-        return dx, dw.to(weight.dtype), db.to(weight.dtype), None, None, dres, None, None, None, None, None, None
+            return dx, None, None, None, None, dres, None, None, None, None, None, None, None
+        return dx, dw.to(weight.dtype), db.to(weight.dtype), None, None, dres, None, None, None, None, None, None, None
 
 
 def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_mean: Optional[torch.Tensor],
            running_var: Optional[torch.Tensor], residual: Optional[torch.Tensor] = None, relu: bool = True,
            eps: float = 1e-5, momentum: float = 0.1, acc: Optional[torch.Tensor] = None,
-           grads=None, res_sink: Optional[dict] = None) -> torch.Tensor:
-    """``acc``: optional zeroed fp32 [4C] whose first 2C already hold the
-    per-channel sum / sum of squares of x (see ops/conv.py Conv1x1).
+           grads=None, res_sink: Optional[dict] = None, have_stats: Optional[bool] = None) -> torch.Tensor:
+    """``acc``: optional fp32 [4C] whose last 2C are zero; with ``have_stats``
+    (the default when ``acc`` is given) its first 2C already hold the
+    per-channel sum / sum of squares of x (see ops/conv.py Conv1x1), else they
+    are zero too and the statistics pass fills them.
     ``grads``: optional (dweight view, dbias view, ready callback): the
     backward writes the parameter gradients there (e.g. into the flat
     gradient buffer) instead of returning them to autograd.
@@ -108,5 +115,7 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
         raise ValueError("bn_act: weight / bias must be fp32")
     if acc is not None and (acc.numel() != 4 * x.shape[1] or acc.dtype != torch.float32):
         raise ValueError("bn_act: acc must be fp32 [4C]")
+    if have_stats is None:
+        have_stats = acc is not None
     return _BnAct.apply(x, weight.contiguous(), bias.contiguous(), running_mean, running_var, residual, relu, eps,
-                        momentum, acc, grads, res_sink)
+                        momentum, acc, grads, res_sink, bool(have_stats))

@@ -42,12 +42,47 @@ BF16 = torch.bfloat16
 
 class ShadowBinding:
     """What a conv module needs from the trainer: its bf16 shadow weight view,
-    its fp32 gradient view, and a callback that reports the gradient ready."""
+    its fp32 gradient view, and a callback that reports the gradient ready.
+    ``wt``: optional [Cin][Cout] bf16 transposed shadow of a 1x1 weight that
+    :class:`WeightTransposes` refreshes once per step (the dgrad B operand)."""
 
-    __slots__ = ("w16", "g32", "ready")
+    __slots__ = ("w16", "g32", "ready", "wt", "wcl")
 
     def __init__(self, w16: torch.Tensor, g32: torch.Tensor, ready):
         self.w16, self.g32, self.ready = w16, g32, ready
+        self.wt = None
+        self.wcl = None  # channels-last copy of a KxK shadow (ChannelsLastWeights), for MIOpen
+
+
+class WeightTransposes:
+    """The transposed bf16 shadows of many 1x1 conv weights, refreshed by ONE
+    kernel launch per step (csrc transpose_many) instead of one transpose per
+    conv in its backward.  ``refresh()`` must run after the optimizer step has
+    written the shadow and before the first dgrad reads ``bind.wt`` -- the
+    model calls it at the start of every training forward."""
+
+    def __init__(self, binds):
+        C = native()
+        binds = list(binds)
+        dev = binds[0].w16.device
+        total = sum(b.w16.numel() for b in binds)
+        self.arena = torch.empty(total, dtype=BF16, device=dev)
+        rows, o, tiles = [], 0, 0
+        for b in binds:
+            cout = b.w16.shape[0]
+            cin = b.w16.numel() // cout
+            b.wt = self.arena[o:o + cout * cin].view(cin, cout)
+            tc = (cin + 63) // 64
+            rows.append([b.w16.data_ptr(), b.wt.data_ptr(), cout | (cin << 32), tiles | (tc << 32)])
+            tiles += ((cout + 63) // 64) * tc
+            o += cout * cin
+        if C.transpose_entry_bytes() != 32:
+            raise RuntimeError("transpose_many: unexpected entry layout")
+        self.table = torch.tensor(rows, dtype=torch.int64).to(dev)
+        self.n, self.tiles = len(binds), tiles
+
+    def refresh(self):
+        native().transpose_many(self.table.data_ptr(), self.n, self.tiles, stream_handle())
 
 
 def _fwd_plan(M: int, N: int, K: int):
@@ -85,13 +120,43 @@ def conv1x1_supported(x: torch.Tensor, cout: int) -> bool:
             and M * max(cin, cout) < (1 << 31))
 
 
+class ChannelsLastWeights:
+    """Channels-last copies of the KxK conv shadows for the MIOpen convolutions,
+    refreshed by ONE launch per step (csrc weights_to_cl).  The flat buffer
+    keeps every weight in [Cout][Cin][K][K] order, and torch copied each one to
+    channels-last inside every F.conv2d / convolution_backward call on a
+    channels-last input (34 copy kernels per ResNet-50 step)."""
+
+    def __init__(self, binds, shapes):
+        C = native()
+        if C.cl_entry_bytes() != 32:
+            raise RuntimeError("weights_to_cl: unexpected entry layout")
+        binds = list(binds)
+        dev = binds[0].w16.device
+        self.arena = torch.empty(sum(b.w16.numel() for b in binds), dtype=BF16, device=dev)
+        rows, o = [], 0
+        for b, (cout, cin, k, _) in zip(binds, shapes):
+            n = cout * cin * k * k
+            b.wcl = self.arena[o:o + n].as_strided((cout, cin, k, k), (k * k * cin, 1, k * cin, cin))
+            rows.append([b.w16.data_ptr(), b.wcl.data_ptr(), cout | (cin << 32), k * k])
+            o += n
+        self.table = torch.tensor(rows, dtype=torch.int64).to(dev)
+        self.n = len(binds)
+
+    def refresh(self):
+        native().weights_to_cl(self.table.data_ptr(), self.n, stream_handle())
+
+
 class Conv1x1(torch.autograd.Function):
     """y = conv1x1(x, W) on the MFMA kernels; x channels-last bf16 [N, Cin, H, W]."""
 
     @staticmethod
-    def forward(ctx, x, weight, bind: ShadowBinding, stats, res_link=None):
+    def forward(ctx, x, weight, bind: ShadowBinding, stats, res_link=None, dx_sink=None):
         C = native()
         ctx.res_link = res_link
+        ctx.dx_sink = dx_sink
+        if dx_sink is not None:
+            dx_sink["expect"] = True  # dx goes to the sink's consumer, not to autograd
         x = x.contiguous(memory_format=torch.channels_last)
         N, cin, H, W = x.shape
         cout = weight.shape[0]
@@ -135,8 +200,10 @@ class Conv1x1(torch.autograd.Function):
                 raise RuntimeError("Conv1x1: the residual branch's gradient did not arrive before the dgrad")
             add = add.contiguous(memory_format=torch.channels_last)
         if ctx.needs_input_grad[0]:
-            wt = torch.empty(cin, cout, dtype=BF16, device=x.device)
-            C.weight_flip_transpose(bind.w16.data_ptr(), wt.data_ptr(), cout, cin, 1, s)
+            wt = bind.wt
+            if wt is None:
+                wt = torch.empty(cin, cout, dtype=BF16, device=x.device)
+                C.weight_flip_transpose(bind.w16.data_ptr(), wt.data_ptr(), cout, cin, 1, s)
             dx = torch.empty_like(x, memory_format=torch.channels_last)
             tile, splits = _plan_1x1(M, cin, cout)
             if add is not None and splits == 1:
@@ -160,7 +227,10 @@ class Conv1x1(torch.autograd.Function):
         C.conv_wgrad(dy.data_ptr(), x.data_ptr(), ws.data_ptr(), M, 1, 1, cin, cout, 1, splits, cin, tile, 0, s)
         C.slab_reduce_add(ws.data_ptr(), bind.g32.data_ptr(), splits, cout, 1, cin, cin, s)
         bind.ready()
-        return dx, None, None, None, None
+        if ctx.dx_sink is not None and dx is not None:
+            ctx.dx_sink["g"] = dx
+            dx = None
+        return dx, None, None, None, None, None
 
 
 class ShadowConv(torch.autograd.Function):
@@ -168,8 +238,11 @@ class ShadowConv(torch.autograd.Function):
     added into the flat buffer."""
 
     @staticmethod
-    def forward(ctx, x, weight, bind: ShadowBinding, stride: int, pad: int):
-        w16 = bind.w16.view(weight.shape)
+    def forward(ctx, x, weight, bind: ShadowBinding, stride: int, pad: int, dx_sink=None):
+        w16 = bind.wcl if bind.wcl is not None else bind.w16.view(weight.shape)
+        ctx.dx_sink = dx_sink
+        if dx_sink is not None:
+            dx_sink["expect"] = True
         ctx.save_for_backward(x)
         ctx.bind, ctx.stride, ctx.pad, ctx.wshape = bind, stride, pad, weight.shape
         return F.conv2d(x, w16, None, stride, pad)
@@ -178,10 +251,15 @@ class ShadowConv(torch.autograd.Function):
     def backward(ctx, dy):
         (x,) = ctx.saved_tensors
         bind = ctx.bind
-        w16 = bind.w16.view(ctx.wshape)
+        w16 = bind.wcl if bind.wcl is not None else bind.w16.view(ctx.wshape)
         dx, dw, _ = torch.ops.aten.convolution_backward(
             dy, x, w16, None, (ctx.stride, ctx.stride), (ctx.pad, ctx.pad), (1, 1), False, (0, 0), 1,
             (ctx.needs_input_grad[0], True, False))
         bind.g32.view(ctx.wshape).add_(dw)
         bind.ready()
-        return dx, None, None, None, None
+        if ctx.dx_sink is not None and dx is not None:
+            # the same input feeds a 1x1 conv whose dgrad epilogue adds this (ResNet
+            # downsample blocks: no separate sum of the two input gradients)
+            ctx.dx_sink["g"] = dx
+            dx = None
+        return dx, None, None, None, None, None
