@@ -81,20 +81,23 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_stats_kernel(const bf16_t* _
   const int64_t row1 = min(g.M, row0 + g.rows_per_block);
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int64_t row = row0 + r;
-  // two rows per iteration: two independent 16-byte loads in flight per thread
-  for (; row + g.RPI < row1; row += 2 * g.RPI) {
-    const u32x4 v0 = *(const u32x4*)(x + row * g.C + c);
-    const u32x4 v1 = *(const u32x4*)(x + (row + g.RPI) * g.C + c);
-    float f[8], h[8];
-    unpack8(v0, f);
-    unpack8(v1, h);
+  // four rows per iteration: four independent 16-byte loads in flight per thread
+  for (; row + 3 * g.RPI < row1; row += 4 * g.RPI) {
+    u32x4 v[4];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      s[k] += f[k] + h[k];
-      q[k] = fmaf(f[k], f[k], fmaf(h[k], h[k], q[k]));
+    for (int u = 0; u < 4; ++u) v[u] = *(const u32x4*)(x + (row + u * g.RPI) * g.C + c);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float f[8];
+      unpack8(v[u], f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s[k] += f[k];
+        q[k] = fmaf(f[k], f[k], q[k]);
+      }
     }
   }
-  if (row < row1) {
+  for (; row < row1; row += g.RPI) {
     float f[8];
     unpack8(*(const u32x4*)(x + row * g.C + c), f);
 #pragma unroll
@@ -147,44 +150,44 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_fwd_apply_kernel(
   }
   const int64_t row0 = (int64_t)blockIdx.x * g.rows_per_block;
   const int64_t row1 = min(g.M, row0 + g.rows_per_block);
-  for (int64_t row = row0 + r; row < row1; row += g.RPI) {
-    const int64_t off = row * g.C + c;
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  auto apply = [&](int64_t off, const u32x4& xr, const u32x4& rr) {
     float f[8];
-    unpack8(*(const u32x4*)(x + off), f);
+    unpack8(xr, f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) f[k] = fmaf(f[k], sc[k], sh[k]);
     if (res != nullptr) {
-      float rr[8];
-      unpack8(*(const u32x4*)(res + off), rr);
+      float q[8];
+      unpack8(rr, q);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) f[k] += rr[k];
+      for (int k = 0; k < 8; ++k) f[k] += q[k];
     }
     if (relu) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) f[k] = fmaxf(f[k], 0.f);
     }
     *(u32x4*)(y + off) = pack8(f);
+  };
+  int64_t row = row0 + r;
+  for (; row + g.RPI < row1; row += 2 * g.RPI) {  // two rows' loads in flight
+    const int64_t o0 = row * g.C + c, o1 = o0 + (int64_t)g.RPI * g.C;
+    const u32x4 x0 = *(const u32x4*)(x + o0), x1 = *(const u32x4*)(x + o1);
+    const u32x4 r0 = res != nullptr ? *(const u32x4*)(res + o0) : z;
+    const u32x4 r1 = res != nullptr ? *(const u32x4*)(res + o1) : z;
+    apply(o0, x0, r0);
+    apply(o1, x1, r1);
+  }
+  if (row < row1) {
+    const int64_t o0 = row * g.C + c;
+    apply(o0, *(const u32x4*)(x + o0), res != nullptr ? *(const u32x4*)(res + o0) : z);
   }
 }
 
 // g = dy * relu'(.): relu 0 = identity, 1 = mask from the saved output y (BN
 // fused with a residual add), 2 = mask recomputed from x (x * sc + sh > 0,
 // bitwise the forward's pre-activation: same fp32 operands and fma), which
-// saves reading y in both backward passes.
-__device__ __forceinline__ void load_g(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, int64_t off,
-                                       int relu, const float* xv, const float* sc, const float* sh, float* gv) {
-  unpack8(*(const u32x4*)(dy + off), gv);
-  if (relu == 2) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) gv[k] = fmaf(xv[k], sc[k], sh[k]) > 0.f ? gv[k] : 0.f;
-  } else if (relu) {
-    float yy[8];
-    unpack8(*(const u32x4*)(y + off), yy);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) gv[k] = yy[k] > 0.f ? gv[k] : 0.f;
-  }
-}
-
+// saves reading y in both backward passes (applied inline by the two kernels
+// below, after all of an iteration's loads are issued).
 __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ save, const float* __restrict__ w, const float* __restrict__ b, BnGeom g, int relu,
@@ -203,16 +206,46 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_reduce_kernel(
   float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int64_t row0 = (int64_t)blockIdx.x * g.rows_per_block;
   const int64_t row1 = min(g.M, row0 + g.rows_per_block);
-  for (int64_t row = row0 + r; row < row1; row += g.RPI) {
-    const int64_t off = row * g.C + c;
+  auto accum = [&](const u32x4& xr, const u32x4& dr, const u32x4& yr) {
     float gv[8], xv[8];
-    unpack8(*(const u32x4*)(x + off), xv);
-    load_g(dy, y, off, relu, xv, sc, sh, gv);
+    unpack8(xr, xv);
+    unpack8(dr, gv);
+    if (relu == 2) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gv[k] = fmaf(xv[k], sc[k], sh[k]) > 0.f ? gv[k] : 0.f;
+    } else if (relu) {
+      float yy[8];
+      unpack8(yr, yy);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gv[k] = yy[k] > 0.f ? gv[k] : 0.f;
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       sg[k] += gv[k];
       sgx[k] = fmaf(gv[k], (xv[k] - mean[k]) * invstd[k], sgx[k]);
     }
+  };
+  // four rows per iteration: every load of the group is issued before any is
+  // consumed (8-12 16-byte loads in flight per lane; the single-row loop ran at
+  // ~2 TB/s on the ResNet-50 shapes, profiles/r2_pmc_hotpath.txt)
+  constexpr int U = 4;
+  int64_t row = row0 + r;
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  for (; row + (U - 1) * g.RPI < row1; row += U * g.RPI) {
+    u32x4 xr[U], dr[U], yr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t off = (row + u * g.RPI) * g.C + c;
+      xr[u] = *(const u32x4*)(x + off);
+      dr[u] = *(const u32x4*)(dy + off);
+      yr[u] = relu == 1 ? *(const u32x4*)(y + off) : z;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) accum(xr[u], dr[u], yr[u]);
+  }
+  for (; row < row1; row += g.RPI) {
+    const int64_t off = row * g.C + c;
+    accum(*(const u32x4*)(x + off), *(const u32x4*)(dy + off), relu == 1 ? *(const u32x4*)(y + off) : z);
   }
   block_reduce_atomic(sg, sgx, g, c0, acc);
 }
@@ -244,11 +277,20 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
   }
   const int64_t row0 = (int64_t)blockIdx.x * g.rows_per_block;
   const int64_t row1 = min(g.M, row0 + g.rows_per_block);
-  for (int64_t row = row0 + r; row < row1; row += g.RPI) {
-    const int64_t off = row * g.C + c;
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  auto apply = [&](int64_t off, const u32x4& xr, const u32x4& dr, const u32x4& yr) {
     float gv[8], xv[8], o[8];
-    unpack8(*(const u32x4*)(x + off), xv);
-    load_g(dy, y, off, relu, xv, a, sh, gv);
+    unpack8(xr, xv);
+    unpack8(dr, gv);
+    if (relu == 2) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gv[k] = fmaf(xv[k], a[k], sh[k]) > 0.f ? gv[k] : 0.f;
+    } else if (relu) {
+      float yy[8];
+      unpack8(yr, yy);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gv[k] = yy[k] > 0.f ? gv[k] : 0.f;
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float xh = (xv[k] - mean[k]) * invstd[k];
@@ -256,6 +298,19 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
     }
     *(u32x4*)(dx + off) = pack8(o);
     if (dres != nullptr) *(u32x4*)(dres + off) = pack8(gv);
+  };
+  int64_t row = row0 + r;
+  for (; row + g.RPI < row1; row += 2 * g.RPI) {  // two rows' loads in flight
+    const int64_t o0 = row * g.C + c, o1 = o0 + (int64_t)g.RPI * g.C;
+    const u32x4 x0 = *(const u32x4*)(x + o0), x1 = *(const u32x4*)(x + o1);
+    const u32x4 d0 = *(const u32x4*)(dy + o0), d1 = *(const u32x4*)(dy + o1);
+    const u32x4 y0 = relu == 1 ? *(const u32x4*)(y + o0) : z, y1 = relu == 1 ? *(const u32x4*)(y + o1) : z;
+    apply(o0, x0, d0, y0);
+    apply(o1, x1, d1, y1);
+  }
+  if (row < row1) {
+    const int64_t o0 = row * g.C + c;
+    apply(o0, *(const u32x4*)(x + o0), *(const u32x4*)(dy + o0), relu == 1 ? *(const u32x4*)(y + o0) : z);
   }
 }
 
