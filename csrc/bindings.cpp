@@ -24,6 +24,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("confusion_update", &confusion_update);
   m.def("bn_nhwc_fwd", &bn_nhwc_fwd);
   m.def("bn_nhwc_bwd", &bn_nhwc_bwd);
+  m.def("set_bn_reduce_blocks", &set_bn_reduce_blocks);
   m.def("bn_rows_reduce", &bn_rows_reduce);
   m.def("gather_normalize", &gather_normalize);
 

@@ -314,7 +314,15 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
   }
 }
 
-BnGeom make_geom(int64_t M, int C, dim3* grid) {
+// max_rb: cap on the row blocks.  The statistics / backward-reduce kernels end
+// with one fp32 atomic per channel per block, and same-address atomics from
+// thousands of blocks serialise (the C = 64 statistics pass ran at ~2 TB/s with
+// 2048 blocks): they use g_reduce_blocks, the apply kernels the default.  Swept
+// on the ResNet-50 shapes (scripts/bench_bn.py BN_RB=..., profiles/r2_bn_reduce_blocks.txt):
+// sum of statistics + backward times 2831 / 2450 / 2527 / 2626 us for 128 / 256 / 512 / 1024.
+static int64_t g_reduce_blocks = 256;
+
+BnGeom make_geom(int64_t M, int C, dim3* grid, int64_t max_rb = 2048) {
   if (M <= 0 || C <= 0 || C % 8 != 0 || (kThreads % (C / 8 < 32 ? C / 8 : 32)) != 0 ||
       (C / 8 > 32 && (C / 8) % 32 != 0))
     throw std::runtime_error("bn_nhwc: C must be a multiple of 8 dividing 256*8 or a multiple of 256 (got " +
@@ -327,7 +335,7 @@ BnGeom make_geom(int64_t M, int C, dim3* grid) {
   const int groups = (C / 8) / g.CVB;
   int64_t cap = 262144 / C;
   if (cap < 64) cap = 64;
-  if (cap > 2048) cap = 2048;
+  if (cap > max_rb) cap = max_rb;
   int64_t rb = (M + (int64_t)g.RPI * 16 - 1) / ((int64_t)g.RPI * 16);
   if (rb > cap) rb = cap;
   if (rb < 1) rb = 1;
@@ -367,6 +375,8 @@ __global__ void __launch_bounds__(kThreads) bn_rows_reduce_kernel(const float* _
   }
 }
 
+void set_bn_reduce_blocks(int n) { g_reduce_blocks = n < 64 ? 64 : n; }
+
 void bn_rows_reduce(uintptr_t rows, int T, int C, uintptr_t acc, uintptr_t stream) {
   if (T <= 0 || C <= 0) throw std::runtime_error("bn_rows_reduce: empty");
   bn_rows_reduce_kernel<<<C, kThreads, 0, as_stream(stream)>>>((const float*)rows, T, C, (float*)acc);
@@ -379,11 +389,12 @@ void bn_rows_reduce(uintptr_t rows, int T, int C, uintptr_t acc, uintptr_t strea
 void bn_nhwc_fwd(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b, uintptr_t save,
                  uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps, double momentum, int relu,
                  int have_stats, uintptr_t stream) {
-  dim3 grid;
+  dim3 grid, grid_r;
   const BnGeom g = make_geom(M, C, &grid);
   hipStream_t s = as_stream(stream);
   if (!have_stats) {
-    bn_nhwc_stats_kernel<<<grid, kThreads, 0, s>>>((const bf16_t*)x, g, (float*)acc);
+    const BnGeom gr = make_geom(M, C, &grid_r, g_reduce_blocks);
+    bn_nhwc_stats_kernel<<<grid_r, kThreads, 0, s>>>((const bf16_t*)x, gr, (float*)acc);
     DL_HIP_CHECK(hipGetLastError());
   }
   bn_nhwc_fwd_apply_kernel<<<grid, kThreads, 0, s>>>((const bf16_t*)x, (const bf16_t*)res, (bf16_t*)y,
@@ -398,12 +409,13 @@ void bn_nhwc_fwd(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr
 void bn_nhwc_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, uintptr_t acc,
                  uintptr_t dx,
                  uintptr_t dres, uintptr_t dw, uintptr_t db, int64_t M, int C, int relu, uintptr_t stream) {
-  dim3 grid;
+  dim3 grid, grid_r;
   const BnGeom g = make_geom(M, C, &grid);
+  const BnGeom gr = make_geom(M, C, &grid_r, g_reduce_blocks);
   hipStream_t s = as_stream(stream);
-  bn_nhwc_bwd_reduce_kernel<<<grid, kThreads, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x,
-                                                       (const float*)save, (const float*)w, (const float*)b, g, relu,
-                                                       (float*)acc);
+  bn_nhwc_bwd_reduce_kernel<<<grid_r, kThreads, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x,
+                                                         (const float*)save, (const float*)w, (const float*)b, gr,
+                                                         relu, (float*)acc);
   DL_HIP_CHECK(hipGetLastError());
   bn_nhwc_bwd_apply_kernel<<<grid, kThreads, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x,
                                                       (const float*)save, (const float*)w, (const float*)b,

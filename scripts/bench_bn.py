@@ -28,6 +28,8 @@ def main():
     from torch_distlearn_amd import _native
 
     C_ = _native.native()
+    if "BN_RB" in os.environ:  # row-block cap of the statistics / backward-reduce kernels
+        C_.set_bn_reduce_blocks(int(os.environ["BN_RB"]))
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream().cuda_stream
     N = int(os.environ.get("BATCH", "256"))
