@@ -192,12 +192,13 @@ class Conv1x1(torch.autograd.Function):
         dx = None
         add = None
         link = ctx.res_link
-        if link is not None and link.get("expect"):
-            # the same input also fed a residual branch whose BatchNorm parked its
-            # gradient here (ops/bn_nhwc.py res_sink): dx = dy W + that gradient
+        if link is not None and link.get("expect") and ctx.needs_input_grad[0]:
+            # the same input also fed another branch (the identity residual's
+            # BatchNorm, ops/bn_nhwc.py res_sink, or the downsample conv's dgrad,
+            # dx_sink) that parked its gradient here: dx = dy W + that gradient
             add = link.pop("g", None)
             if add is None:
-                raise RuntimeError("Conv1x1: the residual branch's gradient did not arrive before the dgrad")
+                raise RuntimeError("Conv1x1: the other branch's input gradient did not arrive before the dgrad")
             add = add.contiguous(memory_format=torch.channels_last)
         if ctx.needs_input_grad[0]:
             wt = bind.wt
