@@ -172,8 +172,9 @@ def main():
             xs = torch.randn(nb, batch, 224, 224, 3, device=dev, generator=g).to(cdt)
             ys = torch.randint(0, 1000, (nb, batch), device=dev, generator=g)
             step_args = lambda i: (xs[i % nb], ys[i % nb])  # noqa: E731
+        unroll = int(os.environ.get("DISTLEARN_UNROLL", "8"))  # steps per replayed graph (tuning)
         if step_args is None:  # device loader: unrolled graph replays of complete steps
-            tr.run(loader, a.warmup)
+            tr.run(loader, a.warmup, unroll=unroll)
         else:
             for i in range(a.warmup):
                 wl = tr.step(*step_args(i))
@@ -181,7 +182,7 @@ def main():
                     print(f"warmup {i} loss {float(wl):.4f} |p| {float(tr.flat.data.norm()):.4e} "
                           f"|g| {float(tr.flat.grad.norm()):.4e}", file=sys.stderr, flush=True)
         if step_args is None:
-            tr.prepare(loader)  # (run() already did; explicit: no capture may fall in the timed region)
+            tr.prepare(loader, unroll)  # (run() already did; explicit: no capture may fall in the timed region)
         comm = {}
         if len(workers) > 1 and a.algo == "sgd" and not cpu:
             # communication profile: eager calibration steps with HIP events around every
@@ -193,7 +194,7 @@ def main():
         sync()
         t0 = time.perf_counter()
         if step_args is None:
-            loss = tr.run(loader, a.steps)
+            loss = tr.run(loader, a.steps, unroll=unroll)
         else:
             trace = os.environ.get("DISTLEARN_BENCH_TRACE", "")  # debug: per-step losses (stderr)
             hist = []
