@@ -26,6 +26,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_nhwc_bwd", &bn_nhwc_bwd);
   m.def("set_bn_reduce_blocks", &set_bn_reduce_blocks);
   m.def("bn_rows_reduce", &bn_rows_reduce);
+  m.def("bn_nhwc_fwd_pad", &bn_nhwc_fwd_pad);
+  m.def("bn_nhwc_bwd_pad", &bn_nhwc_bwd_pad);
+  m.def("zero_border_nhwc", &zero_border_nhwc);
   m.def("gather_normalize", &gather_normalize);
 
   // ---- convnet kernels (MFMA implicit GEMM, BN/ReLU/pool, classifier head) ------
@@ -46,6 +49,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_wgrad", &conv_wgrad);
   m.def("slab_reduce", &slab_reduce);
   m.def("slab_reduce_add", &slab_reduce_add);
+  m.def("slab_reduce_add_oihw", &slab_reduce_add_oihw);
   m.def("weight_flip_transpose", &weight_flip_transpose);
   m.def("transpose_many", &transpose_many);
   m.def("transpose_entry_bytes", &transpose_entry_bytes);

@@ -20,6 +20,13 @@ void cast_f32_bf16(uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream);
 
 // metrics.hip ---------------------------------------------------------------
 // channels-last training BatchNorm (+ReLU, +residual) for the ResNet-50 path
+void bn_nhwc_fwd_pad(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b,
+                     uintptr_t save, uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps,
+                     double momentum, int relu, int have_stats, int H, int W, int opad, uintptr_t stream);
+void bn_nhwc_bwd_pad(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b,
+                     uintptr_t acc, uintptr_t dx, uintptr_t dres, uintptr_t dw, uintptr_t db, int64_t M, int C,
+                     int relu, int H, int W, int opad, uintptr_t stream);
+void zero_border_nhwc(uintptr_t buf, int N, int H, int W, int C, int pad, uintptr_t stream);
 void bn_nhwc_fwd(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b, uintptr_t save,
                  uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps, double momentum, int relu, int have_stats,
                  uintptr_t stream);
@@ -56,6 +63,8 @@ void conv_fwd_add(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t addend, int B
 void set_conv_fwd_tr(int on);
 void slab_reduce(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream);
 void slab_reduce_add(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream);
+void slab_reduce_add_oihw(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C,
+                          uintptr_t stream);
 void transpose_many(uintptr_t table_dev, int n, int total_tiles, uintptr_t stream);
 int transpose_entry_bytes();
 void weights_to_cl(uintptr_t table_dev, int n, uintptr_t stream);

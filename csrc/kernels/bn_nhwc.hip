@@ -19,6 +19,7 @@
 // The apply kernels recompute mean / invstd from the sums; block (0, g) writes
 // the saved statistics (and running stats / weight gradients) of its channels.
 #include "dl_common.h"
+#include "dl_ops.h"
 
 namespace dl {
 
@@ -32,7 +33,26 @@ struct BnGeom {
   int CVB;             // channel vectors (of 8) per block
   int RPI;             // rows per block iteration (= 256 / CVB)
   int64_t rows_per_block;
+  // padded OUTPUT layout (apply kernels' y / dx): row m = (n, h, w) of an H x W
+  // image is stored at pixel (n, h + opad, w + opad) of [N][H+2opad][W+2opad];
+  // opad 0 = the input's row order.  The consumer is a 3x3 convolution that
+  // reads its zero-bordered input directly (ops/conv.py Conv3x3).
+  int H, W, opad;
+  float inv_HW, inv_W;
 };
+
+// output row of input row `row` (see BnGeom); float-reciprocal division with
+// one correction step (rows < 2^24, checked on the host)
+__device__ __forceinline__ int64_t out_row(const BnGeom& g, int64_t row) {
+  if (g.opad == 0) return row;
+  const int HW = g.H * g.W, m = (int)row;
+  int n = (int)((float)m * g.inv_HW), rem = m - n * HW;
+  if (rem < 0) { --n; rem += HW; } else if (rem >= HW) { ++n; rem -= HW; }
+  int h = (int)((float)rem * g.inv_W), w = rem - h * g.W;
+  if (w < 0) { --h; w += g.W; } else if (w >= g.W) { ++h; w -= g.W; }
+  const int Hp = g.H + 2 * g.opad, Wp = g.W + 2 * g.opad;
+  return ((int64_t)n * Hp + h + g.opad) * Wp + w + g.opad;
+}
 
 __device__ __forceinline__ void unpack8(u32x4 v, float* f) {
 #pragma unroll
@@ -174,12 +194,12 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_fwd_apply_kernel(
     const u32x4 x0 = *(const u32x4*)(x + o0), x1 = *(const u32x4*)(x + o1);
     const u32x4 r0 = res != nullptr ? *(const u32x4*)(res + o0) : z;
     const u32x4 r1 = res != nullptr ? *(const u32x4*)(res + o1) : z;
-    apply(o0, x0, r0);
-    apply(o1, x1, r1);
+    apply(out_row(g, row) * g.C + c, x0, r0);
+    apply(out_row(g, row + g.RPI) * g.C + c, x1, r1);
   }
   if (row < row1) {
     const int64_t o0 = row * g.C + c;
-    apply(o0, *(const u32x4*)(x + o0), res != nullptr ? *(const u32x4*)(res + o0) : z);
+    apply(out_row(g, row) * g.C + c, *(const u32x4*)(x + o0), res != nullptr ? *(const u32x4*)(res + o0) : z);
   }
 }
 
@@ -278,7 +298,7 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
   const int64_t row0 = (int64_t)blockIdx.x * g.rows_per_block;
   const int64_t row1 = min(g.M, row0 + g.rows_per_block);
   const u32x4 z = {0u, 0u, 0u, 0u};
-  auto apply = [&](int64_t off, const u32x4& xr, const u32x4& dr, const u32x4& yr) {
+  auto apply = [&](int64_t off, int64_t doff, const u32x4& xr, const u32x4& dr, const u32x4& yr) {
     float gv[8], xv[8], o[8];
     unpack8(xr, xv);
     unpack8(dr, gv);
@@ -296,7 +316,7 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
       const float xh = (xv[k] - mean[k]) * invstd[k];
       o[k] = a[k] * (gv[k] - mg[k] - xh * mgx[k]);
     }
-    *(u32x4*)(dx + off) = pack8(o);
+    *(u32x4*)(dx + doff) = pack8(o);
     if (dres != nullptr) *(u32x4*)(dres + off) = pack8(gv);
   };
   int64_t row = row0 + r;
@@ -305,12 +325,13 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
     const u32x4 x0 = *(const u32x4*)(x + o0), x1 = *(const u32x4*)(x + o1);
     const u32x4 d0 = *(const u32x4*)(dy + o0), d1 = *(const u32x4*)(dy + o1);
     const u32x4 y0 = relu == 1 ? *(const u32x4*)(y + o0) : z, y1 = relu == 1 ? *(const u32x4*)(y + o1) : z;
-    apply(o0, x0, d0, y0);
-    apply(o1, x1, d1, y1);
+    apply(o0, out_row(g, row) * g.C + c, x0, d0, y0);
+    apply(o1, out_row(g, row + g.RPI) * g.C + c, x1, d1, y1);
   }
   if (row < row1) {
     const int64_t o0 = row * g.C + c;
-    apply(o0, *(const u32x4*)(x + o0), *(const u32x4*)(dy + o0), relu == 1 ? *(const u32x4*)(y + o0) : z);
+    apply(o0, out_row(g, row) * g.C + c, *(const u32x4*)(x + o0), *(const u32x4*)(dy + o0),
+          relu == 1 ? *(const u32x4*)(y + o0) : z);
   }
 }
 
@@ -343,8 +364,38 @@ BnGeom make_geom(int64_t M, int C, dim3* grid, int64_t max_rb = 2048) {
   rpb = (rpb + g.RPI - 1) / g.RPI * g.RPI;
   rb = (M + rpb - 1) / rpb;
   g.rows_per_block = rpb;
+  g.H = g.W = 1;
+  g.opad = 0;
+  g.inv_HW = g.inv_W = 1.f;
   *grid = dim3((unsigned)rb, (unsigned)groups);
   return g;
+}
+
+// set the padded output layout of the apply kernels (BnGeom)
+void set_out_pad(BnGeom& g, int H, int W, int opad) {
+  if (opad == 0) return;
+  if (opad < 0 || H <= 0 || W <= 0 || g.M % ((int64_t)H * W) != 0 || g.M >= (1 << 24))
+    throw std::runtime_error("bn_nhwc: bad padded-output geometry");
+  g.H = H;
+  g.W = W;
+  g.opad = opad;
+  g.inv_HW = 1.f / (float)(H * W);
+  g.inv_W = 1.f / (float)W;
+}
+
+// zero the border ring of a [N][H+2p][W+2p][C] bf16 buffer (its interior is
+// written by an apply kernel with the padded output layout)
+__global__ void __launch_bounds__(kThreads) zero_border_kernel(bf16_t* __restrict__ buf, int N, int H, int W, int C,
+                                                               int p) {
+  const int Hp = H + 2 * p, Wp = W + 2 * p, C8 = C >> 3;
+  const int64_t total = (int64_t)N * Hp * Wp * C8;
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t pix = i / C8;
+    const int w = (int)(pix % Wp), h = (int)((pix / Wp) % Hp);
+    if (h >= p && h < H + p && w >= p && w < W + p) continue;
+    *(u32x4*)(buf + pix * C + (i % C8) * 8) = z;
+  }
 }
 
 }  // namespace
@@ -389,8 +440,17 @@ void bn_rows_reduce(uintptr_t rows, int T, int C, uintptr_t acc, uintptr_t strea
 void bn_nhwc_fwd(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b, uintptr_t save,
                  uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps, double momentum, int relu,
                  int have_stats, uintptr_t stream) {
+  bn_nhwc_fwd_pad(x, res, y, acc, w, b, save, run_mean, run_var, M, C, eps, momentum, relu, have_stats, 1, 1, 0,
+                  stream);
+}
+
+// y in the padded layout [N][H+2opad][W+2opad][C] (interior only; see zero_border_nhwc)
+void bn_nhwc_fwd_pad(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b,
+                     uintptr_t save, uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps,
+                     double momentum, int relu, int have_stats, int H, int W, int opad, uintptr_t stream) {
   dim3 grid, grid_r;
-  const BnGeom g = make_geom(M, C, &grid);
+  BnGeom g = make_geom(M, C, &grid);
+  set_out_pad(g, H, W, opad);
   hipStream_t s = as_stream(stream);
   if (!have_stats) {
     const BnGeom gr = make_geom(M, C, &grid_r, g_reduce_blocks);
@@ -409,8 +469,16 @@ void bn_nhwc_fwd(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr
 void bn_nhwc_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, uintptr_t acc,
                  uintptr_t dx,
                  uintptr_t dres, uintptr_t dw, uintptr_t db, int64_t M, int C, int relu, uintptr_t stream) {
+  bn_nhwc_bwd_pad(dy, y, x, save, w, b, acc, dx, dres, dw, db, M, C, relu, 1, 1, 0, stream);
+}
+
+// dx in the padded layout [N][H+2opad][W+2opad][C] (interior only)
+void bn_nhwc_bwd_pad(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b,
+                     uintptr_t acc, uintptr_t dx, uintptr_t dres, uintptr_t dw, uintptr_t db, int64_t M, int C,
+                     int relu, int H, int W, int opad, uintptr_t stream) {
   dim3 grid, grid_r;
-  const BnGeom g = make_geom(M, C, &grid);
+  BnGeom g = make_geom(M, C, &grid);
+  set_out_pad(g, H, W, opad);
   const BnGeom gr = make_geom(M, C, &grid_r, g_reduce_blocks);
   hipStream_t s = as_stream(stream);
   bn_nhwc_bwd_reduce_kernel<<<grid_r, kThreads, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x,
@@ -421,6 +489,13 @@ void bn_nhwc_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr
                                                       (const float*)save, (const float*)w, (const float*)b,
                                                       (const float*)acc, g, relu,
                                                       (bf16_t*)dx, (bf16_t*)dres, (float*)dw, (float*)db);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+void zero_border_nhwc(uintptr_t buf, int N, int H, int W, int C, int pad, uintptr_t stream) {
+  if (C % 8 != 0 || pad <= 0) throw std::runtime_error("zero_border_nhwc: C % 8 and pad > 0 required");
+  const int64_t total = (int64_t)N * (H + 2 * pad) * (W + 2 * pad) * (C / 8);
+  zero_border_kernel<<<stream_grid(total), kThreads, 0, as_stream(stream)>>>((bf16_t*)buf, N, H, W, C, pad);
   DL_HIP_CHECK(hipGetLastError());
 }
 

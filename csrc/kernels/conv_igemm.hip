@@ -55,9 +55,33 @@ struct ConvGeom {
   int Hp, Wp;  // spatially zero-padded input dims (H + 2 pad, W + 2 pad)
   int Cin, Cout;
   int KS, pad;
-  int logW, logHW, logC8;  // log2(W), log2(H*W), log2(Cin/8)
+  int logW, logHW, logC8;  // log2(W), log2(H*W) (valid when pow2), log2(Cin/8)
   int M, K, Kch;           // M = B*H*W, K = KS*KS*Cin, Kch = K/8
+  int pow2;                // H and W powers of two (the region / c8 kernels and the shift addressing)
+  float inv_HW, inv_W;     // reciprocals for the non-pow2 pixel decomposition (fdivmod)
 };
+
+// q = n / d, r = n - q*d for 0 <= n < 2^24 via a float reciprocal and one
+// correction step (the ResNet-50 spatial sizes 56/28/14/7 are not powers of two)
+__device__ __forceinline__ int fdivmod(int n, int d, float inv_d, int& r) {
+  int q = (int)((float)n * inv_d);
+  r = n - q * d;
+  if (r < 0) { --q; r += d; }
+  else if (r >= d) { ++q; r -= d; }
+  return q;
+}
+
+// padded pixel index (b*Hp + oh)*Wp + ow of output pixel m (any H, W)
+__device__ __forceinline__ int out_pix(const ConvGeom& g, int m) {
+  if (g.pow2) {
+    const int b = m >> g.logHW, rem = m & ((1 << g.logHW) - 1);
+    return (b * g.Hp + (rem >> g.logW)) * g.Wp + (rem & (g.W - 1));
+  }
+  int rem, ow;
+  const int b = fdivmod(m, g.H * g.W, g.inv_HW, rem);
+  const int oh = fdivmod(rem, g.W, g.inv_W, ow);
+  return (b * g.Hp + oh) * g.Wp + ow;
+}
 
 static int ilog2_exact(int v, const char* what) {
   int l = 0;
@@ -66,15 +90,22 @@ static int ilog2_exact(int v, const char* what) {
   return l;
 }
 
+static bool is_pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
+
 static ConvGeom make_geom(int B, int H, int W, int Cin, int Cout, int KS) {
   ConvGeom g;
   g.B = B; g.H = H; g.W = W; g.Cin = Cin; g.Cout = Cout; g.KS = KS; g.pad = KS / 2;
   g.Hp = H + 2 * g.pad; g.Wp = W + 2 * g.pad;
   if (KS % 2 != 1) throw std::runtime_error("conv: odd kernel size required");
   if (Cin < 8) throw std::runtime_error("conv: Cin must be >= 8 (pad the input channels)");
-  g.logW = ilog2_exact(W, "W");
-  g.logHW = ilog2_exact(H * W, "H*W");
+  g.pow2 = is_pow2(W) && is_pow2(H) ? 1 : 0;
+  g.logW = g.pow2 ? ilog2_exact(W, "W") : 0;
+  g.logHW = g.pow2 ? ilog2_exact(H * W, "H*W") : 0;
+  g.inv_HW = 1.0f / (float)(H * W);
+  g.inv_W = 1.0f / (float)W;
   g.logC8 = ilog2_exact(Cin / 8, "Cin/8");
+  if (!g.pow2 && (int64_t)B * H * W >= (1 << 24))
+    throw std::runtime_error("conv: non-power-of-two H/W needs B*H*W < 2^24 (float pixel decomposition)");
   g.M = B * H * W;
   g.K = KS * KS * Cin;
   g.Kch = g.K / 8;
@@ -432,7 +463,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   const int panel = id / ntm;
   const int split = panel % splits, tn = panel / splits;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int HW = 1 << g.logHW, Wd = g.W, C8 = 1 << g.logC8;
+  const int C8 = 1 << g.logC8;
   const int nkt_total = (g.Kch + CPR - 1) / CPR;
   const int kt_beg = split * kt_per_split;
   const int kt_end = min(nkt_total, kt_beg + kt_per_split);
@@ -447,9 +478,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
     const int row = 8 * (wid * A_INS + j) + (lane >> 3);
     a_ch[j] = (lane & 7) ^ ((row >> 1) & 7);
     const int m = min(m0 + row, g.M - 1);  // M tail: any valid pixel (masked in the epilogue)
-    const int b = m >> g.logHW, rem = m & (HW - 1);
-    const int pix = (b * g.Hp + (rem >> g.logW)) * g.Wp + (rem & (Wd - 1));
-    a_base[j] = pix * g.Cin + (TAPU ? a_ch[j] * 8 : 0);
+    a_base[j] = out_pix(g, m) * g.Cin + (TAPU ? a_ch[j] * 8 : 0);
   }
   int b_off[B_INS], b_k[B_INS];
 #pragma unroll
@@ -1013,8 +1042,12 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
   const int mend = min(g.M, mbeg + m_per_split);
   const int HW = 1 << g.logHW, Wd = g.W, C8 = 1 << g.logC8;
   const int HpWp = g.Hp * g.Wp;
-  // padded pixel offset of row r inside a 64-aligned step
-  auto lane_pix = [&](int r) { return (r >> g.logHW) * HpWp + ((r & (HW - 1)) >> g.logW) * g.Wp + (r & (Wd - 1)); };
+  // padded pixel offset of row r inside a 64-aligned step (pow2 H, W: the step's
+  // pixel decomposes as wave-uniform step base + per-lane row part; otherwise
+  // every lane decomposes its own pixel each step, out_pix)
+  auto lane_pix = [&](int r) {
+    return g.pow2 ? (r >> g.logHW) * HpWp + ((r & (HW - 1)) >> g.logW) * g.Wp + (r & (Wd - 1)) : 0;
+  };
 
   // A (dy) lanes: row = A_RPI*(wid*A_INS + j) + lane/ACPR, chunk fixed
   int a_off[A_INS], a_row[A_INS];
@@ -1054,13 +1087,31 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
     char* sA = smem + slot * STAGE_BYTES;
     char* sB = sA + A_BYTES;
     const int ms = mbeg + kt * BK;  // 64-aligned first row of the step
-    const int u = (ms >> g.logHW) * HpWp + ((ms & (HW - 1)) >> g.logW) * g.Wp;  // wave-uniform
-    const int left = mend - ms;                                                  // rows left (uniform)
-    const unsigned ua = 2u * (unsigned)(u * g.Cout), ub = 2u * (unsigned)(u * g.Cin);
+    const int left = mend - ms;     // rows left (uniform)
+    if (g.pow2) {
+      const int u = (ms >> g.logHW) * HpWp + ((ms & (HW - 1)) >> g.logW) * g.Wp;  // wave-uniform
+      const unsigned ua = 2u * (unsigned)(u * g.Cout), ub = 2u * (unsigned)(u * g.Cin);
 #pragma unroll
-    for (int j = 0; j < A_INS; ++j) blds16(dyr, a_row[j] < left ? a_v[j] : kOOB, ua, sA + (wid * A_INS + j) * 1024);
+      for (int j = 0; j < A_INS; ++j)
+        blds16(dyr, a_row[j] < left ? a_v[j] : kOOB, ua, sA + (wid * A_INS + j) * 1024);
 #pragma unroll
-    for (int j = 0; j < B_INS; ++j) blds16(xr, b_row[j] < left ? b_v[j] : kOOB, ub, sB + (wid * B_INS + j) * 1024);
+      for (int j = 0; j < B_INS; ++j)
+        blds16(xr, b_row[j] < left ? b_v[j] : kOOB, ub, sB + (wid * B_INS + j) * 1024);
+    } else {
+#pragma unroll
+      for (int j = 0; j < A_INS; ++j) {
+        const bool ok = a_row[j] < left;
+        const int px = out_pix(g, ok ? ms + a_row[j] : 0);
+        blds16(dyr, ok ? a_v[j] + 2u * (unsigned)(px * g.Cout) : kOOB, 0u, sA + (wid * A_INS + j) * 1024);
+      }
+#pragma unroll
+      for (int j = 0; j < B_INS; ++j) {
+        const bool ok = b_row[j] < left;
+        const int px = out_pix(g, ok ? ms + b_row[j] : 0);
+        blds16(xr, ok && b_v[j] != kOOB ? b_v[j] + 2u * (unsigned)(px * g.Cin) : kOOB, 0u,
+               sB + (wid * B_INS + j) * 1024);
+      }
+    }
   };
 
   f32x4 acc[FM][FN];
@@ -1208,7 +1259,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
 // share one output (each sums a strided subset of the splits, then a
 // fixed-order shuffle reduction): enough parallelism for 64-way slabs.
 // ACC: dst += sum (gradient accumulation semantics) instead of dst = sum.
-template <int TPO, bool ACC = false>
+// OIHW: dst in [Cout][C][taps] order (a PyTorch conv weight) instead of [Cout][taps][C].
+template <int TPO, bool ACC = false, bool OIHW = false>
 __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slabs, float* __restrict__ dst,
                                                           int splits, int Cout, int taps, int Cp, int C) {
   const int64_t total = (int64_t)Cout * taps * C;
@@ -1223,7 +1275,14 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restric
     for (int sp = sub; sp < splits; sp += TPO) s += slabs[sp * slab + src];
 #pragma unroll
     for (int o = TPO / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (sub == 0) dst[i] = ACC ? dst[i] + s : s;
+    if (sub == 0) {
+      int64_t o = i;
+      if constexpr (OIHW) {
+        const int64_t co = rest / taps;
+        o = (co * C + c) * taps + (rest - co * taps);
+      }
+      dst[o] = ACC ? dst[o] + s : s;
+    }
   }
 }
 
@@ -1718,7 +1777,7 @@ constexpr int kRegionLdsCap = 160 * 1024 - 20 * 1024;
 // region kernel (then the streaming kernel runs).
 static bool region_geom(const ConvGeom& g, int BN, int splits, RegionGeom& rg) {
   constexpr int BM = 128, STAGES = 3;
-  if (!g_region || g.Cin % 64 != 0 || g.W > BM || BM % g.W != 0) return false;
+  if (!g.pow2 || !g_region || g.Cin % 64 != 0 || g.W > BM || BM % g.W != 0) return false;
   const int HW = g.H * g.W;
   const int chunks = g.Cin / 64;
   if (chunks % splits != 0) return false;
@@ -1815,7 +1874,7 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
   RegionGeom rg;
   const int c8_rows = 128 / std::max(1, W) + KS - 1;
   const size_t c8_lds = (size_t)((c8_rows * g.Wp + 1 + 63) / 64 * 64 + (64 * KS * KS + 63) / 64 * 64) * 16;
-  if (tile == 2 && splits == 1 && g_region && Cin == 8 && W <= 128 && 128 % W == 0 && (H * W) % 128 == 0 &&
+  if (tile == 2 && splits == 1 && g_region && g.pow2 && Cin == 8 && W <= 128 && 128 % W == 0 && (H * W) % 128 == 0 &&
       Cout % 64 == 0 && c8_lds <= 160 * 1024) {
     const int grid = (g.M / 128) * (Cout / 64);
     auto go = [&](auto kern) {
@@ -1888,7 +1947,7 @@ void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, i
   if (Cout % 8 != 0) throw std::runtime_error("conv_wgrad: Cout % 8 != 0");
   const int bm = tile == 1 ? 64 : 128;
   if (Cout % bm != 0) throw std::runtime_error("conv_wgrad: Cout must be a multiple of the Cout tile");
-  if (W > 64) throw std::runtime_error("conv_wgrad: needs W <= 64");
+  if (g.pow2 && W > 64) throw std::runtime_error("conv_wgrad: needs W <= 64");
   if (splits < 1) splits = 1;
   if (atomic_creal > Cin) throw std::runtime_error("conv_wgrad: atomic_creal > Cin");
   int mps = (g.M + splits - 1) / splits;
@@ -1952,21 +2011,21 @@ void set_reduce_atomic_conv(int on) {
   DL_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_red_atomic), &v, sizeof(int)));
 }
 
-template <bool ACC>
+template <bool ACC, bool OIHW = false>
 static void slab_reduce_t(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C,
                           uintptr_t stream) {
   const int64_t total = (int64_t)Cout * taps * C;
   auto s = as_stream(stream);
   if (splits >= 32) {
     int64_t g = (total * 32 + 255) / 256;
-    slab_reduce_kernel<32, ACC><<<(int)std::min<int64_t>(g, 4096), 256, 0, s>>>((const float*)slabs, (float*)dst,
+    slab_reduce_kernel<32, ACC, OIHW><<<(int)std::min<int64_t>(g, 4096), 256, 0, s>>>((const float*)slabs, (float*)dst,
                                                                                splits, Cout, taps, Cp, C);
   } else if (splits >= 8) {
     int64_t g = (total * 8 + 255) / 256;
-    slab_reduce_kernel<8, ACC><<<(int)std::min<int64_t>(g, 4096), 256, 0, s>>>((const float*)slabs, (float*)dst,
+    slab_reduce_kernel<8, ACC, OIHW><<<(int)std::min<int64_t>(g, 4096), 256, 0, s>>>((const float*)slabs, (float*)dst,
                                                                               splits, Cout, taps, Cp, C);
   } else {
-    slab_reduce_kernel<1, ACC><<<stream_grid(total), 256, 0, s>>>((const float*)slabs, (float*)dst, splits, Cout,
+    slab_reduce_kernel<1, ACC, OIHW><<<stream_grid(total), 256, 0, s>>>((const float*)slabs, (float*)dst, splits, Cout,
                                                                   taps, Cp, C);
   }
   DL_HIP_CHECK(hipGetLastError());
@@ -1980,6 +2039,12 @@ void slab_reduce(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps,
 // stores + this reduce beat the atomic split-K 1.3-2.3x, profiles/r2_gemm1x1_wgrad_slab.jsonl)
 void slab_reduce_add(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream) {
   slab_reduce_t<true>(slabs, dst, splits, Cout, taps, Cp, C, stream);
+}
+
+// dst [Cout][C][taps] (OIHW, the flat gradient of a KxK conv weight) += sum of the slabs
+void slab_reduce_add_oihw(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C,
+                          uintptr_t stream) {
+  slab_reduce_t<true, true>(slabs, dst, splits, Cout, taps, Cp, C, stream);
 }
 
 void weight_flip_transpose(uintptr_t w, uintptr_t wt, int Cout, int Cin, int KS, uintptr_t stream) {

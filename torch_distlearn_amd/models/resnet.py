@@ -54,17 +54,20 @@ class _BN(nn.Module):
         return supported(x) and self.weight.dtype == torch.float32 and (
             residual is None or (residual.dtype == x.dtype and residual.shape == x.shape))
 
-    def act(self, x, relu: bool = True, residual=None, acc=None, res_sink=None, have_stats: bool = False):
+    def act(self, x, relu: bool = True, residual=None, acc=None, res_sink=None, have_stats: bool = False,
+            out_pad: int = 0, dx_pad: int = 0):
         """act(BN(x) [+ residual]); one fused HIP kernel pair in "hip" mode
         (``acc`` with ``have_stats``: statistics already accumulated by the
-        producing conv; else the step's zeroed arena slice, if any)."""
+        producing conv; else the step's zeroed arena slice, if any;
+        ``out_pad`` / ``dx_pad``: zero-bordered output / input gradient)."""
         if self.hip_ok(x, residual):
             from ..ops.bn_nhwc import bn_act
 
             if acc is None:
                 acc, have_stats = self.acc, False
             return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual, relu, acc=acc,
-                          grads=self.bind, res_sink=res_sink, have_stats=have_stats if acc is not None else None)
+                          grads=self.bind, res_sink=res_sink, have_stats=have_stats if acc is not None else None,
+                          out_pad=out_pad, dx_pad=dx_pad)
         y = self(x)
         if residual is not None:
             y = y + residual
@@ -83,6 +86,11 @@ _FUSE_STATS = os.environ.get("DISTLEARN_RESNET_FUSE_STATS", "1") == "1"
 # of 74 us (profiles/r2_resnet50_kernels_fuse_res.txt); the transposed epilogue loads
 # the addend 16 bytes at a time and the fusion now wins: 30.33 -> 29.68 ms/step.
 _FUSE_RES = os.environ.get("DISTLEARN_RESNET_FUSE_RES", "1") == "1"
+# stride-1 3x3 convolutions on the hand-written implicit-GEMM kernels (ops/conv.py
+# Conv3x3) for feature maps of at most this size (0 = off: MIOpen for all 3x3);
+# the 56x56 stage stays on MIOpen (its wgrad measured slower on our kernel:
+# profiles/r2_conv3x3_miopen_vs_hip.jsonl.txt)
+_CONV3_MAX_HW = int(os.environ.get("DISTLEARN_RESNET_CONV3_MAX_HW", "28"))
 # channels-last copies of the KxK shadows for MIOpen, one launch per step (ops/conv.py)
 _CL_WEIGHTS = os.environ.get("DISTLEARN_RESNET_CL_WEIGHTS", "1") == "1"
 # stem max-pool on the HIP gather-backward kernels (ops/pool.py)
@@ -105,6 +113,19 @@ class _Conv(nn.Module):
 
         return _CONV_MODE == "hip" and self.k == 1 and self.stride == 1 and conv1x1_supported(x, self.weight.shape[0])
 
+    def hip_3x3(self, x, shape=None) -> bool:
+        """Stride-1 3x3 convolution on the hand-written kernels (needs the
+        channels-last shadow, ChannelsLastWeights) for an input like ``x``
+        (device / dtype) of ``shape`` (default x.shape)."""
+        shape = tuple(x.shape) if shape is None else shape
+        if (self.bind is None or self.bind.wcl is None or self.k != 3 or self.stride != 1 or not x.is_cuda
+                or x.dtype != torch.bfloat16 or not torch.is_grad_enabled() or _CONV_MODE != "hip"
+                or shape[2] > _CONV3_MAX_HW):
+            return False
+        from ..ops.conv import conv3x3_supported
+
+        return conv3x3_supported(shape, self.weight.shape[0])
+
     def forward(self, x, stats=None, res_link=None, dx_sink=None):
         """``stats``: optional fp32 [2*Cout] that receives the output's
         per-channel sum / sum of squares (HIP GEMM path only); ``res_link``:
@@ -121,15 +142,22 @@ class _Conv(nn.Module):
             return F.conv2d(x, w, None, self.stride, self.pad)
         if self.hip_gemm(x):
             return Conv1x1.apply(x, self.weight, b, stats, res_link, dx_sink)
+        if self.hip_3x3(x) and dx_sink is None:
+            from ..ops.conv import Conv3x3
+
+            return Conv3x3.apply(x, self.weight, b, stats)
         return ShadowConv.apply(x, self.weight, b, self.stride, self.pad, dx_sink)
 
 
-def _conv_bn(conv: _Conv, bn: "_BN", x, relu: bool = True, residual=None, link=None, res_sink=None, dx_sink=None):
+def _conv_bn(conv: _Conv, bn: "_BN", x, relu: bool = True, residual=None, link=None, res_sink=None, dx_sink=None,
+             out_pad: int = 0, dx_pad: int = 0):
     """bn.act(conv(x)) with the BatchNorm statistics produced by the conv's
     epilogue when both run on the HIP kernels (one full read of the conv
-    output fewer per BatchNorm)."""
+    output fewer per BatchNorm).  ``out_pad`` / ``dx_pad``: the BatchNorm writes
+    its output / input gradient zero-bordered (for a Conv3x3 neighbour)."""
     kw = {"res_link": link, "dx_sink": dx_sink} if conv.bind is not None else {}
-    if _FUSE_STATS and conv.hip_gemm(x) and _BN_MODE == "hip" and bn.training:
+    pads = {"out_pad": out_pad, "dx_pad": dx_pad}
+    if _FUSE_STATS and (conv.hip_gemm(x) or conv.hip_3x3(x)) and _BN_MODE == "hip" and bn.training:
         from .._native import native
 
         if native().reduce_atomic() == 0:  # partial-row statistics (deterministic)
@@ -137,9 +165,9 @@ def _conv_bn(conv: _Conv, bn: "_BN", x, relu: bool = True, residual=None, link=N
             acc = bn.acc if bn.acc is not None else torch.zeros(4 * cout, device=x.device)
             y = conv(x, stats=acc[:2 * cout], **kw)
             if bn.hip_ok(y, residual):
-                return bn.act(y, relu, residual, acc=acc, res_sink=res_sink, have_stats=True)
+                return bn.act(y, relu, residual, acc=acc, res_sink=res_sink, have_stats=True, **pads)
             return bn.act(y, relu, residual)
-    return bn.act(conv(x, **kw), relu, residual, res_sink=res_sink)
+    return bn.act(conv(x, **kw), relu, residual, res_sink=res_sink, **pads)
 
 
 class _Bottleneck(nn.Module):
@@ -161,8 +189,12 @@ class _Bottleneck(nn.Module):
         # and Conv1x1 raises if the hand-over is missing.
         link = {} if (_FUSE_RES and torch.is_grad_enabled() and self.c1.hip_gemm(x)
                       and (self.down is None or self.down[0].bind is not None)) else None
-        y = _conv_bn(self.c1, self.b1, x, link=link)
-        y = self.b2.act(self.c2(y))
+        # a stride-1 3x3 c2 on the HIP kernels reads b1's output and b2's input
+        # gradient zero-bordered, written so by the BatchNorm kernels themselves
+        n, _, h, w = x.shape  # c1 is 1x1 stride 1: c2's input is [n, width, h, w]
+        pad = 1 if self.c2.hip_3x3(x, (n, self.c2.weight.shape[1], h, w)) else 0
+        y = _conv_bn(self.c1, self.b1, x, link=link, out_pad=pad)
+        y = _conv_bn(self.c2, self.b2, y, dx_pad=pad)
         if self.down is None:
             return _conv_bn(self.c3, self.b3, y, residual=x, res_sink=link)
         s = _conv_bn(self.down[0], self.down[1], x, relu=False, dx_sink=link)

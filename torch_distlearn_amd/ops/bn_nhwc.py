@@ -24,6 +24,19 @@ def _geom(x: torch.Tensor):
     return n * h * w, c
 
 
+def padded_empty(n: int, c: int, h: int, w: int, pad: int, device) -> torch.Tensor:
+    """A [N, C, H, W] channels-last bf16 view of the interior of a fresh
+    [N, H+2p, W+2p, C] buffer whose border ring is zeroed: the zero-bordered
+    layout the implicit-GEMM 3x3 kernels read directly (ops/conv.py Conv3x3).
+    The view carries ``_dl_pad = pad`` so consumers can find the buffer."""
+    hp, wp = h + 2 * pad, w + 2 * pad
+    buf = torch.empty((n, hp, wp, c), dtype=torch.bfloat16, device=device)
+    native().zero_border_nhwc(buf.data_ptr(), n, h, w, c, pad, stream_handle())
+    v = buf.as_strided((n, c, h, w), (hp * wp * c, 1, wp * c, c), (pad * wp + pad) * c)
+    v._dl_pad = pad
+    return v
+
+
 def supported(x: torch.Tensor) -> bool:
     c = x.shape[1]
     ok_c = c % 8 == 0 and ((c < 256 and 256 % (c // 8) == 0) or c % 256 == 0)
@@ -34,9 +47,14 @@ def supported(x: torch.Tensor) -> bool:
 class _BnAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, relu, eps, momentum, acc, grads, res_sink,
-                have_stats):
+                have_stats, out_pad, dx_pad):
         M, C = _geom(x)
-        y = torch.empty_like(x, memory_format=torch.channels_last)
+        N, _, H, W = x.shape
+        if out_pad:
+            y = padded_empty(N, C, H, W, out_pad, x.device)
+        else:
+            y = torch.empty_like(x, memory_format=torch.channels_last)
+        ctx.dx_pad = dx_pad
         # forward and backward per-channel sums in one zeroed buffer (one fill, or a
         # slice of the caller's per-step zeroed arena); with have_stats the first 2C
         # already hold the forward statistics (emitted by the producing convolution's
@@ -47,11 +65,14 @@ class _BnAct(torch.autograd.Function):
         ctx.backwards = 0
         save = torch.empty(2 * C, device=x.device, dtype=torch.float32)
         res = residual.contiguous(memory_format=torch.channels_last) if residual is not None else None
-        native().bn_nhwc_fwd(x.data_ptr(), res.data_ptr() if res is not None else 0, y.data_ptr(), acc.data_ptr(),
-                             weight.data_ptr(), bias.data_ptr(), save.data_ptr(),
-                             running_mean.data_ptr() if running_mean is not None else 0,
-                             running_var.data_ptr() if running_var is not None else 0, M, C, float(eps),
-                             float(momentum), int(relu), int(have_stats), stream_handle())
+        # (with out_pad the kernel writes y's padded buffer: its origin is y.data_ptr()
+        # minus the interior offset)
+        ybase = y.data_ptr() - (out_pad * (W + 2 * out_pad) + out_pad) * C * 2 if out_pad else y.data_ptr()
+        native().bn_nhwc_fwd_pad(x.data_ptr(), res.data_ptr() if res is not None else 0, ybase, acc.data_ptr(),
+                                 weight.data_ptr(), bias.data_ptr(), save.data_ptr(),
+                                 running_mean.data_ptr() if running_mean is not None else 0,
+                                 running_var.data_ptr() if running_var is not None else 0, M, C, float(eps),
+                                 float(momentum), int(relu), int(have_stats), H, W, int(out_pad), stream_handle())
         ctx.has_res = residual is not None
         ctx.grads = grads
         ctx.res_sink = res_sink
@@ -69,7 +90,10 @@ class _BnAct(torch.autograd.Function):
         x, y, weight, bias, save, acc4 = ctx.saved_tensors
         M, C = _geom(x)
         dy = dy.contiguous(memory_format=torch.channels_last)
-        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        N, _, H, W = x.shape
+        p = ctx.dx_pad
+        dx = padded_empty(N, C, H, W, p, x.device) if p else torch.empty_like(x, memory_format=torch.channels_last)
+        dxbase = dx.data_ptr() - (p * (W + 2 * p) + p) * C * 2 if p else dx.data_ptr()
         dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
         acc = acc4[2 * C:]
         if ctx.backwards:  # the kernels accumulate atomically into the zeroed half: a second
@@ -80,22 +104,25 @@ class _BnAct(torch.autograd.Function):
         else:
             dw = torch.empty(C, device=x.device, dtype=torch.float32)
             db = torch.empty(C, device=x.device, dtype=torch.float32)
-        native().bn_nhwc_bwd(dy.data_ptr(), y.data_ptr() if y is not None else 0, x.data_ptr(), save.data_ptr(),
-                             weight.data_ptr(), bias.data_ptr(), acc.data_ptr(), dx.data_ptr(), dres.data_ptr() if dres is not None else 0, dw.data_ptr(),
-                             db.data_ptr(), M, C, ctx.relu, stream_handle())
+        native().bn_nhwc_bwd_pad(dy.data_ptr(), y.data_ptr() if y is not None else 0, x.data_ptr(), save.data_ptr(),
+                                 weight.data_ptr(), bias.data_ptr(), acc.data_ptr(), dxbase,
+                                 dres.data_ptr() if dres is not None else 0, dw.data_ptr(), db.data_ptr(), M, C,
+                                 ctx.relu, H, W, int(p), stream_handle())
         if ctx.res_sink is not None and dres is not None:
             ctx.res_sink["g"] = dres  # consumed by the conv whose input is the residual (ops/conv.py)
             dres = None
         if ctx.grads is not None:
             ready()
-            return dx, None, None, None, None, dres, None, None, None, None, None, None, None
-        return dx, dw.to(weight.dtype), db.to(weight.dtype), None, None, dres, None, None, None, None, None, None, None
+            return dx, None, None, None, None, dres, None, None, None, None, None, None, None, None, None
+        return (dx, dw.to(weight.dtype), db.to(weight.dtype), None, None, dres, None, None, None, None, None, None, None,
+                None, None)
 
 
 def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_mean: Optional[torch.Tensor],
            running_var: Optional[torch.Tensor], residual: Optional[torch.Tensor] = None, relu: bool = True,
            eps: float = 1e-5, momentum: float = 0.1, acc: Optional[torch.Tensor] = None,
-           grads=None, res_sink: Optional[dict] = None, have_stats: Optional[bool] = None) -> torch.Tensor:
+           grads=None, res_sink: Optional[dict] = None, have_stats: Optional[bool] = None, out_pad: int = 0,
+           dx_pad: int = 0) -> torch.Tensor:
     """``acc``: optional fp32 [4C] whose last 2C are zero; with ``have_stats``
     (the default when ``acc`` is given) its first 2C already hold the
     per-channel sum / sum of squares of x (see ops/conv.py Conv1x1), else they
@@ -105,7 +132,10 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
     gradient buffer) instead of returning them to autograd.
     ``res_sink``: a dict that receives the residual's gradient (key ``"g"``)
     instead of autograd, for a consumer that adds it itself (Conv1x1's dgrad
-    epilogue): saves the separate gradient-sum pass of a tensor used twice."""
+    epilogue): saves the separate gradient-sum pass of a tensor used twice.
+    ``out_pad`` / ``dx_pad``: write the output / the input gradient as the
+    interior of a zero-bordered buffer (:func:`padded_empty`) for a 3x3
+    convolution that reads it directly."""
     if not supported(x):
         raise ValueError(f"bn_act: needs a channels-last bf16 CUDA tensor with a supported channel count, got "
                          f"{tuple(x.shape)} {x.dtype} {x.device}")
@@ -115,7 +145,9 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
         raise ValueError("bn_act: weight / bias must be fp32")
     if acc is not None and (acc.numel() != 4 * x.shape[1] or acc.dtype != torch.float32):
         raise ValueError("bn_act: acc must be fp32 [4C]")
+    if out_pad and residual is not None:
+        raise ValueError("bn_act: out_pad with a residual is not supported (the backward reads y linearly)")
     if have_stats is None:
         have_stats = acc is not None
     return _BnAct.apply(x, weight.contiguous(), bias.contiguous(), running_mean, running_var, residual, relu, eps,
-                        momentum, acc, grads, res_sink, bool(have_stats))
+                        momentum, acc, grads, res_sink, bool(have_stats), int(out_pad), int(dx_pad))

@@ -234,6 +234,111 @@ class Conv1x1(torch.autograd.Function):
         return dx, None, None, None, None, None
 
 
+PAD_COPIES = [0]  # Conv3x3 inputs / gradients that had to be padded by a copy (tests)
+
+
+def _padded_base(t: torch.Tensor, pad: int):
+    """(tensor to keep alive, pointer of the [N][H+2p][W+2p][C] zero-bordered
+    buffer) for a [N, C, H, W] activation: ``t`` itself when it is the
+    interior view made by ops.bn_nhwc.padded_empty, else a padded copy."""
+    n, c, h, w = t.shape
+    hp, wp = h + 2 * pad, w + 2 * pad
+    if getattr(t, "_dl_pad", 0) == pad and t.stride() == (hp * wp * c, 1, wp * c, c):
+        return t, t.data_ptr() - (pad * wp + pad) * c * t.element_size()
+    PAD_COPIES[0] += 1
+    tp = F.pad(t.permute(0, 2, 3, 1), (0, 0, pad, pad, pad, pad)).contiguous()
+    return tp, tp.data_ptr()
+
+
+def conv3x3_supported(shape, cout: int, is_cuda: bool = True, dtype=BF16) -> bool:
+    """Whether Conv3x3 takes an input of ``shape`` [N, Cin, H, W]."""
+    n, cin, h, w = shape
+    pow2 = lambda v: v >= 64 and (v & (v - 1)) == 0  # noqa: E731
+    return (is_cuda and dtype == BF16 and pow2(cin) and pow2(cout) and n * h * w < (1 << 24)
+            and n * (h + 2) * (w + 2) * max(cin, cout) < (1 << 31))
+
+
+def _plan_3x3(M: int, N: int, K: int):
+    """Forward / dgrad plan of a 3x3 GEMM (packed tile id, splits): 2-stage
+    ring, 8 waves, no split -- the best of a stage/wave/tile/split sweep on
+    every ResNet-50 stride-1 3x3 shape (scripts/bench_conv3x3.py SWEEP=1,
+    profiles/r2_conv3x3_sweep.jsonl): 71-88 us vs MIOpen's 74-119 us forward."""
+    tile = 0 if N % 128 == 0 else 2
+    return tile | (2 << 4) | (8 << 8), 1
+
+
+def _wgrad_plan_3x3(cout: int, K: int, M: int):
+    """Weight-gradient plan (tile, splits) of a 3x3 conv: about one round of
+    workgroups, two when the tiles alone nearly fill the chip (same sweep)."""
+    tile = 2 if cout % 128 == 0 else 1
+    bm, bn = (128, 128) if tile == 2 else (64, 64)
+    tiles = (cout // bm) * ((K + bn - 1) // bn)
+    splits = max(1, (256 if tiles <= 64 else 512) // tiles)
+    return tile, max(1, min(splits, M // 512))
+
+
+class Conv3x3(torch.autograd.Function):
+    """Stride-1 3x3 convolution (pad 1) on the hand-written implicit-GEMM
+    kernels (csrc/kernels/conv_igemm.hip streaming kernel: any H, W), reading
+    the channels-last shadow ``bind.wcl`` ([Cout][3][3][Cin] in memory) and a
+    zero-bordered input; the weight gradient is split-K slabs reduce-added into
+    the flat gradient in PyTorch's [Cout][Cin][3][3] order.  The padded input
+    and the padded output gradient come straight from the BatchNorm kernels
+    (bn_act out_pad / dx_pad) when the model wires them, else from a pad copy.
+    ``stats``: fp32 [2*Cout] <- the output's per-channel sum / sum of squares
+    (GEMM epilogue rows, as Conv1x1)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bind: ShadowBinding, stats):
+        C = native()
+        N, cin, H, W = x.shape
+        cout = weight.shape[0]
+        keep, xbase = _padded_base(x, 1)
+        M, K = N * H * W, 9 * cin
+        y = torch.empty((N, cout, H, W), dtype=BF16, device=x.device, memory_format=torch.channels_last)
+        tile, splits = _plan_3x3(M, cout, K)
+        slab = torch.empty(splits * M * cout, device=x.device) if splits > 1 else None
+        rows = None
+        s = stream_handle()
+        if stats is not None:
+            if C.reduce_atomic() != 0:
+                raise RuntimeError("Conv3x3 statistics need reduction mode 0 (partial rows)")
+            nrows = C.conv_fwd_stat_rows(N, H, W, cin, cout, 3, tile, splits)
+            rows = torch.empty(max(nrows, 400 if splits > 1 else 1), 2, cout, device=x.device)
+        T = C.conv_fwd(xbase, bind.wcl.data_ptr(), y.data_ptr(), 0 if rows is None else rows.data_ptr(),
+                       0 if slab is None else slab.data_ptr(), N, H, W, cin, cout, 3, tile, splits, s)
+        if rows is not None:
+            C.bn_rows_reduce(rows.data_ptr(), T, cout, stats.data_ptr(), s)
+        ctx.save_for_backward(keep)
+        ctx.xbase, ctx.bind, ctx.geom = xbase, bind, (N, cin, H, W, cout)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        N, cin, H, W, cout = ctx.geom
+        bind = ctx.bind
+        s = stream_handle()
+        keep_dy, dybase = _padded_base(dy, 1)
+        M, K = N * H * W, 9 * cin
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wt = torch.empty(cin, 3, 3, cout, dtype=BF16, device=dy.device)
+            C.weight_flip_transpose(bind.wcl.data_ptr(), wt.data_ptr(), cout, cin, 3, s)
+            dx = torch.empty((N, cin, H, W), dtype=BF16, device=dy.device, memory_format=torch.channels_last)
+            dt, ds = _plan_3x3(M, cin, 9 * cout)
+            slab = torch.empty(ds * M * cin, device=dy.device) if ds > 1 else None
+            C.conv_fwd(dybase, wt.data_ptr(), dx.data_ptr(), 0, 0 if slab is None else slab.data_ptr(), N, H, W,
+                       cout, cin, 3, dt, ds, s)
+        tile, splits = _wgrad_plan_3x3(cout, K, M)
+        ws = torch.empty(splits * cout * K, device=dy.device)
+        C.conv_wgrad(dybase, ctx.xbase, ws.data_ptr(), N, H, W, cin, cout, 3, splits, K, tile, 0, s)
+        C.slab_reduce_add_oihw(ws.data_ptr(), bind.g32.data_ptr(), splits, cout, 9, cin, cin, s)
+        bind.ready()
+        del keep_dy
+        return dx, None, None, None
+
+
 class ShadowConv(torch.autograd.Function):
     """MIOpen convolution on the bf16 shadow weight; fp32 weight gradient
     added into the flat buffer."""
