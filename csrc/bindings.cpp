@@ -67,15 +67,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_relu_pool_bwd_apply", &bn_relu_pool_bwd_apply);
   m.def("bn_relu_pool_bwd_apply_sums", &bn_relu_pool_bwd_apply_sums);
   m.def("bn_relu_pool_fwd_fin", &bn_relu_pool_fwd_fin);
-  // reduction mode of the BN statistics / gradients (0: deterministic partial
-  // rows + finalize kernels, 1: atomic per-channel totals, no finalize launches)
-  static int g_host_red_atomic = 0;  // mirrors the device flags (default 0 = partial rows)
-  m.def("set_reduce_atomic", [](int on) {
-    set_reduce_atomic_conv(on);
-    set_reduce_atomic_bn(on);
-    g_host_red_atomic = on ? 1 : 0;
+  // reduction mode of the BN statistics / gradients: 0 = deterministic partial
+  // rows + finalize kernels; R >= 1 (power of two) = atomic per-channel totals
+  // striped over R rows, no finalize launches.  reduce_atomic() returns R.
+  m.def("set_reduce_atomic", [](int rows) {
+    set_reduce_atomic_conv(rows);
+    set_reduce_atomic_bn(rows);
   });
-  m.def("reduce_atomic", []() { return g_host_red_atomic; });
+  m.def("reduce_atomic", []() { return reduce_rows(); });
   m.def("head_fwd_bwd", &head_fwd_bwd);
   m.def("head_fwd_bwd_pool", &head_fwd_bwd_pool);
   m.def("bn_bwd_reduce_head", &bn_bwd_reduce_head);

@@ -57,7 +57,7 @@ void set_conv_waves(int waves);
 void set_conv_debug(uintptr_t buf);
 void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, int Cin, int Cout, int KS, int splits,
                 int ldo, int tile, int atomic_creal, uintptr_t stream);
-void set_reduce_atomic_conv(int on);
+void set_reduce_atomic_conv(int rows);
 void conv_fwd_add(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t addend, int B, int H, int W, int Cin, int Cout,
                   int KS, int tile, uintptr_t stream);
 void set_conv_fwd_tr(int on);
@@ -96,11 +96,13 @@ void bn_bwd_finalize(uintptr_t partial, int T, int C, int64_t M, uintptr_t gamma
 void bn_relu_pool_bwd_apply(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t acoef, uintptr_t dy, int B, int H,
                             int W, int C, int opad, uintptr_t stream);
 void bn_relu_pool_bwd_apply_sums(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t dgb, uintptr_t gamma, int64_t M,
-                                 uintptr_t dy, int B, int H, int W, int C, int opad, uintptr_t stream);
+                                 uintptr_t dy, int B, int H, int W, int C, int opad, uintptr_t dgamma_out,
+                                 uintptr_t dbeta_out, uintptr_t stream);
 void bn_relu_pool_fwd_fin(uintptr_t y, uintptr_t sums, int64_t M, uintptr_t gamma, uintptr_t beta, uintptr_t bias,
                           uintptr_t rmean, uintptr_t rvar, float eps, float momentum, uintptr_t coef, uintptr_t out,
                           int B, int H, int W, int C, int opad, uintptr_t stream);
-void set_reduce_atomic_bn(int on);
+void set_reduce_atomic_bn(int rows);
+int reduce_rows();
 
 // head.hip --------------------------------------------------------------------
 void head_fwd_bwd(uintptr_t h, uintptr_t w, uintptr_t bias, uintptr_t labels, int F, int B, int NC,

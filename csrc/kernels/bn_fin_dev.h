@@ -1,10 +1,11 @@
 // Train-mode BatchNorm coefficients derived in the CONSUMER kernel from the
-// atomically accumulated per-channel totals (reduction mode 1, see
-// conv_igemm.hip g_red_atomic): sums = [2][C] (sum, sum of squares) of the M
-// bf16 conv outputs.  Every thread derives the scale/shift of the channels it
-// touches (a few flops), and block 0 publishes the full coefficient table
-// coef [4][C] (mean, invstd, scale, shift -- what the backward kernels read)
-// and updates the running statistics: the bn_finalize launch is gone.
+// atomically accumulated per-channel totals (atomic reduction modes, see
+// conv_igemm.hip g_red_atomic): sums = R rows of [2][C] (sum, sum of squares)
+// of the M bf16 conv outputs, summed here in a fixed order.  Every block
+// derives the scale/shift of all channels into LDS (a few flops), and block 0
+// publishes the full coefficient table coef [4][C] (mean, invstd, scale, shift
+// -- what the backward kernels read) and updates the running statistics: the
+// bn_finalize launch is gone.
 // Identical arithmetic to bn_finalize_kernel, so both modes give the same
 // coefficients for the same totals.
 #pragma once
@@ -13,7 +14,7 @@
 namespace dl {
 
 struct BnFin {
-  const float* sums;  // [2][C]; nullptr: coefficients are read from coef (mode 0 / eval)
+  const float* sums;  // [R][2][C]; nullptr: coefficients are read from coef (mode 0 / eval)
   const float* gamma;
   const float* beta;
   const float* bias;  // conv bias (running mean bookkeeping), may be null
@@ -22,49 +23,92 @@ struct BnFin {
   float* coef;        // [4][C] written by block 0
   int64_t M;
   float eps, momentum;
+  int R;              // accumulated rows in sums
 };
+
+constexpr int kFinMaxC = 1024;  // channels of the block-cooperative (LDS) coefficient tables
+constexpr int kMaxRows = 32;    // accumulated rows (set_reduce_atomic caps R at 64; the executors use <= 32)
+
+// t1 = sum_r p[r*stride], t2 = sum_r p[r*stride + off2] over r < R, in row
+// order.  Every load is issued before the first add (straight-line code per
+// row count): the rows were just written by memory-side atomics, so each
+// load is a full memory round trip, and a dependent chain of R of them cost
+// ~0.5 us per row (measured: 4-8 us per consumer kernel at R = 16).
+template <int RR>
+__device__ __forceinline__ void sum_rows2_t(const float* __restrict__ p, int stride, int off2, float& t1, float& t2) {
+  float a[RR], b[RR];
+#pragma unroll
+  for (int r = 0; r < RR; ++r) {
+    a[r] = p[(int64_t)r * stride];
+    b[r] = p[(int64_t)r * stride + off2];
+  }
+  t1 = 0.f;
+  t2 = 0.f;
+#pragma unroll
+  for (int r = 0; r < RR; ++r) { t1 += a[r]; t2 += b[r]; }
+}
+
+__device__ __forceinline__ void sum_rows2(const float* __restrict__ p, int stride, int off2, int R, float& t1,
+                                          float& t2) {
+  switch (R) {  // wave-uniform; R is a power of two <= kMaxRows (host-checked)
+    case 1: sum_rows2_t<1>(p, stride, off2, t1, t2); break;
+    case 2: sum_rows2_t<2>(p, stride, off2, t1, t2); break;
+    case 4: sum_rows2_t<4>(p, stride, off2, t1, t2); break;
+    case 8: sum_rows2_t<8>(p, stride, off2, t1, t2); break;
+    case 16: sum_rows2_t<16>(p, stride, off2, t1, t2); break;
+    default: sum_rows2_t<32>(p, stride, off2, t1, t2); break;
+  }
+}
 
 __device__ __forceinline__ void bn_fin_channel(const BnFin& f, int C, int c, float& mean, float& var, float& invstd,
                                                float& sc, float& sh) {
-  const float t1 = f.sums[c], t2 = f.sums[C + c];
+  const float gam = f.gamma[c], bet = f.beta[c];  // issued with (not after) the row loads
+  float t1, t2;
+  sum_rows2(f.sums + c, 2 * C, C, f.R, t1, t2);
   mean = t1 / (float)f.M;
   var = fmaxf(t2 / (float)f.M - mean * mean, 0.f);
   invstd = rsqrtf(var + f.eps);
-  sc = f.gamma[c] * invstd;
-  sh = f.beta[c] - mean * sc;
+  sc = gam * invstd;
+  sh = bet - mean * sc;
 }
 
-// scale / shift of channels c0..c0+7
-__device__ __forceinline__ void bn_fin_coef8(const BnFin& f, int C, int c0, float* sc, float* sh) {
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    float mean, var, invstd;
-    bn_fin_channel(f, C, c0 + k, mean, var, invstd, sc[k], sh[k]);
-  }
+// LDS-only block barrier: global loads issued before it stay in flight (a
+// consumer issues its first item's loads, then derives the coefficients, so
+// the two memory round trips overlap instead of adding up).
+__device__ __forceinline__ static void fin_block_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
-// block 0: coefficient table + running statistics
-__device__ __forceinline__ void bn_fin_publish(const BnFin& f, int C) {
-  if (blockIdx.x != 0) return;
+// Block-cooperative: scale / shift of ALL C channels into LDS (ssc, ssh [C]),
+// each channel's rows summed once per block instead of once per thread;
+// block 0 also publishes coef + running statistics.  Ends with an LDS barrier.
+__device__ __forceinline__ void bn_fin_block(const BnFin& f, int C, float* ssc, float* ssh) {
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float mean, var, invstd, sc, sh;
     bn_fin_channel(f, C, c, mean, var, invstd, sc, sh);
-    f.coef[c] = mean;
-    f.coef[C + c] = invstd;
-    f.coef[2 * C + c] = sc;
-    f.coef[3 * C + c] = sh;
-    if (f.rmean != nullptr) {
-      const float unbiased = f.M > 1 ? var * (float)f.M / (float)(f.M - 1) : var;
-      f.rmean[c] = (1.f - f.momentum) * f.rmean[c] + f.momentum * (mean + (f.bias ? f.bias[c] : 0.f));
-      f.rvar[c] = (1.f - f.momentum) * f.rvar[c] + f.momentum * unbiased;
+    ssc[c] = sc;
+    ssh[c] = sh;
+    if (blockIdx.x == 0) {
+      f.coef[c] = mean;
+      f.coef[C + c] = invstd;
+      f.coef[2 * C + c] = sc;
+      f.coef[3 * C + c] = sh;
+      if (f.rmean != nullptr) {
+        const float unbiased = f.M > 1 ? var * (float)f.M / (float)(f.M - 1) : var;
+        f.rmean[c] = (1.f - f.momentum) * f.rmean[c] + f.momentum * (mean + (f.bias ? f.bias[c] : 0.f));
+        f.rvar[c] = (1.f - f.momentum) * f.rvar[c] + f.momentum * unbiased;
+      }
     }
   }
+  fin_block_sync();
 }
 
 inline BnFin make_bn_fin(uintptr_t sums, int64_t M, uintptr_t gamma, uintptr_t beta, uintptr_t bias, uintptr_t rmean,
-                         uintptr_t rvar, float eps, float momentum, uintptr_t coef) {
+                         uintptr_t rvar, float eps, float momentum, uintptr_t coef, int R) {
   return BnFin{(const float*)sums, (const float*)gamma, (const float*)beta, (const float*)bias, (float*)rmean,
-               (float*)rvar, (float*)coef, M, eps, momentum};
+               (float*)rvar, (float*)coef, M, eps, momentum, R};
 }
 
 }  // namespace dl

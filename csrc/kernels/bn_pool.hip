@@ -28,10 +28,13 @@
 namespace dl {
 
 // reduction mode (conv_igemm.hip g_red_atomic; set together by set_reduce_atomic):
-// 1 = the backward reduce atomically adds its per-block totals into the BN
-// parameter gradients [dgamma (C) ; dbeta (C)] (zeroed by the step's prep
-// kernel), and the apply kernel derives its coefficients from them.
+// R >= 1 = the backward reduce atomically adds its per-block totals into row
+// (block & (R-1)) of R zeroed [dgamma (C) ; dbeta (C)] rows (R = 1: straight
+// into the BN parameter gradients of the flat buffer), and the apply kernel
+// sums the rows and derives its coefficients from them.
 __device__ int g_red_atomic_bn = 0;
+static int g_host_rows = 0;  // host mirror (BnFin::R of the launchers)
+int reduce_rows() { return g_host_rows; }
 
 __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
   f[0] = lo_bf16(v.x); f[1] = hi_bf16(v.x); f[2] = lo_bf16(v.y); f[3] = hi_bf16(v.y);
@@ -167,51 +170,63 @@ __global__ void __launch_bounds__(256) bn_relu_pool_fwd_kernel(const bf16_t* __r
 __global__ void __launch_bounds__(256) bn_relu_pool_fwd_fin_kernel(const bf16_t* __restrict__ y, const BnFin fin,
                                                                    bf16_t* __restrict__ out, int B, int H, int W, int C,
                                                                    int opad) {
-  bn_fin_publish(fin, C);
+  __shared__ float ssc[kFinMaxC], ssh[kFinMaxC];
   const int C8 = C >> 3, Ho = H >> 1, Wo = W >> 1;
   const int Hop = Ho + 2 * opad, Wop = Wo + 2 * opad;
   const int64_t total = (int64_t)B * Ho * Wo * C8;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int cur = -1;
-  float sc[8], sh[8];
-  for (; i < total; i += stride) {
+  auto item_base = [&](int64_t i, int& c0, int64_t& pix) {
     const int c8 = (int)(i % C8);
-    const int64_t pix = i / C8;
+    pix = i / C8;
+    c0 = c8 * 8;
     const int ow = (int)(pix % Wo);
     const int64_t t = pix / Wo;
     const int oh = (int)(t % Ho);
     const int64_t b = t / Ho;
-    const int c0 = c8 * 8;
-    if (c8 != cur) {  // the chunk is fixed per thread whenever C8 divides the stride
-      bn_fin_coef8(fin, C, c0, sc, sh);
-      cur = c8;
-    }
-    const bf16_t* base = y + (((b * H + 2 * oh) * W) + 2 * ow) * (int64_t)C + c0;
-    const uint4 v0 = *reinterpret_cast<const uint4*>(base);
-    const uint4 v1 = *reinterpret_cast<const uint4*>(base + C);
-    const uint4 v2 = *reinterpret_cast<const uint4*>(base + (int64_t)W * C);
-    const uint4 v3 = *reinterpret_cast<const uint4*>(base + (int64_t)W * C + C);
-    float f[8], mx[8];
-    unpack8(v0, f);
+    return y + (((b * H + 2 * oh) * W) + 2 * ow) * (int64_t)C + c0;
+  };
+  auto load4 = [&](const bf16_t* base, uint4 (&v)[4]) {
+    v[0] = *reinterpret_cast<const uint4*>(base);
+    v[1] = *reinterpret_cast<const uint4*>(base + C);
+    v[2] = *reinterpret_cast<const uint4*>(base + (int64_t)W * C);
+    v[3] = *reinterpret_cast<const uint4*>(base + (int64_t)W * C + C);
+  };
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint4 v[4];
+  int c0 = 0;
+  int64_t pix = 0;
+  if (i < total) load4(item_base(i, c0, pix), v);  // in flight across the coefficient prologue
+  bn_fin_block(fin, C, ssc, ssh);
+  for (; i < total;) {
+    float sc[8], sh[8], f[8], mx[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { sc[k] = ssc[c0 + k]; sh[k] = ssh[c0 + k]; }
+    unpack8(v[0], f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) mx[k] = fmaf(sc[k], f[k], sh[k]);
-    unpack8(v1, f);
+    unpack8(v[1], f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) mx[k] = fmaxf(mx[k], fmaf(sc[k], f[k], sh[k]));
-    unpack8(v2, f);
+    unpack8(v[2], f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) mx[k] = fmaxf(mx[k], fmaf(sc[k], f[k], sh[k]));
-    unpack8(v3, f);
+    unpack8(v[3], f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) mx[k] = fmaxf(fmaxf(mx[k], fmaf(sc[k], f[k], sh[k])), 0.f);
-    *reinterpret_cast<uint4*>(out + ((b * Hop + oh + opad) * Wop + ow + opad) * (int64_t)C + c0) = pack8(mx);
+    const int ow = (int)(pix % Wo);
+    const int64_t t = pix / Wo;
+    const int oh = (int)(t % Ho);
+    const int64_t b = t / Ho;
+    bf16_t* o = out + ((b * Hop + oh + opad) * Wop + ow + opad) * (int64_t)C + c0;
+    i += stride;
+    if (i < total) load4(item_base(i, c0, pix), v);
+    *reinterpret_cast<uint4*>(o) = pack8(mx);
   }
 }
 
-// Recompute the backward signal of one pooled pixel x 8 channels:
-// dz[w][k] = dP[k] at the first (row-major) window position holding the max of
-// relu(z) if that z > 0, else 0; xh[w][k] = (y - mean) * invstd.
+// Backward signal of one pooled pixel x 8 channels: dz[w][k] = dP[k] at the
+// first (row-major) window position holding the max of relu(z) if that z > 0,
+// else 0; xh[w][k] = (y - mean) * invstd.
 struct BwdCtx {
   float sc[8], sh[8], mu[8], is[8];
 };
@@ -219,29 +234,6 @@ struct BwdCtx {
 __device__ __forceinline__ void load8(float* d, const float* s) {
   *reinterpret_cast<float4*>(d) = *reinterpret_cast<const float4*>(s);
   *reinterpret_cast<float4*>(d + 4) = *reinterpret_cast<const float4*>(s + 4);
-}
-
-__device__ __forceinline__ void bwd_window(const bf16_t* __restrict__ y, const bf16_t* __restrict__ dP,
-                                           const BwdCtx& cx, int64_t b, int oh, int ow, int H, int W, int C, int c0,
-                                           float (&yv)[4][8], float (&dz)[4][8]) {
-  const bf16_t* base = y + (((b * H + 2 * oh) * W) + 2 * ow) * (int64_t)C + c0;
-  const int64_t offs[4] = {0, C, (int64_t)W * C, (int64_t)W * C + C};
-#pragma unroll
-  for (int w = 0; w < 4; ++w) unpack8(*reinterpret_cast<const uint4*>(base + offs[w]), yv[w]);
-  float g[8];
-  unpack8(*reinterpret_cast<const uint4*>(dP + (((b * (H >> 1) + oh) * (W >> 1)) + ow) * (int64_t)C + c0), g);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    float best = -INFINITY;
-    int arg = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const float r = fmaxf(fmaf(cx.sc[k], yv[w][k], cx.sh[k]), 0.f);
-      if (r > best) { best = r; arg = w; }
-    }
-#pragma unroll
-    for (int w = 0; w < 4; ++w) dz[w][k] = (w == arg && best > 0.f) ? g[k] : 0.f;
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -329,9 +321,10 @@ __device__ __forceinline__ void bwd_reduce_body(const bf16_t* __restrict__ y, co
     const int first = (int)(((int64_t)ch - ((int64_t)bid * blockDim.x) % C8 + C8) % C8);
     float a = 0.f, bsum = 0.f;
     for (int t = first; t < (int)blockDim.x; t += C8) { a += red[t][k]; bsum += red[t][8 + k]; }
-    if (g_red_atomic_bn) {  // partial = [dgamma ; dbeta] = [sum dz*xhat ; sum dz]
-      unsafeAtomicAdd(partial + c, bsum);
-      unsafeAtomicAdd(partial + C + c, a);
+    if (const int R = g_red_atomic_bn) {  // rows of [dgamma ; dbeta] = [sum dz*xhat ; sum dz]
+      float* p = partial + (int64_t)(bid & (R - 1)) * 2 * C;
+      unsafeAtomicAdd(p + c, bsum);
+      unsafeAtomicAdd(p + C + c, a);
     } else {
       partial[(int64_t)bid * 2 * C + c] = a;
       partial[(int64_t)bid * 2 * C + C + c] = bsum;
@@ -392,8 +385,12 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
   }
 }
 
-// SUMS: acoef is the accumulated [dgamma ; dbeta] (mode 1) and the apply
-// coefficients are derived here: a = gamma*invstd, b = -a*dgamma/M, c = -a*dbeta/M.
+// SUMS: acoef holds R accumulated rows of [dgamma ; dbeta] (reduction mode
+// R >= 1); every block sums them in a fixed order and derives the apply
+// coefficients a = gamma*invstd, b = -a*dgamma/M, c = -a*dbeta/M in LDS
+// (the first item's loads are already in flight); block 0 also writes the
+// totals to dgamma_out / dbeta_out (R > 1: the flat gradient; R = 1
+// accumulated there directly and passes null).
 template <bool SUMS>
 __global__ void __launch_bounds__(256) bn_relu_pool_bwd_apply_kernel(const bf16_t* __restrict__ y,
                                                                      const bf16_t* __restrict__ dP,
@@ -401,19 +398,48 @@ __global__ void __launch_bounds__(256) bn_relu_pool_bwd_apply_kernel(const bf16_
                                                                      const float* __restrict__ acoef,
                                                                      bf16_t* __restrict__ dy, int B, int H, int W,
                                                                      int C, int opad, const float* __restrict__ gamma,
-                                                                     float inv_m) {
+                                                                     float inv_m, int R, float* __restrict__ dgamma_out,
+                                                                     float* __restrict__ dbeta_out) {
   // dy: [B][H+2 opad][W+2 opad][C], written in the interior (zero border =
   // the dgrad convolution's spatial padding)
+  __shared__ float sk[SUMS ? 3 : 1][SUMS ? kFinMaxC : 1];
   const int C8 = C >> 3, Ho = H >> 1, Wo = W >> 1;
   const int Hp = H + 2 * opad, Wp = W + 2 * opad;
   const int64_t total = (int64_t)B * Ho * Wo * C8;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int c8 = (int)(i % C8), c0 = c8 * 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int c0 = 0, oh = 0, ow = 0;
+  int64_t b = 0;
+  uint4 yw[4], gv;
+  auto item_loads = [&](int64_t i) {
+    c0 = (int)(i % C8) * 8;
     const int64_t pix = i / C8;
-    const int ow = (int)(pix % Wo);
+    ow = (int)(pix % Wo);
     const int64_t t = pix / Wo;
-    const int oh = (int)(t % Ho);
-    const int64_t b = t / Ho;
+    oh = (int)(t % Ho);
+    b = t / Ho;
+    const bf16_t* base = y + (((b * H + 2 * oh) * W) + 2 * ow) * (int64_t)C + c0;
+    yw[0] = *reinterpret_cast<const uint4*>(base);
+    yw[1] = *reinterpret_cast<const uint4*>(base + C);
+    yw[2] = *reinterpret_cast<const uint4*>(base + (int64_t)W * C);
+    yw[3] = *reinterpret_cast<const uint4*>(base + (int64_t)W * C + C);
+    gv = *reinterpret_cast<const uint4*>(dP + (((b * Ho + oh) * Wo) + ow) * (int64_t)C + c0);
+  };
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < total) item_loads(i);
+  if constexpr (SUMS) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      const float gam = gamma[c], istd = coef[C + c];  // issued with (not after) the row loads
+      float dg, db;
+      sum_rows2(acoef + c, 2 * C, C, R, dg, db);
+      const float a = gam * istd;
+      sk[0][c] = a;
+      sk[1][c] = -a * dg * inv_m;
+      sk[2][c] = -a * db * inv_m;
+      if (blockIdx.x == 0 && dgamma_out != nullptr) { dgamma_out[c] = dg; dbeta_out[c] = db; }
+    }
+    fin_block_sync();
+  }
+  for (; i < total;) {
     BwdCtx cx;
     load8(cx.mu, coef + c0);
     load8(cx.is, coef + C + c0);
@@ -421,32 +447,43 @@ __global__ void __launch_bounds__(256) bn_relu_pool_bwd_apply_kernel(const bf16_
     load8(cx.sh, coef + 3 * C + c0);
     float ka[8], kb[8], kc[8];
     if constexpr (SUMS) {
-      float gm[8], dg[8], db[8];
-      load8(gm, gamma + c0);
-      load8(dg, acoef + c0);
-      load8(db, acoef + C + c0);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        ka[k] = gm[k] * cx.is[k];
-        kb[k] = -ka[k] * dg[k] * inv_m;
-        kc[k] = -ka[k] * db[k] * inv_m;
-      }
+      for (int k = 0; k < 8; ++k) { ka[k] = sk[0][c0 + k]; kb[k] = sk[1][c0 + k]; kc[k] = sk[2][c0 + k]; }
     } else {
       load8(ka, acoef + c0);
       load8(kb, acoef + C + c0);
       load8(kc, acoef + 2 * C + c0);
     }
-    float yv[4][8], dz[4][8];
-    bwd_window(y, dP, cx, b, oh, ow, H, W, C, c0, yv, dz);
-    bf16_t* base = dy + (((b * Hp + 2 * oh + opad) * Wp) + 2 * ow + opad) * (int64_t)C + c0;
-    const int64_t offs[4] = {0, C, (int64_t)Wp * C, (int64_t)Wp * C + C};
+    float yv[4][8], g[8], dz[4][8];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) unpack8(yw[w], yv[w]);
+    unpack8(gv, g);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float best = -INFINITY;
+      int arg = 0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float r = fmaxf(fmaf(cx.sc[k], yv[w][k], cx.sh[k]), 0.f);
+        if (r > best) { best = r; arg = w; }
+      }
+#pragma unroll
+      for (int w = 0; w < 4; ++w) dz[w][k] = (w == arg && best > 0.f) ? g[k] : 0.f;
+    }
+    uint4 o4[4];
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       float o[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) o[k] = ka[k] * dz[w][k] + kb[k] * ((yv[w][k] - cx.mu[k]) * cx.is[k]) + kc[k];
-      *reinterpret_cast<uint4*>(base + offs[w]) = pack8(o);
+      o4[w] = pack8(o);
     }
+    bf16_t* base = dy + (((b * Hp + 2 * oh + opad) * Wp) + 2 * ow + opad) * (int64_t)C + c0;
+    const int64_t offs[4] = {0, C, (int64_t)Wp * C, (int64_t)Wp * C + C};
+    i += stride;
+    if (i < total) item_loads(i);  // next item's loads before this item's stores
+#pragma unroll
+    for (int w = 0; w < 4; ++w) *reinterpret_cast<uint4*>(base + offs[w]) = o4[w];
   }
 }
 
@@ -533,18 +570,25 @@ void bn_relu_pool_bwd_apply(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t
   const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
   bn_relu_pool_bwd_apply_kernel<false><<<stream_grid(total), 256, 0, as_stream(stream)>>>(
       (const bf16_t*)y, (const bf16_t*)dP, (const float*)coef, (const float*)acoef, (bf16_t*)dy, B, H, W, C, opad,
-      nullptr, 0.f);
+      nullptr, 0.f, 0, nullptr, nullptr);
   DL_HIP_CHECK(hipGetLastError());
 }
 
-// mode 1: dgb = [dgamma ; dbeta] accumulated by the reduce (no bn_bwd_finalize launch)
+// atomic modes: dgb = the reduce's g_host_rows accumulated rows of [dgamma ; dbeta]
+// (no bn_bwd_finalize launch); dgamma_out / dbeta_out receive the totals (0: the
+// single row already is the flat gradient)
 void bn_relu_pool_bwd_apply_sums(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t dgb, uintptr_t gamma, int64_t M,
-                                 uintptr_t dy, int B, int H, int W, int C, int opad, uintptr_t stream) {
+                                 uintptr_t dy, int B, int H, int W, int C, int opad, uintptr_t dgamma_out,
+                                 uintptr_t dbeta_out, uintptr_t stream) {
   check_c(C);
+  if (C > kFinMaxC) throw std::runtime_error("bn_relu_pool_bwd_apply_sums: C too large");
+  if (g_host_rows < 1 || g_host_rows > kMaxRows)
+    throw std::runtime_error("bn_relu_pool_bwd_apply_sums: needs an atomic reduction mode with <= 32 rows");
+  if ((dgamma_out == 0) != (dbeta_out == 0)) throw std::runtime_error("bn_relu_pool_bwd_apply_sums: dgamma/dbeta");
   const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
   bn_relu_pool_bwd_apply_kernel<true><<<stream_grid(total), 256, 0, as_stream(stream)>>>(
       (const bf16_t*)y, (const bf16_t*)dP, (const float*)coef, (const float*)dgb, (bf16_t*)dy, B, H, W, C, opad,
-      (const float*)gamma, 1.0f / (float)M);
+      (const float*)gamma, 1.0f / (float)M, g_host_rows, (float*)dgamma_out, (float*)dbeta_out);
   DL_HIP_CHECK(hipGetLastError());
 }
 
@@ -553,16 +597,22 @@ void bn_relu_pool_fwd_fin(uintptr_t y, uintptr_t sums, int64_t M, uintptr_t gamm
                           uintptr_t rmean, uintptr_t rvar, float eps, float momentum, uintptr_t coef, uintptr_t out,
                           int B, int H, int W, int C, int opad, uintptr_t stream) {
   check_c(C);
+  if (C > kFinMaxC) throw std::runtime_error("bn_relu_pool_fwd_fin: C too large");
+  if (g_host_rows < 1 || g_host_rows > kMaxRows)
+    throw std::runtime_error("bn_relu_pool_fwd_fin: needs an atomic reduction mode with <= 32 rows");
   const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
-  const BnFin fin = make_bn_fin(sums, M, gamma, beta, bias, rmean, rvar, eps, momentum, coef);
+  const BnFin fin = make_bn_fin(sums, M, gamma, beta, bias, rmean, rvar, eps, momentum, coef, g_host_rows);
   bn_relu_pool_fwd_fin_kernel<<<stream_grid(total), 256, 0, as_stream(stream)>>>((const bf16_t*)y, fin,
                                                                                    (bf16_t*)out, B, H, W, C, opad);
   DL_HIP_CHECK(hipGetLastError());
 }
 
-void set_reduce_atomic_bn(int on) {
-  const int v = on ? 1 : 0;
+void set_reduce_atomic_bn(int rows) {
+  if (rows < 0 || rows > 64 || (rows & (rows - 1)) != 0)
+    throw std::runtime_error("set_reduce_atomic: rows must be 0 or a power of two <= 64");
+  const int v = rows;
   DL_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_red_atomic_bn), &v, sizeof(int)));
+  g_host_rows = rows;
 }
 
 }  // namespace dl

@@ -63,9 +63,11 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
                           *reinterpret_cast<const uint4*>(base + (int64_t)hp.yW * hp.yC),
                           *reinterpret_cast<const uint4*>(base + (int64_t)hp.yW * hp.yC + hp.yC)};
       float sc[8], sh[8];
-      if (hp.fin.sums != nullptr) {
-        bn_fin_publish(hp.fin, hp.yC);
-        bn_fin_coef8(hp.fin, hp.yC, c0, sc, sh);
+      if (hp.fin.sums != nullptr) {  // uniform over the block (bn_fin_block ends with a barrier)
+        __shared__ float ssc[kFinMaxC], ssh[kFinMaxC];
+        bn_fin_block(hp.fin, hp.yC, ssc, ssh);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { sc[k] = ssc[c0 + k]; sh[k] = ssh[c0 + k]; }
       } else {
         const float4 sc0 = *reinterpret_cast<const float4*>(hp.coef + 2 * hp.yC + c0);
         const float4 sc1 = *reinterpret_cast<const float4*>(hp.coef + 2 * hp.yC + c0 + 4);
@@ -207,7 +209,7 @@ void head_fwd_bwd(uintptr_t h, uintptr_t w, uintptr_t bias, uintptr_t labels, in
   DL_HIP_CHECK(hipGetLastError());
 }
 
-// fin_sums != 0 (mode 1): the last block's BN coefficients are derived from
+// fin_sums != 0 (atomic modes, reduce_rows() rows): the last block's BN coefficients are derived from
 // the accumulated statistics (block 0 also publishes coef + running stats)
 void head_fwd_bwd_pool(uintptr_t y, uintptr_t coef, int yH, int yW, int yC, uintptr_t h_out, uintptr_t w,
                        uintptr_t bias, uintptr_t labels, int B, int NC, uintptr_t logits_out, uintptr_t dlogits,
@@ -218,8 +220,10 @@ void head_fwd_bwd_pool(uintptr_t y, uintptr_t coef, int yH, int yW, int yC, uint
   const int F = (yH / 2) * (yW / 2) * yC;
   if (F != 2048 || yC % 8 != 0 || yH % 2 != 0 || yW % 2 != 0)
     throw std::runtime_error("head_fwd_bwd_pool: needs a 2048-feature pooled map, C % 8 == 0");
+  if (fin_sums != 0 && (reduce_rows() < 1 || reduce_rows() > kMaxRows || yC > kFinMaxC))
+    throw std::runtime_error("head_fwd_bwd_pool: accumulated statistics need an atomic reduction mode");
   const HeadPool hp{(const bf16_t*)y, (const float*)coef, (bf16_t*)h_out, yH, yW, yC,
-                    make_bn_fin(fin_sums, fin_m, gamma, beta, conv_bias, rmean, rvar, eps, momentum, coef)};
+                    make_bn_fin(fin_sums, fin_m, gamma, beta, conv_bias, rmean, rvar, eps, momentum, coef, reduce_rows())};
   head_fwd_bwd_kernel<10, true><<<B, 256, 0, as_stream(stream)>>>(
       nullptr, (const float*)w, (const float*)bias, (const int64_t*)labels, F, B, (float*)logits_out,
       (float*)dlogits, (float*)loss_b, (bf16_t*)dh, hp);

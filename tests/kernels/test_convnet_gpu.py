@@ -19,10 +19,12 @@ def C():
     return C
 
 
-@pytest.fixture()
-def atomic_mode(C):
-    C.set_reduce_atomic(1)
-    yield C
+@pytest.fixture(params=[1, 16], ids=["rows1", "rows16"])
+def atomic_mode(C, request):
+    """Atomic reduction modes: R = 1 accumulated row (mode 1) and R = 16
+    striped rows (the executor's mode 2).  Yields R."""
+    C.set_reduce_atomic(request.param)
+    yield request.param
     C.set_reduce_atomic(0)
 
 
@@ -352,13 +354,14 @@ def test_bwd_reduce_head_fused(C):
     assert int(res[1][5][0]) == 1 and float(res[1][4]) == 1.0
 
 
-@pytest.mark.parametrize("atomic", ["1", "0"])
+@pytest.mark.parametrize("atomic", ["2", "1", "0"])
 def test_executor_matches_torch_model(C, atomic, monkeypatch):
     """Whole-model check: HIP executor loss + every gradient vs an fp32 PyTorch
     reference of the same parameters; the error must be within 2x of what
-    PyTorch's own bf16 path shows against the same fp32 reference.  Both
-    reduction modes (1 = atomic accumulation, no finalize / slab-reduce
-    launches; 0 = deterministic partial rows)."""
+    PyTorch's own bf16 path shows against the same fp32 reference.  Every
+    reduction mode (2 = striped atomic BN rows + slab weight gradients, 1 =
+    atomic accumulation, no finalize / slab-reduce launches; 0 = deterministic
+    partial rows)."""
     monkeypatch.setenv("DISTLEARN_REDUCE_ATOMIC", atomic)
     from torch_distlearn_amd import FlatParams
     from torch_distlearn_amd.models import CifarConvNet
@@ -406,7 +409,9 @@ def test_executor_matches_torch_model(C, atomic, monkeypatch):
 @pytest.mark.parametrize("shape", [(8, 32, 8, 64, 2, 1), (8, 16, 64, 128, 0, 1), (32, 4, 256, 512, 0, 4),
                                    (8, 8, 128, 256, 2, 1)])
 def test_conv_fwd_stats_atomic(C, atomic_mode, shape):
-    """conv_fwd statistics in mode 1 = the column sums of mode 0's partial rows."""
+    """conv_fwd statistics in the atomic modes (summed over the R rows) = the
+    column sums of mode 0's partial rows."""
+    R = atomic_mode
     B, H, cin, cout, tile, splits = shape
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(cin + cout)
@@ -414,14 +419,16 @@ def test_conv_fwd_stats_atomic(C, atomic_mode, shape):
     w = (torch.randn(cout, 5, 5, cin, device=dev, generator=g) * 0.05).to(torch.bfloat16)
     slab = torch.empty(max(splits, 1) * B * H * H * cout, device=dev)
     res = []
-    for mode in (0, 1):
+    for mode in (0, R):
         C.set_reduce_atomic(mode)
         y = torch.empty(B, H, H, cout, dtype=torch.bfloat16, device=dev)
         stats = torch.zeros(512, 2, cout, device=dev)
         T = C.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), stats.data_ptr(), slab.data_ptr(), B, H, H, cin,
                        cout, 5, tile, splits, _s())
         torch.cuda.synchronize()
-        res.append((y.clone(), stats[:T].sum(0) if mode == 0 else stats[0].clone()))
+        res.append((y.clone(), stats[:T].sum(0) if mode == 0 else stats[:R].sum(0)))
+        if mode:
+            assert float(stats[R:].abs().max()) == 0.0  # nothing outside the R rows
     assert torch.equal(res[0][0], res[1][0])
     torch.testing.assert_close(res[1][1], res[0][1], rtol=1e-5, atol=1e-2)
 
@@ -429,9 +436,11 @@ def test_conv_fwd_stats_atomic(C, atomic_mode, shape):
 @pytest.mark.parametrize("shape", [(8, 32, 64), (8, 16, 128), (16, 4, 512), (3, 8, 32)])
 def test_bn_relu_pool_fused_finalize(C, atomic_mode, shape):
     """bn_relu_pool_fwd_fin (coefficients from the totals) == bn_finalize +
-    bn_relu_pool_fwd, bitwise (same arithmetic); the backward reduce in mode 1
-    accumulates [dgamma; dbeta] and bn_relu_pool_bwd_apply_sums matches
-    bn_bwd_finalize + bn_relu_pool_bwd_apply."""
+    bn_relu_pool_fwd, bitwise (same arithmetic; the totals sit in row 0 of R
+    rows); the backward reduce in the atomic modes accumulates R rows of
+    [dgamma; dbeta] and bn_relu_pool_bwd_apply_sums matches bn_bwd_finalize +
+    bn_relu_pool_bwd_apply (R > 1: it also writes the totals out)."""
+    R = atomic_mode
     B, H, Cc = shape
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(B * H + Cc)
@@ -442,13 +451,15 @@ def test_bn_relu_pool_fused_finalize(C, atomic_mode, shape):
     M = B * H * H
     yf = y.float().reshape(-1, Cc)
     sums = torch.stack([yf.sum(0), (yf * yf).sum(0)]).contiguous()
+    sums_r = torch.zeros(R, 2, Cc, device=dev)
+    sums_r[0] = sums
     outs = []
     for fused in (False, True):
         rm, rv = torch.zeros(Cc, device=dev), torch.ones(Cc, device=dev)
         coef = torch.full((4, Cc), float("nan"), device=dev)
         out = torch.empty(B, H // 2 + 4, H // 2 + 4, Cc, dtype=torch.bfloat16, device=dev)
         if fused:
-            C.bn_relu_pool_fwd_fin(y.data_ptr(), sums.data_ptr(), M, gamma.data_ptr(), beta.data_ptr(),
+            C.bn_relu_pool_fwd_fin(y.data_ptr(), sums_r.data_ptr(), M, gamma.data_ptr(), beta.data_ptr(),
                                    bias.data_ptr(), rm.data_ptr(), rv.data_ptr(), 1e-3, 0.1, coef.data_ptr(),
                                    out.data_ptr(), B, H, H, Cc, 2, _s())
         else:
@@ -472,16 +483,21 @@ def test_bn_relu_pool_fused_finalize(C, atomic_mode, shape):
     dy0 = torch.zeros(B, H + 4, H + 4, Cc, dtype=torch.bfloat16, device=dev)
     C.bn_relu_pool_bwd_apply(y.data_ptr(), dP.data_ptr(), coef.data_ptr(), acoef.data_ptr(), dy0.data_ptr(), B, H, H,
                              Cc, 2, _s())
-    # mode 1
-    C.set_reduce_atomic(1)
-    dgb = torch.zeros(2, Cc, device=dev)
+    # atomic mode (R rows)
+    C.set_reduce_atomic(R)
+    dgb = torch.zeros(R, 2, Cc, device=dev)
     C.bn_relu_pool_bwd_reduce(y.data_ptr(), dP.data_ptr(), coef.data_ptr(), dgb.data_ptr(), B, H, H, Cc, G, _s())
     dy1 = torch.zeros(B, H + 4, H + 4, Cc, dtype=torch.bfloat16, device=dev)
+    out_g = torch.full((2, Cc), float("nan"), device=dev)
+    outp = (out_g[0].data_ptr(), out_g[1].data_ptr()) if R > 1 else (0, 0)
     C.bn_relu_pool_bwd_apply_sums(y.data_ptr(), dP.data_ptr(), coef.data_ptr(), dgb.data_ptr(), gamma.data_ptr(), M,
-                                  dy1.data_ptr(), B, H, H, Cc, 2, _s())
+                                  dy1.data_ptr(), B, H, H, Cc, 2, *outp, _s())
     torch.cuda.synchronize()
-    torch.testing.assert_close(dgb[0], dg, rtol=1e-4, atol=1e-4)
-    torch.testing.assert_close(dgb[1], db, rtol=1e-4, atol=1e-4)
+    tot = dgb.sum(0)
+    torch.testing.assert_close(tot[0], dg, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(tot[1], db, rtol=1e-4, atol=1e-4)
+    if R > 1:
+        torch.testing.assert_close(out_g, tot, rtol=1e-5, atol=1e-5)
     assert _rel(dy1, dy0) < 2e-3
 
 
@@ -495,7 +511,8 @@ def test_head_pool_fused_finalize(C, atomic_mode):
     g = torch.Generator(device=dev).manual_seed(15)
     y = torch.randn(B, H, H, Cc, device=dev, generator=g).to(torch.bfloat16)
     yf = y.float().reshape(-1, Cc)
-    sums = torch.stack([yf.sum(0), (yf * yf).sum(0)]).contiguous()
+    sums = torch.zeros(atomic_mode, 2, Cc, device=dev)  # totals in row 0 of R rows
+    sums[0] = torch.stack([yf.sum(0), (yf * yf).sum(0)])
     gamma = torch.rand(Cc, device=dev, generator=g) + 0.5
     beta = torch.randn(Cc, device=dev, generator=g) * 0.1
     cb = torch.randn(Cc, device=dev, generator=g) * 0.1

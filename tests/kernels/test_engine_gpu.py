@@ -17,8 +17,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 def deterministic(monkeypatch):
     """Graph-vs-eager and side-effect checks compare runs bitwise / to 1e-3:
     they use the deterministic reduction mode (partial rows + finalize
-    kernels).  Mode 1 (atomic accumulation, the bench default) is covered by
-    test_mode1_trains_and_graph_tracks_eager and tests/kernels/test_convnet_gpu.py."""
+    kernels).  The atomic modes (2 = the executor default) are covered by
+    test_atomic_modes_train_and_graph_tracks_eager and tests/kernels/test_convnet_gpu.py."""
     monkeypatch.setenv("DISTLEARN_REDUCE_ATOMIC", "0")
 
 
@@ -243,11 +243,12 @@ def test_comm_profile_is_side_effect_free(dev, monkeypatch):
     assert torch.equal(outs[0][0], outs[1][0])
 
 
-def test_mode1_trains_and_graph_tracks_eager(dev, monkeypatch):
-    """Reduction mode 1 (fp32 atomics: not bitwise reproducible run to run):
-    the model fits a repeated batch, and graph replay tracks eager within the
-    run-to-run noise of the atomics (measured: scripts/diag_mode1.py)."""
-    monkeypatch.setenv("DISTLEARN_REDUCE_ATOMIC", "1")
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_atomic_modes_train_and_graph_tracks_eager(dev, monkeypatch, mode):
+    """Reduction modes 1 and 2 (fp32 atomics: not bitwise reproducible run to
+    run): the model fits a repeated batch, and graph replay tracks eager within
+    the run-to-run noise of the atomics (measured: scripts/diag_mode1.py)."""
+    monkeypatch.setenv("DISTLEARN_REDUCE_ATOMIC", mode)
     g = torch.Generator(device=dev).manual_seed(1)
     x = torch.randn(32, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)
     y = torch.randint(0, 10, (32,), device=dev, generator=g)

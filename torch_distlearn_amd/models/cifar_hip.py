@@ -167,7 +167,7 @@ class CifarHIPExecutor:
         # (the cross-queue edges leave ~150 us of idle gaps per step), so off.
         self.side_reduce = (not self.side_wgrad and self.side is not None
                             and os.environ.get("DISTLEARN_REDUCE_STREAM", "0") == "1")
-        # Reduction mode (csrc/kernels/bn_fin_dev.h).  0 (default) = deterministic
+        # Reduction mode (csrc/kernels/bn_fin_dev.h).  0 = deterministic
         # partial rows + finalize kernels (bitwise run-to-run reproducible).  1 =
         # BN statistics, BN parameter gradients and split-K weight gradients are
         # accumulated with fp32 atomics into buffers the step's prep kernel zeroes
@@ -177,7 +177,20 @@ class CifarHIPExecutor:
         # forward with 1024 workgroups adding into 128 addresses takes 31 us instead
         # of 11, the 128-way split-K wgrad 56 us instead of 15 + 5 (slab reduce)
         # (profiles/r2_mode1_timeline.txt).
-        self.atomic = os.environ.get("DISTLEARN_REDUCE_ATOMIC", "0") == "1"
+        # 2 (default) = the BN part of mode 1 with the atomics striped over R rows
+        # (row = tile / block index mod R, zeroed by the prep kernel, summed by every
+        # consumer block with all row loads in flight at once, overlapped with the
+        # block's first data loads: R-fold less same-address contention) and the
+        # weight gradients on split-K slabs as in mode 0: 7 finalize launches fewer.
+        # Measured interleaved on one box: 0.3466 vs 0.3625 ms/step (mode 0).  Not
+        # bitwise reproducible run to run (fp32 atomics in the BN statistics); the
+        # replicas stay bitwise identical (they apply the same all-reduced gradient).
+        self.mode = int(os.environ.get("DISTLEARN_REDUCE_ATOMIC", "2"))
+        if self.mode not in (0, 1, 2):
+            raise ValueError("DISTLEARN_REDUCE_ATOMIC must be 0, 1 or 2")
+        self.atomic = self.mode > 0             # BN statistics / gradients by atomics, no finalize kernels
+        self.atomic_wgrad = self.mode == 1      # split-K weight gradients by atomics (else slabs)
+        self.rows = {0: 0, 1: 1, 2: int(os.environ.get("DISTLEARN_REDUCE_ROWS", "16"))}[self.mode]
         self._alloc(self.B)
 
     # ------------------------------------------------------------------ buffers
@@ -201,9 +214,13 @@ class CifarHIPExecutor:
         self.coef = [torch.empty(4, c, device=d) for c in self.couts]
         self.acoef = [torch.empty(3, c, device=d) for c in self.couts]
         self.fwd_plan, self.stats = [], []
-        # mode 1: one zeroed [2][C] (sum, sumsq) row per layer in one arena
-        arena = torch.zeros(sum(2 * c for c in self.couts), device=d) if self.atomic else None
+        # atomic modes: R zeroed [2][C] (sum, sumsq) rows per layer in one arena; mode 2
+        # also R [2][C] (dgamma, dbeta) rows per layer for the backward reduce
+        R = self.rows
+        per = sum(2 * R * c for c in self.couts)
+        arena = torch.zeros(per * (2 if self.mode == 2 else 1), device=d) if self.atomic else None
         arena_off = 0
+        self.bwd_rows = [None] * self.nb
         self.dgrad_plan = [None] * self.nb
         self.bwd_blocks, self.bwd_part = [], []
         self.wplan, slab_elems, wslab_elems = [], 0, 0
@@ -217,8 +234,10 @@ class CifarHIPExecutor:
             if splits > 1:
                 slab_elems = max(slab_elems, splits * M * cout)
             if self.atomic:
-                self.stats.append(arena[arena_off:arena_off + 2 * cout].view(2, cout))
-                arena_off += 2 * cout
+                self.stats.append(arena[arena_off:arena_off + 2 * R * cout].view(R, 2, cout))
+                if self.mode == 2:
+                    self.bwd_rows[i] = arena[per + arena_off:per + arena_off + 2 * R * cout].view(R, 2, cout)
+                arena_off += 2 * R * cout
             else:
                 rows = C.conv_fwd_stat_rows(B, h, h, cin, cout, KSIZE, tile, splits)
                 if splits > 1:
@@ -230,21 +249,22 @@ class CifarHIPExecutor:
             tile_w, splits_w = _wgrad_plan(cout, K, M, self.cu_reserve)
             direct = splits_w == 1 and cin == self.cins_real[i]
             self.wplan.append((tile_w, splits_w, direct))
-            if not direct and not self.atomic:
+            if not direct and not self.atomic_wgrad:
                 wslab_elems = max(wslab_elems, splits_w * cout * K)
-            self.wslab_l.append(None if (direct or self.atomic) else torch.empty(splits_w * cout * K, device=d))
+            self.wslab_l.append(None if (direct or self.atomic_wgrad) else torch.empty(splits_w * cout * K, device=d))
             if i > 0:
                 dt, ds = _fwd_plan(M, cin, KSIZE * KSIZE * cout)
                 self.dgrad_plan[i] = (dt, ds)
                 if ds > 1:
                     slab_elems = max(slab_elems, ds * M * cin)
         self.slabs = torch.empty(max(slab_elems, 1), device=d)    # fwd / dgrad split-K (main stream)
-        # what the step's prep kernel zeroes in mode 1: the statistics arena, every
-        # layer's [dgamma; dbeta] and the atomically accumulated weight gradients
+        # what the step's prep kernel zeroes in the atomic modes: the statistics arena
+        # (mode 2: + the backward rows); mode 1: every layer's [dgamma; dbeta] and the
+        # atomically accumulated weight gradients
         self.zero_ranges = []
         if self.atomic:
             self.zero_ranges.append((arena.data_ptr(), arena.numel()))
-            for i in range(self.nb):
+            for i in range(self.nb if self.mode == 1 else 0):
                 gw_, gb_ = self.g32[self._leaf(i, 2)], self.g32[self._leaf(i, 3)]
                 if gb_.data_ptr() != gw_.data_ptr() + 4 * gw_.numel():
                     raise RuntimeError("BN weight/bias gradients must be adjacent in the flat buffer")
@@ -403,8 +423,9 @@ class CifarHIPExecutor:
             M = B * h * h
             G = self.bwd_blocks[i]
             dY = self.dYs[i]
-            # mode 1: the reduce accumulates straight into [dgamma; dbeta] of the flat gradient
-            part = self.g32[self._leaf(i, 2)] if self.atomic else self.bwd_part[i]
+            # mode 1: the reduce accumulates straight into [dgamma; dbeta] of the flat gradient;
+            # mode 2: into R striped rows (the apply kernel writes the totals to the flat gradient)
+            part = {0: self.bwd_part[i], 1: self.g32[self._leaf(i, 2)], 2: self.bwd_rows[i]}[self.mode]
             if i == self.nb - 1 and self.head_wgrad_fused:
                 # one launch: this block's BN backward reduce + the classifier weight gradient
                 C.bn_bwd_reduce_head(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
@@ -415,9 +436,11 @@ class CifarHIPExecutor:
                 C.bn_relu_pool_bwd_reduce(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
                                           part.data_ptr(), B, h, h, cout, G, s)
             if self.atomic:
+                dgo, dbo = ((self.g32[self._leaf(i, 2)].data_ptr(), self.g32[self._leaf(i, 3)].data_ptr())
+                            if self.mode == 2 else (0, 0))
                 C.bn_relu_pool_bwd_apply_sums(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
                                               part.data_ptr(), self.p32[self._leaf(i, 2)].data_ptr(), M,
-                                              dY.data_ptr(), B, h, h, cout, SPAD, s)
+                                              dY.data_ptr(), B, h, h, cout, SPAD, dgo, dbo, s)
             else:
                 C.bn_bwd_finalize(self.bwd_part[i].data_ptr(), G, cout, M, self.p32[self._leaf(i, 2)].data_ptr(),
                                   self.coef[i].data_ptr(), self.g32[self._leaf(i, 2)].data_ptr(),
@@ -434,11 +457,11 @@ class CifarHIPExecutor:
             if direct:
                 C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), gw.data_ptr(), B, h, h, cin, cout, KSIZE, 1, K, tile, 0,
                              wss)
-            elif self.atomic:  # split-K partials atomically added into the zeroed gradient
+            elif self.atomic_wgrad:  # split-K partials atomically added into the zeroed gradient
                 C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), gw.data_ptr(), B, h, h, cin, cout, KSIZE, splits, K, tile,
                              self.cins_real[i], wss)
             rs = ws  # the stream that writes this block's weight gradient last
-            if not direct and not self.atomic:
+            if not direct and not self.atomic_wgrad:
                 slab = self.wslab_l[i]
                 C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), slab.data_ptr(), B, h, h, cin, cout, KSIZE,
                              splits, K, tile, 0, wss)
@@ -472,11 +495,11 @@ class CifarHIPExecutor:
 
     def _set_mode(self) -> None:
         """The reduction mode lives in device globals shared by every executor
-        of the process: (re)select this executor's (a blocking symbol copy --
-        never issued while a hipGraph is being captured; a captured step
+        of the process: (re)select this executor's row count (a blocking symbol
+        copy -- never issued while a hipGraph is being captured; a captured step
         replays with the mode that was active at capture)."""
-        if self.C.reduce_atomic() != int(self.atomic) and not torch.cuda.is_current_stream_capturing():
-            self.C.set_reduce_atomic(int(self.atomic))
+        if self.C.reduce_atomic() != self.rows and not torch.cuda.is_current_stream_capturing():
+            self.C.set_reduce_atomic(self.rows)
 
     def last_logits(self) -> torch.Tensor:
         return self.logits[:self._last_b]
