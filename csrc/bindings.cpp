@@ -78,6 +78,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_fwd_bwd", &head_fwd_bwd);
   m.def("head_fwd_bwd_pool", &head_fwd_bwd_pool);
   m.def("bn_bwd_reduce_head", &bn_bwd_reduce_head);
+  m.def("bn_bwd_reduce_slab", &bn_bwd_reduce_slab);
   m.def("head_wgrad", &head_wgrad);
   m.def("mnist_step", &mnist_step);
   m.def("mnist_scratch_bytes", &mnist_scratch_bytes);

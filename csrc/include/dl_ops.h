@@ -107,6 +107,9 @@ int reduce_rows();
 // head.hip --------------------------------------------------------------------
 void head_fwd_bwd(uintptr_t h, uintptr_t w, uintptr_t bias, uintptr_t labels, int F, int B, int NC,
                   uintptr_t logits_out, uintptr_t dlogits, uintptr_t loss_b, uintptr_t dh, uintptr_t stream);
+void bn_bwd_reduce_slab(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t partial, int B, int H, int W, int C,
+                        int blocks, uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int Creal,
+                        uintptr_t stream);
 void bn_bwd_reduce_head(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t partial, int B, int H, int W, int C,
                         int blocks, uintptr_t h, uintptr_t dlogits, uintptr_t loss_b, int F, int NC, uintptr_t dw,
                         uintptr_t db, uintptr_t loss, uintptr_t slot, uintptr_t step_ctr, uintptr_t stream);

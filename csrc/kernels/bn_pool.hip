@@ -24,6 +24,7 @@
 #include "dl_ops.h"
 #include "head_wgrad_dev.h"
 #include "bn_fin_dev.h"
+#include "slab_reduce_dev.h"
 
 namespace dl {
 
@@ -365,6 +366,30 @@ __global__ void __launch_bounds__(256) bwd_reduce_head_kernel(const bf16_t* __re
                         (int)blockIdx.x - G);
 }
 
+// One launch for two independent jobs: blocks [0, G) = this block's BN
+// backward reduce (waits for the dgrad that produced dP), blocks [G, ...) =
+// the split-K slab reduction of the NEXT conv block's weight gradient (its
+// wgrad finished two launches earlier).  Saves the stand-alone slab_reduce
+// launch and its kernel boundary.
+struct SlabArgs {
+  const float* slabs;
+  float* dst;
+  int splits, Cout, taps, Cp, C;
+};
+
+template <int TPO>
+__global__ void __launch_bounds__(256) bwd_reduce_slab_kernel(const bf16_t* __restrict__ y,
+                                                              const bf16_t* __restrict__ dP,
+                                                              const float* __restrict__ coef,
+                                                              float* __restrict__ partial, int B, int H, int W, int C,
+                                                              int G, const SlabArgs sa) {
+  if ((int)blockIdx.x < G)
+    bwd_reduce_body(y, dP, coef, partial, B, H, W, C, (int)blockIdx.x, G);
+  else
+    slab_reduce_body<TPO>(sa.slabs, sa.dst, sa.splits, sa.Cout, sa.taps, sa.Cp, sa.C, (int)blockIdx.x - G,
+                          (int)gridDim.x - G);
+}
+
 // backward finalize: dgamma = sum(dz*xhat), dbeta = sum(dz);
 // apply coefficients [3][C]: dy = a*dz + b*xhat + c
 __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ partial, int T, int C,
@@ -553,6 +578,28 @@ void bn_bwd_reduce_head(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t par
   const int head_blocks = (F + 31) / 32 + 1;
   bwd_reduce_head_kernel<<<blocks + head_blocks, 256, 0, as_stream(stream)>>>(
       (const bf16_t*)y, (const bf16_t*)dP, (const float*)coef, (float*)partial, B, H, W, C, blocks, ha);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+void bn_bwd_reduce_slab(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t partial, int B, int H, int W, int C,
+                        int blocks, uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int Creal,
+                        uintptr_t stream) {
+  check_c(C);
+  if ((256 % (C / 8)) != 0) throw std::runtime_error("bn_bwd_reduce_slab: C/8 must divide 256");
+  if (!slabs || !dst || splits < 1 || Creal > Cp) throw std::runtime_error("bn_bwd_reduce_slab: bad slab arguments");
+  const SlabArgs sa{(const float*)slabs, (float*)dst, splits, Cout, taps, Cp, Creal};
+  const int g = blocks + slab_reduce_grid(splits, Cout, taps, Creal);
+  const int tpo = slab_reduce_tpo(splits);
+  auto s = as_stream(stream);
+  if (tpo == 32)
+    bwd_reduce_slab_kernel<32><<<g, 256, 0, s>>>((const bf16_t*)y, (const bf16_t*)dP, (const float*)coef,
+                                                 (float*)partial, B, H, W, C, blocks, sa);
+  else if (tpo == 8)
+    bwd_reduce_slab_kernel<8><<<g, 256, 0, s>>>((const bf16_t*)y, (const bf16_t*)dP, (const float*)coef,
+                                                (float*)partial, B, H, W, C, blocks, sa);
+  else
+    bwd_reduce_slab_kernel<1><<<g, 256, 0, s>>>((const bf16_t*)y, (const bf16_t*)dP, (const float*)coef,
+                                                (float*)partial, B, H, W, C, blocks, sa);
   DL_HIP_CHECK(hipGetLastError());
 }
 

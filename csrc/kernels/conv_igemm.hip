@@ -26,6 +26,7 @@
 // one partial row per M tile, reduced by bn_finalize).
 #include "dl_common.h"
 #include "dl_ops.h"
+#include "slab_reduce_dev.h"
 
 #include <algorithm>
 #include <vector>
@@ -1259,35 +1260,11 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
 }
 
 // Sum `splits` fp32 slabs [splits][Cout][Kp] (Kp = taps*Cp) into dst
-// [Cout][taps][C] (C <= Cp: drops zero-padded input channels).  TPO lanes
-// share one output (each sums a strided subset of the splits, then a
-// fixed-order shuffle reduction): enough parallelism for 64-way slabs.
-// ACC: dst += sum (gradient accumulation semantics) instead of dst = sum.
-// OIHW: dst in [Cout][C][taps] order (a PyTorch conv weight) instead of [Cout][taps][C].
+// [Cout][taps][C] (body and options: slab_reduce_dev.h).
 template <int TPO, bool ACC = false, bool OIHW = false>
 __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slabs, float* __restrict__ dst,
                                                           int splits, int Cout, int taps, int Cp, int C) {
-  const int64_t total = (int64_t)Cout * taps * C;
-  const int64_t slab = (int64_t)Cout * taps * Cp;
-  const int sub = threadIdx.x % TPO;
-  const int64_t opb = 256 / TPO;  // outputs per block iteration
-  for (int64_t i = (int64_t)blockIdx.x * opb + threadIdx.x / TPO; i < total + 0; i += (int64_t)gridDim.x * opb) {
-    const int c = (int)(i % C);
-    const int64_t rest = i / C;  // co*taps + tap
-    const int64_t src = rest * Cp + c;
-    float s = 0.f;
-    for (int sp = sub; sp < splits; sp += TPO) s += slabs[sp * slab + src];
-#pragma unroll
-    for (int o = TPO / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (sub == 0) {
-      int64_t o = i;
-      if constexpr (OIHW) {
-        const int64_t co = rest / taps;
-        o = (co * C + c) * taps + (rest - co * taps);
-      }
-      dst[o] = ACC ? dst[o] + s : s;
-    }
-  }
+  slab_reduce_body<TPO, ACC, OIHW>(slabs, dst, splits, Cout, taps, Cp, C, (int)blockIdx.x, (int)gridDim.x);
 }
 
 // --------------------------------------------------------------------------
@@ -2020,20 +1997,15 @@ void set_reduce_atomic_conv(int rows) {
 template <bool ACC, bool OIHW = false>
 static void slab_reduce_t(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C,
                           uintptr_t stream) {
-  const int64_t total = (int64_t)Cout * taps * C;
   auto s = as_stream(stream);
-  if (splits >= 32) {
-    int64_t g = (total * 32 + 255) / 256;
-    slab_reduce_kernel<32, ACC, OIHW><<<(int)std::min<int64_t>(g, 4096), 256, 0, s>>>((const float*)slabs, (float*)dst,
-                                                                               splits, Cout, taps, Cp, C);
-  } else if (splits >= 8) {
-    int64_t g = (total * 8 + 255) / 256;
-    slab_reduce_kernel<8, ACC, OIHW><<<(int)std::min<int64_t>(g, 4096), 256, 0, s>>>((const float*)slabs, (float*)dst,
-                                                                              splits, Cout, taps, Cp, C);
-  } else {
-    slab_reduce_kernel<1, ACC, OIHW><<<stream_grid(total), 256, 0, s>>>((const float*)slabs, (float*)dst, splits, Cout,
-                                                                  taps, Cp, C);
-  }
+  const int g = slab_reduce_grid(splits, Cout, taps, C);
+  const int tpo = slab_reduce_tpo(splits);
+  if (tpo == 32)
+    slab_reduce_kernel<32, ACC, OIHW><<<g, 256, 0, s>>>((const float*)slabs, (float*)dst, splits, Cout, taps, Cp, C);
+  else if (tpo == 8)
+    slab_reduce_kernel<8, ACC, OIHW><<<g, 256, 0, s>>>((const float*)slabs, (float*)dst, splits, Cout, taps, Cp, C);
+  else
+    slab_reduce_kernel<1, ACC, OIHW><<<g, 256, 0, s>>>((const float*)slabs, (float*)dst, splits, Cout, taps, Cp, C);
   DL_HIP_CHECK(hipGetLastError());
 }
 

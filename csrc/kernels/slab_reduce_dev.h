@@ -1,0 +1,49 @@
+// Split-K weight-gradient slab reduction body, shared by the stand-alone
+// slab_reduce kernel (conv_igemm.hip) and the combined launch that runs it
+// beside the previous layer's BatchNorm backward reduce (bn_pool.hip).
+//   dst[co][tap][c] (= / +=) sum_sp slabs[sp][co][tap][c'], c < C <= Cp
+// TPO lanes share one output (each sums a strided subset of the splits, then
+// a fixed-order shuffle reduction): enough parallelism for 64-way slabs.
+// ACC: dst += sum (gradient accumulation semantics) instead of dst = sum.
+// OIHW: dst in [Cout][C][taps] order (a PyTorch conv weight) instead of [Cout][taps][C].
+#pragma once
+#include "dl_common.h"
+
+namespace dl {
+
+template <int TPO, bool ACC = false, bool OIHW = false>
+__device__ __forceinline__ void slab_reduce_body(const float* __restrict__ slabs, float* __restrict__ dst, int splits,
+                                                 int Cout, int taps, int Cp, int C, int bid, int nblk) {
+  const int64_t total = (int64_t)Cout * taps * C;
+  const int64_t slab = (int64_t)Cout * taps * Cp;
+  const int sub = threadIdx.x % TPO;
+  const int64_t opb = 256 / TPO;  // outputs per block iteration
+  for (int64_t i = (int64_t)bid * opb + threadIdx.x / TPO; i < total; i += (int64_t)nblk * opb) {
+    const int c = (int)(i % C);
+    const int64_t rest = i / C;  // co*taps + tap
+    const int64_t src = rest * Cp + c;
+    float s = 0.f;
+    for (int sp = sub; sp < splits; sp += TPO) s += slabs[sp * slab + src];
+#pragma unroll
+    for (int o = TPO / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (sub == 0) {
+      int64_t o = i;
+      if constexpr (OIHW) {
+        const int64_t co = rest / taps;
+        o = (co * C + c) * taps + (rest - co * taps);
+      }
+      dst[o] = ACC ? dst[o] + s : s;
+    }
+  }
+}
+
+// Threads per output and grid of a slab reduction (the stand-alone launcher's rule).
+inline int slab_reduce_tpo(int splits) { return splits >= 32 ? 32 : splits >= 8 ? 8 : 1; }
+inline int slab_reduce_grid(int splits, int Cout, int taps, int C) {
+  const int64_t total = (int64_t)Cout * taps * C;
+  const int tpo = slab_reduce_tpo(splits);
+  if (tpo == 1) return stream_grid(total);
+  return (int)std::min<int64_t>((total * tpo + 255) / 256, 4096);
+}
+
+}  // namespace dl

@@ -581,3 +581,31 @@ def test_prep_zero_ranges(C):
                 [], [], [], [], [b.data_ptr() for b in bufs], [b.numel() for b in bufs], _s())
     torch.cuda.synchronize()
     assert all(not b.any() for b in bufs) and torch.equal(keep, ref)
+
+
+def test_executor_merged_slab_reduce_bitwise(C, monkeypatch):
+    """The weight-gradient slab reduction launched together with the previous
+    block's BN backward reduce (bwd_reduce_slab_kernel) writes exactly what the
+    stand-alone slab_reduce launches write (deterministic mode 0)."""
+    from torch_distlearn_amd import FlatParams
+    from torch_distlearn_amd.models import CifarConvNet
+    from torch_distlearn_amd.models.cifar_hip import CifarHIPExecutor
+
+    monkeypatch.setenv("DISTLEARN_REDUCE_ATOMIC", "0")
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(64, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)
+    y = torch.randint(0, 10, (64,), device=dev, generator=g)
+    grads = []
+    for merge in ("0", "1"):
+        monkeypatch.setenv("DISTLEARN_MERGE_SLAB", merge)
+        mdl = CifarConvNet(seed=4).to(dev)
+        flat = FlatParams(mdl, grads=True, shadow_bf16=True)
+        flat.grad.fill_(float("nan"))  # every gradient element must be (over)written
+        ex = CifarHIPExecutor(mdl, flat, max_batch=64)
+        assert ex.merge_slab == (merge == "1")
+        ex.forward_backward(x.contiguous(), y)
+        torch.cuda.synchronize()
+        grads.append(torch.cat([v.flatten() for v in flat.views_of(flat.grad)]))
+    assert torch.isfinite(grads[1]).all()
+    assert torch.equal(grads[0], grads[1])

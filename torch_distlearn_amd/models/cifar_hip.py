@@ -188,6 +188,13 @@ class CifarHIPExecutor:
         self.mode = int(os.environ.get("DISTLEARN_REDUCE_ATOMIC", "2"))
         if self.mode not in (0, 1, 2):
             raise ValueError("DISTLEARN_REDUCE_ATOMIC must be 0, 1 or 2")
+        # (optional, measured slower -> off) the slab reduction of block i's weight
+        # gradient in the same launch as block i-1's BN backward reduce (csrc
+        # bwd_reduce_slab_kernel): 2 launches fewer, but the combined kernels take
+        # 16.0 / 26.4 us vs 6.7 + 5.7 / 8.0 + 7.7 separately (the slab blocks run with
+        # the reduce's LDS / VGPR footprint): 0.3634 vs 0.3506 ms/step
+        # (profiles/r2_merge_slab_ab.txt)
+        self.merge_slab = os.environ.get("DISTLEARN_MERGE_SLAB", "0") == "1"
         self.atomic = self.mode > 0             # BN statistics / gradients by atomics, no finalize kernels
         self.atomic_wgrad = self.mode == 1      # split-K weight gradients by atomics (else slabs)
         self.rows = {0: 0, 1: 1, 2: int(os.environ.get("DISTLEARN_REDUCE_ROWS", "16"))}[self.mode]
@@ -418,6 +425,8 @@ class CifarHIPExecutor:
         ws = side if self.side_wgrad else main
         wss = ws.cuda_stream
         side_pending = False
+        merge = self.merge_slab and not (self.side_wgrad or self.side_reduce)
+        pending = None  # (slab args, block) of a weight gradient whose slab reduce rides the next BN reduce
         for i in reversed(range(self.nb)):
             h, cin, cout = self.hs[i], self.cins[i], self.couts[i]
             M = B * h * h
@@ -432,6 +441,14 @@ class CifarHIPExecutor:
                                      part.data_ptr(), B, h, h, cout, G, *head_args, s)
                 self._ready(nfc)
                 self._ready(nfc + 1)
+            elif pending is not None:
+                # one launch: this block's BN backward reduce + block i+1's weight-gradient slab reduce
+                sargs, blk = pending
+                C.bn_bwd_reduce_slab(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
+                                     part.data_ptr(), B, h, h, cout, G, *sargs, s)
+                for j in range(4):
+                    self._ready(self._leaf(blk, j))
+                pending = None
             else:
                 C.bn_relu_pool_bwd_reduce(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
                                           part.data_ptr(), B, h, h, cout, G, s)
@@ -465,11 +482,14 @@ class CifarHIPExecutor:
                 slab = self.wslab_l[i]
                 C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), slab.data_ptr(), B, h, h, cin, cout, KSIZE,
                              splits, K, tile, 0, wss)
-                if self.side_reduce and i > 0:  # overlaps this block's dgrad (block 1 has none)
-                    side.wait_stream(main)
-                    rs = side
-                C.slab_reduce(slab.data_ptr(), gw.data_ptr(), splits, cout, KSIZE * KSIZE, cin,
-                              self.cins_real[i], rs.cuda_stream)
+                sargs = (slab.data_ptr(), gw.data_ptr(), splits, cout, KSIZE * KSIZE, cin, self.cins_real[i])
+                if merge and i > 0:  # reduced by block i-1's BN backward reduce launch
+                    pending = (sargs, i)
+                else:
+                    if self.side_reduce and i > 0:  # overlaps this block's dgrad (block 1 has none)
+                        side.wait_stream(main)
+                        rs = side
+                    C.slab_reduce(*sargs, rs.cuda_stream)
             # conv bias grad: exactly 0 under train-mode BN (grad buffer was zero-filled).
             # Bucket launches issued here are ordered after the stream that wrote the grads;
             # a bucket readied on the main stream may also hold leaves reduced on the side
@@ -478,9 +498,10 @@ class CifarHIPExecutor:
                 main.wait_stream(side)
                 side_pending = False
             side_pending |= rs is side
-            with torch.cuda.stream(rs):
-                for j in range(4):
-                    self._ready(self._leaf(i, j))
+            if pending is None or pending[1] != i:
+                with torch.cuda.stream(rs):
+                    for j in range(4):
+                        self._ready(self._leaf(i, j))
             if i > 0:
                 dt, ds = self.dgrad_plan[i]
                 if self.dgrad_stages != 3:
