@@ -63,6 +63,7 @@ struct ConvGeom {
   int logW, logHW, logC8;  // log2(W), log2(H*W) (valid when pow2), log2(Cin/8)
   int M, K, Kch;           // M = B*H*W, K = KS*KS*Cin, Kch = K/8
   int pow2;                // H and W powers of two (the region / c8 kernels and the shift addressing)
+  int posm;                // streaming kernel: position-major M tiles with padding taps skipped (fwd_posm)
   float inv_HW, inv_W;     // reciprocals for the non-pow2 pixel decomposition (fdivmod)
 };
 
@@ -104,6 +105,7 @@ static ConvGeom make_geom(int B, int H, int W, int Cin, int Cout, int KS) {
   if (KS % 2 != 1) throw std::runtime_error("conv: odd kernel size required");
   if (Cin < 8) throw std::runtime_error("conv: Cin must be >= 8 (pad the input channels)");
   g.pow2 = is_pow2(W) && is_pow2(H) ? 1 : 0;
+  g.posm = 0;
   g.logW = g.pow2 ? ilog2_exact(W, "W") : 0;
   g.logHW = g.pow2 ? ilog2_exact(H * W, "H*W") : 0;
   g.inv_HW = 1.0f / (float)(H * W);
@@ -237,7 +239,9 @@ template <int BM, int BN, bool STATS, bool SLAB, int WM, int WN, bool ADD = fals
 __device__ __forceinline__ void conv_fwd_epilogue(const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], const ConvGeom& g,
                                                   bf16_t* __restrict__ y, float* __restrict__ stats,
                                                   float* __restrict__ slab, int split, int tm, int m0, int n0,
-                                                  char* smem) {
+                                                  char* smem, int pm_b0 = 0, int pm_pos = 0) {
+  // position-major tiles (g.posm): logical row ml -> stored row (pm_b0 + ml - m0) * HW + pm_pos
+  auto phys = [&](int ml) { return g.posm ? (pm_b0 + ml - m0) * (g.H * g.W) + pm_pos : ml; };
   constexpr int NT = 64 * WM * WN, TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = tid >> 6, wm = wid / WN, wn = wid % WN;
@@ -252,7 +256,7 @@ __device__ __forceinline__ void conv_fwd_epilogue(const f32x4 (&acc)[BM / WM / 1
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = m0 + wm * TM + a * 16 + rq * 4 + r;
-          if (m < g.M && n < g.Cout) o[(int64_t)m * g.Cout + n] = acc[a][b][r];
+          if (m < g.M && n < g.Cout) o[(int64_t)phys(m) * g.Cout + n] = acc[a][b][r];
         }
       }
   } else {
@@ -268,11 +272,12 @@ __device__ __forceinline__ void conv_fwd_epilogue(const f32x4 (&acc)[BM / WM / 1
         for (int r = 0; r < 4; ++r) {
           const int m = m0 + wm * TM + a * 16 + rq * 4 + r;
           float v0 = acc[a][b][r];
+          const int64_t mo = (int64_t)phys(m) * g.Cout + n;
           if constexpr (ADD) {
-            if (m < g.M && n < g.Cout) v0 += bf16_to_f32(reinterpret_cast<const bf16_t*>(slab)[(int64_t)m * g.Cout + n]);
+            if (m < g.M && n < g.Cout) v0 += bf16_to_f32(reinterpret_cast<const bf16_t*>(slab)[mo]);
           }
           const bf16_t hv = f32_to_bf16(v0);
-          if (m < g.M && n < g.Cout) y[(int64_t)m * g.Cout + n] = hv;
+          if (m < g.M && n < g.Cout) y[mo] = hv;
           if constexpr (STATS) {
             const float v = m < g.M ? bf16_to_f32(hv) : 0.f;  // statistics of exactly what is stored
             s1[b] += v;
@@ -336,7 +341,7 @@ template <int BM, int BN, bool STATS, bool SLAB, int WM, int WN, int FM, int FN,
 __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], const ConvGeom& g,
                                                     bf16_t* __restrict__ y, float* __restrict__ stats,
                                                     float* __restrict__ slab, int split, int tm, int m0, int n0,
-                                                    char* smem) {
+                                                    char* smem, int pm_b0 = 0, int pm_pos = 0) {
   constexpr int NT = 64 * WM * WN, TM = BM / WM, TN = BN / WN, NP = FN / 2;
   static_assert(!(ADD && (SLAB || STATS)), "ADD: plain bf16 output only");
   static_assert(FN % 2 == 0, "N fragments pair up");
@@ -350,8 +355,10 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
     for (int k = 0; k < 8; ++k) { s1[q][k] = 0.f; s2[q][k] = 0.f; }
 #pragma unroll
   for (int a = 0; a < FM; ++a) {
-    const int m = m0 + wm * TM + a * 16 + (lane & 15);
-    const bool ok = m < g.M;
+    const int ml = m0 + wm * TM + a * 16 + (lane & 15);
+    const bool ok = ml < g.M;
+    // stored row: position-major tiles hold image pm_b0 + r at output pixel pm_pos
+    const int m = g.posm ? (pm_b0 + ml - m0) * (g.H * g.W) + pm_pos : ml;
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
       const int n = n0 + nl + 32 * q;
@@ -469,9 +476,27 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   const int split = panel % splits, tn = panel / splits;
   const int m0 = tm * BM, n0 = tn * BN;
   const int C8 = 1 << g.logC8;
-  const int nkt_total = (g.Kch + CPR - 1) / CPR;
-  const int kt_beg = split * kt_per_split;
-  const int kt_end = min(nkt_total, kt_beg + kt_per_split);
+  // Position-major tiles (g.posm, host-enabled for TAPU layers whose output is
+  // smaller than the kernel, B % BM == 0): M tile tm holds images b0..b0+BM-1
+  // at ONE output pixel, so every row of the tile has the same valid taps and
+  // the taps that only read the zero border are skipped (4x4 output, 5x5
+  // kernel: 9-16 of 25 taps per pixel).  K steps are split evenly per tile.
+  int pm_b0 = 0, pm_pos = 0, kh0 = 0, kh1 = g.KS, kw0 = 0, kw1 = g.KS;
+  int nkt_total = (g.Kch + CPR - 1) / CPR, ktps = kt_per_split;
+  if (TAPU && g.posm) {
+    const int nbt = g.B / BM;
+    pm_pos = tm / nbt;
+    pm_b0 = (tm - pm_pos * nbt) * BM;
+    const int oh = pm_pos / g.W, ow = pm_pos - oh * g.W;
+    kh0 = max(0, g.pad - oh);
+    kh1 = min(g.KS, g.H + g.pad - oh);
+    kw0 = max(0, g.pad - ow);
+    kw1 = min(g.KS, g.W + g.pad - ow);
+    nkt_total = (kh1 - kh0) * (kw1 - kw0) * (g.Cin / BK);
+    ktps = (nkt_total + splits - 1) / splits;
+  }
+  const int kt_beg = split * ktps;
+  const int kt_end = min(nkt_total, kt_beg + ktps);
   const int nk = max(0, kt_end - kt_beg);
 
   // per-lane source roles (fixed over the K loop); 32-bit element offsets.
@@ -482,7 +507,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   for (int j = 0; j < A_INS; ++j) {
     const int row = 8 * (wid * A_INS + j) + (lane >> 3);
     a_ch[j] = (lane & 7) ^ ((row >> 1) & 7);
-    const int m = min(m0 + row, g.M - 1);  // M tail: any valid pixel (masked in the epilogue)
+    const int m = (TAPU && g.posm) ? (pm_b0 + row) * (g.H * g.W) + pm_pos
+                                   : min(m0 + row, g.M - 1);  // M tail: any valid pixel (masked in the epilogue)
     a_base[j] = out_pix(g, m) * g.Cin + (TAPU ? a_ch[j] * 8 : 0);
   }
   int b_off[B_INS], b_k[B_INS];
@@ -497,25 +523,45 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   const rsrc_t wr = make_rsrc(w, (unsigned)((int64_t)g.Cout * g.K * 2));
 
   // Wave-uniform tap state of the next K step to load (TAPU: one step = 64
-  // channels of one tap): off = (kh*Wp + kw)*Cin + c0, advanced incrementally
-  // (no divisions in the loop).
-  struct Tap { int off, c0, kw; };
-  Tap tnext{0, 0, 0};
+  // channels of one tap): off = (kh*Wp + kw)*Cin + c0 (activation), wk =
+  // (kh*KS + kw)*Cin + c0 (weight column), advanced incrementally (no
+  // divisions in the loop).
+  struct Tap { int off, c0, kw, kh, wk; };
+  Tap tnext{0, 0, 0, 0, 0};
   if constexpr (TAPU) {
-    const int k0 = kt_beg * BK;
-    const int kpos = k0 >> (g.logC8 + 3);
-    const int kh = kpos / g.KS, kw = kpos - kh * g.KS;
-    tnext.c0 = k0 & (g.Cin - 1);
+    int kh, kw;
+    if (g.posm) {
+      const int chunks = g.Cin / BK, t = kt_beg / chunks, nkw = kw1 - kw0;
+      tnext.c0 = (kt_beg - t * chunks) * BK;
+      kh = kh0 + t / nkw;
+      kw = kw0 + (t - (t / nkw) * nkw);
+    } else {
+      const int k0 = kt_beg * BK;
+      const int kpos = k0 >> (g.logC8 + 3);
+      kh = kpos / g.KS;
+      kw = kpos - kh * g.KS;
+      tnext.c0 = k0 & (g.Cin - 1);
+    }
     tnext.kw = kw;
+    tnext.kh = kh;
     tnext.off = (kh * g.Wp + kw) * g.Cin + tnext.c0;
+    tnext.wk = (kh * g.KS + kw) * g.Cin + tnext.c0;
   }
   auto tap_advance = [&](Tap& t) {
     if constexpr (TAPU) {
       t.off += BK;
+      t.wk += BK;
       t.c0 += BK;
       if (t.c0 == g.Cin) {
         t.c0 = 0;
-        if (++t.kw == g.KS) { t.kw = 0; t.off += (g.Wp - g.KS) * g.Cin; }
+        if (g.posm) {  // next valid tap of the tile's window
+          if (++t.kw == kw1) { t.kw = kw0; ++t.kh; }
+          t.off = (t.kh * g.Wp + t.kw) * g.Cin;
+          t.wk = (t.kh * g.KS + t.kw) * g.Cin;
+        } else if (++t.kw == g.KS) {
+          t.kw = 0;
+          t.off += (g.Wp - g.KS) * g.Cin;
+        }
       }
     }
   };
@@ -539,7 +585,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
       }
     } else {
       const int j = q - A_INS;
-      const int kadd = kt * BK;
+      const int kadd = TAPU ? t.wk : kt * BK;
       unsigned voff = 2u * (unsigned)b_off[j];
       if constexpr (!TAPU) voff = (kadd + b_k[j]) < g.K ? voff : kOOB;  // K tail (first layer only)
       blds16(wr, voff, 2u * (unsigned)kadd, sB + (wid * B_INS + j) * 1024);
@@ -621,9 +667,11 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
     }
   };
   if constexpr (TR)
-    conv_fwd_epilogue_t<BM, BN, STATS, SLAB, WM, WN, FM, FN, ADD>(acc, g, y, stats, slab, split, tm, m0, n0, smem);
+    conv_fwd_epilogue_t<BM, BN, STATS, SLAB, WM, WN, FM, FN, ADD>(acc, g, y, stats, slab, split, tm, m0, n0, smem,
+                                                                  pm_b0, pm_pos);
   else
-    conv_fwd_epilogue<BM, BN, STATS, SLAB, WM, WN, ADD>(acc, g, y, stats, slab, split, tm, m0, n0, smem);
+    conv_fwd_epilogue<BM, BN, STATS, SLAB, WM, WN, ADD>(acc, g, y, stats, slab, split, tm, m0, n0, smem, pm_b0,
+                                                        pm_pos);
   dbg_out();
 }
 
@@ -1635,9 +1683,18 @@ static uintptr_t g_fwd_addend = 0;  // conv_fwd_add: bf16 [M][Cout] added in the
 static int g_fwd_tr = 1;
 void set_conv_fwd_tr(int on) { g_fwd_tr = on ? 1 : 0; }
 
+// Position-major tiles with padding taps skipped (conv_fwd_kernel, g.posm):
+// for TAPU layers whose output is smaller than the kernel (every output pixel
+// then has padding-only taps), the batch a multiple of BM and no addend.
+// set_conv_posm(0) = the pixel-major tiles (A/B).
+static int g_posm = 1;
+void set_conv_posm(int on) { g_posm = on ? 1 : 0; }
+
 template <int BM, int BN, bool TAPU, int ST, int WM, int WN>
-static void launch_fwd_w(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
+static void launch_fwd_w(const ConvGeom& g0, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
                          uintptr_t slab, int splits, hipStream_t s) {
+  ConvGeom g = g0;
+  g.posm = (g_posm && TAPU && !g_fwd_addend && g.B % BM == 0 && (g.H < g.KS || g.W < g.KS)) ? 1 : 0;
   const int ntm = (g.M + BM - 1) / BM, ntn = (g.Cout + BN - 1) / BN;
   const int nkt = (g.Kch + 7) / 8;
   const int ktps = (nkt + splits - 1) / splits;

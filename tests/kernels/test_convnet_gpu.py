@@ -609,3 +609,47 @@ def test_executor_merged_slab_reduce_bitwise(C, monkeypatch):
         grads.append(torch.cat([v.flatten() for v in flat.views_of(flat.grad)]))
     assert torch.isfinite(grads[1]).all()
     assert torch.equal(grads[0], grads[1])
+
+
+# (B, H, Cin, Cout, tile, splits): position-major tiles (batch a multiple of the
+# 128-row tile, output smaller than the 5x5 kernel): the reference's layer 4
+# forward (4x4, 256 -> 512, split 4) and dgrad (512 -> 256, split 8), a 2x2
+# map, a 3x3 map (odd W), 128x64 tiles
+POSM_SHAPES = [(128, 4, 256, 512, 0, 4), (128, 4, 512, 256, 0, 8), (128, 4, 256, 512, 0, 1), (256, 2, 128, 128, 0, 2),
+               (128, 3, 64, 128, 2, 3), (256, 4, 128, 64, 2, 1)]
+
+
+@pytest.mark.parametrize("shape", POSM_SHAPES)
+def test_conv_fwd_position_major(C, shape):
+    """Streaming conv with position-major M tiles and the zero-border taps
+    skipped (g.posm) vs an fp32 reference and vs the pixel-major tiles
+    (bitwise without split-K: skipping exact-zero products keeps every fp32
+    partial sum); BN statistics of exactly the stored values."""
+    B, H, cin, cout, tile, splits = shape
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(B + H * cin + cout)
+    x = torch.randn(B, H, H, cin, device=dev, generator=g).to(torch.bfloat16)
+    w = (torch.randn(cout, 5, 5, cin, device=dev, generator=g) * 0.05).to(torch.bfloat16)
+    xp = _pad(x)
+    rows = C.conv_fwd_stat_rows(B, H, H, cin, cout, 5, tile, splits)
+    slab = torch.empty(splits * B * H * H * cout, device=dev)
+    outs = []
+    for posm in (0, 1):
+        C.set_conv_posm(posm)
+        try:
+            y = torch.full((B, H, H, cout), float("nan"), dtype=torch.bfloat16, device=dev)
+            stats = torch.full((max(rows, 400), 2, cout), float("nan"), device=dev)
+            T = C.conv_fwd(xp.data_ptr(), w.data_ptr(), y.data_ptr(), stats.data_ptr(), slab.data_ptr(), B, H, H,
+                           cin, cout, 5, tile, splits, _s())
+        finally:
+            C.set_conv_posm(1)
+        torch.cuda.synchronize()
+        outs.append((y, stats[:T].sum(0)))
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=2).permute(0, 2, 3, 1)
+    y, st = outs[1]
+    assert _rel(y, ref) < 8e-3
+    if splits == 1:
+        assert torch.equal(outs[0][0], y)
+    yf = y.float().reshape(-1, cout)
+    torch.testing.assert_close(st[0], yf.sum(0), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(st[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
