@@ -1021,11 +1021,27 @@ __global__ void __launch_bounds__(256) splitk_combine_kernel(const float* __rest
         const float4 b = *reinterpret_cast<const float4*>(p + 4);
         v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
       }
-      for (int s = 1; s < splits; ++s) {
-        const float* q = p + (int64_t)s * M * N;
-        const float4 a = *reinterpret_cast<const float4*>(q);
-        const float4 b = *reinterpret_cast<const float4*>(q + 4);
+      // splits in batches of 4 with every load of a batch issued before the
+      // first add (a load->add chain per split was latency-bound); the adds
+      // keep the split order
+      auto add8 = [&](const float4& a, const float4& b) {
         v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+      };
+      int s = 1;
+      for (; s + 3 < splits; s += 4) {
+        float4 a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float* q = p + (int64_t)(s + u) * M * N;
+          a[u] = *reinterpret_cast<const float4*>(q);
+          b[u] = *reinterpret_cast<const float4*>(q + 4);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) add8(a[u], b[u]);
+      }
+      for (; s < splits; ++s) {
+        const float* q = p + (int64_t)s * M * N;
+        add8(*reinterpret_cast<const float4*>(q), *reinterpret_cast<const float4*>(q + 4));
       }
       uint4 o;
       o.x = pack_bf16x2(v[0], v[1]); o.y = pack_bf16x2(v[2], v[3]);

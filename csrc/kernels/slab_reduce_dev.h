@@ -22,8 +22,18 @@ __device__ __forceinline__ void slab_reduce_body(const float* __restrict__ slabs
     const int c = (int)(i % C);
     const int64_t rest = i / C;  // co*taps + tap
     const int64_t src = rest * Cp + c;
+    // splits in batches of 4 loads in flight before the adds (a load->add chain
+    // per split was latency-bound); the adds keep the split order
     float s = 0.f;
-    for (int sp = sub; sp < splits; sp += TPO) s += slabs[sp * slab + src];
+    int sp = sub;
+    for (; sp + 3 * TPO < splits; sp += 4 * TPO) {
+      float a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] = slabs[(int64_t)(sp + u * TPO) * slab + src];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s += a[u];
+    }
+    for (; sp < splits; sp += TPO) s += slabs[(int64_t)sp * slab + src];
 #pragma unroll
     for (int o = TPO / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
     if (sub == 0) {
