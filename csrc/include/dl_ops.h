@@ -62,6 +62,7 @@ void conv_fwd_add(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t addend, int B
                   int KS, int tile, uintptr_t stream);
 void set_conv_fwd_tr(int on);
 void set_conv_posm(int on);
+void set_conv_wgrad_xcd(int on);
 void slab_reduce(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream);
 void slab_reduce_add(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream);
 void slab_reduce_add_oihw(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C,

@@ -1103,10 +1103,23 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const int ntm = g.Cout / BM, ntn = (g.Kch * 8 + BN - 1) / BN;
-  const int tile = xcd_swizzle(blockIdx.x, ntm * ntn);
+  // 1-D grid (gridDim.y == 1): split-major XCD-aware order -- the workgroups of
+  // one K split (same dy rows, same x pixels, different taps / channel tiles)
+  // get consecutive ids after the swizzle, i.e. one XCD, so the split's rows
+  // are fetched into that XCD's L2 once instead of once per XCD.  2-D grid
+  // (x = tile, y = split; the earlier layout): a split's tiles land on
+  // (x + y * gridDim.x) % 8, i.e. on every XCD.
+  int tile, split;
+  if (gridDim.y == 1) {
+    const int id = xcd_swizzle(blockIdx.x, gridDim.x);
+    split = id / (ntm * ntn);
+    tile = id - split * (ntm * ntn);
+  } else {
+    tile = xcd_swizzle(blockIdx.x, ntm * ntn);
+    split = blockIdx.y;
+  }
   const int tm = tile % ntm, tn = tile / ntm;
   const int co0 = tm * BM, k0 = tn * BN;
-  const int split = blockIdx.y;
   const int mbeg = split * m_per_split;
   const int mend = min(g.M, mbeg + m_per_split);
   const int HW = 1 << g.logHW, Wd = g.W, C8 = 1 << g.logC8;
@@ -1993,6 +2006,10 @@ void conv_fwd_add(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t addend, int B
 // out: fp32 [splits][Cout][ldo], ldo >= K (K = KS*KS*Cin); tile 0 = 128x64, 1 = 64x64 (co x k)
 // atomic_creal > 0: every split atomically adds into the ZEROED fp32 gradient
 // out = [Cout][KS*KS][atomic_creal] (no slabs, no slab_reduce).
+// 1 = 1-D split-major XCD-aware wgrad grid (conv_wgrad_kernel), 0 = the 2-D grid (A/B)
+static int g_wgrad_xcd = 1;
+void set_conv_wgrad_xcd(int on) { g_wgrad_xcd = on ? 1 : 0; }
+
 void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, int Cin, int Cout, int KS, int splits,
                 int ldo, int tile, int atomic_creal, uintptr_t stream) {
   ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
@@ -2011,11 +2028,12 @@ void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, i
 #define DL_WGX(BM_, BN_, ST_, WM_, WN_, PF_)                                                                \
   do {                                                                                                     \
     const int nt = ((g.Cout + BM_ - 1) / BM_) * ((g.K + BN_ - 1) / BN_);                                  \
+    const dim3 grid = g_wgrad_xcd ? dim3(nt * splits, 1) : dim3(nt, splits);                              \
     if (atom)                                                                                              \
-      conv_wgrad_kernel<BM_, BN_, ST_, WM_, WN_, PF_, true><<<dim3(nt, splits), 64 * WM_ * WN_, 0, s>>>(   \
+      conv_wgrad_kernel<BM_, BN_, ST_, WM_, WN_, PF_, true><<<grid, 64 * WM_ * WN_, 0, s>>>(               \
           (const bf16_t*)dy, (const bf16_t*)x, (float*)out, g, mps, ldo, atomic_creal);                     \
     else                                                                                                   \
-      conv_wgrad_kernel<BM_, BN_, ST_, WM_, WN_, PF_, false><<<dim3(nt, splits), 64 * WM_ * WN_, 0, s>>>(  \
+      conv_wgrad_kernel<BM_, BN_, ST_, WM_, WN_, PF_, false><<<grid, 64 * WM_ * WN_, 0, s>>>(              \
           (const bf16_t*)dy, (const bf16_t*)x, (float*)out, g, mps, ldo, Cin);                              \
   } while (0)
 #define DL_WG(BM_, BN_, ST_, WM_, WN_) DL_WGX(BM_, BN_, ST_, WM_, WN_, true)

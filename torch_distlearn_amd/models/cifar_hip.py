@@ -145,6 +145,8 @@ class CifarHIPExecutor:
         # CUs held by the concurrent collective's workgroups (wgrad grids leave them free)
         self.cu_reserve = int(os.environ.get("DISTLEARN_CU_RESERVE",
                                              getattr(comm, "cu_reserve", 0) if overlapped else 0))
+        if "DISTLEARN_WGRAD_XCD" in os.environ:  # A/B: split-major XCD-aware wgrad grid (1) or the 2-D grid (0)
+            self.C.set_conv_wgrad_xcd(int(os.environ["DISTLEARN_WGRAD_XCD"]))
         if "DISTLEARN_POSM" in os.environ:  # A/B: position-major conv tiles for the 4x4 layer (1) or not (0)
             self.C.set_conv_posm(int(os.environ["DISTLEARN_POSM"]))
         if "DISTLEARN_FWD_TR" in os.environ:  # A/B: transposed-accumulator streaming kernel (1) or not (0)
