@@ -46,6 +46,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_conv_fwd_tr", &set_conv_fwd_tr);
   m.def("set_conv_posm", &set_conv_posm);
   m.def("set_conv_wgrad_xcd", &set_conv_wgrad_xcd);
+  m.def("set_conv_fwd_order", &set_conv_fwd_order);
   m.def("set_conv_waves", &set_conv_waves);
   m.def("set_conv_debug", &set_conv_debug);
   m.def("conv_wgrad", &conv_wgrad);

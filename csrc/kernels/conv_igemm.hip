@@ -64,6 +64,7 @@ struct ConvGeom {
   int M, K, Kch;           // M = B*H*W, K = KS*KS*Cin, Kch = K/8
   int pow2;                // H and W powers of two (the region / c8 kernels and the shift addressing)
   int posm;                // streaming kernel: position-major M tiles with padding taps skipped (fwd_posm)
+  int mmajor;              // fwd/dgrad tile order after the XCD swizzle: 0 panel-major, 1 M-tile-major
   float inv_HW, inv_W;     // reciprocals for the non-pow2 pixel decomposition (fdivmod)
 };
 
@@ -106,6 +107,7 @@ static ConvGeom make_geom(int B, int H, int W, int Cin, int Cout, int KS) {
   if (Cin < 8) throw std::runtime_error("conv: Cin must be >= 8 (pad the input channels)");
   g.pow2 = is_pow2(W) && is_pow2(H) ? 1 : 0;
   g.posm = 0;
+  g.mmajor = 0;
   g.logW = g.pow2 ? ilog2_exact(W, "W") : 0;
   g.logHW = g.pow2 ? ilog2_exact(H * W, "H*W") : 0;
   g.inv_HW = 1.0f / (float)(H * W);
@@ -470,9 +472,10 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   // swizzle) share one (n-tile, K-split) weight panel and sweep the M tiles,
   // so the panel is fetched into that XCD's L2 once instead of every XCD
   // streaming the whole weight tensor from the Infinity Cache.
-  const int id = xcd_swizzle(blockIdx.x, ntm * (g.Cout / BN) * splits);
-  const int tm = id % ntm;
-  const int panel = id / ntm;
+  const int npanel = (g.Cout / BN) * splits;
+  const int id = xcd_swizzle(blockIdx.x, ntm * npanel);
+  const int tm = g.mmajor ? id / npanel : id % ntm;
+  const int panel = g.mmajor ? id - tm * npanel : id / ntm;
   const int split = panel % splits, tn = panel / splits;
   const int m0 = tm * BM, n0 = tn * BN;
   const int C8 = 1 << g.logC8;
@@ -727,9 +730,10 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf1
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const int ntm = (g.M + BM - 1) / BM;
-  const int id = xcd_swizzle(blockIdx.x, ntm * (g.Cout / BN) * splits);
-  const int tm = id % ntm;
-  const int panel = id / ntm;
+  const int npanel = (g.Cout / BN) * splits;
+  const int id = xcd_swizzle(blockIdx.x, ntm * npanel);
+  const int tm = g.mmajor ? id / npanel : id % ntm;
+  const int panel = g.mmajor ? id - tm * npanel : id / ntm;
   const int split = panel % splits, tn = panel / splits;
   const int m0 = tm * BM, n0 = tn * BN;
   const int HW = 1 << g.logHW, Wd = g.W;
@@ -1928,10 +1932,17 @@ static void launch_fwd_region(const ConvGeom& g, const RegionGeom& rg, uintptr_t
 // tile: 0 = 128x128, 1 = 64x64, 2 = 128x64 (BM x BN, BK = 64).  splits > 1:
 // split-K into `slab` (fp32 [splits][M][Cout]) + combine (bf16 y, BN partials).
 // Returns the number of BN partial rows written to `stats` (if non-null).
+// fwd/dgrad workgroup order after the XCD swizzle (A/B knob): 0 = panel-major
+// (an XCD's workgroups share a weight panel and sweep M tiles), 1 = M-major
+// (they share M tiles and sweep the panels)
+static int g_fwd_mmajor = 0;
+void set_conv_fwd_order(int mmajor) { g_fwd_mmajor = mmajor ? 1 : 0; }
+
 int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab, int B, int H, int W, int Cin,
              int Cout, int KS, int tile, int splits, uintptr_t stream) {
   const FwdCfg cfg(tile);
   ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
+  g.mmajor = g_fwd_mmajor;
   hipStream_t s = as_stream(stream);
   if (splits < 1) splits = 1;
   if (splits > 1 && !slab) throw std::runtime_error("conv_fwd: split-K needs a slab");

@@ -147,6 +147,8 @@ class CifarHIPExecutor:
                                              getattr(comm, "cu_reserve", 0) if overlapped else 0))
         if "DISTLEARN_WGRAD_XCD" in os.environ:  # A/B: split-major XCD-aware wgrad grid (1) or the 2-D grid (0)
             self.C.set_conv_wgrad_xcd(int(os.environ["DISTLEARN_WGRAD_XCD"]))
+        if "DISTLEARN_FWD_MMAJOR" in os.environ:  # A/B: fwd/dgrad tile order after the XCD swizzle
+            self.C.set_conv_fwd_order(int(os.environ["DISTLEARN_FWD_MMAJOR"]))
         if "DISTLEARN_POSM" in os.environ:  # A/B: position-major conv tiles for the 4x4 layer (1) or not (0)
             self.C.set_conv_posm(int(os.environ["DISTLEARN_POSM"]))
         if "DISTLEARN_FWD_TR" in os.environ:  # A/B: transposed-accumulator streaming kernel (1) or not (0)
