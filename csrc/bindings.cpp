@@ -78,6 +78,7 @@ PYBIND11_MODULE(_C, m) {
     set_reduce_atomic_bn(rows);
   });
   m.def("reduce_atomic", []() { return reduce_rows(); });
+  m.def("set_bn_fin_grid", &set_bn_fin_grid);
   m.def("head_fwd_bwd", &head_fwd_bwd);
   m.def("head_fwd_bwd_pool", &head_fwd_bwd_pool);
   m.def("bn_bwd_reduce_head", &bn_bwd_reduce_head);

@@ -106,6 +106,7 @@ void bn_relu_pool_fwd_fin(uintptr_t y, uintptr_t sums, int64_t M, uintptr_t gamm
                           int B, int H, int W, int C, int opad, uintptr_t stream);
 void set_reduce_atomic_bn(int rows);
 int reduce_rows();
+void set_bn_fin_grid(int cap);
 
 // head.hip --------------------------------------------------------------------
 void head_fwd_bwd(uintptr_t h, uintptr_t w, uintptr_t bias, uintptr_t labels, int F, int B, int NC,

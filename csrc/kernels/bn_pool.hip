@@ -37,6 +37,14 @@ __device__ int g_red_atomic_bn = 0;
 static int g_host_rows = 0;  // host mirror (BnFin::R of the launchers)
 int reduce_rows() { return g_host_rows; }
 
+// Grid cap of the consumer kernels that sum the R accumulated rows in a
+// per-block prologue (bn_relu_pool_fwd_fin, bn_relu_pool_bwd_apply_sums):
+// every block re-reads C x R x 2 floats, so fewer blocks with several items
+// per thread (the next item's loads stay in flight) read fewer row bytes.
+static int g_fin_grid = 2048;
+void set_bn_fin_grid(int cap) { g_fin_grid = cap < 1 ? 1 : cap; }
+static int fin_grid(int64_t total) { return std::min(stream_grid(total), g_fin_grid); }
+
 __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
   f[0] = lo_bf16(v.x); f[1] = hi_bf16(v.x); f[2] = lo_bf16(v.y); f[3] = hi_bf16(v.y);
   f[4] = lo_bf16(v.z); f[5] = hi_bf16(v.z); f[6] = lo_bf16(v.w); f[7] = hi_bf16(v.w);
@@ -633,7 +641,7 @@ void bn_relu_pool_bwd_apply_sums(uintptr_t y, uintptr_t dP, uintptr_t coef, uint
     throw std::runtime_error("bn_relu_pool_bwd_apply_sums: needs an atomic reduction mode with <= 32 rows");
   if ((dgamma_out == 0) != (dbeta_out == 0)) throw std::runtime_error("bn_relu_pool_bwd_apply_sums: dgamma/dbeta");
   const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
-  bn_relu_pool_bwd_apply_kernel<true><<<stream_grid(total), 256, 0, as_stream(stream)>>>(
+  bn_relu_pool_bwd_apply_kernel<true><<<fin_grid(total), 256, 0, as_stream(stream)>>>(
       (const bf16_t*)y, (const bf16_t*)dP, (const float*)coef, (const float*)dgb, (bf16_t*)dy, B, H, W, C, opad,
       (const float*)gamma, 1.0f / (float)M, g_host_rows, (float*)dgamma_out, (float*)dbeta_out);
   DL_HIP_CHECK(hipGetLastError());
@@ -649,7 +657,7 @@ void bn_relu_pool_fwd_fin(uintptr_t y, uintptr_t sums, int64_t M, uintptr_t gamm
     throw std::runtime_error("bn_relu_pool_fwd_fin: needs an atomic reduction mode with <= 32 rows");
   const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
   const BnFin fin = make_bn_fin(sums, M, gamma, beta, bias, rmean, rvar, eps, momentum, coef, g_host_rows);
-  bn_relu_pool_fwd_fin_kernel<<<stream_grid(total), 256, 0, as_stream(stream)>>>((const bf16_t*)y, fin,
+  bn_relu_pool_fwd_fin_kernel<<<fin_grid(total), 256, 0, as_stream(stream)>>>((const bf16_t*)y, fin,
                                                                                    (bf16_t*)out, B, H, W, C, opad);
   DL_HIP_CHECK(hipGetLastError());
 }
