@@ -932,7 +932,12 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf1
 template <bool STATS>
 __global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                           bf16_t* __restrict__ y, float* __restrict__ stats,
-                                                          const ConvGeom g, int region_rows) {
+                                                          const ConvGeom g, int region_rows, int mt) {
+  // mt consecutive 128-pixel M tiles per workgroup (whole output rows of one
+  // image): the weight panel (BN x taps x 16 B = 25.6 KiB for the reference's
+  // layer 1) is DMA'd once per workgroup instead of once per tile, the region
+  // covers the mt tiles' rows + the kernel halo, and the tiles are computed
+  // one after the other from LDS (epilogue scratch after the region).
   constexpr int BM = 128, BN = 64, WM = 4, WN = 2, NW = 8, TM = 32, TN = 32, FM = 2, FN = 2;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int taps = g.KS * g.KS;                      // K = taps * 8
@@ -943,16 +948,17 @@ __global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restri
   const int wslots_p = (wslots + 63) / 64 * 64;
   char* sR = smem;
   char* sW = smem + rslots_p * 16;
+  char* sX = sW + wslots_p * 16;  // epilogue scratch ([WM][2][BN] floats)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
-  const int ntm = (g.M + BM - 1) / BM;
-  const int id = xcd_swizzle(blockIdx.x, ntm * (g.Cout / BN));
-  const int tm = id % ntm, tn = id / ntm;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int ntm = (g.M + BM - 1) / BM, ngr = ntm / mt;  // host: mt | ntm, mt * BM | H * W
+  const int id = xcd_swizzle(blockIdx.x, ngr * (g.Cout / BN));
+  const int tg = id % ngr, tn = id / ngr;
+  const int mg0 = tg * mt * BM, n0 = tn * BN;
   const int HW = 1 << g.logHW;
-  const int img0 = m0 >> g.logHW, oh0 = (m0 & (HW - 1)) >> g.logW;
+  const int img0 = mg0 >> g.logHW, oh0 = (mg0 & (HW - 1)) >> g.logW;
   const int start_pix = (img0 * g.Hp + oh0) * g.Wp;
   const rsrc_t xr = make_rsrc(x, (unsigned)((int64_t)g.B * g.Hp * g.Wp * 16));
   const rsrc_t wr = make_rsrc(w, (unsigned)((int64_t)g.Cout * taps * 16));
@@ -966,23 +972,25 @@ __global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restri
     blds16(wr, sl < wslots ? 16u * (unsigned)(n0 * taps + sl) : kOOB, 0u, sW + q * 1024);
   }
   const int i = lane & 15, qg = lane >> 4;
-  int a_pix[FM];
-#pragma unroll
-  for (int a = 0; a < FM; ++a) {
-    const int m = min(m0 + wm * TM + a * 16 + i, g.M - 1) - m0;  // tile-local output pixel
-    a_pix[a] = (m >> g.logW) * g.Wp + (m & (g.W - 1));
-  }
   int b_row[FN];
 #pragma unroll
   for (int b = 0; b < FN; ++b) b_row[b] = wn * TN + 8 * (i >> 2) + 4 * b + (i & 3);
+  wait_vmcnt<0>();
+  block_sync_lds();
+  const int zero_slot = rslots;  // loaded from an out-of-range offset: zeros
+  for (int t_ = 0; t_ < mt; ++t_) {
+  const int tm = tg * mt + t_, m0 = tm * BM;
+  int a_pix[FM];
+#pragma unroll
+  for (int a = 0; a < FM; ++a) {
+    const int m = min(m0 + wm * TM + a * 16 + i, g.M - 1) - mg0;  // group-local output pixel
+    a_pix[a] = (m >> g.logW) * g.Wp + (m & (g.W - 1));
+  }
   f32x4 acc[FM][FN];
 #pragma unroll
   for (int a = 0; a < FM; ++a)
 #pragma unroll
     for (int b = 0; b < FN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  wait_vmcnt<0>();
-  block_sync_lds();
-  const int zero_slot = rslots;  // loaded from an out-of-range offset: zeros
   for (int st = 0; st < nsteps; ++st) {
     const int t = 4 * st + qg;  // this lane group's tap
     const int kh = t / g.KS, kw = t - (t / g.KS) * g.KS;
@@ -999,7 +1007,8 @@ __global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restri
 #pragma unroll
       for (int b = 0; b < FN; ++b) acc[a][b] = mfma16(fb[b], fa[a], acc[a][b]);
   }
-  conv_fwd_epilogue_t<128, BN, STATS, false, WM, WN, FM, FN>(acc, g, y, stats, nullptr, 0, tm, m0, n0, smem);
+  conv_fwd_epilogue_t<128, BN, STATS, false, WM, WN, FM, FN>(acc, g, y, stats, nullptr, 0, tm, m0, n0, sX);
+  }
 }
 
 // split-K combine: y = bf16(sum_s slab[s]) (+ BN partial sums, one row per block)
@@ -1932,6 +1941,16 @@ static void launch_fwd_region(const ConvGeom& g, const RegionGeom& rg, uintptr_t
 // tile: 0 = 128x128, 1 = 64x64, 2 = 128x64 (BM x BN, BK = 64).  splits > 1:
 // split-K into `slab` (fp32 [splits][M][Cout]) + combine (bf16 y, BN partials).
 // Returns the number of BN partial rows written to `stats` (if non-null).
+// M tiles per workgroup of the first-layer (Cin = 8) kernel (upper bound; set_conv_c8_mt).
+// Measured at batch 128 (profiles/r2_c8_mt_ab.txt): 1 tile (1024 workgroups, 4 per CU)
+// 12.0 us, 4 tiles (256 workgroups, one weight-panel DMA each) 14.8 us: the kernel is
+// bound by its epilogue stores overlapping across workgroups, not by the weight DMA.
+static int g_c8_mt = 1;
+void set_conv_c8_mt(int mt) {
+  if (mt != 1 && mt != 2 && mt != 4 && mt != 8) throw std::runtime_error("c8 tiles per workgroup: 1, 2, 4 or 8");
+  g_c8_mt = mt;
+}
+
 // fwd/dgrad workgroup order after the XCD swizzle (A/B knob): 0 = panel-major
 // (an XCD's workgroups share a weight panel and sweep M tiles), 1 = M-major
 // (they share M tiles and sweep the panels)
@@ -1950,18 +1969,30 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
   if (tile < 0 || tile > 2) throw std::runtime_error("conv_fwd: bad tile id");
   if (Cout % fwd_bn(tile) != 0) throw std::runtime_error("conv_fwd: Cout must be a multiple of the N tile");
   RegionGeom rg;
-  const int c8_rows = 128 / std::max(1, W) + KS - 1;
-  const size_t c8_lds = (size_t)((c8_rows * g.Wp + 1 + 63) / 64 * 64 + (64 * KS * KS + 63) / 64 * 64) * 16;
+  // c8 kernel: mt M tiles per workgroup (largest of g_c8_mt, ..., 2, 1 that keeps
+  // >= 256 workgroups and divides the tiles of one image)
+  int c8_mt = 1;
+  const int c8_ntm = (H * W) % 128 == 0 ? g.M / 128 : 0;
+  for (int mt = g_c8_mt; mt > 1; mt /= 2) {
+    if (c8_ntm > 0 && (H * W) % (mt * 128) == 0 && c8_ntm % mt == 0 && (c8_ntm / mt) * std::max(1, Cout / 64) >= 256) {
+      c8_mt = mt;
+      break;
+    }
+  }
+  const int c8_rows = c8_mt * 128 / std::max(1, W) + KS - 1;
+  const size_t c8_lds =
+      (size_t)((c8_rows * g.Wp + 1 + 63) / 64 * 64 + (64 * KS * KS + 63) / 64 * 64) * 16 + 4 * 2 * 64 * 4;
   if (tile == 2 && splits == 1 && g_region && g.pow2 && Cin == 8 && W <= 128 && 128 % W == 0 && (H * W) % 128 == 0 &&
       Cout % 64 == 0 && c8_lds <= 160 * 1024) {
-    const int grid = (g.M / 128) * (Cout / 64);
+    const int grid = (g.M / 128 / c8_mt) * (Cout / 64);
     auto go = [&](auto kern) {
       static bool attr = false;
       if (!attr) {
         DL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
       }
-      kern<<<grid, 512, c8_lds, s>>>((const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)stats, g, c8_rows);
+      kern<<<grid, 512, c8_lds, s>>>((const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)stats, g, c8_rows,
+                                     c8_mt);
     };
     if (stats) go(conv_fwd_c8_kernel<true>);
     else go(conv_fwd_c8_kernel<false>);

@@ -653,3 +653,34 @@ def test_conv_fwd_position_major(C, shape):
     yf = y.float().reshape(-1, cout)
     torch.testing.assert_close(st[0], yf.sum(0), rtol=1e-3, atol=1e-2)
     torch.testing.assert_close(st[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("B", [128, 64])
+def test_conv_c8_tiles_per_workgroup(C, B):
+    """First-layer (Cin = 8) kernel with several M tiles per workgroup sharing
+    one weight-panel DMA == one tile per workgroup, bitwise (output and the
+    per-tile BN partial rows), and vs an fp32 reference."""
+    dev = torch.device("cuda")
+    H, cin, cout = 32, 8, 64
+    g = torch.Generator(device=dev).manual_seed(B)
+    x = torch.randn(B, H, H, cin, device=dev, generator=g).to(torch.bfloat16)
+    w = (torch.randn(cout, 5, 5, cin, device=dev, generator=g) * 0.1).to(torch.bfloat16)
+    xp = _pad(x)
+    rows = C.conv_fwd_stat_rows(B, H, H, cin, cout, 5, 2, 1)
+    outs = []
+    for mt in (1, 4):
+        C.set_conv_c8_mt(mt)
+        try:
+            y = torch.full((B, H, H, cout), float("nan"), dtype=torch.bfloat16, device=dev)
+            stats = torch.full((rows, 2, cout), float("nan"), device=dev)
+            T = C.conv_fwd(xp.data_ptr(), w.data_ptr(), y.data_ptr(), stats.data_ptr(), 0, B, H, H, cin, cout, 5,
+                           2, 1, _s())
+        finally:
+            C.set_conv_c8_mt(1)
+        torch.cuda.synchronize()
+        assert T == rows
+        outs.append((y, stats))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=2).permute(0, 2, 3, 1)
+    assert _rel(outs[1][0], ref) < 8e-3

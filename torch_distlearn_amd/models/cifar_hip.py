@@ -145,6 +145,8 @@ class CifarHIPExecutor:
         # CUs held by the concurrent collective's workgroups (wgrad grids leave them free)
         self.cu_reserve = int(os.environ.get("DISTLEARN_CU_RESERVE",
                                              getattr(comm, "cu_reserve", 0) if overlapped else 0))
+        if "DISTLEARN_C8_MT" in os.environ:  # tuning: layer-1 M tiles per workgroup (1, 2, 4, 8)
+            self.C.set_conv_c8_mt(int(os.environ["DISTLEARN_C8_MT"]))
         if "DISTLEARN_FIN_GRID" in os.environ:  # tuning: grid cap of the row-summing BN consumers
             self.C.set_bn_fin_grid(int(os.environ["DISTLEARN_FIN_GRID"]))
         if "DISTLEARN_WGRAD_XCD" in os.environ:  # A/B: split-major XCD-aware wgrad grid (1) or the 2-D grid (0)
