@@ -260,3 +260,34 @@ def test_atomic_modes_train_and_graph_tracks_eager(dev, monkeypatch, mode):
     for losses in res:
         assert losses[-1] < 0.5 * losses[0]
     assert max(abs(a - b) for a, b in zip(*res)) < 0.05 * res[0][0]
+
+
+def test_ea_run_unrolled_matches_stepwise(dev):
+    """AllReduceEA under trainer.run: tau-step graphs that end with the
+    elastic round (fused elastic kernel + delta all-reduce + center update)
+    plus local-step graphs == one captured step at a time with the round run
+    eagerly every tau steps (deterministic reduction mode: bitwise)."""
+    from torch_distlearn_amd import Tree
+    from torch_distlearn_amd.engine import DataParallelTrainer
+    from torch_distlearn_amd.models import CifarConvNet
+
+    outs = []
+    for unrolled in (False, True):
+        tree = Tree(1, 1, host="127.0.0.1", port=29708, device=dev)
+        model = CifarConvNet(seed=9).to(dev)
+        tr = DataParallelTrainer(model, tree, lr=0.02, algo="ea", tau=3, alpha=0.3, backend="hip",
+                                 compute_dtype=torch.bfloat16, graph=True, max_batch=16)
+        tr.synchronize_parameters()
+        ld = _loader(dev, batch=16)
+        if unrolled:
+            tr.run(ld, 11, unroll=4)
+            assert ("ea", 3) in tr._multi and tr.captures == 4  # 1-, 2-, 4-step graphs + the tau graph
+        else:
+            for _ in range(11):
+                tr.step(ld)
+        torch.cuda.synchronize()
+        outs.append((tr.flat.data.clone(), tr.ea.center.clone(), tr.ea.step, int(ld.ctr[0]), tr.steps))
+    (p0, c0, s0, k0, n0), (p1, c1, s1, k1, n1) = outs
+    assert (s0, k0, n0) == (s1, k1, n1) == (11, 11, 11)
+    assert not torch.equal(c0, p0)  # the rounds moved the center
+    assert torch.equal(p0, p1) and torch.equal(c0, c1)

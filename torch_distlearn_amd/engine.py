@@ -183,7 +183,13 @@ class DataParallelTrainer:
         unroll, unroll/2, ... 2 steps are kept and the largest that fits the
         remaining steps (and the epoch) is replayed, the single-step graph
         covers the rest.  Every step is still a complete step (the same
-        kernels and collectives as :meth:`step`)."""
+        kernels and collectives as :meth:`step`).
+
+        AllReduceEA: the local-step graphs cover the steps between elastic
+        rounds, and when a tau-step cycle starts on a step boundary ONE graph
+        holds the tau local steps plus the elastic round (fused elastic kernel,
+        delta all-reduce, center update: lua/AllReduceEA.lua:25-47); a round
+        that falls elsewhere runs through :meth:`step`."""
         loss = None
         fast = self._unrolled(unroll) and getattr(self.executor, "takes_loader", False)
         if fast:
@@ -194,12 +200,23 @@ class DataParallelTrainer:
             self.prepare(loader, unroll)
         while nsteps > 0:
             left = loader.steps_per_epoch - loader._host_steps
-            k = max((u for u in self._multi if u <= min(nsteps, left)), default=1) if fast else 1
+            cap = min(nsteps, left)
+            key = None
+            if fast and self.ea is not None:
+                phase = self.ea.step % self.ea.tau
+                if phase == 0 and cap >= self.ea.tau and self._ea_key() in self._multi:
+                    key = self._ea_key()
+                cap = min(cap, self.ea.tau - 1 - phase)  # local steps before the round-triggering one
+            k = self.ea.tau if key is not None else (
+                max((u for u in self._multi if isinstance(u, int) and u <= cap), default=1) if fast else 1)
             if k > 1:
-                g, loss = self._multi[k]
+                g, loss = self._multi[key if key is not None else k]
                 g.replay()
+                if self.ea is not None:
+                    self.ea.step += k  # the graph ran k local steps (+ the round when key is set)
                 for _ in range(k):
-                    self.sgd._count_step()
+                    if self.sgd is not None:
+                        self.sgd._count_step()
                     loader.step_done()
                 self.steps += k
                 self._track()
@@ -211,7 +228,10 @@ class DataParallelTrainer:
         return loss
 
     def _unrolled(self, unroll: int) -> bool:
-        return self.graph and self.algo == "sgd" and self.executor is not None and unroll > 1
+        return self.graph and self.algo in ("sgd", "ea") and self.executor is not None and unroll > 1
+
+    def _ea_key(self):
+        return ("ea", self.ea.tau)
 
     @staticmethod
     def _unroll_sizes(unroll: int):
@@ -234,6 +254,8 @@ class DataParallelTrainer:
         if not self._unrolled(unroll):
             return
         new = [k for k in self._unroll_sizes(unroll) if k not in self._multi]
+        if self.ea is not None and self.ea.tau > 1 and self._ea_key() not in self._multi:
+            new.append(self._ea_key())
         for k in new:
             self._capture_multi(loader, k)
         if new:
@@ -247,10 +269,13 @@ class DataParallelTrainer:
     def _snapshot(self, loader=None):
         return (self.flat.data.clone(), None if self.mom is None else self.mom.clone(),
                 [b.detach().clone() for b in self.model.buffers()],
-                loader.ctr.clone() if hasattr(loader, "gather_args") else None)
+                loader.ctr.clone() if hasattr(loader, "gather_args") else None,
+                None if self.ea is None or self.ea.center is None else self.ea.center.clone())
 
     def _restore(self, saved, loader=None) -> None:
-        data, mom, bufs, ctr = saved
+        data, mom, bufs, ctr, center = saved
+        if center is not None:
+            self.ea.center.copy_(center)
         self.flat.data.copy_(data)
         self.flat.refresh_shadow()
         if mom is not None:
@@ -267,15 +292,21 @@ class DataParallelTrainer:
         if track is not None and self.device.type == "cuda":
             track()
 
-    def _capture_multi(self, loader, k: int):
+    def _capture_multi(self, loader, k):
         """Capture k consecutive step bodies on ``loader`` into one graph
-        (capture records kernels without running them; replay counts the steps)."""
+        (capture records kernels without running them; replay counts the steps).
+        k = ("ea", tau): tau local steps followed by the AllReduceEA elastic round."""
         self.captures += 1
+        ea_round = isinstance(k, tuple)
+        n = k[1] if ea_round else k
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            for _ in range(k):
+            for _ in range(n):
                 loss = self._step_body(loader, None)
-        self.sgd.stepsPerNode[self.tree.nodeIndex - 1] -= k  # capture counted k (not executed)
+            if ea_round:
+                self.ea.elastic_round()
+        if self.sgd is not None:
+            self.sgd.stepsPerNode[self.tree.nodeIndex - 1] -= n  # capture counted n (not executed)
         self._multi[k] = (g, loss)
         return self._multi[k]
 

@@ -94,12 +94,17 @@ class AllReduceEA:
         self.step += 1
         if self.step % self.tau != 0:
             return False
+        self.elastic_round()
+        return True
+
+    def elastic_round(self) -> None:
+        """The averaging round's device work, no host synchronisation (also
+        captured into the engine's tau-step hipGraph)."""
         p, c, d, s = self._body()
         # delta = alpha (p - c); p -= delta   (K8, writes the comm buffer)
         elastic_step_(p, c, d, self.alpha, shadow=s)
         self.tree.allReduce(FlatBuffer(self.delta))  # (:41)
         add_(c, d)                                   # c += sum(delta)  (:43-45)
-        return True
 
     def _body(self):
         """(params, center, delta, shadow) without the 64-element header: the

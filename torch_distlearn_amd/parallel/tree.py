@@ -143,7 +143,7 @@ class Tree:
         # ---- zero-copy flat buffer ------------------------------------------------
         if len(leaves) == 1 and getattr(leaves[0], "_dl_flat", False):
             buf = leaves[0]
-            buf[SLOT] = 1 if participating else 0
+            buf[SLOT:SLOT + 1].fill_(1 if participating else 0)  # a fill kernel: capturable in a hipGraph
             if opname == "sum":
                 comm.all_reduce(buf, "sum")
             else:
@@ -163,7 +163,7 @@ class Tree:
             buf = self._stage(key, total, t0.dtype, t0.device)
             buf[:HEADER].zero_()
             if gi == 0:
-                buf[SLOT] = 1 if participating else 0
+                buf[SLOT:SLOT + 1].fill_(1 if participating else 0)
             off = HEADER
             views = []
             for i in idxs:
