@@ -262,11 +262,15 @@ def test_atomic_modes_train_and_graph_tracks_eager(dev, monkeypatch, mode):
     assert max(abs(a - b) for a, b in zip(*res)) < 0.05 * res[0][0]
 
 
-def test_ea_run_unrolled_matches_stepwise(dev):
+@pytest.mark.parametrize("rccl", ["0", "1"])
+def test_ea_run_unrolled_matches_stepwise(dev, monkeypatch, rccl):
     """AllReduceEA under trainer.run: tau-step graphs that end with the
     elastic round (fused elastic kernel + delta all-reduce + center update)
     plus local-step graphs == one captured step at a time with the round run
-    eagerly every tau steps (deterministic reduction mode: bitwise)."""
+    eagerly every tau steps (deterministic reduction mode: bitwise).
+    rccl = 1: the world-1 delta all-reduce goes through RCCL (inside the
+    captured tau-step graph)."""
+    monkeypatch.setenv("DISTLEARN_RCCL_WORLD1", rccl)
     from torch_distlearn_amd import Tree
     from torch_distlearn_amd.engine import DataParallelTrainer
     from torch_distlearn_amd.models import CifarConvNet
@@ -274,6 +278,7 @@ def test_ea_run_unrolled_matches_stepwise(dev):
     outs = []
     for unrolled in (False, True):
         tree = Tree(1, 1, host="127.0.0.1", port=29708, device=dev)
+        assert tree.comm._skip1 == (rccl == "0")
         model = CifarConvNet(seed=9).to(dev)
         tr = DataParallelTrainer(model, tree, lr=0.02, algo="ea", tau=3, alpha=0.3, backend="hip",
                                  compute_dtype=torch.bfloat16, graph=True, max_batch=16)
