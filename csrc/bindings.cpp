@@ -48,6 +48,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_conv_wgrad_xcd", &set_conv_wgrad_xcd);
   m.def("set_conv_fwd_order", &set_conv_fwd_order);
   m.def("set_conv_c8_mt", &set_conv_c8_mt);
+  m.def("set_conv_posm_balance", &set_conv_posm_balance);
   m.def("set_conv_waves", &set_conv_waves);
   m.def("set_conv_debug", &set_conv_debug);
   m.def("conv_wgrad", &conv_wgrad);

@@ -65,6 +65,7 @@ void set_conv_posm(int on);
 void set_conv_wgrad_xcd(int on);
 void set_conv_fwd_order(int mmajor);
 void set_conv_c8_mt(int mt);
+void set_conv_posm_balance(int on);
 void slab_reduce(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream);
 void slab_reduce_add(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream);
 void slab_reduce_add_oihw(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C,

@@ -65,6 +65,7 @@ struct ConvGeom {
   int pow2;                // H and W powers of two (the region / c8 kernels and the shift addressing)
   int posm;                // streaming kernel: position-major M tiles with padding taps skipped (fwd_posm)
   int mmajor;              // fwd/dgrad tile order after the XCD swizzle: 0 panel-major, 1 M-tile-major
+  int pm_kmax, pm_P;       // balanced position-major split-K: max K steps per workgroup, workgroups per N tile
   float inv_HW, inv_W;     // reciprocals for the non-pow2 pixel decomposition (fdivmod)
 };
 
@@ -90,6 +91,15 @@ __device__ __forceinline__ int out_pix(const ConvGeom& g, int m) {
   return (b * g.Hp + oh) * g.Wp + ow;
 }
 
+// K steps (64 channels of one tap) of a position-major tile at output pixel
+// pos: the taps whose input pixel is inside the image, times Cin / 64
+__host__ __device__ __forceinline__ int posm_nk(const ConvGeom& g, int pos) {
+  const int oh = pos / g.W, ow = pos - oh * g.W;
+  const int th = min(g.KS, g.H + g.pad - oh) - max(0, g.pad - oh);
+  const int tw = min(g.KS, g.W + g.pad - ow) - max(0, g.pad - ow);
+  return th * tw * (g.Cin / 64);
+}
+
 static int ilog2_exact(int v, const char* what) {
   int l = 0;
   while ((1 << l) < v) ++l;
@@ -108,6 +118,8 @@ static ConvGeom make_geom(int B, int H, int W, int Cin, int Cout, int KS) {
   g.pow2 = is_pow2(W) && is_pow2(H) ? 1 : 0;
   g.posm = 0;
   g.mmajor = 0;
+  g.pm_kmax = 0;
+  g.pm_P = 0;
   g.logW = g.pow2 ? ilog2_exact(W, "W") : 0;
   g.logHW = g.pow2 ? ilog2_exact(H * W, "H*W") : 0;
   g.inv_HW = 1.0f / (float)(H * W);
@@ -472,11 +484,32 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   // swizzle) share one (n-tile, K-split) weight panel and sweep the M tiles,
   // so the panel is fetched into that XCD's L2 once instead of every XCD
   // streaming the whole weight tensor from the Infinity Cache.
-  const int npanel = (g.Cout / BN) * splits;
-  const int id = xcd_swizzle(blockIdx.x, ntm * npanel);
-  const int tm = g.mmajor ? id / npanel : id % ntm;
-  const int panel = g.mmajor ? id - tm * npanel : id / ntm;
-  const int split = panel % splits, tn = panel / splits;
+  int tm, tn, split, nsp_b = 0;
+  if (TAPU && g.posm && g.pm_kmax > 0) {
+    // balanced position-major split-K: N tile tn owns pm_P workgroups; pixel
+    // pos gets nbt * nsp(pos) of them, nsp(pos) = ceil(nk(pos) / pm_kmax)
+    const int id = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int nbt = g.B / BM;
+    tn = id / g.pm_P;
+    int r = id - tn * g.pm_P, pos = 0, nsp = 1;
+    for (; pos < g.H * g.W - 1; ++pos) {
+      nsp = (posm_nk(g, pos) + g.pm_kmax - 1) / g.pm_kmax;
+      if (r < nbt * nsp) break;
+      r -= nbt * nsp;
+    }
+    if (pos == g.H * g.W - 1) nsp = (posm_nk(g, pos) + g.pm_kmax - 1) / g.pm_kmax;
+    const int bblk = r / nsp;
+    split = r - bblk * nsp;
+    tm = pos * nbt + bblk;
+    nsp_b = nsp;
+  } else {
+    const int npanel = (g.Cout / BN) * splits;
+    const int id = xcd_swizzle(blockIdx.x, ntm * npanel);
+    tm = g.mmajor ? id / npanel : id % ntm;
+    const int panel = g.mmajor ? id - tm * npanel : id / ntm;
+    split = panel % splits;
+    tn = panel / splits;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
   const int C8 = 1 << g.logC8;
   // Position-major tiles (g.posm, host-enabled for TAPU layers whose output is
@@ -496,7 +529,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
     kw0 = max(0, g.pad - ow);
     kw1 = min(g.KS, g.W + g.pad - ow);
     nkt_total = (kh1 - kh0) * (kw1 - kw0) * (g.Cin / BK);
-    ktps = (nkt_total + splits - 1) / splits;
+    const int ns = nsp_b > 0 ? nsp_b : splits;
+    ktps = (nkt_total + ns - 1) / ns;
   }
   const int kt_beg = split * ktps;
   const int kt_end = min(nkt_total, kt_beg + ktps);
@@ -1015,7 +1049,9 @@ __global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restri
 template <bool STATS>
 __global__ void __launch_bounds__(256) splitk_combine_kernel(const float* __restrict__ slab, bf16_t* __restrict__ y,
                                                              float* __restrict__ stats, int splits, int M, int N,
-                                                             int rows_per_block) {
+                                                             int rows_per_block, const ConvGeom g) {
+  // g.pm_kmax > 0: balanced position-major split-K -- row m (output pixel
+  // m % HW) has nsp = ceil(nk / pm_kmax) written slices, not `splits`
   const int N8 = N >> 3;
   const int tpr = N8;                 // threads per row (one 8-column chunk each)
   const int rpi = 256 / tpr;          // rows per iteration
@@ -1027,6 +1063,7 @@ __global__ void __launch_bounds__(256) splitk_combine_kernel(const float* __rest
   for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
   if (rsub < rpi) {
     for (int m = r0 + rsub; m < r1; m += rpi) {
+      const int splits_m = g.pm_kmax > 0 ? (posm_nk(g, m % (g.H * g.W)) + g.pm_kmax - 1) / g.pm_kmax : splits;
       float v[8];
       const float* p = slab + (int64_t)m * N + c8 * 8;
       {
@@ -1041,7 +1078,7 @@ __global__ void __launch_bounds__(256) splitk_combine_kernel(const float* __rest
         v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
       };
       int s = 1;
-      for (; s + 3 < splits; s += 4) {
+      for (; s + 3 < splits_m; s += 4) {
         float4 a[4], b[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -1052,7 +1089,7 @@ __global__ void __launch_bounds__(256) splitk_combine_kernel(const float* __rest
 #pragma unroll
         for (int u = 0; u < 4; ++u) add8(a[u], b[u]);
       }
-      for (; s < splits; ++s) {
+      for (; s < splits_m; ++s) {
         const float* q = p + (int64_t)s * M * N;
         add8(*reinterpret_cast<const float4*>(q), *reinterpret_cast<const float4*>(q + 4));
       }
@@ -1720,6 +1757,7 @@ int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile,
 }
 
 static uintptr_t g_fwd_addend = 0;  // conv_fwd_add: bf16 [M][Cout] added in the epilogue
+static int g_fwd_slab_cap = 0;      // split-K slab capacity of the current conv_fwd call (FwdCfg)
 // A/B knob: 0 = the untransposed accumulator layout for the split-K and BN-statistics
 // instances of the streaming kernel (set_conv_fwd_tr)
 static int g_fwd_tr = 1;
@@ -1732,15 +1770,49 @@ void set_conv_fwd_tr(int on) { g_fwd_tr = on ? 1 : 0; }
 static int g_posm = 1;
 void set_conv_posm(int on) { g_posm = on ? 1 : 0; }
 
+// Balanced position-major split-K (g.pm_kmax): instead of `splits` equal
+// parts of every tile, pixel pos gets nsp(pos) = ceil(nk(pos) / kmax) parts
+// with kmax the smallest value that keeps the grid within the uniform plan's
+// and nsp within the slab capacity (CIFAR layer 4: 13 instead of 16 K steps
+// on the critical workgroups).  Measured (profiles/r2_posm_balance_ab.txt): no
+// gain -- layer-4 forward / dgrad 15.8 / 15.9 us vs 14.6 / 14.7, the combine
+// 5.9 vs 4.7 us (fill / epilogue, not the K loop, dominate these workgroups),
+// so it is off by default (set_conv_posm_balance).
+static bool g_posm_balance = false;
+void set_conv_posm_balance(int on) { g_posm_balance = on != 0; }
+
+static void plan_posm_balance(ConvGeom& g, int BM, int ntn, int splits, int cap) {
+  g.pm_kmax = g.pm_P = 0;
+  if (!g.posm || !g_posm_balance || splits <= 1 || cap < splits) return;
+  const int HW = g.H * g.W, nbt = g.B / BM, target = (g.M / BM) * splits;  // workgroups per N tile
+  int nkmax = 0;
+  for (int pos = 0; pos < HW; ++pos) nkmax = std::max(nkmax, posm_nk(g, pos));
+  const int k_uniform = (nkmax + splits - 1) / splits;
+  for (int kmax = 1; kmax < k_uniform; ++kmax) {
+    int P = 0, smax = 0;
+    for (int pos = 0; pos < HW; ++pos) {
+      const int ns = (posm_nk(g, pos) + kmax - 1) / kmax;
+      P += nbt * ns;
+      smax = std::max(smax, ns);
+    }
+    if (P <= target && smax <= cap) {
+      g.pm_kmax = kmax;
+      g.pm_P = P;
+      return;
+    }
+  }
+  (void)ntn;
+}
+
 template <int BM, int BN, bool TAPU, int ST, int WM, int WN>
-static void launch_fwd_w(const ConvGeom& g0, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
+static void launch_fwd_w(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
                          uintptr_t slab, int splits, hipStream_t s) {
-  ConvGeom g = g0;
   g.posm = (g_posm && TAPU && !g_fwd_addend && g.B % BM == 0 && (g.H < g.KS || g.W < g.KS)) ? 1 : 0;
   const int ntm = (g.M + BM - 1) / BM, ntn = (g.Cout + BN - 1) / BN;
+  plan_posm_balance(g, BM, ntn, splits, g_fwd_slab_cap);
   const int nkt = (g.Kch + 7) / 8;
   const int ktps = (nkt + splits - 1) / splits;
-  const int grid = ntm * ntn * splits;
+  const int grid = g.pm_kmax > 0 ? ntn * g.pm_P : ntm * ntn * splits;
   constexpr int NT = 64 * WM * WN;
   if (g_fwd_addend && (splits > 1 || stats)) throw std::runtime_error("conv_fwd_add: no split-K / statistics");
   if (g_fwd_addend)
@@ -1772,21 +1844,25 @@ static int g_fwd_stages = 3, g_wgrad_stages = 0;  // tuning knobs (set_conv_stag
 // (96 -> 64 KiB of LDS: two workgroups per CU, which is what the short-K
 // GEMMs need -- scripts/bench_gemm1x1.py SWEEP=1, ops/conv.py _plan_1x1),
 // while the CIFAR layers keep the tuned global default.
+// bits 12-19: the slab's capacity in K splits (0 = exactly `splits`); a larger
+// capacity lets a position-major layer use the balanced split-K plan
+// (g_fwd_slab_cap, declared with g_fwd_addend).
 struct FwdCfg {
   int saved_st, saved_wv;
   explicit FwdCfg(int& tile) : saved_st(g_fwd_stages), saved_wv(g_fwd_waves) {
     const int st = (tile >> 4) & 15, wv = (tile >> 8) & 15;
+    g_fwd_slab_cap = (tile >> 12) & 255;
     tile &= 15;
     if (st && (st < 2 || st > 4)) throw std::runtime_error("conv_fwd: packed stages must be 2..4");
     if (wv && wv != 4 && wv != 8) throw std::runtime_error("conv_fwd: packed waves must be 4 or 8");
     if (st) g_fwd_stages = st;
     if (wv) g_fwd_waves = wv;
   }
-  ~FwdCfg() { g_fwd_stages = saved_st; g_fwd_waves = saved_wv; }
+  ~FwdCfg() { g_fwd_stages = saved_st; g_fwd_waves = saved_wv; g_fwd_slab_cap = 0; }
 };
 
 template <int BM, int BN, bool TAPU, int ST>
-static void launch_fwd_t(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
+static void launch_fwd_t(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
                          uintptr_t slab, int splits, hipStream_t s) {
   if (g_fwd_waves == 8) {
     if constexpr (BN >= 128) launch_fwd_w<BM, BN, TAPU, ST, 2, 4>(g, x, w, y, stats, slab, splits, s);
@@ -1813,7 +1889,7 @@ void set_conv_stages(int fwd, int wgrad) {
 }
 
 template <int BM, int BN>
-static void launch_fwd(const ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
+static void launch_fwd(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
                        uintptr_t slab, int splits, hipStream_t s) {
   const int st = (BM * 64 * 2 + BN * 64 * 2) * 4 > 160 * 1024 ? std::min(g_fwd_stages, 3) : g_fwd_stages;
   if (g.Cin >= 64) {
@@ -2014,9 +2090,10 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
   const int nb = (g.M + rpb - 1) / rpb;
   if (stats)
     splitk_combine_kernel<true><<<nb, 256, 0, s>>>((const float*)slab, (bf16_t*)y, (float*)stats, splits, g.M, Cout,
-                                                   rpb);
+                                                   rpb, g);
   else
-    splitk_combine_kernel<false><<<nb, 256, 0, s>>>((const float*)slab, (bf16_t*)y, nullptr, splits, g.M, Cout, rpb);
+    splitk_combine_kernel<false><<<nb, 256, 0, s>>>((const float*)slab, (bf16_t*)y, nullptr, splits, g.M, Cout, rpb,
+                                                    g);
   DL_HIP_CHECK(hipGetLastError());
   return nb;
 }

@@ -620,11 +620,14 @@ POSM_SHAPES = [(128, 4, 256, 512, 0, 4), (128, 4, 512, 256, 0, 8), (128, 4, 256,
 
 
 @pytest.mark.parametrize("shape", POSM_SHAPES)
-def test_conv_fwd_position_major(C, shape):
+@pytest.mark.parametrize("cap", [0, 2])
+def test_conv_fwd_position_major(C, shape, cap):
     """Streaming conv with position-major M tiles and the zero-border taps
     skipped (g.posm) vs an fp32 reference and vs the pixel-major tiles
     (bitwise without split-K: skipping exact-zero products keeps every fp32
-    partial sum); BN statistics of exactly the stored values."""
+    partial sum); BN statistics of exactly the stored values.  cap = 2: the
+    slab holds 2 x splits slices (tile-id bits 12-19), so split-K layers use
+    the balanced plan (per-pixel split counts, combine reads each row's own)."""
     B, H, cin, cout, tile, splits = shape
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(B + H * cin + cout)
@@ -632,17 +635,20 @@ def test_conv_fwd_position_major(C, shape):
     w = (torch.randn(cout, 5, 5, cin, device=dev, generator=g) * 0.05).to(torch.bfloat16)
     xp = _pad(x)
     rows = C.conv_fwd_stat_rows(B, H, H, cin, cout, 5, tile, splits)
-    slab = torch.empty(splits * B * H * H * cout, device=dev)
+    ncap = cap * splits if splits > 1 else 0
+    slab = torch.full((max(ncap, splits) * B * H * H * cout,), float("nan"), device=dev)
     outs = []
     for posm in (0, 1):
         C.set_conv_posm(posm)
+        C.set_conv_posm_balance(1 if cap else 0)
         try:
             y = torch.full((B, H, H, cout), float("nan"), dtype=torch.bfloat16, device=dev)
             stats = torch.full((max(rows, 400), 2, cout), float("nan"), device=dev)
             T = C.conv_fwd(xp.data_ptr(), w.data_ptr(), y.data_ptr(), stats.data_ptr(), slab.data_ptr(), B, H, H,
-                           cin, cout, 5, tile, splits, _s())
+                           cin, cout, 5, tile | (ncap << 12), splits, _s())
         finally:
             C.set_conv_posm(1)
+            C.set_conv_posm_balance(0)
         torch.cuda.synchronize()
         outs.append((y, stats[:T].sum(0)))
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=2).permute(0, 2, 3, 1)

@@ -51,6 +51,18 @@ _FWD_TILES = {0: (128, 128), 1: (64, 64), 2: (128, 64)}
 _NOSPLIT_128x64 = os.environ.get("DISTLEARN_FWD_NOSPLIT", "1") == "1"
 
 
+# The fwd/dgrad split-K slab holds SLAB_CAP x splits slices, announced to
+# conv_fwd in tile-id bits 12-19: a position-major layer (output smaller than
+# the kernel) may then split its K steps per output pixel in proportion to
+# that pixel's valid taps (balanced plan, csrc conv_igemm.hip plan_posm_balance;
+# measured no faster, off: DISTLEARN_POSM_BALANCE=1 with DISTLEARN_SLAB_CAP=2).
+SLAB_CAP = int(os.environ.get("DISTLEARN_SLAB_CAP", "1"))
+
+
+def _slab_cap_bits(splits: int) -> int:
+    return (SLAB_CAP * splits) << 12 if splits > 1 else 0
+
+
 def _fwd_plan(M: int, N: int, K: int):
     """(tile, splits) for a forward/dgrad implicit GEMM: the biggest tile the
     channel count allows, then split-K until the grid covers the 256 CUs
@@ -153,6 +165,8 @@ class CifarHIPExecutor:
             self.C.set_conv_wgrad_xcd(int(os.environ["DISTLEARN_WGRAD_XCD"]))
         if "DISTLEARN_FWD_MMAJOR" in os.environ:  # A/B: fwd/dgrad tile order after the XCD swizzle
             self.C.set_conv_fwd_order(int(os.environ["DISTLEARN_FWD_MMAJOR"]))
+        if "DISTLEARN_POSM_BALANCE" in os.environ:  # A/B: balanced (1) or uniform (0) position-major split-K
+            self.C.set_conv_posm_balance(int(os.environ["DISTLEARN_POSM_BALANCE"]))
         if "DISTLEARN_POSM" in os.environ:  # A/B: position-major conv tiles for the 4x4 layer (1) or not (0)
             self.C.set_conv_posm(int(os.environ["DISTLEARN_POSM"]))
         if "DISTLEARN_FWD_TR" in os.environ:  # A/B: transposed-accumulator streaming kernel (1) or not (0)
@@ -248,8 +262,8 @@ class CifarHIPExecutor:
             K = KSIZE * KSIZE * cin
             tile, splits = _fwd_plan(M, cout, K)
             self.fwd_plan.append((tile, splits))
-            if splits > 1:
-                slab_elems = max(slab_elems, splits * M * cout)
+            if splits > 1:  # x SLAB_CAP: room for the balanced position-major split-K plan
+                slab_elems = max(slab_elems, SLAB_CAP * splits * M * cout)
             if self.atomic:
                 self.stats.append(arena[arena_off:arena_off + 2 * R * cout].view(R, 2, cout))
                 if self.mode == 2:
@@ -273,7 +287,7 @@ class CifarHIPExecutor:
                 dt, ds = _fwd_plan(M, cin, KSIZE * KSIZE * cout)
                 self.dgrad_plan[i] = (dt, ds)
                 if ds > 1:
-                    slab_elems = max(slab_elems, ds * M * cin)
+                    slab_elems = max(slab_elems, SLAB_CAP * ds * M * cin)
         self.slabs = torch.empty(max(slab_elems, 1), device=d)    # fwd / dgrad split-K (main stream)
         # what the step's prep kernel zeroes in the atomic modes: the statistics arena
         # (mode 2: + the backward rows); mode 1: every layer's [dgamma; dbeta] and the
@@ -357,7 +371,7 @@ class CifarHIPExecutor:
             t, sp = self.fwd_plan[i]
             ntm = C.conv_fwd(inp.data_ptr(), w.data_ptr(), self.y[i].data_ptr(),
                              self.stats[i].data_ptr() if train else 0, self.slabs.data_ptr(), B, h, h, cin, cout, KSIZE,
-                             t | self.fwd_cfg, sp, s)
+                             t | self.fwd_cfg | _slab_cap_bits(sp), sp, s)
             fused = train and self.atomic  # coefficients derived by the consumer kernel
             if not fused:
                 C.bn_finalize(self.stats[i].data_ptr(), ntm, cout, M, self.p32[self._leaf(i, 2)].data_ptr(),
@@ -517,7 +531,7 @@ class CifarHIPExecutor:
                 if self.dgrad_stages != 3:
                     C.set_conv_stages(self.dgrad_stages, self._wgrad_stages)
                 C.conv_fwd(dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), 0,
-                           self.slabs.data_ptr(), B, h, h, cout, cin, KSIZE, dt, ds, s)
+                           self.slabs.data_ptr(), B, h, h, cout, cin, KSIZE, dt | _slab_cap_bits(ds), ds, s)
                 if self.dgrad_stages != 3:
                     C.set_conv_stages(3, self._wgrad_stages)
         if self.side_wgrad or self.side_reduce:
