@@ -404,25 +404,42 @@ __global__ void __launch_bounds__(kThreads) zero_border_kernel(bf16_t* __restric
 // rows [T][2][C] (sum, sum of squares) into acc [2C] (one block per channel,
 // fixed order): the BatchNorm statistics of a 1x1 conv output for T*2C reads
 // instead of a pass over the M*C activation (ops/conv.py).
+// acc[c] += sum_t rows[t][0][c], acc[C + c] += sum_t rows[t][1][c] (acc zeroed by
+// the caller: the per-step BatchNorm arena).  Grid (C/64 channel groups, S row
+// chunks), block = 64 consecutive channels x 4 row lanes: every row read is a
+// coalesced 256-B segment (one block per channel read one float per 64-B line,
+// 16x the bytes), 4 rows of loads in flight per thread, one atomic per channel
+// per block.
 __global__ void __launch_bounds__(kThreads) bn_rows_reduce_kernel(const float* __restrict__ rows, int T, int C,
-                                                                  float* __restrict__ acc) {
-  const int c = blockIdx.x;
+                                                                  float* __restrict__ acc, int rows_per_chunk) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), ly = threadIdx.x >> 6;
+  const int t0 = blockIdx.y * rows_per_chunk, t1 = min(T, t0 + rows_per_chunk);
   float s1 = 0.f, s2 = 0.f;
-  for (int t = threadIdx.x; t < T; t += kThreads) {
-    s1 += rows[(int64_t)t * 2 * C + c];
-    s2 += rows[(int64_t)t * 2 * C + C + c];
+  if (c < C) {
+    int t = t0 + ly;
+    for (; t + 12 < t1; t += 16) {
+      float a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] = rows[(int64_t)(t + 4 * u) * 2 * C + c];
+        b[u] = rows[(int64_t)(t + 4 * u) * 2 * C + C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { s1 += a[u]; s2 += b[u]; }
+    }
+    for (; t < t1; t += 4) {
+      s1 += rows[(int64_t)t * 2 * C + c];
+      s2 += rows[(int64_t)t * 2 * C + C + c];
+    }
   }
-  __shared__ float red[2][kThreads / 64];
-  s1 = wave_sum(s1);
-  s2 = wave_sum(s2);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (lane == 0) { red[0][wid] = s1; red[1][wid] = s2; }
+  __shared__ float red[2][4][64];
+  red[0][ly][threadIdx.x & 63] = s1;
+  red[1][ly][threadIdx.x & 63] = s2;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    float a = 0.f, b = 0.f;
-    for (int w = 0; w < kThreads / 64; ++w) { a += red[0][w]; b += red[1][w]; }
-    acc[c] = a;
-    acc[C + c] = b;
+  if (ly == 0 && c < C) {
+    const int i = threadIdx.x & 63;
+    atomicAdd(acc + c, red[0][0][i] + red[0][1][i] + red[0][2][i] + red[0][3][i]);
+    atomicAdd(acc + C + c, red[1][0][i] + red[1][1][i] + red[1][2][i] + red[1][3][i]);
   }
 }
 
@@ -430,7 +447,11 @@ void set_bn_reduce_blocks(int n) { g_reduce_blocks = n < 64 ? 64 : n; }
 
 void bn_rows_reduce(uintptr_t rows, int T, int C, uintptr_t acc, uintptr_t stream) {
   if (T <= 0 || C <= 0) throw std::runtime_error("bn_rows_reduce: empty");
-  bn_rows_reduce_kernel<<<C, kThreads, 0, as_stream(stream)>>>((const float*)rows, T, C, (float*)acc);
+  const int cg = (C + 63) / 64;
+  const int chunks = std::max(1, std::min((T + 63) / 64, (256 + cg - 1) / cg));  // ~256 blocks, >= 64 rows each
+  const int rpc = (T + chunks - 1) / chunks;
+  bn_rows_reduce_kernel<<<dim3(cg, (T + rpc - 1) / rpc), kThreads, 0, as_stream(stream)>>>((const float*)rows, T, C,
+                                                                                       (float*)acc, rpc);
   DL_HIP_CHECK(hipGetLastError());
 }
 
