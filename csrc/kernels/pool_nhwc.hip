@@ -101,6 +101,97 @@ __global__ void __launch_bounds__(256) maxpool_nhwc_bwd_kernel(const bf16_t* __r
   }
 }
 
+// The ResNet-50 stem window (3x3, stride 2, pad 1) with 32-bit indexing and
+// every load of an item issued before its first use: the generic kernels above
+// run a dependent load chain per window position with 64-bit divisions and
+// measured 154 us (forward) / 256 us (backward) per batch-256 step, about
+// 3.7 / 2.2 TB/s.  Out-of-image taps load a valid pixel and are masked.
+__global__ void __launch_bounds__(256) maxpool3s2_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                             uint8_t* __restrict__ idx, const PoolGeom g) {
+  const int C8 = g.C >> 3;
+  const int total = g.N * g.Ho * g.Wo * C8;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c8 = i % C8, pix = i / C8;
+    const int ow = pix % g.Wo, t = pix / g.Wo;
+    const int oh = t % g.Ho, n = t / g.Ho;
+    const int h0 = 2 * oh - 1, w0 = 2 * ow - 1;
+    uint4 v[9];
+    bool ok[9];
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int h = h0 + u, w = w0 + q;
+        ok[u * 3 + q] = h >= 0 && h < g.H && w >= 0 && w < g.W;
+        const int hh = ok[u * 3 + q] ? h : oh * 2, ww = ok[u * 3 + q] ? w : ow * 2;  // (2 oh, 2 ow) is inside
+        v[u * 3 + q] = *reinterpret_cast<const uint4*>(x + ((int64_t)(n * g.H + hh) * g.W + ww) * g.C + c8 * 8);
+      }
+    float best[8];
+    uint8_t arg[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; arg[k] = 0; }
+#pragma unroll
+    for (int p = 0; p < 9; ++p) {
+      if (!ok[p]) continue;
+      float f[8];
+      unpack8p(v[p], f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (f[k] > best[k]) { best[k] = f[k]; arg[k] = (uint8_t)p; }
+    }
+    const int64_t o = (int64_t)pix * g.C + c8 * 8;
+    *reinterpret_cast<uint4*>(y + o) = pack8p(best);
+    uint2 a;
+    a.x = (uint32_t)arg[0] | ((uint32_t)arg[1] << 8) | ((uint32_t)arg[2] << 16) | ((uint32_t)arg[3] << 24);
+    a.y = (uint32_t)arg[4] | ((uint32_t)arg[5] << 8) | ((uint32_t)arg[6] << 16) | ((uint32_t)arg[7] << 24);
+    *reinterpret_cast<uint2*>(idx + o) = a;
+  }
+}
+
+// input row h is covered by the windows oh = h/2 (and (h+1)/2 when h is odd)
+__global__ void __launch_bounds__(256) maxpool3s2_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                             const uint8_t* __restrict__ idx, bf16_t* __restrict__ dx,
+                                                             const PoolGeom g) {
+  const int C8 = g.C >> 3;
+  const int total = g.N * g.H * g.W * C8;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c8 = i % C8, pix = i / C8;
+    const int w = pix % g.W, t = pix / g.W;
+    const int h = t % g.H, n = t / g.H;
+    const int ohs[2] = {h >> 1, min(g.Ho - 1, (h + 1) >> 1)};
+    const int ows[2] = {w >> 1, min(g.Wo - 1, (w + 1) >> 1)};
+    uint4 d[4];
+    uint2 a[4];
+    bool ok[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int oh = ohs[j >> 1], ow = ows[j & 1];
+      ok[j] = (j < 2 || ohs[1] != ohs[0]) && ((j & 1) == 0 || ows[1] != ows[0]);
+      const int64_t o = ((int64_t)(n * g.Ho + oh) * g.Wo + ow) * g.C + c8 * 8;
+      d[j] = *reinterpret_cast<const uint4*>(dy + o);
+      a[j] = *reinterpret_cast<const uint2*>(idx + o);
+    }
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!ok[j]) continue;
+      const int oh = ohs[j >> 1], ow = ows[j & 1];
+      const uint32_t pos = (uint32_t)((h - (2 * oh - 1)) * 3 + (w - (2 * ow - 1)));
+      float f[8];
+      unpack8p(d[j], f);
+      const uint32_t aw[2] = {a[j].x, a[j].y};
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (((aw[k >> 2] >> (8 * (k & 3))) & 0xffu) == pos) acc[k] += f[k];
+    }
+    *reinterpret_cast<uint4*>(dx + (int64_t)pix * g.C + c8 * 8) = pack8p(acc);
+  }
+}
+
+static bool stem_window(const PoolGeom& g, int64_t in_items) {
+  return g.K == 3 && g.S == 2 && g.P == 1 && in_items < (1ll << 31);
+}
+
 PoolGeom pool_geom(int N, int H, int W, int C, int K, int S, int P) {
   if (C % 8 != 0) throw std::runtime_error("maxpool_nhwc: C % 8 != 0");
   if (K * K > 255 || K <= 0 || S <= 0 || P < 0 || 2 * P > K) throw std::runtime_error("maxpool_nhwc: bad window");
@@ -114,8 +205,12 @@ void maxpool_nhwc_fwd(uintptr_t x, uintptr_t y, uintptr_t idx, int N, int H, int
                       uintptr_t stream) {
   const PoolGeom g = pool_geom(N, H, W, C, K, S, P);
   const int64_t total = (int64_t)N * g.Ho * g.Wo * (C / 8);
-  maxpool_nhwc_fwd_kernel<<<stream_grid(total), 256, 0, as_stream(stream)>>>((const bf16_t*)x, (bf16_t*)y,
-                                                                              (uint8_t*)idx, g);
+  if (stem_window(g, (int64_t)N * H * W * (C / 8)))
+    maxpool3s2_fwd_kernel<<<(int)std::min<int64_t>((total + 255) / 256, 8192), 256, 0, as_stream(stream)>>>(
+        (const bf16_t*)x, (bf16_t*)y, (uint8_t*)idx, g);
+  else
+    maxpool_nhwc_fwd_kernel<<<stream_grid(total), 256, 0, as_stream(stream)>>>((const bf16_t*)x, (bf16_t*)y,
+                                                                                (uint8_t*)idx, g);
   DL_HIP_CHECK(hipGetLastError());
 }
 
@@ -123,8 +218,12 @@ void maxpool_nhwc_bwd(uintptr_t dy, uintptr_t idx, uintptr_t dx, int N, int H, i
                       uintptr_t stream) {
   const PoolGeom g = pool_geom(N, H, W, C, K, S, P);
   const int64_t total = (int64_t)N * H * W * (C / 8);
-  maxpool_nhwc_bwd_kernel<<<stream_grid(total), 256, 0, as_stream(stream)>>>((const bf16_t*)dy, (const uint8_t*)idx,
-                                                                              (bf16_t*)dx, g);
+  if (stem_window(g, total))
+    maxpool3s2_bwd_kernel<<<(int)std::min<int64_t>((total + 255) / 256, 8192), 256, 0, as_stream(stream)>>>(
+        (const bf16_t*)dy, (const uint8_t*)idx, (bf16_t*)dx, g);
+  else
+    maxpool_nhwc_bwd_kernel<<<stream_grid(total), 256, 0, as_stream(stream)>>>((const bf16_t*)dy, (const uint8_t*)idx,
+                                                                                (bf16_t*)dx, g);
   DL_HIP_CHECK(hipGetLastError());
 }
 
