@@ -87,10 +87,12 @@ _FUSE_STATS = os.environ.get("DISTLEARN_RESNET_FUSE_STATS", "1") == "1"
 # the addend 16 bytes at a time and the fusion now wins: 30.33 -> 29.68 ms/step.
 _FUSE_RES = os.environ.get("DISTLEARN_RESNET_FUSE_RES", "1") == "1"
 # stride-1 3x3 convolutions on the hand-written implicit-GEMM kernels (ops/conv.py
-# Conv3x3) for feature maps of at most this size (0 = off: MIOpen for all 3x3);
-# the 56x56 stage stays on MIOpen (its wgrad measured slower on our kernel:
-# profiles/r2_conv3x3_miopen_vs_hip.jsonl.txt)
-_CONV3_MAX_HW = int(os.environ.get("DISTLEARN_RESNET_CONV3_MAX_HW", "28"))
+# Conv3x3) for feature maps of at most this size (0 = off: MIOpen for all 3x3).
+# The 56x56 stage joined once the wgrad ran on the XCD-aware grid with one round
+# of 512 64x64 workgroups (161 vs MIOpen's 167 us; forward 88 vs 117 us:
+# profiles/r2_conv3x3_sweep_v2.jsonl); end to end 25.93 vs 25.94 ms/step with
+# the stage on MIOpen (profiles/r2_resnet_conv3_56_ab.txt).
+_CONV3_MAX_HW = int(os.environ.get("DISTLEARN_RESNET_CONV3_MAX_HW", "56"))
 # channels-last copies of the KxK shadows for MIOpen, one launch per step (ops/conv.py)
 _CL_WEIGHTS = os.environ.get("DISTLEARN_RESNET_CL_WEIGHTS", "1") == "1"
 # stem max-pool on the HIP gather-backward kernels (ops/pool.py)

@@ -269,11 +269,15 @@ def _plan_3x3(M: int, N: int, K: int):
 
 def _wgrad_plan_3x3(cout: int, K: int, M: int):
     """Weight-gradient plan (tile, splits) of a 3x3 conv: about one round of
-    workgroups, two when the tiles alone nearly fill the chip (same sweep)."""
+    workgroups, two when the tiles alone nearly fill the chip (same sweep).
+    64x64 tiles (Cout = 64, the 56x56 stage) run two workgroups per CU, so one
+    round is 512 of them: 56 splits, 161 us vs 28 splits' ~177 and MIOpen's
+    167 (profiles/r2_conv3x3_sweep_v2.jsonl)."""
     tile = 2 if cout % 128 == 0 else 1
     bm, bn = (128, 128) if tile == 2 else (64, 64)
     tiles = (cout // bm) * ((K + bn - 1) // bn)
-    splits = max(1, (256 if tiles <= 64 else 512) // tiles)
+    slots = 512 if (tile == 1 or tiles > 64) else 256
+    splits = max(1, slots // tiles)
     return tile, max(1, min(splits, M // 512))
 
 
