@@ -3,8 +3,16 @@
 convnet trained with AllReduceSGD (BASELINE.json "metric"), bf16 compute,
 synthetic CIFAR-shaped data, random-init weights.
 
-    python bench.py --gpus N --steps K --warmup W           (N == 1)
+    python bench.py --gpus N --steps K --warmup W
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+With ``--gpus N > 1`` and no torch.distributed environment (WORLD_SIZE
+unset), bench.py launches itself: the parent spawns N child processes (one
+rank per GPU: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / a free
+MASTER_PORT), never touches the GPU and never execs, forwards rank 0's JSON
+line as its own last stdout line, and exits non-zero (killing the siblings) as
+soon as any child fails or the launch times out -- the reference's launchers
+fork their own N processes the same way (examples/cifar10-cuda.sh:4-7).
 
 One rank per GPU; gradients are all-reduced over RCCL (xGMI) in buckets that
 overlap backward; the timed region is EXACTLY K full training steps (forward,
@@ -39,8 +47,8 @@ def parse():
                     help="sgd = AllReduceSGD (headline), ea = AllReduceEA (tau, alpha), "
                          "async = AsyncEA: rank 0 parameter server + N-1 clients (BASELINE configs 2-4)")
     ap.add_argument("--model", default="cifar10", choices=["cifar10", "resnet50"],
-                    help="resnet50 = BASELINE config 5 (ImageNet shape 224x224; 1x1 convs on the HIP MFMA kernels, "
-                         "3x3/strided convs on MIOpen, HIP BatchNorm)")
+                    help="resnet50 = BASELINE config 5 (ImageNet shape 224x224; stride-1 1x1 and 3x3 convs on the "
+                         "HIP MFMA kernels, HIP BatchNorm; see models/resnet.py for the rest)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = gloo plumbing check of the same code path (tests only; not a benchmark)")
     ap.add_argument("--tau", type=int, default=10)
@@ -57,7 +65,92 @@ def parse():
     ap.add_argument("--lr", type=float, default=None,
                     help="SGD learning rate (default: cifar10 0.1 = examples/cifar10.lua:7; resnet50 0.02)")
     ap.add_argument("--overlap", type=int, default=1, help="bucketed all-reduce overlapped with backward")
+    ap.add_argument("--grad-comm-dtype", default=os.environ.get("DISTLEARN_GRAD_COMM_DTYPE", "fp32"),
+                    choices=["fp32", "bf16"],
+                    help="gradient all-reduce wire dtype (bf16: half the xGMI bytes, count in an fp32 side slot)")
+    ap.add_argument("--launch-timeout", type=float, default=1800.0,
+                    help="self-launch (--gpus N > 1 without torch.distributed.run): seconds before the children "
+                         "are killed and bench.py exits non-zero")
     return ap.parse_args()
+
+
+def _self_launch(a) -> int:
+    """Spawn ``a.gpus`` ranks of this script as child processes (no exec, no
+    GPU use in this parent), forward rank 0's JSON line, fail fast."""
+    import signal
+    import socket
+    import subprocess
+    import threading
+
+    n = a.gpus
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs, lines, readers = [], [], []
+    sys.stdout.flush()
+
+    def pump(r, stream):
+        for raw in iter(stream.readline, ""):
+            if r == 0 and raw.startswith("{") and '"metric"' in raw:
+                lines.append(raw.rstrip("\n"))
+            else:  # everything else (RCCL banners, other ranks) goes to stderr
+                sys.stderr.write(raw if r == 0 else f"[rank {r}] {raw}")
+        stream.close()
+
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DISTLEARN_SELF_LAUNCHED="1")
+        p = subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                             stdout=subprocess.PIPE, text=True, start_new_session=True)
+        procs.append(p)
+        t = threading.Thread(target=pump, args=(r, p.stdout), daemon=True)
+        t.start()
+        readers.append(t)
+
+    def kill_all():
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except OSError:
+                    pass
+        for p in procs:
+            p.wait()
+
+    def on_term(signum, frame):
+        kill_all()
+        sys.exit(128 + signum)
+
+    signal.signal(signal.SIGTERM, on_term)
+    deadline = time.time() + a.launch_timeout
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                r, rc = bad[0]
+                print(f"bench.py: rank {r} exited with code {rc}; stopping the other ranks", file=sys.stderr)
+                break
+            if all(c == 0 for c in codes):
+                break
+            if time.time() > deadline:
+                print(f"bench.py: ranks still running after --launch-timeout {a.launch_timeout:.0f} s; killing them",
+                      file=sys.stderr)
+                rc = 124
+                break
+            time.sleep(0.05)
+    finally:
+        kill_all()
+        for t in readers:
+            t.join(timeout=5)
+    if rc == 0:
+        if not lines:
+            print("bench.py: rank 0 printed no result line", file=sys.stderr)
+            return 1
+        print(lines[-1], flush=True)
+    return rc
 
 
 METRICS = {
@@ -76,14 +169,16 @@ MODEL_DESC = {
 
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_self_launch(a))  # before torch is imported: the parent never touches the GPU
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus and world == 1 and a.gpus > 1:
-        print(f"bench.py: --gpus {a.gpus} needs torch.distributed.run with {a.gpus} processes", file=sys.stderr)
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
     if a.algo == "async" and world < 2:
         print("bench.py: --algo async needs >= 2 ranks (1 server + clients)", file=sys.stderr)
@@ -93,10 +188,14 @@ def main():
         dev = torch.device("cpu")
         sync = lambda: None  # noqa: E731
     else:
-        ndev = torch.cuda.device_count()
+        ndev = torch.cuda.device_count()  # does not initialise the GPU
+        if ndev < world and os.environ.get("DISTLEARN_ALLOW_SHARED_GPU", "0") != "1":
+            # one rank per GPU (RCCL refuses two ranks on one GPU): fail fast
+            print(f"bench.py: --gpus {world} needs {world} GPUs, this node has {ndev}", file=sys.stderr)
+            sys.exit(2)
         if local >= ndev:
-            # more ranks than GPUs (a functional rehearsal of the multi-rank
-            # path on a small box; not a benchmark configuration)
+            # DISTLEARN_ALLOW_SHARED_GPU=1: more ranks than GPUs (a functional
+            # rehearsal of the multi-rank path on a small box; not a benchmark)
             print(f"bench.py: rank {rank}: LOCAL_RANK {local} >= {ndev} GPUs, sharing GPU {local % ndev}",
                   file=sys.stderr)
             local = local % ndev
@@ -112,8 +211,8 @@ def main():
         a.bucket_mb = 1.0 if a.model == "cifar10" else 16.0
     backend = a.backend if (a.model == "cifar10" and not cpu) else "torch"
     if backend == "torch" and not cpu and os.environ.get("DISTLEARN_MIOPEN_FIND", "1") == "1":
-        # MIOpen solver search per conv shape (the remaining 3x3 / strided / stem convs of
-        # ResNet-50); runs in the graph-capture warm-up steps, before the timed region.
+        # MIOpen solver search per conv shape (the convs of ResNet-50 not on the HIP
+        # kernels: strided / stem); runs in the graph-capture warm-up steps, before the timed region.
         # Measured 32.69 vs 33.93 ms/step at batch 256 (profiles/r2_bench_resnet50.txt)
         torch.backends.cudnn.benchmark = True
     cdt = torch.float32 if cpu else torch.bfloat16
@@ -221,6 +320,21 @@ def main():
                      dtype=torch.float64)
     tree.comm.all_reduce_host(t, "max")
     dt, lval = float(t[0]), float(t[1])
+    # which device each rank ran on (a SCALE record must show N distinct GPUs)
+    devs = torch.full((world,), -1, dtype=torch.int64)
+    devs[rank] = -1 if cpu else torch.cuda.current_device()
+    tree.comm.all_reduce_host(devs, "max")
+    ex = getattr(tr, "executor", None) if not is_server else None
+    policy = {
+        "rccl_world": getattr(tree.comm, "world_size", world) if type(tree.comm).__name__ == "RcclCommunicator"
+        else 0,
+        "comm": type(tree.comm).__name__,
+        "device_ids": sorted(set(int(d) for d in devs.tolist())),
+        "nccl_max_nchannels": os.environ.get("NCCL_MAX_NCHANNELS"),
+        "cu_reserve": getattr(ex, "cu_reserve", None),
+        "dgrad_stages": getattr(ex, "dgrad_stages", None),
+        "grad_comm_dtype": a.grad_comm_dtype if a.algo == "sgd" else "fp32",
+    }
     ms = dt / a.steps * 1e3
     imgs = batch * len(workers) * a.steps / dt
     if rank == 0:
@@ -242,7 +356,7 @@ def main():
             "config": {"model": MODEL_DESC[a.model],
                        "global_batch": batch * len(workers), "per_gpu_batch": batch, "seq_len": None,
                        "parallelism": f"dp{len(workers)}" + ("+ps1" if a.algo == "async" else ""), "algo": a.algo,
-                       "backend": backend, "hipgraph": bool(a.graph), "bucket_mb": a.bucket_mb,
+                       "backend": backend, "hipgraph": bool(a.graph), "bucket_mb": a.bucket_mb, **policy,
                        **({"tau": a.tau, "alpha": a.alpha} if a.algo != "sgd" else {})},
             "final_loss": round(lval, 4),
         }

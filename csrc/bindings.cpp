@@ -39,7 +39,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_conv_region_stages", &set_conv_region_stages);
   m.def("set_conv_wgrad_pf", &set_conv_wgrad_pf);
   m.def("set_bn_bwd_items", &set_bn_bwd_items);
-  m.def("occupy_cus", &occupy_cus);
   m.def("set_conv_region_ablate", &set_conv_region_ablate);
   m.def("set_conv_region_waves", &set_conv_region_waves);
   m.def("set_conv_stages", &set_conv_stages);

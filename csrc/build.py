@@ -28,13 +28,18 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 
 
-def ext_path() -> str:
-    return os.path.join(PKG, "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+TESTING = os.path.join(CSRC, "testing")  # test/diagnostic kernels -> separate _C_testing extension
 
 
-def _sources():
+def ext_path(name: str = "_C") -> str:
+    return os.path.join(PKG, name + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _sources(testing: bool = False):
     srcs = []
     for d, _, files in os.walk(CSRC):
+        if (os.path.commonpath([d, TESTING]) == TESTING) != testing:
+            continue
         for f in sorted(files):
             if f.endswith((".hip", ".cpp")):
                 srcs.append(os.path.join(d, f))
@@ -75,7 +80,7 @@ def _compile(src: str, force: bool, verbose: bool, newest_header: float):
         return obj, 0.0, False
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-c", src, "-o", obj] + COMMON + _includes()
     cmd += os.environ.get("DISTLEARN_CFLAGS", "").split()  # A/B experiments (e.g. -DDL_FWD_SWAP=0)
-    if src.endswith(".cpp") and "bindings" in src:
+    if "bindings" in src or "testing" in src:
         cmd += ["-fvisibility=hidden"]
     t0 = time.time()
     if verbose:
@@ -87,8 +92,14 @@ def _compile(src: str, force: bool, verbose: bool, newest_header: float):
 
 
 def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> str:
+    """Build the product extension ``_C`` and the test-support ``_C_testing``."""
+    out = _build_ext("_C", _sources(False), force, jobs, verbose, ["-lrccl"])
+    _build_ext("_C_testing", _sources(True), force, jobs, verbose, [])
+    return out
+
+
+def _build_ext(name, srcs, force, jobs, verbose, libs) -> str:
     os.makedirs(BUILD, exist_ok=True)
-    srcs = _sources()
     hdr = max([os.path.getmtime(h) for h in _headers()] + [0.0])
     jobs = jobs or min(8, os.cpu_count() or 4)
     objs = []
@@ -101,10 +112,10 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
             rebuilt |= did
             if did:
                 print(f"[distlearn build] {os.path.relpath(futs[f], ROOT)}  {dt:.1f}s", flush=True)
-    out = ext_path()
+    out = ext_path(name)
     if rebuilt or force or not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + sorted(objs) + [
-            "-L" + os.path.join(ROCM, "lib"), "-lrccl"]
+            "-L" + os.path.join(ROCM, "lib")] + libs
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -107,6 +107,7 @@ class RcclCommunicator {
 
   void destroy() {
     stop_watchdog();
+    std::lock_guard<std::mutex> c(call_mu_);
     std::lock_guard<std::mutex> g(mu_);
     if (comm_) {
       ncclCommDestroy(comm_);
@@ -129,76 +130,77 @@ class RcclCommunicator {
   int world() const { return world_; }
   int device() const { return dev_; }
 
+  // Every RCCL host call holds call_mu_ (RCCL calls on one communicator are not
+  // thread-safe) but NOT mu_: mu_ guards only the watchdog's state (pending
+  // events, abort reason), so the watchdog can always take it and abort a
+  // communicator whose host call is blocked on a stuck peer.
   void all_reduce(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int op, uintptr_t stream) {
-    std::lock_guard<std::mutex> g(mu_);
-    live();
-    DL_NCCL_CHECK(ncclAllReduce((const void*)send, (void*)recv, (size_t)count, to_nccl(dtype), to_nccl_op(op), comm_,
-                                as_stream(stream)));
-    track_locked(stream);
+    std::lock_guard<std::mutex> c(call_mu_);
+    DL_NCCL_CHECK(ncclAllReduce((const void*)send, (void*)recv, (size_t)count, to_nccl(dtype), to_nccl_op(op),
+                                live(), as_stream(stream)));
+    enqueued(stream);
   }
   void broadcast(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int root, uintptr_t stream) {
-    std::lock_guard<std::mutex> g(mu_);
-    live();
+    std::lock_guard<std::mutex> c(call_mu_);
     DL_NCCL_CHECK(
-        ncclBroadcast((const void*)send, (void*)recv, (size_t)count, to_nccl(dtype), root, comm_, as_stream(stream)));
-    track_locked(stream);
+        ncclBroadcast((const void*)send, (void*)recv, (size_t)count, to_nccl(dtype), root, live(), as_stream(stream)));
+    enqueued(stream);
   }
   void reduce(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int op, int root, uintptr_t stream) {
-    std::lock_guard<std::mutex> g(mu_);
-    live();
+    std::lock_guard<std::mutex> c(call_mu_);
     DL_NCCL_CHECK(ncclReduce((const void*)send, (void*)recv, (size_t)count, to_nccl(dtype), to_nccl_op(op), root,
-                             comm_, as_stream(stream)));
-    track_locked(stream);
+                             live(), as_stream(stream)));
+    enqueued(stream);
   }
   // recvcount elements per rank
   void reduce_scatter(uintptr_t send, uintptr_t recv, int64_t recvcount, int dtype, int op, uintptr_t stream) {
-    std::lock_guard<std::mutex> g(mu_);
-    live();
+    std::lock_guard<std::mutex> c(call_mu_);
     DL_NCCL_CHECK(ncclReduceScatter((const void*)send, (void*)recv, (size_t)recvcount, to_nccl(dtype),
-                                    to_nccl_op(op), comm_, as_stream(stream)));
-    track_locked(stream);
+                                    to_nccl_op(op), live(), as_stream(stream)));
+    enqueued(stream);
   }
   void all_gather(uintptr_t send, uintptr_t recv, int64_t sendcount, int dtype, uintptr_t stream) {
-    std::lock_guard<std::mutex> g(mu_);
-    live();
+    std::lock_guard<std::mutex> c(call_mu_);
     DL_NCCL_CHECK(
-        ncclAllGather((const void*)send, (void*)recv, (size_t)sendcount, to_nccl(dtype), comm_, as_stream(stream)));
-    track_locked(stream);
+        ncclAllGather((const void*)send, (void*)recv, (size_t)sendcount, to_nccl(dtype), live(), as_stream(stream)));
+    enqueued(stream);
   }
   void send(uintptr_t buf, int64_t count, int dtype, int peer, uintptr_t stream) {
-    std::lock_guard<std::mutex> g(mu_);
-    live();
-    DL_NCCL_CHECK(ncclSend((const void*)buf, (size_t)count, to_nccl(dtype), peer, comm_, as_stream(stream)));
-    if (group_depth_ == 0) track_locked(stream);
-    else grouped_streams_.push_back(stream);
+    std::lock_guard<std::mutex> c(call_mu_);
+    DL_NCCL_CHECK(ncclSend((const void*)buf, (size_t)count, to_nccl(dtype), peer, live(), as_stream(stream)));
+    enqueued(stream);
   }
   void recv(uintptr_t buf, int64_t count, int dtype, int peer, uintptr_t stream) {
-    std::lock_guard<std::mutex> g(mu_);
-    live();
-    DL_NCCL_CHECK(ncclRecv((void*)buf, (size_t)count, to_nccl(dtype), peer, comm_, as_stream(stream)));
-    if (group_depth_ == 0) track_locked(stream);
-    else grouped_streams_.push_back(stream);
+    std::lock_guard<std::mutex> c(call_mu_);
+    DL_NCCL_CHECK(ncclRecv((void*)buf, (size_t)count, to_nccl(dtype), peer, live(), as_stream(stream)));
+    enqueued(stream);
   }
   void group_start() {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<std::mutex> c(call_mu_);
     live();
     DL_NCCL_CHECK(ncclGroupStart());
     ++group_depth_;
   }
   void group_end() {
-    std::lock_guard<std::mutex> g(mu_);
-    DL_NCCL_CHECK(ncclGroupEnd());
+    std::lock_guard<std::mutex> c(call_mu_);
+    if (group_depth_ <= 0) throw std::runtime_error("group_end without group_start");
+    ncclResult_t r = ncclGroupEnd();
     if (--group_depth_ == 0) {
-      // grouped p2p is only launched at the outermost group end: time it from here
-      for (uintptr_t s : grouped_streams_) track_locked(s);
-      grouped_streams_.clear();
+      // RCCL launches grouped work (collectives AND p2p) only at the outermost
+      // group end: an event recorded earlier would sit in front of the kernels
+      // and complete at once, so every grouped op is timed from here
+      std::vector<uintptr_t> streams;
+      streams.swap(grouped_streams_);
+      std::lock_guard<std::mutex> g(mu_);
+      for (uintptr_t s : streams) track_locked(s);
     }
+    DL_NCCL_CHECK(r);
   }
 
   // Time the work enqueued so far on `stream` (no-op while it is being captured).
   void track(uintptr_t stream) {
     std::lock_guard<std::mutex> g(mu_);
-    live();
+    live_locked();
     track_locked(stream);
   }
   void set_timeout(double s) { timeout_s_.store(s); }
@@ -231,9 +233,24 @@ class RcclCommunicator {
     std::chrono::steady_clock::time_point t;
   };
 
-  void live() const {
+  void live_locked() const {
     if (!reason_.empty()) throw std::runtime_error("RCCL communicator failed: " + reason_);
     if (!comm_) throw std::runtime_error("RCCL communicator used after destroy");
+  }
+  // the communicator handle if healthy (checked under mu_, used outside it)
+  ncclComm_t live() {
+    std::lock_guard<std::mutex> g(mu_);
+    live_locked();
+    return comm_;
+  }
+  // after an enqueue (caller holds call_mu_): time it now, or at the outermost group end
+  void enqueued(uintptr_t stream) {
+    if (group_depth_ > 0) {
+      grouped_streams_.push_back(stream);
+      return;
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    track_locked(stream);
   }
 
   void track_locked(uintptr_t stream) {
@@ -321,9 +338,10 @@ class RcclCommunicator {
   int rank_, world_, dev_;
   std::atomic<double> timeout_s_;
   int poll_ms_ = 50;
-  int group_depth_ = 0;
-  std::vector<uintptr_t> grouped_streams_;
-  std::mutex mu_;
+  int group_depth_ = 0;                    // guarded by call_mu_
+  std::vector<uintptr_t> grouped_streams_;  // guarded by call_mu_
+  std::mutex call_mu_;                      // serialises RCCL host calls
+  std::mutex mu_;                           // watchdog state: comm_, reason_, pending_, free_
   std::condition_variable cv_;
   bool stop_ = false;
   std::string reason_;

@@ -50,7 +50,6 @@ void set_conv_region(int on);
 void set_conv_region_stages(int st);
 void set_conv_wgrad_pf(int pf);
 void set_bn_bwd_items(int n);
-void occupy_cus(int blocks, int us, uintptr_t sink, uintptr_t stream);
 void set_conv_region_ablate(int a);
 void set_conv_region_waves(int w);
 void set_conv_stages(int fwd, int wgrad);

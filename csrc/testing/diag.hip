@@ -1,4 +1,7 @@
-// Diagnostics: emulate the CU footprint of a concurrently running RCCL
+// Test/diagnostic support (NOT part of the product library): built into the
+// separate extension torch_distlearn_amd._C_testing by csrc/build.py.
+//
+// Emulate the CU footprint of a concurrently running RCCL
 // collective on one GPU.
 //
 // RCCL's gfx950 all-reduce workgroup (rcclGenericKernel in librccl's code
@@ -9,8 +12,9 @@
 // so the effect of R occupied CUs on the training step can be measured on a
 // one-GPU box (scripts/emulate_rccl.py).  Each workgroup spins on the 100 MHz
 // constant clock for `us` microseconds and exits: every wave reaches the end.
+#include <pybind11/pybind11.h>
+
 #include "dl_common.h"
-#include "dl_ops.h"
 
 namespace dl {
 
@@ -47,3 +51,8 @@ void occupy_cus(int blocks, int us, uintptr_t sink, uintptr_t stream) {
 }
 
 }  // namespace dl
+
+PYBIND11_MODULE(_C_testing, m) {
+  m.doc() = "distlearn test/diagnostic kernels (not part of the product library)";
+  m.def("occupy_cus", &dl::occupy_cus);
+}

@@ -1,6 +1,12 @@
 """Micro-benchmark of the implicit-GEMM conv kernels on the reference model's
 layer shapes (per-GPU batch B): forward, dgrad, wgrad; prints us and TFLOP/s.
     python scripts/bench_conv.py [--batch 128] [--iters 50] [--only fwd2]"""
+
+def _native_testing():
+    from torch_distlearn_amd import _native
+
+    return _native.testing()
+
 import argparse
 import os
 import sys
@@ -21,7 +27,7 @@ def main():
     ap.add_argument("--splits", type=int, default=-1)
     ap.add_argument("--wsplits", type=int, default=-1, help="override the wgrad split count")
     ap.add_argument("--occupy", type=int, default=0,
-                    help="hold R CUs with RCCL-sized workgroups on a side stream while timing (diag.hip)")
+                    help="hold R CUs with RCCL-sized workgroups on a side stream while timing (testing/diag.hip)")
     ap.add_argument("--dtile", type=int, default=-1, help="override the dgrad tile")
     ap.add_argument("--dsplits", type=int, default=-1, help="override the dgrad split count")
     ap.add_argument("--stages", default="3,0", help="fwd,wgrad LDS ring depth (wgrad 0 = per-tile default)")
@@ -105,7 +111,7 @@ def main():
             g.replay()
             torch.cuda.synchronize()
             if a.occupy:
-                C.occupy_cus(a.occupy, 300000, 0, occ_stream.cuda_stream)
+                _native_testing().occupy_cus(a.occupy, 300000, 0, occ_stream.cuda_stream)
                 torch.cuda._sleep(2_000_000)
             ev0.record()
             g.replay()

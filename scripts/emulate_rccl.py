@@ -1,6 +1,6 @@
 """Step time of the 1-GPU CIFAR-10 training step while R CUs are held by
 workgroups with RCCL's all-reduce footprint (256 threads, ~288 registers per
-wave, 19.7 KiB LDS: csrc/kernels/diag.hip).  On a multi-GPU run the bucketed
+wave, 19.7 KiB LDS: csrc/testing/diag.hip).  On a multi-GPU run the bucketed
 all-reduce overlaps the backward pass on a comm stream; compute kernels whose
 workgroups do not fit beside an RCCL workgroup lose those CUs.  This measures
 that effect on one GPU (R = 0 is the plain step).
@@ -11,6 +11,12 @@ A negative count -R launches R light one-wave workgroups instead (no LDS, few
 registers: they fit beside anything), the control for the cost of a second
 active queue alone.
 """
+
+def _native_testing():
+    from torch_distlearn_amd import _native
+
+    return _native.testing()
+
 import argparse
 import os
 import sys
@@ -47,7 +53,7 @@ sink = torch.zeros(1024, device=dev)
 for r in [int(v) for v in a.cus.split(",")]:
     torch.cuda.synchronize()
     # hold the CUs for longer than the timed run (~0.5 ms/step bound)
-    C.occupy_cus(r, int(a.steps * 600 + 20000), sink.data_ptr(), side.cuda_stream)
+    _native_testing().occupy_cus(r, int(a.steps * 600 + 20000), sink.data_ptr(), side.cuda_stream)
     torch.cuda._sleep(2_000_000)  # let the occupying workgroups land first
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()

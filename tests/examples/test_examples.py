@@ -104,6 +104,39 @@ def test_bench_contract_cpu(algo):
     assert abs(out["value"] - 4 * workers * 1000.0 / out["ms_per_step"]) / out["value"] < 1e-3
 
 
+def test_bench_self_launch_cpu():
+    """``python3 bench.py --gpus 4`` as a plain command (the driver's BENCH
+    command shape): bench.py spawns its own 4 ranks and prints ONE JSON line."""
+    import json
+
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gpus", "4", "--steps", "3",
+           "--warmup", "1", "--batch", "4"]
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 4 and out["config"]["parallelism"] == "dp4" and out["config"]["global_batch"] == 16
+    assert out["config"]["grad_comm_dtype"] == "fp32" and "device_ids" in out["config"]
+
+
+def test_bench_self_launch_fails_fast_without_gpus():
+    """``--gpus 2`` on a box with fewer GPUs: every rank exits with a clear
+    message before any rendezvous and the launcher returns non-zero at once."""
+    import time
+
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1"]
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    env.pop("WORLD_SIZE", None)
+    t0 = time.time()
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and time.time() - t0 < 90
+    assert "needs 2 GPUs" in r.stderr, r.stderr[-2000:]
+    assert r.stdout.strip() == ""
+
+
 def test_allreduce_bw_script_gloo():
     # scripts/allreduce_bw.py (data-plane bandwidth sweep) on 2 gloo ranks
     import json

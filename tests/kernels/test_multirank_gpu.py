@@ -5,8 +5,9 @@ hand-written HIP executor, the gradient bucketer, the participation slot,
 the uneven-step drain and the epoch-end winner broadcast; parameters must be
 BITWISE identical across ranks (the reference's AllReduceSGD oracle,
 test/test_AllReduceSGD.lua:37-39).  The RCCL + hipGraph data plane itself is
-exercised at world 1 by the other GPU tests and at N>1 by the driver's
-scaling runs."""
+exercised at world 1 by the other GPU tests; with one rank per GPU over RCCL
+by tests/kernels/test_rccl_multigpu.py (its ``rccl`` rows need >= 2 GPUs and
+skip on a 1-GPU box) and by ``bench.py --gpus N``."""
 import pytest
 import torch
 

@@ -206,7 +206,7 @@ def test_async_ea_payload_stream(backend, world):
 # ---------------------------------------------------------------------------
 def test_watchdog_aborts_stuck_work(monkeypatch):
     """World-1 RCCL communicator with a 0.5 s timeout; a 2 s spin kernel
-    (csrc/kernels/diag.hip occupy_cus, light variant: every wave exits by
+    (csrc/testing/diag.hip occupy_cus, light variant: every wave exits by
     itself) is handed to the watchdog: it must abort the communicator and
     every later call must raise CommError instead of hanging."""
     _need("gloo", 1)
@@ -217,7 +217,7 @@ def test_watchdog_aborts_stuck_work(monkeypatch):
 
     monkeypatch.setenv("DISTLEARN_RCCL_WORLD1", "1")
     dev = torch.device("cuda", 0)
-    C = _native.native()
+    T = _native.testing()
     comm = RcclCommunicator(0, 1, dev, ctrl_group=None, timeout_s=30.0)
     x = torch.ones(1024, device=dev)
     comm.all_reduce(x)
@@ -226,7 +226,7 @@ def test_watchdog_aborts_stuck_work(monkeypatch):
     assert comm.health() == "" and comm._c.pending() == 0  # healthy work retires
     comm.set_timeout(0.5)
     s = torch.cuda.Stream(device=dev)
-    C.occupy_cus(-1, 2_000_000, 0, s.cuda_stream)
+    T.occupy_cus(-1, 2_000_000, 0, s.cuda_stream)
     comm.track(s)
     t0 = time.time()
     while comm.health() == "" and time.time() - t0 < 5:
@@ -238,4 +238,38 @@ def test_watchdog_aborts_stuck_work(monkeypatch):
     with pytest.raises(CommError):
         comm.check()
     s.synchronize()  # the spin ends by itself
+    comm.close()
+
+
+def test_watchdog_times_grouped_collectives_from_group_end(monkeypatch):
+    """RCCL launches grouped work only at the outermost ncclGroupEnd, so the
+    watchdog's completion event for a collective issued inside ``group()`` must
+    be recorded there: nothing is pending inside the group, one
+    event per grouped op afterwards, and a grouped all-reduce queued behind a
+    stuck kernel trips the timeout."""
+    _need("gloo", 1)
+    import time
+
+    from torch_distlearn_amd import _native
+    from torch_distlearn_amd.parallel.comm import RcclCommunicator
+
+    monkeypatch.setenv("DISTLEARN_RCCL_WORLD1", "1")
+    dev = torch.device("cuda", 0)
+    T = _native.testing()
+    comm = RcclCommunicator(0, 1, dev, ctrl_group=None, timeout_s=30.0)
+    x = torch.ones(1024, device=dev)
+    y = torch.ones(256, device=dev)
+    s = torch.cuda.Stream(device=dev)
+    T.occupy_cus(-1, 1_500_000, 0, s.cuda_stream)  # keeps s busy for 1.5 s
+    with comm.group():
+        comm.all_reduce(x, stream=s)
+        comm.all_reduce(y, stream=s)
+        assert comm._c.pending() == 0  # not launched yet: nothing to time
+    assert comm._c.pending() == 2
+    comm.set_timeout(0.5)
+    t0 = time.time()
+    while comm.health() == "" and time.time() - t0 < 5:
+        time.sleep(0.05)
+    assert "did not complete within" in comm.health()
+    s.synchronize()
     comm.close()

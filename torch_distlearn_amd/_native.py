@@ -55,6 +55,14 @@ def native():
     return _C
 
 
+def testing():
+    """The test/diagnostic extension ``_C_testing`` (csrc/testing/: CU-occupancy
+    spin kernels for the watchdog test and the RCCL footprint emulation).  It is
+    deliberately not part of the product library ``_C``."""
+    native()
+    return importlib.import_module("torch_distlearn_amd._C_testing")
+
+
 def stream_handle(stream=None) -> int:
     """Raw HIP stream handle of a torch stream (default: current stream)."""
     if stream is None:

@@ -331,7 +331,7 @@ class DataParallelTrainer:
                 self._step_body(x, y)
                 if i == 0:
                     self.bucketer.profile.clear()
-            out = comm_summary(self.bucketer.profile)
+            out = comm_summary(self.bucketer.profile, self.tree.numNodes)
         finally:
             self.bucketer.profile = None
         self.sgd.stepsPerNode[self.tree.nodeIndex - 1] -= steps + 1

@@ -4,8 +4,11 @@ bandwidth stress)".  Not a model of the reference; it exists to exercise the
 bucketed gradient all-reduce with a 102 MB fp32 gradient (~25 MB
 buckets, >= 4 per step).
 
-Compute path: PyTorch ops (MIOpen) in channels-last bf16 with fp32 master
-weights in the flat buffer; BatchNorm in fp32 statistics.  Parameters are
+Compute path: channels-last bf16 with fp32 master weights in the flat
+buffer.  Every stride-1 convolution (the 1x1 GEMMs and the 3x3s) runs on the
+hand-written MFMA kernels (ops/conv.py); BatchNorm(+ReLU, +residual) runs on
+the channels-last HIP kernels with fp32 statistics (ops/bn_nhwc.py); the
+remaining convolutions (see ``_CONV_MODE`` below) go through PyTorch/MIOpen.  Parameters are
 registered in forward order, so :meth:`FlatParams.buckets` (reverse order)
 puts the classifier and last stage in the first bucket to be reduced.
 """

@@ -18,9 +18,12 @@ fused SGD kernel already keeps a bf16 shadow of every parameter
   ``dx = dy W`` (same kernel on the transposed shadow) and wgrad
   ``dW = dy^T x`` in fp32 (split-K partial slabs, reduced and added into the
   flat gradient by one kernel).
-* :class:`ShadowConv` -- every other convolution (3x3, strided, the 7x7 stem)
-  stays on MIOpen but reads the shadow and adds its weight gradient into the
-  flat buffer (one cast-add instead of three elementwise kernels).
+* :class:`Conv3x3` -- stride-1 3x3 convolutions on the same streaming MFMA
+  kernel (zero-bordered NHWC inputs written by the BatchNorm kernels).
+* :class:`ShadowConv` -- the convolutions not covered by the kernels above
+  (strided, the 7x7 stem) on MIOpen, reading the shadow and adding the weight
+  gradient into the flat buffer (one cast-add instead of three elementwise
+  kernels).
 
 Both mark their weight's gradient ready for the bucketed all-reduce
 themselves (the autograd graph gets no weight gradient, so the

@@ -386,4 +386,3 @@ def init_communicator(rank: Optional[int] = None, world_size: Optional[int] = No
         raise ValueError(f"unknown backend {backend!r}")
     comm.timeout_s = timeout_s
     return comm
-    raise ValueError(f"unknown backend {backend!r}")

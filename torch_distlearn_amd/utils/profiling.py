@@ -42,7 +42,7 @@ class StepTimer:
         return items_per_step * len(self.times) / max(sum(self.times), 1e-12)
 
 
-def comm_summary(records) -> dict:
+def comm_summary(records, world_size: int = 1) -> dict:
     """Summarise :class:`~torch_distlearn_amd.parallel.buckets.GradBucketer`
     profile records (HIP events on the comm stream around every bucket
     all-reduce, and on the compute stream where the backward ends and where
@@ -54,7 +54,7 @@ def comm_summary(records) -> dict:
     * ``overlap_fraction`` -- 1 - exposed / comm, clamped to [0, 1] (the
       exposed wait also holds the event / queue latency of the last bucket);
     * ``busbw_GBps``       -- ring bus bandwidth of the bucket all-reduces,
-      2 (n-1)/n * bytes / time (set by the caller's world size).
+      2 (n-1)/n * bytes / comm time, with n = ``world_size`` (0 at world 1).
     """
     recs = [r for r in records if r.get("buckets") and "comm_joined" in r]
     if not recs:
@@ -70,7 +70,9 @@ def comm_summary(records) -> dict:
     return {"steps": n, "comm_ms": round(comm / n, 4), "exposed_comm_ms": round(exposed / n, 4),
             # exposed can exceed comm when issue latency dominates tiny collectives: clamp
             "overlap_fraction": round(min(1.0, max(0.0, 1.0 - (exposed / comm if comm > 0 else 0.0))), 4),
-            "bytes_per_step": nbytes // n, "buckets": len(recs[0]["buckets"])}
+            "bytes_per_step": nbytes // n, "buckets": len(recs[0]["buckets"]),
+            "busbw_GBps": round(2.0 * (world_size - 1) / world_size * (nbytes / n) / (comm / n * 1e6), 2)
+            if comm > 0 and world_size > 1 else 0.0}
 
 
 @contextlib.contextmanager
