@@ -249,7 +249,8 @@ def main():
     else:
         tr = DataParallelTrainer(model, tree, lr=a.lr, algo=a.algo, tau=a.tau, alpha=a.alpha, backend=backend,
                                  compute_dtype=cdt, bucket_bytes=int(a.bucket_mb * (1 << 20)), overlap=bool(a.overlap),
-                                 graph=bool(a.graph) and not cpu, max_batch=batch)
+                                 graph=bool(a.graph) and not cpu, max_batch=batch,
+                                 grad_comm_dtype=a.grad_comm_dtype if a.algo == "sgd" else "fp32")
         tr.synchronize_parameters()
         if a.model == "cifar10":
             # synthetic CIFAR-10-shaped uint8 dataset resident in HBM (this rank's
@@ -333,7 +334,8 @@ def main():
         "nccl_max_nchannels": os.environ.get("NCCL_MAX_NCHANNELS"),
         "cu_reserve": getattr(ex, "cu_reserve", None),
         "dgrad_stages": getattr(ex, "dgrad_stages", None),
-        "grad_comm_dtype": a.grad_comm_dtype if a.algo == "sgd" else "fp32",
+        # the wire dtype actually used (world 1: no collective, fp32)
+        "grad_comm_dtype": getattr(tr, "grad_comm_dtype", "fp32") if not is_server else "fp32",
     }
     ms = dt / a.steps * 1e3
     imgs = batch * len(workers) * a.steps / dt

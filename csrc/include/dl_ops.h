@@ -17,6 +17,9 @@ void elastic_step(uintptr_t p, uintptr_t c, uintptr_t pending, uintptr_t out, ui
 void add_inplace(uintptr_t y, uintptr_t x, int64_t n, uintptr_t stream);
 void fill_f32(uintptr_t x, float v, int64_t n, int64_t slot_index, float slot_value, uintptr_t stream);
 void cast_f32_bf16(uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream);
+void cast_bf16_f32(uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream);
+void sgd_update_g16(uintptr_t p, uintptr_t g16, uintptr_t mom, uintptr_t p16, uintptr_t slot, float lr,
+                    float momentum, float wd, int64_t n, uintptr_t stream);
 
 // metrics.hip ---------------------------------------------------------------
 // channels-last training BatchNorm (+ReLU, +residual) for the ResNet-50 path

@@ -28,8 +28,19 @@ __device__ __forceinline__ float participation_scale(const float* slot) {
 // SGD (+ optional momentum / weight decay), fused with 1/n normalisation and
 // the bf16 shadow-weight refresh used by the bf16 compute path.
 // ---------------------------------------------------------------------------
-template <bool kMomentum, bool kShadow>
-__global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
+// G16: the gradient is the bf16 all-reduced wire copy (grad_comm_dtype="bf16":
+// half the xGMI bytes; read here directly, never widened back to fp32).
+__device__ __forceinline__ float4 load_grad4(const float* g, int64_t i) {
+  return reinterpret_cast<const float4*>(g)[i];
+}
+__device__ __forceinline__ float4 load_grad4(const bf16_t* g, int64_t i) {
+  const uint2 u = reinterpret_cast<const uint2*>(g)[i];
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+
+template <bool kMomentum, bool kShadow, typename GT = float>
+__global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, const GT* __restrict__ g,
                                                   float* __restrict__ mom, bf16_t* __restrict__ p16,
                                                   const float* __restrict__ slot, float lr, float momentum,
                                                   float wd, int64_t n4) {
@@ -37,7 +48,7 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, const f
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 pv = reinterpret_cast<float4*>(p)[i];
-    float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float4 gv = load_grad4(g, i);
     float gx = gv.x * s + wd * pv.x, gy = gv.y * s + wd * pv.y;
     float gz = gv.z * s + wd * pv.z, gw = gv.w * s + wd * pv.w;
     if constexpr (kMomentum) {
@@ -144,6 +155,14 @@ __global__ void __launch_bounds__(256) cast_f32_bf16_kernel(const float* __restr
   }
 }
 
+// bf16 -> fp32 (the all-reduced bf16 wire copy back into the fp32 gradient)
+__global__ void __launch_bounds__(256) cast_bf16_f32_kernel(const bf16_t* __restrict__ x, float* __restrict__ y,
+                                                            int64_t n4) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride)
+    reinterpret_cast<float4*>(y)[i] = load_grad4(x, i);
+}
+
 // ---------------------------------------------------------------------------
 // Host launchers (C ABI-ish, raw pointers + stream handle)
 // ---------------------------------------------------------------------------
@@ -164,6 +183,30 @@ void sgd_update(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, uintptr_
   else if (mom) sgd_kernel<true, false><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4);
   else if (p16) sgd_kernel<false, true><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4);
   else sgd_kernel<false, false><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+void sgd_update_g16(uintptr_t p, uintptr_t g16, uintptr_t mom, uintptr_t p16, uintptr_t slot, float lr,
+                    float momentum, float wd, int64_t n, uintptr_t stream) {
+  check_vec4(n, "sgd_update_g16");
+  const int64_t n4 = n / 4;
+  if (n4 == 0) return;
+  dim3 grid(stream_grid(n4)), block(256);
+  auto s = as_stream(stream);
+  float* P = (float*)p; const bf16_t* G = (const bf16_t*)g16; float* M = (float*)mom; bf16_t* P16 = (bf16_t*)p16;
+  const float* S = (const float*)slot;
+  if (mom && p16) sgd_kernel<true, true, bf16_t><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4);
+  else if (mom) sgd_kernel<true, false, bf16_t><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4);
+  else if (p16) sgd_kernel<false, true, bf16_t><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4);
+  else sgd_kernel<false, false, bf16_t><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+void cast_bf16_f32(uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream) {
+  check_vec4(n, "cast_bf16_f32");
+  const int64_t n4 = n / 4;
+  if (n4 == 0) return;
+  cast_bf16_f32_kernel<<<stream_grid(n4), 256, 0, as_stream(stream)>>>((const bf16_t*)x, (float*)y, n4);
   DL_HIP_CHECK(hipGetLastError());
 }
 

@@ -41,7 +41,11 @@ def _sgd_worker(rank, world, port, trials, mode):
             w = torch.nn.Parameter(torch.randn(7, 3))
             b = torch.nn.Parameter(torch.randn(5))
             flat = FlatParams([w, b])
-            bucketer = GradBucketer(tree.comm, flat, bucket_bytes=64, hooks=False) if mode == "bucket" else None
+            bucketer = GradBucketer(tree.comm, flat, bucket_bytes=64, hooks=False,
+                                    wire="bf16" if mode == "bucket16" else "fp32") \
+                if mode.startswith("bucket") else None
+            if mode == "bucket16":
+                assert bucketer.wire16 and flat.grad16 is not None
             sgd = AllReduceSGD(tree, bucketer=bucketer)
             sgd.synchronizeParameters(flat)
             for _epoch in range(5):
@@ -64,7 +68,7 @@ TRIALS = 10
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
-@pytest.mark.parametrize("mode", ["table", "flat", "bucket"])
+@pytest.mark.parametrize("mode", ["table", "flat", "bucket", "bucket16"])
 def test_allreduce_sgd_bitwise(world, mode):
     # 10 randomized trials like test/test_AllReduceSGD.lua:23
     res = mp.run(_sgd_worker, world, TRIALS, mode)
@@ -72,3 +76,14 @@ def test_allreduce_sgd_bitwise(world, mode):
         r0 = res[0][trial]
         for r in range(1, world):
             assert (r0 == res[r][trial]).all() and r0.tobytes() == res[r][trial].tobytes(), f"node {r+1} params differ (trial {trial}, mode {mode})"
+
+
+def test_bf16_wire_matches_fp32_wire():
+    """grad_comm_dtype bf16 (bf16 bucket all-reduce, fp32 participation count)
+    ends at the fp32-wire parameters to bf16 tolerance, with uneven epochs
+    (drain + winner broadcast) on 4 gloo ranks."""
+    r32 = mp.run(_sgd_worker, 4, 3, "bucket")
+    r16 = mp.run(_sgd_worker, 4, 3, "bucket16")
+    for t in range(3):
+        a, b = r32[0][t], r16[0][t]
+        assert abs(a - b).max() <= 2e-2 * max(1.0, abs(a).max()), (a, b)

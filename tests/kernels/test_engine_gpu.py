@@ -58,7 +58,7 @@ def test_gather_normalize_and_confusion(dev):
     assert torch.equal(cg.mat.cpu(), cc.mat)
 
 
-def _trainer(dev, backend, graph, port):
+def _trainer(dev, backend, graph, port, **kw):
     from torch_distlearn_amd import Tree
     from torch_distlearn_amd.engine import DataParallelTrainer
     from torch_distlearn_amd.models import CifarConvNet
@@ -66,7 +66,7 @@ def _trainer(dev, backend, graph, port):
     tree = Tree(1, 1, host="127.0.0.1", port=port, device=dev)
     model = CifarConvNet(seed=7).to(dev)
     tr = DataParallelTrainer(model, tree, lr=0.02, backend=backend, compute_dtype=torch.bfloat16, graph=graph,
-                             max_batch=32)
+                             max_batch=32, **kw)
     tr.synchronize_parameters()
     return tr
 
@@ -296,3 +296,30 @@ def test_ea_run_unrolled_matches_stepwise(dev, monkeypatch, rccl):
     assert (s0, k0, n0) == (s1, k1, n1) == (11, 11, 11)
     assert not torch.equal(c0, p0)  # the rounds moved the center
     assert torch.equal(p0, p1) and torch.equal(c0, c1)
+
+
+def test_bf16_grad_wire_through_rccl(dev, monkeypatch):
+    """grad_comm_dtype="bf16" (world-1 collectives forced through RCCL, inside
+    the captured graph): the bucket all-reduces move half the bytes, the fp32
+    participation count rides in the same group, and the update (the fused
+    SGD reading the bf16 wire copy) matches the fp32 wire to bf16 tolerance."""
+    monkeypatch.setenv("DISTLEARN_RCCL_WORLD1", "1")
+    g = torch.Generator(device=dev).manual_seed(4)
+    xs = torch.randn(3, 32, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)
+    ys = torch.randint(0, 10, (3, 32), device=dev, generator=g)
+    res = {}
+    for wire in ("fp32", "bf16"):
+        tr = _trainer(dev, "hip", True, 29707, grad_comm_dtype=wire)
+        assert tr.grad_comm_dtype == wire
+        before = tr.flat.data.clone()
+        for i in range(3):
+            tr.step(xs[i], ys[i])
+        torch.cuda.synchronize()
+        assert float(tr.flat.slot) == 1.0
+        ld = _loader(dev, batch=16)
+        st = tr.comm_profile(ld, steps=2)
+        res[wire] = (tr.flat.data - before, st["bytes_per_step"])
+    (d32, b32), (d16, b16) = res["fp32"], res["bf16"]
+    assert b16 * 2 == b32
+    rel = float((d16 - d32).norm() / d32.norm())
+    assert rel < 0.05, rel

@@ -45,7 +45,7 @@ class DataParallelTrainer:
                  backend: str = "torch", compute_dtype: torch.dtype = torch.bfloat16,
                  bucket_bytes: int = 4 << 20, overlap: bool = True, graph: bool = False,
                  loss_fn: Optional[Callable] = None, max_batch: Optional[int] = None,
-                 async_ea: Optional[Any] = None):
+                 async_ea: Optional[Any] = None, grad_comm_dtype: str = "fp32"):
         self.model = model
         self.tree = tree
         self.lr, self.momentum, self.weight_decay = lr, momentum, weight_decay
@@ -59,8 +59,12 @@ class DataParallelTrainer:
         self.mom = self.flat.like(0.0) if momentum else None
         self.loss_fn = loss_fn or getattr(model, "loss", None) or torch.nn.functional.nll_loss
         hooks = overlap and backend == "torch"
-        self.bucketer = GradBucketer(tree.comm, self.flat, bucket_bytes=bucket_bytes, hooks=hooks) \
+        # grad_comm_dtype="bf16": the bucketed all-reduce sends a bf16 copy of the
+        # gradient (half the xGMI bytes) with the participation count in fp32
+        self.bucketer = GradBucketer(tree.comm, self.flat, bucket_bytes=bucket_bytes, hooks=hooks,
+                                     wire=grad_comm_dtype) \
             if (tree.numNodes > 1 or dev.type == "cuda") and algo == "sgd" else None
+        self.grad_comm_dtype = self.bucketer.wire if self.bucketer is not None else "fp32"
         self.aea = None
         if algo == "sgd":
             self.sgd = AllReduceSGD(tree, bucketer=self.bucketer)

@@ -85,6 +85,19 @@ class FlatParams:
         if shadow_bf16:
             self.shadow = torch.zeros(self.total, dtype=torch.bfloat16, device=self.device)
             self.refresh_shadow()
+        self.grad16 = None  # bf16 wire copy of the gradient (enable_grad16)
+
+    def enable_grad16(self) -> torch.Tensor:
+        """Allocate the bf16 gradient wire buffer (same layout as ``grad``):
+        with ``grad_comm_dtype="bf16"`` the bucketed all-reduce sends this
+        copy -- half the xGMI bytes -- and the fused SGD reads it directly;
+        the participation count stays fp32 (``grad``'s header, all-reduced
+        beside it in the same group)."""
+        if self.grad is None:
+            raise ValueError("FlatParams.enable_grad16: no gradient buffer")
+        if self.grad16 is None:
+            self.grad16 = torch.zeros(self.total, dtype=torch.bfloat16, device=self.device)
+        return self.grad16
 
     # ----------------------------------------------------------------- views
     def _views(self, buf: torch.Tensor) -> List[torch.Tensor]:
@@ -166,13 +179,15 @@ def _scale_from_slot(slot):
 def sgd_update_(p: torch.Tensor, g: torch.Tensor, lr: float, slot: torch.Tensor | None = None,
                 mom: torch.Tensor | None = None, momentum: float = 0.0, weight_decay: float = 0.0,
                 shadow: torch.Tensor | None = None) -> None:
-    """p -= lr * (g/n + wd*p) [with momentum buffer]; n from ``slot`` (device)."""
+    """p -= lr * (g/n + wd*p) [with momentum buffer]; n from ``slot`` (device).
+    ``g`` is fp32, or bf16 (the all-reduced wire copy of grad_comm_dtype="bf16")."""
     if p.is_cuda:
-        native().sgd_update(p.data_ptr(), g.data_ptr(), _ptr(mom), _ptr(shadow), _ptr(slot), float(lr),
-                            float(momentum), float(weight_decay), p.numel(), stream_handle())
+        fn = native().sgd_update_g16 if g.dtype == torch.bfloat16 else native().sgd_update
+        fn(p.data_ptr(), g.data_ptr(), _ptr(mom), _ptr(shadow), _ptr(slot), float(lr), float(momentum),
+           float(weight_decay), p.numel(), stream_handle())
         return
     with torch.no_grad():
-        d = g * _scale_from_slot(slot)
+        d = g.float() * _scale_from_slot(slot)
         if weight_decay:
             d = d + weight_decay * p
         if mom is not None:
@@ -191,12 +206,14 @@ def _overlaps(x: torch.Tensor, y: torch.Tensor) -> bool:
 
 
 def flat_sgd_(flat: "FlatParams", lr: float, slot: torch.Tensor | None = None, mom: torch.Tensor | None = None,
-              momentum: float = 0.0, weight_decay: float = 0.0) -> None:
+              momentum: float = 0.0, weight_decay: float = 0.0, grad: torch.Tensor | None = None) -> None:
     """The fused update over a FlatParams' parameter body: the 64-element
     header (whose gradient element is the participation count) is left out,
-    so ``n`` never flows into the parameter buffer."""
+    so ``n`` never flows into the parameter buffer.  ``grad``: the gradient
+    buffer to read (default ``flat.grad``; ``flat.grad16`` for bf16 comm)."""
     H = HEADER
-    sgd_update_(flat.data[H:], flat.grad[H:], lr, slot=slot, mom=None if mom is None else mom[H:],
+    g = flat.grad if grad is None else grad
+    sgd_update_(flat.data[H:], g[H:], lr, slot=slot, mom=None if mom is None else mom[H:],
                 momentum=momentum, weight_decay=weight_decay,
                 shadow=None if flat.shadow is None else flat.shadow[H:])
 
@@ -230,6 +247,18 @@ def elastic_step_(p: torch.Tensor, c: torch.Tensor, out: torch.Tensor, alpha: fl
         p.sub_(out)
         if shadow is not None:
             shadow.copy_(p)
+
+
+def cast_(dst: torch.Tensor, src: torch.Tensor) -> None:
+    """dst = src between fp32 and bf16 (same length, multiple of 4 on GPU)."""
+    if dst.is_cuda and dst.numel() % 4 == 0:
+        if src.dtype == torch.float32 and dst.dtype == torch.bfloat16:
+            native().cast_f32_bf16(src.data_ptr(), dst.data_ptr(), dst.numel(), stream_handle())
+            return
+        if src.dtype == torch.bfloat16 and dst.dtype == torch.float32:
+            native().cast_bf16_f32(src.data_ptr(), dst.data_ptr(), dst.numel(), stream_handle())
+            return
+    dst.copy_(src)
 
 
 def add_(y: torch.Tensor, x: torch.Tensor) -> None:

@@ -102,14 +102,18 @@ class AllReduceSGD:
         all-reduce (unless the bucketer already did), then ONE kernel
         ``p -= lr*(g/n + wd*p)`` (+momentum, + bf16 shadow refresh).  This is
         examples/cifar10.lua:184-191 in one launch."""
+        g = None
+        bk = self.bucketer if (self.bucketer is not None and flat is self.bucketer.flat) else None
         if not already_reduced:
-            if self.bucketer is not None and flat is self.bucketer.flat:
-                self.bucketer.finish()
+            if bk is not None:
+                bk.finish(widen=False)  # bf16 wire: the update reads the reduced bf16 copy directly
             else:
                 self.tree.allReduce(FlatBuffer(flat.grad))
             self._count_step()
             self._remember(flat)
-        flat_sgd_(flat, lr, slot=flat.slot, mom=momentum_buf, momentum=momentum, weight_decay=weight_decay)
+        if bk is not None and bk.wire16 and not already_reduced:
+            g = flat.grad16
+        flat_sgd_(flat, lr, slot=flat.slot, mom=momentum_buf, momentum=momentum, weight_decay=weight_decay, grad=g)
 
     def _remember(self, grads):
         if self._drain_template is None:

@@ -19,6 +19,14 @@ The participation slot (``n``) lives in the header of the flat buffer, which
 is inside the bucket launched *last*, so ``n`` is complete once all buckets
 have landed; draining nodes replay the same bucket sequence with zeros and
 slot 0 (:meth:`drain`).
+
+Wire dtype (``wire="bf16"``): each bucket's fp32 gradient is
+cast to the FlatParams' bf16 wire buffer on the comm stream and THAT copy is
+all-reduced -- half the xGMI bytes per step -- while the header (participation
+count) is all-reduced in fp32 beside it in the same group.  The fused SGD
+reads the bf16 result directly (``AllReduceSGD.step``); API callers that read
+``flat.grad`` get it widened back to fp32 by :meth:`finish`.  At world 1 the
+all-reduce is the identity and the wire stays fp32.
 """
 from __future__ import annotations
 
@@ -26,14 +34,27 @@ from typing import List, Optional, Tuple
 
 import torch
 
-from ..ops.flat import SLOT, FlatParams, fill_
+import contextlib
+
+from ..ops.flat import HEADER, SLOT, FlatParams, cast_, fill_
+
+
+def _nullctx():
+    return contextlib.nullcontext()
 
 
 class GradBucketer:
     def __init__(self, comm, flat: FlatParams, bucket_bytes: int = 4 << 20, hooks: bool = True,
-                 stream: Optional["torch.cuda.Stream"] = None):
+                 stream: Optional["torch.cuda.Stream"] = None, wire: str = "fp32"):
+        if wire not in ("fp32", "bf16"):
+            raise ValueError(f"wire dtype {wire!r}: fp32 or bf16")
         self.comm = comm
         self.flat = flat
+        # bf16 wire only where a collective actually runs (world 1 skips it unless forced)
+        self.wire16 = wire == "bf16" and (comm.world_size > 1 or getattr(comm, "_skip1", True) is False)
+        self.wire = "bf16" if self.wire16 else "fp32"
+        if self.wire16:
+            flat.enable_grad16()
         self.ranges: List[Tuple[int, int]] = flat.buckets(bucket_bytes)
         self.nb = len(self.ranges)
         # leaf -> bucket
@@ -79,9 +100,21 @@ class GradBucketer:
         ev.record(stream)
         return ev
 
+    def _reduce(self, s: int, e: int, stream=None):
+        """All-reduce grad[s:e] (fp32 wire) or its bf16 copy + the fp32 header."""
+        f = self.flat
+        if not self.wire16:
+            self.comm.all_reduce(f.grad[s:e], "sum", stream=stream)
+            return
+        cast_(f.grad16[s:e], f.grad[s:e])
+        with self.comm.group():
+            self.comm.all_reduce(f.grad16[s:e], "sum", stream=stream)
+            if s < HEADER:  # the participation count stays exact in fp32
+                self.comm.all_reduce(f.grad[0:HEADER], "sum", stream=stream)
+
     def _launch(self, b: int):
         s, e = self.ranges[b]
-        buf = self.flat.grad[s:e]
+        buf = (self.flat.grad16 if self.wire16 else self.flat.grad)[s:e]
         if self.cuda:
             cur = torch.cuda.current_stream()
             self.stream.wait_stream(cur)
@@ -91,12 +124,12 @@ class GradBucketer:
                     self._rec = {"buckets": []}
                 t0 = self._event(self.stream)
             with torch.cuda.stream(self.stream):
-                self.comm.all_reduce(buf, "sum", stream=self.stream)
+                self._reduce(s, e, stream=self.stream)
             if prof:
                 self._rec["buckets"].append((t0, self._event(self.stream), (e - s) * buf.element_size()))
             buf.record_stream(self.stream)
         else:
-            self.comm.all_reduce(buf, "sum")
+            self._reduce(s, e)
         self.launched += 1
 
     def _pump(self):
@@ -114,12 +147,19 @@ class GradBucketer:
         self.remaining[b] = 0
         self._pump()
 
-    def finish(self):
+    def finish(self, widen: bool = True):
         """Launch what is left (params without grads), then order the compute
-        stream after the comm stream.  Resets for the next step."""
+        stream after the comm stream.  Resets for the next step.  With the
+        bf16 wire, ``widen`` copies the all-reduced bf16 gradient back into
+        ``flat.grad`` (callers that read the bf16 copy pass False)."""
         for b in range(self.nb):
             self.remaining[b] = 0
         self._pump()
+        if self.wire16 and widen:
+            f = self.flat
+            ctx = torch.cuda.stream(self.stream) if self.cuda else _nullctx()
+            with ctx:
+                cast_(f.grad[HEADER:], f.grad16[HEADER:])
         if self.cuda:
             cur = torch.cuda.current_stream()
             prof = self._profiling() and self._rec is not None
@@ -136,7 +176,7 @@ class GradBucketer:
         """Replay zero buckets (slot 0) until no node is active any more."""
         while True:
             fill_(self.flat.grad, 0.0, slot_value=0.0)
-            self.finish()
+            self.finish(widen=False)
             n = int(self.flat.grad[SLOT].item())
             if n == 0:
                 return
