@@ -53,6 +53,20 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_conv_waves", &set_conv_waves);
   m.def("set_conv_debug", &set_conv_debug);
   m.def("conv_wgrad", &conv_wgrad);
+  m.def("combine_bwd_reduce", &combine_bwd_reduce);
+  m.def("combine_bwd_reduce_blocks", &combine_bwd_reduce_blocks);
+  m.def("conv_fwd_ex", &conv_fwd_ex);
+  m.def("conv_wgrad_ex", &conv_wgrad_ex);
+  // ---- ResNet-50 glue (resnet_glue.hip) ------------------------------------------
+  m.def("s2d_stem_input", &s2d_stem_input);
+  m.def("stem_weight_pack", &stem_weight_pack);
+  m.def("stem_wgrad_unpack", &stem_wgrad_unpack);
+  m.def("phase_weights", &phase_weights);
+  m.def("head_pool", &head_pool);
+  m.def("head_softmax_nll", &head_softmax_nll);
+  m.def("head_weight_prep", &head_weight_prep);
+  m.def("head_broadcast", &head_broadcast);
+  m.def("head_wgrad_reduce", &head_wgrad_reduce);
   m.def("slab_reduce", &slab_reduce);
   m.def("slab_reduce_add", &slab_reduce_add);
   m.def("slab_reduce_add_oihw", &slab_reduce_add_oihw);

@@ -58,6 +58,12 @@ void set_conv_region_waves(int w);
 void set_conv_stages(int fwd, int wgrad);
 void set_conv_waves(int waves);
 void set_conv_debug(uintptr_t buf);
+int conv_fwd_ex(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab, int B, int Ho, int Wo, int Hp,
+                int Wp, int Cin, int Cout, int KH, int KW, int S, int om_S, int om_H0, int om_W0, int om_W, int om_HW,
+                uintptr_t addend, int tile, int splits, uintptr_t stream);
+void conv_wgrad_ex(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int Ho, int Wo, int Hp, int Wp, int dHp, int dWp,
+                   int dpad, int Cin, int Cout, int KH, int KW, int S, int splits, int ldo, int tile,
+                   uintptr_t stream);
 void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, int Cin, int Cout, int KS, int splits,
                 int ldo, int tile, int atomic_creal, uintptr_t stream);
 void set_reduce_atomic_conv(int rows);
@@ -97,6 +103,9 @@ void bn_finalize(uintptr_t partial, int T, int C, int64_t M, uintptr_t gamma, ui
 void bn_relu_pool_fwd(uintptr_t y, uintptr_t coef, uintptr_t out, int B, int H, int W, int C, int opad,
                       uintptr_t stream);
 int bn_bwd_blocks(int B, int H, int W, int C);
+int combine_bwd_reduce(uintptr_t slab, int splits, uintptr_t dP, uintptr_t y, uintptr_t coef, uintptr_t partial, int B,
+                       int H, int W, int C, uintptr_t stream);
+int combine_bwd_reduce_blocks(int B, int H, int W, int C);
 void bn_relu_pool_bwd_reduce(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t partial, int B, int H, int W, int C,
                              int blocks, uintptr_t stream);
 void bn_bwd_finalize(uintptr_t partial, int T, int C, int64_t M, uintptr_t gamma, uintptr_t coef, uintptr_t dgamma,
@@ -141,5 +150,19 @@ void mnist_step(uintptr_t x, int x_bf16, uintptr_t labels, uintptr_t w1, uintptr
                 uintptr_t wf, uintptr_t bf, uintptr_t gw1, uintptr_t gb1, uintptr_t gw2, uintptr_t gb2, uintptr_t gwf,
                 uintptr_t gbf, uintptr_t logp, uintptr_t loss_b, uintptr_t scratch, int B, uintptr_t stream);
 int64_t mnist_scratch_bytes(int B);
+
+// resnet_glue.hip ---------------------------------------------------------------
+void s2d_stem_input(uintptr_t x, uintptr_t S, int N, int H, int W, int Hs, int Ws, int pad, uintptr_t stream);
+void stem_weight_pack(uintptr_t w7, uintptr_t w4, int Cout, uintptr_t stream);
+void stem_wgrad_unpack(uintptr_t slab, uintptr_t dw7, int splits, int Cout, uintptr_t stream);
+void phase_weights(uintptr_t wt, uintptr_t out, int Cin, int Cout, uintptr_t stream);
+void head_pool(uintptr_t h, uintptr_t f, int B, int HW, int C, uintptr_t loss, uintptr_t stream);
+void head_softmax_nll(uintptr_t slab, int splits, int B, int NC, int NCp, uintptr_t bias, uintptr_t labels,
+                      uintptr_t logp, uintptr_t loss_b, uintptr_t dl, float dscale, uintptr_t db, uintptr_t loss,
+                      uintptr_t stream);
+void head_weight_prep(uintptr_t w, uintptr_t wb, uintptr_t wbt, int NC, int NCp, int C, uintptr_t stream);
+void head_broadcast(uintptr_t df, uintptr_t dh, int B, int HW, int C, uintptr_t stream);
+void head_wgrad_reduce(uintptr_t slab, uintptr_t dw, int splits, int NC, int NCp, int C, float scale,
+                       uintptr_t stream);
 
 }  // namespace dl

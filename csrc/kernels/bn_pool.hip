@@ -341,6 +341,120 @@ __device__ __forceinline__ void bwd_reduce_body(const bf16_t* __restrict__ y, co
   }
 }
 
+// Split-K combine of a dgrad (SPL fp32 slabs [SPL][M][C], M = B*Ho*Wo pooled
+// pixels) fused with the BN backward reduce of the block below, in the
+// combine's row-blocked layout (the fast one for the slab reads: each block
+// owns rows [r0, r1), each thread one 8-channel chunk, splits summed in
+// order in batches of 4 with all loads of a batch in flight): dP = bf16(sum),
+// stored once, and the reduce's window loads of y issued beside the first
+// batch.  One partial row per block (mode 0, `partial` needs gridDim.x rows)
+// or striped atomics (mode 2).
+template <int SPL>
+__global__ void __launch_bounds__(256) combine_bwd_reduce_kernel(const float* __restrict__ slab,
+                                                                 bf16_t* __restrict__ dP, const bf16_t* __restrict__ y,
+                                                                 const float* __restrict__ coef,
+                                                                 float* __restrict__ partial, int B, int H, int W,
+                                                                 int C, int rows_per_block) {
+  const int C8 = C >> 3, Ho = H >> 1, Wo = W >> 1;
+  const int M = B * Ho * Wo;
+  const int tpr = C8, rpi = 256 / tpr;
+  const int c8 = threadIdx.x % tpr, rsub = threadIdx.x / tpr, c0 = c8 * 8;
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  const int64_t MN = (int64_t)M * C;
+  BwdCtx cx;
+  load8(cx.mu, coef + c0);
+  load8(cx.is, coef + C + c0);
+  load8(cx.sc, coef + 2 * C + c0);
+  load8(cx.sh, coef + 3 * C + c0);
+  float s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
+  if (rsub < rpi) {
+    for (int m = r0 + rsub; m < r1; m += rpi) {
+      const int ow = m % Wo, t = m / Wo, oh = t % Ho, b = t / Ho;
+      const bf16_t* base = y + (((int64_t)(b * H + 2 * oh) * W) + 2 * ow) * C + c0;
+      uint4 yw[4];
+      yw[0] = *reinterpret_cast<const uint4*>(base);
+      yw[1] = *reinterpret_cast<const uint4*>(base + C);
+      yw[2] = *reinterpret_cast<const uint4*>(base + (int64_t)W * C);
+      yw[3] = *reinterpret_cast<const uint4*>(base + (int64_t)W * C + C);
+      const float* q = slab + (int64_t)m * C + c0;
+      constexpr int BT = SPL < 4 ? SPL : 4;
+      float v[8];
+      {
+        float4 a[BT], bb[BT];
+#pragma unroll
+        for (int u = 0; u < BT; ++u) {
+          a[u] = *reinterpret_cast<const float4*>(q + u * MN);
+          bb[u] = *reinterpret_cast<const float4*>(q + u * MN + 4);
+        }
+        v[0] = a[0].x; v[1] = a[0].y; v[2] = a[0].z; v[3] = a[0].w;
+        v[4] = bb[0].x; v[5] = bb[0].y; v[6] = bb[0].z; v[7] = bb[0].w;
+#pragma unroll
+        for (int u = 1; u < BT; ++u) {
+          v[0] += a[u].x; v[1] += a[u].y; v[2] += a[u].z; v[3] += a[u].w;
+          v[4] += bb[u].x; v[5] += bb[u].y; v[6] += bb[u].z; v[7] += bb[u].w;
+        }
+      }
+#pragma unroll
+      for (int s0 = BT; s0 < SPL; s0 += 4) {
+        float4 a[4], bb[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          a[u] = *reinterpret_cast<const float4*>(q + (s0 + u) * MN);
+          bb[u] = *reinterpret_cast<const float4*>(q + (s0 + u) * MN + 4);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          v[0] += a[u].x; v[1] += a[u].y; v[2] += a[u].z; v[3] += a[u].w;
+          v[4] += bb[u].x; v[5] += bb[u].y; v[6] += bb[u].z; v[7] += bb[u].w;
+        }
+      }
+      uint4 gv;
+      gv.x = pack_bf16x2(v[0], v[1]); gv.y = pack_bf16x2(v[2], v[3]);
+      gv.z = pack_bf16x2(v[4], v[5]); gv.w = pack_bf16x2(v[6], v[7]);
+      *reinterpret_cast<uint4*>(dP + (int64_t)m * C + c0) = gv;
+      float yv[4][8], g[8];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) unpack8(yw[w], yv[w]);
+      unpack8(gv, g);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float best = -INFINITY;
+        int arg = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const float r = fmaxf(fmaf(cx.sc[k], yv[w][k], cx.sh[k]), 0.f);
+          if (r > best) { best = r; arg = w; }
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const float dz = (w == arg && best > 0.f) ? g[k] : 0.f;
+          s1[k] += dz;
+          s2[k] += dz * (yv[w][k] - cx.mu[k]) * cx.is[k];
+        }
+      }
+    }
+  }
+  __shared__ float red[256][17];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { red[threadIdx.x][k] = s1[k]; red[threadIdx.x][8 + k] = s2[k]; }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const int ch = c >> 3, k = c & 7;
+    float a = 0.f, bsum = 0.f;
+    for (int t = ch; t < rpi * tpr; t += tpr) { a += red[t][k]; bsum += red[t][8 + k]; }
+    if (const int R = g_red_atomic_bn) {  // rows of [dgamma ; dbeta] = [sum dz*xhat ; sum dz]
+      float* p = partial + (int64_t)(blockIdx.x & (R - 1)) * 2 * C;
+      unsafeAtomicAdd(p + c, bsum);
+      unsafeAtomicAdd(p + C + c, a);
+    } else {
+      partial[(int64_t)blockIdx.x * 2 * C + c] = a;
+      partial[(int64_t)blockIdx.x * 2 * C + C + c] = bsum;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) bn_relu_pool_bwd_reduce_kernel(const bf16_t* __restrict__ y,
                                                                       const bf16_t* __restrict__ dP,
                                                                       const float* __restrict__ coef,
@@ -573,6 +687,47 @@ void bn_relu_pool_bwd_reduce(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_
   bn_relu_pool_bwd_reduce_kernel<<<blocks, 256, 0, as_stream(stream)>>>(
       (const bf16_t*)y, (const bf16_t*)dP, (const float*)coef, (float*)partial, B, H, W, C);
   DL_HIP_CHECK(hipGetLastError());
+}
+
+// dP = bf16(sum of the `splits` fp32 slabs of its split-K dgrad) fused with
+// the BN backward reduce over (y, dP) (conv_fwd was called with the
+// keep-slabs bit, so it launched no combine of its own).
+// rows per block / blocks of combine_bwd_reduce (~384 blocks of whole row iterations)
+static int cbr_rows_per_block(int M, int C) {
+  const int rpi = 256 / (C / 8);
+  int rpb = (M + 383) / 384;
+  rpb = ((rpb + rpi - 1) / rpi) * rpi;
+  return rpb < rpi ? rpi : rpb;
+}
+
+int combine_bwd_reduce_blocks(int B, int H, int W, int C) {
+  const int M = B * (H / 2) * (W / 2), rpb = cbr_rows_per_block(M, C);
+  return (M + rpb - 1) / rpb;
+}
+
+// dP = bf16(sum of the `splits` fp32 slabs of its split-K dgrad) fused with
+// the BN backward reduce over (y, dP) (conv_fwd was called with the
+// keep-slabs bit, so it launched no combine of its own).  Returns the number
+// of partial rows written (mode 0: `partial` must hold that many).
+int combine_bwd_reduce(uintptr_t slab, int splits, uintptr_t dP, uintptr_t y, uintptr_t coef, uintptr_t partial, int B,
+                       int H, int W, int C, uintptr_t stream) {
+  check_c(C);
+  if ((256 % (C / 8)) != 0) throw std::runtime_error("combine_bwd_reduce: C/8 must divide 256");
+  const int M = B * (H / 2) * (W / 2), rpb = cbr_rows_per_block(M, C), nb = (M + rpb - 1) / rpb;
+  auto s = as_stream(stream);
+  const float* S = (const float*)slab;
+  bf16_t* D = (bf16_t*)dP;
+  const bf16_t* Y = (const bf16_t*)y;
+  const float* K = (const float*)coef;
+  float* P = (float*)partial;
+  switch (splits) {
+    case 2: combine_bwd_reduce_kernel<2><<<nb, 256, 0, s>>>(S, D, Y, K, P, B, H, W, C, rpb); break;
+    case 4: combine_bwd_reduce_kernel<4><<<nb, 256, 0, s>>>(S, D, Y, K, P, B, H, W, C, rpb); break;
+    case 8: combine_bwd_reduce_kernel<8><<<nb, 256, 0, s>>>(S, D, Y, K, P, B, H, W, C, rpb); break;
+    default: throw std::runtime_error("combine_bwd_reduce: splits must be 2, 4 or 8");
+  }
+  DL_HIP_CHECK(hipGetLastError());
+  return nb;
 }
 
 void bn_bwd_reduce_head(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t partial, int B, int H, int W, int C,

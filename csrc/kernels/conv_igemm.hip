@@ -67,6 +67,16 @@ struct ConvGeom {
   int mmajor;              // fwd/dgrad tile order after the XCD swizzle: 0 panel-major, 1 M-tile-major
   int pm_kmax, pm_P;       // balanced position-major split-K: max K steps per workgroup, workgroups per N tile
   float inv_HW, inv_W;     // reciprocals for the non-pow2 pixel decomposition (fdivmod)
+  // Generalised geometry (make_geom_ex; the streaming forward and the wgrad
+  // kernels only, non-pow2 addressing): tap (kh, kw) of output pixel (oh, ow)
+  // reads padded input pixel (S*oh + kh, S*ow + kw) of the [B][Hp][Wp][Cin]
+  // buffer; kernels may be KH x KW (K = KH*KW*Cin, taps row-major).
+  int S, KH, KW;
+  int dsep, dHp, dWp, dpad;  // wgrad: dy has its own buffer geometry [B][dHp][dWp][Cout], interior at dpad
+  // epilogue output-row map (om != 0): output pixel (b, oh, ow) is stored at
+  // row b*omHW + (omS*oh + omH0)*omW + omS*ow + omW0 (the phases of a strided
+  // convolution's input gradient, written interleaved into the full tensor)
+  int om, omS, omH0, omW0, omW, omHW;
 };
 
 // q = n / d, r = n - q*d for 0 <= n < 2^24 via a float reciprocal and one
@@ -79,7 +89,8 @@ __device__ __forceinline__ int fdivmod(int n, int d, float inv_d, int& r) {
   return q;
 }
 
-// padded pixel index (b*Hp + oh)*Wp + ow of output pixel m (any H, W)
+// padded pixel index (b*Hp + S*oh)*Wp + S*ow of tap (0, 0) of output pixel m
+// (any H, W; pow2 addressing only ever runs with S == 1)
 __device__ __forceinline__ int out_pix(const ConvGeom& g, int m) {
   if (g.pow2) {
     const int b = m >> g.logHW, rem = m & ((1 << g.logHW) - 1);
@@ -88,7 +99,23 @@ __device__ __forceinline__ int out_pix(const ConvGeom& g, int m) {
   int rem, ow;
   const int b = fdivmod(m, g.H * g.W, g.inv_HW, rem);
   const int oh = fdivmod(rem, g.W, g.inv_W, ow);
-  return (b * g.Hp + oh) * g.Wp + ow;
+  return (b * g.Hp + g.S * oh) * g.Wp + g.S * ow;
+}
+
+// wgrad with a separate dy geometry (g.dsep): interior pixel of output m in dy
+__device__ __forceinline__ int dy_pix(const ConvGeom& g, int m) {
+  int rem, ow;
+  const int b = fdivmod(m, g.H * g.W, g.inv_HW, rem);
+  const int oh = fdivmod(rem, g.W, g.inv_W, ow);
+  return (b * g.dHp + oh + g.dpad) * g.dWp + ow + g.dpad;
+}
+
+// epilogue row of output pixel m under the output map (g.om)
+__device__ __forceinline__ int om_row(const ConvGeom& g, int m) {
+  int rem, ow;
+  const int b = fdivmod(m, g.H * g.W, g.inv_HW, rem);
+  const int oh = fdivmod(rem, g.W, g.inv_W, ow);
+  return b * g.omHW + (g.omS * oh + g.omH0) * g.omW + g.omS * ow + g.omW0;
 }
 
 // K steps (64 channels of one tap) of a position-major tile at output pixel
@@ -120,6 +147,9 @@ static ConvGeom make_geom(int B, int H, int W, int Cin, int Cout, int KS) {
   g.mmajor = 0;
   g.pm_kmax = 0;
   g.pm_P = 0;
+  g.S = 1; g.KH = KS; g.KW = KS;
+  g.dsep = 0; g.dHp = g.Hp; g.dWp = g.Wp; g.dpad = g.pad;
+  g.om = 0; g.omS = 1; g.omH0 = 0; g.omW0 = 0; g.omW = W; g.omHW = H * W;
   g.logW = g.pow2 ? ilog2_exact(W, "W") : 0;
   g.logHW = g.pow2 ? ilog2_exact(H * W, "H*W") : 0;
   g.inv_HW = 1.0f / (float)(H * W);
@@ -255,7 +285,9 @@ __device__ __forceinline__ void conv_fwd_epilogue(const f32x4 (&acc)[BM / WM / 1
                                                   float* __restrict__ slab, int split, int tm, int m0, int n0,
                                                   char* smem, int pm_b0 = 0, int pm_pos = 0) {
   // position-major tiles (g.posm): logical row ml -> stored row (pm_b0 + ml - m0) * HW + pm_pos
-  auto phys = [&](int ml) { return g.posm ? (pm_b0 + ml - m0) * (g.H * g.W) + pm_pos : ml; };
+  auto phys = [&](int ml) {
+    return g.posm ? (pm_b0 + ml - m0) * (g.H * g.W) + pm_pos : (g.om ? om_row(g, ml) : ml);
+  };
   constexpr int NT = 64 * WM * WN, TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = tid >> 6, wm = wid / WN, wn = wid % WN;
@@ -372,7 +404,7 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
     const int ml = m0 + wm * TM + a * 16 + (lane & 15);
     const bool ok = ml < g.M;
     // stored row: position-major tiles hold image pm_b0 + r at output pixel pm_pos
-    const int m = g.posm ? (pm_b0 + ml - m0) * (g.H * g.W) + pm_pos : ml;
+    const int m = g.posm ? (pm_b0 + ml - m0) * (g.H * g.W) + pm_pos : (g.om && ok ? om_row(g, ml) : ml);
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
       const int n = n0 + nl + 32 * q;
@@ -575,14 +607,14 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
     } else {
       const int k0 = kt_beg * BK;
       const int kpos = k0 >> (g.logC8 + 3);
-      kh = kpos / g.KS;
-      kw = kpos - kh * g.KS;
+      kh = kpos / g.KW;
+      kw = kpos - kh * g.KW;
       tnext.c0 = k0 & (g.Cin - 1);
     }
     tnext.kw = kw;
     tnext.kh = kh;
     tnext.off = (kh * g.Wp + kw) * g.Cin + tnext.c0;
-    tnext.wk = (kh * g.KS + kw) * g.Cin + tnext.c0;
+    tnext.wk = (kh * g.KW + kw) * g.Cin + tnext.c0;
   }
   auto tap_advance = [&](Tap& t) {
     if constexpr (TAPU) {
@@ -595,9 +627,9 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
           if (++t.kw == kw1) { t.kw = kw0; ++t.kh; }
           t.off = (t.kh * g.Wp + t.kw) * g.Cin;
           t.wk = (t.kh * g.KS + t.kw) * g.Cin;
-        } else if (++t.kw == g.KS) {
+        } else if (++t.kw == g.KW) {
           t.kw = 0;
-          t.off += (g.Wp - g.KS) * g.Cin;
+          t.off += (g.Wp - g.KW) * g.Cin;
         }
       }
     }
@@ -616,7 +648,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
         const int kc = kt * CPR + a_ch[j];
         const int kpos = kc >> g.logC8;
         const int c0 = (kc & (C8 - 1)) << 3;
-        const int kh = kpos / g.KS, kw = kpos - kh * g.KS;
+        const int kh = kpos / g.KW, kw = kpos - kh * g.KW;
         const unsigned off = kc < g.Kch ? 2u * (unsigned)(a_base[j] + (kh * g.Wp + kw) * g.Cin + c0) : kOOB;
         blds16(xr, off, 0u, sA + (wid * A_INS + j) * 1024);
       }
@@ -1188,7 +1220,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
     const int row = A_RPI * (wid * A_INS + j) + lane / ACPR;
     a_row[j] = row;
     const int ch = swz_tr<ACPR>(row, lane % ACPR) - row * ACPR;  // logical chunk (involution)
-    a_off[j] = (lane_pix(row) + g.pad * g.Wp + g.pad) * g.Cout + co0 + ch * 8;
+    a_off[j] = (lane_pix(row) + (g.dsep ? 0 : g.pad * g.Wp + g.pad)) * g.Cout + co0 + ch * 8;
   }
   // B (im2col of x) lanes: chunk -> fixed tap (kh, kw, c0)
   int b_off[B_INS], b_row[B_INS];
@@ -1201,10 +1233,10 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
     const int kc = k0 / 8 + ch;
     b_kok[j] = kc < g.Kch;
     const int kpos = kc >> g.logC8;
-    const int kh = kpos / g.KS, kw = kpos - kh * g.KS;
+    const int kh = kpos / g.KW, kw = kpos - kh * g.KW;
     b_off[j] = (lane_pix(row) + kh * g.Wp + kw) * g.Cin + ((kc & (C8 - 1)) << 3);
   }
-  const rsrc_t dyr = make_rsrc(dy, (unsigned)((int64_t)g.B * g.Hp * g.Wp * g.Cout * 2));
+  const rsrc_t dyr = make_rsrc(dy, (unsigned)((int64_t)g.B * g.dHp * g.dWp * g.Cout * 2));
   const rsrc_t xr = make_rsrc(x, (unsigned)((int64_t)g.B * g.Hp * g.Wp * g.Cin * 2));
   unsigned a_v[A_INS], b_v[B_INS];  // per-lane byte offsets (K-tail lanes: out of range -> zeros)
 #pragma unroll
@@ -1233,7 +1265,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
 #pragma unroll
       for (int j = 0; j < A_INS; ++j) {
         const bool ok = a_row[j] < left;
-        const int px = out_pix(g, ok ? ms + a_row[j] : 0);
+        const int mr = ok ? ms + a_row[j] : 0;
+        const int px = g.dsep ? dy_pix(g, mr) : out_pix(g, mr);
         blds16(dyr, ok ? a_v[j] + 2u * (unsigned)(px * g.Cout) : kOOB, 0u, sA + (wid * A_INS + j) * 1024);
       }
 #pragma unroll
@@ -1357,7 +1390,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
 
   const int col_l = lane & 15, rq = lane >> 4;
   if constexpr (ATOM) {
-    const int logCin = g.logC8 + 3, taps = g.KS * g.KS;
+    const int logCin = g.logC8 + 3, taps = g.KH * g.KW;
 #pragma unroll
     for (int a = 0; a < FM; ++a)
 #pragma unroll
@@ -1758,6 +1791,7 @@ int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile,
 
 static uintptr_t g_fwd_addend = 0;  // conv_fwd_add: bf16 [M][Cout] added in the epilogue
 static int g_fwd_slab_cap = 0;      // split-K slab capacity of the current conv_fwd call (FwdCfg)
+static int g_fwd_keep_slabs = 0;    // FwdCfg bit 20: leave the split-K slabs (the caller combines them)
 // A/B knob: 0 = the untransposed accumulator layout for the split-K and BN-statistics
 // instances of the streaming kernel (set_conv_fwd_tr)
 static int g_fwd_tr = 1;
@@ -1807,7 +1841,8 @@ static void plan_posm_balance(ConvGeom& g, int BM, int ntn, int splits, int cap)
 template <int BM, int BN, bool TAPU, int ST, int WM, int WN>
 static void launch_fwd_w(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
                          uintptr_t slab, int splits, hipStream_t s) {
-  g.posm = (g_posm && TAPU && !g_fwd_addend && g.B % BM == 0 && (g.H < g.KS || g.W < g.KS)) ? 1 : 0;
+  g.posm = (g_posm && TAPU && !g_fwd_addend && g.B % BM == 0 && (g.H < g.KS || g.W < g.KS) && g.S == 1 && !g.om &&
+            g.KH == g.KS && g.KW == g.KS && g.Hp == g.H + 2 * g.pad && g.Wp == g.W + 2 * g.pad) ? 1 : 0;
   const int ntm = (g.M + BM - 1) / BM, ntn = (g.Cout + BN - 1) / BN;
   plan_posm_balance(g, BM, ntn, splits, g_fwd_slab_cap);
   const int nkt = (g.Kch + 7) / 8;
@@ -1847,18 +1882,22 @@ static int g_fwd_stages = 3, g_wgrad_stages = 0;  // tuning knobs (set_conv_stag
 // bits 12-19: the slab's capacity in K splits (0 = exactly `splits`); a larger
 // capacity lets a position-major layer use the balanced split-K plan
 // (g_fwd_slab_cap, declared with g_fwd_addend).
+// bit 20: keep the split-K slabs -- no combine launch; the consumer sums them
+// (bn_pool.hip combine_bwd_reduce: a dgrad's combine fused with the BN
+// backward reduce of the block below).
 struct FwdCfg {
   int saved_st, saved_wv;
   explicit FwdCfg(int& tile) : saved_st(g_fwd_stages), saved_wv(g_fwd_waves) {
     const int st = (tile >> 4) & 15, wv = (tile >> 8) & 15;
     g_fwd_slab_cap = (tile >> 12) & 255;
+    g_fwd_keep_slabs = (tile >> 20) & 1;
     tile &= 15;
     if (st && (st < 2 || st > 4)) throw std::runtime_error("conv_fwd: packed stages must be 2..4");
     if (wv && wv != 4 && wv != 8) throw std::runtime_error("conv_fwd: packed waves must be 4 or 8");
     if (st) g_fwd_stages = st;
     if (wv) g_fwd_waves = wv;
   }
-  ~FwdCfg() { g_fwd_stages = saved_st; g_fwd_waves = saved_wv; g_fwd_slab_cap = 0; }
+  ~FwdCfg() { g_fwd_stages = saved_st; g_fwd_waves = saved_wv; g_fwd_slab_cap = 0; g_fwd_keep_slabs = 0; }
 };
 
 template <int BM, int BN, bool TAPU, int ST>
@@ -2085,6 +2124,10 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
   else throw std::runtime_error("conv_fwd: bad tile id");
   DL_HIP_CHECK(hipGetLastError());
   if (splits == 1) return (g.M + fwd_bm(tile) - 1) / fwd_bm(tile);
+  if (g_fwd_keep_slabs) {
+    if (stats || g.pm_kmax > 0) throw std::runtime_error("conv_fwd keep-slabs: no statistics / balanced split-K");
+    return 0;
+  }
   if (256 % (Cout / 8) != 0) throw std::runtime_error("conv_fwd split-K combine: Cout/8 must divide 256");
   const int rpb = combine_rows_per_block(g.M, Cout);
   const int nb = (g.M + rpb - 1) / rpb;
@@ -2122,6 +2165,79 @@ void conv_fwd_add(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t addend, int B
   DL_HIP_CHECK(hipGetLastError());
 }
 
+// ---- generalised geometry (strided / KH x KW / phase-mapped convolutions) ----
+// The ResNet-50 convolutions that are not stride-1 odd-square: the stride-2
+// 1x1 downsample and 3x3 convs, the stem (a stride-2 7x7 over 3 channels,
+// rewritten as a 4x4 stride-1 conv over its 2x2 space-to-depth image: 12 -> 16
+// channels), and the stride-2 convs' input gradients (one phase conv per
+// output parity, stored interleaved through the epilogue's output map).
+// Streaming forward kernel and wgrad kernel only, float-reciprocal pixel
+// addressing (never the pow2 / region / c8 paths).
+static ConvGeom make_geom_ex(int B, int Ho, int Wo, int Hp, int Wp, int Cin, int Cout, int KH, int KW, int S) {
+  if (KH < 1 || KW < 1 || S < 1) throw std::runtime_error("conv_ex: bad kernel / stride");
+  if (Hp < S * (Ho - 1) + KH || Wp < S * (Wo - 1) + KW) throw std::runtime_error("conv_ex: input buffer too small");
+  ConvGeom g = make_geom(B, Ho, Wo, Cin, Cout, 1);
+  g.KS = std::max(KH, KW);
+  g.pad = 0;
+  g.Hp = Hp; g.Wp = Wp;
+  g.S = S; g.KH = KH; g.KW = KW;
+  g.dHp = Ho; g.dWp = Wo; g.dpad = 0;
+  g.pow2 = 0;
+  g.K = KH * KW * Cin;
+  g.Kch = g.K / 8;
+  if ((int64_t)B * Ho * Wo >= (1 << 24)) throw std::runtime_error("conv_ex: B*Ho*Wo must be < 2^24");
+  if ((int64_t)B * Hp * Wp * std::max(Cin, Cout) >= (1ll << 31) || (int64_t)Cout * g.K >= (1ll << 31))
+    throw std::runtime_error("conv_ex: operand too large for 32-bit offsets");
+  return g;
+}
+
+// y[om(m)] = conv(x, w)[m] (+ addend[om(m)] when addend != 0: an in-place
+// accumulate when addend == y) with the generalised geometry; om_S == 0: no
+// output map.  Returns the number of BN statistics rows (stats != 0, no split).
+int conv_fwd_ex(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab, int B, int Ho, int Wo, int Hp,
+                int Wp, int Cin, int Cout, int KH, int KW, int S, int om_S, int om_H0, int om_W0, int om_W, int om_HW,
+                uintptr_t addend, int tile, int splits, uintptr_t stream) {
+  const FwdCfg cfg(tile);
+  ConvGeom g = make_geom_ex(B, Ho, Wo, Hp, Wp, Cin, Cout, KH, KW, S);
+  if (om_S > 0) {
+    g.om = 1; g.omS = om_S; g.omH0 = om_H0; g.omW0 = om_W0; g.omW = om_W; g.omHW = om_HW;
+    if ((int64_t)B * om_HW * std::max(Cin, Cout) >= (1ll << 31)) throw std::runtime_error("conv_fwd_ex: output too large");
+  }
+  hipStream_t s = as_stream(stream);
+  if (splits < 1) splits = 1;
+  if (splits > 1 && (!slab || addend || g.om)) throw std::runtime_error("conv_fwd_ex: split-K needs a slab, no addend / map");
+  if (stats && (addend || splits > 1)) throw std::runtime_error("conv_fwd_ex: statistics need a plain, unsplit output");
+  if (Cin % 8 != 0 || (Cin < 64 && Cin % 8 != 0)) throw std::runtime_error("conv_fwd_ex: Cin % 8 != 0");
+  if (Cin >= 64 && Cin % 64 != 0) throw std::runtime_error("conv_fwd_ex: Cin >= 64 must be a multiple of 64");
+  if (tile < 0 || tile > 2) throw std::runtime_error("conv_fwd_ex: bad tile id");
+  if (Cout % fwd_bn(tile) != 0) throw std::runtime_error("conv_fwd_ex: Cout must be a multiple of the N tile");
+  g_fwd_addend = addend;
+  try {
+    if (tile == 0) launch_fwd<128, 128>(g, x, w, y, stats, slab, splits, s);
+    else if (tile == 1) launch_fwd<64, 64>(g, x, w, y, stats, slab, splits, s);
+    else launch_fwd<128, 64>(g, x, w, y, stats, slab, splits, s);
+  } catch (...) {
+    g_fwd_addend = 0;
+    throw;
+  }
+  g_fwd_addend = 0;
+  DL_HIP_CHECK(hipGetLastError());
+  if (splits == 1) return (g.M + fwd_bm(tile) - 1) / fwd_bm(tile);
+  if (g_fwd_keep_slabs) return 0;
+  if (256 % (Cout / 8) != 0) throw std::runtime_error("conv_fwd_ex split-K combine: Cout/8 must divide 256");
+  const int rpb = combine_rows_per_block(g.M, Cout);
+  const int nb = (g.M + rpb - 1) / rpb;
+  splitk_combine_kernel<false><<<nb, 256, 0, s>>>((const float*)slab, (bf16_t*)y, nullptr, splits, g.M, Cout, rpb, g);
+  DL_HIP_CHECK(hipGetLastError());
+  return nb;
+}
+
+// out: fp32 [splits][Cout][ldo] weight-gradient slabs of a generalised-geometry
+// conv: x as in conv_fwd_ex, dy [B][dHp][dWp][Cout] with the output interior at dpad.
+void conv_wgrad_ex(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int Ho, int Wo, int Hp, int Wp, int dHp, int dWp,
+                   int dpad, int Cin, int Cout, int KH, int KW, int S, int splits, int ldo, int tile,
+                   uintptr_t stream);
+
 // out: fp32 [splits][Cout][ldo], ldo >= K (K = KS*KS*Cin); tile 0 = 128x64, 1 = 64x64 (co x k)
 // atomic_creal > 0: every split atomically adds into the ZEROED fp32 gradient
 // out = [Cout][KS*KS][atomic_creal] (no slabs, no slab_reduce).
@@ -2129,9 +2245,27 @@ void conv_fwd_add(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t addend, int B
 static int g_wgrad_xcd = 1;
 void set_conv_wgrad_xcd(int on) { g_wgrad_xcd = on ? 1 : 0; }
 
+static void conv_wgrad_g(const ConvGeom& g, uintptr_t dy, uintptr_t x, uintptr_t out, int splits, int ldo, int tile,
+                         int atomic_creal, uintptr_t stream);
+
 void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, int Cin, int Cout, int KS, int splits,
                 int ldo, int tile, int atomic_creal, uintptr_t stream) {
-  ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
+  conv_wgrad_g(make_geom(B, H, W, Cin, Cout, KS), dy, x, out, splits, ldo, tile, atomic_creal, stream);
+}
+
+void conv_wgrad_ex(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int Ho, int Wo, int Hp, int Wp, int dHp, int dWp,
+                   int dpad, int Cin, int Cout, int KH, int KW, int S, int splits, int ldo, int tile,
+                   uintptr_t stream) {
+  ConvGeom g = make_geom_ex(B, Ho, Wo, Hp, Wp, Cin, Cout, KH, KW, S);
+  g.dsep = 1; g.dHp = dHp; g.dWp = dWp; g.dpad = dpad;
+  if (dHp < Ho + dpad || dWp < Wo + dpad) throw std::runtime_error("conv_wgrad_ex: dy buffer too small");
+  if ((int64_t)B * dHp * dWp * Cout >= (1ll << 31)) throw std::runtime_error("conv_wgrad_ex: dy too large");
+  conv_wgrad_g(g, dy, x, out, splits, ldo, tile, 0, stream);
+}
+
+static void conv_wgrad_g(const ConvGeom& g, uintptr_t dy, uintptr_t x, uintptr_t out, int splits, int ldo, int tile,
+                         int atomic_creal, uintptr_t stream) {
+  const int Cin = g.Cin, Cout = g.Cout, W = g.W;
   if (ldo < g.K) throw std::runtime_error("conv_wgrad: ldo < K");
   if (ldo % 4 != 0) throw std::runtime_error("conv_wgrad: ldo % 4 != 0 (16-byte slab stores)");
   if (Cout % 8 != 0) throw std::runtime_error("conv_wgrad: Cout % 8 != 0");

@@ -592,6 +592,7 @@ def test_executor_merged_slab_reduce_bitwise(C, monkeypatch):
     from torch_distlearn_amd.models.cifar_hip import CifarHIPExecutor
 
     monkeypatch.setenv("DISTLEARN_REDUCE_ATOMIC", "0")
+    monkeypatch.setenv("DISTLEARN_FUSE_COMBINE", "0")  # (merge=1 turns the fused combine off for its layers)
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(5)
     x = torch.randn(64, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)
@@ -609,6 +610,39 @@ def test_executor_merged_slab_reduce_bitwise(C, monkeypatch):
         grads.append(torch.cat([v.flatten() for v in flat.views_of(flat.grad)]))
     assert torch.isfinite(grads[1]).all()
     assert torch.equal(grads[0], grads[1])
+
+
+@pytest.mark.parametrize("B,atomic", [(128, "0"), (64, "0"), (128, "2")])
+def test_executor_fused_combine_bwd_reduce(C, monkeypatch, B, atomic):
+    """A split-K dgrad's combine fused into the next BN backward reduce
+    (combine_bwd_reduce: one launch writes dP and the reduce's partial rows)
+    matches the separate combine + reduce launches to fp32 summation-order
+    noise, and is itself run-to-run deterministic in reduction mode 0."""
+    from torch_distlearn_amd import FlatParams
+    from torch_distlearn_amd.models import CifarConvNet
+    from torch_distlearn_amd.models.cifar_hip import CifarHIPExecutor
+
+    monkeypatch.setenv("DISTLEARN_REDUCE_ATOMIC", atomic)
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(6)
+    x = torch.randn(B, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)
+    y = torch.randint(0, 10, (B,), device=dev, generator=g)
+    grads = []
+    for fuse in ("0", "1", "1"):
+        monkeypatch.setenv("DISTLEARN_FUSE_COMBINE", fuse)
+        mdl = CifarConvNet(seed=4).to(dev)
+        flat = FlatParams(mdl, grads=True, shadow_bf16=True)
+        flat.grad.fill_(float("nan"))
+        ex = CifarHIPExecutor(mdl, flat, max_batch=B)
+        assert ex.fuse_combine == (fuse == "1")
+        assert any(p is not None and p[1] in (2, 4, 8) for p in ex.dgrad_plan)  # the fused path is exercised
+        ex.forward_backward(x.contiguous(), y)
+        torch.cuda.synchronize()
+        grads.append(torch.cat([v.flatten() for v in flat.views_of(flat.grad)]))
+    assert torch.isfinite(grads[1]).all()
+    assert float((grads[0] - grads[1]).norm() / grads[0].norm()) < (1e-3 if atomic == "0" else 1e-2)
+    if atomic == "0":
+        assert torch.equal(grads[1], grads[2])
 
 
 # (B, H, Cin, Cout, tile, splits): position-major tiles (batch a multiple of the

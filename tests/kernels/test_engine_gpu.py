@@ -175,18 +175,57 @@ def test_device_loader_graph_matches_eager(dev):
     assert float((tr.flat.data - p1).abs().max()) < 1e-3
 
 
-def _run(args, timeout=600):
-    env = dict(os.environ, PYTHONPATH=ROOT)
+def _run(args, timeout=600, env=None):
+    env = dict(os.environ, PYTHONPATH=ROOT, **(env or {}))
     r = subprocess.run([sys.executable] + args, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     return r.stdout
 
 
 def test_cifar10_example_cuda(dev):
-    out = _run(["-m", "torch_distlearn_amd.launch", "--nproc", "1", "--gpus", "examples/cifar10.py", "--epochs", "1",
+    out = _run(["-m", "torch_distlearn_amd.launch", "--nproc", "1", "--gpus", "examples/cifar10.py", "--epochs", "2",
                 "--maxSteps", "20", "--batchSize", "64", "--trainSize", "2048", "--testSize", "256",
                 "--learningRate", "0.05"])
     assert "test accuracy" in out
+    # the reference example runs on bench.py's path: device sampler + unrolled graph
+    # replays, every capture made before the first epoch (same count after epoch 2)
+    eps = [ln for ln in out.splitlines() if ln.startswith("Epoch") and "img/s" in ln]
+    assert len(eps) == 2 and all("unrolled hipGraphs x16" in ln for ln in eps), eps
+    assert eps[0].split("x16, ")[1] == eps[1].split("x16, ")[1]
+
+
+def test_cifar10_example_resume_bitwise_mode0(dev, tmp_path):
+    """The CIFAR-10 example on the HIP fast path (unrolled graphs, device
+    sampler) in the deterministic reduction mode 0: 2 epochs straight ==
+    1 epoch + --save, then a fresh process --resume + epoch 2, BITWISE.
+    (Mode 2, the default, accumulates BN statistics with fp32 atomics: not
+    run-to-run reproducible, so a resumed run matches only statistically.)"""
+    root = str(tmp_path)
+    common = ["-m", "torch_distlearn_amd.launch", "--nproc", "1", "--gpus", "examples/cifar10.py", "--maxSteps", "19",
+              "--batchSize", "32", "--trainSize", "1024", "--testSize", "64", "--resultsRoot", root]
+    env = {"DISTLEARN_REDUCE_ATOMIC": "0"}
+    _run(common + ["--epochs", "2", "--save", "straight"], env=env)
+    _run(common + ["--epochs", "1", "--save", "split"], env=env)
+    out = _run(common + ["--epochs", "2", "--save", "split", "--resume"], env=env)
+    assert "resumed from" in out
+    a = torch.load(os.path.join(root, "straight", "Net"), weights_only=True)
+    b = torch.load(os.path.join(root, "split", "Net"), weights_only=True)
+    assert len(a) == len(b) > 0
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
+def test_cifar10_example_confusion_counts_every_sample(dev):
+    """The captured confusion-matrix hook sees every training sample exactly
+    once per step (steps x per-node batch entries per epoch)."""
+    import re
+
+    out = _run(["-m", "torch_distlearn_amd.launch", "--nproc", "1", "--gpus", "examples/cifar10.py", "--epochs", "1",
+                "--maxSteps", "37", "--batchSize", "32", "--trainSize", "4096", "--testSize", "64"])
+    rows = [ln for ln in out.split("Epoch 1: train loss")[1].split("Epoch 1: test")[0].splitlines()
+            if ln.strip().startswith(("[[", "["))]
+    total = sum(sum(int(v) for v in re.findall(r"\d+", ln.split("]")[0])) for ln in rows)
+    assert total == 37 * 32, (total, rows)
 
 
 def test_mnist_examples_cuda(dev):
@@ -302,7 +341,8 @@ def test_bf16_grad_wire_through_rccl(dev, monkeypatch):
     """grad_comm_dtype="bf16" (world-1 collectives forced through RCCL, inside
     the captured graph): the bucket all-reduces move half the bytes, the fp32
     participation count rides in the same group, and the update (the fused
-    SGD reading the bf16 wire copy) matches the fp32 wire to bf16 tolerance."""
+    SGD reading the bf16 wire copy) matches the fp32 wire to bf16 tolerance
+    (one step from the same state: later steps add chaotic training drift)."""
     monkeypatch.setenv("DISTLEARN_RCCL_WORLD1", "1")
     g = torch.Generator(device=dev).manual_seed(4)
     xs = torch.randn(3, 32, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)
@@ -312,14 +352,18 @@ def test_bf16_grad_wire_through_rccl(dev, monkeypatch):
         tr = _trainer(dev, "hip", True, 29707, grad_comm_dtype=wire)
         assert tr.grad_comm_dtype == wire
         before = tr.flat.data.clone()
-        for i in range(3):
-            tr.step(xs[i], ys[i])
+        tr.step(xs[0], ys[0])
         torch.cuda.synchronize()
         assert float(tr.flat.slot) == 1.0
+        delta = tr.flat.data - before
+        for i in range(1, 3):  # keeps training (replays) with the wire
+            tr.step(xs[i], ys[i])
+        torch.cuda.synchronize()
+        assert bool(torch.isfinite(tr.flat.data).all())
         ld = _loader(dev, batch=16)
         st = tr.comm_profile(ld, steps=2)
-        res[wire] = (tr.flat.data - before, st["bytes_per_step"])
+        res[wire] = (delta, st["bytes_per_step"])
     (d32, b32), (d16, b16) = res["fp32"], res["bf16"]
     assert b16 * 2 == b32
     rel = float((d16 - d32).norm() / d32.norm())
-    assert rel < 0.05, rel
+    assert rel < 0.01, rel

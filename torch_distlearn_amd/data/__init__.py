@@ -243,6 +243,21 @@ class DeviceLoader:
 
     num_batches = numBatches
 
+    @property
+    def drawn(self) -> int:
+        """Batches consumed so far (checkpointed: a resumed run continues the stream)."""
+        return self.epoch * self.steps_per_epoch + self._host_steps
+
+    def skip(self, nbatches: int) -> None:
+        """Advance the sample stream by ``nbatches`` batches (resume)."""
+        n = int(nbatches)
+        while n >= self.steps_per_epoch - self._host_steps:
+            n -= self.steps_per_epoch - self._host_steps
+            self.epoch += 1
+            self._fill_epoch()
+        self._host_steps += n
+        self.ctr[0] = self._host_steps
+
     def gather_args(self):
         ds = self.ds
         return (ds.images.data_ptr(), self.order.data_ptr(), ds.labels.data_ptr(), self.labels_out.data_ptr(),

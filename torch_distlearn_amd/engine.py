@@ -100,15 +100,24 @@ class DataParallelTrainer:
         self.captures = 0    # hipGraph captures so far (none may happen in a timed region)
         self.last_loss: Optional[torch.Tensor] = None
         self.steps = 0
+        # callables hook(logits, labels) run INSIDE every step body, after the
+        # backward (so they are captured into the step's hipGraphs): e.g. the
+        # examples' every-sample training confusion matrix (one GPU kernel)
+        self.step_hooks: list = []
 
     # ------------------------------------------------------------------
     def _forward_backward(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         if self.executor is not None:
             return self.executor.forward_backward(x, y)
         self.model.train()
-        logp = self.model(x, compute_dtype=self.compute_dtype)
+        fused = getattr(self.model, "forward_loss", None)
+        out = fused(x, y, compute_dtype=self.compute_dtype) if (fused is not None and x.is_cuda) else None
+        if out is not None:  # the model computes its loss (and the head's backward) itself
+            loss, logp = out
+        else:
+            logp = self.model(x, compute_dtype=self.compute_dtype)
+            loss = self.loss_fn(logp, y)
         self._last_logp = logp.detach()
-        loss = self.loss_fn(logp, y)
         loss.backward()
         return loss.detach()
 
@@ -122,6 +131,10 @@ class DataParallelTrainer:
         if not getattr(self.executor, "overwrites_grads", False):
             fill_(f.grad, 0.0, slot_value=1.0)
         loss = self._forward_backward(x, y)
+        if self.step_hooks:
+            labels = x.labels_out if hasattr(x, "gather_args") else y
+            for h in self.step_hooks:
+                h(self.last_logits(), labels)
         if self.algo == "sgd":
             self.sgd.step(f, self.lr, momentum=self.momentum, weight_decay=self.weight_decay,
                           momentum_buf=self.mom)

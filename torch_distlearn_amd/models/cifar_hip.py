@@ -219,6 +219,10 @@ class CifarHIPExecutor:
         # the reduce's LDS / VGPR footprint): 0.3634 vs 0.3506 ms/step
         # (profiles/r2_merge_slab_ab.txt)
         self.merge_slab = os.environ.get("DISTLEARN_MERGE_SLAB", "0") == "1"
+        # a split-K dgrad's combine runs inside the BN backward reduce of the block
+        # below (csrc bn_pool.hip combine_bwd_reduce): dP is produced, stored and
+        # reduced by one launch (DISTLEARN_FUSE_COMBINE=0: separate kernels, A/B)
+        self.fuse_combine = os.environ.get("DISTLEARN_FUSE_COMBINE", "1") == "1"
         self.atomic = self.mode > 0             # BN statistics / gradients by atomics, no finalize kernels
         self.atomic_wgrad = self.mode == 1      # split-K weight gradients by atomics (else slabs)
         self.rows = {0: 0, 1: 1, 2: int(os.environ.get("DISTLEARN_REDUCE_ROWS", "16"))}[self.mode]
@@ -276,7 +280,10 @@ class CifarHIPExecutor:
                 self.stats.append(torch.empty(rows, 2, cout, device=d))
             g = C.bn_bwd_blocks(B, h, h, cout)
             self.bwd_blocks.append(g)
-            self.bwd_part.append(None if self.atomic else torch.empty(g, 2, cout, device=d))
+            # (mode 0) partial rows of the BN backward reduce -- or of the fused
+            # split-K combine + reduce, which writes one row per combine block
+            gp = max(g, C.combine_bwd_reduce_blocks(B, h, h, cout)) if i + 1 < self.nb else g
+            self.bwd_part.append(None if self.atomic else torch.empty(gp, 2, cout, device=d))
             tile_w, splits_w = _wgrad_plan(cout, K, M, self.cu_reserve)
             direct = splits_w == 1 and cin == self.cins_real[i]
             self.wplan.append((tile_w, splits_w, direct))
@@ -451,7 +458,9 @@ class CifarHIPExecutor:
         side_pending = False
         merge = self.merge_slab and not (self.side_wgrad or self.side_reduce)
         pending = None  # (slab args, block) of a weight gradient whose slab reduce rides the next BN reduce
+        dp_splits = 0   # > 0: dP[i] is still in the split-K slabs of block i+1's dgrad (fused combine)
         for i in reversed(range(self.nb)):
+            T = self.bwd_blocks[i]  # partial rows written by this block's backward reduce
             h, cin, cout = self.hs[i], self.cins[i], self.couts[i]
             M = B * h * h
             G = self.bwd_blocks[i]
@@ -465,6 +474,12 @@ class CifarHIPExecutor:
                                      part.data_ptr(), B, h, h, cout, G, *head_args, s)
                 self._ready(nfc)
                 self._ready(nfc + 1)
+            elif dp_splits:
+                # one launch: block i+1's dgrad split-K combine (dP[i]) + this block's BN backward reduce
+                T = C.combine_bwd_reduce(self.slabs.data_ptr(), dp_splits, self.dP[i].data_ptr(),
+                                         self.y[i].data_ptr(), self.coef[i].data_ptr(), part.data_ptr(), B, h, h, cout,
+                                         s)
+                dp_splits = 0
             elif pending is not None:
                 # one launch: this block's BN backward reduce + block i+1's weight-gradient slab reduce
                 sargs, blk = pending
@@ -483,7 +498,7 @@ class CifarHIPExecutor:
                                               part.data_ptr(), self.p32[self._leaf(i, 2)].data_ptr(), M,
                                               dY.data_ptr(), B, h, h, cout, SPAD, dgo, dbo, s)
             else:
-                C.bn_bwd_finalize(self.bwd_part[i].data_ptr(), G, cout, M, self.p32[self._leaf(i, 2)].data_ptr(),
+                C.bn_bwd_finalize(self.bwd_part[i].data_ptr(), T, cout, M, self.p32[self._leaf(i, 2)].data_ptr(),
                                   self.coef[i].data_ptr(), self.g32[self._leaf(i, 2)].data_ptr(),
                                   self.g32[self._leaf(i, 3)].data_ptr(), self.acoef[i].data_ptr(), s)
                 C.bn_relu_pool_bwd_apply(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
@@ -530,8 +545,11 @@ class CifarHIPExecutor:
                 dt, ds = self.dgrad_plan[i]
                 if self.dgrad_stages != 3:
                     C.set_conv_stages(self.dgrad_stages, self._wgrad_stages)
+                keep = self.fuse_combine and ds in (2, 4, 8) and not (merge and pending is not None)
                 C.conv_fwd(dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), 0,
-                           self.slabs.data_ptr(), B, h, h, cout, cin, KSIZE, dt | _slab_cap_bits(ds), ds, s)
+                           self.slabs.data_ptr(), B, h, h, cout, cin, KSIZE,
+                           dt | _slab_cap_bits(ds) | ((1 << 20) if keep else 0), ds, s)
+                dp_splits = ds if keep else 0
                 if self.dgrad_stages != 3:
                     C.set_conv_stages(3, self._wgrad_stages)
         if self.side_wgrad or self.side_reduce:

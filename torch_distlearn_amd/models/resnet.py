@@ -100,6 +100,12 @@ _CONV3_MAX_HW = int(os.environ.get("DISTLEARN_RESNET_CONV3_MAX_HW", "56"))
 _CL_WEIGHTS = os.environ.get("DISTLEARN_RESNET_CL_WEIGHTS", "1") == "1"
 # stem max-pool on the HIP gather-backward kernels (ops/pool.py)
 _POOL_HIP = os.environ.get("DISTLEARN_RESNET_POOL", "hip") == "hip"
+# stride-2 1x1 / 3x3 convolutions and the stem on the generalised MFMA kernels
+# (ops/conv.py Conv1x1S2 / Conv3x3S2 / StemConv; 0 = MIOpen, A/B)
+_STRIDED_HIP = os.environ.get("DISTLEARN_RESNET_STRIDED", "1") == "1"
+# classifier (mean + Linear + LogSoftMax + NLL, forward and backward) in one node on the
+# MFMA kernels (ops/head.py; 0 = torch mean / hipBLAS linear / torch log-softmax)
+_HEAD_HIP = os.environ.get("DISTLEARN_RESNET_HEAD", "hip") == "hip"
 
 
 class _Conv(nn.Module):
@@ -112,11 +118,28 @@ class _Conv(nn.Module):
 
     def hip_gemm(self, x) -> bool:
         """Stride-1 1x1 convolution on the hand-written MFMA GEMM kernels."""
-        if self.bind is None or not x.is_cuda or x.dtype != torch.bfloat16 or not torch.is_grad_enabled():
+        if self.bind is None or not x.is_cuda or x.dtype != torch.bfloat16:
             return False
         from ..ops.conv import conv1x1_supported
 
         return _CONV_MODE == "hip" and self.k == 1 and self.stride == 1 and conv1x1_supported(x, self.weight.shape[0])
+
+    def hip_strided(self, x, shape=None) -> bool:
+        """The stride-2 1x1 / 3x3 convolutions and the 7x7 stem on the
+        generalised MFMA kernels (ops/conv.py Conv1x1S2 / Conv3x3S2 / StemConv)."""
+        shape = tuple(x.shape) if shape is None else shape
+        if (self.bind is None or not x.is_cuda or x.dtype != torch.bfloat16 or _CONV_MODE != "hip"
+                or not _STRIDED_HIP or self.stride != 2):
+            return False
+        n, cin, h, w = shape
+        cout = self.weight.shape[0]
+        pow2 = lambda v: v >= 64 and (v & (v - 1)) == 0  # noqa: E731
+        if self.k == 7:
+            return cin == 3 and cout % 64 == 0
+        if self.k == 3:
+            return (self.bind.wcl is not None and pow2(cin) and pow2(cout) and h % 2 == 0 and w % 2 == 0
+                    and n * (h + 2) * (w + 2) * max(cin, cout) < (1 << 31))
+        return self.k == 1 and pow2(cin) and pow2(cout) and n * h * w * max(cin, cout) < (1 << 31)
 
     def hip_3x3(self, x, shape=None) -> bool:
         """Stride-1 3x3 convolution on the hand-written kernels (needs the
@@ -124,8 +147,7 @@ class _Conv(nn.Module):
         (device / dtype) of ``shape`` (default x.shape)."""
         shape = tuple(x.shape) if shape is None else shape
         if (self.bind is None or self.bind.wcl is None or self.k != 3 or self.stride != 1 or not x.is_cuda
-                or x.dtype != torch.bfloat16 or not torch.is_grad_enabled() or _CONV_MODE != "hip"
-                or shape[2] > _CONV3_MAX_HW):
+                or x.dtype != torch.bfloat16 or _CONV_MODE != "hip" or shape[2] > _CONV3_MAX_HW):
             return False
         from ..ops.conv import conv3x3_supported
 
@@ -142,15 +164,26 @@ class _Conv(nn.Module):
             return F.conv2d(x, self.weight.to(x.dtype), None, self.stride, self.pad)
         from ..ops.conv import Conv1x1, ShadowConv
 
-        if not torch.is_grad_enabled():
-            w = b.wcl if b.wcl is not None else b.w16.view(self.weight.shape)
-            return F.conv2d(x, w, None, self.stride, self.pad)
+        # the same HIP kernels in training and in eval / predict (no-grad) mode
         if self.hip_gemm(x):
-            return Conv1x1.apply(x, self.weight, b, stats, res_link, dx_sink)
+            return Conv1x1.apply(x, self.weight, b, stats, res_link if torch.is_grad_enabled() else None,
+                                 dx_sink if torch.is_grad_enabled() else None)
         if self.hip_3x3(x) and dx_sink is None:
             from ..ops.conv import Conv3x3
 
             return Conv3x3.apply(x, self.weight, b, stats)
+        if self.hip_strided(x):
+            from ..ops.conv import Conv1x1S2, Conv3x3S2, StemConv
+
+            if self.k == 7:
+                return StemConv.apply(x, self.weight, b, stats)
+            if self.k == 3 and dx_sink is None:
+                return Conv3x3S2.apply(x, self.weight, b, stats)
+            if self.k == 1:
+                return Conv1x1S2.apply(x, self.weight, b, stats, dx_sink if torch.is_grad_enabled() else None)
+        if not torch.is_grad_enabled():
+            w = b.wcl if b.wcl is not None else b.w16.view(self.weight.shape)
+            return F.conv2d(x, w, None, self.stride, self.pad)
         return ShadowConv.apply(x, self.weight, b, self.stride, self.pad, dx_sink)
 
 
@@ -162,7 +195,8 @@ def _conv_bn(conv: _Conv, bn: "_BN", x, relu: bool = True, residual=None, link=N
     its output / input gradient zero-bordered (for a Conv3x3 neighbour)."""
     kw = {"res_link": link, "dx_sink": dx_sink} if conv.bind is not None else {}
     pads = {"out_pad": out_pad, "dx_pad": dx_pad}
-    if _FUSE_STATS and (conv.hip_gemm(x) or conv.hip_3x3(x)) and _BN_MODE == "hip" and bn.training:
+    if _FUSE_STATS and (conv.hip_gemm(x) or conv.hip_3x3(x) or conv.hip_strided(x)) and _BN_MODE == "hip" \
+            and bn.training:
         from .._native import native
 
         if native().reduce_atomic() == 0:  # partial-row statistics (deterministic)
@@ -197,7 +231,8 @@ class _Bottleneck(nn.Module):
         # a stride-1 3x3 c2 on the HIP kernels reads b1's output and b2's input
         # gradient zero-bordered, written so by the BatchNorm kernels themselves
         n, _, h, w = x.shape  # c1 is 1x1 stride 1: c2's input is [n, width, h, w]
-        pad = 1 if self.c2.hip_3x3(x, (n, self.c2.weight.shape[1], h, w)) else 0
+        c2in = (n, self.c2.weight.shape[1], h, w)
+        pad = 1 if (self.c2.hip_3x3(x, c2in) or (self.c2.k == 3 and self.c2.hip_strided(x, c2in))) else 0
         y = _conv_bn(self.c1, self.b1, x, link=link, out_pad=pad)
         y = _conv_bn(self.c2, self.b2, y, dx_pad=pad)
         if self.down is None:
@@ -220,9 +255,10 @@ class ResNet50(nn.Module):
         self.blocks = nn.ModuleList(blocks)
         self.fc_w = nn.Parameter(torch.randn(num_classes, cin, generator=g) * (1.0 / cin) ** 0.5)
         self.fc_b = nn.Parameter(torch.zeros(num_classes))
+        self._fc_bind = None  # (fc_w grad view, fc_b grad view, ready) -- attach_flat
 
-    def forward(self, x: torch.Tensor, compute_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
-        """x: NHWC [B, H, W, 3] (or NCHW); returns log-probabilities (fp32)."""
+    def trunk(self, x: torch.Tensor, compute_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+        """Stem + max-pool + the 16 bottlenecks: [B, 2048, 7, 7] features."""
         if x.dim() == 4 and x.shape[-1] == 3:
             x = x.permute(0, 3, 1, 2)
         cd = compute_dtype or x.dtype
@@ -230,16 +266,45 @@ class ResNet50(nn.Module):
         if h.is_cuda:
             h = h.contiguous(memory_format=torch.channels_last)
         self._begin_step(h)
-        h = self.stem_bn.act(self.stem(h))
+        h = _conv_bn(self.stem, self.stem_bn, h)
         from ..ops.pool import max_pool2d_nhwc, supported
 
         h = max_pool2d_nhwc(h, 3, 2, 1) if (_POOL_HIP and supported(h)) else F.max_pool2d(h, 3, 2, 1)
         for b in self.blocks:
             h = b(h)
+        return h
+
+    def _hip_head(self, h) -> bool:
+        from ..ops.head import head_supported
+
+        return _HEAD_HIP and _CONV_MODE == "hip" and head_supported(h, self.fc_w.shape[0])
+
+    def forward(self, x: torch.Tensor, compute_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+        """x: NHWC [B, H, W, 3] (or NCHW); returns log-probabilities (fp32)."""
+        h = self.trunk(x, compute_dtype)
+        if self._hip_head(h):
+            from ..ops.head import ResNetHeadNLL
+
+            return ResNetHeadNLL.apply(h, self.fc_w, self.fc_b, None, None)[1]
         # classifier in fp32 (2048 x 1000: negligible cost): bf16 logits of a
         # memorising synthetic run overflowed into NaN at lr 0.1
         h = h.float().mean((2, 3))
         return F.log_softmax(F.linear(h, self.fc_w, self.fc_b), dim=1)
+
+    def forward_loss(self, x: torch.Tensor, y: torch.Tensor, compute_dtype: Optional[torch.dtype] = None):
+        """(mean NLL loss, log-probabilities) of a training step with the
+        classifier head fused into one node (ops/head.py: mean + Linear +
+        LogSoftMax + NLL forward and backward on the MFMA kernels), or None
+        when that path does not apply (the caller then uses forward + loss)."""
+        if self._fc_bind is None or not torch.is_grad_enabled():
+            return None
+        h = self.trunk(x, compute_dtype)
+        if not self._hip_head(h):
+            logp = F.log_softmax(F.linear(h.float().mean((2, 3)), self.fc_w, self.fc_b), dim=1)
+            return F.nll_loss(logp, y), logp
+        from ..ops.head import ResNetHeadNLL
+
+        return ResNetHeadNLL.apply(h, self.fc_w, self.fc_b, y, self._fc_bind)
 
     def _begin_step(self, h) -> None:
         """Per training step: ONE zero fill for every BatchNorm's forward and
@@ -282,7 +347,7 @@ class ResNet50(nn.Module):
             if isinstance(m, _Conv):
                 i = index[id(m.weight)]
                 m.bind = ShadowBinding(w16[i], g32[i], (lambda i=i: ready(i)) if ready else (lambda: None))
-                if m.k == 1 and m.stride == 1 and w16[i].is_cuda:
+                if m.k == 1 and w16[i].is_cuda:  # stride 1 and 2: transposed shadow for the dgrad
                     gemm.append(m.bind)
                 elif m.k > 1 and w16[i].is_cuda:
                     spatial.append((m.bind, tuple(m.weight.shape)))
@@ -290,6 +355,8 @@ class ResNet50(nn.Module):
                 # the HIP BatchNorm backward writes dgamma / dbeta straight into the flat gradient
                 iw, ib = index[id(m.weight)], index[id(m.bias)]
                 m.bind = (g32[iw], g32[ib], (lambda iw=iw, ib=ib: (ready(iw), ready(ib))) if ready else (lambda: None))
+        iw, ib = index[id(self.fc_w)], index[id(self.fc_b)]
+        self._fc_bind = (g32[iw], g32[ib], (lambda: (ready(iw), ready(ib))) if ready else (lambda: None))
         if gemm and _CONV_MODE == "hip":
             from ..ops.conv import WeightTransposes
 

@@ -108,8 +108,10 @@ class _BnAct(torch.autograd.Function):
                                  weight.data_ptr(), bias.data_ptr(), acc.data_ptr(), dxbase,
                                  dres.data_ptr() if dres is not None else 0, dw.data_ptr(), db.data_ptr(), M, C,
                                  ctx.relu, H, W, int(p), stream_handle())
-        if ctx.res_sink is not None and dres is not None:
-            ctx.res_sink["g"] = dres  # consumed by the conv whose input is the residual (ops/conv.py)
+        if ctx.res_sink is not None and dres is not None and not ctx.res_sink.get("done"):
+            # consumed by the conv whose input is the residual (ops/conv.py); if that
+            # conv's backward already ran ("done"), autograd sums the gradients instead
+            ctx.res_sink["g"] = dres
             dres = None
         if ctx.grads is not None:
             ready()

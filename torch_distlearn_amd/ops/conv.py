@@ -193,16 +193,21 @@ class Conv1x1(torch.autograd.Function):
         s = stream_handle()
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = None
-        add = None
+        add = s2 = None
         link = ctx.res_link
         if link is not None and link.get("expect") and ctx.needs_input_grad[0]:
             # the same input also fed another branch (the identity residual's
             # BatchNorm, ops/bn_nhwc.py res_sink, or the downsample conv's dgrad,
             # dx_sink) that parked its gradient here: dx = dy W + that gradient
+            # (a stride-2 downsample parks its deferred dgrad instead: "s2")
             add = link.pop("g", None)
-            if add is None:
-                raise RuntimeError("Conv1x1: the other branch's input gradient did not arrive before the dgrad")
-            add = add.contiguous(memory_format=torch.channels_last)
+            s2 = link.pop("s2", None)
+            if add is None and s2 is None:
+                # autograd ran this branch first (no ordering guarantee): the other
+                # branch returns its gradient through autograd, which sums them
+                link["done"] = True
+            elif add is not None:
+                add = add.contiguous(memory_format=torch.channels_last)
         if ctx.needs_input_grad[0]:
             wt = bind.wt
             if wt is None:
@@ -220,6 +225,8 @@ class Conv1x1(torch.autograd.Function):
                            M, 1, 1, cout, cin, 1, tile, splits, s)
             if add is not None:
                 dx.add_(add)
+            if s2 is not None:  # dx[:, ::2, ::2] += the stride-2 downsample's dgrad (in place)
+                Conv1x1S2.deferred_dgrad(C, s2[0], s2[1], s2[2], dx, s)
         elif add is not None:
             dx = add
         # fp32 weight gradient added into the flat buffer: split-K partials in plain
@@ -370,9 +377,220 @@ class ShadowConv(torch.autograd.Function):
             (ctx.needs_input_grad[0], True, False))
         bind.g32.view(ctx.wshape).add_(dw)
         bind.ready()
-        if ctx.dx_sink is not None and dx is not None:
+        if ctx.dx_sink is not None and dx is not None and not ctx.dx_sink.get("done"):
             # the same input feeds a 1x1 conv whose dgrad epilogue adds this (ResNet
             # downsample blocks: no separate sum of the two input gradients)
             ctx.dx_sink["g"] = dx
             dx = None
         return dx, None, None, None, None, None
+
+
+# ---------------------------------------------------------------------------
+# strided convolutions and the stem on the generalised MFMA kernels
+# (csrc conv_fwd_ex / conv_wgrad_ex): no MIOpen convolution in the ResNet-50
+# training step
+# ---------------------------------------------------------------------------
+def _stream():
+    return stream_handle()
+
+
+class StemConv(torch.autograd.Function):
+    """The ResNet-50 stem: 7x7 stride-2 pad-3 conv over 3 input channels.
+    A stride-2 conv over a 2x2 space-to-depth image is a stride-1 conv: the
+    padded image becomes S[n][i][j][(a*2+b)*3 + c] = x[n][2i+a-3][2j+b-3][c]
+    (12 channels, zero-padded to 16: one 32-byte vector per pixel) and the
+    7x7 weights a 4x4x16 kernel (zero taps past 7), so the stem runs as a
+    4x4 stride-1 implicit GEMM with K = 256 on the MFMA kernels (csrc
+    resnet_glue.hip s2d_stem_input / stem_weight_pack / stem_wgrad_unpack).
+    No input gradient (the image).  ``stats``: BN sum / sum of squares rows."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bind: ShadowBinding, stats):
+        C = native()
+        N, cin, H, W = x.shape
+        if cin != 3 or not x.is_contiguous(memory_format=torch.channels_last) or x.dtype != BF16:
+            raise ValueError("StemConv: channels-last bf16 [N, 3, H, W] input")
+        cout = weight.shape[0]
+        Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+        Hs, Ws = Ho + 3, Wo + 3
+        s = _stream()
+        S = torch.empty(N, Hs, Ws, 16, dtype=BF16, device=x.device)
+        C.s2d_stem_input(x.data_ptr(), S.data_ptr(), N, H, W, Hs, Ws, 3, s)
+        w4 = torch.empty(cout, 4, 4, 16, dtype=BF16, device=x.device)
+        C.stem_weight_pack(bind.w16.data_ptr(), w4.data_ptr(), cout, s)
+        y = torch.empty((N, cout, Ho, Wo), dtype=BF16, device=x.device, memory_format=torch.channels_last)
+        tile = 0 if cout % 128 == 0 else 2
+        rows = None
+        if stats is not None:
+            if C.reduce_atomic() != 0:
+                raise RuntimeError("StemConv statistics need reduction mode 0 (partial rows)")
+            rows = torch.empty((N * Ho * Wo + 127) // 128, 2, cout, device=x.device)
+        T = C.conv_fwd_ex(S.data_ptr(), w4.data_ptr(), y.data_ptr(), 0 if rows is None else rows.data_ptr(), 0, N, Ho,
+                          Wo, Hs, Ws, 16, cout, 4, 4, 1, 0, 0, 0, 0, 0, 0, tile, 1, s)
+        if rows is not None:
+            C.bn_rows_reduce(rows.data_ptr(), T, cout, stats.data_ptr(), s)
+        ctx.save_for_backward(S)
+        ctx.bind, ctx.geom = bind, (N, Ho, Wo, Hs, Ws, cout)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        (S,) = ctx.saved_tensors
+        N, Ho, Wo, Hs, Ws, cout = ctx.geom
+        s = _stream()
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        tile, splits = _wgrad_plan_3x3(cout, 256, N * Ho * Wo)
+        ws = torch.empty(splits * cout * 256, device=dy.device)
+        C.conv_wgrad_ex(dy.data_ptr(), S.data_ptr(), ws.data_ptr(), N, Ho, Wo, Hs, Ws, Ho, Wo, 0, 16, cout, 4, 4, 1,
+                        splits, 256, tile, s)
+        C.stem_wgrad_unpack(ws.data_ptr(), ctx.bind.g32.data_ptr(), splits, cout, s)
+        ctx.bind.ready()
+        return None, None, None, None
+
+
+class Conv1x1S2(torch.autograd.Function):
+    """Stride-2 1x1 convolution (the ResNet-50 downsample) as an implicit GEMM
+    whose rows read every other pixel of the unpadded input (conv_fwd_ex,
+    S = 2): no gather copy.  Weight gradient: conv_wgrad_ex (stride-2 rows).
+    Input gradient: nonzero only at the even pixels, dx[2q] = dy[q] W --
+    handed to the c1 (stride-1 1x1) conv of the same block, whose backward
+    accumulates it IN PLACE into its own dx at those rows (the GEMM
+    epilogue's output map + addend = dx itself: no zero-filled full-size
+    tensor, no elementwise sum).  If c1's backward already ran (autograd
+    gives no ordering guarantee), the gradient is materialised and returned
+    through autograd instead."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bind: ShadowBinding, stats, dx_sink=None):
+        C = native()
+        x = x.contiguous(memory_format=torch.channels_last)
+        N, cin, H, W = x.shape
+        cout = weight.shape[0]
+        Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        ctx.dx_sink = dx_sink
+        if dx_sink is not None:
+            dx_sink["expect"] = True
+        y = torch.empty((N, cout, Ho, Wo), dtype=BF16, device=x.device, memory_format=torch.channels_last)
+        tile = 0 if cout % 128 == 0 else 2
+        s = _stream()
+        rows = None
+        if stats is not None:
+            if C.reduce_atomic() != 0:
+                raise RuntimeError("Conv1x1S2 statistics need reduction mode 0 (partial rows)")
+            rows = torch.empty((N * Ho * Wo + 127) // 128, 2, cout, device=x.device)
+        T = C.conv_fwd_ex(x.data_ptr(), bind.w16.data_ptr(), y.data_ptr(), 0 if rows is None else rows.data_ptr(), 0,
+                          N, Ho, Wo, H, W, cin, cout, 1, 1, 2, 0, 0, 0, 0, 0, 0, tile, 1, s)
+        if rows is not None:
+            C.bn_rows_reduce(rows.data_ptr(), T, cout, stats.data_ptr(), s)
+        ctx.save_for_backward(x)
+        ctx.bind, ctx.geom = bind, (N, cin, H, W, cout, Ho, Wo)
+        return y
+
+    @staticmethod
+    def deferred_dgrad(C, dy, wt, geom, dx, s):
+        """dx[:, 0::2, 0::2] += dy W (in place, bf16) -- the c1 conv's backward calls this."""
+        N, cin, H, W, cout, Ho, Wo = geom
+        tile = 0 if cin % 128 == 0 else 2
+        C.conv_fwd_ex(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, 0, N, Ho, Wo, Ho, Wo, cout, cin, 1, 1, 1, 2, 0, 0,
+                      W, H * W, dx.data_ptr(), tile, 1, s)
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        (x,) = ctx.saved_tensors
+        bind = ctx.bind
+        N, cin, H, W, cout, Ho, Wo = ctx.geom
+        s = _stream()
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        M = N * Ho * Wo
+        tile, splits = _wgrad_plan(cout, cin, M)
+        ws = torch.empty(splits * cout * cin, device=x.device)
+        C.conv_wgrad_ex(dy.data_ptr(), x.data_ptr(), ws.data_ptr(), N, Ho, Wo, H, W, Ho, Wo, 0, cin, cout, 1, 1, 2,
+                        splits, cin, tile, s)
+        C.slab_reduce_add(ws.data_ptr(), bind.g32.data_ptr(), splits, cout, 1, cin, cin, s)
+        bind.ready()
+        if not ctx.needs_input_grad[0]:
+            return None, None, None, None, None
+        wt = bind.wt
+        if wt is None:
+            wt = torch.empty(cin, cout, dtype=BF16, device=x.device)
+            C.weight_flip_transpose(bind.w16.data_ptr(), wt.data_ptr(), cout, cin, 1, s)
+        sink = ctx.dx_sink
+        if sink is not None and not sink.get("done"):
+            sink["s2"] = (dy, wt, ctx.geom)  # accumulated by the c1 dgrad (Conv1x1.backward)
+            return None, None, None, None, None
+        dx = torch.zeros((N, cin, H, W), dtype=BF16, device=x.device, memory_format=torch.channels_last)
+        Conv1x1S2.deferred_dgrad(C, dy, wt, ctx.geom, dx, s)
+        return dx, None, None, None, None
+
+
+class Conv3x3S2(torch.autograd.Function):
+    """Stride-2 3x3 pad-1 convolution (the first bottleneck of stages 2-4)
+    on the generalised MFMA kernels: forward and weight gradient read the
+    zero-bordered input with stride-2 rows (conv_fwd_ex / conv_wgrad_ex).
+    Input gradient by output parity: dx[2q + r] (per axis) only sees the
+    kernel taps of parity r -- 1 tap for r = 0, 2 for r = 1 -- so it is four
+    phase convolutions (1x1, 1x2, 2x1, 2x2 over the zero-bordered dy, weights
+    from csrc phase_weights) each storing its pixels interleaved into dx
+    through the epilogue's output map: exactly the 9 taps of work, no
+    zero-stuffed upsampling."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bind: ShadowBinding, stats):
+        C = native()
+        N, cin, H, W = x.shape
+        cout = weight.shape[0]
+        Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        keep, xbase = _padded_base(x, 1)
+        y = torch.empty((N, cout, Ho, Wo), dtype=BF16, device=x.device, memory_format=torch.channels_last)
+        tile = 0 if cout % 128 == 0 else 2
+        s = _stream()
+        rows = None
+        if stats is not None:
+            if C.reduce_atomic() != 0:
+                raise RuntimeError("Conv3x3S2 statistics need reduction mode 0 (partial rows)")
+            rows = torch.empty((N * Ho * Wo + 127) // 128, 2, cout, device=x.device)
+        T = C.conv_fwd_ex(xbase, bind.wcl.data_ptr(), y.data_ptr(), 0 if rows is None else rows.data_ptr(), 0, N, Ho,
+                          Wo, H + 2, W + 2, cin, cout, 3, 3, 2, 0, 0, 0, 0, 0, 0, tile, 1, s)
+        if rows is not None:
+            C.bn_rows_reduce(rows.data_ptr(), T, cout, stats.data_ptr(), s)
+        ctx.save_for_backward(keep)
+        ctx.xbase, ctx.bind, ctx.geom = xbase, bind, (N, cin, H, W, cout, Ho, Wo)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        N, cin, H, W, cout, Ho, Wo = ctx.geom
+        bind = ctx.bind
+        s = _stream()
+        keep_dy, dybase = _padded_base(dy, 1)  # [N][Ho+2][Wo+2][cout], interior at (1, 1)
+        Hq, Wq = Ho + 2, Wo + 2
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if H != 2 * Ho or W != 2 * Wo:
+                raise ValueError("Conv3x3S2: even input sizes only")
+            wt = torch.empty(cin, 3, 3, cout, dtype=BF16, device=dy.device)
+            C.weight_flip_transpose(bind.wcl.data_ptr(), wt.data_ptr(), cout, cin, 3, s)
+            ph = torch.empty(9 * cin * cout, dtype=BF16, device=dy.device)
+            C.phase_weights(wt.data_ptr(), ph.data_ptr(), cin, cout, s)
+            dx = torch.empty((N, cin, H, W), dtype=BF16, device=dy.device, memory_format=torch.channels_last)
+            interior = dybase + (Wq + 1) * cout * 2  # dy[0][0]: tap t of phase pixel q reads dy[q + t]
+            tile = 0 if cin % 128 == 0 else 2
+            off = 0
+            for rh in (0, 1):
+                for rw in (0, 1):
+                    kh, kw = 1 + rh, 1 + rw
+                    C.conv_fwd_ex(interior, ph[off * cin * cout:].data_ptr(), dx.data_ptr(), 0, 0, N, Ho, Wo, Hq, Wq,
+                                  cout, cin, kh, kw, 1, 2, rh, rw, W, H * W, 0, tile, 1, s)
+                    off += kh * kw
+        K = 9 * cin
+        tile_w, splits = _wgrad_plan_3x3(cout, K, N * Ho * Wo)
+        ws = torch.empty(splits * cout * K, device=dy.device)
+        C.conv_wgrad_ex(dybase, ctx.xbase, ws.data_ptr(), N, Ho, Wo, H + 2, W + 2, Hq, Wq, 1, cin, cout, 3, 3, 2,
+                        splits, K, tile_w, s)
+        C.slab_reduce_add_oihw(ws.data_ptr(), bind.g32.data_ptr(), splits, cout, 9, cin, cin, s)
+        bind.ready()
+        del keep_dy
+        return dx, None, None, None
