@@ -54,6 +54,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_conv_debug", &set_conv_debug);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("combine_bwd_reduce", &combine_bwd_reduce);
+  m.def("bn_bwd_apply_head", &bn_bwd_apply_head);
   m.def("combine_bwd_reduce_blocks", &combine_bwd_reduce_blocks);
   m.def("conv_fwd_ex", &conv_fwd_ex);
   m.def("conv_wgrad_ex", &conv_wgrad_ex);

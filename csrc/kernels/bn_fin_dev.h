@@ -84,12 +84,18 @@ __device__ __forceinline__ static void fin_block_sync() {
 // Block-cooperative: scale / shift of ALL C channels into LDS (ssc, ssh [C]),
 // each channel's rows summed once per block instead of once per thread;
 // block 0 also publishes coef + running statistics.  Ends with an LDS barrier.
-__device__ __forceinline__ void bn_fin_block(const BnFin& f, int C, float* ssc, float* ssh) {
+// smu / sis (optional): also the mean and invstd per channel.
+__device__ __forceinline__ void bn_fin_block(const BnFin& f, int C, float* ssc, float* ssh, float* smu = nullptr,
+                                             float* sis = nullptr) {
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float mean, var, invstd, sc, sh;
     bn_fin_channel(f, C, c, mean, var, invstd, sc, sh);
     ssc[c] = sc;
     ssh[c] = sh;
+    if (smu != nullptr) {
+      smu[c] = mean;
+      sis[c] = invstd;
+    }
     if (blockIdx.x == 0) {
       f.coef[c] = mean;
       f.coef[C + c] = invstd;

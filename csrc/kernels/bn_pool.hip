@@ -539,21 +539,19 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
 // totals to dgamma_out / dbeta_out (R > 1: the flat gradient; R = 1
 // accumulated there directly and passes null).
 template <bool SUMS>
-__global__ void __launch_bounds__(256) bn_relu_pool_bwd_apply_kernel(const bf16_t* __restrict__ y,
-                                                                     const bf16_t* __restrict__ dP,
-                                                                     const float* __restrict__ coef,
-                                                                     const float* __restrict__ acoef,
-                                                                     bf16_t* __restrict__ dy, int B, int H, int W,
-                                                                     int C, int opad, const float* __restrict__ gamma,
-                                                                     float inv_m, int R, float* __restrict__ dgamma_out,
-                                                                     float* __restrict__ dbeta_out) {
+__device__ __forceinline__ void bwd_apply_body(const bf16_t* __restrict__ y, const bf16_t* __restrict__ dP,
+                                               const float* __restrict__ coef, const float* __restrict__ acoef,
+                                               bf16_t* __restrict__ dy, int B, int H, int W, int C, int opad,
+                                               const float* __restrict__ gamma, float inv_m, int R,
+                                               float* __restrict__ dgamma_out, float* __restrict__ dbeta_out, int bid,
+                                               int nblk) {
   // dy: [B][H+2 opad][W+2 opad][C], written in the interior (zero border =
   // the dgrad convolution's spatial padding)
   __shared__ float sk[SUMS ? 3 : 1][SUMS ? kFinMaxC : 1];
   const int C8 = C >> 3, Ho = H >> 1, Wo = W >> 1;
   const int Hp = H + 2 * opad, Wp = W + 2 * opad;
   const int64_t total = (int64_t)B * Ho * Wo * C8;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t stride = (int64_t)nblk * blockDim.x;
   int c0 = 0, oh = 0, ow = 0;
   int64_t b = 0;
   uint4 yw[4], gv;
@@ -571,7 +569,7 @@ __global__ void __launch_bounds__(256) bn_relu_pool_bwd_apply_kernel(const bf16_
     yw[3] = *reinterpret_cast<const uint4*>(base + (int64_t)W * C + C);
     gv = *reinterpret_cast<const uint4*>(dP + (((b * Ho + oh) * Wo) + ow) * (int64_t)C + c0);
   };
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t i = (int64_t)bid * blockDim.x + threadIdx.x;
   if (i < total) item_loads(i);
   if constexpr (SUMS) {
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -582,7 +580,7 @@ __global__ void __launch_bounds__(256) bn_relu_pool_bwd_apply_kernel(const bf16_
       sk[0][c] = a;
       sk[1][c] = -a * dg * inv_m;
       sk[2][c] = -a * db * inv_m;
-      if (blockIdx.x == 0 && dgamma_out != nullptr) { dgamma_out[c] = dg; dbeta_out[c] = db; }
+      if (bid == 0 && dgamma_out != nullptr) { dgamma_out[c] = dg; dbeta_out[c] = db; }
     }
     fin_block_sync();
   }
@@ -632,6 +630,49 @@ __global__ void __launch_bounds__(256) bn_relu_pool_bwd_apply_kernel(const bf16_
 #pragma unroll
     for (int w = 0; w < 4; ++w) *reinterpret_cast<uint4*>(base + offs[w]) = o4[w];
   }
+}
+
+template <bool SUMS>
+__global__ void __launch_bounds__(256) bn_relu_pool_bwd_apply_kernel(const bf16_t* __restrict__ y,
+                                                                     const bf16_t* __restrict__ dP,
+                                                                     const float* __restrict__ coef,
+                                                                     const float* __restrict__ acoef,
+                                                                     bf16_t* __restrict__ dy, int B, int H, int W,
+                                                                     int C, int opad, const float* __restrict__ gamma,
+                                                                     float inv_m, int R, float* __restrict__ dgamma_out,
+                                                                     float* __restrict__ dbeta_out) {
+  bwd_apply_body<SUMS>(y, dP, coef, acoef, dy, B, H, W, C, opad, gamma, inv_m, R, dgamma_out, dbeta_out,
+                       (int)blockIdx.x, (int)gridDim.x);
+}
+
+// One launch for two jobs that both wait only for the head kernel (which also
+// did the last block's BN backward reduce, head.hip RED): blocks [0, Ga) =
+// this block's BN backward apply (atomic-rows mode), blocks [Ga, ...) = the
+// classifier weight gradient (head_wgrad_body).
+struct HeadWgradArgs2 {
+  const bf16_t* h;
+  const float* dlogits;
+  const float* loss_b;
+  int F, B;
+  float *dw, *db, *loss, *slot;
+  unsigned long long* step_ctr;
+};
+
+__global__ void __launch_bounds__(256) bwd_apply_head_kernel(const bf16_t* __restrict__ y,
+                                                             const bf16_t* __restrict__ dP,
+                                                             const float* __restrict__ coef,
+                                                             const float* __restrict__ acoef,
+                                                             bf16_t* __restrict__ dy, int B, int H, int W, int C,
+                                                             int opad, const float* __restrict__ gamma, float inv_m,
+                                                             int R, float* __restrict__ dgamma_out,
+                                                             float* __restrict__ dbeta_out, int Ga,
+                                                             const HeadWgradArgs2 ha) {
+  if ((int)blockIdx.x < Ga)
+    bwd_apply_body<true>(y, dP, coef, acoef, dy, B, H, W, C, opad, gamma, inv_m, R, dgamma_out, dbeta_out,
+                         (int)blockIdx.x, Ga);
+  else
+    head_wgrad_body<10>(ha.h, ha.dlogits, ha.loss_b, ha.F, ha.B, ha.dw, ha.db, ha.loss, ha.slot, ha.step_ctr,
+                        (int)blockIdx.x - Ga);
 }
 
 // ---------------------------------------------------------------------------
@@ -799,6 +840,27 @@ void bn_relu_pool_bwd_apply_sums(uintptr_t y, uintptr_t dP, uintptr_t coef, uint
   bn_relu_pool_bwd_apply_kernel<true><<<fin_grid(total), 256, 0, as_stream(stream)>>>(
       (const bf16_t*)y, (const bf16_t*)dP, (const float*)coef, (const float*)dgb, (bf16_t*)dy, B, H, W, C, opad,
       (const float*)gamma, 1.0f / (float)M, g_host_rows, (float*)dgamma_out, (float*)dbeta_out);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+// bn_relu_pool_bwd_apply_sums + the classifier weight gradient in one launch
+void bn_bwd_apply_head(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t dgb, uintptr_t gamma, int64_t M,
+                       uintptr_t dy, int B, int H, int W, int C, int opad, uintptr_t dgamma_out, uintptr_t dbeta_out,
+                       uintptr_t h, uintptr_t dlogits, uintptr_t loss_b, int F, int NC, uintptr_t dw, uintptr_t db,
+                       uintptr_t loss, uintptr_t slot, uintptr_t step_ctr, uintptr_t stream) {
+  check_c(C);
+  if (C > kFinMaxC) throw std::runtime_error("bn_bwd_apply_head: C too large");
+  if (g_host_rows < 1 || g_host_rows > kMaxRows)
+    throw std::runtime_error("bn_bwd_apply_head: needs an atomic reduction mode with <= 32 rows");
+  if (NC != 10) throw std::runtime_error("bn_bwd_apply_head: built for 10 classes");
+  const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
+  const int Ga = fin_grid(total);
+  const HeadWgradArgs2 ha{(const bf16_t*)h, (const float*)dlogits, (const float*)loss_b, F, B, (float*)dw,
+                          (float*)db, (float*)loss, (float*)slot, (unsigned long long*)step_ctr};
+  const int head_blocks = (F + 31) / 32 + 1;
+  bwd_apply_head_kernel<<<Ga + head_blocks, 256, 0, as_stream(stream)>>>(
+      (const bf16_t*)y, (const bf16_t*)dP, (const float*)coef, (const float*)dgb, (bf16_t*)dy, B, H, W, C, opad,
+      (const float*)gamma, 1.0f / (float)M, g_host_rows, (float*)dgamma_out, (float*)dbeta_out, Ga, ha);
   DL_HIP_CHECK(hipGetLastError());
 }
 

@@ -30,9 +30,15 @@ struct HeadPool {
   bf16_t* h_out;
   int yH, yW, yC;
   BnFin fin;  // fin.sums != nullptr: derive the coefficients from the accumulated statistics (mode 1)
+  // RED: the last conv block's BatchNorm backward reduce, fused: each block
+  // adds its sample's sum(dz) / sum(dz * xhat) per channel into row
+  // (blockIdx & (fin.R - 1)) of red_rows [R][dgamma (C); dbeta (C)] (zeroed by
+  // the step's prep kernel) -- the work of bn_relu_pool_bwd_reduce for that
+  // block, done while dP, the window values and the coefficients are in registers
+  float* red_rows;
 };
 
-template <int NC, bool POOL = false>
+template <int NC, bool POOL = false, bool RED = false>
 __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restrict__ h, const float* __restrict__ w,
                                                            const float* __restrict__ bias,
                                                            const int64_t* __restrict__ labels, int F, int B,
@@ -50,6 +56,8 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
   // weights stay in registers for the dh pass (W is read once per sample)
   const bool one = F == 256 * 8;
   float4 wc[NC][2];
+  uint4 v[4];                           // RED: the window values, kept for the backward reduce
+  float rsc[8], rsh[8], rmu[8], ris[8];  // RED: BN coefficients of the thread's 8 channels
   if (one) {
     const int j0 = tid * 8;
     uint4 hv;
@@ -59,15 +67,21 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
       const int pix = j0 / hp.yC, c0 = j0 - pix * hp.yC;
       const int oh = pix / Wo, ow = pix - oh * Wo;
       const bf16_t* base = hp.y + (((int64_t)b * hp.yH + 2 * oh) * hp.yW + 2 * ow) * hp.yC + c0;
-      const uint4 v[4] = {*reinterpret_cast<const uint4*>(base), *reinterpret_cast<const uint4*>(base + hp.yC),
-                          *reinterpret_cast<const uint4*>(base + (int64_t)hp.yW * hp.yC),
-                          *reinterpret_cast<const uint4*>(base + (int64_t)hp.yW * hp.yC + hp.yC)};
+      v[0] = *reinterpret_cast<const uint4*>(base);
+      v[1] = *reinterpret_cast<const uint4*>(base + hp.yC);
+      v[2] = *reinterpret_cast<const uint4*>(base + (int64_t)hp.yW * hp.yC);
+      v[3] = *reinterpret_cast<const uint4*>(base + (int64_t)hp.yW * hp.yC + hp.yC);
       float sc[8], sh[8];
       if (hp.fin.sums != nullptr) {  // uniform over the block (bn_fin_block ends with a barrier)
         __shared__ float ssc[kFinMaxC], ssh[kFinMaxC];
-        bn_fin_block(hp.fin, hp.yC, ssc, ssh);
+        __shared__ float smu[RED ? kFinMaxC : 1], sis[RED ? kFinMaxC : 1];
+        bn_fin_block(hp.fin, hp.yC, ssc, ssh, RED ? smu : nullptr, RED ? sis : nullptr);
 #pragma unroll
         for (int k = 0; k < 8; ++k) { sc[k] = ssc[c0 + k]; sh[k] = ssh[c0 + k]; }
+        if constexpr (RED) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { rmu[k] = smu[c0 + k]; ris[k] = sis[c0 + k]; }
+        }
       } else {
         const float4 sc0 = *reinterpret_cast<const float4*>(hp.coef + 2 * hp.yC + c0);
         const float4 sc1 = *reinterpret_cast<const float4*>(hp.coef + 2 * hp.yC + c0 + 4);
@@ -78,6 +92,8 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
         sh[0] = sh0.x; sh[1] = sh0.y; sh[2] = sh0.z; sh[3] = sh0.w; sh[4] = sh1.x; sh[5] = sh1.y; sh[6] = sh1.z;
         sh[7] = sh1.w;
       }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { rsc[k] = sc[k]; rsh[k] = sh[k]; }
       float mx[8];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -169,8 +185,56 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
       o[0] += d[c] * wc[c][0].x; o[1] += d[c] * wc[c][0].y; o[2] += d[c] * wc[c][0].z; o[3] += d[c] * wc[c][0].w;
       o[4] += d[c] * wc[c][1].x; o[5] += d[c] * wc[c][1].y; o[6] += d[c] * wc[c][1].z; o[7] += d[c] * wc[c][1].w;
     }
-    *reinterpret_cast<uint4*>(dh + (int64_t)b * F + j0) =
+    const uint4 dpk =
         make_uint4(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]), pack_bf16x2(o[6], o[7]));
+    *reinterpret_cast<uint4*>(dh + (int64_t)b * F + j0) = dpk;
+    if constexpr (POOL && RED) {
+      // the backward reduce of this sample: dz routed to the pool argmax (ReLU
+      // mask), sum(dz) and sum(dz * xhat) per channel, from the bf16 dP that the
+      // apply kernel will read -- bwd_reduce_body's arithmetic, item for item
+      float g[8], s1[8], s2[8];
+      g[0] = lo_bf16(dpk.x); g[1] = hi_bf16(dpk.x); g[2] = lo_bf16(dpk.y); g[3] = hi_bf16(dpk.y);
+      g[4] = lo_bf16(dpk.z); g[5] = hi_bf16(dpk.z); g[6] = lo_bf16(dpk.w); g[7] = hi_bf16(dpk.w);
+      float yv[4][8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        yv[q][0] = lo_bf16(v[q].x); yv[q][1] = hi_bf16(v[q].x); yv[q][2] = lo_bf16(v[q].y); yv[q][3] = hi_bf16(v[q].y);
+        yv[q][4] = lo_bf16(v[q].z); yv[q][5] = hi_bf16(v[q].z); yv[q][6] = lo_bf16(v[q].w); yv[q][7] = hi_bf16(v[q].w);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float best = -INFINITY;
+        int arg = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const float r = fmaxf(fmaf(rsc[k], yv[w][k], rsh[k]), 0.f);
+          if (r > best) { best = r; arg = w; }
+        }
+        s1[k] = 0.f;
+        s2[k] = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const float dz = (w == arg && best > 0.f) ? g[k] : 0.f;
+          s1[k] += dz;
+          s2[k] += dz * (yv[w][k] - rmu[k]) * ris[k];
+        }
+      }
+      // the 4 waves hold the 4 pooled pixels of the same 64 channel chunks
+      __shared__ float rr[4][64][17];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { rr[wid][lane][k] = s1[k]; rr[wid][lane][8 + k] = s2[k]; }
+      __syncthreads();
+      // 256 threads: chunk = tid & 63, (sum, k-quad) = tid >> 6
+      const int ch = tid & 63, part = tid >> 6, which = part >> 1, k0 = (part & 1) * 4;
+      float* row = hp.red_rows + (int64_t)(blockIdx.x & (hp.fin.R - 1)) * 2 * hp.yC;
+#pragma unroll
+      for (int k = k0; k < k0 + 4; ++k) {
+        const float t = rr[0][ch][which * 8 + k] + rr[1][ch][which * 8 + k] + rr[2][ch][which * 8 + k] +
+                        rr[3][ch][which * 8 + k];
+        // row = [dgamma (= sum dz*xhat) ; dbeta (= sum dz)]
+        unsafeAtomicAdd(row + (which == 1 ? 0 : hp.yC) + ch * 8 + k, t);
+      }
+    }
     return;
   }
   for (int j0 = tid * 8; j0 < F; j0 += 256 * 8) {
@@ -215,18 +279,26 @@ void head_fwd_bwd_pool(uintptr_t y, uintptr_t coef, int yH, int yW, int yC, uint
                        uintptr_t bias, uintptr_t labels, int B, int NC, uintptr_t logits_out, uintptr_t dlogits,
                        uintptr_t loss_b, uintptr_t dh, uintptr_t fin_sums, int64_t fin_m, uintptr_t gamma,
                        uintptr_t beta, uintptr_t conv_bias, uintptr_t rmean, uintptr_t rvar, float eps, float momentum,
-                       uintptr_t stream) {
+                       uintptr_t red_rows, uintptr_t stream) {
   if (NC != 10) throw std::runtime_error("head_fwd_bwd_pool: built for 10 classes");
   const int F = (yH / 2) * (yW / 2) * yC;
   if (F != 2048 || yC % 8 != 0 || yH % 2 != 0 || yW % 2 != 0)
     throw std::runtime_error("head_fwd_bwd_pool: needs a 2048-feature pooled map, C % 8 == 0");
   if (fin_sums != 0 && (reduce_rows() < 1 || reduce_rows() > kMaxRows || yC > kFinMaxC))
     throw std::runtime_error("head_fwd_bwd_pool: accumulated statistics need an atomic reduction mode");
+  if (red_rows != 0 && (fin_sums == 0 || labels == 0 || yC != 512))
+    throw std::runtime_error("head_fwd_bwd_pool: the fused BN backward reduce needs the atomic statistics, labels, C 512");
   const HeadPool hp{(const bf16_t*)y, (const float*)coef, (bf16_t*)h_out, yH, yW, yC,
-                    make_bn_fin(fin_sums, fin_m, gamma, beta, conv_bias, rmean, rvar, eps, momentum, coef, reduce_rows())};
-  head_fwd_bwd_kernel<10, true><<<B, 256, 0, as_stream(stream)>>>(
-      nullptr, (const float*)w, (const float*)bias, (const int64_t*)labels, F, B, (float*)logits_out,
-      (float*)dlogits, (float*)loss_b, (bf16_t*)dh, hp);
+                    make_bn_fin(fin_sums, fin_m, gamma, beta, conv_bias, rmean, rvar, eps, momentum, coef, reduce_rows()),
+                    (float*)red_rows};
+  if (red_rows)
+    head_fwd_bwd_kernel<10, true, true><<<B, 256, 0, as_stream(stream)>>>(
+        nullptr, (const float*)w, (const float*)bias, (const int64_t*)labels, F, B, (float*)logits_out,
+        (float*)dlogits, (float*)loss_b, (bf16_t*)dh, hp);
+  else
+    head_fwd_bwd_kernel<10, true><<<B, 256, 0, as_stream(stream)>>>(
+        nullptr, (const float*)w, (const float*)bias, (const int64_t*)labels, F, B, (float*)logits_out,
+        (float*)dlogits, (float*)loss_b, (bf16_t*)dh, hp);
   DL_HIP_CHECK(hipGetLastError());
 }
 

@@ -46,7 +46,10 @@ def add_node_flags(ap: argparse.ArgumentParser, batch: int = 32, lr: float = 0.1
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--commTimeout", type=float, default=None,
-                    help="seconds before a dead/stuck peer turns into an error (default 600; DISTLEARN_COMM_TIMEOUT)")
+                    help="seconds before a dead/stuck peer turns into an error (default 600; DISTLEARN_COMM_TIMEOUT). "
+                         "AsyncEA: the server's wait for the next client sync is bounded by it, so it must exceed "
+                         "tau training steps of the slowest client; the tester's wait for its next snapshot is "
+                         "unbounded (a dead server fails it at once)")
     return ap
 
 

@@ -49,6 +49,7 @@ SPAD = KSIZE // 2  # spatial zero border of every convolution input (written onc
 # tile ids of conv_fwd: 0 = 128x128, 1 = 64x64, 2 = 128x64 (BK = 64) ; conv_wgrad: 0 = 128x64, 1 = 64x64, 2 = 128x128
 _FWD_TILES = {0: (128, 128), 1: (64, 64), 2: (128, 64)}
 _NOSPLIT_128x64 = os.environ.get("DISTLEARN_FWD_NOSPLIT", "1") == "1"
+_NOSPLIT_64 = os.environ.get("DISTLEARN_FWD_NOSPLIT64", "0") == "1"
 
 
 # The fwd/dgrad split-K slab holds SLAB_CAP x splits slices, announced to
@@ -78,6 +79,10 @@ def _fwd_plan(M: int, N: int, K: int):
         # 128x64 tiles already fill the chip without a K split: no slab round
         # trip and no combine launch (fwd3 at batch 128: 28.5 -> 24.7 us)
         return 2, 1
+    if splits > 1 and _NOSPLIT_64 and (M // 64) * (N // 64) >= 256 and M % 64 == 0 and N % 64 == 0:
+        # 64x64 tiles fill the chip without a K split: no fp32 slab round trip
+        # and no combine launch, at twice the LDS traffic per MFMA (A/B knob)
+        return 1, 1
     return tile, splits
 
 
@@ -177,6 +182,9 @@ class CifarHIPExecutor:
         self.head_pool = (os.environ.get("DISTLEARN_HEAD_POOL", "1") == "1"
                           and (self.hs[-1] // 2) ** 2 * self.couts[-1] == 2048 and self.nclass == 10)
         self.head_wgrad_fused = os.environ.get("DISTLEARN_HEAD_WGRAD_FUSED", "1") == "1" and self.nclass == 10
+        # (atomic-rows mode 2) the last block's BN backward reduce runs inside the head
+        # kernel and the classifier weight gradient rides the BN backward apply launch:
+        # bwd_reduce_head's launch is gone (DISTLEARN_HEAD_REDUCE=0: A/B)
         if "DISTLEARN_REGION" in os.environ:  # tuning: tap-reuse region conv kernel (0 off, 1 rows, 2 + images)
             self.C.set_conv_region(int(os.environ["DISTLEARN_REGION"]))
         if "DISTLEARN_BN_BWD_ITEMS" in os.environ:  # tuning: pooled pixels per thread of the BN backward reduce
@@ -224,6 +232,8 @@ class CifarHIPExecutor:
         # reduced by one launch (DISTLEARN_FUSE_COMBINE=0: separate kernels, A/B)
         self.fuse_combine = os.environ.get("DISTLEARN_FUSE_COMBINE", "1") == "1"
         self.atomic = self.mode > 0             # BN statistics / gradients by atomics, no finalize kernels
+        self.head_reduce = (os.environ.get("DISTLEARN_HEAD_REDUCE", "1") == "1" and self.mode == 2 and self.head_pool
+                            and self.head_wgrad_fused and self.couts[-1] == 512)
         self.atomic_wgrad = self.mode == 1      # split-K weight gradients by atomics (else slabs)
         self.rows = {0: 0, 1: 1, 2: int(os.environ.get("DISTLEARN_REDUCE_ROWS", "16"))}[self.mode]
         self._alloc(self.B)
@@ -438,7 +448,8 @@ class CifarHIPExecutor:
             C.head_fwd_bwd_pool(self.y[-1].data_ptr(), self.coef[-1].data_ptr(), hl, hl, self.couts[-1],
                                 self.p[-1].data_ptr(), self.p32[nfc].data_ptr(), self.p32[nfc + 1].data_ptr(),
                                 labels.data_ptr(), B, self.nclass, self.logits.data_ptr(), self.dlogits.data_ptr(),
-                                self.loss_b.data_ptr(), self.dP[-1].data_ptr(), *fin, s)
+                                self.loss_b.data_ptr(), self.dP[-1].data_ptr(), *fin,
+                                self.bwd_rows[last].data_ptr() if self.head_reduce else 0, s)
         else:
             C.head_fwd_bwd(self.p[-1].data_ptr(), self.p32[nfc].data_ptr(), self.p32[nfc + 1].data_ptr(),
                            labels.data_ptr(), self.feat, B, self.nclass, self.logits.data_ptr(),
@@ -468,7 +479,9 @@ class CifarHIPExecutor:
             # mode 1: the reduce accumulates straight into [dgamma; dbeta] of the flat gradient;
             # mode 2: into R striped rows (the apply kernel writes the totals to the flat gradient)
             part = {0: self.bwd_part[i], 1: self.g32[self._leaf(i, 2)], 2: self.bwd_rows[i]}[self.mode]
-            if i == self.nb - 1 and self.head_wgrad_fused:
+            if i == self.nb - 1 and self.head_reduce:
+                pass  # reduced inside the head kernel; the classifier wgrad rides the apply launch
+            elif i == self.nb - 1 and self.head_wgrad_fused:
                 # one launch: this block's BN backward reduce + the classifier weight gradient
                 C.bn_bwd_reduce_head(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
                                      part.data_ptr(), B, h, h, cout, G, *head_args, s)
@@ -494,9 +507,18 @@ class CifarHIPExecutor:
             if self.atomic:
                 dgo, dbo = ((self.g32[self._leaf(i, 2)].data_ptr(), self.g32[self._leaf(i, 3)].data_ptr())
                             if self.mode == 2 else (0, 0))
-                C.bn_relu_pool_bwd_apply_sums(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
-                                              part.data_ptr(), self.p32[self._leaf(i, 2)].data_ptr(), M,
-                                              dY.data_ptr(), B, h, h, cout, SPAD, dgo, dbo, s)
+                if i == self.nb - 1 and self.head_reduce:
+                    h_, dl_, lb_, F_, nc_, dw_, db_, loss_, slot_, ctr_ = head_args
+                    C.bn_bwd_apply_head(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
+                                        part.data_ptr(), self.p32[self._leaf(i, 2)].data_ptr(), M, dY.data_ptr(), B, h,
+                                        h, cout, SPAD, dgo, dbo, h_, dl_, lb_, F_, nc_, dw_, db_, loss_, slot_, ctr_, s)
+                    self._ready(nfc)
+                    self._ready(nfc + 1)
+                else:
+                    C.bn_relu_pool_bwd_apply_sums(self.y[i].data_ptr(), self.dP[i].data_ptr(),
+                                                  self.coef[i].data_ptr(), part.data_ptr(),
+                                                  self.p32[self._leaf(i, 2)].data_ptr(), M, dY.data_ptr(), B, h, h,
+                                                  cout, SPAD, dgo, dbo, s)
             else:
                 C.bn_bwd_finalize(self.bwd_part[i].data_ptr(), T, cout, M, self.p32[self._leaf(i, 2)].data_ptr(),
                                   self.coef[i].data_ptr(), self.g32[self._leaf(i, 2)].data_ptr(),

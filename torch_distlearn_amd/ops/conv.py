@@ -520,7 +520,7 @@ class Conv1x1S2(torch.autograd.Function):
         if sink is not None and not sink.get("done"):
             sink["s2"] = (dy, wt, ctx.geom)  # accumulated by the c1 dgrad (Conv1x1.backward)
             return None, None, None, None, None
-        dx = torch.zeros((N, cin, H, W), dtype=BF16, device=x.device, memory_format=torch.channels_last)
+        dx = torch.zeros_like(x, memory_format=torch.channels_last)
         Conv1x1S2.deferred_dgrad(C, dy, wt, ctx.geom, dx, s)
         return dx, None, None, None, None
 

@@ -44,7 +44,13 @@ MI355X mapping:
   timeout, ``--commTimeout``).  A client that dies or stops syncing makes the
   server raise :class:`~torch_distlearn_amd.parallel.comm.CommError` naming
   the clients that never finished; the tester stops the same way when the
-  server disappears.
+  server disappears.  Waits that a HEALTHY run can legitimately make long are
+  not bounded by that timeout: the tester waiting for its next snapshot (TEST
+  comes only every ``testTime`` syncs, and not while a test is in flight) uses
+  ``idle_timeout`` (default: none -- a dead server closes its connection, which
+  fails the wait at once); the server's wait for the next ENTER stays bounded
+  by ``timeout``, which must therefore exceed ``tau`` training steps of the
+  slowest client (``--commTimeout`` help).
 """
 from __future__ import annotations
 
@@ -79,7 +85,8 @@ class AsyncEA:
 
     def __init__(self, server=None, serverBroadcast=None, client=None, clientBroadcast=None,  # noqa: N803
                  serverTest=None, clientTest=None, numNodes: int = 1, node: int = 0, tau: int = 10,  # noqa: N803
-                 alpha: float = 0.2, comm: Optional[Communicator] = None, timeout: Optional[float] = None):
+                 alpha: float = 0.2, comm: Optional[Communicator] = None, timeout: Optional[float] = None,
+                 idle_timeout: Optional[float] = None):
         if comm is None:
             for c in (server, serverBroadcast, client, clientBroadcast, serverTest, clientTest):
                 if isinstance(c, Tree):
@@ -108,6 +115,8 @@ class AsyncEA:
         self.syncs = 0
         self.server_syncs = 0  # tester: sync count of the last snapshot
         self.timeout = float(timeout) if timeout is not None else float(getattr(comm, "timeout_s", comm_timeout()))
+        # tester's wait for the next snapshot (None: unbounded; a dead server still fails it)
+        self.idle_timeout = None if idle_timeout is None else float(idle_timeout)
         self._ps = None        # payload stream (GPU)
         self._done = set()     # clients that said BYE (server)
 
@@ -156,9 +165,12 @@ class AsyncEA:
         self._seq += 1
         self.comm.send_msg([typ, self.comm.rank, self._seq, *extra], dst, tag)
 
-    def _expect(self, src, tag, *types, what: str = ""):
+    def _expect(self, src, tag, *types, what: str = "", idle: bool = False):
         try:
-            sender, m = self.comm.recv_msg(src, tag, timeout=self.timeout)
+            if idle and self.idle_timeout is None:
+                sender, m = self.comm.recv_msg(src, tag, timeout=None, unbounded=True)
+            else:
+                sender, m = self.comm.recv_msg(src, tag, timeout=self.idle_timeout if idle else self.timeout)
         except CommError as e:
             raise CommError(f"AsyncEA {what or 'wait'}: {e}") from e
         if m[0] not in types:
@@ -278,7 +290,7 @@ class AsyncEA:
     def startTest(self, params: Any) -> bool:  # noqa: N802  (:268-285)
         """Receive the next snapshot into params; False when the server stops."""
         self._one_time_init(params)
-        _, m = self._expect(SERVER_RANK, TAG_TEST, TEST, STOP, what="tester waiting for the server")
+        _, m = self._expect(SERVER_RANK, TAG_TEST, TEST, STOP, what="tester waiting for the server", idle=True)
         if m[0] == STOP:
             return False
         self.server_syncs = int(m[3])  # the server's sync count when it took this snapshot

@@ -95,13 +95,20 @@ class Communicator:
             dist.send(buf, dst=dst, group=self.ctrl, tag=tag)
 
     def recv_msg(self, src: Optional[int] = None, tag: int = 0,
-                 timeout: Optional[float] = None) -> Tuple[int, List[int]]:
+                 timeout: Optional[float] = None, unbounded: bool = False) -> Tuple[int, List[int]]:
         """Receive a control message; ``src=None`` = any source (recvAny).
-        ``timeout`` (seconds) bounds the wait; default: the group's timeout."""
+        ``timeout`` (seconds) bounds the wait; default: the group's timeout;
+        ``unbounded``: no time limit (a peer that dies still fails the wait:
+        its connection closes)."""
         buf = torch.zeros(MSG_LEN, dtype=torch.int64)
         what = "receive from " + ("any rank" if src is None else f"rank {src}")
         with _ctrl_errors(what):
-            if timeout is None:
+            if unbounded:
+                work = (dist.irecv(buf, src=src, group=self.ctrl, tag=tag) if src is not None
+                        else self.ctrl.recv_anysource([buf], tag))
+                work.wait(datetime.timedelta(days=365))
+                sender = src if src is not None else work._source_rank()
+            elif timeout is None:
                 sender = dist.recv(buf, src=src, group=self.ctrl, tag=tag)
             else:
                 work = (dist.irecv(buf, src=src, group=self.ctrl, tag=tag) if src is not None
