@@ -57,6 +57,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_apply_head", &bn_bwd_apply_head);
   m.def("combine_bwd_reduce_blocks", &combine_bwd_reduce_blocks);
   m.def("conv_fwd_ex", &conv_fwd_ex);
+  m.def("conv_fwd_bnred", &conv_fwd_bnred);
+  m.def("conv_region_ok", &conv_region_ok);
   m.def("conv_wgrad_ex", &conv_wgrad_ex);
   // ---- ResNet-50 glue (resnet_glue.hip) ------------------------------------------
   m.def("s2d_stem_input", &s2d_stem_input);

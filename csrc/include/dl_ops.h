@@ -58,6 +58,9 @@ void set_conv_region_waves(int w);
 void set_conv_stages(int fwd, int wgrad);
 void set_conv_waves(int waves);
 void set_conv_debug(uintptr_t buf);
+int conv_region_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile);
+int conv_fwd_bnred(uintptr_t x, uintptr_t w, uintptr_t y, int B, int H, int W, int Cin, int Cout, int KS, int tile,
+                   uintptr_t y_prev, uintptr_t coef, uintptr_t rows, uintptr_t stream);
 int conv_fwd_ex(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab, int B, int Ho, int Wo, int Hp,
                 int Wp, int Cin, int Cout, int KH, int KW, int S, int om_S, int om_H0, int om_W0, int om_W, int om_HW,
                 uintptr_t addend, int tile, int splits, uintptr_t stream);

@@ -55,6 +55,21 @@ __device__ __forceinline__ void put_stats(float* __restrict__ stats, int64_t row
   }
 }
 
+// BatchNorm backward reduce fused into a dgrad epilogue (BNRED): the dgrad's
+// output is dP, the gradient of the pooled output of the previous block; for
+// every stored element the epilogue also loads that block's pre-BN values y
+// under the 2x2 pool window, routes dP to the window's argmax of relu(BN(y))
+// and accumulates sum(dz) and sum(dz * xhat) per channel (bn_pool.hip
+// bwd_reduce_body's arithmetic) -- the stand-alone reduce launch, and its
+// re-read of dP, are gone.  rows: mode 0 = one partial row per M tile
+// [T][sum dz (C); sum dz*xhat (C)], atomic modes = R striped rows
+// [R][dgamma = sum dz*xhat (C); dbeta = sum dz (C)] (the layouts of the reduce).
+struct BnRedArgs {
+  const bf16_t* y;     // [B][2Ho][2Wo][C] pre-BN output of the previous block
+  const float* coef;   // [4][C] mean, invstd, scale, shift
+  float* rows;
+};
+
 struct ConvGeom {
   int B, H, W;
   int Hp, Wp;  // spatially zero-padded input dims (H + 2 pad, W + 2 pad)
@@ -383,13 +398,15 @@ __device__ __forceinline__ float row16_sum(float v) {
 // over the 16 pixels of a lane group, then a fixed-order sum over the WM wave
 // rows through LDS (deterministic).  ADD: + a bf16 [M][Cout] addend (16-byte
 // loads), passed through the slab pointer.
-template <int BM, int BN, bool STATS, bool SLAB, int WM, int WN, int FM, int FN, bool ADD = false>
+template <int BM, int BN, bool STATS, bool SLAB, int WM, int WN, int FM, int FN, bool ADD = false, bool BNRED = false>
 __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], const ConvGeom& g,
                                                     bf16_t* __restrict__ y, float* __restrict__ stats,
                                                     float* __restrict__ slab, int split, int tm, int m0, int n0,
-                                                    char* smem, int pm_b0 = 0, int pm_pos = 0) {
+                                                    char* smem, int pm_b0 = 0, int pm_pos = 0,
+                                                    const BnRedArgs br = BnRedArgs{}) {
   constexpr int NT = 64 * WM * WN, TM = BM / WM, TN = BN / WN, NP = FN / 2;
   static_assert(!(ADD && (SLAB || STATS)), "ADD: plain bf16 output only");
+  static_assert(!(BNRED && (SLAB || STATS || ADD)), "BNRED: plain bf16 output only");
   static_assert(FN % 2 == 0, "N fragments pair up");
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = tid >> 6, wm = wid / WN, wn = wid % WN;
@@ -399,6 +416,21 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
   for (int q = 0; q < NP; ++q)
 #pragma unroll
     for (int k = 0; k < 8; ++k) { s1[q][k] = 0.f; s2[q][k] = 0.f; }
+  // BNRED: the lane's channels are fixed per q -- their BN coefficients once
+  float rmu[BNRED ? NP : 1][8], ris[BNRED ? NP : 1][8], rsc[BNRED ? NP : 1][8], rsh[BNRED ? NP : 1][8];
+  if constexpr (BNRED) {
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const int n = n0 + nl + 32 * q;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        rmu[q][k] = br.coef[n + k];
+        ris[q][k] = br.coef[g.Cout + n + k];
+        rsc[q][k] = br.coef[2 * g.Cout + n + k];
+        rsh[q][k] = br.coef[3 * g.Cout + n + k];
+      }
+    }
+  }
 #pragma unroll
   for (int a = 0; a < FM; ++a) {
     const int ml = m0 + wm * TM + a * 16 + (lane & 15);
@@ -428,6 +460,46 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
         const uint4 pk = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
                                     pack_bf16x2(v[6], v[7]));
         if (ok) *reinterpret_cast<uint4*>(y + (int64_t)m * g.Cout + n) = pk;
+        if constexpr (BNRED) {
+          if (ok) {
+            // pooled pixel m = (b, oh, ow) of the [B][H][W] dgrad output; its window in y
+            int rem, ow;
+            const int b = fdivmod(m, g.H * g.W, g.inv_HW, rem);
+            const int oh = fdivmod(rem, g.W, g.inv_W, ow);
+            const int W2 = 2 * g.W;
+            const bf16_t* base = br.y + ((int64_t)(b * 2 * g.H + 2 * oh) * W2 + 2 * ow) * g.Cout + n;
+            const uint4 w0 = *reinterpret_cast<const uint4*>(base);
+            const uint4 w1 = *reinterpret_cast<const uint4*>(base + g.Cout);
+            const uint4 w2 = *reinterpret_cast<const uint4*>(base + (int64_t)W2 * g.Cout);
+            const uint4 w3 = *reinterpret_cast<const uint4*>(base + (int64_t)W2 * g.Cout + g.Cout);
+            const uint4 wv[4] = {w0, w1, w2, w3};
+            const float gd[8] = {lo_bf16(pk.x), hi_bf16(pk.x), lo_bf16(pk.y), hi_bf16(pk.y),
+                                 lo_bf16(pk.z), hi_bf16(pk.z), lo_bf16(pk.w), hi_bf16(pk.w)};
+            float yv[4][8];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+              yv[w][0] = lo_bf16(wv[w].x); yv[w][1] = hi_bf16(wv[w].x); yv[w][2] = lo_bf16(wv[w].y);
+              yv[w][3] = hi_bf16(wv[w].y); yv[w][4] = lo_bf16(wv[w].z); yv[w][5] = hi_bf16(wv[w].z);
+              yv[w][6] = lo_bf16(wv[w].w); yv[w][7] = hi_bf16(wv[w].w);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              float best = -INFINITY;
+              int arg = 0;
+#pragma unroll
+              for (int w = 0; w < 4; ++w) {
+                const float r = fmaxf(fmaf(rsc[q][k], yv[w][k], rsh[q][k]), 0.f);
+                if (r > best) { best = r; arg = w; }
+              }
+#pragma unroll
+              for (int w = 0; w < 4; ++w) {
+                const float dz = (w == arg && best > 0.f) ? gd[k] : 0.f;
+                s1[q][k] += dz;
+                s2[q][k] += dz * (yv[w][k] - rmu[q][k]) * ris[q][k];
+              }
+            }
+          }
+        }
         if constexpr (STATS) {
           const float h[8] = {lo_bf16(pk.x), hi_bf16(pk.x), lo_bf16(pk.y), hi_bf16(pk.y),
                               lo_bf16(pk.z), hi_bf16(pk.z), lo_bf16(pk.w), hi_bf16(pk.w)};
@@ -441,7 +513,7 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
       }
     }
   }
-  if constexpr (STATS && !SLAB) {
+  if constexpr ((STATS || BNRED) && !SLAB) {
 #pragma unroll
     for (int q = 0; q < NP; ++q)
 #pragma unroll
@@ -462,7 +534,13 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
       float sa = 0.f, sb = 0.f;
 #pragma unroll
       for (int q = 0; q < WM; ++q) { sa += red[(q * 2) * BN + c]; sb += red[(q * 2 + 1) * BN + c]; }
-      put_stats(stats, tm, g.Cout, n0 + c, sa, sb);
+      if constexpr (BNRED) {
+        // sa = sum dz, sb = sum dz*xhat; atomic rows hold [dgamma; dbeta] (the reduce's layouts)
+        if (g_red_atomic) put_stats(br.rows, tm, g.Cout, n0 + c, sb, sa);
+        else put_stats(br.rows, tm, g.Cout, n0 + c, sa, sb);
+      } else {
+        put_stats(stats, tm, g.Cout, n0 + c, sa, sb);
+      }
     }
   }
 }
@@ -774,12 +852,13 @@ struct RegionGeom {
 };
 
 
-template <int BN, bool STATS, bool SLAB, int STAGES, int WM, int WN>
+template <int BN, bool STATS, bool SLAB, int STAGES, int WM, int WN, bool BNRED = false>
 __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf16_t* __restrict__ x,
                                                               const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
                                                               float* __restrict__ stats, float* __restrict__ slab,
                                                               const ConvGeom g, const RegionGeom rg, int splits,
-                                                              unsigned long long* dbg, int ablate) {
+                                                              unsigned long long* dbg, int ablate,
+                                                              const BnRedArgs br) {
   const unsigned long long t_start = dbg ? stamp() : 0ull;
   constexpr int BM = 128, BK = 64, CPR = 8, NW = WM * WN, PD = STAGES - 1;
   constexpr int B_BYTES = BN * BK * 2, B_INS = B_BYTES / 1024 / NW, LPS = B_INS;
@@ -977,7 +1056,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf1
   }
   if (i < nk) step(fa0, fb0, fa1, fb1);
   const unsigned long long t_loop = dbg ? stamp() : 0ull;
-  conv_fwd_epilogue_t<128, BN, STATS, SLAB, WM, WN, FM, FN>(acc, g, y, stats, slab, split, tm, m0, n0, smem);
+  conv_fwd_epilogue_t<128, BN, STATS, SLAB, WM, WN, FM, FN, false, BNRED>(acc, g, y, stats, slab, split, tm, m0, n0,
+                                                                          smem, 0, 0, br);
   if (dbg && threadIdx.x == 0) {
     unsigned long long* d = dbg + (size_t)blockIdx.x * 5;
     d[0] = t_start; d[1] = t_issued; d[2] = t_first; d[3] = t_loop; d[4] = stamp();
@@ -1792,6 +1872,7 @@ int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile,
 static uintptr_t g_fwd_addend = 0;  // conv_fwd_add: bf16 [M][Cout] added in the epilogue
 static int g_fwd_slab_cap = 0;      // split-K slab capacity of the current conv_fwd call (FwdCfg)
 static int g_fwd_keep_slabs = 0;    // FwdCfg bit 20: leave the split-K slabs (the caller combines them)
+static BnRedArgs g_bnred{};         // conv_fwd_bnred: fused BN backward reduce (region dgrad only)
 // A/B knob: 0 = the untransposed accumulator layout for the split-K and BN-statistics
 // instances of the streaming kernel (set_conv_fwd_tr)
 static int g_fwd_tr = 1;
@@ -2027,9 +2108,12 @@ static void launch_fwd_region_st(const ConvGeom& g, const RegionGeom& rg, uintpt
       attr = true;
     }
     kern<<<grid, 64 * WM * WN, lds, s>>>((const bf16_t*)x, (const bf16_t*)w, yy, st, sl, g, rg, splits, g_conv_dbg,
-                                         g_region_ablate);
+                                         g_region_ablate, g_bnred);
   };
-  if (splits > 1)
+  if (g_bnred.rows != nullptr) {
+    if (splits > 1 || stats) throw std::runtime_error("conv_fwd_bnred: plain unsplit dgrad only");
+    go(conv_fwd_region_kernel<BN, false, false, ST, WM, WN, true>, (bf16_t*)y, nullptr, nullptr);
+  } else if (splits > 1)
     go(conv_fwd_region_kernel<BN, false, true, ST, WM, WN>, nullptr, nullptr, (float*)slab);
   else if (stats)
     go(conv_fwd_region_kernel<BN, true, false, ST, WM, WN>, (bf16_t*)y, (float*)stats, nullptr);
@@ -2139,6 +2223,38 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
                                                     g);
   DL_HIP_CHECK(hipGetLastError());
   return nb;
+}
+
+// Whether conv_fwd runs this unsplit shape on the region (tap-reuse) kernel --
+// the kernel that carries the fused BN backward reduce epilogue.
+int conv_region_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile) {
+  ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
+  RegionGeom rg;
+  const int t = tile & 15;
+  return (t == 2 && region_geom(g, 64, 1, rg)) || (t == 0 && region_geom(g, 128, 1, rg)) ? 1 : 0;
+}
+
+// conv_fwd (a dgrad) with the previous block's BatchNorm backward reduce in its
+// epilogue (BnRedArgs): only the region kernel path; returns the number of
+// rows written (M tiles, mode 0) or throws if the shape takes another kernel.
+int conv_fwd_bnred(uintptr_t x, uintptr_t w, uintptr_t y, int B, int H, int W, int Cin, int Cout, int KS, int tile,
+                   uintptr_t y_prev, uintptr_t coef, uintptr_t rows, uintptr_t stream) {
+  ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
+  RegionGeom rg;
+  const int t = tile & 15;
+  if (!(t == 2 && region_geom(g, 64, 1, rg)) && !(t == 0 && region_geom(g, 128, 1, rg)))
+    throw std::runtime_error("conv_fwd_bnred: the shape does not take the region kernel");
+  if (!rows || !coef || !y_prev) throw std::runtime_error("conv_fwd_bnred: null operand");
+  g_bnred = BnRedArgs{(const bf16_t*)y_prev, (const float*)coef, (float*)rows};
+  int T;
+  try {
+    T = conv_fwd(x, w, y, 0, 0, B, H, W, Cin, Cout, KS, tile, 1, stream);
+  } catch (...) {
+    g_bnred = BnRedArgs{};
+    throw;
+  }
+  g_bnred = BnRedArgs{};
+  return T;
 }
 
 // y = conv(x, w) + addend (bf16, same layout as y), streaming kernel only

@@ -678,6 +678,41 @@ def test_executor_head_fused_bn_reduce(C, monkeypatch):
     assert float((grads[0] - grads[1]).norm() / grads[0].norm()) < 1e-2
 
 
+@pytest.mark.parametrize("B,atomic", [(128, "0"), (32, "0"), (128, "2")])
+def test_executor_dgrad_bn_reduce_epilogue(C, monkeypatch, B, atomic):
+    """The region dgrad with the previous block's BN backward reduce in its
+    epilogue (conv_fwd_bnred) matches the stand-alone reduce launch to
+    summation-order noise (mode 0: also run-to-run deterministic; mode 2:
+    within the fp32-atomic noise of the path itself)."""
+    from torch_distlearn_amd import FlatParams
+    from torch_distlearn_amd.models import CifarConvNet
+    from torch_distlearn_amd.models.cifar_hip import CifarHIPExecutor
+
+    monkeypatch.setenv("DISTLEARN_REDUCE_ATOMIC", atomic)
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(9)
+    x = torch.randn(B, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)
+    y = torch.randint(0, 10, (B,), device=dev, generator=g)
+    grads = []
+    for on in ("0", "1", "1"):
+        monkeypatch.setenv("DISTLEARN_DGRAD_BNRED", on)
+        mdl = CifarConvNet(seed=4).to(dev)
+        flat = FlatParams(mdl, grads=True, shadow_bf16=True)
+        flat.grad.fill_(float("nan"))
+        ex = CifarHIPExecutor(mdl, flat, max_batch=B)
+        assert ex.dgrad_bnred == (on == "1") and ex._region_dgrad(1, B)
+        ex.forward_backward(x.contiguous(), y)
+        torch.cuda.synchronize()
+        grads.append(torch.cat([v.flatten() for v in flat.views_of(flat.grad)]))
+    assert torch.isfinite(grads[1]).all()
+    rel = lambda a, b: float((a - b).norm() / b.norm())  # noqa: E731
+    if atomic == "0":
+        assert rel(grads[1], grads[0]) < 1e-3
+        assert torch.equal(grads[1], grads[2])
+    else:
+        assert rel(grads[1], grads[0]) < 3 * rel(grads[2], grads[1]) + 1e-3
+
+
 # (B, H, Cin, Cout, tile, splits): position-major tiles (batch a multiple of the
 # 128-row tile, output smaller than the 5x5 kernel): the reference's layer 4
 # forward (4x4, 256 -> 512, split 4) and dgrad (512 -> 256, split 8), a 2x2

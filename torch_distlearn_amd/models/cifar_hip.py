@@ -231,6 +231,9 @@ class CifarHIPExecutor:
         # below (csrc bn_pool.hip combine_bwd_reduce): dP is produced, stored and
         # reduced by one launch (DISTLEARN_FUSE_COMBINE=0: separate kernels, A/B)
         self.fuse_combine = os.environ.get("DISTLEARN_FUSE_COMBINE", "1") == "1"
+        # an unsplit (region-kernel) dgrad runs the BN backward reduce of the block
+        # below in its epilogue (csrc conv_fwd_bnred; DISTLEARN_DGRAD_BNRED=0: A/B)
+        self.dgrad_bnred = os.environ.get("DISTLEARN_DGRAD_BNRED", "1") == "1"
         self.atomic = self.mode > 0             # BN statistics / gradients by atomics, no finalize kernels
         self.head_reduce = (os.environ.get("DISTLEARN_HEAD_REDUCE", "1") == "1" and self.mode == 2 and self.head_pool
                             and self.head_wgrad_fused and self.couts[-1] == 512)
@@ -292,7 +295,9 @@ class CifarHIPExecutor:
             self.bwd_blocks.append(g)
             # (mode 0) partial rows of the BN backward reduce -- or of the fused
             # split-K combine + reduce, which writes one row per combine block
-            gp = max(g, C.combine_bwd_reduce_blocks(B, h, h, cout)) if i + 1 < self.nb else g
+            # ... or of the next block's dgrad with the reduce in its epilogue (one row per M tile)
+            gp = max(g, C.combine_bwd_reduce_blocks(B, h, h, cout), (B * (h // 2) * (h // 2) + 127) // 128) \
+                if i + 1 < self.nb else g
             self.bwd_part.append(None if self.atomic else torch.empty(gp, 2, cout, device=d))
             tile_w, splits_w = _wgrad_plan(cout, K, M, self.cu_reserve)
             direct = splits_w == 1 and cin == self.cins_real[i]
@@ -470,6 +475,7 @@ class CifarHIPExecutor:
         merge = self.merge_slab and not (self.side_wgrad or self.side_reduce)
         pending = None  # (slab args, block) of a weight gradient whose slab reduce rides the next BN reduce
         dp_splits = 0   # > 0: dP[i] is still in the split-K slabs of block i+1's dgrad (fused combine)
+        dp_reduced = 0  # > 0: block i+1's dgrad epilogue already reduced dP[i] (rows written)
         for i in reversed(range(self.nb)):
             T = self.bwd_blocks[i]  # partial rows written by this block's backward reduce
             h, cin, cout = self.hs[i], self.cins[i], self.couts[i]
@@ -481,6 +487,9 @@ class CifarHIPExecutor:
             part = {0: self.bwd_part[i], 1: self.g32[self._leaf(i, 2)], 2: self.bwd_rows[i]}[self.mode]
             if i == self.nb - 1 and self.head_reduce:
                 pass  # reduced inside the head kernel; the classifier wgrad rides the apply launch
+            elif dp_reduced:
+                T = dp_reduced  # reduced in block i+1's dgrad epilogue
+                dp_reduced = 0
             elif i == self.nb - 1 and self.head_wgrad_fused:
                 # one launch: this block's BN backward reduce + the classifier weight gradient
                 C.bn_bwd_reduce_head(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
@@ -568,15 +577,30 @@ class CifarHIPExecutor:
                 if self.dgrad_stages != 3:
                     C.set_conv_stages(self.dgrad_stages, self._wgrad_stages)
                 keep = self.fuse_combine and ds in (2, 4, 8) and not (merge and pending is not None)
-                C.conv_fwd(dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), 0,
-                           self.slabs.data_ptr(), B, h, h, cout, cin, KSIZE,
-                           dt | _slab_cap_bits(ds) | ((1 << 20) if keep else 0), ds, s)
+                bnred = (self.dgrad_bnred and ds == 1 and not keep and self._region_dgrad(i, B)
+                         and not (merge and pending is not None))
+                if bnred:
+                    prt = {0: self.bwd_part[i - 1], 1: self.g32[self._leaf(i - 1, 2)], 2: self.bwd_rows[i - 1]}[self.mode]
+                    dp_reduced = C.conv_fwd_bnred(dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), B,
+                                                  h, h, cout, cin, KSIZE, dt, self.y[i - 1].data_ptr(),
+                                                  self.coef[i - 1].data_ptr(), prt.data_ptr(), s)
+                else:
+                    C.conv_fwd(dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), 0,
+                               self.slabs.data_ptr(), B, h, h, cout, cin, KSIZE,
+                               dt | _slab_cap_bits(ds) | ((1 << 20) if keep else 0), ds, s)
                 dp_splits = ds if keep else 0
                 if self.dgrad_stages != 3:
                     C.set_conv_stages(3, self._wgrad_stages)
         if self.side_wgrad or self.side_reduce:
             main.wait_stream(side)  # join
         return self.loss[0]
+
+    def _region_dgrad(self, i: int, B: int) -> bool:
+        """Whether block i's (unsplit) dgrad runs on the region (tap-reuse)
+        kernel, the one with the fused BN-reduce epilogue (asked from the
+        native dispatch, csrc conv_region_ok)."""
+        h, cout, cin = self.hs[i], self.couts[i], self.cins[i]
+        return bool(self.C.conv_region_ok(B, h, h, cout, cin, KSIZE, self.dgrad_plan[i][0]))
 
     def _set_mode(self) -> None:
         """The reduction mode lives in device globals shared by every executor
