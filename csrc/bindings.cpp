@@ -29,7 +29,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_bn_reduce_blocks", &set_bn_reduce_blocks);
   m.def("bn_rows_reduce", &bn_rows_reduce);
   m.def("bn_nhwc_fwd_pad", &bn_nhwc_fwd_pad);
-  m.def("bn_nhwc_bwd_pad", &bn_nhwc_bwd_pad);
+  m.def("bn_nhwc_bwd_pad", &bn_nhwc_bwd_pad, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("save"),
+        py::arg("w"), py::arg("b"), py::arg("acc"), py::arg("dx"), py::arg("dres"), py::arg("dw"), py::arg("db"),
+        py::arg("M"), py::arg("C"), py::arg("relu"), py::arg("H"), py::arg("W"), py::arg("opad"), py::arg("stream"),
+        py::arg("have_sums") = 0);
   m.def("zero_border_nhwc", &zero_border_nhwc);
   m.def("gather_normalize", &gather_normalize);
 
@@ -59,6 +62,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_fwd_ex", &conv_fwd_ex);
   m.def("conv_fwd_bnred", &conv_fwd_bnred);
   m.def("conv_region_ok", &conv_region_ok);
+  m.def("set_conv_bn_reduce", &set_conv_bn_reduce, py::arg("x"), py::arg("save"), py::arg("w"), py::arg("b"),
+        py::arg("rows"), py::arg("ym") = 0);
   m.def("conv_wgrad_ex", &conv_wgrad_ex);
   // ---- ResNet-50 glue (resnet_glue.hip) ------------------------------------------
   m.def("s2d_stem_input", &s2d_stem_input);

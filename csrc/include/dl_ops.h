@@ -28,7 +28,7 @@ void bn_nhwc_fwd_pad(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uin
                      double momentum, int relu, int have_stats, int H, int W, int opad, uintptr_t stream);
 void bn_nhwc_bwd_pad(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b,
                      uintptr_t acc, uintptr_t dx, uintptr_t dres, uintptr_t dw, uintptr_t db, int64_t M, int C,
-                     int relu, int H, int W, int opad, uintptr_t stream);
+                     int relu, int H, int W, int opad, uintptr_t stream, int have_sums = 0);
 void zero_border_nhwc(uintptr_t buf, int N, int H, int W, int C, int pad, uintptr_t stream);
 void bn_nhwc_fwd(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b, uintptr_t save,
                  uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps, double momentum, int relu, int have_stats,
@@ -58,6 +58,7 @@ void set_conv_region_waves(int w);
 void set_conv_stages(int fwd, int wgrad);
 void set_conv_waves(int waves);
 void set_conv_debug(uintptr_t buf);
+void set_conv_bn_reduce(uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, uintptr_t rows, uintptr_t ym = 0);
 int conv_region_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile);
 int conv_fwd_bnred(uintptr_t x, uintptr_t w, uintptr_t y, int B, int H, int W, int Cin, int Cout, int KS, int tile,
                    uintptr_t y_prev, uintptr_t coef, uintptr_t rows, uintptr_t stream);

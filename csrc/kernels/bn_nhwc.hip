@@ -493,19 +493,24 @@ void bn_nhwc_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr
   bn_nhwc_bwd_pad(dy, y, x, save, w, b, acc, dx, dres, dw, db, M, C, relu, 1, 1, 0, stream);
 }
 
-// dx in the padded layout [N][H+2opad][W+2opad][C] (interior only)
+// dx in the padded layout [N][H+2opad][W+2opad][C] (interior only).
+// have_sums: acc already holds sum(g), sum(g*xhat) -- computed by the epilogue
+// of the convolution that produced dy (conv_igemm.hip set_conv_bn_reduce,
+// ops/conv.py): the reduce pass over dy and x is skipped.
 void bn_nhwc_bwd_pad(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b,
                      uintptr_t acc, uintptr_t dx, uintptr_t dres, uintptr_t dw, uintptr_t db, int64_t M, int C,
-                     int relu, int H, int W, int opad, uintptr_t stream) {
+                     int relu, int H, int W, int opad, uintptr_t stream, int have_sums) {
   dim3 grid, grid_r;
   BnGeom g = make_geom(M, C, &grid);
   set_out_pad(g, H, W, opad);
-  const BnGeom gr = make_geom(M, C, &grid_r, g_reduce_blocks);
   hipStream_t s = as_stream(stream);
-  bn_nhwc_bwd_reduce_kernel<<<grid_r, kThreads, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x,
-                                                         (const float*)save, (const float*)w, (const float*)b, gr,
-                                                         relu, (float*)acc);
-  DL_HIP_CHECK(hipGetLastError());
+  if (!have_sums) {
+    const BnGeom gr = make_geom(M, C, &grid_r, g_reduce_blocks);
+    bn_nhwc_bwd_reduce_kernel<<<grid_r, kThreads, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x,
+                                                           (const float*)save, (const float*)w, (const float*)b, gr,
+                                                           relu, (float*)acc);
+    DL_HIP_CHECK(hipGetLastError());
+  }
   bn_nhwc_bwd_apply_kernel<<<grid, kThreads, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x,
                                                       (const float*)save, (const float*)w, (const float*)b,
                                                       (const float*)acc, g, relu,

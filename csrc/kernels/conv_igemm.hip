@@ -64,10 +64,23 @@ __device__ __forceinline__ void put_stats(float* __restrict__ stats, int64_t row
 // re-read of dP, are gone.  rows: mode 0 = one partial row per M tile
 // [T][sum dz (C); sum dz*xhat (C)], atomic modes = R striped rows
 // [R][dgamma = sum dz*xhat (C); dbeta = sum dz (C)] (the layouts of the reduce).
+// BNR == 2 (ResNet-50 channels-last BatchNorm, no pool): the dgrad output is
+// the gradient dz of a BN(+ReLU) output whose input x has the output's layout;
+// g = dz * (x*scale + shift > 0) and sum(g), sum(g * xhat) per channel go to
+// deterministic partial rows [T][sum g (C); sum g*xhat (C)] (one per M tile,
+// reduced by bn_rows_reduce into the BatchNorm's backward accumulator) --
+// bn_nhwc_bwd_reduce_kernel's arithmetic (relu mode 2), fused.
+// BNR == 3: the same for a BN + residual + ReLU output (relu mode 1: the mask
+// is out > 0 of the saved block output `ym`); the dgrad is the next block's c1
+// with the residual gradient added in the epilogue (ADD), so dz is complete.
 struct BnRedArgs {
-  const bf16_t* y;     // [B][2Ho][2Wo][C] pre-BN output of the previous block
-  const float* coef;   // [4][C] mean, invstd, scale, shift
+  const bf16_t* y;     // BNR 1: [B][2Ho][2Wo][C] pre-BN output of the previous block; BNR 2: x [M][C]
+  const float* coef;   // BNR 1: [4][C] mean, invstd, scale, shift
   float* rows;
+  const float* save;   // BNR 2: [2][C] mean, invstd
+  const float* w;      // BNR 2: gamma
+  const float* b;      // BNR 2: beta
+  const bf16_t* ym;    // BNR 3: block output [M][C] (ReLU mask)
 };
 
 struct ConvGeom {
@@ -398,7 +411,7 @@ __device__ __forceinline__ float row16_sum(float v) {
 // over the 16 pixels of a lane group, then a fixed-order sum over the WM wave
 // rows through LDS (deterministic).  ADD: + a bf16 [M][Cout] addend (16-byte
 // loads), passed through the slab pointer.
-template <int BM, int BN, bool STATS, bool SLAB, int WM, int WN, int FM, int FN, bool ADD = false, bool BNRED = false>
+template <int BM, int BN, bool STATS, bool SLAB, int WM, int WN, int FM, int FN, bool ADD = false, int BNR = 0>
 __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], const ConvGeom& g,
                                                     bf16_t* __restrict__ y, float* __restrict__ stats,
                                                     float* __restrict__ slab, int split, int tm, int m0, int n0,
@@ -406,7 +419,9 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
                                                     const BnRedArgs br = BnRedArgs{}) {
   constexpr int NT = 64 * WM * WN, TM = BM / WM, TN = BN / WN, NP = FN / 2;
   static_assert(!(ADD && (SLAB || STATS)), "ADD: plain bf16 output only");
-  static_assert(!(BNRED && (SLAB || STATS || ADD)), "BNRED: plain bf16 output only");
+  constexpr bool BNRED = BNR != 0;
+  static_assert(!(BNRED && (SLAB || STATS)) && !(BNR == 1 && ADD) && !(BNR == 3 && !ADD),
+                "BNRED: plain bf16 output (BNR 3: with the residual addend)");
   static_assert(FN % 2 == 0, "N fragments pair up");
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = tid >> 6, wm = wid / WN, wn = wid % WN;
@@ -418,7 +433,7 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
     for (int k = 0; k < 8; ++k) { s1[q][k] = 0.f; s2[q][k] = 0.f; }
   // BNRED: the lane's channels are fixed per q -- their BN coefficients once
   float rmu[BNRED ? NP : 1][8], ris[BNRED ? NP : 1][8], rsc[BNRED ? NP : 1][8], rsh[BNRED ? NP : 1][8];
-  if constexpr (BNRED) {
+  if constexpr (BNR == 1) {
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
       const int n = n0 + nl + 32 * q;
@@ -428,6 +443,18 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
         ris[q][k] = br.coef[g.Cout + n + k];
         rsc[q][k] = br.coef[2 * g.Cout + n + k];
         rsh[q][k] = br.coef[3 * g.Cout + n + k];
+      }
+    }
+  } else if constexpr (BNR == 2 || BNR == 3) {
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const int n = n0 + nl + 32 * q;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {  // bn_nhwc: sc = w*invstd, sh = fma(-mean, sc, b)
+        rmu[q][k] = br.save[n + k];
+        ris[q][k] = br.save[g.Cout + n + k];
+        rsc[q][k] = br.w[n + k] * ris[q][k];
+        rsh[q][k] = fmaf(-rmu[q][k], rsc[q][k], br.b[n + k]);
       }
     }
   }
@@ -460,7 +487,27 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
         const uint4 pk = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
                                     pack_bf16x2(v[6], v[7]));
         if (ok) *reinterpret_cast<uint4*>(y + (int64_t)m * g.Cout + n) = pk;
-        if constexpr (BNRED) {
+        if constexpr (BNR == 2 || BNR == 3) {
+          if (ok) {
+            const uint4 xv4 = *reinterpret_cast<const uint4*>(br.y + (int64_t)m * g.Cout + n);
+            uint4 mv4 = xv4;
+            if constexpr (BNR == 3) mv4 = *reinterpret_cast<const uint4*>(br.ym + (int64_t)m * g.Cout + n);
+            const float mv[8] = {lo_bf16(mv4.x), hi_bf16(mv4.x), lo_bf16(mv4.y), hi_bf16(mv4.y),
+                                 lo_bf16(mv4.z), hi_bf16(mv4.z), lo_bf16(mv4.w), hi_bf16(mv4.w)};
+            const float gd[8] = {lo_bf16(pk.x), hi_bf16(pk.x), lo_bf16(pk.y), hi_bf16(pk.y),
+                                 lo_bf16(pk.z), hi_bf16(pk.z), lo_bf16(pk.w), hi_bf16(pk.w)};
+            const float xv[8] = {lo_bf16(xv4.x), hi_bf16(xv4.x), lo_bf16(xv4.y), hi_bf16(xv4.y),
+                                 lo_bf16(xv4.z), hi_bf16(xv4.z), lo_bf16(xv4.w), hi_bf16(xv4.w)};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const bool pos = BNR == 3 ? mv[k] > 0.f : fmaf(xv[k], rsc[q][k], rsh[q][k]) > 0.f;
+              const float gk = pos ? gd[k] : 0.f;
+              s1[q][k] += gk;
+              s2[q][k] = fmaf(gk, (xv[k] - rmu[q][k]) * ris[q][k], s2[q][k]);
+            }
+          }
+        }
+        if constexpr (BNR == 1) {
           if (ok) {
             // pooled pixel m = (b, oh, ow) of the [B][H][W] dgrad output; its window in y
             int rem, ow;
@@ -534,7 +581,10 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
       float sa = 0.f, sb = 0.f;
 #pragma unroll
       for (int q = 0; q < WM; ++q) { sa += red[(q * 2) * BN + c]; sb += red[(q * 2 + 1) * BN + c]; }
-      if constexpr (BNRED) {
+      if constexpr (BNR >= 2) {  // deterministic partial row per M tile (bn_rows_reduce follows)
+        br.rows[(int64_t)tm * 2 * g.Cout + n0 + c] = sa;
+        br.rows[(int64_t)tm * 2 * g.Cout + g.Cout + n0 + c] = sb;
+      } else if constexpr (BNR == 1) {
         // sa = sum dz, sb = sum dz*xhat; atomic rows hold [dgamma; dbeta] (the reduce's layouts)
         if (g_red_atomic) put_stats(br.rows, tm, g.Cout, n0 + c, sb, sa);
         else put_stats(br.rows, tm, g.Cout, n0 + c, sa, sb);
@@ -563,11 +613,12 @@ __device__ __forceinline__ int b_frag_row(int b, int i) { return 32 * (b >> 1) +
 // 3-stage LDS ring filled by LDS-DMA, one barrier per K step.
 // --------------------------------------------------------------------------
 template <int BM, int BN, bool STATS, bool SLAB, bool TAPU, int STAGES, int WM = 2, int WN = 2, bool ADD = false,
-          bool TRP = true>
+          bool TRP = true, int BNR = 0>
 __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                        bf16_t* __restrict__ y, float* __restrict__ stats,
                                                        float* __restrict__ slab, const ConvGeom g, int splits,
-                                                       int kt_per_split, unsigned long long* dbg) {
+                                                       int kt_per_split, unsigned long long* dbg,
+                                                       const BnRedArgs br = BnRedArgs{}) {
   // x is the SPATIALLY ZERO-PADDED input [B][Hp][Wp][Cin]: every tap of every
   // output pixel is in bounds, so an activation load is (per-lane pixel base)
   // + (wave-uniform tap offset) with no bounds test.  Cout % BN == 0
@@ -813,9 +864,10 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
       d[0] = t_start; d[1] = t_setup; d[2] = t_loop; d[3] = stamp();
     }
   };
+  static_assert(BNR == 0 || TR, "the fused BN reduce needs the transposed epilogue");
   if constexpr (TR)
-    conv_fwd_epilogue_t<BM, BN, STATS, SLAB, WM, WN, FM, FN, ADD>(acc, g, y, stats, slab, split, tm, m0, n0, smem,
-                                                                  pm_b0, pm_pos);
+    conv_fwd_epilogue_t<BM, BN, STATS, SLAB, WM, WN, FM, FN, ADD, BNR>(acc, g, y, stats, slab, split, tm, m0, n0, smem,
+                                                                       pm_b0, pm_pos, br);
   else
     conv_fwd_epilogue<BM, BN, STATS, SLAB, WM, WN, ADD>(acc, g, y, stats, slab, split, tm, m0, n0, smem, pm_b0,
                                                         pm_pos);
@@ -1056,8 +1108,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf1
   }
   if (i < nk) step(fa0, fb0, fa1, fb1);
   const unsigned long long t_loop = dbg ? stamp() : 0ull;
-  conv_fwd_epilogue_t<128, BN, STATS, SLAB, WM, WN, FM, FN, false, BNRED>(acc, g, y, stats, slab, split, tm, m0, n0,
-                                                                          smem, 0, 0, br);
+  conv_fwd_epilogue_t<128, BN, STATS, SLAB, WM, WN, FM, FN, false, BNRED ? 1 : 0>(acc, g, y, stats, slab, split, tm,
+                                                                                 m0, n0, smem, 0, 0, br);
   if (dbg && threadIdx.x == 0) {
     unsigned long long* d = dbg + (size_t)blockIdx.x * 5;
     d[0] = t_start; d[1] = t_issued; d[2] = t_first; d[3] = t_loop; d[4] = stamp();
@@ -1873,6 +1925,7 @@ static uintptr_t g_fwd_addend = 0;  // conv_fwd_add: bf16 [M][Cout] added in the
 static int g_fwd_slab_cap = 0;      // split-K slab capacity of the current conv_fwd call (FwdCfg)
 static int g_fwd_keep_slabs = 0;    // FwdCfg bit 20: leave the split-K slabs (the caller combines them)
 static BnRedArgs g_bnred{};         // conv_fwd_bnred: fused BN backward reduce (region dgrad only)
+static BnRedArgs g_bnred2{};        // set_conv_bn_reduce: NHWC BN backward reduce in the streaming epilogue
 // A/B knob: 0 = the untransposed accumulator layout for the split-K and BN-statistics
 // instances of the streaming kernel (set_conv_fwd_tr)
 static int g_fwd_tr = 1;
@@ -1922,7 +1975,7 @@ static void plan_posm_balance(ConvGeom& g, int BM, int ntn, int splits, int cap)
 template <int BM, int BN, bool TAPU, int ST, int WM, int WN>
 static void launch_fwd_w(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
                          uintptr_t slab, int splits, hipStream_t s) {
-  g.posm = (g_posm && TAPU && !g_fwd_addend && g.B % BM == 0 && (g.H < g.KS || g.W < g.KS) && g.S == 1 && !g.om &&
+  g.posm = (g_posm && TAPU && !g_fwd_addend && !g_bnred2.rows && g.B % BM == 0 && (g.H < g.KS || g.W < g.KS) && g.S == 1 && !g.om &&
             g.KH == g.KS && g.KW == g.KS && g.Hp == g.H + 2 * g.pad && g.Wp == g.W + 2 * g.pad) ? 1 : 0;
   const int ntm = (g.M + BM - 1) / BM, ntn = (g.Cout + BN - 1) / BN;
   plan_posm_balance(g, BM, ntn, splits, g_fwd_slab_cap);
@@ -1931,7 +1984,22 @@ static void launch_fwd_w(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uin
   const int grid = g.pm_kmax > 0 ? ntn * g.pm_P : ntm * ntn * splits;
   constexpr int NT = 64 * WM * WN;
   if (g_fwd_addend && (splits > 1 || stats)) throw std::runtime_error("conv_fwd_add: no split-K / statistics");
-  if (g_fwd_addend)
+  if (g_bnred2.rows != nullptr) {
+    if (splits > 1 || stats) throw std::runtime_error("conv BN reduce: plain unsplit output only");
+    if ((g_bnred2.ym != nullptr) != (g_fwd_addend != 0))
+      throw std::runtime_error("conv BN reduce: the output-mask form (relu 1) goes with the residual addend");
+    if constexpr ((BN / WN / 16) % 2 == 0) {  // the transposed epilogue (paired N fragments)
+      if (g_fwd_addend)
+        conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, true, true, 3><<<grid, NT, 0, s>>>(
+            (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, (float*)g_fwd_addend, g, 1, ktps, g_conv_dbg,
+            g_bnred2);
+      else
+        conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, false, true, 2><<<grid, NT, 0, s>>>(
+            (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, nullptr, g, 1, ktps, g_conv_dbg, g_bnred2);
+    } else {
+      throw std::runtime_error("conv BN reduce: tile without the transposed epilogue");
+    }
+  } else if (g_fwd_addend)
     conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, true><<<grid, NT, 0, s>>>(
         (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, (float*)g_fwd_addend, g, 1, ktps, g_conv_dbg);
   else if (splits > 1 && !g_fwd_tr)
@@ -2181,7 +2249,8 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
   const int c8_rows = c8_mt * 128 / std::max(1, W) + KS - 1;
   const size_t c8_lds =
       (size_t)((c8_rows * g.Wp + 1 + 63) / 64 * 64 + (64 * KS * KS + 63) / 64 * 64) * 16 + 4 * 2 * 64 * 4;
-  if (tile == 2 && splits == 1 && g_region && g.pow2 && Cin == 8 && W <= 128 && 128 % W == 0 && (H * W) % 128 == 0 &&
+  const bool streaming_only = g_bnred2.rows != nullptr;  // the NHWC BN reduce epilogue is on the streaming kernel
+  if (!streaming_only && tile == 2 && splits == 1 && g_region && g.pow2 && Cin == 8 && W <= 128 && 128 % W == 0 && (H * W) % 128 == 0 &&
       Cout % 64 == 0 && c8_lds <= 160 * 1024) {
     const int grid = (g.M / 128 / c8_mt) * (Cout / 64);
     auto go = [&](auto kern) {
@@ -2195,10 +2264,10 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
     };
     if (stats) go(conv_fwd_c8_kernel<true>);
     else go(conv_fwd_c8_kernel<false>);
-  } else if (tile == 0 && region_geom(g, 128, splits, rg)) {
+  } else if (!streaming_only && tile == 0 && region_geom(g, 128, splits, rg)) {
     if (g_region_waves == 4) launch_fwd_region<128, 2, 2>(g, rg, x, w, y, stats, slab, splits, s);
     else launch_fwd_region<128, 2, 4>(g, rg, x, w, y, stats, slab, splits, s);
-  } else if (tile == 2 && region_geom(g, 64, splits, rg)) {
+  } else if (!streaming_only && tile == 2 && region_geom(g, 64, splits, rg)) {
     if (g_region_waves == 4) launch_fwd_region<64, 2, 2>(g, rg, x, w, y, stats, slab, splits, s);
     else launch_fwd_region<64, 4, 2>(g, rg, x, w, y, stats, slab, splits, s);
   }
@@ -2223,6 +2292,18 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
                                                     g);
   DL_HIP_CHECK(hipGetLastError());
   return nb;
+}
+
+// Arm (rows != 0) / disarm (rows == 0) the channels-last BatchNorm backward
+// reduce (BnRedArgs, BNR 2) for the following conv_fwd / conv_fwd_ex calls on
+// the streaming kernel: x = the BN's input [M][C] (the conv output's layout),
+// save = its [mean; invstd], w / b = gamma / beta, rows = [T][2][C] partials;
+// ym != 0: the ReLU mask is ym > 0 (BN + residual + ReLU, BNR 3; the call
+// must be a conv_fwd_add, whose addend completes the gradient).
+void set_conv_bn_reduce(uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, uintptr_t rows, uintptr_t ym) {
+  g_bnred2 = rows ? BnRedArgs{(const bf16_t*)x, nullptr, (float*)rows, (const float*)save, (const float*)w,
+                              (const float*)b, (const bf16_t*)ym}
+                  : BnRedArgs{};
 }
 
 // Whether conv_fwd runs this unsplit shape on the region (tap-reuse) kernel --

@@ -294,10 +294,14 @@ class DeviceLoader:
 # sources
 # ---------------------------------------------------------------------------
 def synthetic_images(n: int, hw: int, c: int, num_classes: int = 10, seed: int = 0):
-    """Deterministic class-dependent uint8 images (learnable, not pure noise)."""
+    """Deterministic class-dependent uint8 images (learnable, not pure noise).
+    The class prototypes do not depend on ``seed`` (only labels and noise
+    do), so a train split and a test split drawn with different seeds share
+    their classes and test accuracy measures generalisation."""
     g = torch.Generator().manual_seed(seed)
     labels = torch.randint(0, num_classes, (n,), generator=g)
-    proto = torch.randint(0, 256, (num_classes, hw, hw, c), generator=g, dtype=torch.int32)
+    gp = torch.Generator().manual_seed(0x5EED0 + num_classes * 1000 + hw * 10 + c)
+    proto = torch.randint(0, 256, (num_classes, hw, hw, c), generator=gp, dtype=torch.int32)
     noise = torch.randint(-48, 49, (n, hw, hw, c), generator=g, dtype=torch.int32)
     imgs = (proto[labels] + noise).clamp_(0, 255).to(torch.uint8)
     return imgs, labels

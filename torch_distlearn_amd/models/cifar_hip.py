@@ -50,6 +50,10 @@ SPAD = KSIZE // 2  # spatial zero border of every convolution input (written onc
 _FWD_TILES = {0: (128, 128), 1: (64, 64), 2: (128, 64)}
 _NOSPLIT_128x64 = os.environ.get("DISTLEARN_FWD_NOSPLIT", "1") == "1"
 _NOSPLIT_64 = os.environ.get("DISTLEARN_FWD_NOSPLIT64", "0") == "1"
+# split-K layers on 128x64 tiles with half the splits (fwd4 / dgrad4 at batch 128): half
+# the fp32 slab bytes written and combined, twice the workgroups per split;
+# 0.3306 vs 0.3347 ms/step (profiles/r3_split128x64_ab.txt)
+_SPLIT_128x64 = os.environ.get("DISTLEARN_SPLIT_128x64", "1") == "1"
 
 
 # The fwd/dgrad split-K slab holds SLAB_CAP x splits slices, announced to
@@ -79,6 +83,8 @@ def _fwd_plan(M: int, N: int, K: int):
         # 128x64 tiles already fill the chip without a K split: no slab round
         # trip and no combine launch (fwd3 at batch 128: 28.5 -> 24.7 us)
         return 2, 1
+    if splits > 1 and tile == 0 and _SPLIT_128x64:
+        return 2, max(1, splits // 2)
     if splits > 1 and _NOSPLIT_64 and (M // 64) * (N // 64) >= 256 and M % 64 == 0 and N % 64 == 0:
         # 64x64 tiles fill the chip without a K split: no fp32 slab round trip
         # and no combine launch, at twice the LDS traffic per MFMA (A/B knob)

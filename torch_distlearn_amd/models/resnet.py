@@ -58,7 +58,7 @@ class _BN(nn.Module):
             residual is None or (residual.dtype == x.dtype and residual.shape == x.shape))
 
     def act(self, x, relu: bool = True, residual=None, acc=None, res_sink=None, have_stats: bool = False,
-            out_pad: int = 0, dx_pad: int = 0):
+            out_pad: int = 0, dx_pad: int = 0, bn_link=None):
         """act(BN(x) [+ residual]); one fused HIP kernel pair in "hip" mode
         (``acc`` with ``have_stats``: statistics already accumulated by the
         producing conv; else the step's zeroed arena slice, if any;
@@ -70,7 +70,7 @@ class _BN(nn.Module):
                 acc, have_stats = self.acc, False
             return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual, relu, acc=acc,
                           grads=self.bind, res_sink=res_sink, have_stats=have_stats if acc is not None else None,
-                          out_pad=out_pad, dx_pad=dx_pad)
+                          out_pad=out_pad, dx_pad=dx_pad, bn_link=bn_link)
         y = self(x)
         if residual is not None:
             y = y + residual
@@ -106,6 +106,13 @@ _STRIDED_HIP = os.environ.get("DISTLEARN_RESNET_STRIDED", "1") == "1"
 # classifier (mean + Linear + LogSoftMax + NLL, forward and backward) in one node on the
 # MFMA kernels (ops/head.py; 0 = torch mean / hipBLAS linear / torch log-softmax)
 _HEAD_HIP = os.environ.get("DISTLEARN_RESNET_HEAD", "hip") == "hip"
+# the BatchNorm backward sums (sum g, sum g*xhat) from the epilogue of the dgrad that
+# produces the BN's output gradient (b1 / b2: the c2 / c3 dgrads; b3: the next block's
+# c1 dgrad, which adds the residual gradient) instead of the BN's reduce pass over dz
+# and x (ops/conv.py _bn_reduce_begin).  Off: the epilogue's extra read of x costs the
+# dgrads what the reduce pass saves -- every ResNet-50 BN kernel already streams at
+# ~5.5 TB/s, so a fusion only pays if it removes bytes (profiles/r3_resnet_bn_dgrad_ab.txt)
+_BN_DGRAD = os.environ.get("DISTLEARN_RESNET_BN_DGRAD", "0") == "1"
 
 
 class _Conv(nn.Module):
@@ -153,32 +160,35 @@ class _Conv(nn.Module):
 
         return conv3x3_supported(shape, self.weight.shape[0])
 
-    def forward(self, x, stats=None, res_link=None, dx_sink=None):
+    def forward(self, x, stats=None, res_link=None, dx_sink=None, bn_link=None):
         """``stats``: optional fp32 [2*Cout] that receives the output's
         per-channel sum / sum of squares (HIP GEMM path only); ``res_link``:
         a dict through which another branch hands over its gradient of the
         same input (added in the dgrad epilogue); ``dx_sink``: the dict that
-        receives THIS conv's input gradient instead of autograd."""
+        receives THIS conv's input gradient instead of autograd; ``bn_link``:
+        the dict of the BatchNorm that produced ``x`` (its backward sums come
+        from this conv's dgrad epilogue)."""
         b = self.bind
         if b is None or not x.is_cuda or x.dtype != torch.bfloat16:
             return F.conv2d(x, self.weight.to(x.dtype), None, self.stride, self.pad)
         from ..ops.conv import Conv1x1, ShadowConv
 
         # the same HIP kernels in training and in eval / predict (no-grad) mode
+        grad = torch.is_grad_enabled()
         if self.hip_gemm(x):
-            return Conv1x1.apply(x, self.weight, b, stats, res_link if torch.is_grad_enabled() else None,
-                                 dx_sink if torch.is_grad_enabled() else None)
+            return Conv1x1.apply(x, self.weight, b, stats, res_link if grad else None, dx_sink if grad else None,
+                                 bn_link if grad else None)
         if self.hip_3x3(x) and dx_sink is None:
             from ..ops.conv import Conv3x3
 
-            return Conv3x3.apply(x, self.weight, b, stats)
+            return Conv3x3.apply(x, self.weight, b, stats, bn_link if grad else None)
         if self.hip_strided(x):
             from ..ops.conv import Conv1x1S2, Conv3x3S2, StemConv
 
             if self.k == 7:
                 return StemConv.apply(x, self.weight, b, stats)
             if self.k == 3 and dx_sink is None:
-                return Conv3x3S2.apply(x, self.weight, b, stats)
+                return Conv3x3S2.apply(x, self.weight, b, stats, bn_link if grad else None)
             if self.k == 1:
                 return Conv1x1S2.apply(x, self.weight, b, stats, dx_sink if torch.is_grad_enabled() else None)
         if not torch.is_grad_enabled():
@@ -188,13 +198,16 @@ class _Conv(nn.Module):
 
 
 def _conv_bn(conv: _Conv, bn: "_BN", x, relu: bool = True, residual=None, link=None, res_sink=None, dx_sink=None,
-             out_pad: int = 0, dx_pad: int = 0):
+             out_pad: int = 0, dx_pad: int = 0, in_link=None, out_link=None):
     """bn.act(conv(x)) with the BatchNorm statistics produced by the conv's
     epilogue when both run on the HIP kernels (one full read of the conv
     output fewer per BatchNorm).  ``out_pad`` / ``dx_pad``: the BatchNorm writes
-    its output / input gradient zero-bordered (for a Conv3x3 neighbour)."""
-    kw = {"res_link": link, "dx_sink": dx_sink} if conv.bind is not None else {}
-    pads = {"out_pad": out_pad, "dx_pad": dx_pad}
+    its output / input gradient zero-bordered (for a Conv3x3 neighbour).
+    ``in_link``: the bn_link of the BatchNorm that produced ``x`` (the conv's
+    dgrad epilogue computes its backward sums); ``out_link``: this
+    BatchNorm's own bn_link, for the next conv."""
+    kw = {"res_link": link, "dx_sink": dx_sink, "bn_link": in_link} if conv.bind is not None else {}
+    pads = {"out_pad": out_pad, "dx_pad": dx_pad, "bn_link": out_link}
     if _FUSE_STATS and (conv.hip_gemm(x) or conv.hip_3x3(x) or conv.hip_strided(x)) and _BN_MODE == "hip" \
             and bn.training:
         from .._native import native
@@ -221,6 +234,12 @@ class _Bottleneck(nn.Module):
             self.down = nn.ModuleList([_Conv(cin, cout, 1, stride, g), _BN(cout)])
 
     def forward(self, x):
+        return self.forward_linked(x)[0]
+
+    def forward_linked(self, x, in_link=None):
+        """(output, bn_link of b3): ``in_link`` is the previous block's b3
+        bn_link -- its backward sums come from this block's c1 dgrad epilogue,
+        which also adds the residual's gradient (identity-residual blocks)."""
         # x feeds c1 (HIP GEMM) and a second branch: the identity residual (its
         # BatchNorm b3 hands the gradient of x over) or the downsample conv (hands
         # its dgrad over); c1's dgrad epilogue adds it -- no separate gradient sum.
@@ -233,12 +252,16 @@ class _Bottleneck(nn.Module):
         n, _, h, w = x.shape  # c1 is 1x1 stride 1: c2's input is [n, width, h, w]
         c2in = (n, self.c2.weight.shape[1], h, w)
         pad = 1 if (self.c2.hip_3x3(x, c2in) or (self.c2.k == 3 and self.c2.hip_strided(x, c2in))) else 0
-        y = _conv_bn(self.c1, self.b1, x, link=link, out_pad=pad)
-        y = _conv_bn(self.c2, self.b2, y, dx_pad=pad)
+        l1 = {} if (_BN_DGRAD and torch.is_grad_enabled()) else None
+        l2 = {} if l1 is not None else None
+        l3 = {} if l1 is not None else None
+        y = _conv_bn(self.c1, self.b1, x, link=link, out_pad=pad, out_link=l1,
+                     in_link=in_link if self.down is None else None)
+        y = _conv_bn(self.c2, self.b2, y, dx_pad=pad, in_link=l1, out_link=l2)
         if self.down is None:
-            return _conv_bn(self.c3, self.b3, y, residual=x, res_sink=link)
+            return _conv_bn(self.c3, self.b3, y, residual=x, res_sink=link, in_link=l2, out_link=l3), l3
         s = _conv_bn(self.down[0], self.down[1], x, relu=False, dx_sink=link)
-        return _conv_bn(self.c3, self.b3, y, residual=s)
+        return _conv_bn(self.c3, self.b3, y, residual=s, in_link=l2, out_link=l3), l3
 
 
 class ResNet50(nn.Module):
@@ -270,8 +293,9 @@ class ResNet50(nn.Module):
         from ..ops.pool import max_pool2d_nhwc, supported
 
         h = max_pool2d_nhwc(h, 3, 2, 1) if (_POOL_HIP and supported(h)) else F.max_pool2d(h, 3, 2, 1)
+        link = None
         for b in self.blocks:
-            h = b(h)
+            h, link = b.forward_linked(h, link)
         return h
 
     def _hip_head(self, h) -> bool:

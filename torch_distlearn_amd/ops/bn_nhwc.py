@@ -47,7 +47,7 @@ def supported(x: torch.Tensor) -> bool:
 class _BnAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, relu, eps, momentum, acc, grads, res_sink,
-                have_stats, out_pad, dx_pad):
+                have_stats, out_pad, dx_pad, bn_link):
         M, C = _geom(x)
         N, _, H, W = x.shape
         if out_pad:
@@ -83,6 +83,12 @@ class _BnAct(torch.autograd.Function):
         # neither saved nor read)
         ctx.relu = (1 if ctx.has_res else 2) if relu else 0
         ctx.save_for_backward(x, y if ctx.relu == 1 else None, weight, bias, save, acc)
+        ctx.bn_link = bn_link if ctx.relu else None
+        if ctx.bn_link is not None:
+            # what the consuming convolution's dgrad epilogue needs to compute this
+            # BatchNorm's backward sums itself (ops/conv.py _bn_reduce_begin); with a
+            # residual the ReLU mask is the output's sign (relu mode 1)
+            bn_link["fwd"] = (x, save, weight, bias, acc, C, y if ctx.relu == 1 else None)
         return y
 
     @staticmethod
@@ -96,8 +102,10 @@ class _BnAct(torch.autograd.Function):
         dxbase = dx.data_ptr() - (p * (W + 2 * p) + p) * C * 2 if p else dx.data_ptr()
         dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
         acc = acc4[2 * C:]
-        if ctx.backwards:  # the kernels accumulate atomically into the zeroed half: a second
-            acc.zero_()    # backward (retain_graph) must start from 0 again
+        # the consumer's dgrad epilogue already reduced sum(g), sum(g*xhat) into acc
+        have_sums = bool(ctx.bn_link is not None and ctx.bn_link.pop("sums", False))
+        if ctx.backwards and not have_sums:  # the kernels accumulate atomically into the zeroed
+            acc.zero_()                       # half: a second backward (retain_graph) restarts at 0
         ctx.backwards += 1
         if ctx.grads is not None:  # dgamma / dbeta straight into the flat gradient (overwritten)
             dw, db, ready = ctx.grads
@@ -107,7 +115,7 @@ class _BnAct(torch.autograd.Function):
         native().bn_nhwc_bwd_pad(dy.data_ptr(), y.data_ptr() if y is not None else 0, x.data_ptr(), save.data_ptr(),
                                  weight.data_ptr(), bias.data_ptr(), acc.data_ptr(), dxbase,
                                  dres.data_ptr() if dres is not None else 0, dw.data_ptr(), db.data_ptr(), M, C,
-                                 ctx.relu, H, W, int(p), stream_handle())
+                                 ctx.relu, H, W, int(p), stream_handle(), int(have_sums))
         if ctx.res_sink is not None and dres is not None and not ctx.res_sink.get("done"):
             # consumed by the conv whose input is the residual (ops/conv.py); if that
             # conv's backward already ran ("done"), autograd sums the gradients instead
@@ -115,16 +123,16 @@ class _BnAct(torch.autograd.Function):
             dres = None
         if ctx.grads is not None:
             ready()
-            return dx, None, None, None, None, dres, None, None, None, None, None, None, None, None, None
+            return dx, None, None, None, None, dres, None, None, None, None, None, None, None, None, None, None
         return (dx, dw.to(weight.dtype), db.to(weight.dtype), None, None, dres, None, None, None, None, None, None, None,
-                None, None)
+                None, None, None)
 
 
 def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_mean: Optional[torch.Tensor],
            running_var: Optional[torch.Tensor], residual: Optional[torch.Tensor] = None, relu: bool = True,
            eps: float = 1e-5, momentum: float = 0.1, acc: Optional[torch.Tensor] = None,
            grads=None, res_sink: Optional[dict] = None, have_stats: Optional[bool] = None, out_pad: int = 0,
-           dx_pad: int = 0) -> torch.Tensor:
+           dx_pad: int = 0, bn_link: Optional[dict] = None) -> torch.Tensor:
     """``acc``: optional fp32 [4C] whose last 2C are zero; with ``have_stats``
     (the default when ``acc`` is given) its first 2C already hold the
     per-channel sum / sum of squares of x (see ops/conv.py Conv1x1), else they
@@ -137,7 +145,13 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
     epilogue): saves the separate gradient-sum pass of a tensor used twice.
     ``out_pad`` / ``dx_pad``: write the output / the input gradient as the
     interior of a zero-bordered buffer (:func:`padded_empty`) for a 3x3
-    convolution that reads it directly."""
+    convolution that reads it directly.
+    ``bn_link``: a dict shared with the convolution that consumes this
+    BatchNorm's output (ReLU only; with a residual, a consumer whose dgrad
+    epilogue adds the residual's gradient): the forward parks what that
+    convolution's dgrad epilogue needs to produce the backward sums
+    sum(g), sum(g*xhat) (ops/conv.py ``fused_bn_reduce``); the backward then
+    skips its own reduce pass over dy and x."""
     if not supported(x):
         raise ValueError(f"bn_act: needs a channels-last bf16 CUDA tensor with a supported channel count, got "
                          f"{tuple(x.shape)} {x.dtype} {x.device}")
@@ -152,4 +166,5 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
     if have_stats is None:
         have_stats = acc is not None
     return _BnAct.apply(x, weight.contiguous(), bias.contiguous(), running_mean, running_var, residual, relu, eps,
-                        momentum, acc, grads, res_sink, bool(have_stats), int(out_pad), int(dx_pad))
+                        momentum, acc, grads, res_sink, bool(have_stats), int(out_pad), int(dx_pad),
+                        bn_link if relu else None)

@@ -115,6 +115,53 @@ def _wgrad_plan(cout: int, K: int, M: int):
     return plan(cout, K, M, 0)
 
 
+def _bn_reduce_begin(C, link, M: int, cin: int, nrows: int, residual_add: bool = False):
+    """Arm the dgrad epilogue's BatchNorm backward reduce: ``link`` is the dict
+    the BatchNorm that produced this conv's input filled in its forward
+    (ops/bn_nhwc.py ``bn_link``: its input x, [mean; invstd], gamma, beta and
+    its [4C] sums buffer).  The dgrad output IS that BatchNorm's output
+    gradient dz, so the epilogue computes g = dz * (x*scale + shift > 0) and
+    per-M-tile partial rows of sum(g), sum(g*xhat) while dz is still in
+    registers (csrc conv_igemm.hip set_conv_bn_reduce, BnRedArgs BNR 2): the
+    BatchNorm backward's reduce pass -- a full read of dz and x -- goes away.
+    A BatchNorm + residual + ReLU (the bottleneck's b3) takes its mask from
+    its saved output; its output gradient is only complete in the epilogue of
+    the next block's c1 dgrad that adds the residual's gradient
+    (``residual_add``).  Returns the state for :func:`_bn_reduce_end`, or
+    None (not linked / not applicable)."""
+    f = link.get("fwd") if link is not None else None
+    if f is None:
+        return None
+    x, save, w, b, acc4, cc, ym = f
+    if (ym is not None) != residual_add:
+        return None
+    if cc != cin or x.numel() != M * cin or not x.is_contiguous(memory_format=torch.channels_last):
+        return None
+    if ym is not None and (ym.numel() != M * cin or not ym.is_contiguous(memory_format=torch.channels_last)):
+        return None
+    rows = torch.empty(max(1, nrows), 2, cc, device=x.device)
+    C.set_conv_bn_reduce(x.data_ptr(), save.data_ptr(), w.data_ptr(), b.data_ptr(), rows.data_ptr(),
+                         0 if ym is None else ym.data_ptr())
+    return rows, f
+
+
+def _bn_reduce_end(C, link, st, T: int, s) -> None:
+    """Disarm, then column-sum the partial rows into the BatchNorm's backward
+    half of its sums buffer and tell its backward (``link["sums"]``)."""
+    C.set_conv_bn_reduce(0, 0, 0, 0, 0)
+    rows, (x, save, w, b, acc4, cc, _) = st
+    accb = acc4[2 * cc:]
+    if link.get("nbwd", 0):  # a second backward (retain_graph): start from 0 again
+        accb.zero_()
+    link["nbwd"] = link.get("nbwd", 0) + 1
+    C.bn_rows_reduce(rows.data_ptr(), T, cc, accb.data_ptr(), s)
+    link["sums"] = True
+
+
+def _bn_disarm(C):
+    C.set_conv_bn_reduce(0, 0, 0, 0, 0)
+
+
 def conv1x1_supported(x: torch.Tensor, cout: int) -> bool:
     cin = x.shape[1]
     pow2 = lambda v: v >= 8 and (v & (v - 1)) == 0  # noqa: E731
@@ -154,9 +201,10 @@ class Conv1x1(torch.autograd.Function):
     """y = conv1x1(x, W) on the MFMA kernels; x channels-last bf16 [N, Cin, H, W]."""
 
     @staticmethod
-    def forward(ctx, x, weight, bind: ShadowBinding, stats, res_link=None, dx_sink=None):
+    def forward(ctx, x, weight, bind: ShadowBinding, stats, res_link=None, dx_sink=None, bn_link=None):
         C = native()
         ctx.res_link = res_link
+        ctx.bn_link = bn_link
         ctx.dx_sink = dx_sink
         if dx_sink is not None:
             dx_sink["expect"] = True  # dx goes to the sink's consumer, not to autograd
@@ -216,13 +264,31 @@ class Conv1x1(torch.autograd.Function):
             dx = torch.empty_like(x, memory_format=torch.channels_last)
             tile, splits = _plan_1x1(M, cin, cout)
             if add is not None and splits == 1:
-                C.conv_fwd_add(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), add.data_ptr(), M, 1, 1, cout, cin, 1,
-                               tile, s)
+                # the previous block's b3 (BN + residual + ReLU) backward sums in this epilogue
+                bst = _bn_reduce_begin(C, ctx.bn_link, M, cin, (M + 127) // 128, residual_add=True) \
+                    if s2 is None else None
+                try:
+                    C.conv_fwd_add(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), add.data_ptr(), M, 1, 1, cout, cin,
+                                   1, tile, s)
+                finally:
+                    if bst is not None:
+                        _bn_disarm(C)
+                if bst is not None:
+                    _bn_reduce_end(C, ctx.bn_link, bst, (M + 127) // 128, s)
                 add = None
             else:
                 slab = torch.empty(splits * M * cin, device=x.device) if splits > 1 else None
-                C.conv_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, 0 if slab is None else slab.data_ptr(),
-                           M, 1, 1, cout, cin, 1, tile, splits, s)
+                bst = None
+                if splits == 1 and add is None and s2 is None:
+                    bst = _bn_reduce_begin(C, ctx.bn_link, M, cin, (M + 127) // 128)
+                try:
+                    T = C.conv_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0,
+                                   0 if slab is None else slab.data_ptr(), M, 1, 1, cout, cin, 1, tile, splits, s)
+                finally:
+                    if bst is not None:
+                        _bn_disarm(C)
+                if bst is not None:
+                    _bn_reduce_end(C, ctx.bn_link, bst, T, s)
             if add is not None:
                 dx.add_(add)
             if s2 is not None:  # dx[:, ::2, ::2] += the stride-2 downsample's dgrad (in place)
@@ -241,7 +307,7 @@ class Conv1x1(torch.autograd.Function):
         if ctx.dx_sink is not None and dx is not None:
             ctx.dx_sink["g"] = dx
             dx = None
-        return dx, None, None, None, None, None
+        return dx, None, None, None, None, None, None
 
 
 PAD_COPIES = [0]  # Conv3x3 inputs / gradients that had to be padded by a copy (tests)
@@ -303,11 +369,12 @@ class Conv3x3(torch.autograd.Function):
     (GEMM epilogue rows, as Conv1x1)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bind: ShadowBinding, stats):
+    def forward(ctx, x, weight, bind: ShadowBinding, stats, bn_link=None):
         C = native()
         N, cin, H, W = x.shape
         cout = weight.shape[0]
         keep, xbase = _padded_base(x, 1)
+        ctx.bn_link = bn_link
         M, K = N * H * W, 9 * cin
         y = torch.empty((N, cout, H, W), dtype=BF16, device=x.device, memory_format=torch.channels_last)
         tile, splits = _plan_3x3(M, cout, K)
@@ -342,15 +409,22 @@ class Conv3x3(torch.autograd.Function):
             dx = torch.empty((N, cin, H, W), dtype=BF16, device=dy.device, memory_format=torch.channels_last)
             dt, ds = _plan_3x3(M, cin, 9 * cout)
             slab = torch.empty(ds * M * cin, device=dy.device) if ds > 1 else None
-            C.conv_fwd(dybase, wt.data_ptr(), dx.data_ptr(), 0, 0 if slab is None else slab.data_ptr(), N, H, W,
-                       cout, cin, 3, dt, ds, s)
+            bst = _bn_reduce_begin(C, ctx.bn_link, M, cin, (M + 127) // 128) if ds == 1 else None
+            try:
+                T = C.conv_fwd(dybase, wt.data_ptr(), dx.data_ptr(), 0, 0 if slab is None else slab.data_ptr(), N, H,
+                               W, cout, cin, 3, dt, ds, s)
+            finally:
+                if bst is not None:
+                    _bn_disarm(C)
+            if bst is not None:
+                _bn_reduce_end(C, ctx.bn_link, bst, T, s)
         tile, splits = _wgrad_plan_3x3(cout, K, M)
         ws = torch.empty(splits * cout * K, device=dy.device)
         C.conv_wgrad(dybase, ctx.xbase, ws.data_ptr(), N, H, W, cin, cout, 3, splits, K, tile, 0, s)
         C.slab_reduce_add_oihw(ws.data_ptr(), bind.g32.data_ptr(), splits, cout, 9, cin, cin, s)
         bind.ready()
         del keep_dy
-        return dx, None, None, None
+        return dx, None, None, None, None
 
 
 class ShadowConv(torch.autograd.Function):
@@ -537,12 +611,13 @@ class Conv3x3S2(torch.autograd.Function):
     zero-stuffed upsampling."""
 
     @staticmethod
-    def forward(ctx, x, weight, bind: ShadowBinding, stats):
+    def forward(ctx, x, weight, bind: ShadowBinding, stats, bn_link=None):
         C = native()
         N, cin, H, W = x.shape
         cout = weight.shape[0]
         Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
         keep, xbase = _padded_base(x, 1)
+        ctx.bn_link = bn_link
         y = torch.empty((N, cout, Ho, Wo), dtype=BF16, device=x.device, memory_format=torch.channels_last)
         tile = 0 if cout % 128 == 0 else 2
         s = _stream()
@@ -578,13 +653,23 @@ class Conv3x3S2(torch.autograd.Function):
             dx = torch.empty((N, cin, H, W), dtype=BF16, device=dy.device, memory_format=torch.channels_last)
             interior = dybase + (Wq + 1) * cout * 2  # dy[0][0]: tap t of phase pixel q reads dy[q + t]
             tile = 0 if cin % 128 == 0 else 2
-            off = 0
-            for rh in (0, 1):
-                for rw in (0, 1):
-                    kh, kw = 1 + rh, 1 + rw
-                    C.conv_fwd_ex(interior, ph[off * cin * cout:].data_ptr(), dx.data_ptr(), 0, 0, N, Ho, Wo, Hq, Wq,
-                                  cout, cin, kh, kw, 1, 2, rh, rw, W, H * W, 0, tile, 1, s)
-                    off += kh * kw
+            tp = (N * Ho * Wo + 127) // 128  # M tiles (partial BN rows) per phase conv
+            bst = _bn_reduce_begin(C, ctx.bn_link, N * H * W, cin, 4 * tp)
+            off = T = 0
+            try:
+                for rh in (0, 1):
+                    for rw in (0, 1):
+                        kh, kw = 1 + rh, 1 + rw
+                        if bst is not None:  # each phase conv writes its own block of rows
+                            C.set_conv_bn_reduce(*[t.data_ptr() for t in bst[1][:4]], bst[0][T:].data_ptr())
+                        T += C.conv_fwd_ex(interior, ph[off * cin * cout:].data_ptr(), dx.data_ptr(), 0, 0, N, Ho,
+                                           Wo, Hq, Wq, cout, cin, kh, kw, 1, 2, rh, rw, W, H * W, 0, tile, 1, s)
+                        off += kh * kw
+            finally:
+                if bst is not None:
+                    _bn_disarm(C)
+            if bst is not None:
+                _bn_reduce_end(C, ctx.bn_link, bst, T, s)
         K = 9 * cin
         tile_w, splits = _wgrad_plan_3x3(cout, K, N * Ho * Wo)
         ws = torch.empty(splits * cout * K, device=dy.device)
@@ -593,4 +678,4 @@ class Conv3x3S2(torch.autograd.Function):
         C.slab_reduce_add_oihw(ws.data_ptr(), bind.g32.data_ptr(), splits, cout, 9, cin, cin, s)
         bind.ready()
         del keep_dy
-        return dx, None, None, None
+        return dx, None, None, None, None
