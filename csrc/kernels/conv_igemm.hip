@@ -273,6 +273,33 @@ __device__ __forceinline__ void blds16(rsrc_t r, unsigned voff, unsigned soff, v
                                            (int)soff, 0, 0);
 }
 
+// The same LDS-DMA as inline asm, for loops that read the staged tiles with
+// ds_read_b64_tr_b16: hipcc (ROCm 7.2) puts an `s_waitcnt vmcnt(0)` in front of
+// every __builtin_amdgcn_ds_read_tr16_b64 while a builtin LDS-DMA may be in
+// flight (it cannot tell which LDS bytes the transposed read touches), which
+// drains the whole DMA ring at every K step -- the wgrad kernel waited for the
+// stages it had just issued.  Issued from asm, the DMA is invisible to that
+// analysis; the kernel's own counted `s_waitcnt vmcnt(N)` before each barrier
+// orders it (and the compiler still tracks lgkmcnt for the tr16 results).
+// M0 carries the LDS base (nothing else in those kernels uses M0).
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4 make_rsrc4(const void* p, unsigned bytes) {
+  const unsigned long long a = reinterpret_cast<unsigned long long>(p);
+  return i32x4{(int)(unsigned)a, (int)(unsigned)(a >> 32), (int)bytes, 0x00020000};
+}
+
+__device__ __forceinline__ void blds16_asm(const i32x4& r, unsigned voff, unsigned soff, void* lds_wave_base) {
+  // wave-uniform operands in SGPRs (readfirstlane: the compiler may not prove them uniform)
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(
+      (unsigned)reinterpret_cast<unsigned long long>((__attribute__((address_space(3))) char*)lds_wave_base));
+  const unsigned so = __builtin_amdgcn_readfirstlane(soff);
+  const i32x4 rs{__builtin_amdgcn_readfirstlane(r[0]), __builtin_amdgcn_readfirstlane(r[1]),
+                 __builtin_amdgcn_readfirstlane(r[2]), __builtin_amdgcn_readfirstlane(r[3])};
+  asm volatile("s_mov_b32 m0, %3\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rs), "s"(so),
+               "s"(m0)
+               : "memory");
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -1368,8 +1395,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
     const int kh = kpos / g.KW, kw = kpos - kh * g.KW;
     b_off[j] = (lane_pix(row) + kh * g.Wp + kw) * g.Cin + ((kc & (C8 - 1)) << 3);
   }
-  const rsrc_t dyr = make_rsrc(dy, (unsigned)((int64_t)g.B * g.dHp * g.dWp * g.Cout * 2));
-  const rsrc_t xr = make_rsrc(x, (unsigned)((int64_t)g.B * g.Hp * g.Wp * g.Cin * 2));
+  const i32x4 dyr = make_rsrc4(dy, (unsigned)((int64_t)g.B * g.dHp * g.dWp * g.Cout * 2));
+  const i32x4 xr = make_rsrc4(x, (unsigned)((int64_t)g.B * g.Hp * g.Wp * g.Cin * 2));
   unsigned a_v[A_INS], b_v[B_INS];  // per-lane byte offsets (K-tail lanes: out of range -> zeros)
 #pragma unroll
   for (int j = 0; j < A_INS; ++j) a_v[j] = 2u * (unsigned)a_off[j];
@@ -1389,24 +1416,24 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
       const unsigned ua = 2u * (unsigned)(u * g.Cout), ub = 2u * (unsigned)(u * g.Cin);
 #pragma unroll
       for (int j = 0; j < A_INS; ++j)
-        blds16(dyr, a_row[j] < left ? a_v[j] : kOOB, ua, sA + (wid * A_INS + j) * 1024);
+        blds16_asm(dyr, a_row[j] < left ? a_v[j] : kOOB, ua, sA + (wid * A_INS + j) * 1024);
 #pragma unroll
       for (int j = 0; j < B_INS; ++j)
-        blds16(xr, b_row[j] < left ? b_v[j] : kOOB, ub, sB + (wid * B_INS + j) * 1024);
+        blds16_asm(xr, b_row[j] < left ? b_v[j] : kOOB, ub, sB + (wid * B_INS + j) * 1024);
     } else {
 #pragma unroll
       for (int j = 0; j < A_INS; ++j) {
         const bool ok = a_row[j] < left;
         const int mr = ok ? ms + a_row[j] : 0;
         const int px = g.dsep ? dy_pix(g, mr) : out_pix(g, mr);
-        blds16(dyr, ok ? a_v[j] + 2u * (unsigned)(px * g.Cout) : kOOB, 0u, sA + (wid * A_INS + j) * 1024);
+        blds16_asm(dyr, ok ? a_v[j] + 2u * (unsigned)(px * g.Cout) : kOOB, 0u, sA + (wid * A_INS + j) * 1024);
       }
 #pragma unroll
       for (int j = 0; j < B_INS; ++j) {
         const bool ok = b_row[j] < left;
         const int px = out_pix(g, ok ? ms + b_row[j] : 0);
-        blds16(xr, ok && b_v[j] != kOOB ? b_v[j] + 2u * (unsigned)(px * g.Cin) : kOOB, 0u,
-               sB + (wid * B_INS + j) * 1024);
+        blds16_asm(xr, ok && b_v[j] != kOOB ? b_v[j] + 2u * (unsigned)(px * g.Cin) : kOOB, 0u,
+                   sB + (wid * B_INS + j) * 1024);
       }
     }
   };

@@ -306,7 +306,9 @@ class ResNet50(nn.Module):
     def forward(self, x: torch.Tensor, compute_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
         """x: NHWC [B, H, W, 3] (or NCHW); returns log-probabilities (fp32)."""
         h = self.trunk(x, compute_dtype)
-        if self._hip_head(h):
+        # the fused head node computes gradients only for the training loss
+        # (forward_loss); a differentiable forward() keeps the torch classifier
+        if self._hip_head(h) and not (torch.is_grad_enabled() and (h.requires_grad or self.fc_w.requires_grad)):
             from ..ops.head import ResNetHeadNLL
 
             return ResNetHeadNLL.apply(h, self.fc_w, self.fc_b, None, None)[1]
