@@ -1318,6 +1318,9 @@ __global__ void __launch_bounds__(256) splitk_combine_kernel(const float* __rest
 // ATOM: split-K partials are atomically added straight into the zeroed fp32
 // weight gradient [Cout][taps][creal] (creal <= Cin drops zero-padded input
 // channels) -- no slab round trip and no slab_reduce launch.
+// wgrad slab stores staged through LDS as whole rows (set_conv_wgrad_stage_store; A/B)
+__constant__ int g_wgrad_stage_store = 1;
+
 template <int BM, int BN, int STAGES, int WM = 2, int WN = 2, bool PF = true, bool ATOM = false>
 __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                          float* __restrict__ out, const ConvGeom g, int m_per_split,
@@ -1566,6 +1569,36 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
     return;
   }
   float* o = out + (int64_t)split * g.Cout * ldo;
+  if (BN >= 128 && g_wgrad_stage_store) {  // (64-wide tiles: measured no gain)
+    // Slab rows through LDS: straight from the accumulators a store
+    // instruction writes 16 rows x 64 B; staged, every instruction writes whole
+    // BN*4-byte rows (64 lanes x 16 B).  The C^T tile goes into the (drained)
+    // DMA ring as [co][k] fp32 with a 16-byte row pad (row stride 2^n + 16 B:
+    // the 16 co rows of a store group fall on distinct banks).
+    constexpr int LROW = BN + 4;
+    static_assert(BM * LROW * 4 <= STAGES * STAGE_BYTES, "staged slab tile fits the ring");
+    wait_vmcnt<0>();  // the unconditional pipeline's trailing (zero-fill) DMAs still target the ring
+    block_sync_lds();
+    float* st = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int a = 0; a < FM; ++a)
+#pragma unroll
+      for (int b = 0; b < FN; ++b)
+        *reinterpret_cast<float4*>(st + (wm * TM + a * 16 + col_l) * LROW + wn * TN + b * 16 + rq * 4) =
+            make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+    block_sync_lds();
+    constexpr int C4 = BN / 4, NTH = 64 * NW;  // 16-byte chunks per row, threads
+    static_assert(BM * C4 % NTH == 0, "whole store passes");
+#pragma unroll
+    for (int i = 0; i < BM * C4 / NTH; ++i) {
+      const int idx = tid + i * NTH, r = idx / C4, c4 = idx - r * C4;
+      const int co = co0 + r, k = k0 + 4 * c4;
+      if (co < g.Cout && k < ldo)
+        *reinterpret_cast<float4*>(o + (int64_t)co * ldo + k) =
+            *reinterpret_cast<const float4*>(st + r * LROW + 4 * c4);
+    }
+    return;
+  }
 #pragma unroll
   for (int a = 0; a < FM; ++a)
 #pragma unroll
@@ -2095,6 +2128,10 @@ void set_conv_waves(int waves) {
 
 static int g_wgrad_pf = -1;  // wgrad fragment prefetch: -1 = by stage count, 0 off, 1 on
 void set_conv_wgrad_pf(int pf) { g_wgrad_pf = pf; }
+void set_conv_wgrad_stage_store(int on) {
+  const int v = on ? 1 : 0;
+  DL_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_wgrad_stage_store), &v, sizeof(int)));
+}
 void set_conv_debug(uintptr_t buf) { g_conv_dbg = (unsigned long long*)buf; }
 
 void set_conv_stages(int fwd, int wgrad) {

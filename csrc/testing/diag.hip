@@ -50,9 +50,42 @@ void occupy_cus(int blocks, int us, uintptr_t sink, uintptr_t stream) {
   DL_HIP_CHECK(hipGetLastError());
 }
 
+// Price of the per-K-step synchronisation of the conv kernels: `n` rounds of
+// (mode 0) s_barrier, (1) lgkmcnt(0) + s_barrier, (2) one ds_read_b128 of the
+// ring + lgkmcnt(0) + s_barrier, in `blocks` workgroups of `threads` holding
+// `lds` bytes of dynamic LDS (128 KiB = the wgrad's one workgroup per CU).
+__global__ void barrier_loop_kernel(int n, int mode, float* __restrict__ sink) {
+  extern __shared__ float dyn[];
+  float acc = 0.f;
+  for (int i = 0; i < n; ++i) {
+    if (mode == 2) {
+      acc += dyn[(threadIdx.x * 4 + i * 64) & 1023];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else if (mode == 1) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+  }
+  if (threadIdx.x == 0 && sink) sink[blockIdx.x] = acc;
+}
+
+void barrier_loop(int blocks, int threads, int n, int mode, int lds, uintptr_t sink, uintptr_t stream) {
+  if (threads % 64 || threads > 1024 || lds < 4096 || lds > 160 * 1024 || n < 0 || n > 1000000)
+    throw std::runtime_error("barrier_loop: bad launch");
+  static bool attr = false;
+  if (!attr) {
+    DL_HIP_CHECK(hipFuncSetAttribute((const void*)barrier_loop_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024));
+    attr = true;
+  }
+  barrier_loop_kernel<<<blocks, threads, lds, as_stream(stream)>>>(n, mode, (float*)sink);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace dl
 
 PYBIND11_MODULE(_C_testing, m) {
+  m.def("barrier_loop", &dl::barrier_loop);
   m.doc() = "distlearn test/diagnostic kernels (not part of the product library)";
   m.def("occupy_cus", &dl::occupy_cus);
 }

@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--region", type=int, default=1, help="1: tap-reuse (LDS-resident region) fwd/dgrad kernel")
     ap.add_argument("--rstages", type=int, default=0, help="region kernel B-ring stages (0 = max that fits)")
     ap.add_argument("--rwaves", type=int, default=8, help="region kernel waves per workgroup (4 or 8)")
+    ap.add_argument("--wstage", type=int, default=1, help="wgrad slab stores staged through LDS as whole rows")
     a = ap.parse_args()
     C = _native.native()
     fs, ws = (int(v) for v in a.stages.split(","))
@@ -46,6 +47,7 @@ def main():
     C.set_conv_region(a.region)
     C.set_conv_region_stages(a.rstages)
     C.set_conv_region_waves(a.rwaves)
+    C.set_conv_wgrad_stage_store(a.wstage)
     print(f"# stages fwd={fs} wgrad={ws} region={a.region}")
     dev = torch.device("cuda")
     def cur():  # current-stream handle at call time (graph capture switches streams)
