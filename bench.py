@@ -272,10 +272,11 @@ def main():
             xs = torch.randn(nb, batch, 224, 224, 3, device=dev, generator=g).to(cdt)
             ys = torch.randint(0, 1000, (nb, batch), device=dev, generator=g)
             step_args = lambda i: (xs[i % nb], ys[i % nb])  # noqa: E731
-        # steps per replayed graph: 16 measured 1.3 % faster than 8 on the driver's 20-step
-        # window (2 replays instead of 3: 0.3397 vs 0.3442 ms/step, profiles/r2_unroll20_ab.txt),
-        # equal over 400 steps
-        unroll = int(os.environ.get("DISTLEARN_UNROLL", "16"))
+        # steps per replayed graph: a timed window of at most 32 steps is ONE replay of a graph
+        # holding exactly those steps (the driver's 20: 0.3307 vs 0.3335 ms/step as 16 + 4,
+        # = the 600-step figure 0.3305, profiles/r3_unroll_ab.txt); longer runs replay 16-step
+        # graphs (16 measured 1.3 % faster than 8, profiles/r2_unroll20_ab.txt)
+        unroll = int(os.environ.get("DISTLEARN_UNROLL", str(a.steps if 1 < a.steps <= 32 else 16)))
         if step_args is None:  # device loader: unrolled graph replays of complete steps
             tr.run(loader, a.warmup, unroll=unroll)
         else:
