@@ -105,6 +105,10 @@ struct ConvGeom {
   // row b*omHW + (omS*oh + omH0)*omW + omS*ow + omW0 (the phases of a strided
   // convolution's input gradient, written interleaved into the full tensor)
   int om, omS, omH0, omW0, omW, omHW;
+  // BN statistics (reduction mode 0, transposed epilogue): one partial row per
+  // (M tile, wave row) written straight from the lanes -- no LDS round and no
+  // barriers in the epilogue (FwdCfg bit 21; T = M tiles x WM rows)
+  int swave;
 };
 
 // q = n / d, r = n - q*d for 0 <= n < 2^24 via a float reciprocal and one
@@ -592,6 +596,22 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
     for (int q = 0; q < NP; ++q)
 #pragma unroll
       for (int k = 0; k < 8; ++k) { s1[q][k] = row16_sum(s1[q][k]); s2[q][k] = row16_sum(s2[q][k]); }
+    if constexpr (STATS && !BNRED) {
+      if (g.swave) {  // per-wave-row partial rows: lane 15 of each 16-lane group holds 8 channels' sums
+        if ((lane & 15) == 15) {
+          float* r0 = stats + ((int64_t)tm * WM + wm) * 2 * g.Cout + n0 + nl;
+#pragma unroll
+          for (int q = 0; q < NP; ++q) {
+            *reinterpret_cast<float4*>(r0 + 32 * q) = make_float4(s1[q][0], s1[q][1], s1[q][2], s1[q][3]);
+            *reinterpret_cast<float4*>(r0 + 32 * q + 4) = make_float4(s1[q][4], s1[q][5], s1[q][6], s1[q][7]);
+            *reinterpret_cast<float4*>(r0 + g.Cout + 32 * q) = make_float4(s2[q][0], s2[q][1], s2[q][2], s2[q][3]);
+            *reinterpret_cast<float4*>(r0 + g.Cout + 32 * q + 4) =
+                make_float4(s2[q][4], s2[q][5], s2[q][6], s2[q][7]);
+          }
+        }
+        return;
+      }
+    }
     __syncthreads();  // every wave done with the LDS ring and region
     float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]
     if ((lane & 15) == 15) {
@@ -1984,6 +2004,9 @@ int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile,
 static uintptr_t g_fwd_addend = 0;  // conv_fwd_add: bf16 [M][Cout] added in the epilogue
 static int g_fwd_slab_cap = 0;      // split-K slab capacity of the current conv_fwd call (FwdCfg)
 static int g_fwd_keep_slabs = 0;    // FwdCfg bit 20: leave the split-K slabs (the caller combines them)
+static int g_fwd_swave_req = 0;     // FwdCfg bit 21: per-wave-row BN statistics rows (ConvGeom::swave)
+static int g_stat_rows_mult = 1;    // rows per M tile of the last streaming launch (WM when swave)
+static int g_red_atomic_host = 0;   // host mirror of g_red_atomic
 static BnRedArgs g_bnred{};         // conv_fwd_bnred: fused BN backward reduce (region dgrad only)
 static BnRedArgs g_bnred2{};        // set_conv_bn_reduce: NHWC BN backward reduce in the streaming epilogue
 // A/B knob: 0 = the untransposed accumulator layout for the split-K and BN-statistics
@@ -2043,6 +2066,9 @@ static void launch_fwd_w(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uin
   const int ktps = (nkt + splits - 1) / splits;
   const int grid = g.pm_kmax > 0 ? ntn * g.pm_P : ntm * ntn * splits;
   constexpr int NT = 64 * WM * WN;
+  constexpr bool kTR = (BN / WN / 16) % 2 == 0;
+  g.swave = (g_fwd_swave_req && stats && splits == 1 && !g_red_atomic_host && g_fwd_tr && kTR && !g.posm) ? 1 : 0;
+  g_stat_rows_mult = g.swave ? WM : 1;
   if (g_fwd_addend && (splits > 1 || stats)) throw std::runtime_error("conv_fwd_add: no split-K / statistics");
   if (g_bnred2.rows != nullptr) {
     if (splits > 1 || stats) throw std::runtime_error("conv BN reduce: plain unsplit output only");
@@ -2100,13 +2126,17 @@ struct FwdCfg {
     const int st = (tile >> 4) & 15, wv = (tile >> 8) & 15;
     g_fwd_slab_cap = (tile >> 12) & 255;
     g_fwd_keep_slabs = (tile >> 20) & 1;
+    g_fwd_swave_req = (tile >> 21) & 1;
+    g_stat_rows_mult = 1;
     tile &= 15;
     if (st && (st < 2 || st > 4)) throw std::runtime_error("conv_fwd: packed stages must be 2..4");
     if (wv && wv != 4 && wv != 8) throw std::runtime_error("conv_fwd: packed waves must be 4 or 8");
     if (st) g_fwd_stages = st;
     if (wv) g_fwd_waves = wv;
   }
-  ~FwdCfg() { g_fwd_stages = saved_st; g_fwd_waves = saved_wv; g_fwd_slab_cap = 0; g_fwd_keep_slabs = 0; }
+  ~FwdCfg() {
+    g_fwd_stages = saved_st; g_fwd_waves = saved_wv; g_fwd_slab_cap = 0; g_fwd_keep_slabs = 0; g_fwd_swave_req = 0;
+  }
 };
 
 template <int BM, int BN, bool TAPU, int ST>
@@ -2340,7 +2370,7 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
   else if (tile == 2) launch_fwd<128, 64>(g, x, w, y, stats, slab, splits, s);
   else throw std::runtime_error("conv_fwd: bad tile id");
   DL_HIP_CHECK(hipGetLastError());
-  if (splits == 1) return (g.M + fwd_bm(tile) - 1) / fwd_bm(tile);
+  if (splits == 1) return (g.M + fwd_bm(tile) - 1) / fwd_bm(tile) * g_stat_rows_mult;
   if (g_fwd_keep_slabs) {
     if (stats || g.pm_kmax > 0) throw std::runtime_error("conv_fwd keep-slabs: no statistics / balanced split-K");
     return 0;
@@ -2483,7 +2513,7 @@ int conv_fwd_ex(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_
   }
   g_fwd_addend = 0;
   DL_HIP_CHECK(hipGetLastError());
-  if (splits == 1) return (g.M + fwd_bm(tile) - 1) / fwd_bm(tile);
+  if (splits == 1) return (g.M + fwd_bm(tile) - 1) / fwd_bm(tile) * g_stat_rows_mult;
   if (g_fwd_keep_slabs) return 0;
   if (256 % (Cout / 8) != 0) throw std::runtime_error("conv_fwd_ex split-K combine: Cout/8 must divide 256");
   const int rpb = combine_rows_per_block(g.M, Cout);
@@ -2597,6 +2627,7 @@ void set_reduce_atomic_conv(int rows) {
     throw std::runtime_error("set_reduce_atomic: rows must be 0 or a power of two <= 64");
   const int v = rows;
   DL_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_red_atomic), &v, sizeof(int)));
+  g_red_atomic_host = rows;
 }
 
 template <bool ACC, bool OIHW = false>

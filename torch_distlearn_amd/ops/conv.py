@@ -35,12 +35,29 @@ Reference parity: these are the ResNet-50 stress config of BASELINE.json
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
 from .._native import native, stream_handle
 
 BF16 = torch.bfloat16
+
+# BN statistics of the forward convs as one partial row per (M tile, wave row), written
+# straight from the epilogue lanes (conv_igemm.hip ConvGeom::swave, tile-id bit 21):
+# no LDS round trip and no barriers in the epilogue; up to 4x the rows for bn_rows_reduce.
+# Off: 25.62 vs 25.58 ms/step (profiles/r3_resnet_stats_wave_ab.txt) -- the epilogue's
+# barriers are not what the statistics cost
+_STATS_WAVE = os.environ.get("DISTLEARN_RESNET_STATS_WAVE", "0") == "1"
+_SWAVE_BIT = 1 << 21
+
+
+def _stats_cfg(tile: int, nrows: int):
+    """(tile id, row capacity) of a forward conv that emits BN statistics."""
+    if _STATS_WAVE:
+        return tile | _SWAVE_BIT, 4 * nrows
+    return tile, nrows
 
 
 class ShadowBinding:
@@ -222,6 +239,8 @@ class Conv1x1(torch.autograd.Function):
             if C.reduce_atomic() != 0:
                 raise RuntimeError("Conv1x1 statistics need reduction mode 0 (partial rows)")
             nrows = C.conv_fwd_stat_rows(M, 1, 1, cin, cout, 1, tile, splits)
+            if splits == 1:
+                tile, nrows = _stats_cfg(tile, nrows)
             rows = torch.empty(max(nrows, 400 if splits > 1 else 1), 2, cout, device=x.device)
         T = C.conv_fwd(x.data_ptr(), bind.w16.data_ptr(), y.data_ptr(), 0 if rows is None else rows.data_ptr(),
                        0 if slab is None else slab.data_ptr(), M, 1, 1, cin, cout, 1, tile, splits, s)
@@ -385,6 +404,8 @@ class Conv3x3(torch.autograd.Function):
             if C.reduce_atomic() != 0:
                 raise RuntimeError("Conv3x3 statistics need reduction mode 0 (partial rows)")
             nrows = C.conv_fwd_stat_rows(N, H, W, cin, cout, 3, tile, splits)
+            if splits == 1:
+                tile, nrows = _stats_cfg(tile, nrows)
             rows = torch.empty(max(nrows, 400 if splits > 1 else 1), 2, cout, device=x.device)
         T = C.conv_fwd(xbase, bind.wcl.data_ptr(), y.data_ptr(), 0 if rows is None else rows.data_ptr(),
                        0 if slab is None else slab.data_ptr(), N, H, W, cin, cout, 3, tile, splits, s)
@@ -498,7 +519,8 @@ class StemConv(torch.autograd.Function):
         if stats is not None:
             if C.reduce_atomic() != 0:
                 raise RuntimeError("StemConv statistics need reduction mode 0 (partial rows)")
-            rows = torch.empty((N * Ho * Wo + 127) // 128, 2, cout, device=x.device)
+            tile, nrows = _stats_cfg(tile, (N * Ho * Wo + 127) // 128)
+            rows = torch.empty(nrows, 2, cout, device=x.device)
         T = C.conv_fwd_ex(S.data_ptr(), w4.data_ptr(), y.data_ptr(), 0 if rows is None else rows.data_ptr(), 0, N, Ho,
                           Wo, Hs, Ws, 16, cout, 4, 4, 1, 0, 0, 0, 0, 0, 0, tile, 1, s)
         if rows is not None:
@@ -552,7 +574,8 @@ class Conv1x1S2(torch.autograd.Function):
         if stats is not None:
             if C.reduce_atomic() != 0:
                 raise RuntimeError("Conv1x1S2 statistics need reduction mode 0 (partial rows)")
-            rows = torch.empty((N * Ho * Wo + 127) // 128, 2, cout, device=x.device)
+            tile, nrows = _stats_cfg(tile, (N * Ho * Wo + 127) // 128)
+            rows = torch.empty(nrows, 2, cout, device=x.device)
         T = C.conv_fwd_ex(x.data_ptr(), bind.w16.data_ptr(), y.data_ptr(), 0 if rows is None else rows.data_ptr(), 0,
                           N, Ho, Wo, H, W, cin, cout, 1, 1, 2, 0, 0, 0, 0, 0, 0, tile, 1, s)
         if rows is not None:
@@ -625,7 +648,8 @@ class Conv3x3S2(torch.autograd.Function):
         if stats is not None:
             if C.reduce_atomic() != 0:
                 raise RuntimeError("Conv3x3S2 statistics need reduction mode 0 (partial rows)")
-            rows = torch.empty((N * Ho * Wo + 127) // 128, 2, cout, device=x.device)
+            tile, nrows = _stats_cfg(tile, (N * Ho * Wo + 127) // 128)
+            rows = torch.empty(nrows, 2, cout, device=x.device)
         T = C.conv_fwd_ex(xbase, bind.wcl.data_ptr(), y.data_ptr(), 0 if rows is None else rows.data_ptr(), 0, N, Ho,
                           Wo, H + 2, W + 2, cin, cout, 3, 3, 2, 0, 0, 0, 0, 0, 0, tile, 1, s)
         if rows is not None:
