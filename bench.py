@@ -211,9 +211,9 @@ def main():
         a.bucket_mb = 1.0 if a.model == "cifar10" else 16.0
     backend = a.backend if (a.model == "cifar10" and not cpu) else "torch"
     if backend == "torch" and not cpu and os.environ.get("DISTLEARN_MIOPEN_FIND", "1") == "1":
-        # MIOpen solver search per conv shape (the convs of ResNet-50 not on the HIP
-        # kernels: strided / stem); runs in the graph-capture warm-up steps, before the timed region.
-        # Measured 32.69 vs 33.93 ms/step at batch 256 (profiles/r2_bench_resnet50.txt)
+        # MIOpen solver search per conv shape: only matters for the MIOpen A/B modes
+        # (every ResNet-50 conv is on the HIP kernels by default); runs in the warm-up
+        # steps, before the timed region (r2: 32.69 vs 33.93 ms/step, profiles/r2_bench_resnet50.txt)
         torch.backends.cudnn.benchmark = True
     cdt = torch.float32 if cpu else torch.bfloat16
 

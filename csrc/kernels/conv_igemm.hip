@@ -169,7 +169,7 @@ static int ilog2_exact(int v, const char* what) {
 static bool is_pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
 
 static ConvGeom make_geom(int B, int H, int W, int Cin, int Cout, int KS) {
-  ConvGeom g;
+  ConvGeom g{};  // value-initialised: a field added later (e.g. swave) must not read stack garbage
   g.B = B; g.H = H; g.W = W; g.Cin = Cin; g.Cout = Cout; g.KS = KS; g.pad = KS / 2;
   g.Hp = H + 2 * g.pad; g.Wp = W + 2 * g.pad;
   if (KS % 2 != 1) throw std::runtime_error("conv: odd kernel size required");
@@ -182,6 +182,7 @@ static ConvGeom make_geom(int B, int H, int W, int Cin, int Cout, int KS) {
   g.S = 1; g.KH = KS; g.KW = KS;
   g.dsep = 0; g.dHp = g.Hp; g.dWp = g.Wp; g.dpad = g.pad;
   g.om = 0; g.omS = 1; g.omH0 = 0; g.omW0 = 0; g.omW = W; g.omHW = H * W;
+  g.swave = 0;
   g.logW = g.pow2 ? ilog2_exact(W, "W") : 0;
   g.logHW = g.pow2 ? ilog2_exact(H * W, "H*W") : 0;
   g.inv_HW = 1.0f / (float)(H * W);
@@ -2329,7 +2330,7 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
   if (Cout % 8 != 0) throw std::runtime_error("conv_fwd: Cout % 8 != 0");
   if (tile < 0 || tile > 2) throw std::runtime_error("conv_fwd: bad tile id");
   if (Cout % fwd_bn(tile) != 0) throw std::runtime_error("conv_fwd: Cout must be a multiple of the N tile");
-  RegionGeom rg;
+  RegionGeom rg{};
   // c8 kernel: mt M tiles per workgroup (largest of g_c8_mt, ..., 2, 1 that keeps
   // >= 256 workgroups and divides the tiles of one image)
   int c8_mt = 1;
@@ -2404,7 +2405,7 @@ void set_conv_bn_reduce(uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, u
 // the kernel that carries the fused BN backward reduce epilogue.
 int conv_region_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile) {
   ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
-  RegionGeom rg;
+  RegionGeom rg{};
   const int t = tile & 15;
   return (t == 2 && region_geom(g, 64, 1, rg)) || (t == 0 && region_geom(g, 128, 1, rg)) ? 1 : 0;
 }
@@ -2415,7 +2416,7 @@ int conv_region_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile) {
 int conv_fwd_bnred(uintptr_t x, uintptr_t w, uintptr_t y, int B, int H, int W, int Cin, int Cout, int KS, int tile,
                    uintptr_t y_prev, uintptr_t coef, uintptr_t rows, uintptr_t stream) {
   ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
-  RegionGeom rg;
+  RegionGeom rg{};
   const int t = tile & 15;
   if (!(t == 2 && region_geom(g, 64, 1, rg)) && !(t == 0 && region_geom(g, 128, 1, rg)))
     throw std::runtime_error("conv_fwd_bnred: the shape does not take the region kernel");

@@ -5,10 +5,13 @@ bucketed gradient all-reduce with a 102 MB fp32 gradient (~25 MB
 buckets, >= 4 per step).
 
 Compute path: channels-last bf16 with fp32 master weights in the flat
-buffer.  Every stride-1 convolution (the 1x1 GEMMs and the 3x3s) runs on the
-hand-written MFMA kernels (ops/conv.py); BatchNorm(+ReLU, +residual) runs on
-the channels-last HIP kernels with fp32 statistics (ops/bn_nhwc.py); the
-remaining convolutions (see ``_CONV_MODE`` below) go through PyTorch/MIOpen.  Parameters are
+buffer.  Every convolution -- the stride-1 1x1 GEMMs and 3x3s, the stride-2
+1x1 / 3x3 convolutions and the 7x7 stem -- runs on the hand-written MFMA
+kernels (ops/conv.py), the classifier on the fused head kernels (ops/head.py);
+BatchNorm(+ReLU, +residual) runs on the channels-last HIP kernels with fp32
+statistics (ops/bn_nhwc.py).  MIOpen is only an A/B option (``_CONV_MODE``,
+``_STRIDED_HIP``) and the eval-mode fallback of modules that were never bound
+to a trainer's flat buffers.  Parameters are
 registered in forward order, so :meth:`FlatParams.buckets` (reverse order)
 puts the classifier and last stage in the first bucket to be reduced.
 """
@@ -78,9 +81,9 @@ class _BN(nn.Module):
 
 
 # Convolution path once the trainer has bound the flat buffers (attach_flat):
-# "hip" = stride-1 1x1 convolutions on the hand-written MFMA GEMM kernels,
-# the rest on MIOpen, all reading the bf16 shadow weights (ops/conv.py);
-# "miopen" = every convolution on MIOpen (shadow weights still used).
+# "hip" = every convolution on the hand-written MFMA kernels (stride-1 1x1 / 3x3,
+# and with _STRIDED_HIP the strided ones and the stem), all reading the bf16 shadow
+# weights (ops/conv.py); "miopen" = every convolution on MIOpen (A/B baseline).
 _CONV_MODE = os.environ.get("DISTLEARN_RESNET_CONV", "hip")
 # BatchNorm statistics from the 1x1 GEMM epilogue (skips the BN statistics pass)
 _FUSE_STATS = os.environ.get("DISTLEARN_RESNET_FUSE_STATS", "1") == "1"
@@ -96,7 +99,8 @@ _FUSE_RES = os.environ.get("DISTLEARN_RESNET_FUSE_RES", "1") == "1"
 # profiles/r2_conv3x3_sweep_v2.jsonl); end to end 25.93 vs 25.94 ms/step with
 # the stage on MIOpen (profiles/r2_resnet_conv3_56_ab.txt).
 _CONV3_MAX_HW = int(os.environ.get("DISTLEARN_RESNET_CONV3_MAX_HW", "56"))
-# channels-last copies of the KxK shadows for MIOpen, one launch per step (ops/conv.py)
+# channels-last copies of the KxK shadows (the HIP 3x3 / stem kernels' KRSC operand and
+# MIOpen's layout in the A/B mode), one launch per step (ops/conv.py)
 _CL_WEIGHTS = os.environ.get("DISTLEARN_RESNET_CL_WEIGHTS", "1") == "1"
 # stem max-pool on the HIP gather-backward kernels (ops/pool.py)
 _POOL_HIP = os.environ.get("DISTLEARN_RESNET_POOL", "hip") == "hip"
@@ -243,8 +247,9 @@ class _Bottleneck(nn.Module):
         # x feeds c1 (HIP GEMM) and a second branch: the identity residual (its
         # BatchNorm b3 hands the gradient of x over) or the downsample conv (hands
         # its dgrad over); c1's dgrad epilogue adds it -- no separate gradient sum.
-        # Autograd runs the second branch's backward first (its nodes are younger),
-        # and Conv1x1 raises if the hand-over is missing.
+        # Autograd normally runs the second branch's backward first (its nodes are
+        # younger); if it does not, Conv1x1 marks the link done and the other branch
+        # returns its gradient through autograd, which sums the two.
         link = {} if (_FUSE_RES and torch.is_grad_enabled() and self.c1.hip_gemm(x)
                       and (self.down is None or self.down[0].bind is not None)) else None
         # a stride-1 3x3 c2 on the HIP kernels reads b1's output and b2's input

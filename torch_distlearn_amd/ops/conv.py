@@ -20,10 +20,12 @@ fused SGD kernel already keeps a bf16 shadow of every parameter
   flat gradient by one kernel).
 * :class:`Conv3x3` -- stride-1 3x3 convolutions on the same streaming MFMA
   kernel (zero-bordered NHWC inputs written by the BatchNorm kernels).
-* :class:`ShadowConv` -- the convolutions not covered by the kernels above
-  (strided, the 7x7 stem) on MIOpen, reading the shadow and adding the weight
-  gradient into the flat buffer (one cast-add instead of three elementwise
-  kernels).
+* :class:`Conv1x1S2` / :class:`Conv3x3S2` / :class:`StemConv` -- the strided
+  convolutions and the 7x7 stem on the generalised MFMA kernels (conv_fwd_ex /
+  conv_wgrad_ex).
+* :class:`ShadowConv` -- MIOpen on the shadow weight, adding the weight gradient
+  into the flat buffer: only the A/B baseline (``DISTLEARN_RESNET_CONV=miopen`` /
+  ``DISTLEARN_RESNET_STRIDED=0``), not used by the default training step.
 
 Both mark their weight's gradient ready for the bucketed all-reduce
 themselves (the autograd graph gets no weight gradient, so the
