@@ -60,16 +60,51 @@ __device__ __forceinline__ void sum_rows2(const float* __restrict__ p, int strid
   }
 }
 
-__device__ __forceinline__ void bn_fin_channel(const BnFin& f, int C, int c, float& mean, float& var, float& invstd,
-                                               float& sc, float& sh) {
-  const float gam = f.gamma[c], bet = f.beta[c];  // issued with (not after) the row loads
-  float t1, t2;
-  sum_rows2(f.sums + c, 2 * C, C, f.R, t1, t2);
+__device__ __forceinline__ void bn_fin_from_sums(const BnFin& f, float gam, float bet, float t1, float t2, float& mean,
+                                                 float& var, float& invstd, float& sc, float& sh) {
   mean = t1 / (float)f.M;
   var = fmaxf(t2 / (float)f.M - mean * mean, 0.f);
   invstd = rsqrtf(var + f.eps);
   sc = gam * invstd;
   sh = bet - mean * sc;
+}
+
+__device__ __forceinline__ void bn_fin_channel(const BnFin& f, int C, int c, float& mean, float& var, float& invstd,
+                                               float& sc, float& sh) {
+  const float gam = f.gamma[c], bet = f.beta[c];  // issued with (not after) the row loads
+  float t1, t2;
+  sum_rows2(f.sums + c, 2 * C, C, f.R, t1, t2);
+  bn_fin_from_sums(f, gam, bet, t1, t2, mean, var, invstd, sc, sh);
+}
+
+// Two channels per thread (c and c + off) with all 4R row loads in flight at
+// once: the C = 2 x blockDim case (the head's 512 channels over 256 threads),
+// which as two loop iterations paid two dependent memory round trips.
+template <int RR>
+__device__ __forceinline__ void sum_rows2x2_t(const float* __restrict__ p, int off, int stride, int off2, float (&t)[4]) {
+  float a[RR], b[RR], c[RR], d[RR];
+#pragma unroll
+  for (int r = 0; r < RR; ++r) {
+    a[r] = p[(int64_t)r * stride];
+    b[r] = p[(int64_t)r * stride + off2];
+    c[r] = p[(int64_t)r * stride + off];
+    d[r] = p[(int64_t)r * stride + off + off2];
+  }
+  t[0] = t[1] = t[2] = t[3] = 0.f;
+#pragma unroll
+  for (int r = 0; r < RR; ++r) { t[0] += a[r]; t[1] += b[r]; t[2] += c[r]; t[3] += d[r]; }
+}
+
+__device__ __forceinline__ void sum_rows2x2(const float* __restrict__ p, int off, int stride, int off2, int R,
+                                            float (&t)[4]) {
+  switch (R) {
+    case 1: sum_rows2x2_t<1>(p, off, stride, off2, t); break;
+    case 2: sum_rows2x2_t<2>(p, off, stride, off2, t); break;
+    case 4: sum_rows2x2_t<4>(p, off, stride, off2, t); break;
+    case 8: sum_rows2x2_t<8>(p, off, stride, off2, t); break;
+    case 16: sum_rows2x2_t<16>(p, off, stride, off2, t); break;
+    default: sum_rows2x2_t<32>(p, off, stride, off2, t); break;
+  }
 }
 
 // LDS-only block barrier: global loads issued before it stay in flight (a
@@ -85,8 +120,42 @@ __device__ __forceinline__ static void fin_block_sync() {
 // each channel's rows summed once per block instead of once per thread;
 // block 0 also publishes coef + running statistics.  Ends with an LDS barrier.
 // smu / sis (optional): also the mean and invstd per channel.
+__device__ __forceinline__ void bn_fin_publish(const BnFin& f, int C, int c, float mean, float var, float invstd, float sc,
+                                               float sh, float* ssc, float* ssh, float* smu, float* sis) {
+  ssc[c] = sc;
+  ssh[c] = sh;
+  if (smu != nullptr) {
+    smu[c] = mean;
+    sis[c] = invstd;
+  }
+  if (blockIdx.x == 0) {
+    f.coef[c] = mean;
+    f.coef[C + c] = invstd;
+    f.coef[2 * C + c] = sc;
+    f.coef[3 * C + c] = sh;
+    if (f.rmean != nullptr) {
+      const float unbiased = f.M > 1 ? var * (float)f.M / (float)(f.M - 1) : var;
+      f.rmean[c] = (1.f - f.momentum) * f.rmean[c] + f.momentum * (mean + (f.bias ? f.bias[c] : 0.f));
+      f.rvar[c] = (1.f - f.momentum) * f.rvar[c] + f.momentum * unbiased;
+    }
+  }
+}
+
 __device__ __forceinline__ void bn_fin_block(const BnFin& f, int C, float* ssc, float* ssh, float* smu = nullptr,
                                              float* sis = nullptr) {
+  if (C == 2 * (int)blockDim.x) {  // block-uniform: both channels' rows in one memory round trip
+    const int c0 = threadIdx.x, c1 = c0 + blockDim.x;
+    const float g0 = f.gamma[c0], b0 = f.beta[c0], g1 = f.gamma[c1], b1 = f.beta[c1];
+    float t[4];
+    sum_rows2x2(f.sums + c0, blockDim.x, 2 * C, C, f.R, t);
+    float mean, var, invstd, sc, sh;
+    bn_fin_from_sums(f, g0, b0, t[0], t[1], mean, var, invstd, sc, sh);
+    bn_fin_publish(f, C, c0, mean, var, invstd, sc, sh, ssc, ssh, smu, sis);
+    bn_fin_from_sums(f, g1, b1, t[2], t[3], mean, var, invstd, sc, sh);
+    bn_fin_publish(f, C, c1, mean, var, invstd, sc, sh, ssc, ssh, smu, sis);
+    fin_block_sync();
+    return;
+  }
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float mean, var, invstd, sc, sh;
     bn_fin_channel(f, C, c, mean, var, invstd, sc, sh);

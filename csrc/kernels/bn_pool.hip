@@ -571,6 +571,16 @@ __device__ __forceinline__ void bwd_apply_body(const bf16_t* __restrict__ y, con
   };
   int64_t i = (int64_t)bid * blockDim.x + threadIdx.x;
   if (i < total) item_loads(i);
+  // stride % C8 == 0 (C8 | 256): a thread's channel chunk c0 is the same for
+  // every item, so its forward coefficients are loaded once, here -- with the
+  // item's loads, before the coefficient-row prologue (after its barrier they
+  // were one more dependent L2 round trip per item)
+  c0 = (int)(i % C8) * 8;
+  BwdCtx cx;
+  load8(cx.mu, coef + c0);
+  load8(cx.is, coef + C + c0);
+  load8(cx.sc, coef + 2 * C + c0);
+  load8(cx.sh, coef + 3 * C + c0);
   if constexpr (SUMS) {
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
       const float gam = gamma[c], istd = coef[C + c];  // issued with (not after) the row loads
@@ -584,21 +594,16 @@ __device__ __forceinline__ void bwd_apply_body(const bf16_t* __restrict__ y, con
     }
     fin_block_sync();
   }
-  for (; i < total;) {
-    BwdCtx cx;
-    load8(cx.mu, coef + c0);
-    load8(cx.is, coef + C + c0);
-    load8(cx.sc, coef + 2 * C + c0);
-    load8(cx.sh, coef + 3 * C + c0);
-    float ka[8], kb[8], kc[8];
-    if constexpr (SUMS) {
+  float ka[8], kb[8], kc[8];
+  if constexpr (SUMS) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) { ka[k] = sk[0][c0 + k]; kb[k] = sk[1][c0 + k]; kc[k] = sk[2][c0 + k]; }
-    } else {
-      load8(ka, acoef + c0);
-      load8(kb, acoef + C + c0);
-      load8(kc, acoef + 2 * C + c0);
-    }
+    for (int k = 0; k < 8; ++k) { ka[k] = sk[0][c0 + k]; kb[k] = sk[1][c0 + k]; kc[k] = sk[2][c0 + k]; }
+  } else {
+    load8(ka, acoef + c0);
+    load8(kb, acoef + C + c0);
+    load8(kc, acoef + 2 * C + c0);
+  }
+  for (; i < total;) {
     float yv[4][8], g[8], dz[4][8];
 #pragma unroll
     for (int w = 0; w < 4; ++w) unpack8(yw[w], yv[w]);
@@ -680,6 +685,11 @@ __global__ void __launch_bounds__(256) bwd_apply_head_kernel(const bf16_t* __res
 // ---------------------------------------------------------------------------
 static void check_c(int C) {
   if (C % 8 != 0) throw std::runtime_error("bn/pool: C must be a multiple of 8");
+}
+// the backward apply keeps a thread's channel chunk for all its items (grid stride % C/8 == 0)
+static void check_c_apply(int C) {
+  check_c(C);
+  if (256 % (C / 8) != 0) throw std::runtime_error("bn backward apply: C/8 must divide 256");
 }
 
 void bn_finalize(uintptr_t partial, int T, int C, int64_t M, uintptr_t gamma, uintptr_t beta, uintptr_t bias,
@@ -817,7 +827,7 @@ void bn_bwd_finalize(uintptr_t partial, int T, int C, int64_t M, uintptr_t gamma
 
 void bn_relu_pool_bwd_apply(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t acoef, uintptr_t dy, int B, int H,
                             int W, int C, int opad, uintptr_t stream) {
-  check_c(C);
+  check_c_apply(C);
   const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
   bn_relu_pool_bwd_apply_kernel<false><<<stream_grid(total), 256, 0, as_stream(stream)>>>(
       (const bf16_t*)y, (const bf16_t*)dP, (const float*)coef, (const float*)acoef, (bf16_t*)dy, B, H, W, C, opad,
@@ -831,7 +841,7 @@ void bn_relu_pool_bwd_apply(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t
 void bn_relu_pool_bwd_apply_sums(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t dgb, uintptr_t gamma, int64_t M,
                                  uintptr_t dy, int B, int H, int W, int C, int opad, uintptr_t dgamma_out,
                                  uintptr_t dbeta_out, uintptr_t stream) {
-  check_c(C);
+  check_c_apply(C);
   if (C > kFinMaxC) throw std::runtime_error("bn_relu_pool_bwd_apply_sums: C too large");
   if (g_host_rows < 1 || g_host_rows > kMaxRows)
     throw std::runtime_error("bn_relu_pool_bwd_apply_sums: needs an atomic reduction mode with <= 32 rows");
@@ -848,7 +858,7 @@ void bn_bwd_apply_head(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t dgb,
                        uintptr_t dy, int B, int H, int W, int C, int opad, uintptr_t dgamma_out, uintptr_t dbeta_out,
                        uintptr_t h, uintptr_t dlogits, uintptr_t loss_b, int F, int NC, uintptr_t dw, uintptr_t db,
                        uintptr_t loss, uintptr_t slot, uintptr_t step_ctr, uintptr_t stream) {
-  check_c(C);
+  check_c_apply(C);
   if (C > kFinMaxC) throw std::runtime_error("bn_bwd_apply_head: C too large");
   if (g_host_rows < 1 || g_host_rows > kMaxRows)
     throw std::runtime_error("bn_bwd_apply_head: needs an atomic reduction mode with <= 32 rows");

@@ -29,6 +29,7 @@
 #include "slab_reduce_dev.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 namespace dl {
@@ -213,11 +214,13 @@ __device__ __forceinline__ int swz_row(int row, int ch) {
 // Transposed reads (ds_read_b64_tr_b16): a 32-lane half reads rows
 // {r0..r0+3, r0+8..r0+11} (or +4) x two adjacent chunks; the XOR spreads those
 // 8 rows over distinct 32-byte slot pairs of the 256-byte bank row.
+// CPR = 32 (512-B rows, the 256-wide wgrad tile): chunks ch and ch + 16 share
+// banks, so the CPR = 16 XOR on the low four chunk bits spreads the rows the same.
 template <int CPR>
 __device__ __forceinline__ int swz_tr(int row, int ch) {
-  if constexpr (CPR == 16) {
+  if constexpr (CPR == 16 || CPR == 32) {
     const int f = 2 * ((row & 3) | (((row >> 3) & 1) << 2));
-    return row * 16 + (ch ^ f);
+    return row * CPR + (ch ^ f);
   } else {
     static_assert(CPR == 8, "swz_tr: rows of 8 or 16 chunks");
     const int f = 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));
@@ -1341,6 +1344,12 @@ __global__ void __launch_bounds__(256) splitk_combine_kernel(const float* __rest
 // channels) -- no slab round trip and no slab_reduce launch.
 // wgrad slab stores staged through LDS as whole rows (set_conv_wgrad_stage_store; A/B)
 __constant__ int g_wgrad_stage_store = 1;
+// wgrad main-loop order (set_conv_wgrad_order; A/B): 1 = DMA issued before the fragment reads
+__constant__ int g_wgrad_order = 1;
+// DL_WGRAD_STAMPS builds only (diagnostics): per-workgroup s_memtime phase
+// sums of waves 0 and NW-1 -> [wg][2][6] = start, loop begin, sum of the
+// steps' wait+barrier, sum of the steps' issue work, loop end, end
+__device__ unsigned long long* g_wgrad_stamps = nullptr;
 
 template <int BM, int BN, int STAGES, int WM = 2, int WN = 2, bool PF = true, bool ATOM = false>
 __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
@@ -1364,6 +1373,9 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
   static_assert(A_INS >= 1 && B_INS >= 1, "tile too small");
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
 
+#ifdef DL_WGRAD_STAMPS
+  unsigned long long st_start = stamp(), st_loop = 0, st_wait = 0, st_work = 0, st_prev = 0, st_lend = 0;
+#endif
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
@@ -1530,17 +1542,50 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
   __builtin_amdgcn_sched_barrier(0);
   read_frags(fa0, fb0);
   int kt_next = PD;
-  auto step = [&](bf16x8 (&fca)[BK / 32][FM], bf16x8 (&fcb)[BK / 32][FN], bf16x8 (&fna)[BK / 32][FM],
-                  bf16x8 (&fnb)[BK / 32][FN]) {
+  // DMA_FIRST (g_wgrad_order = 1): the step's LDS-DMA is issued right after
+  // the barrier, BEFORE the fragment reads.  The asm DMA carries a memory
+  // clobber, so reads issued before it cannot move past it: in the old order
+  // (reads, DMA, MFMAs) the 24 reads were bunched ahead of all MFMAs and the
+  // compiler hoisted the next step's lgkmcnt(0) + barrier to after the 4th
+  // MFMA -- the reads' latency was covered by 4 MFMAs and the other 12 ran
+  // with no reads beside them.  DMA first, the reads and MFMAs share one
+  // scheduling region and interleave (MFMA, 2 reads) as the group barriers
+  // ask, and a closing sched_barrier keeps the next barrier after them.
+  auto step = [&](auto dma_first, bf16x8 (&fca)[BK / 32][FM], bf16x8 (&fcb)[BK / 32][FN],
+                  bf16x8 (&fna)[BK / 32][FM], bf16x8 (&fnb)[BK / 32][FN]) {
+    constexpr bool DF = decltype(dma_first)::value;
+#ifdef DL_WGRAD_STAMPS
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long sa = stamp();
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     wait_vmcnt<(PD - 2) * LPS>();        // stage i+1 landed
     __builtin_amdgcn_s_waitcnt(0xC07F);  // step i's fragments in registers (compiler-visible wait)
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+#ifdef DL_WGRAD_STAMPS
+    {
+      const unsigned long long sb = stamp();
+      __builtin_amdgcn_sched_barrier(0);
+      st_wait += sb - sa;
+      if (st_prev) st_work += sa - st_prev;
+      st_prev = sb;
+    }
+#endif
+    if constexpr (DF) {
+      issue(kt_next, dslot);  // into the slot read two steps ago
+      ++kt_next;
+      ++dslot;
+      dslot -= (dslot == STAGES) * STAGES;
+      __builtin_amdgcn_sched_barrier(0);
+    }
     read_frags(fna, fnb);
-    issue(kt_next, dslot);  // into the slot read two steps ago
-    ++kt_next;
-    ++dslot;
-    dslot -= (dslot == STAGES) * STAGES;
+    if constexpr (!DF) {
+      issue(kt_next, dslot);  // into the slot read two steps ago
+      ++kt_next;
+      ++dslot;
+      dslot -= (dslot == STAGES) * STAGES;
+    }
     // C^T (k x co): lane holds 4 consecutive k of one co -> 16-byte stores
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk)
@@ -1555,7 +1600,10 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
       __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
     }
     if constexpr (NRD > 2 * P1) __builtin_amdgcn_sched_group_barrier(0x100, NRD - 2 * P1, 0);
-    if constexpr (NMF > P1) {
+    if constexpr (DF) {
+      if constexpr (NMF > P1) __builtin_amdgcn_sched_group_barrier(0x008, NMF - P1, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    } else if constexpr (NMF > P1) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x020, LPS, 0);
       if constexpr (NMF > P1 + 1) __builtin_amdgcn_sched_group_barrier(0x008, NMF - P1 - 1, 0);
@@ -1564,13 +1612,40 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
     }
   };
   int i = 0;
-  for (; i + 1 < nk; i += 2) {
-    step(fa0, fb0, fa1, fb1);
-    step(fa1, fb1, fa0, fb0);
+#ifdef DL_WGRAD_STAMPS
+  st_loop = stamp();
+#endif
+  if (g_wgrad_order) {
+    const std::integral_constant<bool, true> df{};
+    for (; i + 1 < nk; i += 2) {
+      step(df, fa0, fb0, fa1, fb1);
+      step(df, fa1, fb1, fa0, fb0);
+    }
+    if (i < nk) step(df, fa0, fb0, fa1, fb1);
+  } else {
+    const std::integral_constant<bool, false> df{};
+    for (; i + 1 < nk; i += 2) {
+      step(df, fa0, fb0, fa1, fb1);
+      step(df, fa1, fb1, fa0, fb0);
+    }
+    if (i < nk) step(df, fa0, fb0, fa1, fb1);
   }
-  if (i < nk) step(fa0, fb0, fa1, fb1);
   }
 
+#ifdef DL_WGRAD_STAMPS
+  st_lend = stamp();
+  struct StampOut {
+    unsigned long long* p;
+    unsigned long long v[5];
+    int w;
+    __device__ ~StampOut() {
+      if (p && (threadIdx.x & 63) == 0 && (w == 0 || w == (int)(blockDim.x >> 6) - 1)) {
+        unsigned long long* d = p + ((size_t)(blockIdx.x + blockIdx.y * gridDim.x) * 2 + (w ? 1 : 0)) * 6;
+        d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3]; d[4] = v[4]; d[5] = stamp();
+      }
+    }
+  } stamp_out{g_wgrad_stamps, {st_start, st_loop, st_wait, st_work, st_lend}, wid};
+#endif
   const int col_l = lane & 15, rq = lane >> 4;
   if constexpr (ATOM) {
     const int logCin = g.logC8 + 3, taps = g.KH * g.KW;
@@ -2163,7 +2238,15 @@ void set_conv_wgrad_stage_store(int on) {
   const int v = on ? 1 : 0;
   DL_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_wgrad_stage_store), &v, sizeof(int)));
 }
+void set_conv_wgrad_order(int dma_first) {
+  const int v = dma_first ? 1 : 0;
+  DL_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_wgrad_order), &v, sizeof(int)));
+}
 void set_conv_debug(uintptr_t buf) { g_conv_dbg = (unsigned long long*)buf; }
+void set_conv_wgrad_stamps(uintptr_t buf) {
+  unsigned long long* p = (unsigned long long*)buf;
+  DL_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_wgrad_stamps), &p, sizeof(p)));
+}
 
 void set_conv_stages(int fwd, int wgrad) {
   if (fwd < 2 || fwd > 4 || wgrad < 0 || wgrad > 4) throw std::runtime_error("stages must be 2..4 (wgrad 0 = default)");
@@ -2561,8 +2644,9 @@ static void conv_wgrad_g(const ConvGeom& g, uintptr_t dy, uintptr_t x, uintptr_t
   if (ldo < g.K) throw std::runtime_error("conv_wgrad: ldo < K");
   if (ldo % 4 != 0) throw std::runtime_error("conv_wgrad: ldo % 4 != 0 (16-byte slab stores)");
   if (Cout % 8 != 0) throw std::runtime_error("conv_wgrad: Cout % 8 != 0");
-  const int bm = tile == 1 ? 64 : 128;
+  const int bm = tile == 1 ? 64 : (tile == 3 ? 256 : 128);
   if (Cout % bm != 0) throw std::runtime_error("conv_wgrad: Cout must be a multiple of the Cout tile");
+  if (tile == 3 && g_fwd_waves != 8) throw std::runtime_error("conv_wgrad: the 256x128 tile needs 8 waves");
   if (g.pow2 && W > 64) throw std::runtime_error("conv_wgrad: needs W <= 64");
   if (splits < 1) splits = 1;
   if (atomic_creal > Cin) throw std::runtime_error("conv_wgrad: atomic_creal > Cin");
@@ -2605,6 +2689,14 @@ static void conv_wgrad_g(const ConvGeom& g, uintptr_t dy, uintptr_t x, uintptr_t
       } else {
         if (pf) DL_WG(128, 128, 3, 2, 4); else DL_WGN(128, 128, 3, 2, 4);
       }
+    } else if (tile == 3) {
+      // 256 (co) x 128 (k): 48 KiB per 64-row stage, 3 stages = 144 KiB (one WG
+      // per CU); half again the MFMAs per DMA'd byte of the 128x128 tile, whose
+      // steps were bound by LDS-DMA issue and L2->LDS bytes, not by the MFMAs
+      // (scripts/stamp_wgrad.py: ~1240 cycles per step vs 512 of MFMA per SIMD)
+      // no fragment prefetch by default: the double fragment set does not fit the
+      // 256 registers of 2 waves per SIMD (spills: 275 vs 37 us at 100 workgroups)
+      if (g_wgrad_pf == 1) DL_WG(256, 128, 3, 4, 2); else DL_WGN(256, 128, 3, 4, 2);
     } else {
       if (st >= 4) DL_WG(64, 64, 4, 2, 4); else DL_WG(64, 64, 3, 2, 4);
     }

@@ -60,6 +60,14 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
   float rsc[8], rsh[8], rmu[8], ris[8];  // RED: BN coefficients of the thread's 8 channels
   if (one) {
     const int j0 = tid * 8;
+    // the classifier weights first: independent of everything below, so their
+    // L2 round trip overlaps the window loads and the BN coefficient rows
+    // (issued after bn_fin_block's barrier they were a third round trip)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      wc[c][0] = *reinterpret_cast<const float4*>(w + (int64_t)c * F + j0);
+      wc[c][1] = *reinterpret_cast<const float4*>(w + (int64_t)c * F + j0 + 4);
+    }
     uint4 hv;
     if constexpr (POOL) {
       // feature j0 = (oh * Wo + ow) * yC + c0 of the pooled NHWC map
@@ -112,11 +120,6 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
       *reinterpret_cast<uint4*>(hp.h_out + (int64_t)b * F + j0) = hv;
     } else {
       hv = *reinterpret_cast<const uint4*>(hb + j0);
-    }
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      wc[c][0] = *reinterpret_cast<const float4*>(w + (int64_t)c * F + j0);
-      wc[c][1] = *reinterpret_cast<const float4*>(w + (int64_t)c * F + j0 + 4);
     }
     const float hf[8] = {lo_bf16(hv.x), hi_bf16(hv.x), lo_bf16(hv.y), hi_bf16(hv.y),
                          lo_bf16(hv.z), hi_bf16(hv.z), lo_bf16(hv.w), hi_bf16(hv.w)};

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--rstages", type=int, default=0, help="region kernel B-ring stages (0 = max that fits)")
     ap.add_argument("--rwaves", type=int, default=8, help="region kernel waves per workgroup (4 or 8)")
     ap.add_argument("--wstage", type=int, default=1, help="wgrad slab stores staged through LDS as whole rows")
+    ap.add_argument("--worder", type=int, default=1, help="wgrad main loop: 1 DMA before the fragment reads, 0 after")
     a = ap.parse_args()
     C = _native.native()
     fs, ws = (int(v) for v in a.stages.split(","))
@@ -86,9 +87,9 @@ def main():
                 cur()),
                 f"tile{dt} split{ds}"))
         wtile, wsp = _wgrad_plan(cout, K, M)
-        if a.wtile >= 0 and cout % 128 == 0:
+        if a.wtile >= 0 and cout % (256 if a.wtile == 3 else 128) == 0:
             wtile = a.wtile
-            bm, bn = (128, 128) if wtile == 2 else ((128, 64) if wtile == 0 else (64, 64))
+            bm, bn = {3: (256, 128), 2: (128, 128), 0: (128, 64)}.get(wtile, (64, 64))
             tiles = (cout // bm) * ((K + bn - 1) // bn)
             wsp = 1
             while tiles * wsp < 256 and M // (wsp * 2) >= 2048:

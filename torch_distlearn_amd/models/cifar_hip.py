@@ -54,6 +54,10 @@ _NOSPLIT_64 = os.environ.get("DISTLEARN_FWD_NOSPLIT64", "0") == "1"
 # the fp32 slab bytes written and combined, twice the workgroups per split;
 # 0.3306 vs 0.3347 ms/step (profiles/r3_split128x64_ab.txt)
 _SPLIT_128x64 = os.environ.get("DISTLEARN_SPLIT_128x64", "1") == "1"
+# weight gradients of Cout % 256 == 0 layers on 256x128 tiles (csrc conv_wgrad tile 3;
+# A/B, off): without fragment prefetch (the double fragment set spills at 2 waves per
+# SIMD) wgrad3 24.5 vs 22.4 us, end to end 0.358 vs 0.331 ms (profiles/r3_wgrad_tile256_ab.txt)
+_WGRAD_256 = os.environ.get("DISTLEARN_WGRAD_256", "0") == "1"
 
 
 # The fwd/dgrad split-K slab holds SLAB_CAP x splits slices, announced to
@@ -92,7 +96,7 @@ def _fwd_plan(M: int, N: int, K: int):
     return tile, splits
 
 
-def _wgrad_plan(cout: int, K: int, M: int, reserve: int = 0):
+def _wgrad_plan(cout: int, K: int, M: int, reserve: int = 0, wide: Optional[bool] = None):
     """(tile, splits) for the weight gradient.  128x128 tiles (tile 2: 4-stage
     DMA ring, fragment prefetch, one workgroup per CU) whenever Cout allows,
     else 64x64 (two per CU).  Every workgroup is one ~20 us "round", so the
@@ -102,9 +106,13 @@ def _wgrad_plan(cout: int, K: int, M: int, reserve: int = 0):
     ``reserve`` CUs are left to a concurrent RCCL collective (its workgroups do
     not fit beside these: parallel/comm.py)."""
     tile = 2 if cout % 128 == 0 else 1
-    if tile == 2 and "DISTLEARN_WGRAD_TILE" in os.environ:  # tuning: 0 = 128x64 tiles
+    if cout % 256 == 0 and (_WGRAD_256 if wide is None else wide):
+        tile = 3
+    if tile >= 2 and "DISTLEARN_WGRAD_TILE" in os.environ:  # tuning: 0 = 128x64, 2 = 128x128, 3 = 256x128
         tile = int(os.environ["DISTLEARN_WGRAD_TILE"])
-    bm, bn = {2: (128, 128), 1: (64, 64), 0: (128, 64)}[tile]
+        if tile == 3 and cout % 256 != 0:
+            tile = 2
+    bm, bn = {3: (256, 128), 2: (128, 128), 1: (64, 64), 0: (128, 64)}[tile]
     slots = 2 * (256 - reserve) if tile == 1 else 256 - reserve
     tiles = (cout // bm) * ((K + bn - 1) // bn)
     splits = max(1, min(slots // tiles, M // 512))
@@ -182,6 +190,8 @@ class CifarHIPExecutor:
             self.C.set_conv_posm(int(os.environ["DISTLEARN_POSM"]))
         if "DISTLEARN_FWD_TR" in os.environ:  # A/B: transposed-accumulator streaming kernel (1) or not (0)
             self.C.set_conv_fwd_tr(int(os.environ["DISTLEARN_FWD_TR"]))
+        if "DISTLEARN_WGRAD_ORDER" in os.environ:  # A/B: wgrad DMA before (1) or after (0) the fragment reads
+            self.C.set_conv_wgrad_order(int(os.environ["DISTLEARN_WGRAD_ORDER"]))
         if "DISTLEARN_WGRAD_PF" in os.environ:  # tuning: wgrad fragment prefetch (-1 auto, 0, 1)
             self.C.set_conv_wgrad_pf(int(os.environ["DISTLEARN_WGRAD_PF"]))
         # fuse the last block's BN/ReLU/pool into the head kernel (2048 pooled features)

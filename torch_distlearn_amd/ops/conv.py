@@ -128,10 +128,14 @@ def _plan_1x1(M: int, N: int, K: int):
     return tile | (stages << 4) | (waves << 8), 1
 
 
+# ResNet-50 1x1 weight gradients on the 256x128 tile where Cout allows (A/B, default off)
+_WGRAD_256 = os.environ.get("DISTLEARN_RESNET_WGRAD_256", "0") == "1"
+
+
 def _wgrad_plan(cout: int, K: int, M: int):
     from ..models.cifar_hip import _wgrad_plan as plan
 
-    return plan(cout, K, M, 0)
+    return plan(cout, K, M, 0, wide=_WGRAD_256)
 
 
 def _bn_reduce_begin(C, link, M: int, cin: int, nrows: int, residual_add: bool = False):
