@@ -1351,7 +1351,7 @@ __constant__ int g_wgrad_order = 1;
 // steps' wait+barrier, sum of the steps' issue work, loop end, end
 __device__ unsigned long long* g_wgrad_stamps = nullptr;
 
-template <int BM, int BN, int STAGES, int WM = 2, int WN = 2, bool PF = true, bool ATOM = false>
+template <int BM, int BN, int STAGES, int WM = 2, int WN = 2, bool PF = true, bool ATOM = false, int BK_ = 64>
 __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                          float* __restrict__ out, const ConvGeom g, int m_per_split,
                                                          int ldo, int creal) {
@@ -1361,8 +1361,12 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
   // step is U(step) + L(r): a wave-uniform part plus a per-lane constant, so
   // a load is one add, no bounds test (m_per_split % 64 == 0, Cout % BM == 0);
   // only a partial last step (M % 64 != 0) tests rows (wave-uniform branch).
-  constexpr int BK = 64, NW = WM * WN, PD = STAGES - 1;
-  static_assert(STAGES >= 2 && STAGES <= 4, "2..4 stages");
+  // BK_ = 32 (the 256x128 tile): 32-row steps, which start at multiples of 32
+  // -- the host then needs W | 32 for the pow2 decomposition (H*W and 32 are
+  // powers of two, so one divides the other)
+  constexpr int BK = BK_, NW = WM * WN, PD = STAGES - 1;
+  static_assert(BK == 32 || BK == 64, "32- or 64-row steps");
+  static_assert(STAGES >= 2 && STAGES <= 8, "2..8 stages");
   constexpr int ACPR = BM / 8, BCPR = BN / 8;  // chunks per LDS row (row = one m)
   constexpr int A_BYTES = BK * BM * 2, B_BYTES = BK * BN * 2, STAGE_BYTES = A_BYTES + B_BYTES;
   constexpr int A_INS = A_BYTES / 1024 / NW, B_INS = B_BYTES / 1024 / NW;
@@ -2644,9 +2648,9 @@ static void conv_wgrad_g(const ConvGeom& g, uintptr_t dy, uintptr_t x, uintptr_t
   if (ldo < g.K) throw std::runtime_error("conv_wgrad: ldo < K");
   if (ldo % 4 != 0) throw std::runtime_error("conv_wgrad: ldo % 4 != 0 (16-byte slab stores)");
   if (Cout % 8 != 0) throw std::runtime_error("conv_wgrad: Cout % 8 != 0");
-  const int bm = tile == 1 ? 64 : (tile == 3 ? 256 : 128);
+  const int bm = tile == 1 ? 64 : (tile >= 3 ? 256 : 128);
   if (Cout % bm != 0) throw std::runtime_error("conv_wgrad: Cout must be a multiple of the Cout tile");
-  if (tile == 3 && g_fwd_waves != 8) throw std::runtime_error("conv_wgrad: the 256x128 tile needs 8 waves");
+  if (tile >= 3 && g_fwd_waves != 8) throw std::runtime_error("conv_wgrad: the 256x128 tiles need the 8-wave config");
   if (g.pow2 && W > 64) throw std::runtime_error("conv_wgrad: needs W <= 64");
   if (splits < 1) splits = 1;
   if (atomic_creal > Cin) throw std::runtime_error("conv_wgrad: atomic_creal > Cin");
@@ -2654,17 +2658,18 @@ static void conv_wgrad_g(const ConvGeom& g, uintptr_t dy, uintptr_t x, uintptr_t
   mps = (mps + 63) / 64 * 64;  // 64-row aligned M steps (padded-layout addressing)
   hipStream_t s = as_stream(stream);
   const bool atom = atomic_creal > 0;
-#define DL_WGX(BM_, BN_, ST_, WM_, WN_, PF_)                                                                \
+#define DL_WGXK(BM_, BN_, ST_, WM_, WN_, PF_, BK_)                                                         \
   do {                                                                                                     \
     const int nt = ((g.Cout + BM_ - 1) / BM_) * ((g.K + BN_ - 1) / BN_);                                  \
     const dim3 grid = g_wgrad_xcd ? dim3(nt * splits, 1) : dim3(nt, splits);                              \
     if (atom)                                                                                              \
-      conv_wgrad_kernel<BM_, BN_, ST_, WM_, WN_, PF_, true><<<grid, 64 * WM_ * WN_, 0, s>>>(               \
+      conv_wgrad_kernel<BM_, BN_, ST_, WM_, WN_, PF_, true, BK_><<<grid, 64 * WM_ * WN_, 0, s>>>(          \
           (const bf16_t*)dy, (const bf16_t*)x, (float*)out, g, mps, ldo, atomic_creal);                     \
     else                                                                                                   \
-      conv_wgrad_kernel<BM_, BN_, ST_, WM_, WN_, PF_, false><<<grid, 64 * WM_ * WN_, 0, s>>>(              \
+      conv_wgrad_kernel<BM_, BN_, ST_, WM_, WN_, PF_, false, BK_><<<grid, 64 * WM_ * WN_, 0, s>>>(         \
           (const bf16_t*)dy, (const bf16_t*)x, (float*)out, g, mps, ldo, Cin);                              \
   } while (0)
+#define DL_WGX(BM_, BN_, ST_, WM_, WN_, PF_) DL_WGXK(BM_, BN_, ST_, WM_, WN_, PF_, 64)
 #define DL_WG(BM_, BN_, ST_, WM_, WN_) DL_WGX(BM_, BN_, ST_, WM_, WN_, true)
 #define DL_WGN(BM_, BN_, ST_, WM_, WN_) DL_WGX(BM_, BN_, ST_, WM_, WN_, false)
   // the wgrad pipeline keeps >= 2 stages in flight beyond the one being read.
@@ -2697,6 +2702,13 @@ static void conv_wgrad_g(const ConvGeom& g, uintptr_t dy, uintptr_t x, uintptr_t
       // no fragment prefetch by default: the double fragment set does not fit the
       // 256 registers of 2 waves per SIMD (spills: 275 vs 37 us at 100 workgroups)
       if (g_wgrad_pf == 1) DL_WG(256, 128, 3, 4, 2); else DL_WGN(256, 128, 3, 4, 2);
+    } else if (tile == 4) {
+      // 256x128 with 32-row steps: 24 KiB per stage, a 6-stage ring (144 KiB,
+      // one WG per CU); per step and wave 16 MFMAs (as the 128x128 tile), 16
+      // fragment reads (24) and 3 LDS-DMA pieces (4): the L2->LDS bytes per MFMA
+      // drop by a third and the halved fragment set fits with prefetch
+      if (g.pow2 && W > 32) throw std::runtime_error("conv_wgrad tile 4: needs W <= 32");
+      DL_WGXK(256, 128, 6, 4, 2, true, 32);
     } else {
       if (st >= 4) DL_WG(64, 64, 4, 2, 4); else DL_WG(64, 64, 3, 2, 4);
     }
@@ -2712,6 +2724,7 @@ static void conv_wgrad_g(const ConvGeom& g, uintptr_t dy, uintptr_t x, uintptr_t
 #undef DL_WG
 #undef DL_WGN
 #undef DL_WGX
+#undef DL_WGXK
   DL_HIP_CHECK(hipGetLastError());
 }
 

@@ -87,9 +87,9 @@ def main():
                 cur()),
                 f"tile{dt} split{ds}"))
         wtile, wsp = _wgrad_plan(cout, K, M)
-        if a.wtile >= 0 and cout % (256 if a.wtile == 3 else 128) == 0:
+        if a.wtile >= 0 and cout % (256 if a.wtile >= 3 else 128) == 0:
             wtile = a.wtile
-            bm, bn = {3: (256, 128), 2: (128, 128), 0: (128, 64)}.get(wtile, (64, 64))
+            bm, bn = {4: (256, 128), 3: (256, 128), 2: (128, 128), 0: (128, 64)}.get(wtile, (64, 64))
             tiles = (cout // bm) * ((K + bn - 1) // bn)
             wsp = 1
             while tiles * wsp < 256 and M // (wsp * 2) >= 2048:

@@ -56,7 +56,8 @@ _NOSPLIT_64 = os.environ.get("DISTLEARN_FWD_NOSPLIT64", "0") == "1"
 _SPLIT_128x64 = os.environ.get("DISTLEARN_SPLIT_128x64", "1") == "1"
 # weight gradients of Cout % 256 == 0 layers on 256x128 tiles (csrc conv_wgrad tile 3;
 # A/B, off): without fragment prefetch (the double fragment set spills at 2 waves per
-# SIMD) wgrad3 24.5 vs 22.4 us, end to end 0.358 vs 0.331 ms (profiles/r3_wgrad_tile256_ab.txt)
+# SIMD) wgrad3 24.5 vs 22.4 us, end to end 0.358 vs 0.331 ms; tile 4 = 256x128 with 32-row
+# steps (fits with prefetch): wgrad3 25.7 vs 22.2 us, 0.361 vs 0.332 ms (profiles/r3_wgrad_tile256_ab.txt)
 _WGRAD_256 = os.environ.get("DISTLEARN_WGRAD_256", "0") == "1"
 
 
@@ -110,9 +111,9 @@ def _wgrad_plan(cout: int, K: int, M: int, reserve: int = 0, wide: Optional[bool
         tile = 3
     if tile >= 2 and "DISTLEARN_WGRAD_TILE" in os.environ:  # tuning: 0 = 128x64, 2 = 128x128, 3 = 256x128
         tile = int(os.environ["DISTLEARN_WGRAD_TILE"])
-        if tile == 3 and cout % 256 != 0:
+        if tile >= 3 and cout % 256 != 0:
             tile = 2
-    bm, bn = {3: (256, 128), 2: (128, 128), 1: (64, 64), 0: (128, 64)}[tile]
+    bm, bn = {4: (256, 128), 3: (256, 128), 2: (128, 128), 1: (64, 64), 0: (128, 64)}[tile]
     slots = 2 * (256 - reserve) if tile == 1 else 256 - reserve
     tiles = (cout // bm) * ((K + bn - 1) // bn)
     splits = max(1, min(slots // tiles, M // 512))
