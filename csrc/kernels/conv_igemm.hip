@@ -271,6 +271,9 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
 // line for K/M tails.
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 constexpr unsigned kOOB = 0x40000000u;  // a voffset past every operand: loads zeros
+// streaming fwd/dgrad kernel main loop (set_conv_fwd_pf; A/B): 1 = register
+// prefetch of the next step's fragments + unconditional DMA pipeline (4 stages)
+__constant__ int g_fwd_pf = 1;
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
@@ -848,64 +851,174 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const unsigned long long t_setup = dbg ? stamp() : 0ull;
+  // Fragment-prefetch pipeline (g_fwd_pf, STAGES >= 3): every step issues one
+  // stage unconditionally (zero-fill past nk keeps the vmcnt count constant),
+  // right after the barrier and before the fragment reads (asm DMA: the reads
+  // cannot be hoisted above it, and hipcc's LDS-DMA alias waits stay out);
+  // the fragments of step i+1 are read while the MFMAs of step i run.  The
+  // plain loop below read each step's fragments and waited for them before
+  // its first MFMA: the LDS latency was exposed at every step.
+  // (4 stages: two in flight beyond the one being read; at 3 the step waited
+  // for the stage issued one step earlier: 0.352 vs 0.341 ms/step, at 4 0.336)
+  bool done = false;
+  if constexpr (STAGES >= 4) {
+    if (g_fwd_pf) {
+      done = true;
+      const i32x4 xr4 = make_rsrc4(x, (unsigned)((int64_t)g.B * g.Hp * g.Wp * g.Cin * 2));
+      const i32x4 wr4 = make_rsrc4(w, (unsigned)((int64_t)g.Cout * g.K * 2));
+      auto issue_stage = [&](int kt, int slot, bool valid) {
+        char* sA = smem + slot * STAGE_BYTES;
+        char* sB = sA + A_BYTES;
 #pragma unroll
-  for (int p = 0; p < PD; ++p)
-    if (p < nk) {
-#pragma unroll
-      for (int q = 0; q < LPS; ++q) issue_one(q, kt_beg + p, p, tnext);
-      tap_advance(tnext);
-    }
-  // MFMAs per K step and the spacing of the next stage's DMA issues between them
-  constexpr int NMF = (BK / 32) * FM * FN;
-  constexpr int IL = NMF / LPS > 0 ? NMF / LPS : 1;
-  int slot_c = 0, slot_n = PD % STAGES;
-  auto kstep = [&](int i) {
-    block_sync_lds();  // stage i landed for every wave; slot (i+PD)%STAGES no longer read
-    const bool pf = i + PD < nk;
-    const int kt_n = kt_beg + i + PD;
-    const uint4* As = reinterpret_cast<const uint4*>(smem + slot_c * STAGE_BYTES);
-    const uint4* Bs = reinterpret_cast<const uint4*>(smem + slot_c * STAGE_BYTES + A_BYTES);
-    bf16x8 af[BK / 32][FM], bfr[BK / 32][FN];
-#pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
-      const int ch = kk * 4 + (lane >> 4);
-#pragma unroll
-      for (int a = 0; a < FM; ++a)
-        af[kk][a] = __builtin_bit_cast(bf16x8, As[swz_row<CPR>(wm * TM + a * 16 + (lane & 15), ch)]);
-#pragma unroll
-      for (int b = 0; b < FN; ++b) {
-        const int row = wn * TN + (TR ? b_frag_row(b, lane & 15) : b * 16 + (lane & 15));
-        bfr[kk][b] = __builtin_bit_cast(bf16x8, Bs[row * CPR + (ch ^ swz_b(row))]);
-      }
-    }
-    // the next stage's LDS-DMA issues ride between the MFMAs (their issue cost
-    // overlaps matrix-core execution instead of serialising in front of it)
-#pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk)
-#pragma unroll
-      for (int a = 0; a < FM; ++a)
-#pragma unroll
-        for (int b = 0; b < FN; ++b) {
-          acc[a][b] = TR ? mfma16(bfr[kk][b], af[kk][a], acc[a][b]) : mfma16(af[kk][a], bfr[kk][b], acc[a][b]);
-          const int idx = (kk * FM + a) * FN + b;
-          if (idx % IL == IL - 1 && idx / IL < LPS) {
-            if (pf) issue_one(idx / IL, kt_n, slot_n, tnext);
-            __builtin_amdgcn_sched_barrier(0);
+        for (int j = 0; j < A_INS; ++j) {
+          if constexpr (TAPU) {
+            blds16_asm(xr4, valid ? 2u * (unsigned)a_base[j] : kOOB, valid ? 2u * (unsigned)tnext.off : 0u,
+                       sA + (wid * A_INS + j) * 1024);
+          } else {
+            const int kc = kt * CPR + a_ch[j];
+            const int kpos = kc >> g.logC8;
+            const int c0 = (kc & (C8 - 1)) << 3;
+            const int kh = kpos / g.KW, kw = kpos - kh * g.KW;
+            const unsigned off =
+                (valid && kc < g.Kch) ? 2u * (unsigned)(a_base[j] + (kh * g.Wp + kw) * g.Cin + c0) : kOOB;
+            blds16_asm(xr4, off, 0u, sA + (wid * A_INS + j) * 1024);
           }
         }
-    if (pf) tap_advance(tnext);
-    slot_c = slot_c + 1 == STAGES ? 0 : slot_c + 1;
-    slot_n = slot_n + 1 == STAGES ? 0 : slot_n + 1;
-  };
-  // steady state (constant wait: stage i landed, PD-1 younger stages in flight), then the drain
-  int i = 0;
-  for (; i < nk - (PD - 1); ++i) {
-    wait_vmcnt<(PD - 1) * LPS>();
-    kstep(i);
+#pragma unroll
+        for (int j = 0; j < B_INS; ++j) {
+          const int kadd = TAPU ? tnext.wk : kt * BK;
+          unsigned voff = 2u * (unsigned)b_off[j];
+          if constexpr (!TAPU) voff = (kadd + b_k[j]) < g.K ? voff : kOOB;
+          blds16_asm(wr4, valid ? voff : kOOB, valid ? 2u * (unsigned)kadd : 0u, sB + (wid * B_INS + j) * 1024);
+        }
+        if (valid) tap_advance(tnext);
+      };
+      auto read_frags = [&](int slot, bf16x8 (&af)[BK / 32][FM], bf16x8 (&bfr)[BK / 32][FN]) {
+        const uint4* As = reinterpret_cast<const uint4*>(smem + slot * STAGE_BYTES);
+        const uint4* Bs = reinterpret_cast<const uint4*>(smem + slot * STAGE_BYTES + A_BYTES);
+#pragma unroll
+        for (int kk = 0; kk < BK / 32; ++kk) {
+          const int ch = kk * 4 + (lane >> 4);
+#pragma unroll
+          for (int a = 0; a < FM; ++a)
+            af[kk][a] = __builtin_bit_cast(bf16x8, As[swz_row<CPR>(wm * TM + a * 16 + (lane & 15), ch)]);
+#pragma unroll
+          for (int b = 0; b < FN; ++b) {
+            const int row = wn * TN + (TR ? b_frag_row(b, lane & 15) : b * 16 + (lane & 15));
+            bfr[kk][b] = __builtin_bit_cast(bf16x8, Bs[row * CPR + (ch ^ swz_b(row))]);
+          }
+        }
+      };
+#pragma unroll
+      for (int p = 0; p < PD; ++p) issue_stage(kt_beg + p, p, p < nk);
+      constexpr int NRD = (BK / 32) * (FM + FN);  // ds_read_b128 per step
+      constexpr int NMF = (BK / 32) * FM * FN;
+      bf16x8 fa0[BK / 32][FM], fb0[BK / 32][FN], fa1[BK / 32][FM], fb1[BK / 32][FN];
+      wait_vmcnt<(PD - 1) * LPS>();  // stage 0 landed
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      read_frags(0, fa0, fb0);
+      int kt_next = kt_beg + PD, slot_n = PD % STAGES, slot_r = 1 % STAGES;
+      auto step = [&](int i, bf16x8 (&fca)[BK / 32][FM], bf16x8 (&fcb)[BK / 32][FN], bf16x8 (&fna)[BK / 32][FM],
+                      bf16x8 (&fnb)[BK / 32][FN]) {
+        wait_vmcnt<(PD - 2) * LPS>();        // stage i+1 landed
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // step i's fragments in registers
+        __builtin_amdgcn_s_barrier();        // every wave done reading slot i-1
+        __builtin_amdgcn_sched_barrier(0);
+        issue_stage(kt_next, slot_n, i + PD < nk);
+        ++kt_next;
+        slot_n = slot_n + 1 == STAGES ? 0 : slot_n + 1;
+        __builtin_amdgcn_sched_barrier(0);
+        read_frags(slot_r, fna, fnb);  // (past nk: zeros, never used)
+        slot_r = slot_r + 1 == STAGES ? 0 : slot_r + 1;
+#pragma unroll
+        for (int kk = 0; kk < BK / 32; ++kk)
+#pragma unroll
+          for (int a = 0; a < FM; ++a)
+#pragma unroll
+            for (int b = 0; b < FN; ++b)
+              acc[a][b] = TR ? mfma16(fcb[kk][b], fca[kk][a], acc[a][b]) : mfma16(fca[kk][a], fcb[kk][b], acc[a][b]);
+        constexpr int P1 = NRD < NMF ? NRD : NMF;  // (MFMA, read) pairs
+#pragma unroll
+        for (int q = 0; q < P1; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        if constexpr (NRD > P1) __builtin_amdgcn_sched_group_barrier(0x100, NRD - P1, 0);
+        if constexpr (NMF > P1) __builtin_amdgcn_sched_group_barrier(0x008, NMF - P1, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      int i = 0;
+      for (; i + 1 < nk; i += 2) {
+        step(i, fa0, fb0, fa1, fb1);
+        step(i + 1, fa1, fb1, fa0, fb0);
+      }
+      if (i < nk) step(i, fa0, fb0, fa1, fb1);
+      wait_vmcnt<0>();  // the trailing zero-fill DMAs still target the ring (the epilogue reuses it)
+    }
   }
-  for (; i < nk; ++i) {
-    wait_stages<LPS>(nk - 1 - i);
-    kstep(i);
+  if (!done) {
+#pragma unroll
+    for (int p = 0; p < PD; ++p)
+      if (p < nk) {
+#pragma unroll
+        for (int q = 0; q < LPS; ++q) issue_one(q, kt_beg + p, p, tnext);
+        tap_advance(tnext);
+      }
+    // MFMAs per K step and the spacing of the next stage's DMA issues between them
+    constexpr int NMF = (BK / 32) * FM * FN;
+    constexpr int IL = NMF / LPS > 0 ? NMF / LPS : 1;
+    int slot_c = 0, slot_n = PD % STAGES;
+    auto kstep = [&](int i) {
+      block_sync_lds();  // stage i landed for every wave; slot (i+PD)%STAGES no longer read
+      const bool pf = i + PD < nk;
+      const int kt_n = kt_beg + i + PD;
+      const uint4* As = reinterpret_cast<const uint4*>(smem + slot_c * STAGE_BYTES);
+      const uint4* Bs = reinterpret_cast<const uint4*>(smem + slot_c * STAGE_BYTES + A_BYTES);
+      bf16x8 af[BK / 32][FM], bfr[BK / 32][FN];
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        const int ch = kk * 4 + (lane >> 4);
+#pragma unroll
+        for (int a = 0; a < FM; ++a)
+          af[kk][a] = __builtin_bit_cast(bf16x8, As[swz_row<CPR>(wm * TM + a * 16 + (lane & 15), ch)]);
+#pragma unroll
+        for (int b = 0; b < FN; ++b) {
+          const int row = wn * TN + (TR ? b_frag_row(b, lane & 15) : b * 16 + (lane & 15));
+          bfr[kk][b] = __builtin_bit_cast(bf16x8, Bs[row * CPR + (ch ^ swz_b(row))]);
+        }
+      }
+      // the next stage's LDS-DMA issues ride between the MFMAs (their issue cost
+      // overlaps matrix-core execution instead of serialising in front of it)
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk)
+#pragma unroll
+        for (int a = 0; a < FM; ++a)
+#pragma unroll
+          for (int b = 0; b < FN; ++b) {
+            acc[a][b] = TR ? mfma16(bfr[kk][b], af[kk][a], acc[a][b]) : mfma16(af[kk][a], bfr[kk][b], acc[a][b]);
+            const int idx = (kk * FM + a) * FN + b;
+            if (idx % IL == IL - 1 && idx / IL < LPS) {
+              if (pf) issue_one(idx / IL, kt_n, slot_n, tnext);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+      if (pf) tap_advance(tnext);
+      slot_c = slot_c + 1 == STAGES ? 0 : slot_c + 1;
+      slot_n = slot_n + 1 == STAGES ? 0 : slot_n + 1;
+    };
+    // steady state (constant wait: stage i landed, PD-1 younger stages in flight), then the drain
+    int i = 0;
+    for (; i < nk - (PD - 1); ++i) {
+      wait_vmcnt<(PD - 1) * LPS>();
+      kstep(i);
+    }
+    for (; i < nk; ++i) {
+      wait_stages<LPS>(nk - 1 - i);
+      kstep(i);
+    }
+
   }
 
   const unsigned long long t_loop = dbg ? stamp() : 0ull;
@@ -2242,6 +2355,10 @@ void set_conv_wgrad_stage_store(int on) {
   const int v = on ? 1 : 0;
   DL_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_wgrad_stage_store), &v, sizeof(int)));
 }
+void set_conv_fwd_pf(int on) {
+  const int v = on ? 1 : 0;
+  DL_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_fwd_pf), &v, sizeof(int)));
+}
 void set_conv_wgrad_order(int dma_first) {
   const int v = dma_first ? 1 : 0;
   DL_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_wgrad_order), &v, sizeof(int)));
@@ -2253,7 +2370,8 @@ void set_conv_wgrad_stamps(uintptr_t buf) {
 }
 
 void set_conv_stages(int fwd, int wgrad) {
-  if (fwd < 2 || fwd > 4 || wgrad < 0 || wgrad > 4) throw std::runtime_error("stages must be 2..4 (wgrad 0 = default)");
+  if (fwd < 2 || fwd > 4 || wgrad < 0 || wgrad > 5)
+    throw std::runtime_error("stages must be 2..4 (wgrad 0 = default, 5 = 128x128 tiles only)");
   g_fwd_stages = fwd;
   g_wgrad_stages = wgrad;
 }
@@ -2689,7 +2807,9 @@ static void conv_wgrad_g(const ConvGeom& g, uintptr_t dy, uintptr_t x, uintptr_t
         if (pf) DL_WG(128, 64, 3, 4, 2); else DL_WGN(128, 64, 3, 4, 2);
       }
     } else if (tile == 2) {
-      if (st >= 4) {
+      if (st >= 5) {
+        DL_WG(128, 128, 5, 2, 4);  // the whole 160 KiB LDS: three stages in flight beyond the one read
+      } else if (st >= 4) {
         if (pf) DL_WG(128, 128, 4, 2, 4); else DL_WGN(128, 128, 4, 2, 4);
       } else {
         if (pf) DL_WG(128, 128, 3, 2, 4); else DL_WGN(128, 128, 3, 2, 4);

@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--rwaves", type=int, default=8, help="region kernel waves per workgroup (4 or 8)")
     ap.add_argument("--wstage", type=int, default=1, help="wgrad slab stores staged through LDS as whole rows")
     ap.add_argument("--worder", type=int, default=1, help="wgrad main loop: 1 DMA before the fragment reads, 0 after")
+    ap.add_argument("--fpf", type=int, default=1, help="streaming fwd/dgrad fragment prefetch (>= 3 stages)")
     a = ap.parse_args()
     C = _native.native()
     fs, ws = (int(v) for v in a.stages.split(","))

@@ -95,6 +95,49 @@ def test_conv_fwd_and_stats(C, shape, tile, splits, region):
 
 
 @pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_fwd_prefetch_pipeline_bitwise(C, shape):
+    """The streaming kernel's fragment-prefetch main loop (set_conv_fwd_pf 1,
+    >= 3 ring stages; unconditional zero-fill DMA pipeline) computes the same
+    MFMA sequence as the plain loop: bitwise equal outputs and statistics at
+    every ring depth, tile and split, and within bf16 error of fp32."""
+    B, H, cin, cout = shape
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(7 + B * H + cin)
+    x = torch.randn(B, H, H, cin, device=dev, generator=g).to(torch.bfloat16)
+    w = (torch.randn(cout, 5, 5, cin, device=dev, generator=g) * 0.05).to(torch.bfloat16)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=2).permute(0, 2, 3, 1)
+    xp = _pad(x)
+    C.set_conv_region(0)
+    try:
+        for tile in (0, 2):
+            if cout % _TILE_BN[tile] != 0:
+                continue
+            for splits in (1, 3):
+                if splits > 1 and 256 % (cout // 8) != 0:
+                    continue
+                rows = C.conv_fwd_stat_rows(B, H, H, cin, cout, 5, tile, splits)
+                outs = {}
+                for st in (3, 4):
+                    for pf in (0, 1):
+                        C.set_conv_stages(st, 0)
+                        C.set_conv_fwd_pf(pf)
+                        y = torch.empty(B, H, H, cout, dtype=torch.bfloat16, device=dev)
+                        stats = torch.full((rows, 2, cout), float("nan"), device=dev)
+                        slab = torch.empty(splits * B * H * H * cout, device=dev)
+                        C.conv_fwd(xp.data_ptr(), w.data_ptr(), y.data_ptr(), stats.data_ptr(), slab.data_ptr(), B,
+                                   H, H, cin, cout, 5, tile, splits, _s())
+                        torch.cuda.synchronize()
+                        outs[(st, pf)] = (y, stats)
+                        assert _rel(y, ref) < 8e-3, (tile, splits, st, pf)
+                    assert torch.equal(outs[(st, 0)][0], outs[(st, 1)][0]), (tile, splits, st)
+                    assert torch.equal(outs[(st, 0)][1], outs[(st, 1)][1]), (tile, splits, st)
+    finally:
+        C.set_conv_region(1)
+        C.set_conv_stages(3, 0)
+        C.set_conv_fwd_pf(1)
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
 def test_conv_dgrad_wgrad(C, shape):
     B, H, cin, cout = shape
     dev = torch.device("cuda")
@@ -146,7 +189,7 @@ def test_conv_dgrad_wgrad(C, shape):
     for tile in (0, 2):
         if cout % 128 != 0:
             continue
-        for st, pf in ((3, 1), (3, 0), (4, 0), (4, 1)):
+        for st, pf in ((3, 1), (3, 0), (4, 0), (4, 1), (5, 1)):
             C.set_conv_stages(3, st)
             C.set_conv_wgrad_pf(pf)
             try:

@@ -169,6 +169,9 @@ class CifarHIPExecutor:
         # With a real all-reduce (world > 1) the dgrads use the 2-stage ring.
         comm = getattr(bucketer, "comm", None)
         overlapped = comm is not None and getattr(comm, "world_size", 1) > 1
+        # 4 stages switch the streaming kernel to its fragment-prefetch loop (csrc
+        # conv_fwd_kernel, g_fwd_pf; fwd via DISTLEARN_FWD_STAGES=4): measured -1.3 % on one
+        # box and +0.7 % on the next (profiles/r3_fwd_prefetch_ab.txt), so 3 stays.
         self.dgrad_stages = int(os.environ.get("DISTLEARN_DGRAD_STAGES", "2" if overlapped else "3"))
         # streaming-kernel forward configuration packed into the tile id (csrc conv_fwd
         # FwdCfg: bits 4-7 ring stages, 8-11 waves; 0 = the global default)
@@ -191,6 +194,8 @@ class CifarHIPExecutor:
             self.C.set_conv_posm(int(os.environ["DISTLEARN_POSM"]))
         if "DISTLEARN_FWD_TR" in os.environ:  # A/B: transposed-accumulator streaming kernel (1) or not (0)
             self.C.set_conv_fwd_tr(int(os.environ["DISTLEARN_FWD_TR"]))
+        if "DISTLEARN_FWD_PF" in os.environ:  # A/B: streaming fwd/dgrad fragment prefetch (1) or not (0)
+            self.C.set_conv_fwd_pf(int(os.environ["DISTLEARN_FWD_PF"]))
         if "DISTLEARN_WGRAD_ORDER" in os.environ:  # A/B: wgrad DMA before (1) or after (0) the fragment reads
             self.C.set_conv_wgrad_order(int(os.environ["DISTLEARN_WGRAD_ORDER"]))
         if "DISTLEARN_WGRAD_PF" in os.environ:  # tuning: wgrad fragment prefetch (-1 auto, 0, 1)
