@@ -359,7 +359,9 @@ def main():
             "config": {"model": MODEL_DESC[a.model],
                        "global_batch": batch * len(workers), "per_gpu_batch": batch, "seq_len": None,
                        "parallelism": f"dp{len(workers)}" + ("+ps1" if a.algo == "async" else ""), "algo": a.algo,
-                       "backend": backend, "hipgraph": bool(a.graph), "bucket_mb": a.bucket_mb, **policy,
+                       "backend": (backend if a.model == "cifar10" or cpu
+                                   else "torch autograd over the hand-written HIP conv/BN/head kernels"),
+                       "hipgraph": bool(a.graph), "bucket_mb": a.bucket_mb, **policy,
                        **({"tau": a.tau, "alpha": a.alpha} if a.algo != "sgd" else {})},
             "final_loss": round(lval, 4),
         }

@@ -91,8 +91,24 @@ def _compile(src: str, force: bool, verbose: bool, newest_header: float):
     return obj, time.time() - t0, True
 
 
+def _flags_changed() -> bool:
+    """Objects are reused by mtime only, so a change of DISTLEARN_CFLAGS (e.g. a
+    diagnostic -DDL_WGRAD_STAMPS build and back) forces a full rebuild: an object
+    compiled under other flags must never be linked silently."""
+    os.makedirs(BUILD, exist_ok=True)
+    stamp = os.path.join(BUILD, "cflags.txt")
+    cur = os.environ.get("DISTLEARN_CFLAGS", "").strip()
+    old = open(stamp).read() if os.path.exists(stamp) else None
+    if old != cur:
+        with open(stamp, "w") as f:
+            f.write(cur)
+        return old is not None or bool(cur)
+    return False
+
+
 def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> str:
     """Build the product extension ``_C`` and the test-support ``_C_testing``."""
+    force = _flags_changed() or force
     out = _build_ext("_C", _sources(False), force, jobs, verbose, ["-lrccl"])
     _build_ext("_C_testing", _sources(True), force, jobs, verbose, [])
     return out

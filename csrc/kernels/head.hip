@@ -18,6 +18,20 @@
 
 namespace dl {
 
+// DL_HEAD_STAMPS builds only (diagnostics): s_memtime of thread 0 of every
+// head_fwd_bwd block at its phase boundaries -> [block][8]
+__device__ unsigned long long* g_head_stamps = nullptr;
+#ifdef DL_HEAD_STAMPS
+__device__ __forceinline__ unsigned long long hstamp() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+#define HEAD_STAMP(k) do { if (threadIdx.x == 0 && g_head_stamps) g_head_stamps[blockIdx.x * 8 + (k)] = hstamp(); } while (0)
+#else
+#define HEAD_STAMP(k) do { } while (0)
+#endif
+
 // POOL: the head's input h is not read but computed here from the last conv
 // block's pre-BN output y [B][yH][yW][yC] (bf16) and its BN coefficients
 // (coef [4][yC]: scale at 2*yC, shift at 3*yC) -- the work of
@@ -45,9 +59,17 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
                                                            float* __restrict__ logits_out, float* __restrict__ dlogits,
                                                            float* __restrict__ loss_b, bf16_t* __restrict__ dh,
                                                            const HeadPool hp = HeadPool{}) {
+  HEAD_STAMP(0);
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  __shared__ float red[4][NC];
+  __shared__ float lgp[NC][257];  // per-thread logit partials, transposed (+1: conflict-free rows)
+  __shared__ float redc[NC];
   __shared__ float dl[NC];
+  // the label and the bias, loaded now: read by thread 0 after the logits
+  // barrier they were one more dependent memory round trip on its serial path
+  const int ylab = labels ? (int)labels[b] : -1;
+  float bv[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) bv[c] = bias[c];
   const bf16_t* hb = h + (int64_t)b * F;
   float acc[NC];
 #pragma unroll
@@ -84,6 +106,7 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
         __shared__ float ssc[kFinMaxC], ssh[kFinMaxC];
         __shared__ float smu[RED ? kFinMaxC : 1], sis[RED ? kFinMaxC : 1];
         bn_fin_block(hp.fin, hp.yC, ssc, ssh, RED ? smu : nullptr, RED ? sis : nullptr);
+        HEAD_STAMP(1);
 #pragma unroll
         for (int k = 0; k < 8; ++k) { sc[k] = ssc[c0 + k]; sh[k] = ssh[c0 + k]; }
         if constexpr (RED) {
@@ -140,17 +163,29 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
                 hf[6] * w1.z + hf[7] * w1.w;
     }
   }
+  // logits: sum of the 256 threads' partials per class through LDS (16 threads
+  // per class, 16 values each, then a 16-lane butterfly) instead of NC
+  // 64-lane shuffle reductions (6 dependent ds_bpermute rounds each)
 #pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const float v = wave_sum(acc[c]);
-    if (lane == 0) red[wid][c] = v;
+  for (int c = 0; c < NC; ++c) lgp[c][tid] = acc[c];
+  HEAD_STAMP(2);
+  __syncthreads();
+  if (tid < NC * 16) {
+    const int c = tid >> 4, j = tid & 15;
+    float sp = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) sp += lgp[c][q * 16 + j];
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) sp += __shfl_xor(sp, o, 16);
+    if (j == 0) redc[c] = sp;
   }
   __syncthreads();
+  HEAD_STAMP(3);
   if (tid == 0) {
     float lg[NC], mx = -INFINITY;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      lg[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c] + bias[c];
+      lg[c] = redc[c] + bv[c];
       mx = fmaxf(mx, lg[c]);
     }
     float se = 0.f;
@@ -162,7 +197,7 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
       for (int c = 0; c < NC; ++c) logits_out[(int64_t)b * NC + c] = lg[c] - lse;  // log-probabilities
     }
     if (labels) {
-      const int y = (int)labels[b];
+      const int y = ylab;
       float lb = 0.f;
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
@@ -177,6 +212,7 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
   }
   if (!labels) return;
   __syncthreads();
+  HEAD_STAMP(4);
   float d[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) d[c] = dl[c];
@@ -191,6 +227,7 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
     const uint4 dpk =
         make_uint4(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]), pack_bf16x2(o[6], o[7]));
     *reinterpret_cast<uint4*>(dh + (int64_t)b * F + j0) = dpk;
+    HEAD_STAMP(5);
     if constexpr (POOL && RED) {
       // the backward reduce of this sample: dz routed to the pool argmax (ReLU
       // mask), sum(dz) and sum(dz * xhat) per channel, from the bf16 dP that the
@@ -227,16 +264,17 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
 #pragma unroll
       for (int k = 0; k < 8; ++k) { rr[wid][lane][k] = s1[k]; rr[wid][lane][8 + k] = s2[k]; }
       __syncthreads();
-      // 256 threads: chunk = tid & 63, (sum, k-quad) = tid >> 6
-      const int ch = tid & 63, part = tid >> 6, which = part >> 1, k0 = (part & 1) * 4;
+      HEAD_STAMP(6);
+      // row = [dgamma (= sum dz*xhat) ; dbeta (= sum dz)]: thread t adds outputs
+      // t, t + 256, ... so a wave's 64 atomics hit 64 consecutive floats (2 cache
+      // lines; the chunk-major lane order spread them over 16)
       float* row = hp.red_rows + (int64_t)(blockIdx.x & (hp.fin.R - 1)) * 2 * hp.yC;
-#pragma unroll
-      for (int k = k0; k < k0 + 4; ++k) {
-        const float t = rr[0][ch][which * 8 + k] + rr[1][ch][which * 8 + k] + rr[2][ch][which * 8 + k] +
-                        rr[3][ch][which * 8 + k];
-        // row = [dgamma (= sum dz*xhat) ; dbeta (= sum dz)]
-        unsafeAtomicAdd(row + (which == 1 ? 0 : hp.yC) + ch * 8 + k, t);
+      for (int o = tid; o < 2 * hp.yC; o += 256) {
+        const int which = o < hp.yC ? 1 : 0;  // rr: [0..8) sum dz, [8..16) sum dz*xhat
+        const int c = o - (o < hp.yC ? 0 : hp.yC), ch = c >> 3, k = which * 8 + (c & 7);
+        unsafeAtomicAdd(row + o, rr[0][ch][k] + rr[1][ch][k] + rr[2][ch][k] + rr[3][ch][k]);
       }
+      HEAD_STAMP(7);
     }
     return;
   }
@@ -313,6 +351,11 @@ void head_wgrad(uintptr_t h, uintptr_t dlogits, uintptr_t loss_b, int F, int B, 
                                                                         (float*)db, (float*)loss, (float*)slot,
                                                                         (unsigned long long*)step_ctr);
   DL_HIP_CHECK(hipGetLastError());
+}
+
+void set_head_stamps(uintptr_t buf) {
+  unsigned long long* p = (unsigned long long*)buf;
+  DL_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_head_stamps), &p, sizeof(p)));
 }
 
 }  // namespace dl

@@ -82,9 +82,31 @@ void barrier_loop(int blocks, int threads, int n, int mode, int lds, uintptr_t s
   DL_HIP_CHECK(hipGetLastError());
 }
 
+// Fill every CU's LDS with a bit pattern (all 160 KiB of dynamic LDS, one
+// workgroup per CU x `rounds`): a kernel that reads LDS it never wrote in its
+// own launch then sees the pattern instead of whatever an earlier kernel left.
+__global__ void __launch_bounds__(256) lds_poison_kernel(unsigned pattern) {
+  extern __shared__ unsigned dynp[];
+  for (int i = threadIdx.x; i < 160 * 1024 / 4; i += 256) dynp[i] = pattern;
+  __syncthreads();
+}
+
+void lds_poison(int blocks, unsigned pattern, uintptr_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    DL_HIP_CHECK(hipFuncSetAttribute((const void*)lds_poison_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024));
+    attr = true;
+  }
+  if (blocks < 1 || blocks > 65536) throw std::runtime_error("lds_poison: bad grid");
+  lds_poison_kernel<<<blocks, 256, 160 * 1024, as_stream(stream)>>>(pattern);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace dl
 
 PYBIND11_MODULE(_C_testing, m) {
+  m.def("lds_poison", &dl::lds_poison);
   m.def("barrier_loop", &dl::barrier_loop);
   m.doc() = "distlearn test/diagnostic kernels (not part of the product library)";
   m.def("occupy_cus", &dl::occupy_cus);

@@ -145,12 +145,15 @@ def test_conv_dgrad_wgrad(C, shape):
     x = torch.randn(B, H, H, cin, device=dev, generator=g).to(torch.bfloat16)
     w = (torch.randn(cout, 5, 5, cin, device=dev, generator=g) * 0.05).to(torch.bfloat16)
     dy = torch.randn(B, H, H, cout, device=dev, generator=g).to(torch.bfloat16)
-    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
-    wr = w.float().permute(0, 3, 1, 2).requires_grad_(True)
+    # reference on the CPU in fp64: MIOpen's fp32 backward-weights solver picked
+    # in some processes was off by ~8 % relative on (3, 8, 16, 64) while our
+    # kernel's output stayed bit-identical (scripts/diag_wgrad_race.py)
+    xr = x.double().cpu().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.double().cpu().permute(0, 3, 1, 2).requires_grad_(True)
     out = F.conv2d(xr, wr, padding=2)
-    out.backward(dy.float().permute(0, 3, 1, 2))
-    dx_ref = xr.grad.permute(0, 2, 3, 1)
-    dw_ref = wr.grad.permute(0, 2, 3, 1)
+    out.backward(dy.double().cpu().permute(0, 3, 1, 2))
+    dx_ref = xr.grad.permute(0, 2, 3, 1).float().to(dev)
+    dw_ref = wr.grad.permute(0, 2, 3, 1).float().to(dev)
     # dgrad = forward conv of dy with flipped + transposed weights
     wt = torch.empty(cin, 5, 5, cout, dtype=torch.bfloat16, device=dev)
     C.weight_flip_transpose(w.data_ptr(), wt.data_ptr(), cout, cin, 5, _s())
