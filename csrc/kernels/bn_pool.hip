@@ -582,15 +582,27 @@ __device__ __forceinline__ void bwd_apply_body(const bf16_t* __restrict__ y, con
   load8(cx.sc, coef + 2 * C + c0);
   load8(cx.sh, coef + 3 * C + c0);
   if constexpr (SUMS) {
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-      const float gam = gamma[c], istd = coef[C + c];  // issued with (not after) the row loads
-      float dg, db;
-      sum_rows2(acoef + c, 2 * C, C, R, dg, db);
+    auto put = [&](int c, float gam, float istd, float dg, float db) {
       const float a = gam * istd;
       sk[0][c] = a;
       sk[1][c] = -a * dg * inv_m;
       sk[2][c] = -a * db * inv_m;
       if (bid == 0 && dgamma_out != nullptr) { dgamma_out[c] = dg; dbeta_out[c] = db; }
+    };
+    if (C == 2 * (int)blockDim.x) {  // both channels' rows in one memory round trip (the last block, C = 512)
+      const int c0 = threadIdx.x, c1 = c0 + blockDim.x;
+      const float g0 = gamma[c0], i0 = coef[C + c0], g1 = gamma[c1], i1 = coef[C + c1];
+      float t[4];
+      sum_rows2x2(acoef + c0, blockDim.x, 2 * C, C, R, t);
+      put(c0, g0, i0, t[0], t[1]);
+      put(c1, g1, i1, t[2], t[3]);
+    } else {
+      for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        const float gam = gamma[c], istd = coef[C + c];  // issued with (not after) the row loads
+        float dg, db;
+        sum_rows2(acoef + c, 2 * C, C, R, dg, db);
+        put(c, gam, istd, dg, db);
+      }
     }
     fin_block_sync();
   }

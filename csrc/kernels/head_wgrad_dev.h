@@ -28,6 +28,16 @@ __device__ __forceinline__ void head_wgrad_body(const bf16_t* __restrict__ h, co
       // rows in batches of 4 with every load issued before the FMAs (the
       // serial load->use chain was latency-bound)
       int b = grp;
+      // 16 rows per trip (B = 128: the whole column in one memory round trip)
+      for (; b + 8 * 15 < B; b += 128) {
+        float hv[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) hv[u] = bf16_to_f32(h[(int64_t)(b + 8 * u) * F + j]);
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+#pragma unroll
+          for (int c = 0; c < NC; ++c) acc[c] += dlogits[(int64_t)(b + 8 * u) * NC + c] * hv[u];
+      }
       for (; b + 24 < B; b += 32) {
         float hv[4];
 #pragma unroll
