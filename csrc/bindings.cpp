@@ -66,6 +66,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_conv_wgrad_order", &set_conv_wgrad_order);
   m.def("set_conv_fwd_pf", &set_conv_fwd_pf);
   m.def("set_head_stamps", &set_head_stamps);
+  m.def("set_bn_stamps", &set_bn_stamps);
   m.def("set_conv_wgrad_stamps", &set_conv_wgrad_stamps);
   m.def("set_conv_bn_reduce", &set_conv_bn_reduce, py::arg("x"), py::arg("save"), py::arg("w"), py::arg("b"),
         py::arg("rows"), py::arg("ym") = 0);

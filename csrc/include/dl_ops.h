@@ -62,6 +62,7 @@ void set_conv_wgrad_stage_store(int on);
 void set_conv_wgrad_order(int dma_first);
 void set_conv_fwd_pf(int on);
 void set_head_stamps(uintptr_t buf);
+void set_bn_stamps(uintptr_t buf);
 void set_conv_wgrad_stamps(uintptr_t buf);
 void set_conv_bn_reduce(uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, uintptr_t rows, uintptr_t ym = 0);
 int conv_region_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile);

@@ -28,6 +28,28 @@
 
 namespace dl {
 
+// DL_BN_STAMPS builds only (diagnostics): s_memtime of thread 0 of every block
+// of the fused fwd-fin / bwd-apply kernels -> [kernel (0 fwd, 1 bwd)][C/64 - 1][block][4]
+__device__ unsigned long long* g_bn_stamps = nullptr;
+#ifdef DL_BN_STAMPS
+__device__ __forceinline__ unsigned long long bstamp() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+#define BN_STAMP(kind, C, k)                                                                              \
+  do {                                                                                                    \
+    if (threadIdx.x == 0 && g_bn_stamps && (C) <= 256)                                                   \
+      g_bn_stamps[(((size_t)(kind) * 4 + ((C) >> 6) - 1) * 2048 + blockIdx.x) * 4 + (k)] = bstamp();     \
+  } while (0)
+#else
+#define BN_STAMP(kind, C, k) do { } while (0)
+#endif
+void set_bn_stamps(uintptr_t buf) {
+  unsigned long long* p = (unsigned long long*)buf;
+  DL_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_bn_stamps), &p, sizeof(p)));
+}
+
 // reduction mode (conv_igemm.hip g_red_atomic; set together by set_reduce_atomic):
 // R >= 1 = the backward reduce atomically adds its per-block totals into row
 // (block & (R-1)) of R zeroed [dgamma (C) ; dbeta (C)] rows (R = 1: straight
@@ -204,8 +226,10 @@ __global__ void __launch_bounds__(256) bn_relu_pool_fwd_fin_kernel(const bf16_t*
   uint4 v[4];
   int c0 = 0;
   int64_t pix = 0;
+  BN_STAMP(0, C, 0);
   if (i < total) load4(item_base(i, c0, pix), v);  // in flight across the coefficient prologue
   bn_fin_block(fin, C, ssc, ssh);
+  BN_STAMP(0, C, 1);
   for (; i < total;) {
     float sc[8], sh[8], f[8], mx[8];
 #pragma unroll
@@ -231,6 +255,7 @@ __global__ void __launch_bounds__(256) bn_relu_pool_fwd_fin_kernel(const bf16_t*
     if (i < total) load4(item_base(i, c0, pix), v);
     *reinterpret_cast<uint4*>(o) = pack8(mx);
   }
+  BN_STAMP(0, C, 2);
 }
 
 // Backward signal of one pooled pixel x 8 channels: dz[w][k] = dP[k] at the
@@ -569,6 +594,7 @@ __device__ __forceinline__ void bwd_apply_body(const bf16_t* __restrict__ y, con
     yw[3] = *reinterpret_cast<const uint4*>(base + (int64_t)W * C + C);
     gv = *reinterpret_cast<const uint4*>(dP + (((b * Ho + oh) * Wo) + ow) * (int64_t)C + c0);
   };
+  BN_STAMP(1, C, 0);
   int64_t i = (int64_t)bid * blockDim.x + threadIdx.x;
   if (i < total) item_loads(i);
   // stride % C8 == 0 (C8 | 256): a thread's channel chunk c0 is the same for
@@ -606,6 +632,7 @@ __device__ __forceinline__ void bwd_apply_body(const bf16_t* __restrict__ y, con
     }
     fin_block_sync();
   }
+  BN_STAMP(1, C, 1);
   float ka[8], kb[8], kc[8];
   if constexpr (SUMS) {
 #pragma unroll
@@ -647,6 +674,7 @@ __device__ __forceinline__ void bwd_apply_body(const bf16_t* __restrict__ y, con
 #pragma unroll
     for (int w = 0; w < 4; ++w) *reinterpret_cast<uint4*>(base + offs[w]) = o4[w];
   }
+  BN_STAMP(1, C, 2);
 }
 
 template <bool SUMS>
