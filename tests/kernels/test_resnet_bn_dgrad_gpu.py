@@ -65,7 +65,10 @@ def test_dgrad_epilogue_bn_sums_match_reduce_pass(dev, kind, N, C, H, cout):
     xa, ga, ba, _, _, link, ya = _chain(dev, kind, N, C, H, cout, linked=True)
     xb, gb, bb, _, _, none, yb = _chain(dev, kind, N, C, H, cout, linked=False)
     assert link.get("nbwd") == 1 and "sums" not in link  # produced by the conv, consumed by the BN
-    assert torch.equal(ya, yb)
+    # the forward is the same in both runs, but the BatchNorm statistics pass
+    # sums with fp32 atomics across row blocks (bn_nhwc.hip block_reduce_atomic):
+    # the add order -- and so a rare bf16 rounding of y -- varies run to run
+    assert _rel(ya, yb) < 1e-3
     assert _rel(ga.grad, gb.grad) < 1e-4
     assert _rel(ba.grad, bb.grad) < 1e-4
     assert _rel(xa.grad, xb.grad) < 2e-3
