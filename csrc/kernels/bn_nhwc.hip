@@ -72,9 +72,10 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
 
 // Sum a[8] and b[8] of every thread over the RPI row lanes of the block; add
 // the block totals of its channels to acc[c] / acc[C + c].
+template <int NT>
 __device__ __forceinline__ void block_reduce_atomic(const float* a, const float* b, const BnGeom& g, int c0,
                                                     float* __restrict__ acc) {
-  __shared__ float red[kThreads * 16];
+  __shared__ float red[NT * 16];
   const int t = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -83,7 +84,7 @@ __device__ __forceinline__ void block_reduce_atomic(const float* a, const float*
   }
   __syncthreads();
   const int nch = g.CVB * 8;
-  for (int j = t; j < 2 * nch; j += kThreads) {
+  for (int j = t; j < 2 * nch; j += NT) {
     const int which = j / nch, ch = j - which * nch;
     const int cv = ch >> 3, k = ch & 7;
     float s = 0.f;
@@ -92,8 +93,9 @@ __device__ __forceinline__ void block_reduce_atomic(const float* a, const float*
   }
 }
 
-__global__ void __launch_bounds__(kThreads) bn_nhwc_stats_kernel(const bf16_t* __restrict__ x, BnGeom g,
-                                                                   float* __restrict__ acc) {
+template <int NT>
+__global__ void __launch_bounds__(NT) bn_nhwc_stats_kernel(const bf16_t* __restrict__ x, BnGeom g,
+                                                             float* __restrict__ acc) {
   const int t = threadIdx.x, cv = t % g.CVB, r = t / g.CVB;
   const int c0 = blockIdx.y * g.CVB * 8;
   const int c = c0 + cv * 8;
@@ -126,7 +128,7 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_stats_kernel(const bf16_t* _
       q[k] = fmaf(f[k], f[k], q[k]);
     }
   }
-  block_reduce_atomic(s, q, g, c0, acc);
+  block_reduce_atomic<NT>(s, q, g, c0, acc);
 }
 
 __device__ __forceinline__ void stats8(const float* __restrict__ acc, int C, int c, float invM, float eps,
@@ -140,6 +142,7 @@ __device__ __forceinline__ void stats8(const float* __restrict__ acc, int C, int
   }
 }
 
+template <int U>
 __global__ void __launch_bounds__(kThreads) bn_nhwc_fwd_apply_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
     const float* __restrict__ acc, const float* __restrict__ w, const float* __restrict__ b, BnGeom g, float eps,
@@ -189,15 +192,18 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_fwd_apply_kernel(
     *(u32x4*)(y + off) = pack8(f);
   };
   int64_t row = row0 + r;
-  for (; row + g.RPI < row1; row += 2 * g.RPI) {  // two rows' loads in flight
-    const int64_t o0 = row * g.C + c, o1 = o0 + (int64_t)g.RPI * g.C;
-    const u32x4 x0 = *(const u32x4*)(x + o0), x1 = *(const u32x4*)(x + o1);
-    const u32x4 r0 = res != nullptr ? *(const u32x4*)(res + o0) : z;
-    const u32x4 r1 = res != nullptr ? *(const u32x4*)(res + o1) : z;
-    apply(out_row(g, row) * g.C + c, x0, r0);
-    apply(out_row(g, row + g.RPI) * g.C + c, x1, r1);
+  for (; row + (U - 1) * g.RPI < row1; row += U * g.RPI) {  // U rows' loads in flight
+    u32x4 xv[U], rv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t o = (row + u * g.RPI) * g.C + c;
+      xv[u] = *(const u32x4*)(x + o);
+      rv[u] = res != nullptr ? *(const u32x4*)(res + o) : z;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) apply(out_row(g, row + u * g.RPI) * g.C + c, xv[u], rv[u]);
   }
-  if (row < row1) {
+  for (; row < row1; row += g.RPI) {
     const int64_t o0 = row * g.C + c;
     apply(out_row(g, row) * g.C + c, *(const u32x4*)(x + o0), res != nullptr ? *(const u32x4*)(res + o0) : z);
   }
@@ -208,7 +214,8 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_fwd_apply_kernel(
 // bitwise the forward's pre-activation: same fp32 operands and fma), which
 // saves reading y in both backward passes (applied inline by the two kernels
 // below, after all of an iteration's loads are issued).
-__global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_reduce_kernel(
+template <int NT>
+__global__ void __launch_bounds__(NT) bn_nhwc_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ save, const float* __restrict__ w, const float* __restrict__ b, BnGeom g, int relu,
     float* __restrict__ acc) {
@@ -267,9 +274,10 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_reduce_kernel(
     const int64_t off = row * g.C + c;
     accum(*(const u32x4*)(x + off), *(const u32x4*)(dy + off), relu == 1 ? *(const u32x4*)(y + off) : z);
   }
-  block_reduce_atomic(sg, sgx, g, c0, acc);
+  block_reduce_atomic<NT>(sg, sgx, g, c0, acc);
 }
 
+template <int U>
 __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ save, const float* __restrict__ w, const float* __restrict__ b,
@@ -320,15 +328,20 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
     if (dres != nullptr) *(u32x4*)(dres + off) = pack8(gv);
   };
   int64_t row = row0 + r;
-  for (; row + g.RPI < row1; row += 2 * g.RPI) {  // two rows' loads in flight
-    const int64_t o0 = row * g.C + c, o1 = o0 + (int64_t)g.RPI * g.C;
-    const u32x4 x0 = *(const u32x4*)(x + o0), x1 = *(const u32x4*)(x + o1);
-    const u32x4 d0 = *(const u32x4*)(dy + o0), d1 = *(const u32x4*)(dy + o1);
-    const u32x4 y0 = relu == 1 ? *(const u32x4*)(y + o0) : z, y1 = relu == 1 ? *(const u32x4*)(y + o1) : z;
-    apply(o0, out_row(g, row) * g.C + c, x0, d0, y0);
-    apply(o1, out_row(g, row + g.RPI) * g.C + c, x1, d1, y1);
+  for (; row + (U - 1) * g.RPI < row1; row += U * g.RPI) {  // U rows' loads in flight
+    u32x4 xv[U], dv[U], yv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t o = (row + u * g.RPI) * g.C + c;
+      xv[u] = *(const u32x4*)(x + o);
+      dv[u] = *(const u32x4*)(dy + o);
+      yv[u] = relu == 1 ? *(const u32x4*)(y + o) : z;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      apply((row + u * g.RPI) * g.C + c, out_row(g, row + u * g.RPI) * g.C + c, xv[u], dv[u], yv[u]);
   }
-  if (row < row1) {
+  for (; row < row1; row += g.RPI) {
     const int64_t o0 = row * g.C + c;
     apply(o0, out_row(g, row) * g.C + c, *(const u32x4*)(x + o0), *(const u32x4*)(dy + o0),
           relu == 1 ? *(const u32x4*)(y + o0) : z);
@@ -342,9 +355,14 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
 // on the ResNet-50 shapes (scripts/bench_bn.py BN_RB=..., profiles/r2_bn_reduce_blocks.txt):
 // sum of statistics + backward times 2831 / 2450 / 2527 / 2626 us for 128 / 256 / 512 / 1024.
 static int64_t g_reduce_blocks = 256;
+// rows in flight per thread in the apply kernels (2 or 4) and the block size
+// of the statistics / backward-reduce kernels (256, 512 or 1024): with the
+// grid capped at g_reduce_blocks, the block size sets the waves per CU
+static int g_apply_rows = 4;
+static int g_reduce_threads = 256;
 
-BnGeom make_geom(int64_t M, int C, dim3* grid, int64_t max_rb = 2048) {
-  if (M <= 0 || C <= 0 || C % 8 != 0 || (kThreads % (C / 8 < 32 ? C / 8 : 32)) != 0 ||
+BnGeom make_geom(int64_t M, int C, dim3* grid, int64_t max_rb = 2048, int nt = kThreads) {
+  if (M <= 0 || C <= 0 || C % 8 != 0 || (nt % (C / 8 < 32 ? C / 8 : 32)) != 0 ||
       (C / 8 > 32 && (C / 8) % 32 != 0))
     throw std::runtime_error("bn_nhwc: C must be a multiple of 8 dividing 256*8 or a multiple of 256 (got " +
                              std::to_string(C) + ")");
@@ -352,7 +370,7 @@ BnGeom make_geom(int64_t M, int C, dim3* grid, int64_t max_rb = 2048) {
   g.M = M;
   g.C = C;
   g.CVB = C / 8 < 32 ? C / 8 : 32;
-  g.RPI = kThreads / g.CVB;
+  g.RPI = nt / g.CVB;
   const int groups = (C / 8) / g.CVB;
   int64_t cap = 262144 / C;
   if (cap < 64) cap = 64;
@@ -445,6 +463,14 @@ __global__ void __launch_bounds__(kThreads) bn_rows_reduce_kernel(const float* _
 
 void set_bn_reduce_blocks(int n) { g_reduce_blocks = n < 64 ? 64 : n; }
 
+void set_bn_tuning(int apply_rows, int reduce_threads) {
+  if ((apply_rows != 2 && apply_rows != 4) ||
+      (reduce_threads != 256 && reduce_threads != 512 && reduce_threads != 1024))
+    throw std::runtime_error("set_bn_tuning: apply_rows 2|4, reduce_threads 256|512|1024");
+  g_apply_rows = apply_rows;
+  g_reduce_threads = reduce_threads;
+}
+
 void bn_rows_reduce(uintptr_t rows, int T, int C, uintptr_t acc, uintptr_t stream) {
   if (T <= 0 || C <= 0) throw std::runtime_error("bn_rows_reduce: empty");
   const int cg = (C + 63) / 64;
@@ -474,14 +500,20 @@ void bn_nhwc_fwd_pad(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uin
   set_out_pad(g, H, W, opad);
   hipStream_t s = as_stream(stream);
   if (!have_stats) {
-    const BnGeom gr = make_geom(M, C, &grid_r, g_reduce_blocks);
-    bn_nhwc_stats_kernel<<<grid_r, kThreads, 0, s>>>((const bf16_t*)x, gr, (float*)acc);
+    const int nt = g_reduce_threads;
+    const BnGeom gr = make_geom(M, C, &grid_r, g_reduce_blocks, nt);
+    if (nt == 1024)
+      bn_nhwc_stats_kernel<1024><<<grid_r, 1024, 0, s>>>((const bf16_t*)x, gr, (float*)acc);
+    else if (nt == 512)
+      bn_nhwc_stats_kernel<512><<<grid_r, 512, 0, s>>>((const bf16_t*)x, gr, (float*)acc);
+    else
+      bn_nhwc_stats_kernel<256><<<grid_r, 256, 0, s>>>((const bf16_t*)x, gr, (float*)acc);
     DL_HIP_CHECK(hipGetLastError());
   }
-  bn_nhwc_fwd_apply_kernel<<<grid, kThreads, 0, s>>>((const bf16_t*)x, (const bf16_t*)res, (bf16_t*)y,
-                                                      (const float*)acc, (const float*)w, (const float*)b, g,
-                                                      (float)eps, relu, (float*)save, (float*)run_mean,
-                                                      (float*)run_var, (float)momentum);
+  auto fk = g_apply_rows == 4 ? bn_nhwc_fwd_apply_kernel<4> : bn_nhwc_fwd_apply_kernel<2>;
+  fk<<<grid, kThreads, 0, s>>>((const bf16_t*)x, (const bf16_t*)res, (bf16_t*)y, (const float*)acc,
+                               (const float*)w, (const float*)b, g, (float)eps, relu, (float*)save,
+                               (float*)run_mean, (float*)run_var, (float)momentum);
   DL_HIP_CHECK(hipGetLastError());
 }
 
@@ -505,16 +537,18 @@ void bn_nhwc_bwd_pad(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uin
   set_out_pad(g, H, W, opad);
   hipStream_t s = as_stream(stream);
   if (!have_sums) {
-    const BnGeom gr = make_geom(M, C, &grid_r, g_reduce_blocks);
-    bn_nhwc_bwd_reduce_kernel<<<grid_r, kThreads, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x,
-                                                           (const float*)save, (const float*)w, (const float*)b, gr,
-                                                           relu, (float*)acc);
+    const int nt = g_reduce_threads;
+    const BnGeom gr = make_geom(M, C, &grid_r, g_reduce_blocks, nt);
+    auto rk = nt == 1024 ? bn_nhwc_bwd_reduce_kernel<1024>
+              : nt == 512 ? bn_nhwc_bwd_reduce_kernel<512> : bn_nhwc_bwd_reduce_kernel<256>;
+    rk<<<grid_r, nt, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, (const float*)save,
+                             (const float*)w, (const float*)b, gr, relu, (float*)acc);
     DL_HIP_CHECK(hipGetLastError());
   }
-  bn_nhwc_bwd_apply_kernel<<<grid, kThreads, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x,
-                                                      (const float*)save, (const float*)w, (const float*)b,
-                                                      (const float*)acc, g, relu,
-                                                      (bf16_t*)dx, (bf16_t*)dres, (float*)dw, (float*)db);
+  auto ak = g_apply_rows == 4 ? bn_nhwc_bwd_apply_kernel<4> : bn_nhwc_bwd_apply_kernel<2>;
+  ak<<<grid, kThreads, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, (const float*)save,
+                               (const float*)w, (const float*)b, (const float*)acc, g, relu, (bf16_t*)dx,
+                               (bf16_t*)dres, (float*)dw, (float*)db);
   DL_HIP_CHECK(hipGetLastError());
 }
 

@@ -30,6 +30,9 @@ def main():
     C_ = _native.native()
     if "BN_RB" in os.environ:  # row-block cap of the statistics / backward-reduce kernels
         C_.set_bn_reduce_blocks(int(os.environ["BN_RB"]))
+    tune = os.environ.get("BN_TUNE", "")  # "apply_rows,reduce_threads", e.g. 2,256 (round 2) / 4,1024
+    if tune:
+        C_.set_bn_tuning(*[int(v) for v in tune.split(",")])
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream().cuda_stream
     N = int(os.environ.get("BATCH", "256"))
@@ -65,16 +68,26 @@ def main():
                            w.data_ptr(), b.data_ptr(), acc[2 * C:].data_ptr(), dx.data_ptr(),
                            dres.data_ptr() if res else 0, dw.data_ptr(), db.data_ptr(), M, C, relu, s)
 
+        def bwd_apply():
+            C_.bn_nhwc_bwd_pad(dy.data_ptr(), y.data_ptr() if relu == 1 else 0, x.data_ptr(), save.data_ptr(),
+                               w.data_ptr(), b.data_ptr(), acc[2 * C:].data_ptr(), dx.data_ptr(),
+                               dres.data_ptr() if res else 0, dw.data_ptr(), db.data_ptr(), M, C, relu, 1, 1, 0,
+                               s, 1)
+
         z = timeit(lambda: acc.zero_())
         t_full = timeit(lambda: fwd(False)) - z
         t_apply = timeit(lambda: fwd(True))
         t_bwd = timeit(bwd) - z
+        t_bapply = timeit(bwd_apply)
         E = M * C * 2  # bytes of one bf16 activation
         out = {"H": H, "C": C, "relu": relu, "res": res, "M": M,
                "stats_us": round(t_full - t_apply, 1), "stats_GBs": round(E / max(t_full - t_apply, 1e-3) / 1e3),
                "fwd_apply_us": round(t_apply, 1), "fwd_apply_GBs": round(E * (3 if res else 2) / t_apply / 1e3),
-               "bwd_us": round(t_bwd, 1),
+               "bwd_us": round(t_bwd, 1), "bwd_apply_us": round(t_bapply, 1),
+               "bwd_apply_GBs": round(E * (2 + (relu == 1) + 1 + res) / t_bapply / 1e3),
+               "bwd_reduce_GBs": round(E * (2 + (relu == 1)) / max(t_bwd - t_bapply, 1e-3) / 1e3),
                "bwd_GBs": round(E * ((2 + (relu == 1)) + (3 + (relu == 1) + res)) / t_bwd / 1e3)}
+        out["tune"] = tune or "default"
         print(json.dumps(out), flush=True)
 
 

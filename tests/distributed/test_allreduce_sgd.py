@@ -42,11 +42,14 @@ def _sgd_worker(rank, world, port, trials, mode):
             b = torch.nn.Parameter(torch.randn(5))
             flat = FlatParams([w, b])
             bucketer = GradBucketer(tree.comm, flat, bucket_bytes=64, hooks=False,
-                                    wire="bf16" if mode == "bucket16" else "fp32") \
+                                    wire="bf16" if mode.startswith("bucket16") else "fp32") \
                 if mode.startswith("bucket") else None
-            if mode == "bucket16":
+            if mode.startswith("bucket16"):
                 assert bucketer.wire16 and flat.grad16 is not None
             sgd = AllReduceSGD(tree, bucketer=bucketer)
+            if mode.endswith("_early"):  # per-bucket update right after each all-reduce
+                assert sgd.enable_bucket_updates(flat, lambda: -1.0)
+                assert bucketer.nb > 1 and bucketer.hdr_first
             sgd.synchronizeParameters(flat)
             for _epoch in range(5):
                 steps = rng.randint(4, 13)
@@ -58,6 +61,8 @@ def _sgd_worker(rank, world, port, trials, mode):
                         for k in range(bucketer.nb):
                             bucketer.mark_bucket_ready(k)
                     sgd.step(flat, lr=-1.0)  # p -= -1 * g/n  == p += g/n (reference adds grads)
+                    if mode.endswith("_early"):
+                        assert bucketer.early_applied
                 sgd.synchronizeParameters(flat)
             outs.append(torch.cat([w.detach().reshape(-1), b.detach().reshape(-1)]).clone())
     tree.comm.barrier()
@@ -68,7 +73,7 @@ TRIALS = 10
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
-@pytest.mark.parametrize("mode", ["table", "flat", "bucket", "bucket16"])
+@pytest.mark.parametrize("mode", ["table", "flat", "bucket", "bucket16", "bucket_early"])
 def test_allreduce_sgd_bitwise(world, mode):
     # 10 randomized trials like test/test_AllReduceSGD.lua:23
     res = mp.run(_sgd_worker, world, TRIALS, mode)
@@ -87,3 +92,21 @@ def test_bf16_wire_matches_fp32_wire():
     for t in range(3):
         a, b = r32[0][t], r16[0][t]
         assert abs(a - b).max() <= 2e-2 * max(1.0, abs(a).max()), (a, b)
+
+
+@pytest.mark.parametrize("wire", ["bucket", "bucket16"])
+def test_bucket_updates_match_single_update(wire):
+    """Per-bucket SGD on the comm stream right after each all-reduce
+    (participation count all-reduced with the first bucket; draining nodes
+    issue the same collectives and update nothing) ends at the single
+    full-buffer update, uneven epochs on 4 gloo ranks.  Not bitwise: the
+    header bucket's all-reduce no longer carries the header, and gloo's ring
+    sums an element in an order set by its chunk of the message (replicas
+    stay bitwise equal: test_allreduce_sgd_bitwise[bucket_early])."""
+    a = mp.run(_sgd_worker, 4, 3, wire)
+    b = mp.run(_sgd_worker, 4, 3, wire + "_early")
+    tol = 1e-6 if wire == "bucket" else 2e-2
+    for r in range(4):
+        for t in range(3):
+            x, y = a[r][t], b[r][t]
+            assert abs(x - y).max() <= tol * max(1.0, abs(x).max()), (r, t, abs(x - y).max())

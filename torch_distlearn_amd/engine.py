@@ -27,6 +27,8 @@ way to drive them:
 """
 from __future__ import annotations
 
+import os
+
 import contextlib
 from typing import Any, Callable, Optional
 
@@ -93,6 +95,18 @@ class DataParallelTrainer:
 
             self.executor = make_executor(model, self.flat, bucketer=self.bucketer if algo == "sgd" else None,
                                           max_batch=max_batch)
+        # per-bucket SGD on the comm stream right after each bucket's all-reduce
+        # (parallel/buckets.py set_early_update): only for executors whose
+        # backward never reads a parameter once its bucket is complete.  Off by
+        # default: inside the replayed hipGraph every fork/join edge between the
+        # compute and comm streams stalled the compute stream by 5-15 us, so the
+        # overlapped updates cost 0.378-0.401 vs 0.328-0.330 ms/step at N = 1
+        # (profiles/r3_bucket_update_ab.txt)
+        self.bucket_updates = False
+        if (algo == "sgd" and getattr(self.executor, "bucket_updates_safe", False)
+                and os.environ.get("DISTLEARN_BUCKET_UPDATE", "0") == "1"):
+            self.bucket_updates = self.sgd.enable_bucket_updates(
+                self.flat, lambda: self.lr, momentum=momentum, weight_decay=weight_decay, momentum_buf=self.mom)
         self.graph = graph
         self._graph = None
         self._static = None

@@ -155,6 +155,12 @@ class CifarHIPExecutor:
         # head_wgrad sets the participation slot: the engine skips the per-step
         # fill of the gradient buffer
         self.overwrites_grads = True
+        # nothing in the backward reads a parameter once its gradient bucket is
+        # complete (the dgrads read the step's flipped/transposed weight copies,
+        # the BN/head kernels read gamma / the classifier before the block's
+        # leaves are reported): the trainer may update each bucket on the comm
+        # stream right after its all-reduce (engine.py bucket_updates)
+        self.bucket_updates_safe = True
         for i in range(self.nb):
             self.g32[self._leaf(i, 1)].zero_()
         self._wgrad_stages = int(os.environ.get("DISTLEARN_WGRAD_STAGES", "0"))  # tuning (3/4, 0 = per tile)

@@ -12,11 +12,27 @@ op (tests/kernels/test_resnet_gpu.py).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
 
 from .._native import native, stream_handle
+
+# "apply_rows,reduce_threads" (csrc bn_nhwc.hip set_bn_tuning): A/B knob of the
+# kernels' rows in flight / reduce block size; empty = the compiled defaults
+_TUNE = os.environ.get("DISTLEARN_BN_TUNE", "")
+_tuned = False
+
+
+def _bn():
+    global _tuned
+    C = native()
+    if not _tuned:
+        _tuned = True
+        if _TUNE:
+            C.set_bn_tuning(*[int(v) for v in _TUNE.split(",")])
+    return C
 
 
 def _geom(x: torch.Tensor):
@@ -68,7 +84,7 @@ class _BnAct(torch.autograd.Function):
         # (with out_pad the kernel writes y's padded buffer: its origin is y.data_ptr()
         # minus the interior offset)
         ybase = y.data_ptr() - (out_pad * (W + 2 * out_pad) + out_pad) * C * 2 if out_pad else y.data_ptr()
-        native().bn_nhwc_fwd_pad(x.data_ptr(), res.data_ptr() if res is not None else 0, ybase, acc.data_ptr(),
+        _bn().bn_nhwc_fwd_pad(x.data_ptr(), res.data_ptr() if res is not None else 0, ybase, acc.data_ptr(),
                                  weight.data_ptr(), bias.data_ptr(), save.data_ptr(),
                                  running_mean.data_ptr() if running_mean is not None else 0,
                                  running_var.data_ptr() if running_var is not None else 0, M, C, float(eps),
@@ -112,7 +128,7 @@ class _BnAct(torch.autograd.Function):
         else:
             dw = torch.empty(C, device=x.device, dtype=torch.float32)
             db = torch.empty(C, device=x.device, dtype=torch.float32)
-        native().bn_nhwc_bwd_pad(dy.data_ptr(), y.data_ptr() if y is not None else 0, x.data_ptr(), save.data_ptr(),
+        _bn().bn_nhwc_bwd_pad(dy.data_ptr(), y.data_ptr() if y is not None else 0, x.data_ptr(), save.data_ptr(),
                                  weight.data_ptr(), bias.data_ptr(), acc.data_ptr(), dxbase,
                                  dres.data_ptr() if dres is not None else 0, dw.data_ptr(), db.data_ptr(), M, C,
                                  ctx.relu, H, W, int(p), stream_handle(), int(have_sums))

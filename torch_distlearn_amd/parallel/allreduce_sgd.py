@@ -38,7 +38,7 @@ from typing import Any, Optional
 
 import torch
 
-from ..ops.flat import HEADER, FlatParams, flat_sgd_, scale_by_count_
+from ..ops.flat import HEADER, FlatParams, flat_sgd_, scale_by_count_, sgd_update_
 from ..utils.walk import walk_table
 from .tree import FlatBuffer, Tree
 
@@ -67,7 +67,13 @@ class AllReduceSGD:
         self.stepsPerNode[self.tree.nodeIndex - 1] += 1
 
     # ------------------------------------------------------------------ API
+    def _no_bucket_updates(self, what: str) -> None:
+        if self.bucketer is not None and self.bucketer.early is not None:
+            raise RuntimeError(f"{what}: the bucketer updates parameters per bucket (enable_bucket_updates); "
+                               "use step()")
+
     def sumGradients(self, grads: Any) -> None:  # noqa: N802  (:10-15)
+        self._no_bucket_updates("sumGradients")
         if self.bucketer is not None and _flat_of(grads) is self.bucketer.flat:
             self.bucketer.finish()
         else:
@@ -76,6 +82,7 @@ class AllReduceSGD:
         self._count_step()
 
     def sumAndNormalizeGradients(self, grads: Any) -> None:  # noqa: N802  (:18-30)
+        self._no_bucket_updates("sumAndNormalizeGradients")
         f = _flat_of(grads)
         if self.bucketer is not None and f is self.bucketer.flat:
             self.bucketer.finish()
@@ -111,9 +118,30 @@ class AllReduceSGD:
                 self.tree.allReduce(FlatBuffer(flat.grad))
             self._count_step()
             self._remember(flat)
+        if bk is not None and not already_reduced and bk.early_applied:
+            return  # every bucket was updated on the comm stream right after its all-reduce
         if bk is not None and bk.wire16 and not already_reduced:
             g = flat.grad16
         flat_sgd_(flat, lr, slot=flat.slot, mom=momentum_buf, momentum=momentum, weight_decay=weight_decay, grad=g)
+
+    def enable_bucket_updates(self, flat: FlatParams, lr_fn, momentum: float = 0.0, weight_decay: float = 0.0,
+                              momentum_buf: Optional[torch.Tensor] = None) -> bool:
+        """Fold the fused SGD of :meth:`step` into the bucketer: each bucket's
+        parameters are updated on the comm stream right after its all-reduce
+        (buckets.py set_early_update).  ``lr_fn()`` returns the current rate.
+        Only for callers whose backward never reads a parameter after its
+        bucket is complete (the HIP executors).  Returns whether it is on."""
+        bk = self.bucketer
+        if bk is None or flat is not bk.flat:
+            return False
+
+        def update(s: int, e: int, g: torch.Tensor) -> None:
+            sgd_update_(flat.data[s:e], g[s:e], lr_fn(), slot=flat.slot,
+                        mom=None if momentum_buf is None else momentum_buf[s:e], momentum=momentum,
+                        weight_decay=weight_decay, shadow=None if flat.shadow is None else flat.shadow[s:e])
+
+        bk.set_early_update(update)
+        return True
 
     def _remember(self, grads):
         if self._drain_template is None:

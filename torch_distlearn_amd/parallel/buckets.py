@@ -27,6 +27,17 @@ count) is all-reduced in fp32 beside it in the same group.  The fused SGD
 reads the bf16 result directly (``AllReduceSGD.step``); API callers that read
 ``flat.grad`` get it widened back to fp32 by :meth:`finish`.  At world 1 the
 all-reduce is the identity and the wire stays fp32.
+
+Per-bucket update (:meth:`set_early_update`, used by the native executors):
+the fused SGD of a bucket's parameters runs on the comm stream right after
+that bucket's all-reduce, so the update of the largest (last-layer) bucket
+overlaps the earlier layers' backward instead of one full-buffer SGD kernel
+after the last bucket lands.  The participation count is then all-reduced
+with the FIRST launched bucket (in the same group, fp32), so every bucket's
+update already divides by the final ``n``; draining nodes issue the same
+collectives and apply no update.  Only valid when nothing reads a bucket's
+parameters after its gradients are final (true for the HIP executors: the
+dgrads read the step's transposed weight copies).
 """
 from __future__ import annotations
 
@@ -74,6 +85,12 @@ class GradBucketer:
         self._rec = None
         self.stream = stream if stream is not None else (
             torch.cuda.Stream(device=flat.device, priority=-1) if self.cuda else None)
+        # per-bucket update (set_early_update): fn(start, end, grad_buffer) on the comm stream
+        self.early = None
+        self.hdr_bucket = next(b for b, (s, _) in enumerate(self.ranges) if s < HEADER)
+        self.hdr_first = False  # the count rides the first launched bucket
+        self._draining = False
+        self.early_applied = False  # the last finish() ran every bucket's update
         self._reset()
         self._hooks = []
         if hooks:
@@ -100,16 +117,34 @@ class GradBucketer:
         ev.record(stream)
         return ev
 
-    def _reduce(self, s: int, e: int, stream=None):
-        """All-reduce grad[s:e] (fp32 wire) or its bf16 copy + the fp32 header."""
+    def set_early_update(self, fn) -> None:
+        """``fn(start, end, grad)`` updates parameters [start, end) from the
+        all-reduced ``grad`` buffer (fp32 grad or the bf16 wire copy) on the
+        current (comm) stream; None restores the single update after finish()."""
+        self.early = fn
+        self.hdr_first = fn is not None and self.nb > 1
+
+    def _reduce(self, s: int, e: int, stream=None, b: int = -1):
+        """All-reduce grad[s:e] (fp32 wire) or its bf16 copy, and the fp32
+        header (participation count) exactly once per step: with the bucket
+        that holds it, or -- per-bucket updates -- with the first bucket."""
         f = self.flat
+        hdr_here = (b == 0) if self.hdr_first else (s < HEADER)
+        if self.hdr_first and s < HEADER:
+            s = HEADER  # the header went with bucket 0
         if not self.wire16:
-            self.comm.all_reduce(f.grad[s:e], "sum", stream=stream)
+            if hdr_here and s >= HEADER:
+                with self.comm.group():
+                    self.comm.all_reduce(f.grad[s:e], "sum", stream=stream)
+                    self.comm.all_reduce(f.grad[0:HEADER], "sum", stream=stream)
+            else:
+                self.comm.all_reduce(f.grad[s:e], "sum", stream=stream)
             return
-        cast_(f.grad16[s:e], f.grad[s:e])
+        s16 = max(s, HEADER)  # the bf16 copy of the header is never read
+        cast_(f.grad16[s16:e], f.grad[s16:e])
         with self.comm.group():
-            self.comm.all_reduce(f.grad16[s:e], "sum", stream=stream)
-            if s < HEADER:  # the participation count stays exact in fp32
+            self.comm.all_reduce(f.grad16[s16:e], "sum", stream=stream)
+            if hdr_here:  # the participation count stays exact in fp32
                 self.comm.all_reduce(f.grad[0:HEADER], "sum", stream=stream)
 
     def _launch(self, b: int):
@@ -124,12 +159,16 @@ class GradBucketer:
                     self._rec = {"buckets": []}
                 t0 = self._event(self.stream)
             with torch.cuda.stream(self.stream):
-                self._reduce(s, e, stream=self.stream)
+                self._reduce(s, e, stream=self.stream, b=b)
+                if self.early is not None and not self._draining:
+                    self.early(max(s, HEADER), e, self.flat.grad16 if self.wire16 else self.flat.grad)
             if prof:
                 self._rec["buckets"].append((t0, self._event(self.stream), (e - s) * buf.element_size()))
             buf.record_stream(self.stream)
         else:
-            self._reduce(s, e)
+            self._reduce(s, e, b=b)
+            if self.early is not None and not self._draining:
+                self.early(max(s, HEADER), e, self.flat.grad16 if self.wire16 else self.flat.grad)
         self.launched += 1
 
     def _pump(self):
@@ -155,6 +194,7 @@ class GradBucketer:
         for b in range(self.nb):
             self.remaining[b] = 0
         self._pump()
+        self.early_applied = self.early is not None and not self._draining
         if self.wire16 and widen:
             f = self.flat
             ctx = torch.cuda.stream(self.stream) if self.cuda else _nullctx()
@@ -174,12 +214,16 @@ class GradBucketer:
 
     def drain(self):
         """Replay zero buckets (slot 0) until no node is active any more."""
-        while True:
-            fill_(self.flat.grad, 0.0, slot_value=0.0)
-            self.finish(widen=False)
-            n = int(self.flat.grad[SLOT].item())
-            if n == 0:
-                return
+        self._draining = True  # same collectives, no parameter update
+        try:
+            while True:
+                fill_(self.flat.grad, 0.0, slot_value=0.0)
+                self.finish(widen=False)
+                n = int(self.flat.grad[SLOT].item())
+                if n == 0:
+                    return
+        finally:
+            self._draining = False
 
     def remove_hooks(self):
         for h in self._hooks:
