@@ -403,16 +403,34 @@ void set_out_pad(BnGeom& g, int H, int W, int opad) {
 
 // zero the border ring of a [N][H+2p][W+2p][C] bf16 buffer (its interior is
 // written by an apply kernel with the padded output layout)
+// Items enumerate only the border pixels (top p rows, the p left + p right
+// pixels of the H interior rows, bottom p rows; 6.8 % of a 58x58 image): the
+// first version swept the whole buffer and skipped the interior (9.8 us per
+// call on the 56x56x64 ResNet-50 buffers, 32 calls per step).
 __global__ void __launch_bounds__(kThreads) zero_border_kernel(bf16_t* __restrict__ buf, int N, int H, int W, int C,
                                                                int p) {
   const int Hp = H + 2 * p, Wp = W + 2 * p, C8 = C >> 3;
-  const int64_t total = (int64_t)N * Hp * Wp * C8;
+  const int per_img = Hp * Wp - H * W;
+  const int64_t total = (int64_t)N * per_img * C8;
   const u32x4 z = {0u, 0u, 0u, 0u};
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t pix = i / C8;
-    const int w = (int)(pix % Wp), h = (int)((pix / Wp) % Hp);
-    if (h >= p && h < H + p && w >= p && w < W + p) continue;
-    *(u32x4*)(buf + pix * C + (i % C8) * 8) = z;
+    const int c8 = (int)(i % C8);
+    const int64_t t = i / C8;
+    const int64_t n = t / per_img;
+    int b = (int)(t - n * per_img), h, w;
+    if (b < p * Wp) {  // top rows
+      h = b / Wp;
+      w = b - h * Wp;
+    } else if ((b -= p * Wp) < H * 2 * p) {  // left / right columns of the interior rows
+      const int r = b / (2 * p), k = b - r * 2 * p;
+      h = p + r;
+      w = k < p ? k : W + k;
+    } else {  // bottom rows
+      b -= H * 2 * p;
+      h = p + H + b / Wp;
+      w = b % Wp;
+    }
+    *(u32x4*)(buf + ((n * Hp + h) * Wp + w) * C + c8 * 8) = z;
   }
 }
 
@@ -554,7 +572,7 @@ void bn_nhwc_bwd_pad(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uin
 
 void zero_border_nhwc(uintptr_t buf, int N, int H, int W, int C, int pad, uintptr_t stream) {
   if (C % 8 != 0 || pad <= 0) throw std::runtime_error("zero_border_nhwc: C % 8 and pad > 0 required");
-  const int64_t total = (int64_t)N * (H + 2 * pad) * (W + 2 * pad) * (C / 8);
+  const int64_t total = (int64_t)N * ((int64_t)(H + 2 * pad) * (W + 2 * pad) - (int64_t)H * W) * (C / 8);
   zero_border_kernel<<<stream_grid(total), kThreads, 0, as_stream(stream)>>>((bf16_t*)buf, N, H, W, C, pad);
   DL_HIP_CHECK(hipGetLastError());
 }

@@ -151,3 +151,21 @@ def test_resnet50_mixed_bn_train_step(monkeypatch):
 
     monkeypatch.setattr(resnet, "_BN_MODE", "mixed")
     test_resnet50_train_step()
+
+
+@pytest.mark.parametrize("N,H,W,C,p", [(3, 56, 56, 64, 1), (2, 7, 5, 512, 1), (2, 6, 9, 16, 2)])
+def test_zero_border_only_touches_the_border(N, H, W, C, p):
+    """zero_border_nhwc enumerates the border pixels directly (bn_nhwc.hip):
+    the ring is zeroed, the interior is left as it was."""
+    from torch_distlearn_amd import _native
+    from torch_distlearn_amd._native import stream_handle
+
+    buf = torch.randn(N, H + 2 * p, W + 2 * p, C, device="cuda").to(torch.bfloat16) + 5
+    before = buf.clone()
+    _native.native().zero_border_nhwc(buf.data_ptr(), N, H, W, C, p, stream_handle())
+    torch.cuda.synchronize()
+    inner = (slice(None), slice(p, p + H), slice(p, p + W))
+    assert torch.equal(buf[inner], before[inner])
+    ring = torch.ones(H + 2 * p, W + 2 * p, dtype=torch.bool, device="cuda")
+    ring[p:p + H, p:p + W] = False
+    assert (buf[:, ring] == 0).all()
