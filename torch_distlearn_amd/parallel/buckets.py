@@ -87,7 +87,6 @@ class GradBucketer:
             torch.cuda.Stream(device=flat.device, priority=-1) if self.cuda else None)
         # per-bucket update (set_early_update): fn(start, end, grad_buffer) on the comm stream
         self.early = None
-        self.hdr_bucket = next(b for b, (s, _) in enumerate(self.ranges) if s < HEADER)
         self.hdr_first = False  # the count rides the first launched bucket
         self._draining = False
         self.early_applied = False  # the last finish() ran every bucket's update
