@@ -56,7 +56,20 @@ __device__ __forceinline__ void sum_rows2(const float* __restrict__ p, int strid
     case 4: sum_rows2_t<4>(p, stride, off2, t1, t2); break;
     case 8: sum_rows2_t<8>(p, stride, off2, t1, t2); break;
     case 16: sum_rows2_t<16>(p, stride, off2, t1, t2); break;
-    default: sum_rows2_t<32>(p, stride, off2, t1, t2); break;
+    default: {
+      // R = 32 as two 16-row passes: a 32-deep instance held 64 loads in flight
+      // and set the register budget of every kernel that includes this switch
+      // (the row-summing consumers then ran at 2-3 blocks per CU)
+      t1 = t2 = 0.f;
+#pragma unroll 1
+      for (int h = 0; h < R; h += 16) {
+        float u1, u2;
+        sum_rows2_t<16>(p + (int64_t)h * stride, stride, off2, u1, u2);
+        t1 += u1;
+        t2 += u2;
+      }
+      break;
+    }
   }
 }
 
@@ -103,7 +116,16 @@ __device__ __forceinline__ void sum_rows2x2(const float* __restrict__ p, int off
     case 4: sum_rows2x2_t<4>(p, off, stride, off2, t); break;
     case 8: sum_rows2x2_t<8>(p, off, stride, off2, t); break;
     case 16: sum_rows2x2_t<16>(p, off, stride, off2, t); break;
-    default: sum_rows2x2_t<32>(p, off, stride, off2, t); break;
+    default: {  // R = 32: two 16-row passes (see sum_rows2)
+      t[0] = t[1] = t[2] = t[3] = 0.f;
+#pragma unroll 1
+      for (int h = 0; h < R; h += 16) {
+        float u[4];
+        sum_rows2x2_t<16>(p + (int64_t)h * stride, off, stride, off2, u);
+        t[0] += u[0]; t[1] += u[1]; t[2] += u[2]; t[3] += u[3];
+      }
+      break;
+    }
   }
 }
 

@@ -66,6 +66,17 @@ int reduce_rows() { return g_host_rows; }
 static int g_fin_grid = 2048;
 void set_bn_fin_grid(int cap) { g_fin_grid = cap < 1 ? 1 : cap; }
 static int fin_grid(int64_t total) { return std::min(stream_grid(total), g_fin_grid); }
+// register cap of the row-summing BN consumers (bn_relu_pool_fwd_fin /
+// bn_relu_pool_bwd_apply_sums): 1 = compiler's choice, 4 = >= 4 waves per SIMD
+// (fwd_fin, bwd_apply).  Measured: bwd_apply capped spills 76 B/lane and ran
+// 0.3336-0.3351 vs 0.3290-0.3301 ms/step uncapped (profiles/r3_bn_minw_ab.txt);
+// fwd_fin capped needs no scratch (107 VGPRs)
+static int g_bn_minw_fwd = 4, g_bn_minw_bwd = 1;
+void set_bn_minw(int fwd, int bwd) {
+  if ((fwd != 1 && fwd != 4) || (bwd != 1 && bwd != 4)) throw std::runtime_error("set_bn_minw: 1 or 4");
+  g_bn_minw_fwd = fwd;
+  g_bn_minw_bwd = bwd;
+}
 
 __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
   f[0] = lo_bf16(v.x); f[1] = hi_bf16(v.x); f[2] = lo_bf16(v.y); f[3] = hi_bf16(v.y);
@@ -198,7 +209,8 @@ __global__ void __launch_bounds__(256) bn_relu_pool_fwd_kernel(const bf16_t* __r
 
 // Same, with the BN coefficients derived from the atomically accumulated
 // statistics (bn_fin_dev.h); block 0 publishes coef + running statistics.
-__global__ void __launch_bounds__(256) bn_relu_pool_fwd_fin_kernel(const bf16_t* __restrict__ y, const BnFin fin,
+template <int MINW = 1>  // (see bn_relu_pool_bwd_apply_kernel: uncapped 160 VGPRs = 3 blocks per CU)
+__global__ void __launch_bounds__(256, MINW) bn_relu_pool_fwd_fin_kernel(const bf16_t* __restrict__ y, const BnFin fin,
                                                                    bf16_t* __restrict__ out, int B, int H, int W, int C,
                                                                    int opad) {
   __shared__ float ssc[kFinMaxC], ssh[kFinMaxC];
@@ -563,7 +575,7 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
 // (the first item's loads are already in flight); block 0 also writes the
 // totals to dgamma_out / dbeta_out (R > 1: the flat gradient; R = 1
 // accumulated there directly and passes null).
-template <bool SUMS>
+template <bool SUMS, bool TWO_CH = false>
 __device__ __forceinline__ void bwd_apply_body(const bf16_t* __restrict__ y, const bf16_t* __restrict__ dP,
                                                const float* __restrict__ coef, const float* __restrict__ acoef,
                                                bf16_t* __restrict__ dy, int B, int H, int W, int C, int opad,
@@ -615,7 +627,7 @@ __device__ __forceinline__ void bwd_apply_body(const bf16_t* __restrict__ y, con
       sk[2][c] = -a * db * inv_m;
       if (bid == 0 && dgamma_out != nullptr) { dgamma_out[c] = dg; dbeta_out[c] = db; }
     };
-    if (C == 2 * (int)blockDim.x) {  // both channels' rows in one memory round trip (the last block, C = 512)
+    if (TWO_CH && C == 2 * (int)blockDim.x) {  // both channels' rows in one memory round trip (the last block, C = 512)
       const int c0 = threadIdx.x, c1 = c0 + blockDim.x;
       const float g0 = gamma[c0], i0 = coef[C + c0], g1 = gamma[c1], i1 = coef[C + c1];
       float t[4];
@@ -623,6 +635,7 @@ __device__ __forceinline__ void bwd_apply_body(const bf16_t* __restrict__ y, con
       put(c0, g0, i0, t[0], t[1]);
       put(c1, g1, i1, t[2], t[3]);
     } else {
+#pragma unroll 1
       for (int c = threadIdx.x; c < C; c += blockDim.x) {
         const float gam = gamma[c], istd = coef[C + c];  // issued with (not after) the row loads
         float dg, db;
@@ -633,52 +646,65 @@ __device__ __forceinline__ void bwd_apply_body(const bf16_t* __restrict__ y, con
     fin_block_sync();
   }
   BN_STAMP(1, C, 1);
-  float ka[8], kb[8], kc[8];
+  // ka * dz + kb * xhat + kc with xhat = (y - mu) * is, as ka * dz + kbi * (y - mu) + kc
+  // (kbi = kb * is): the loop keeps no per-window float copies of y and no
+  // is[] -- with them the <SUMS> instance needed 206 VGPRs (2 blocks per CU:
+  // CIFAR layer 1's 1024 blocks ran in two rounds)
+  float ka[8], kbi[8], kc[8];
   if constexpr (SUMS) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { ka[k] = sk[0][c0 + k]; kb[k] = sk[1][c0 + k]; kc[k] = sk[2][c0 + k]; }
+    for (int k = 0; k < 8; ++k) { ka[k] = sk[0][c0 + k]; kbi[k] = sk[1][c0 + k] * cx.is[k]; kc[k] = sk[2][c0 + k]; }
   } else {
     load8(ka, acoef + c0);
-    load8(kb, acoef + C + c0);
+    load8(kbi, acoef + C + c0);
     load8(kc, acoef + 2 * C + c0);
-  }
-  for (; i < total;) {
-    float yv[4][8], g[8], dz[4][8];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) unpack8(yw[w], yv[w]);
+    for (int k = 0; k < 8; ++k) kbi[k] *= cx.is[k];
+  }
+  auto yk = [&](int w, int k) {  // element k of window position w
+    const uint32_t u = k < 2 ? yw[w].x : k < 4 ? yw[w].y : k < 6 ? yw[w].z : yw[w].w;
+    return (k & 1) ? hi_bf16(u) : lo_bf16(u);
+  };
+  for (; i < total;) {
+    float g[8];
     unpack8(gv, g);
+    int sel[8];  // window position of the pooled max (-1: the max is not > 0, no gradient)
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float best = -INFINITY;
       int arg = 0;
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
-        const float r = fmaxf(fmaf(cx.sc[k], yv[w][k], cx.sh[k]), 0.f);
+        const float r = fmaxf(fmaf(cx.sc[k], yk(w, k), cx.sh[k]), 0.f);
         if (r > best) { best = r; arg = w; }
       }
-#pragma unroll
-      for (int w = 0; w < 4; ++w) dz[w][k] = (w == arg && best > 0.f) ? g[k] : 0.f;
+      sel[k] = best > 0.f ? arg : -1;
     }
     uint4 o4[4];
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       float o[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = ka[k] * dz[w][k] + kb[k] * ((yv[w][k] - cx.mu[k]) * cx.is[k]) + kc[k];
+      for (int k = 0; k < 8; ++k) o[k] = ka[k] * (sel[k] == w ? g[k] : 0.f) + kbi[k] * (yk(w, k) - cx.mu[k]) + kc[k];
       o4[w] = pack8(o);
     }
     bf16_t* base = dy + (((b * Hp + 2 * oh + opad) * Wp) + 2 * ow + opad) * (int64_t)C + c0;
     const int64_t offs[4] = {0, C, (int64_t)Wp * C, (int64_t)Wp * C + C};
-    i += stride;
-    if (i < total) item_loads(i);  // next item's loads before this item's stores
 #pragma unroll
     for (int w = 0; w < 4; ++w) *reinterpret_cast<uint4*>(base + offs[w]) = o4[w];
+    // next item's loads after this item's stores (the stores' 16 registers are
+    // free again; at the CIFAR shapes every thread has one item anyway)
+    i += stride;
+    if (i < total) item_loads(i);
   }
   BN_STAMP(1, C, 2);
 }
 
-template <bool SUMS>
-__global__ void __launch_bounds__(256) bn_relu_pool_bwd_apply_kernel(const bf16_t* __restrict__ y,
+// MINW: minimum waves per SIMD the compiler must allow (register cap: 4 ->
+// <= 128 VGPRs, 4 blocks per CU, so CIFAR layer 1's 1024 blocks fit one round;
+// uncapped the <true> instance took 206 VGPRs = 2 blocks per CU, two rounds)
+template <bool SUMS, int MINW = 1>
+__global__ void __launch_bounds__(256, MINW) bn_relu_pool_bwd_apply_kernel(const bf16_t* __restrict__ y,
                                                                      const bf16_t* __restrict__ dP,
                                                                      const float* __restrict__ coef,
                                                                      const float* __restrict__ acoef,
@@ -713,7 +739,7 @@ __global__ void __launch_bounds__(256) bwd_apply_head_kernel(const bf16_t* __res
                                                              float* __restrict__ dbeta_out, int Ga,
                                                              const HeadWgradArgs2 ha) {
   if ((int)blockIdx.x < Ga)
-    bwd_apply_body<true>(y, dP, coef, acoef, dy, B, H, W, C, opad, gamma, inv_m, R, dgamma_out, dbeta_out,
+    bwd_apply_body<true, true>(y, dP, coef, acoef, dy, B, H, W, C, opad, gamma, inv_m, R, dgamma_out, dbeta_out,
                          (int)blockIdx.x, Ga);
   else
     head_wgrad_body<10>(ha.h, ha.dlogits, ha.loss_b, ha.F, ha.B, ha.dw, ha.db, ha.loss, ha.slot, ha.step_ctr,
@@ -887,7 +913,8 @@ void bn_relu_pool_bwd_apply_sums(uintptr_t y, uintptr_t dP, uintptr_t coef, uint
     throw std::runtime_error("bn_relu_pool_bwd_apply_sums: needs an atomic reduction mode with <= 32 rows");
   if ((dgamma_out == 0) != (dbeta_out == 0)) throw std::runtime_error("bn_relu_pool_bwd_apply_sums: dgamma/dbeta");
   const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
-  bn_relu_pool_bwd_apply_kernel<true><<<fin_grid(total), 256, 0, as_stream(stream)>>>(
+  auto k = g_bn_minw_bwd == 4 ? bn_relu_pool_bwd_apply_kernel<true, 4> : bn_relu_pool_bwd_apply_kernel<true, 1>;
+  k<<<fin_grid(total), 256, 0, as_stream(stream)>>>(
       (const bf16_t*)y, (const bf16_t*)dP, (const float*)coef, (const float*)dgb, (bf16_t*)dy, B, H, W, C, opad,
       (const float*)gamma, 1.0f / (float)M, g_host_rows, (float*)dgamma_out, (float*)dbeta_out);
   DL_HIP_CHECK(hipGetLastError());
@@ -924,7 +951,8 @@ void bn_relu_pool_fwd_fin(uintptr_t y, uintptr_t sums, int64_t M, uintptr_t gamm
     throw std::runtime_error("bn_relu_pool_fwd_fin: needs an atomic reduction mode with <= 32 rows");
   const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
   const BnFin fin = make_bn_fin(sums, M, gamma, beta, bias, rmean, rvar, eps, momentum, coef, g_host_rows);
-  bn_relu_pool_fwd_fin_kernel<<<fin_grid(total), 256, 0, as_stream(stream)>>>((const bf16_t*)y, fin,
+  auto k = g_bn_minw_fwd == 4 ? bn_relu_pool_fwd_fin_kernel<4> : bn_relu_pool_fwd_fin_kernel<1>;
+  k<<<fin_grid(total), 256, 0, as_stream(stream)>>>((const bf16_t*)y, fin,
                                                                                    (bf16_t*)out, B, H, W, C, opad);
   DL_HIP_CHECK(hipGetLastError());
 }
