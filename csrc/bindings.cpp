@@ -28,7 +28,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_nhwc_bwd", &bn_nhwc_bwd);
   m.def("set_bn_reduce_blocks", &set_bn_reduce_blocks);
   m.def("set_bn_tuning", &set_bn_tuning);
-  m.def("set_prep_taps", &set_prep_taps);
   m.def("set_bn_minw", &set_bn_minw);
   m.def("bn_rows_reduce", &bn_rows_reduce);
   m.def("bn_nhwc_fwd_pad", &bn_nhwc_fwd_pad);

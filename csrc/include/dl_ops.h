@@ -35,7 +35,6 @@ void bn_nhwc_fwd(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr
                  uintptr_t stream);
 void set_bn_reduce_blocks(int n);
 void set_bn_tuning(int apply_rows, int reduce_threads);
-void set_prep_taps(int t);
 void set_bn_minw(int fwd, int bwd);
 // acc[0:2C] += the column sums of T partial rows [T][2][C] (acc zeroed by the caller)
 void bn_rows_reduce(uintptr_t rows, int T, int C, uintptr_t acc, uintptr_t stream);

@@ -1947,7 +1947,6 @@ struct PrepArgs {
   int nt;                                                        // transposes
   const bf16_t* tw[4]; bf16_t* twt[4]; int tcout[4], tcin[4];
   int nb_pad, nb_pack, nb_t[4];
-  int tpb;   // taps per transpose block (64x64 tiles of tpb consecutive taps, all loads issued first)
   int quad;  // fast gather/pad path: one block per image, 4 pixels per thread
   // zero job: the step's atomic accumulators (BN statistics, BN parameter
   // gradients, split-K weight gradients) -- float4 granularity
@@ -2051,51 +2050,37 @@ __global__ void __launch_bounds__(256) prep_step_kernel(const PrepArgs a) {
     if (blk >= a.nb_t[j]) { blk -= a.nb_t[j]; continue; }
     const int Cin = a.tcin[j], Cout = a.tcout[j], taps = a.taps;
     if (Cin % 64 == 0 && Cout % 64 == 0) {
-      // 64 (co) x 64 (ci) tiles of tpb consecutive taps through LDS, 16-byte
-      // loads and stores: in, 8 lanes sweep one 128-B weight row (the tpb taps
-      // of a row are adjacent 128-B pieces; every load of the block is issued
-      // before the first LDS write); out, the 64 lanes of a wave own 64
-      // consecutive ci and each gathers 8 consecutive co (row stride 72
-      // elements: the column reads are conflict-free).
-      constexpr int kTT = 4;
-      __shared__ __attribute__((aligned(16))) bf16_t tt[kTT][64][72];
+      // 64 (co) x 64 (ci) tile of one tap through LDS, 16-byte loads and
+      // stores: in, 8 lanes sweep one 128-B weight row; out, the 64 lanes of
+      // a wave own 64 consecutive ci and each gathers 8 consecutive co
+      // (row stride 72 elements: the column reads are conflict-free).
+      // (Tiles of 4 consecutive taps per block with every load issued first
+      // measured slower: 0.3314-0.3332 vs 0.3296-0.3307 ms/step, 4x fewer
+      // blocks and 4x the static LDS of the whole prep launch,
+      // profiles/r3_prep_taps_ab.txt.)
+      __shared__ __attribute__((aligned(16))) bf16_t tt[64][72];
       const int nci = Cin / 64, nco = Cout / 64;
-      const int tg = blk / (nci * nco);
+      const int tap = blk / (nci * nco);
       const int r = blk % (nci * nco);
       const int ci0 = (r % nci) * 64, co0 = (r / nci) * 64;
-      const int t0 = tg * a.tpb, nt = min(a.tpb, taps - t0);
       const bf16_t* src = a.tw[j];
-      uint4 v[kTT][2];
 #pragma unroll
-      for (int u = 0; u < kTT; ++u)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int q = threadIdx.x + 256 * h, row = q >> 3, ch = q & 7;
-          if (u < nt)
-            v[u][h] = *reinterpret_cast<const uint4*>(src + ((int64_t)(co0 + row) * taps + t0 + u) * Cin + ci0 + ch * 8);
-        }
-#pragma unroll
-      for (int u = 0; u < kTT; ++u)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int q = threadIdx.x + 256 * h, row = q >> 3, ch = q & 7;
-          if (u < nt) *reinterpret_cast<uint4*>(&tt[u][row][ch * 8]) = v[u][h];
-        }
+      for (int q = threadIdx.x; q < 512; q += 256) {
+        const int row = q >> 3, ch = q & 7;
+        *reinterpret_cast<uint4*>(&tt[row][ch * 8]) =
+            *reinterpret_cast<const uint4*>(src + ((int64_t)(co0 + row) * taps + tap) * Cin + ci0 + ch * 8);
+      }
       __syncthreads();
+      const int ftap = taps - 1 - tap;
 #pragma unroll
-      for (int u = 0; u < kTT; ++u) {
-        if (u >= nt) break;
-        const int ftap = taps - 1 - (t0 + u);
+      for (int q = threadIdx.x; q < 512; q += 256) {
+        const int ci = q & 63, ch = q >> 6;
+        uint32_t w4[4];
 #pragma unroll
-        for (int q = threadIdx.x; q < 512; q += 256) {
-          const int ci = q & 63, ch = q >> 6;
-          uint32_t w4[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            w4[e] = (uint32_t)tt[u][ch * 8 + 2 * e][ci] | ((uint32_t)tt[u][ch * 8 + 2 * e + 1][ci] << 16);
-          *reinterpret_cast<uint4*>(a.twt[j] + ((int64_t)(ci0 + ci) * taps + ftap) * Cout + co0 + ch * 8) =
-              make_uint4(w4[0], w4[1], w4[2], w4[3]);
-        }
+        for (int e = 0; e < 4; ++e)
+          w4[e] = (uint32_t)tt[ch * 8 + 2 * e][ci] | ((uint32_t)tt[ch * 8 + 2 * e + 1][ci] << 16);
+        *reinterpret_cast<uint4*>(a.twt[j] + ((int64_t)(ci0 + ci) * taps + ftap) * Cout + co0 + ch * 8) =
+            make_uint4(w4[0], w4[1], w4[2], w4[3]);
       }
       return;
     }
@@ -2116,14 +2101,6 @@ __global__ void __launch_bounds__(256) prep_step_kernel(const PrepArgs a) {
     }
     return;
   }
-}
-
-// taps per 64x64 weight-transpose block of the prep launch (1..4; A/B knob).
-// Measured 4 vs 1: 0.3314-0.3332 vs 0.3296-0.3307 ms/step (profiles/r3_prep_taps_ab.txt): 1 stays
-static int g_prep_tpb = 1;
-void set_prep_taps(int t) {
-  if (t < 1 || t > 4) throw std::runtime_error("set_prep_taps: 1..4");
-  g_prep_tpb = t;
 }
 
 static void launch_prep(PrepArgs& a, int64_t P, uintptr_t w1, uintptr_t w1p, int w1_cout, int taps, int w1_c,
@@ -2147,7 +2124,6 @@ static void launch_prep(PrepArgs& a, int64_t P, uintptr_t w1, uintptr_t w1p, int
   a.P = (int)P;
   a.w1 = (const float*)w1; a.w1p = (bf16_t*)w1p; a.w1_cout = w1_cout; a.taps = taps; a.w1_c = w1_c; a.w1_cp = w1_cp;
   a.nt = (int)tw.size();
-  a.tpb = g_prep_tpb;
   if (a.nt > 4 || twt.size() != tw.size() || tcout.size() != tw.size() || tcin.size() != tw.size())
     throw std::runtime_error("prep_step: up to 4 consistent transposes");
   a.quad = (a.C == 3 && a.Cp == 8 && P > 0 && a.W % 4 == 0) ? 1 : 0;
@@ -2157,9 +2133,8 @@ static void launch_prep(PrepArgs& a, int64_t P, uintptr_t w1, uintptr_t w1p, int
   for (int j = 0; j < a.nt; ++j) {
     a.tw[j] = (const bf16_t*)tw[j]; a.twt[j] = (bf16_t*)twt[j];
     a.tcout[j] = tcout[j]; a.tcin[j] = tcin[j];
-    a.nb_t[j] = (tcin[j] % 64 == 0 && tcout[j] % 64 == 0)
-                    ? (tcin[j] / 64) * (tcout[j] / 64) * ((taps + g_prep_tpb - 1) / g_prep_tpb)
-                    : ((tcin[j] + 31) / 32) * ((tcout[j] + 31) / 32) * taps;
+    a.nb_t[j] = (tcin[j] % 64 == 0 && tcout[j] % 64 == 0) ? (tcin[j] / 64) * (tcout[j] / 64) * taps
+                                                          : ((tcin[j] + 31) / 32) * ((tcout[j] + 31) / 32) * taps;
     total += a.nb_t[j];
   }
   if (total == 0) return;

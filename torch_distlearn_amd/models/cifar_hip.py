@@ -188,8 +188,6 @@ class CifarHIPExecutor:
                                              getattr(comm, "cu_reserve", 0) if overlapped else 0))
         if "DISTLEARN_BN_MINW" in os.environ:  # A/B: "fwd,bwd" register caps of the BN fwd-fin / bwd-apply kernels (1|4)
             self.C.set_bn_minw(*[int(v) for v in os.environ["DISTLEARN_BN_MINW"].split(",")])
-        if "DISTLEARN_PREP_TAPS" in os.environ:  # A/B: taps per weight-transpose block of the prep launch (1-4)
-            self.C.set_prep_taps(int(os.environ["DISTLEARN_PREP_TAPS"]))
         if "DISTLEARN_C8_MT" in os.environ:  # tuning: layer-1 M tiles per workgroup (1, 2, 4, 8)
             self.C.set_conv_c8_mt(int(os.environ["DISTLEARN_C8_MT"]))
         if "DISTLEARN_FIN_GRID" in os.environ:  # tuning: grid cap of the row-summing BN consumers
