@@ -68,10 +68,12 @@ void set_bn_fin_grid(int cap) { g_fin_grid = cap < 1 ? 1 : cap; }
 static int fin_grid(int64_t total) { return std::min(stream_grid(total), g_fin_grid); }
 // register cap of the row-summing BN consumers (bn_relu_pool_fwd_fin /
 // bn_relu_pool_bwd_apply_sums): 1 = compiler's choice, 4 = >= 4 waves per SIMD
-// (fwd_fin, bwd_apply).  Measured: bwd_apply capped spills 76 B/lane and ran
-// 0.3336-0.3351 vs 0.3290-0.3301 ms/step uncapped (profiles/r3_bn_minw_ab.txt);
-// fwd_fin capped needs no scratch (107 VGPRs)
-static int g_bn_minw_fwd = 4, g_bn_minw_bwd = 1;
+// (fwd_fin, bwd_apply).  fwd_fin capped: 107 VGPRs, no scratch, 0.3273-0.3285
+// vs 0.3293-0.3328 ms/step uncapped.  bwd_apply: with the forward coefficients
+// held in registers across the row sums the capped instance spilled 76 B/lane
+// (0.3336-0.3351 vs 0.3290-0.3301 ms/step, profiles/r3_bn_minw_ab.txt); with
+// them derived into LDS it needs 110-117 VGPRs either way
+static int g_bn_minw_fwd = 4, g_bn_minw_bwd = 4;
 void set_bn_minw(int fwd, int bwd) {
   if ((fwd != 1 && fwd != 4) || (bwd != 1 && bwd != 4)) throw std::runtime_error("set_bn_minw: 1 or 4");
   g_bn_minw_fwd = fwd;
@@ -584,7 +586,12 @@ __device__ __forceinline__ void bwd_apply_body(const bf16_t* __restrict__ y, con
                                                int nblk) {
   // dy: [B][H+2 opad][W+2 opad][C], written in the interior (zero border =
   // the dgrad convolution's spatial padding)
-  __shared__ float sk[SUMS ? 3 : 1][SUMS ? kFinMaxC : 1];
+  // SUMS: per-channel loop coefficients derived in the prologue into LDS:
+  // ka, kbi, kc (below) and the forward mu, sc, sh -- nothing but the item's
+  // loads is live in registers across the row sums (with the forward
+  // coefficients held in 32 registers there the kernel needed 146 VGPRs, 3
+  // blocks per CU)
+  __shared__ float sk[SUMS ? 6 : 1][SUMS ? kFinMaxC : 1];
   const int C8 = C >> 3, Ho = H >> 1, Wo = W >> 1;
   const int Hp = H + 2 * opad, Wp = W + 2 * opad;
   const int64_t total = (int64_t)B * Ho * Wo * C8;
@@ -610,57 +617,60 @@ __device__ __forceinline__ void bwd_apply_body(const bf16_t* __restrict__ y, con
   int64_t i = (int64_t)bid * blockDim.x + threadIdx.x;
   if (i < total) item_loads(i);
   // stride % C8 == 0 (C8 | 256): a thread's channel chunk c0 is the same for
-  // every item, so its forward coefficients are loaded once, here -- with the
-  // item's loads, before the coefficient-row prologue (after its barrier they
-  // were one more dependent L2 round trip per item)
+  // every item
   c0 = (int)(i % C8) * 8;
-  BwdCtx cx;
-  load8(cx.mu, coef + c0);
-  load8(cx.is, coef + C + c0);
-  load8(cx.sc, coef + 2 * C + c0);
-  load8(cx.sh, coef + 3 * C + c0);
+  // ka * dz + kb * xhat + kc with xhat = (y - mu) * is, as ka * dz + kbi * (y - mu) + kc
+  // (kbi = kb * is): the loop keeps no per-window float copies of y and no is[]
+  float ka[8], kbi[8], kc[8], mu[8], sc[8], sh[8];
   if constexpr (SUMS) {
-    auto put = [&](int c, float gam, float istd, float dg, float db) {
+    auto put = [&](int c, float gam, float istd, float m, float s, float h, float dg, float db) {
       const float a = gam * istd;
       sk[0][c] = a;
-      sk[1][c] = -a * dg * inv_m;
+      sk[1][c] = -a * dg * inv_m * istd;
       sk[2][c] = -a * db * inv_m;
+      sk[3][c] = m;
+      sk[4][c] = s;
+      sk[5][c] = h;
       if (bid == 0 && dgamma_out != nullptr) { dgamma_out[c] = dg; dbeta_out[c] = db; }
     };
     if (TWO_CH && C == 2 * (int)blockDim.x) {  // both channels' rows in one memory round trip (the last block, C = 512)
       const int c0 = threadIdx.x, c1 = c0 + blockDim.x;
       const float g0 = gamma[c0], i0 = coef[C + c0], g1 = gamma[c1], i1 = coef[C + c1];
+      const float m0 = coef[c0], s0 = coef[2 * C + c0], h0 = coef[3 * C + c0];
+      const float m1 = coef[c1], s1 = coef[2 * C + c1], h1 = coef[3 * C + c1];
       float t[4];
       sum_rows2x2(acoef + c0, blockDim.x, 2 * C, C, R, t);
-      put(c0, g0, i0, t[0], t[1]);
-      put(c1, g1, i1, t[2], t[3]);
+      put(c0, g0, i0, m0, s0, h0, t[0], t[1]);
+      put(c1, g1, i1, m1, s1, h1, t[2], t[3]);
     } else {
 #pragma unroll 1
       for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        const float gam = gamma[c], istd = coef[C + c];  // issued with (not after) the row loads
+        // issued with (not after) the row loads
+        const float gam = gamma[c], istd = coef[C + c], m = coef[c], sv = coef[2 * C + c], hv = coef[3 * C + c];
         float dg, db;
         sum_rows2(acoef + c, 2 * C, C, R, dg, db);
-        put(c, gam, istd, dg, db);
+        put(c, gam, istd, m, sv, hv, dg, db);
       }
     }
     fin_block_sync();
-  }
-  BN_STAMP(1, C, 1);
-  // ka * dz + kb * xhat + kc with xhat = (y - mu) * is, as ka * dz + kbi * (y - mu) + kc
-  // (kbi = kb * is): the loop keeps no per-window float copies of y and no
-  // is[] -- with them the <SUMS> instance needed 206 VGPRs (2 blocks per CU:
-  // CIFAR layer 1's 1024 blocks ran in two rounds)
-  float ka[8], kbi[8], kc[8];
-  if constexpr (SUMS) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { ka[k] = sk[0][c0 + k]; kbi[k] = sk[1][c0 + k] * cx.is[k]; kc[k] = sk[2][c0 + k]; }
+    for (int k = 0; k < 8; ++k) {
+      ka[k] = sk[0][c0 + k]; kbi[k] = sk[1][c0 + k]; kc[k] = sk[2][c0 + k];
+      mu[k] = sk[3][c0 + k]; sc[k] = sk[4][c0 + k]; sh[k] = sk[5][c0 + k];
+    }
   } else {
+    float is[8];
+    load8(mu, coef + c0);
+    load8(is, coef + C + c0);
+    load8(sc, coef + 2 * C + c0);
+    load8(sh, coef + 3 * C + c0);
     load8(ka, acoef + c0);
     load8(kbi, acoef + C + c0);
     load8(kc, acoef + 2 * C + c0);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) kbi[k] *= cx.is[k];
+    for (int k = 0; k < 8; ++k) kbi[k] *= is[k];
   }
+  BN_STAMP(1, C, 1);
   auto yk = [&](int w, int k) {  // element k of window position w
     const uint32_t u = k < 2 ? yw[w].x : k < 4 ? yw[w].y : k < 6 ? yw[w].z : yw[w].w;
     return (k & 1) ? hi_bf16(u) : lo_bf16(u);
@@ -675,7 +685,7 @@ __device__ __forceinline__ void bwd_apply_body(const bf16_t* __restrict__ y, con
       int arg = 0;
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
-        const float r = fmaxf(fmaf(cx.sc[k], yk(w, k), cx.sh[k]), 0.f);
+        const float r = fmaxf(fmaf(sc[k], yk(w, k), sh[k]), 0.f);
         if (r > best) { best = r; arg = w; }
       }
       sel[k] = best > 0.f ? arg : -1;
@@ -685,7 +695,7 @@ __device__ __forceinline__ void bwd_apply_body(const bf16_t* __restrict__ y, con
     for (int w = 0; w < 4; ++w) {
       float o[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = ka[k] * (sel[k] == w ? g[k] : 0.f) + kbi[k] * (yk(w, k) - cx.mu[k]) + kc[k];
+      for (int k = 0; k < 8; ++k) o[k] = ka[k] * (sel[k] == w ? g[k] : 0.f) + kbi[k] * (yk(w, k) - mu[k]) + kc[k];
       o4[w] = pack8(o);
     }
     bf16_t* base = dy + (((b * Hp + 2 * oh + opad) * Wp) + 2 * ow + opad) * (int64_t)C + c0;

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 S=scripts/gpu_step.sh
 $S 400 gpurun_out/pytest_cifar.log python -u -m pytest tests/kernels/test_convnet_gpu.py tests/kernels/test_engine_gpu.py -x -q --timeout 200 --timeout-method thread || exit 1
 for rep in 1 2 3 4; do
-  for w in 1,1 4,1; do
+  for w in 4,1 4,4; do
     DISTLEARN_BN_MINW=$w $S 120 gpurun_out/minw${w}_$rep.log python bench.py --steps 400 --warmup 24 || exit 1
   done
 done
