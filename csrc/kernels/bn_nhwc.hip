@@ -286,19 +286,15 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
   const int c0 = blockIdx.y * g.CVB * 8;
   const int c = c0 + cv * 8;
   const float invM = 1.f / (float)g.M;
-  // dx = a (g - mg - xhat mgx), xhat = (x - mean) invstd, folded to
-  // dx = a g - k1 x + k0 (k1 = a invstd mgx, k0 = k1 mean - a mg): 32 live
-  // coefficients instead of 48 (178 -> fewer VGPRs, more waves per SIMD).
-  // The k1 x / k0 cancellation costs ~2^-24 |mean| / std relative, far
-  // below the bf16 output's 2^-8.
-  float a[8], sh[8], k1[8], k0[8];
+  float mean[8], invstd[8], a[8], sh[8], mg[8], mgx[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const float mean = save[c + k], invstd = save[g.C + c + k];
-    a[k] = w[c + k] * invstd;
-    sh[k] = fmaf(-mean, a[k], b[c + k]);
-    k1[k] = a[k] * invstd * (acc[g.C + c + k] * invM);
-    k0[k] = fmaf(k1[k], mean, -a[k] * (acc[c + k] * invM));
+    mean[k] = save[c + k];
+    invstd[k] = save[g.C + c + k];
+    a[k] = w[c + k] * invstd[k];
+    sh[k] = fmaf(-mean[k], a[k], b[c + k]);
+    mg[k] = acc[c + k] * invM;
+    mgx[k] = acc[g.C + c + k] * invM;
   }
   if (blockIdx.x == 0 && r == 0) {
 #pragma unroll
@@ -324,7 +320,10 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
       for (int k = 0; k < 8; ++k) gv[k] = yy[k] > 0.f ? gv[k] : 0.f;
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = fmaf(a[k], gv[k], fmaf(-k1[k], xv[k], k0[k]));
+    for (int k = 0; k < 8; ++k) {
+      const float xh = (xv[k] - mean[k]) * invstd[k];
+      o[k] = a[k] * (gv[k] - mg[k] - xh * mgx[k]);
+    }
     *(u32x4*)(dx + doff) = pack8(o);
     if (dres != nullptr) *(u32x4*)(dres + off) = pack8(gv);
   };
