@@ -9,6 +9,7 @@ export TMPDIR=/tmp
 S=scripts/gpu_step.sh
 $S 600 gpurun_out/pytest_gpu.log python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread || exit 1
 $S 180 gpurun_out/smoke.log python -c "import __graft_entry__ as g; g.smoke()" || exit 1
+$S 180 gpurun_out/bench_driver.log python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1
 $S 180 gpurun_out/bench_sgd.log python bench.py --steps 400 --warmup 24 || exit 1
 $S 180 gpurun_out/bench_ea.log python bench.py --algo ea --steps 400 --warmup 24 || exit 1
 $S 240 gpurun_out/rocprof.log rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --steps 60 --warmup 4 || exit 1
