@@ -114,6 +114,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_bn_fin_grid", &set_bn_fin_grid);
   m.def("head_fwd_bwd", &head_fwd_bwd);
   m.def("head_fwd_bwd_pool", &head_fwd_bwd_pool);
+  m.def("head_fwd_bwd_pool_wt", &head_fwd_bwd_pool_wt);
   m.def("bn_bwd_reduce_head", &bn_bwd_reduce_head);
   m.def("bn_bwd_reduce_slab", &bn_bwd_reduce_slab);
   m.def("head_wgrad", &head_wgrad);

@@ -148,6 +148,12 @@ void head_fwd_bwd_pool(uintptr_t y, uintptr_t coef, int yH, int yW, int yC, uint
                        uintptr_t loss_b, uintptr_t dh, uintptr_t fin_sums, int64_t fin_m, uintptr_t gamma,
                        uintptr_t beta, uintptr_t conv_bias, uintptr_t rmean, uintptr_t rvar, float eps, float momentum,
                        uintptr_t red_rows, uintptr_t stream);
+void head_fwd_bwd_pool_wt(uintptr_t y, uintptr_t coef, int yH, int yW, int yC, uintptr_t h_out, uintptr_t w,
+                          uintptr_t bias, uintptr_t labels, int B, int NC, uintptr_t logits_out, uintptr_t dlogits,
+                          uintptr_t loss_b, uintptr_t dh, uintptr_t fin_sums, int64_t fin_m, uintptr_t gamma,
+                          uintptr_t beta, uintptr_t conv_bias, uintptr_t rmean, uintptr_t rvar, float eps,
+                          float momentum, uintptr_t red_rows, uintptr_t stream, std::vector<uintptr_t> tw,
+                          std::vector<uintptr_t> twt, std::vector<int> tcout, std::vector<int> tcin, int taps);
 void bn_bwd_apply_head(uintptr_t y, uintptr_t dP, uintptr_t coef, uintptr_t dgb, uintptr_t gamma, int64_t M,
                        uintptr_t dy, int B, int H, int W, int C, int opad, uintptr_t dgamma_out, uintptr_t dbeta_out,
                        uintptr_t h, uintptr_t dlogits, uintptr_t loss_b, int F, int NC, uintptr_t dw, uintptr_t db,

@@ -27,6 +27,7 @@
 #include "dl_common.h"
 #include "dl_ops.h"
 #include "slab_reduce_dev.h"
+#include "wtrans_dev.h"
 
 #include <algorithm>
 #include <type_traits>
@@ -2050,38 +2051,12 @@ __global__ void __launch_bounds__(256) prep_step_kernel(const PrepArgs a) {
     if (blk >= a.nb_t[j]) { blk -= a.nb_t[j]; continue; }
     const int Cin = a.tcin[j], Cout = a.tcout[j], taps = a.taps;
     if (Cin % 64 == 0 && Cout % 64 == 0) {
-      // 64 (co) x 64 (ci) tile of one tap through LDS, 16-byte loads and
-      // stores: in, 8 lanes sweep one 128-B weight row; out, the 64 lanes of
-      // a wave own 64 consecutive ci and each gathers 8 consecutive co
-      // (row stride 72 elements: the column reads are conflict-free).
-      // (Tiles of 4 consecutive taps per block with every load issued first
-      // measured slower: 0.3314-0.3332 vs 0.3296-0.3307 ms/step, 4x fewer
-      // blocks and 4x the static LDS of the whole prep launch,
+      // (wtrans_dev.h.  Tiles of 4 consecutive taps per block with every load
+      // issued first measured slower: 0.3314-0.3332 vs 0.3296-0.3307 ms/step,
+      // 4x fewer blocks and 4x the static LDS of the whole prep launch,
       // profiles/r3_prep_taps_ab.txt.)
       __shared__ __attribute__((aligned(16))) bf16_t tt[64][72];
-      const int nci = Cin / 64, nco = Cout / 64;
-      const int tap = blk / (nci * nco);
-      const int r = blk % (nci * nco);
-      const int ci0 = (r % nci) * 64, co0 = (r / nci) * 64;
-      const bf16_t* src = a.tw[j];
-#pragma unroll
-      for (int q = threadIdx.x; q < 512; q += 256) {
-        const int row = q >> 3, ch = q & 7;
-        *reinterpret_cast<uint4*>(&tt[row][ch * 8]) =
-            *reinterpret_cast<const uint4*>(src + ((int64_t)(co0 + row) * taps + tap) * Cin + ci0 + ch * 8);
-      }
-      __syncthreads();
-      const int ftap = taps - 1 - tap;
-#pragma unroll
-      for (int q = threadIdx.x; q < 512; q += 256) {
-        const int ci = q & 63, ch = q >> 6;
-        uint32_t w4[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          w4[e] = (uint32_t)tt[ch * 8 + 2 * e][ci] | ((uint32_t)tt[ch * 8 + 2 * e + 1][ci] << 16);
-        *reinterpret_cast<uint4*>(a.twt[j] + ((int64_t)(ci0 + ci) * taps + ftap) * Cout + co0 + ch * 8) =
-            make_uint4(w4[0], w4[1], w4[2], w4[3]);
-      }
+      wtrans_tile(a.tw[j], a.twt[j], Cin, Cout, taps, blk, tt);
       return;
     }
     const int nci = (Cin + 31) / 32, nco = (Cout + 31) / 32;

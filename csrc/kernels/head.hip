@@ -12,9 +12,11 @@
 //   head_wgrad   : dW[c][j] = sum_b dlogits[b][c] h[b][j], db, mean loss
 //                  (fixed summation order: deterministic)
 #include "dl_common.h"
+#include <vector>
 #include "dl_ops.h"
 #include "head_wgrad_dev.h"
 #include "bn_fin_dev.h"
+#include "wtrans_dev.h"
 
 namespace dl {
 
@@ -58,7 +60,12 @@ __global__ void __launch_bounds__(256) head_fwd_bwd_kernel(const bf16_t* __restr
                                                            const int64_t* __restrict__ labels, int F, int B,
                                                            float* __restrict__ logits_out, float* __restrict__ dlogits,
                                                            float* __restrict__ loss_b, bf16_t* __restrict__ dh,
-                                                           const HeadPool hp = HeadPool{}) {
+                                                           const HeadPool hp = HeadPool{},
+                                                           const WTransArgs wt = WTransArgs{}) {
+  if ((int)blockIdx.x >= B) {  // blocks past the batch: the step's dgrad weight transposes (wtrans_dev.h)
+    wtrans_block(wt, (int)blockIdx.x - B);
+    return;
+  }
   HEAD_STAMP(0);
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   __shared__ float lgp[NC][257];  // per-thread logit partials, transposed (+1: conflict-free rows)
@@ -316,12 +323,29 @@ void head_fwd_bwd(uintptr_t h, uintptr_t w, uintptr_t bias, uintptr_t labels, in
 
 // fin_sums != 0 (atomic modes, reduce_rows() rows): the last block's BN coefficients are derived from
 // the accumulated statistics (block 0 also publishes coef + running stats)
-void head_fwd_bwd_pool(uintptr_t y, uintptr_t coef, int yH, int yW, int yC, uintptr_t h_out, uintptr_t w,
-                       uintptr_t bias, uintptr_t labels, int B, int NC, uintptr_t logits_out, uintptr_t dlogits,
-                       uintptr_t loss_b, uintptr_t dh, uintptr_t fin_sums, int64_t fin_m, uintptr_t gamma,
-                       uintptr_t beta, uintptr_t conv_bias, uintptr_t rmean, uintptr_t rvar, float eps, float momentum,
-                       uintptr_t red_rows, uintptr_t stream) {
+void head_fwd_bwd_pool_wt(uintptr_t y, uintptr_t coef, int yH, int yW, int yC, uintptr_t h_out, uintptr_t w,
+                          uintptr_t bias, uintptr_t labels, int B, int NC, uintptr_t logits_out, uintptr_t dlogits,
+                          uintptr_t loss_b, uintptr_t dh, uintptr_t fin_sums, int64_t fin_m, uintptr_t gamma,
+                          uintptr_t beta, uintptr_t conv_bias, uintptr_t rmean, uintptr_t rvar, float eps,
+                          float momentum, uintptr_t red_rows, uintptr_t stream, std::vector<uintptr_t> tw,
+                          std::vector<uintptr_t> twt, std::vector<int> tcout, std::vector<int> tcin, int taps) {
   if (NC != 10) throw std::runtime_error("head_fwd_bwd_pool: built for 10 classes");
+  // optional: the dgrad weight flip-transposes ride this launch (blocks B..)
+  WTransArgs wt{};
+  if (tw.size() > 4 || twt.size() != tw.size() || tcout.size() != tw.size() || tcin.size() != tw.size())
+    throw std::runtime_error("head_fwd_bwd_pool: up to 4 consistent transposes");
+  wt.nt = (int)tw.size();
+  wt.taps = taps;
+  for (int j = 0; j < wt.nt; ++j) {
+    if (tcin[j] % 64 != 0 || tcout[j] % 64 != 0 || taps <= 0)
+      throw std::runtime_error("head_fwd_bwd_pool: transposes need channel counts that are multiples of 64");
+    wt.tw[j] = (const bf16_t*)tw[j];
+    wt.twt[j] = (bf16_t*)twt[j];
+    wt.tcout[j] = tcout[j];
+    wt.tcin[j] = tcin[j];
+    wt.nb[j] = (tcin[j] / 64) * (tcout[j] / 64) * taps;
+  }
+  const int grid = B + wtrans_blocks(wt);
   const int F = (yH / 2) * (yW / 2) * yC;
   if (F != 2048 || yC % 8 != 0 || yH % 2 != 0 || yW % 2 != 0)
     throw std::runtime_error("head_fwd_bwd_pool: needs a 2048-feature pooled map, C % 8 == 0");
@@ -333,14 +357,23 @@ void head_fwd_bwd_pool(uintptr_t y, uintptr_t coef, int yH, int yW, int yC, uint
                     make_bn_fin(fin_sums, fin_m, gamma, beta, conv_bias, rmean, rvar, eps, momentum, coef, reduce_rows()),
                     (float*)red_rows};
   if (red_rows)
-    head_fwd_bwd_kernel<10, true, true><<<B, 256, 0, as_stream(stream)>>>(
+    head_fwd_bwd_kernel<10, true, true><<<grid, 256, 0, as_stream(stream)>>>(
         nullptr, (const float*)w, (const float*)bias, (const int64_t*)labels, F, B, (float*)logits_out,
-        (float*)dlogits, (float*)loss_b, (bf16_t*)dh, hp);
+        (float*)dlogits, (float*)loss_b, (bf16_t*)dh, hp, wt);
   else
-    head_fwd_bwd_kernel<10, true><<<B, 256, 0, as_stream(stream)>>>(
+    head_fwd_bwd_kernel<10, true><<<grid, 256, 0, as_stream(stream)>>>(
         nullptr, (const float*)w, (const float*)bias, (const int64_t*)labels, F, B, (float*)logits_out,
-        (float*)dlogits, (float*)loss_b, (bf16_t*)dh, hp);
+        (float*)dlogits, (float*)loss_b, (bf16_t*)dh, hp, wt);
   DL_HIP_CHECK(hipGetLastError());
+}
+
+void head_fwd_bwd_pool(uintptr_t y, uintptr_t coef, int yH, int yW, int yC, uintptr_t h_out, uintptr_t w,
+                       uintptr_t bias, uintptr_t labels, int B, int NC, uintptr_t logits_out, uintptr_t dlogits,
+                       uintptr_t loss_b, uintptr_t dh, uintptr_t fin_sums, int64_t fin_m, uintptr_t gamma,
+                       uintptr_t beta, uintptr_t conv_bias, uintptr_t rmean, uintptr_t rvar, float eps, float momentum,
+                       uintptr_t red_rows, uintptr_t stream) {
+  head_fwd_bwd_pool_wt(y, coef, yH, yW, yC, h_out, w, bias, labels, B, NC, logits_out, dlogits, loss_b, dh, fin_sums,
+                       fin_m, gamma, beta, conv_bias, rmean, rvar, eps, momentum, red_rows, stream, {}, {}, {}, {}, 0);
 }
 
 void head_wgrad(uintptr_t h, uintptr_t dlogits, uintptr_t loss_b, int F, int B, int NC, uintptr_t dw, uintptr_t db,

@@ -222,6 +222,12 @@ class CifarHIPExecutor:
         self.side = torch.cuda.Stream(device=self.dev, priority=int(os.environ.get("DISTLEARN_SIDE_PRIORITY", "0"))) \
             if self.dev.type == "cuda" else None
         self.fork_transposes = os.environ.get("DISTLEARN_PREP_FORK", "0") == "1"
+        # the dgrad weight flip-transposes ride the head launch (blocks past the batch,
+        # on the CUs its 128 blocks leave idle) instead of the step's prep launch:
+        # prep 9.0 -> 4.8 us (profiles/r3_head_transposes_ab.txt)
+        self.head_transposes = (os.environ.get("DISTLEARN_HEAD_TRANSPOSES", "1") == "1" and self.head_pool
+                                and not self.fork_transposes
+                                and all(self.cins[i] % 64 == 0 and self.couts[i] % 64 == 0 for i in range(1, self.nb)))
         self.side_wgrad = os.environ.get("DISTLEARN_WGRAD_STREAM", "0") == "1"
         # (optional) split-K slab reduce of a layer's weight gradient on the side
         # stream, concurrent with that layer's dgrad; every layer has its own
@@ -463,7 +469,7 @@ class CifarHIPExecutor:
             ctr = x.ctr.data_ptr()  # advanced by head_wgrad after the gather read it
         if labels.dtype != torch.int64:
             raise ValueError("labels must be int64")
-        B = self._prep(x, s, with_transposes=not self.fork_transposes)
+        B = self._prep(x, s, with_transposes=not (self.fork_transposes or self.head_transposes))
         self._last_b = B
         if self.fork_transposes:  # dgrad weight transposes overlap the forward
             side.wait_stream(main)
@@ -480,11 +486,12 @@ class CifarHIPExecutor:
                 fin = (sums, Ml, gam, bet, cb, rm, rv, eps, mom)
             else:
                 fin = (0, 0, 0, 0, 0, 0, 0, 0.0, 0.0)
-            C.head_fwd_bwd_pool(self.y[-1].data_ptr(), self.coef[-1].data_ptr(), hl, hl, self.couts[-1],
-                                self.p[-1].data_ptr(), self.p32[nfc].data_ptr(), self.p32[nfc + 1].data_ptr(),
-                                labels.data_ptr(), B, self.nclass, self.logits.data_ptr(), self.dlogits.data_ptr(),
-                                self.loss_b.data_ptr(), self.dP[-1].data_ptr(), *fin,
-                                self.bwd_rows[last].data_ptr() if self.head_reduce else 0, s)
+            C.head_fwd_bwd_pool_wt(self.y[-1].data_ptr(), self.coef[-1].data_ptr(), hl, hl, self.couts[-1],
+                                   self.p[-1].data_ptr(), self.p32[nfc].data_ptr(), self.p32[nfc + 1].data_ptr(),
+                                   labels.data_ptr(), B, self.nclass, self.logits.data_ptr(), self.dlogits.data_ptr(),
+                                   self.loss_b.data_ptr(), self.dP[-1].data_ptr(), *fin,
+                                   self.bwd_rows[last].data_ptr() if self.head_reduce else 0, s,
+                                   *self._transpose_args(self.head_transposes), KSIZE * KSIZE)
         else:
             C.head_fwd_bwd(self.p[-1].data_ptr(), self.p32[nfc].data_ptr(), self.p32[nfc + 1].data_ptr(),
                            labels.data_ptr(), self.feat, B, self.nclass, self.logits.data_ptr(),
