@@ -149,6 +149,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_timeout", &RcclCommunicator::set_timeout)
       .def("timeout", &RcclCommunicator::timeout)
       .def("pending", &RcclCommunicator::pending)
+      .def("inflight", &RcclCommunicator::inflight)
       .def("error", &RcclCommunicator::error)
       .def("async_error", &RcclCommunicator::async_error)
       .def("destroy", &RcclCommunicator::destroy, py::call_guard<py::gil_scoped_release>())

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "dl_common.h"
+#include "retirable.h"
 
 #define DL_NCCL_CHECK(expr)                                                                                      \
   do {                                                                                                           \
@@ -100,21 +101,29 @@ class RcclCommunicator {
     ncclUniqueId id;
     std::memcpy(&id, uid.data(), sizeof(id));
     DL_HIP_CHECK(hipSetDevice(device));
-    DL_NCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
+    ncclComm_t c = nullptr;
+    DL_NCCL_CHECK(ncclCommInitRank(&c, world, id, rank));
+    comm_ = Retirable<ncclComm_t>(c);
     if (timeout_s_ > 0) watcher_ = std::thread([this] { watch_loop(); });
   }
   ~RcclCommunicator() { destroy(); }
 
   void destroy() {
     stop_watchdog();
-    std::lock_guard<std::mutex> c(call_mu_);
-    std::lock_guard<std::mutex> g(mu_);
-    if (comm_) {
-      ncclCommDestroy(comm_);
-      comm_ = nullptr;
+    ncclComm_t live = nullptr, doomed = nullptr;
+    {
+      std::lock_guard<std::mutex> c(call_mu_);  // no host call is in flight past this point
+      std::lock_guard<std::mutex> g(mu_);
+      live = comm_.take_live();
+      doomed = comm_.take_doomed();
+      release_events_locked();
     }
-    release_events_locked();
+    if (live) ncclCommDestroy(live);
+    if (doomed) ncclCommAbort(doomed);  // retired by the watchdog, abort still owed
   }
+  // Take the communicator out of service.  With no host call in flight the
+  // handle is aborted here; otherwise the last in-flight call aborts it when
+  // it returns (never while RCCL may still be using it).
   void abort() {
     stop_watchdog();
     ncclComm_t c;
@@ -132,53 +141,69 @@ class RcclCommunicator {
 
   // Every RCCL host call holds call_mu_ (RCCL calls on one communicator are not
   // thread-safe) but NOT mu_: mu_ guards only the watchdog's state (pending
-  // events, abort reason), so the watchdog can always take it and abort a
-  // communicator whose host call is blocked on a stuck peer.
+  // events, abort reason), so the watchdog can always take it and mark the
+  // communicator failed.  The handle itself is held through a CallGuard for
+  // the duration of the call (a group: from the outermost group_start to its
+  // group_end), and a failed communicator is aborted only once no call holds
+  // it (retirable.h): ncclCommAbort frees the handle.
   void all_reduce(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int op, uintptr_t stream) {
     std::lock_guard<std::mutex> c(call_mu_);
+    CallGuard g(this);
     DL_NCCL_CHECK(ncclAllReduce((const void*)send, (void*)recv, (size_t)count, to_nccl(dtype), to_nccl_op(op),
-                                live(), as_stream(stream)));
+                                g.comm, as_stream(stream)));
     enqueued(stream);
   }
   void broadcast(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int root, uintptr_t stream) {
     std::lock_guard<std::mutex> c(call_mu_);
+    CallGuard g(this);
     DL_NCCL_CHECK(
-        ncclBroadcast((const void*)send, (void*)recv, (size_t)count, to_nccl(dtype), root, live(), as_stream(stream)));
+        ncclBroadcast((const void*)send, (void*)recv, (size_t)count, to_nccl(dtype), root, g.comm, as_stream(stream)));
     enqueued(stream);
   }
   void reduce(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int op, int root, uintptr_t stream) {
     std::lock_guard<std::mutex> c(call_mu_);
+    CallGuard g(this);
     DL_NCCL_CHECK(ncclReduce((const void*)send, (void*)recv, (size_t)count, to_nccl(dtype), to_nccl_op(op), root,
-                             live(), as_stream(stream)));
+                             g.comm, as_stream(stream)));
     enqueued(stream);
   }
   // recvcount elements per rank
   void reduce_scatter(uintptr_t send, uintptr_t recv, int64_t recvcount, int dtype, int op, uintptr_t stream) {
     std::lock_guard<std::mutex> c(call_mu_);
+    CallGuard g(this);
     DL_NCCL_CHECK(ncclReduceScatter((const void*)send, (void*)recv, (size_t)recvcount, to_nccl(dtype),
-                                    to_nccl_op(op), live(), as_stream(stream)));
+                                    to_nccl_op(op), g.comm, as_stream(stream)));
     enqueued(stream);
   }
   void all_gather(uintptr_t send, uintptr_t recv, int64_t sendcount, int dtype, uintptr_t stream) {
     std::lock_guard<std::mutex> c(call_mu_);
+    CallGuard g(this);
     DL_NCCL_CHECK(
-        ncclAllGather((const void*)send, (void*)recv, (size_t)sendcount, to_nccl(dtype), live(), as_stream(stream)));
+        ncclAllGather((const void*)send, (void*)recv, (size_t)sendcount, to_nccl(dtype), g.comm, as_stream(stream)));
     enqueued(stream);
   }
   void send(uintptr_t buf, int64_t count, int dtype, int peer, uintptr_t stream) {
     std::lock_guard<std::mutex> c(call_mu_);
-    DL_NCCL_CHECK(ncclSend((const void*)buf, (size_t)count, to_nccl(dtype), peer, live(), as_stream(stream)));
+    CallGuard g(this);
+    DL_NCCL_CHECK(ncclSend((const void*)buf, (size_t)count, to_nccl(dtype), peer, g.comm, as_stream(stream)));
     enqueued(stream);
   }
   void recv(uintptr_t buf, int64_t count, int dtype, int peer, uintptr_t stream) {
     std::lock_guard<std::mutex> c(call_mu_);
-    DL_NCCL_CHECK(ncclRecv((void*)buf, (size_t)count, to_nccl(dtype), peer, live(), as_stream(stream)));
+    CallGuard g(this);
+    DL_NCCL_CHECK(ncclRecv((void*)buf, (size_t)count, to_nccl(dtype), peer, g.comm, as_stream(stream)));
     enqueued(stream);
   }
   void group_start() {
     std::lock_guard<std::mutex> c(call_mu_);
-    live();
-    DL_NCCL_CHECK(ncclGroupStart());
+    // the outermost group holds the handle until its group_end: RCCL issues
+    // the grouped work there, with the handles the calls inside were given
+    if (group_depth_ == 0) acquire_call();
+    ncclResult_t r = ncclGroupStart();
+    if (r != ncclSuccess) {
+      if (group_depth_ == 0) release_call();
+      DL_NCCL_CHECK(r);
+    }
     ++group_depth_;
   }
   void group_end() {
@@ -186,6 +211,10 @@ class RcclCommunicator {
     if (group_depth_ <= 0) throw std::runtime_error("group_end without group_start");
     ncclResult_t r = ncclGroupEnd();
     if (--group_depth_ == 0) {
+      struct Release {
+        RcclCommunicator* self;
+        ~Release() { self->release_call(); }
+      } rel{this};
       // RCCL launches grouped work (collectives AND p2p) only at the outermost
       // group end: an event recorded earlier would sit in front of the kernels
       // and complete at once, so every grouped op is timed from here
@@ -195,6 +224,11 @@ class RcclCommunicator {
       for (uintptr_t s : streams) track_locked(s);
     }
     DL_NCCL_CHECK(r);
+  }
+  // host calls currently holding the handle (tests)
+  int inflight() {
+    std::lock_guard<std::mutex> g(mu_);
+    return comm_.inflight();
   }
 
   // Time the work enqueued so far on `stream` (no-op while it is being captured).
@@ -220,9 +254,9 @@ class RcclCommunicator {
   std::string async_error() {
     std::lock_guard<std::mutex> g(mu_);
     if (!reason_.empty()) return reason_;
-    if (!comm_) return "communicator destroyed";
+    if (!comm_.get()) return "communicator destroyed";
     ncclResult_t r;
-    DL_NCCL_CHECK(ncclCommGetAsyncError(comm_, &r));
+    DL_NCCL_CHECK(ncclCommGetAsyncError(comm_.get(), &r));
     if (r == ncclSuccess || r == ncclInProgress) return "";
     return ncclGetErrorString(r);
   }
@@ -235,14 +269,31 @@ class RcclCommunicator {
 
   void live_locked() const {
     if (!reason_.empty()) throw std::runtime_error("RCCL communicator failed: " + reason_);
-    if (!comm_) throw std::runtime_error("RCCL communicator used after destroy");
+    if (!comm_.get()) throw std::runtime_error("RCCL communicator used after destroy");
   }
-  // the communicator handle if healthy (checked under mu_, used outside it)
-  ncclComm_t live() {
+  // the handle for one host call if healthy (checked under mu_, used outside
+  // it); every acquire_call is paired with a release_call
+  ncclComm_t acquire_call() {
     std::lock_guard<std::mutex> g(mu_);
     live_locked();
-    return comm_;
+    return comm_.acquire();
   }
+  void release_call() {
+    ncclComm_t doomed;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      doomed = comm_.release();
+    }
+    if (doomed) ncclCommAbort(doomed);  // retired while this call held it
+  }
+  struct CallGuard {
+    RcclCommunicator* self;
+    ncclComm_t comm;
+    explicit CallGuard(RcclCommunicator* s) : self(s), comm(s->acquire_call()) {}
+    ~CallGuard() { self->release_call(); }
+    CallGuard(const CallGuard&) = delete;
+    CallGuard& operator=(const CallGuard&) = delete;
+  };
   // after an enqueue (caller holds call_mu_): time it now, or at the outermost group end
   void enqueued(uintptr_t stream) {
     if (group_depth_ > 0) {
@@ -271,12 +322,11 @@ class RcclCommunicator {
 
   // Record why the communicator failed and take it out of service; the caller
   // aborts the returned handle WITHOUT holding mu_ (ncclCommAbort can wait for
-  // the device), so health()/error() answer immediately.
+  // the device), so health()/error() answer immediately.  Null while a host
+  // call holds the handle: that call's release_call aborts it.
   ncclComm_t detach_locked(const std::string& why) {
     if (reason_.empty()) reason_ = why;
-    ncclComm_t c = comm_;
-    comm_ = nullptr;
-    return c;
+    return comm_.retire();
   }
 
   void release_events_locked() {
@@ -302,8 +352,9 @@ class RcclCommunicator {
     std::unique_lock<std::mutex> lk(mu_);
     while (!stop_) {
       cv_.wait_for(lk, std::chrono::milliseconds(poll_ms_));
-      if (stop_ || !comm_) continue;
+      if (stop_ || !comm_.get()) continue;
       ncclComm_t dead = nullptr;
+      bool failed = false;
       // retire completed work (in order: events of one stream complete in order;
       // across streams an old unfinished event simply keeps the queue from draining)
       while (!pending_.empty()) {
@@ -311,21 +362,27 @@ class RcclCommunicator {
         if (q == hipErrorNotReady) break;
         if (q != hipSuccess) {
           dead = detach_locked(std::string("HIP error while waiting for a collective: ") + hipGetErrorString(q));
+          failed = true;
           break;
         }
         free_.push_back(pending_.front().ev);
         pending_.pop_front();
       }
       ncclResult_t r = ncclSuccess;
-      if (!dead && ncclCommGetAsyncError(comm_, &r) == ncclSuccess && r != ncclSuccess && r != ncclInProgress)
+      if (!failed && ncclCommGetAsyncError(comm_.get(), &r) == ncclSuccess && r != ncclSuccess &&
+          r != ncclInProgress) {
         dead = detach_locked(std::string("RCCL async error: ") + ncclGetErrorString(r));
+        failed = true;
+      }
       const double limit = timeout_s_.load();
-      if (!dead && !pending_.empty() && limit > 0) {
+      if (!failed && !pending_.empty() && limit > 0) {
         double age = std::chrono::duration<double>(std::chrono::steady_clock::now() - pending_.front().t).count();
         if (age > limit)
           dead = detach_locked("collective on rank " + std::to_string(rank_) + " did not complete within " +
                                std::to_string(limit) + " s (dead or stuck peer?)");
       }
+      // dead == nullptr after a failure: a host call still holds the handle and
+      // aborts it on release (release_call)
       if (dead) {  // abort outside the lock: the in-flight RCCL kernels see the abort flag and exit
         lk.unlock();
         ncclCommAbort(dead);
@@ -334,7 +391,7 @@ class RcclCommunicator {
     }
   }
 
-  ncclComm_t comm_ = nullptr;
+  Retirable<ncclComm_t> comm_;             // guarded by mu_
   int rank_, world_, dev_;
   std::atomic<double> timeout_s_;
   int poll_ms_ = 50;

@@ -2797,7 +2797,7 @@ static void conv_wgrad_g(const ConvGeom& g, uintptr_t dy, uintptr_t x, uintptr_t
       // 256 (co) x 128 (k): 48 KiB per 64-row stage, 3 stages = 144 KiB (one WG
       // per CU); half again the MFMAs per DMA'd byte of the 128x128 tile, whose
       // steps were bound by LDS-DMA issue and L2->LDS bytes, not by the MFMAs
-      // (scripts/stamp_wgrad.py: ~1240 cycles per step vs 512 of MFMA per SIMD)
+      // (profiles/r3_wgrad_stamps.txt: ~1240 cycles per step vs 512 of MFMA per SIMD)
       // no fragment prefetch by default: the double fragment set does not fit the
       // 256 registers of 2 waves per SIMD (spills: 275 vs 37 us at 100 workgroups)
       if (g_wgrad_pf == 1) DL_WG(256, 128, 3, 4, 2); else DL_WGN(256, 128, 3, 4, 2);

@@ -185,7 +185,14 @@ __global__ void __launch_bounds__(256) head_softmax_nll_kernel(const float* __re
   if ((tid & 63) == 0) red[tid >> 6] = se;
   __syncthreads();
   const float lse = mx + __logf(red[0] + red[1] + red[2] + red[3]);
-  const int y = labels ? (int)labels[b] : -1;
+  const int64_t y64 = labels ? labels[b] : -1;
+  const int y = (int)y64;
+  if (labels && tid == 0 && (y64 < 0 || y64 >= NC)) {
+    // out-of-range label: this sample's loss (and the mean) become NaN rather
+    // than silently leaving loss_b unwritten (the gradient row is label-free)
+    loss_b[b] = __builtin_nanf("");
+    if (loss) unsafeAtomicAdd(loss, __builtin_nanf(""));
+  }
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int c = tid + k * 256;

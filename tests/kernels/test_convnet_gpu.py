@@ -147,7 +147,7 @@ def test_conv_dgrad_wgrad(C, shape):
     dy = torch.randn(B, H, H, cout, device=dev, generator=g).to(torch.bfloat16)
     # reference on the CPU in fp64: MIOpen's fp32 backward-weights solver picked
     # in some processes was off by ~8 % relative on (3, 8, 16, 64) while our
-    # kernel's output stayed bit-identical (scripts/diag_wgrad_race.py)
+    # kernel's output stayed bit-identical (a one-off race probe, since removed)
     xr = x.double().cpu().permute(0, 3, 1, 2).requires_grad_(True)
     wr = w.double().cpu().permute(0, 3, 1, 2).requires_grad_(True)
     out = F.conv2d(xr, wr, padding=2)

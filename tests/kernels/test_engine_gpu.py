@@ -286,7 +286,7 @@ def test_comm_profile_is_side_effect_free(dev, monkeypatch):
 def test_atomic_modes_train_and_graph_tracks_eager(dev, monkeypatch, mode):
     """Reduction modes 1 and 2 (fp32 atomics: not bitwise reproducible run to
     run): the model fits a repeated batch, and graph replay tracks eager within
-    the run-to-run noise of the atomics (measured: scripts/diag_mode1.py)."""
+    the run-to-run noise of the atomics (measured with a one-off probe, since removed)."""
     monkeypatch.setenv("DISTLEARN_REDUCE_ATOMIC", mode)
     g = torch.Generator(device=dev).manual_seed(1)
     x = torch.randn(32, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)

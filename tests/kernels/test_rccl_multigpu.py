@@ -273,3 +273,175 @@ def test_watchdog_times_grouped_collectives_from_group_end(monkeypatch):
     assert "did not complete within" in comm.health()
     s.synchronize()
     comm.close()
+
+
+# ---------------------------------------------------------------------------
+# Every RCCL entry point at world 1.  NCCL/RCCL let a rank
+# send to itself inside a group, so the p2p binding, all-gather,
+# reduce-scatter and broadcast all run on the 1-GPU box through the same
+# native communicator the N-GPU runs use (DISTLEARN_RCCL_WORLD1=1 forces the
+# identity collectives through RCCL too).
+def _world1(monkeypatch):
+    _need("gloo", 1)
+    from torch_distlearn_amd.parallel.comm import RcclCommunicator
+
+    monkeypatch.setenv("DISTLEARN_RCCL_WORLD1", "1")
+    dev = torch.device("cuda", 0)
+    return dev, RcclCommunicator(0, 1, dev, ctrl_group=None, timeout_s=60.0)
+
+
+def _drained(comm):
+    import time
+
+    t0 = time.time()
+    while comm._c.pending() and time.time() - t0 < 5:
+        time.sleep(0.02)
+    return comm._c.pending() == 0 and comm._c.inflight() == 0
+
+
+def test_rccl_world1_every_entry_point(monkeypatch):
+    dev, comm = _world1(monkeypatch)
+    g = torch.Generator(device=dev).manual_seed(3)
+    # all-reduce (sum / max) and broadcast: identity at one rank, byte for byte
+    x = torch.randn(1 << 16, device=dev, generator=g)
+    x0 = x.clone()
+    comm.all_reduce(x)
+    comm.all_reduce(x, op="max")
+    b = torch.randn(4099, device=dev, generator=g).to(torch.bfloat16)
+    b0 = b.clone()
+    comm.broadcast(b, root=0)
+    # all-gather / reduce-scatter (world * n == n)
+    src = torch.randint(-1000, 1000, (777,), device=dev, generator=g, dtype=torch.int64)
+    gat = torch.empty_like(src)
+    comm.all_gather(gat, src)
+    rs_in = torch.randn(513, device=dev, generator=g)
+    rs = torch.empty_like(rs_in)
+    comm.reduce_scatter(rs, rs_in)
+    # self send/recv inside a group (fp32, bf16, int64, uint8 payloads)
+    pay = [torch.randn(12345, device=dev, generator=g), torch.randn(333, device=dev, generator=g).to(torch.bfloat16),
+           torch.randint(0, 1 << 40, (99,), device=dev, generator=g, dtype=torch.int64),
+           torch.randint(0, 255, (4096,), device=dev, generator=g, dtype=torch.uint8)]
+    got = [torch.empty_like(p) for p in pay]
+    with comm.group():
+        for p, r in zip(pay, got):
+            comm.send(p, 0)
+            comm.recv(r, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(x, x0) and torch.equal(b, b0)
+    assert torch.equal(gat, src) and torch.equal(rs, rs_in)
+    for p, r in zip(pay, got):
+        assert torch.equal(p, r)
+    assert _drained(comm) and comm.health() == ""
+    comm.close()
+
+
+def test_rccl_world1_p2p_inside_hipgraph(monkeypatch):
+    """Grouped self send/recv captured into a hipGraph and replayed: each replay
+    moves the CURRENT contents of the send buffer."""
+    dev, comm = _world1(monkeypatch)
+    s = torch.zeros(4096, device=dev)
+    r = torch.full((4096,), -1.0, device=dev)
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):  # warm-up outside capture (connection setup)
+        with comm.group():
+            comm.send(s, 0)
+            comm.recv(r, 0)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        with comm.group():
+            comm.send(s, 0)
+            comm.recv(r, 0)
+    for k in range(3):
+        s.fill_(float(k + 1))
+        graph.replay()
+        comm.track()
+        torch.cuda.synchronize()
+        assert float(r.min()) == float(r.max()) == float(k + 1)
+    assert _drained(comm)
+    # a graph holding captured RCCL work keeps a reference on the communicator:
+    # ncclCommDestroy waits for it, so the graph goes first
+    del graph
+    torch.cuda.synchronize()
+    comm.close()
+
+
+def test_rccl_world1_async_payload_side_stream(monkeypatch):
+    """The AsyncEA payload pattern (lua/AsyncEA.lua:95-132,180-228) at one
+    rank: the center pull and the delta push are grouped self send/recv on a
+    side stream, ordered against the compute stream by events only (no host
+    synchronisation between the steps): compute writes the center, the side
+    stream ships it into the client's buffer, compute derives the elastic
+    delta from it, the side stream pushes the delta back, and the server's
+    center += delta runs after the push."""
+    dev, comm = _world1(monkeypatch)
+    n = 300 * 200 + 200 * 10 + 210
+    g = torch.Generator(device=dev).manual_seed(9)
+    main = torch.cuda.current_stream()
+    ps = torch.cuda.Stream(device=dev)
+    center = torch.randn(n, device=dev, generator=g)   # server's center
+    params = torch.randn(n, device=dev, generator=g)   # client's replica
+    c_recv = torch.empty(n, device=dev)                # client's copy of the center
+    delta = torch.empty(n, device=dev)
+    d_recv = torch.empty(n, device=dev)                # server's receive buffer
+    alpha = 0.25
+    want_center, want_params = center.clone(), params.clone()
+    for _ in range(5):
+        want_delta = alpha * (want_params - want_center)
+        want_params -= want_delta
+        want_center += want_delta
+        center_ready = torch.cuda.Event()
+        center_ready.record(main)
+        ps.wait_event(center_ready)
+        with torch.cuda.stream(ps):  # pull: server -> client
+            with comm.group():
+                comm.send(center, 0, stream=ps)
+                comm.recv(c_recv, 0, stream=ps)
+        pulled = torch.cuda.Event()
+        pulled.record(ps)
+        main.wait_event(pulled)
+        torch.sub(params, c_recv, out=delta).mul_(alpha)   # calculateUpdateDiff
+        params.sub_(delta)
+        delta_ready = torch.cuda.Event()
+        delta_ready.record(main)
+        ps.wait_event(delta_ready)
+        with torch.cuda.stream(ps):  # push: client -> server
+            with comm.group():
+                comm.send(delta, 0, stream=ps)
+                comm.recv(d_recv, 0, stream=ps)
+        pushed = torch.cuda.Event()
+        pushed.record(ps)
+        main.wait_event(pushed)
+        center.add_(d_recv)                                 # serverGetUpdateDiff
+    torch.cuda.synchronize()
+    torch.testing.assert_close(center, want_center, rtol=0, atol=1e-5)
+    torch.testing.assert_close(params, want_params, rtol=0, atol=1e-5)
+    assert _drained(comm)
+    comm.close()
+
+
+def test_rccl_abort_waits_for_open_group(monkeypatch):
+    """an abort while a host call holds the communicator (here: an
+    open group) must not free it under that call; the abort completes at the
+    group's end and later calls raise CommError."""
+    from torch_distlearn_amd.parallel.comm import CommError
+
+    dev, comm = _world1(monkeypatch)
+    x = torch.ones(64, device=dev)
+    r = torch.empty(64, device=dev)
+    with comm.group():
+        comm.send(x, 0)
+        comm.recv(r, 0)
+        assert comm._c.inflight() == 1  # the group holds the handle until its end
+        comm._c.abort()                 # watchdog/user abort from "another thread"
+        assert comm._c.inflight() == 1 and "aborted" in comm.health()
+        with pytest.raises(CommError):
+            comm.send(x, 0)             # no new call on a failed communicator
+    # group end issued the matched pair on the still-valid handle, then aborted it
+    assert comm._c.inflight() == 0
+    torch.cuda.synchronize()
+    with pytest.raises(CommError):
+        comm.all_reduce(x)
+    comm.close()

@@ -154,6 +154,49 @@ def test_resnet_head_matches_fp32(dev, B, C, ncls):
     assert _rel(lp_eval, lr_) < 1e-2
 
 
+def test_resnet_head_honours_loss_scale_and_labels(dev):
+    """the fused head's gradients follow d loss (a scaled loss
+    scales every gradient), a loss built on the log-probabilities raises
+    instead of training wrong, a second backward raises, int32 labels are
+    refused and an out-of-range label gives a NaN loss."""
+    from torch_distlearn_amd.ops.head import ResNetHeadNLL
+
+    B, C, ncls = 8, 256, 100
+    g = torch.Generator(device=dev).manual_seed(5)
+    h = torch.randn(B, C, 7, 7, device=dev, generator=g).to(BF).contiguous(memory_format=CL)
+    w = torch.randn(ncls, C, device=dev, generator=g) * C ** -0.5
+    b = torch.randn(ncls, device=dev, generator=g) * 0.1
+    y = torch.randint(0, ncls, (B,), device=dev, generator=g)
+
+    def run(scale):
+        gw, gb = torch.zeros(ncls, C, device=dev), torch.zeros(ncls, device=dev)
+        hi = h.detach().requires_grad_(True)
+        loss, _ = ResNetHeadNLL.apply(hi, torch.nn.Parameter(w), torch.nn.Parameter(b), y, (gw, gb, lambda: None))
+        (loss * scale).backward()
+        torch.cuda.synchronize()
+        return hi.grad.float(), gw, gb
+
+    d1, w1, b1 = run(1.0)
+    d3, w3, b3 = run(3.0)
+    assert _rel(d3, 3 * d1) < 1e-2 and _rel(w3, 3 * w1) < 1e-2 and _rel(b3, 3 * b1) < 1e-5
+    hi = h.detach().requires_grad_(True)
+    bind = (torch.zeros(ncls, C, device=dev), torch.zeros(ncls, device=dev), lambda: None)
+    loss, logp = ResNetHeadNLL.apply(hi, torch.nn.Parameter(w), torch.nn.Parameter(b), y, bind)
+    with pytest.raises(RuntimeError, match="not differentiable"):
+        (loss + logp.sum()).backward()
+    loss, _ = ResNetHeadNLL.apply(hi, torch.nn.Parameter(w), torch.nn.Parameter(b), y, bind)
+    loss.backward(retain_graph=True)
+    with pytest.raises(RuntimeError, match="twice"):
+        loss.backward()
+    with pytest.raises(ValueError, match="int64"):
+        ResNetHeadNLL.apply(hi, torch.nn.Parameter(w), torch.nn.Parameter(b), y.int(), bind)
+    bad = y.clone()
+    bad[3] = ncls + 7
+    with torch.no_grad():
+        loss, _ = ResNetHeadNLL.apply(h, w, b, bad, bind)
+    assert torch.isnan(loss).item()
+
+
 def test_resnet50_step_has_no_vendor_convs(dev):
     """A ResNet-50 training step (batch 64, 64x64 images) dispatches no MIOpen
     convolution and no hipBLAS GEMM: every conv, the classifier and the loss

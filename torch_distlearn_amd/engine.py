@@ -60,6 +60,10 @@ class DataParallelTrainer:
         self.flat = FlatParams(model, grads=True, shadow_bf16=bf16_shadow)
         self.mom = self.flat.like(0.0) if momentum else None
         self.loss_fn = loss_fn or getattr(model, "loss", None) or torch.nn.functional.nll_loss
+        # a model's fused forward_loss (ResNet-50: mean NLL with the classifier
+        # backward in the same node) trains the model's own loss, so it is used
+        # only when the caller did not pass a loss_fn of their own
+        self._fused_loss_ok = loss_fn is None
         hooks = overlap and backend == "torch"
         # grad_comm_dtype="bf16": the bucketed all-reduce sends a bf16 copy of the
         # gradient (half the xGMI bytes) with the participation count in fp32
@@ -124,7 +128,7 @@ class DataParallelTrainer:
         if self.executor is not None:
             return self.executor.forward_backward(x, y)
         self.model.train()
-        fused = getattr(self.model, "forward_loss", None)
+        fused = getattr(self.model, "forward_loss", None) if self._fused_loss_ok else None
         out = fused(x, y, compute_dtype=self.compute_dtype) if (fused is not None and x.is_cuda) else None
         if out is not None:  # the model computes its loss (and the head's backward) itself
             loss, logp = out

@@ -332,7 +332,7 @@ class ResNet50(nn.Module):
         h = self.trunk(x, compute_dtype)
         if not self._hip_head(h):
             logp = F.log_softmax(F.linear(h.float().mean((2, 3)), self.fc_w, self.fc_b), dim=1)
-            return F.nll_loss(logp, y), logp
+            return self.loss(logp, y), logp
         from ..ops.head import ResNetHeadNLL
 
         return ResNetHeadNLL.apply(h, self.fc_w, self.fc_b, y, self._fc_bind)

@@ -12,14 +12,20 @@ Forward (training, labels given):
   slabs bit: fp32 partial slabs, no bf16 logits);
 * ``head_softmax_nll``: sums the slabs + bias in fp32, log-softmax, per-sample
   loss and its mean, dlogits (bf16, scaled by 1/(B*49): the mean's backward
-  folded in), the bias gradient (fp32 atomics into the flat gradient);
-* the backward GEMMs run here too (the loss is the graph's root, so its
-  gradient is 1): d(pooled) = dlogits W (``conv_fwd``), the weight gradient
-  dlogits^T f (``conv_wgrad`` + ``head_wgrad_reduce`` x 49 into the flat
-  gradient), and ``head_broadcast`` expands d(pooled) over the 7x7 positions.
+  folded in), the bias gradient (fp32 atomics into a per-step buffer);
+* backward (``d loss`` from autograd, 1 when the loss is the graph's root):
+  dlogits and the bias gradient are scaled by ``d loss`` on the device (no
+  host sync), then d(pooled) = dlogits W (``conv_fwd``), the weight gradient
+  dlogits^T f (``conv_wgrad`` + ``head_wgrad_reduce`` x 49, accumulated into
+  the flat gradient) and ``head_broadcast`` expands d(pooled) over the 7x7
+  positions; the bucket is reported ready.
 
-``backward`` only hands the stashed input gradient to autograd: the loss is
-the root of the training graph (``loss.backward()``, d loss = 1).
+Contract: the loss output may be scaled or combined with other terms (its
+gradient is honoured); the log-probability output is for metrics only -- a
+loss built on it raises in backward instead of training with a wrong
+gradient.  One backward per forward.  Labels must be int64 on the device; an
+out-of-range label makes that sample's loss (and the mean) NaN instead of
+reading past the logits.
 """
 from __future__ import annotations
 
@@ -71,36 +77,49 @@ class ResNetHeadNLL(torch.autograd.Function):
         if not train:
             C.head_softmax_nll(slab.data_ptr(), splits, B, ncls, NCp, fc_b.data_ptr(), 0, logp.data_ptr(), 0, 0, 1.0,
                                0, 0, s)
-            ctx.dh = None
+            ctx.saved = None
             return loss[0], logp
-        gw, gb, ready = bind
+        if labels.dtype != torch.int64 or labels.device != h.device or labels.numel() != B:
+            raise ValueError("ResNetHeadNLL: labels must be int64 [B] on the activations' device")
         loss_b = torch.empty(B, device=dev)
         dl = torch.empty(B, NCp, dtype=BF16, device=dev)
+        db = torch.zeros(ncls, device=dev)  # this step's bias gradient, scaled by d loss in backward
         C.head_softmax_nll(slab.data_ptr(), splits, B, ncls, NCp, fc_b.data_ptr(), labels.data_ptr(), logp.data_ptr(),
-                           loss_b.data_ptr(), dl.data_ptr(), 1.0 / (B * HW), gb.data_ptr(), loss.data_ptr(), s)
+                           loss_b.data_ptr(), dl.data_ptr(), 1.0 / (B * HW), db.data_ptr(), loss.data_ptr(), s)
+        ctx.set_materialize_grads(False)
+        ctx.saved = (f, dl, db, wbt, bind, (B, Cc, H, W, ncls, NCp))
+        return loss[0], logp
+
+    @staticmethod
+    def backward(ctx, dloss, dlogp):
+        if dlogp is not None:
+            raise RuntimeError("ResNetHeadNLL: the log-probability output is not differentiable (use the loss output)")
+        if getattr(ctx, "saved", None) is None:
+            raise RuntimeError("ResNetHeadNLL: backward ran twice (or on an eval forward)")
+        f, dl, db, wbt, (gw, gb, ready), (B, Cc, H, W, ncls, NCp) = ctx.saved
+        ctx.saved = None
+        if dloss is None:
+            return None, None, None, None, None
+        C = native()
+        s = stream_handle()
+        dev = f.device
+        HW = H * W
+        dl.mul_(dloss)              # d loss (1.0 at the root: exact)
+        gb.add_(db * dloss)
         # d(pooled) = dl W  ([B, NCp] x [NCp, C]: a 1x1 conv whose weight is W^T)
+        from .conv import _fwd_plan, _wgrad_plan
+
         df = torch.empty(B, Cc, dtype=BF16, device=dev)
         dt, ds = _fwd_plan(B, Cc, NCp)
         dslab = torch.empty(ds * B * Cc, device=dev) if ds > 1 else None
         C.conv_fwd(dl.data_ptr(), wbt.data_ptr(), df.data_ptr(), 0, 0 if dslab is None else dslab.data_ptr(), B, 1, 1,
                    NCp, Cc, 1, dt, ds, s)
-        dh = torch.empty_like(h, memory_format=torch.channels_last)
+        dh = torch.empty(B, Cc, H, W, dtype=BF16, device=dev, memory_format=torch.channels_last)
         C.head_broadcast(df.data_ptr(), dh.data_ptr(), B, HW, Cc, s)
-        # dW = dl^T f ([NCp, B] x [B, C]) -> x HW (dl carries 1/(B*HW)) into the flat gradient
-        from .conv import _wgrad_plan
-
+        # dW = dl^T f ([NCp, B] x [B, C]) -> x HW (dl carries 1/(B*HW)) accumulated into the flat gradient
         wt_tile, wsplits = _wgrad_plan(NCp, Cc, B)
         ws = torch.empty(wsplits * NCp * Cc, device=dev)
         C.conv_wgrad(dl.data_ptr(), f.data_ptr(), ws.data_ptr(), B, 1, 1, Cc, NCp, 1, wsplits, Cc, wt_tile, 0, s)
         C.head_wgrad_reduce(ws.data_ptr(), gw.data_ptr(), wsplits, ncls, NCp, Cc, float(HW), s)
         ready()
-        ctx.dh = dh
-        return loss[0], logp
-
-    @staticmethod
-    def backward(ctx, dloss, dlogp):
-        dh = ctx.dh
-        ctx.dh = None
-        # the loss is the root of the training graph (d loss = 1): every gradient
-        # was computed in forward for exactly that root
         return dh, None, None, None, None
