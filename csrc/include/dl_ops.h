@@ -20,6 +20,11 @@ void cast_f32_bf16(uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream);
 void cast_bf16_f32(uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream);
 void sgd_update_g16(uintptr_t p, uintptr_t g16, uintptr_t mom, uintptr_t p16, uintptr_t slot, float lr,
                     float momentum, float wd, int64_t n, uintptr_t stream);
+// sgd_update whose gradient in up to 4 ranges [offs, offs+lens) is the sum of the
+// split-K slabs [splits][lens] at slabs[j] (bitwise slab_reduce's sum)
+void sgd_update_slabs(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, uintptr_t slot, float lr,
+                      float momentum, float wd, int64_t n, std::vector<int64_t> offs, std::vector<int64_t> lens,
+                      std::vector<uintptr_t> slabs, std::vector<int> splits, uintptr_t stream);
 
 // metrics.hip ---------------------------------------------------------------
 // channels-last training BatchNorm (+ReLU, +residual) for the ResNet-50 path

@@ -11,7 +11,10 @@
 // All kernels are grid-stride streaming kernels with 16-byte (float4) accesses;
 // the participation count `n` is read on the device from the all-reduced slot,
 // so the normalisation needs no host synchronisation (graph-capturable).
+#include <vector>
+
 #include "dl_common.h"
+#include "slab_reduce_dev.h"
 
 namespace dl {
 
@@ -82,6 +85,106 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, const G
     }
     update(i, pa, ga, ma);
     if (two) update(j, pb, gb, mb);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// SGD whose gradient for some ranges still lies in split-K weight-gradient
+// slabs (one GPU, nothing to all-reduce: the conv executor skips the slab
+// reduce launches and the update sums the slabs itself).  The sum per element
+// is bitwise the one slab_reduce_body<TPO> computes (slab_reduce_dev.h):
+// TPO lanes each add a strided subset of the splits in split order, then a
+// xor-shuffle tree -- so deferring the reduce changes no bit of the update.
+// ---------------------------------------------------------------------------
+constexpr int kSlabRanges = 4;
+constexpr int kSlabMaxSplits = 31;  // the stand-alone reduce uses 1 or 8 lanes per output up to here
+struct SlabRanges {
+  int n;
+  int64_t lo4[kSlabRanges], hi4[kSlabRanges];  // float4 index range in the updated buffer
+  const float* slab[kSlabRanges];               // [splits][len] fp32, len = (hi4 - lo4) * 4
+  int64_t stride4[kSlabRanges];                 // float4s per split
+  int splits[kSlabRanges], tpo[kSlabRanges];
+};
+
+template <int TPO>
+__device__ __forceinline__ void add4(float4 (&part)[TPO], int t, const float4& v) {
+  // t is a compile-time constant after unrolling (no dynamic register indexing)
+  float4& q = part[t];
+  q.x += v.x; q.y += v.y; q.z += v.z; q.w += v.w;
+}
+
+template <int TPO>
+__device__ __forceinline__ float4 slab_sum4(const float4* __restrict__ s, int64_t stride4, int splits) {
+  float4 part[TPO];
+#pragma unroll
+  for (int t = 0; t < TPO; ++t) part[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+  // chunks of 4 splits, the chunk's loads in flight before its adds; lane t of
+  // the stand-alone reduce adds splits t, t+TPO, ... in order: same here
+  for (int sp0 = 0; sp0 < splits; sp0 += 4) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (sp0 + u < splits) v[u] = s[(int64_t)(sp0 + u) * stride4];
+    const bool hi = TPO == 8 && (sp0 & 4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (sp0 + u >= splits) break;
+      if constexpr (TPO == 1) add4<TPO>(part, 0, v[u]);
+      else if (hi) add4<TPO>(part, 4 + u, v[u]);
+      else add4<TPO>(part, u, v[u]);
+    }
+  }
+#pragma unroll
+  for (int o = TPO / 2; o > 0; o >>= 1) {
+    float4 np[TPO];
+#pragma unroll
+    for (int t = 0; t < TPO; ++t) {
+      const float4 a = part[t], b = part[t ^ o];
+      np[t] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    }
+#pragma unroll
+    for (int t = 0; t < TPO; ++t) part[t] = np[t];
+  }
+  return part[0];
+}
+
+__device__ __forceinline__ float4 grad4_or_slabs(const float* __restrict__ g, const SlabRanges& r, int64_t i) {
+  for (int k = 0; k < r.n; ++k) {
+    if (i >= r.lo4[k] && i < r.hi4[k]) {
+      const float4* s = reinterpret_cast<const float4*>(r.slab[k]) + (i - r.lo4[k]);
+      return r.tpo[k] == 8 ? slab_sum4<8>(s, r.stride4[k], r.splits[k]) : slab_sum4<1>(s, r.stride4[k], r.splits[k]);
+    }
+  }
+  return load_grad4(g, i);
+}
+
+template <bool kMomentum, bool kShadow>
+__global__ void __launch_bounds__(256) sgd_slabs_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ mom, bf16_t* __restrict__ p16,
+                                                        const float* __restrict__ slot, float lr, float momentum,
+                                                        float wd, int64_t n4, const SlabRanges r) {
+  const float s = participation_scale(slot);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pv = reinterpret_cast<const float4*>(p)[i];
+    const float4 gv = grad4_or_slabs(g, r, i);
+    float gx = gv.x * s + wd * pv.x, gy = gv.y * s + wd * pv.y;
+    float gz = gv.z * s + wd * pv.z, gw = gv.w * s + wd * pv.w;
+    if constexpr (kMomentum) {
+      float4 mv = reinterpret_cast<const float4*>(mom)[i];
+      mv.x = momentum * mv.x + gx; mv.y = momentum * mv.y + gy;
+      mv.z = momentum * mv.z + gz; mv.w = momentum * mv.w + gw;
+      reinterpret_cast<float4*>(mom)[i] = mv;
+      gx = mv.x; gy = mv.y; gz = mv.z; gw = mv.w;
+    }
+    pv.x -= lr * gx; pv.y -= lr * gy; pv.z -= lr * gz; pv.w -= lr * gw;
+    reinterpret_cast<float4*>(p)[i] = pv;
+    if constexpr (kShadow) {
+      uint2 packed;
+      packed.x = pack_bf16x2(pv.x, pv.y);
+      packed.y = pack_bf16x2(pv.z, pv.w);
+      reinterpret_cast<uint2*>(p16)[i] = packed;
+    }
   }
 }
 
@@ -199,6 +302,41 @@ void sgd_update(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, uintptr_
   else if (mom) sgd_kernel<true, false><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4);
   else if (p16) sgd_kernel<false, true><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4);
   else sgd_kernel<false, false><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+void sgd_update_slabs(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, uintptr_t slot, float lr,
+                      float momentum, float wd, int64_t n, std::vector<int64_t> offs, std::vector<int64_t> lens,
+                      std::vector<uintptr_t> slabs, std::vector<int> splits, uintptr_t stream) {
+  check_vec4(n, "sgd_update_slabs");
+  const size_t k = offs.size();
+  if (k > (size_t)kSlabRanges || lens.size() != k || slabs.size() != k || splits.size() != k)
+    throw std::runtime_error("sgd_update_slabs: up to 4 consistent slab ranges");
+  SlabRanges r{};
+  r.n = (int)k;
+  for (size_t j = 0; j < k; ++j) {
+    if (offs[j] % 4 || lens[j] % 4 || offs[j] < 0 || offs[j] + lens[j] > n || slabs[j] % 16)
+      throw std::runtime_error("sgd_update_slabs: ranges must be 16-byte aligned and inside the buffer");
+    if (splits[j] < 1 || splits[j] > kSlabMaxSplits)
+      throw std::runtime_error("sgd_update_slabs: 1..31 splits per range");
+    if (j > 0 && offs[j] < offs[j - 1] + lens[j - 1]) throw std::runtime_error("sgd_update_slabs: ranges overlap");
+    r.lo4[j] = offs[j] / 4;
+    r.hi4[j] = (offs[j] + lens[j]) / 4;
+    r.slab[j] = (const float*)slabs[j];
+    r.stride4[j] = lens[j] / 4;
+    r.splits[j] = splits[j];
+    r.tpo[j] = slab_reduce_tpo(splits[j]) == 1 ? 1 : 8;  // the stand-alone slab_reduce's lane split
+  }
+  const int64_t n4 = n / 4;
+  if (n4 == 0) return;
+  dim3 grid(stream_grid(n4)), block(256);
+  auto s = as_stream(stream);
+  float* P = (float*)p; const float* G = (const float*)g; float* M = (float*)mom; bf16_t* P16 = (bf16_t*)p16;
+  const float* S = (const float*)slot;
+  if (mom && p16) sgd_slabs_kernel<true, true><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4, r);
+  else if (mom) sgd_slabs_kernel<true, false><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4, r);
+  else if (p16) sgd_slabs_kernel<false, true><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4, r);
+  else sgd_slabs_kernel<false, false><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4, r);
   DL_HIP_CHECK(hipGetLastError());
 }
 

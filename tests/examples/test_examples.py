@@ -41,6 +41,19 @@ def test_cifar10_two_nodes():
     assert "test accuracy" in out
 
 
+def test_cifar10_two_nodes_reaches_test_accuracy():
+    """The reference example's purpose is the all-reduced test confusion
+    matrix (examples/cifar10.lua:213-236): on the synthetic CIFAR-shaped data
+    (class prototypes + noise, shared by the train and test splits) one epoch
+    of 64 steps per node must classify the held-out split (>= 95 %)."""
+    import re
+
+    out = _launch(2, "cifar10.py", "--epochs", "1", "--batchSize", "64", "--trainSize", "4096", "--testSize", "256",
+                  timeout=600)
+    acc = [float(m) for m in re.findall(r"test accuracy ([0-9.]+)%", out)]
+    assert acc and acc[-1] >= 95.0, out[-2000:]
+
+
 def test_async_easgd_roles(tmp_path):
     out = _launch(4, "easgd.py", "--numNodes", "2", "--dataset", "mnist", "--trainSize", "256", "--batchSize", "16",
                   "--communicationTime", "2", "--testTime", "2", "--numEpochs", "1",

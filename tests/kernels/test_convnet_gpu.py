@@ -459,6 +459,51 @@ def test_executor_matches_torch_model(C, atomic, monkeypatch):
 
 
 
+@pytest.mark.parametrize("atomic", ["2", "0"])
+def test_executor_tracks_torch_over_30_steps(C, atomic, monkeypatch):
+    """30 training steps of the HIP executor (through the trainer:
+    bucketed update, fused SGD) vs an fp32 PyTorch model trained on the same
+    batches: every layer's running MEAN and running VARIANCE and the eval-mode
+    prediction (running statistics) stay within 2x of the drift PyTorch's own
+    bf16 path shows against the same fp32 run, and the held-out accuracy of
+    the HIP predict equals the fp32 model's."""
+    monkeypatch.setenv("DISTLEARN_REDUCE_ATOMIC", atomic)
+    from torch_distlearn_amd import Tree
+    from torch_distlearn_amd.data import CIFAR_MEAN, CIFAR_STD, synthetic_cifar10
+    from torch_distlearn_amd.engine import DataParallelTrainer
+    from torch_distlearn_amd.models import CifarConvNet
+
+    dev = torch.device("cuda")
+    imgs, labels = synthetic_cifar10(32 * 30 + 256, seed=11)
+    x_all = ((imgs.float() / 255 - torch.tensor(CIFAR_MEAN)) / torch.tensor(CIFAR_STD)).to(dev)
+    y_all = labels.to(dev)
+    runs = {}
+    for name, backend, dt in (("hip", "hip", torch.bfloat16), ("bf16", "torch", torch.bfloat16),
+                              ("fp32", "torch", torch.float32)):
+        tree = Tree(1, 1, host="127.0.0.1", port=29741, device=dev)
+        model = CifarConvNet(seed=3).to(dev)
+        tr = DataParallelTrainer(model, tree, lr=0.02, backend=backend, compute_dtype=dt, max_batch=32)
+        tr.synchronize_parameters()
+        for k in range(30):
+            xb = x_all[32 * k:32 * (k + 1)].to(dt).contiguous()
+            tr.step(xb, y_all[32 * k:32 * (k + 1)])
+        xt, yt = x_all[960:992].to(dt).contiguous(), y_all[960:992]
+        lp = tr.predict(xt).float()
+        torch.cuda.synchronize()
+        runs[name] = ([getattr(model, f"bn{i + 1}_rm").clone() for i in range(4)],
+                      [getattr(model, f"bn{i + 1}_rv").clone() for i in range(4)], lp, yt)
+    lp32, yt = runs["fp32"][2], runs["fp32"][3]
+    for i in range(4):
+        for j, what in ((0, "running_mean"), (1, "running_var")):
+            ref = runs["fp32"][j][i]
+            e_hip, e_bf = _rel(runs["hip"][j][i], ref), _rel(runs["bf16"][j][i], ref)
+            assert e_hip < max(5e-2, 2 * e_bf), (f"bn{i + 1} {what}", e_hip, e_bf)
+    e_hip, e_bf = _rel(runs["hip"][2], lp32), _rel(runs["bf16"][2], lp32)
+    assert e_hip < max(5e-2, 2 * e_bf), ("predict", e_hip, e_bf)
+    acc = lambda lp: float((lp.argmax(1) == yt).float().mean())  # noqa: E731
+    assert acc(runs["hip"][2]) >= acc(lp32) - 1 / 32, (acc(runs["hip"][2]), acc(lp32))
+
+
 # ---------------------------------------------------------------------------
 # reduction mode 1 (atomic per-channel totals, finalize fused into consumers)
 # ---------------------------------------------------------------------------

@@ -111,6 +111,15 @@ class DataParallelTrainer:
                 and os.environ.get("DISTLEARN_BUCKET_UPDATE", "0") == "1"):
             self.bucket_updates = self.sgd.enable_bucket_updates(
                 self.flat, lambda: self.lr, momentum=momentum, weight_decay=weight_decay, momentum_buf=self.mom)
+        # One node: the conv executor leaves the split-K weight gradients of the
+        # layers whose slabs the update can read in their slabs, and the fused SGD
+        # sums them itself (bitwise the same update, two launches fewer per step;
+        # nothing is all-reduced at one node).  DISTLEARN_DEFER_SLABS=0: off (A/B).
+        self._slabs = None
+        if (tree.numNodes == 1 and algo in ("sgd", "ea") and not self.bucket_updates
+                and callable(getattr(self.executor, "defer_slab_reduce", None))
+                and os.environ.get("DISTLEARN_DEFER_SLABS", "1") == "1"):
+            self._slabs = self.executor.defer_slab_reduce() or None
         self.graph = graph
         self._graph = None
         self._static = None
@@ -155,7 +164,7 @@ class DataParallelTrainer:
                 h(self.last_logits(), labels)
         if self.algo == "sgd":
             self.sgd.step(f, self.lr, momentum=self.momentum, weight_decay=self.weight_decay,
-                          momentum_buf=self.mom)
+                          momentum_buf=self.mom, slabs=self._slabs)
         elif self.algo == "ea":
             self._local_update()
         return loss
@@ -164,7 +173,7 @@ class DataParallelTrainer:
         from .ops.flat import flat_sgd_
 
         flat_sgd_(self.flat, self.lr, slot=None, mom=self.mom, momentum=self.momentum,
-                  weight_decay=self.weight_decay)
+                  weight_decay=self.weight_decay, slabs=self._slabs)
 
     def step(self, x, y: Optional[torch.Tensor] = None) -> torch.Tensor:
         """One training step on this node's mini-batch; returns the loss

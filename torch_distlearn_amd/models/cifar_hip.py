@@ -276,6 +276,7 @@ class CifarHIPExecutor:
         self.atomic_wgrad = self.mode == 1      # split-K weight gradients by atomics (else slabs)
         self.rows = {0: 0, 1: 1, 2: int(os.environ.get("DISTLEARN_REDUCE_ROWS", "16"))}[self.mode]
         self._alloc(self.B)
+        self._deferred = ()  # blocks whose weight-gradient slab reduce the update performs (defer_slab_reduce)
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self, B: int):
@@ -592,6 +593,8 @@ class CifarHIPExecutor:
                 sargs = (slab.data_ptr(), gw.data_ptr(), splits, cout, KSIZE * KSIZE, cin, self.cins_real[i])
                 if merge and i > 0:  # reduced by block i-1's BN backward reduce launch
                     pending = (sargs, i)
+                elif i in self._deferred:
+                    pass  # summed by the update kernel (defer_slab_reduce)
                 else:
                     if self.side_reduce and i > 0:  # overlaps this block's dgrad (block 1 has none)
                         side.wait_stream(main)
@@ -631,6 +634,21 @@ class CifarHIPExecutor:
         if self.side_wgrad or self.side_reduce:
             main.wait_stream(side)  # join
         return self.loss[0]
+
+    def defer_slab_reduce(self):
+        """Leave the split-K weight gradients of the blocks whose slabs the
+        fused SGD can read in place (slab layout == weight layout: no channel
+        padding; < 32 splits) in their slabs: the slab_reduce launches are
+        skipped and the update sums the slabs (flat.py flat_sgd_ ``slabs``,
+        bitwise the same sum).  Only for a trainer that all-reduces nothing
+        (one node): the flat gradient of those weights is then never written.
+        Returns [(leaf, slab, splits)] for the update."""
+        if self.mode == 1 or self.side_wgrad or self.side_reduce or self.merge_slab:
+            return []
+        blocks = [i for i in range(self.nb)
+                  if not self.wplan[i][2] and self.cins[i] == self.cins_real[i] and self.wplan[i][1] < 32]
+        self._deferred = tuple(blocks)
+        return [(self._leaf(i, 0), self.wslab_l[i], self.wplan[i][1]) for i in blocks]
 
     def _region_dgrad(self, i: int, B: int) -> bool:
         """Whether block i's (unsplit) dgrad runs on the region (tap-reuse)

@@ -178,9 +178,21 @@ def _scale_from_slot(slot):
 
 def sgd_update_(p: torch.Tensor, g: torch.Tensor, lr: float, slot: torch.Tensor | None = None,
                 mom: torch.Tensor | None = None, momentum: float = 0.0, weight_decay: float = 0.0,
-                shadow: torch.Tensor | None = None) -> None:
+                shadow: torch.Tensor | None = None, slabs=None) -> None:
     """p -= lr * (g/n + wd*p) [with momentum buffer]; n from ``slot`` (device).
-    ``g`` is fp32, or bf16 (the all-reduced wire copy of grad_comm_dtype="bf16")."""
+    ``g`` is fp32, or bf16 (the all-reduced wire copy of grad_comm_dtype="bf16").
+    ``slabs``: [(offset into p, numel, slab tensor [splits * numel], splits)]:
+    in those ranges the gradient is the sum of the split-K slabs instead of
+    ``g`` (one GPU: the conv executor's deferred slab reduce; bitwise the
+    stand-alone reduce's sum)."""
+    if slabs:
+        if not p.is_cuda or g.dtype != torch.float32:
+            raise ValueError("sgd_update_: slab gradients need an fp32 gradient on the GPU")
+        native().sgd_update_slabs(p.data_ptr(), g.data_ptr(), _ptr(mom), _ptr(shadow), _ptr(slot), float(lr),
+                                  float(momentum), float(weight_decay), p.numel(), [int(o) for o, _, _, _ in slabs],
+                                  [int(n) for _, n, _, _ in slabs], [t.data_ptr() for _, _, t, _ in slabs],
+                                  [int(k) for _, _, _, k in slabs], stream_handle())
+        return
     if p.is_cuda:
         fn = native().sgd_update_g16 if g.dtype == torch.bfloat16 else native().sgd_update
         fn(p.data_ptr(), g.data_ptr(), _ptr(mom), _ptr(shadow), _ptr(slot), float(lr), float(momentum),
@@ -206,16 +218,22 @@ def _overlaps(x: torch.Tensor, y: torch.Tensor) -> bool:
 
 
 def flat_sgd_(flat: "FlatParams", lr: float, slot: torch.Tensor | None = None, mom: torch.Tensor | None = None,
-              momentum: float = 0.0, weight_decay: float = 0.0, grad: torch.Tensor | None = None) -> None:
+              momentum: float = 0.0, weight_decay: float = 0.0, grad: torch.Tensor | None = None,
+              slabs=None) -> None:
     """The fused update over a FlatParams' parameter body: the 64-element
     header (whose gradient element is the participation count) is left out,
     so ``n`` never flows into the parameter buffer.  ``grad``: the gradient
-    buffer to read (default ``flat.grad``; ``flat.grad16`` for bf16 comm)."""
+    buffer to read (default ``flat.grad``; ``flat.grad16`` for bf16 comm).
+    ``slabs``: [(leaf index, slab tensor, splits)] whose gradient is still in
+    split-K slabs (see :func:`sgd_update_`)."""
     H = HEADER
     g = flat.grad if grad is None else grad
+    rng = None
+    if slabs:
+        rng = sorted((flat.offsets[i] - H, flat.numels[i], t, k) for i, t, k in slabs)
     sgd_update_(flat.data[H:], g[H:], lr, slot=slot, mom=None if mom is None else mom[H:],
                 momentum=momentum, weight_decay=weight_decay,
-                shadow=None if flat.shadow is None else flat.shadow[H:])
+                shadow=None if flat.shadow is None else flat.shadow[H:], slabs=rng)
 
 
 def scale_by_count_(x: torch.Tensor, slot: torch.Tensor) -> None:
