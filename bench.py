@@ -337,6 +337,9 @@ def main():
         "dgrad_stages": getattr(ex, "dgrad_stages", None),
         # the wire dtype actually used (world 1: no collective, fp32)
         "grad_comm_dtype": getattr(tr, "grad_comm_dtype", "fp32") if not is_server else "fp32",
+        # world > 1: the overlap policy measured on this machine during warm-up
+        # (engine.py select_policy: both candidates' ms per step, max over ranks)
+        "policy": getattr(tr, "policy", None) if not is_server else None,
     }
     ms = dt / a.steps * 1e3
     imgs = batch * len(workers) * a.steps / dt

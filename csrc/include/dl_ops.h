@@ -21,10 +21,13 @@ void cast_bf16_f32(uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream);
 void sgd_update_g16(uintptr_t p, uintptr_t g16, uintptr_t mom, uintptr_t p16, uintptr_t slot, float lr,
                     float momentum, float wd, int64_t n, uintptr_t stream);
 // sgd_update whose gradient in up to 4 ranges [offs, offs+lens) is the sum of the
-// split-K slabs [splits][lens] at slabs[j] (bitwise slab_reduce's sum)
+// split-K slabs [splits][lens] at slabs[j], and in one optional channel-padded
+// "tail" range (offset, numel, splits, Cout, taps, Cp, C) the sum of tail_slab
+// (bitwise slab_reduce's sums)
 void sgd_update_slabs(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, uintptr_t slot, float lr,
                       float momentum, float wd, int64_t n, std::vector<int64_t> offs, std::vector<int64_t> lens,
-                      std::vector<uintptr_t> slabs, std::vector<int> splits, uintptr_t stream);
+                      std::vector<uintptr_t> slabs, std::vector<int> splits, std::vector<int64_t> tail,
+                      uintptr_t tail_slab, uintptr_t stream);
 
 // metrics.hip ---------------------------------------------------------------
 // channels-last training BatchNorm (+ReLU, +residual) for the ResNet-50 path

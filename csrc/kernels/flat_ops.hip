@@ -42,6 +42,30 @@ __device__ __forceinline__ float4 load_grad4(const bf16_t* g, int64_t i) {
                      __uint_as_float(u.y & 0xffff0000u));
 }
 
+// One element of the fused update, with every rounding step explicit (fma
+// contraction left to the compiler differs between the float4 and the scalar
+// code paths; the slab-consuming update must match this kernel bit for bit).
+template <bool kMomentum>
+__device__ __forceinline__ float sgd_elem(float p, float g, float* m, float s, float wd, float lr, float momentum) {
+  float gx = __builtin_fmaf(g, s, wd * p);
+  if constexpr (kMomentum) {
+    const float mv = __builtin_fmaf(momentum, *m, gx);
+    *m = mv;
+    gx = mv;
+  }
+  return __builtin_fmaf(-lr, gx, p);
+}
+
+template <bool kMomentum>
+__device__ __forceinline__ float4 sgd_elem4(float4 p, const float4 g, float4& m, float s, float wd, float lr,
+                                            float momentum) {
+  p.x = sgd_elem<kMomentum>(p.x, g.x, &m.x, s, wd, lr, momentum);
+  p.y = sgd_elem<kMomentum>(p.y, g.y, &m.y, s, wd, lr, momentum);
+  p.z = sgd_elem<kMomentum>(p.z, g.z, &m.z, s, wd, lr, momentum);
+  p.w = sgd_elem<kMomentum>(p.w, g.w, &m.w, s, wd, lr, momentum);
+  return p;
+}
+
 template <bool kMomentum, bool kShadow, typename GT = float>
 __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, const GT* __restrict__ g,
                                                   float* __restrict__ mom, bf16_t* __restrict__ p16,
@@ -50,15 +74,8 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, const G
   const float s = participation_scale(slot);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   auto update = [&](int64_t i, float4 pv, const float4 gv, float4 mv) {
-    float gx = gv.x * s + wd * pv.x, gy = gv.y * s + wd * pv.y;
-    float gz = gv.z * s + wd * pv.z, gw = gv.w * s + wd * pv.w;
-    if constexpr (kMomentum) {
-      mv.x = momentum * mv.x + gx; mv.y = momentum * mv.y + gy;
-      mv.z = momentum * mv.z + gz; mv.w = momentum * mv.w + gw;
-      reinterpret_cast<float4*>(mom)[i] = mv;
-      gx = mv.x; gy = mv.y; gz = mv.z; gw = mv.w;
-    }
-    pv.x -= lr * gx; pv.y -= lr * gy; pv.z -= lr * gz; pv.w -= lr * gw;
+    pv = sgd_elem4<kMomentum>(pv, gv, mv, s, wd, lr, momentum);
+    if constexpr (kMomentum) reinterpret_cast<float4*>(mom)[i] = mv;
     reinterpret_cast<float4*>(p)[i] = pv;
     if constexpr (kShadow) {
       uint2 packed;
@@ -104,6 +121,14 @@ struct SlabRanges {
   const float* slab[kSlabRanges];               // [splits][len] fp32, len = (hi4 - lo4) * 4
   int64_t stride4[kSlabRanges];                 // float4s per split
   int splits[kSlabRanges], tpo[kSlabRanges];
+  // one "tail" range whose slabs are channel-padded (Cp > C) or have >= 32
+  // splits (the first conv layer: 3 -> 8 channels, 128 splits): reduced by
+  // extra blocks of the same launch with the stand-alone reduce's lane split
+  // (slab_reduce_each) and updated element by element
+  int tail_nblk;  // 0: none
+  int64_t tail_lo, tail_lo4, tail_hi4;  // element offset; float4 range the main blocks skip
+  const float* tail_slab;
+  int tail_splits, tail_cout, tail_taps, tail_cp, tail_c, tail_tpo;
 };
 
 template <int TPO>
@@ -164,20 +189,37 @@ __global__ void __launch_bounds__(256) sgd_slabs_kernel(float* __restrict__ p, c
                                                         const float* __restrict__ slot, float lr, float momentum,
                                                         float wd, int64_t n4, const SlabRanges r) {
   const float s = participation_scale(slot);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int nmain = (int)gridDim.x - r.tail_nblk;
+  if ((int)blockIdx.x >= nmain) {
+    auto upd = [&](int64_t i, int64_t, int, float gs) {
+      const int64_t e = r.tail_lo + i;  // KRSC weight: element i of the reduce's output order
+      float mv = kMomentum ? mom[e] : 0.f;
+      const float pv = sgd_elem<kMomentum>(p[e], gs, &mv, s, wd, lr, momentum);
+      if constexpr (kMomentum) mom[e] = mv;
+      p[e] = pv;
+      if constexpr (kShadow) p16[e] = f32_to_bf16(pv);
+    };
+    const int bid = (int)blockIdx.x - nmain;
+    if (r.tail_tpo == 32)
+      slab_reduce_each<32>(r.tail_slab, r.tail_splits, r.tail_cout, r.tail_taps, r.tail_cp, r.tail_c, bid,
+                           r.tail_nblk, upd);
+    else if (r.tail_tpo == 8)
+      slab_reduce_each<8>(r.tail_slab, r.tail_splits, r.tail_cout, r.tail_taps, r.tail_cp, r.tail_c, bid,
+                          r.tail_nblk, upd);
+    else
+      slab_reduce_each<1>(r.tail_slab, r.tail_splits, r.tail_cout, r.tail_taps, r.tail_cp, r.tail_c, bid,
+                          r.tail_nblk, upd);
+    return;
+  }
+  const int64_t stride = (int64_t)nmain * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    if (i >= r.tail_lo4 && i < r.tail_hi4) continue;  // the tail blocks update these
     float4 pv = reinterpret_cast<const float4*>(p)[i];
     const float4 gv = grad4_or_slabs(g, r, i);
-    float gx = gv.x * s + wd * pv.x, gy = gv.y * s + wd * pv.y;
-    float gz = gv.z * s + wd * pv.z, gw = gv.w * s + wd * pv.w;
-    if constexpr (kMomentum) {
-      float4 mv = reinterpret_cast<const float4*>(mom)[i];
-      mv.x = momentum * mv.x + gx; mv.y = momentum * mv.y + gy;
-      mv.z = momentum * mv.z + gz; mv.w = momentum * mv.w + gw;
-      reinterpret_cast<float4*>(mom)[i] = mv;
-      gx = mv.x; gy = mv.y; gz = mv.z; gw = mv.w;
-    }
-    pv.x -= lr * gx; pv.y -= lr * gy; pv.z -= lr * gz; pv.w -= lr * gw;
+    float4 mv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (kMomentum) mv = reinterpret_cast<const float4*>(mom)[i];
+    pv = sgd_elem4<kMomentum>(pv, gv, mv, s, wd, lr, momentum);
+    if constexpr (kMomentum) reinterpret_cast<float4*>(mom)[i] = mv;
     reinterpret_cast<float4*>(p)[i] = pv;
     if constexpr (kShadow) {
       uint2 packed;
@@ -307,7 +349,8 @@ void sgd_update(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, uintptr_
 
 void sgd_update_slabs(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, uintptr_t slot, float lr,
                       float momentum, float wd, int64_t n, std::vector<int64_t> offs, std::vector<int64_t> lens,
-                      std::vector<uintptr_t> slabs, std::vector<int> splits, uintptr_t stream) {
+                      std::vector<uintptr_t> slabs, std::vector<int> splits, std::vector<int64_t> tail,
+                      uintptr_t tail_slab, uintptr_t stream) {
   check_vec4(n, "sgd_update_slabs");
   const size_t k = offs.size();
   if (k > (size_t)kSlabRanges || lens.size() != k || slabs.size() != k || splits.size() != k)
@@ -327,9 +370,28 @@ void sgd_update_slabs(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, ui
     r.splits[j] = splits[j];
     r.tpo[j] = slab_reduce_tpo(splits[j]) == 1 ? 1 : 8;  // the stand-alone slab_reduce's lane split
   }
+  // tail = {offset, numel, splits, Cout, taps, Cp, C} or empty
+  r.tail_lo4 = r.tail_hi4 = -1;
+  if (!tail.empty()) {
+    if (tail.size() != 7) throw std::runtime_error("sgd_update_slabs: tail = (offset, numel, splits, Cout, taps, Cp, C)");
+    const int64_t off = tail[0], len = tail[1];
+    r.tail_splits = (int)tail[2]; r.tail_cout = (int)tail[3]; r.tail_taps = (int)tail[4];
+    r.tail_cp = (int)tail[5]; r.tail_c = (int)tail[6];
+    if (off % 4 || len % 4 || off < 0 || off + len > n || len != (int64_t)r.tail_cout * r.tail_taps * r.tail_c ||
+        r.tail_c > r.tail_cp || r.tail_splits < 1 || tail_slab == 0)
+      throw std::runtime_error("sgd_update_slabs: inconsistent tail range");
+    for (size_t j = 0; j < k; ++j)
+      if (offs[j] < off + len && off < offs[j] + lens[j]) throw std::runtime_error("sgd_update_slabs: tail overlaps");
+    r.tail_lo = off;
+    r.tail_lo4 = off / 4;
+    r.tail_hi4 = (off + len) / 4;
+    r.tail_slab = (const float*)tail_slab;
+    r.tail_tpo = slab_reduce_tpo(r.tail_splits);
+    r.tail_nblk = slab_reduce_grid(r.tail_splits, r.tail_cout, r.tail_taps, r.tail_c);
+  }
   const int64_t n4 = n / 4;
   if (n4 == 0) return;
-  dim3 grid(stream_grid(n4)), block(256);
+  dim3 grid(stream_grid(n4) + r.tail_nblk), block(256);
   auto s = as_stream(stream);
   float* P = (float*)p; const float* G = (const float*)g; float* M = (float*)mom; bf16_t* P16 = (bf16_t*)p16;
   const float* S = (const float*)slot;

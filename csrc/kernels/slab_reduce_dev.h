@@ -11,9 +11,13 @@
 
 namespace dl {
 
-template <int TPO, bool ACC = false, bool OIHW = false>
-__device__ __forceinline__ void slab_reduce_body(const float* __restrict__ slabs, float* __restrict__ dst, int splits,
-                                                 int Cout, int taps, int Cp, int C, int bid, int nblk) {
+// The reduction itself: f(i, rest, c, s) is called by lane sub == 0 of each
+// output i (rest = co*taps + tap) with its sum s.  Shared by the reduce
+// kernels below and by the one-node SGD that consumes the slabs directly
+// (flat_ops.hip), so both produce bitwise the same sums.
+template <int TPO, class F>
+__device__ __forceinline__ void slab_reduce_each(const float* __restrict__ slabs, int splits, int Cout, int taps,
+                                                 int Cp, int C, int bid, int nblk, F&& f) {
   const int64_t total = (int64_t)Cout * taps * C;
   const int64_t slab = (int64_t)Cout * taps * Cp;
   const int sub = threadIdx.x % TPO;
@@ -36,15 +40,21 @@ __device__ __forceinline__ void slab_reduce_body(const float* __restrict__ slabs
     for (; sp < splits; sp += TPO) s += slabs[(int64_t)sp * slab + src];
 #pragma unroll
     for (int o = TPO / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (sub == 0) {
-      int64_t o = i;
-      if constexpr (OIHW) {
-        const int64_t co = rest / taps;
-        o = (co * C + c) * taps + (rest - co * taps);
-      }
-      dst[o] = ACC ? dst[o] + s : s;
-    }
+    if (sub == 0) f(i, rest, c, s);
   }
+}
+
+template <int TPO, bool ACC = false, bool OIHW = false>
+__device__ __forceinline__ void slab_reduce_body(const float* __restrict__ slabs, float* __restrict__ dst, int splits,
+                                                 int Cout, int taps, int Cp, int C, int bid, int nblk) {
+  slab_reduce_each<TPO>(slabs, splits, Cout, taps, Cp, C, bid, nblk, [&](int64_t i, int64_t rest, int c, float s) {
+    int64_t o = i;
+    if constexpr (OIHW) {
+      const int64_t co = rest / taps;
+      o = (co * C + c) * taps + (rest - co * taps);
+    }
+    dst[o] = ACC ? dst[o] + s : s;
+  });
 }
 
 // Threads per output and grid of a slab reduction (the stand-alone launcher's rule).

@@ -1,0 +1,85 @@
+"""World > 1 overlap-policy selection (engine.py select_policy /
+agree_on_policy) on gloo: every rank measures its own
+step time per candidate policy; a step is as slow as its slowest rank, so the
+ranks agree on the policy whose MAXIMUM is smallest -- the same one on every
+rank even when the local minima disagree."""
+import pytest
+
+from tests import mp
+
+# rank -> local ms per policy: rank 0 alone would pick "full", rank 1 "reserve";
+# max over ranks: full 0.50, reserve 0.41 -> "reserve"
+TIMES = [{"full": 0.30, "reserve": 0.40}, {"full": 0.50, "reserve": 0.41}, {"full": 0.35, "reserve": 0.38},
+         {"full": 0.31, "reserve": 0.39}]
+
+
+class _FakeExecutor:
+    def __init__(self):
+        self.calls = []
+
+    def policies(self):
+        return {"full": {"dgrad_stages": 3, "cu_reserve": 0}, "reserve": {"dgrad_stages": 2, "cu_reserve": 32}}
+
+    def set_policy(self, dgrad_stages, cu_reserve):
+        self.calls.append((dgrad_stages, cu_reserve))
+
+
+def _worker(rank, world, port):
+    import torch
+
+    from torch_distlearn_amd import Tree
+    from torch_distlearn_amd.engine import DataParallelTrainer, agree_on_policy
+
+    tree = Tree(rank + 1, world, host="127.0.0.1", port=port)
+    name, table = agree_on_policy(tree.comm, TIMES[rank])
+    tr = DataParallelTrainer(torch.nn.Linear(4, 2), tree, lr=0.1)
+    ex = _FakeExecutor()
+    tr.executor, tr.graph = ex, True
+    seen = []
+
+    def fake_time(loader, reps):
+        seen.append(ex.calls[-1])
+        return TIMES[rank]["full" if ex.calls[-1][0] == 3 else "reserve"]
+
+    tr._time_step_graph = fake_time
+    pol = tr.select_policy(None)
+    again = tr.select_policy(None)  # runs once
+    return {"agree": (name, table), "policy": pol, "again": again is pol, "calls": ex.calls, "seen": seen}
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ranks_agree_on_the_fastest_slowest_rank(world):
+    res = mp.run(_worker, world)
+    want_table = {p: max(TIMES[r][p] for r in range(world)) for p in ("full", "reserve")}
+    want = min(want_table, key=want_table.get)
+    assert want == "reserve"
+    for r in res:
+        name, table = r["agree"]
+        assert name == want and table == pytest.approx(want_table)
+        pol = r["policy"]
+        assert pol["chosen"] == want and pol["ms_per_step"] == pytest.approx(want_table)
+        assert r["again"]
+        # both candidates measured (sorted order), then the winner set for good
+        assert r["seen"] == [(3, 0), (2, 32)] and r["calls"][-1] == (2, 32)
+
+
+def _forced_worker(rank, world, port):
+    import os
+
+    import torch
+
+    from torch_distlearn_amd import Tree
+    from torch_distlearn_amd.engine import DataParallelTrainer
+
+    os.environ["DISTLEARN_POLICY"] = "full"
+    tree = Tree(rank + 1, world, host="127.0.0.1", port=port)
+    tr = DataParallelTrainer(torch.nn.Linear(4, 2), tree, lr=0.1)
+    ex = _FakeExecutor()
+    tr.executor, tr.graph = ex, True
+    tr._time_step_graph = lambda loader, reps: (_ for _ in ()).throw(AssertionError("measured a forced policy"))
+    return {"policy": tr.select_policy(None), "calls": ex.calls}
+
+
+def test_forced_policy_is_not_measured():
+    for r in mp.run(_forced_worker, 2):
+        assert r["policy"]["chosen"] == "full" and r["calls"] == [(3, 0)]

@@ -388,11 +388,12 @@ def test_bf16_grad_wire_through_rccl(dev, monkeypatch):
 
 @pytest.mark.parametrize("momentum", [0.0, 0.9])
 def test_deferred_slab_reduce_is_bitwise(dev, monkeypatch, momentum):
-    """One node: the split-K weight-gradient slabs of blocks 2-3 are summed by
+    """One node: the split-K weight-gradient slabs of blocks 1-3 are summed by
     the fused SGD itself (no slab_reduce launches; engine.py _slabs) -- the
     parameters after unrolled-graph training are BITWISE those of the path with
-    the stand-alone reduce (deterministic reduction mode; batch 128: 10 splits
-    (19 splits summed on 8 lanes + a shuffle tree, 5 sequentially)."""
+    the stand-alone reduce (deterministic reduction mode; batch 128: 19 splits
+    summed on 8 lanes + a shuffle tree, 5 sequentially, and the first layer's
+    channel-padded 128 splits on 32 lanes in extra blocks of the launch)."""
     from torch_distlearn_amd import Tree
     from torch_distlearn_amd.data import DeviceLoader, PartitionedDataset, synthetic_cifar10
     from torch_distlearn_amd.engine import DataParallelTrainer
@@ -408,10 +409,10 @@ def test_deferred_slab_reduce_is_bitwise(dev, monkeypatch, momentum):
                                  compute_dtype=torch.bfloat16, graph=True, max_batch=128)
         tr.synchronize_parameters()
         if defer == "1":
-            blocks = sorted(l // 4 for l, _, _ in tr._slabs)
-            assert blocks == [1, 2], blocks
-            ks = sorted(k for _, _, k in tr._slabs)
-            assert ks[0] < 8 <= ks[1] < 32, ks  # one sequential, one 8-lane + tree
+            blocks = sorted(e[0] // 4 for e in tr._slabs)
+            assert blocks == [0, 1, 2], blocks  # block 4's wgrad has no split
+            ks = {e[0] // 4: e[2] for e in tr._slabs}
+            assert ks[2] < 8 <= ks[1] < 32 <= ks[0], ks  # sequential, 8 lanes + tree, 32 lanes (padded tail)
         else:
             assert tr._slabs is None
         ld = DeviceLoader(PartitionedDataset(imgs, labels, device=dev), "permutation", 128, seed=2)
@@ -419,3 +420,28 @@ def test_deferred_slab_reduce_is_bitwise(dev, monkeypatch, momentum):
         torch.cuda.synchronize()
         outs.append(tr.flat.data.clone())
     assert torch.equal(outs[0], outs[1])
+
+
+def test_policy_selected_on_the_machine(dev, monkeypatch):
+    """the world > 1 overlap policy is measured, not guessed.
+    Forced RCCL at world 1 with DISTLEARN_POLICY_SELECT=1: prepare() captures
+    each candidate as a one-step graph, times its replays, keeps the faster
+    (recorded with both timings), restores the training state, and the run
+    afterwards trains normally on the chosen policy."""
+    monkeypatch.setenv("DISTLEARN_RCCL_WORLD1", "1")
+    monkeypatch.setenv("DISTLEARN_POLICY_SELECT", "1")
+    tr = _trainer(dev, "hip", True, 29714)
+    ld = _loader(dev)
+    p0 = tr.flat.data.clone()
+    tr.prepare(ld, 4)
+    torch.cuda.synchronize()
+    pol = tr.policy
+    assert pol is not None and pol["chosen"] in ("full", "reserve"), pol
+    assert set(pol["ms_per_step"]) == {"full", "reserve"} and all(v > 0 for v in pol["ms_per_step"].values())
+    assert pol["chosen"] == min(pol["ms_per_step"], key=pol["ms_per_step"].get)
+    want = pol["candidates"][pol["chosen"]]
+    assert (tr.executor.dgrad_stages, tr.executor.cu_reserve) == (want["dgrad_stages"], want["cu_reserve"])
+    assert torch.equal(tr.flat.data, p0) and int(ld.ctr[0]) == 0  # selection changed no training state
+    loss = tr.run(ld, 6, unroll=4)
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).all() and int(tr.sgd.stepsPerNode.sum()) == 6

@@ -41,6 +41,20 @@ from .parallel.buckets import GradBucketer
 from .parallel.tree import Tree
 
 
+def agree_on_policy(comm, local_ms: dict) -> tuple:
+    """Pick one executor policy on every rank from each rank's measured
+    step times: a step is as slow as its slowest rank, so the times are
+    max-reduced over the ranks (control plane) and the policy with the
+    smallest maximum wins.  Collective: every rank calls it with the same
+    policy names.  Returns (name, {name: max ms})."""
+    names = sorted(local_ms)
+    t = torch.tensor([float(local_ms[n]) for n in names], dtype=torch.float64)
+    comm.all_reduce_host(t, "max")
+    table = {n: round(float(v), 4) for n, v in zip(names, t.tolist())}
+    best = min(names, key=lambda n: (table[n], n))
+    return best, table
+
+
 class DataParallelTrainer:
     def __init__(self, model: torch.nn.Module, tree: Tree, lr: float = 0.1, momentum: float = 0.0,
                  weight_decay: float = 0.0, algo: str = "sgd", tau: int = 10, alpha: float = 0.2,
@@ -120,6 +134,9 @@ class DataParallelTrainer:
                 and callable(getattr(self.executor, "defer_slab_reduce", None))
                 and os.environ.get("DISTLEARN_DEFER_SLABS", "1") == "1"):
             self._slabs = self.executor.defer_slab_reduce() or None
+        # executor policy for the world > 1 overlap (select_policy): None until chosen
+        self.policy: Optional[dict] = None
+        self._policy_done = False
         self.graph = graph
         self._graph = None
         self._static = None
@@ -293,6 +310,7 @@ class DataParallelTrainer:
         Idempotent; changes no training state."""
         if not self.graph:
             return
+        self.select_policy(loader)
         if self._graph is None:
             self._capture(loader, None)
         if not self._unrolled(unroll):
@@ -309,6 +327,69 @@ class DataParallelTrainer:
                 self._multi[k][0].replay()
             self._restore(saved, loader)
             torch.cuda.current_stream().synchronize()
+
+    def select_policy(self, loader, reps: int = 10) -> Optional[dict]:
+        """Choose the executor's overlap policy on THIS machine, before any
+        graph is captured (README "Compute / all-reduce co-residency").  With
+        world > 1 the bucketed all-reduce runs beside the backward convs and
+        RCCL's workgroups hold CUs; the candidates are the executor's
+        ``policies()`` -- full-chip grids with 3-stage dgrads vs wgrad grids
+        that leave the channel cap of CUs free with 2-stage dgrads.  Each is
+        captured as a one-step graph and replayed ``reps`` times, timed with
+        HIP events, training state restored; every rank takes the policy
+        whose slowest rank is fastest (:func:`agree_on_policy`).  Runs once;
+        ``DISTLEARN_POLICY=<name>`` forces a candidate, one node keeps the
+        executor default unless ``DISTLEARN_POLICY_SELECT=1``.  The choice
+        and both timings land in :attr:`policy` (bench.py's JSON config)."""
+        ex = self.executor
+        if self._policy_done or not self.graph or ex is None or not callable(getattr(ex, "policies", None)):
+            return self.policy
+        self._policy_done = True
+        cands = ex.policies()
+        want = os.environ.get("DISTLEARN_POLICY", "auto")
+        if want in cands:
+            self._set_policy(cands[want])
+            self.policy = {"chosen": want, "how": "forced (DISTLEARN_POLICY)"}
+            return self.policy
+        if len(cands) < 2 or (self.tree.numNodes == 1 and os.environ.get("DISTLEARN_POLICY_SELECT", "0") != "1"):
+            return self.policy
+        local = {}
+        for name, kw in sorted(cands.items()):
+            self._set_policy(kw)
+            local[name] = self._time_step_graph(loader, reps)
+        name, table = agree_on_policy(self.tree.comm, local)
+        self._set_policy(cands[name])
+        self.policy = {"chosen": name, "ms_per_step": table, "how": f"measured ({reps} graph replays per policy)",
+                       "candidates": {n: dict(kw) for n, kw in cands.items()}}
+        return self.policy
+
+    def _set_policy(self, kw: dict) -> None:
+        self.executor.set_policy(**kw)
+        if self._slabs is not None:  # the re-planned workspaces have new slabs
+            self._slabs = self.executor.defer_slab_reduce() or None
+
+    def _time_step_graph(self, loader, reps: int) -> float:
+        """ms per replay of a freshly captured one-step graph (state restored;
+        the graph is dropped)."""
+        saved = self._snapshot(loader)
+        self._capture(loader, None)
+        g = self._graph
+        g.replay()
+        torch.cuda.synchronize()
+        self.tree.comm.barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        self._track()
+        self._restore(saved, loader)
+        torch.cuda.synchronize()
+        self._graph, self._static = None, None
+        del g
+        return ms
 
     def _snapshot(self, loader=None):
         return (self.flat.data.clone(), None if self.mom is None else self.mom.clone(),

@@ -635,20 +635,49 @@ class CifarHIPExecutor:
             main.wait_stream(side)  # join
         return self.loss[0]
 
+    def policies(self) -> dict:
+        """Candidate overlap policies for DataParallelTrainer.select_policy
+        (world > 1): "full" = full-chip grids and 3-stage dgrads (fastest when
+        nothing else holds a CU), "reserve" = 2-stage dgrads and wgrad grids
+        that leave the RCCL channel cap of CUs free (what the single-CU
+        emulation favoured).  Empty when DISTLEARN_DGRAD_STAGES /
+        DISTLEARN_CU_RESERVE pin the policy."""
+        if "DISTLEARN_DGRAD_STAGES" in os.environ or "DISTLEARN_CU_RESERVE" in os.environ:
+            return {}
+        from ..parallel.comm import rccl_channel_cap
+
+        comm = getattr(self.bucketer, "comm", None)
+        cap = getattr(comm, "cu_reserve", 0) or rccl_channel_cap()
+        return {"full": {"dgrad_stages": 3, "cu_reserve": 0}, "reserve": {"dgrad_stages": 2, "cu_reserve": int(cap)}}
+
+    def set_policy(self, dgrad_stages: int, cu_reserve: int) -> None:
+        """Switch the overlap policy (re-plans the weight-gradient grids and
+        re-allocates the workspaces: graphs captured before are invalid, and
+        a trainer that deferred the slab reduces calls defer_slab_reduce
+        again for the new slabs)."""
+        self.dgrad_stages, self.cu_reserve = int(dgrad_stages), int(cu_reserve)
+        self._alloc(self.B)
+        self._deferred = ()
+
     def defer_slab_reduce(self):
-        """Leave the split-K weight gradients of the blocks whose slabs the
-        fused SGD can read in place (slab layout == weight layout: no channel
-        padding; < 32 splits) in their slabs: the slab_reduce launches are
-        skipped and the update sums the slabs (flat.py flat_sgd_ ``slabs``,
-        bitwise the same sum).  Only for a trainer that all-reduces nothing
-        (one node): the flat gradient of those weights is then never written.
-        Returns [(leaf, slab, splits)] for the update."""
+        """Leave every split-K weight gradient in its slabs: the slab_reduce
+        launches are skipped and the fused SGD sums the slabs itself -- in
+        place where the slab layout is the weight's (no channel padding, < 32
+        splits), and the first layer's channel-padded 128-way slabs in extra
+        blocks of the same launch (flat.py flat_sgd_ ``slabs``; bitwise the
+        same sums).  Only for a trainer that all-reduces nothing (one node):
+        the flat gradient of those weights is then never written.
+        Returns [(leaf, slab, splits, Cout, taps, Cp, C)] for the update."""
         if self.mode == 1 or self.side_wgrad or self.side_reduce or self.merge_slab:
             return []
-        blocks = [i for i in range(self.nb)
-                  if not self.wplan[i][2] and self.cins[i] == self.cins_real[i] and self.wplan[i][1] < 32]
+        taps = KSIZE * KSIZE
+        blocks = [i for i in range(self.nb) if not self.wplan[i][2]]
+        padded = [i for i in blocks if not (self.cins[i] == self.cins_real[i] and self.wplan[i][1] < 32)]
+        if len(padded) > 1:  # the update reduces at most one such range
+            blocks = [i for i in blocks if i not in padded[1:]]
         self._deferred = tuple(blocks)
-        return [(self._leaf(i, 0), self.wslab_l[i], self.wplan[i][1]) for i in blocks]
+        return [(self._leaf(i, 0), self.wslab_l[i], self.wplan[i][1], self.couts[i], taps, self.cins[i],
+                 self.cins_real[i]) for i in blocks]
 
     def _region_dgrad(self, i: int, B: int) -> bool:
         """Whether block i's (unsplit) dgrad runs on the region (tap-reuse)

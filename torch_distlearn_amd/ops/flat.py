@@ -178,20 +178,27 @@ def _scale_from_slot(slot):
 
 def sgd_update_(p: torch.Tensor, g: torch.Tensor, lr: float, slot: torch.Tensor | None = None,
                 mom: torch.Tensor | None = None, momentum: float = 0.0, weight_decay: float = 0.0,
-                shadow: torch.Tensor | None = None, slabs=None) -> None:
+                shadow: torch.Tensor | None = None, slabs=None, tail=None) -> None:
     """p -= lr * (g/n + wd*p) [with momentum buffer]; n from ``slot`` (device).
     ``g`` is fp32, or bf16 (the all-reduced wire copy of grad_comm_dtype="bf16").
     ``slabs``: [(offset into p, numel, slab tensor [splits * numel], splits)]:
     in those ranges the gradient is the sum of the split-K slabs instead of
     ``g`` (one GPU: the conv executor's deferred slab reduce; bitwise the
-    stand-alone reduce's sum)."""
-    if slabs:
+    stand-alone reduce's sum).  ``tail``: one channel-padded range
+    (offset, numel, slab tensor, splits, Cout, taps, Cp, C) reduced by extra
+    blocks of the same launch."""
+    if slabs or tail is not None:
         if not p.is_cuda or g.dtype != torch.float32:
             raise ValueError("sgd_update_: slab gradients need an fp32 gradient on the GPU")
+        slabs = slabs or []
+        tl, tptr = [], 0
+        if tail is not None:
+            o, n, t, k, cout, taps, cp, c = tail
+            tl, tptr = [int(o), int(n), int(k), int(cout), int(taps), int(cp), int(c)], t.data_ptr()
         native().sgd_update_slabs(p.data_ptr(), g.data_ptr(), _ptr(mom), _ptr(shadow), _ptr(slot), float(lr),
                                   float(momentum), float(weight_decay), p.numel(), [int(o) for o, _, _, _ in slabs],
                                   [int(n) for _, n, _, _ in slabs], [t.data_ptr() for _, _, t, _ in slabs],
-                                  [int(k) for _, _, _, k in slabs], stream_handle())
+                                  [int(k) for _, _, _, k in slabs], tl, tptr, stream_handle())
         return
     if p.is_cuda:
         fn = native().sgd_update_g16 if g.dtype == torch.bfloat16 else native().sgd_update
@@ -224,16 +231,29 @@ def flat_sgd_(flat: "FlatParams", lr: float, slot: torch.Tensor | None = None, m
     header (whose gradient element is the participation count) is left out,
     so ``n`` never flows into the parameter buffer.  ``grad``: the gradient
     buffer to read (default ``flat.grad``; ``flat.grad16`` for bf16 comm).
-    ``slabs``: [(leaf index, slab tensor, splits)] whose gradient is still in
-    split-K slabs (see :func:`sgd_update_`)."""
+    ``slabs``: [(leaf index, slab tensor, splits, Cout, taps, Cp, C)] whose
+    gradient is still in split-K slabs [splits][Cout][taps][Cp] (see
+    :func:`sgd_update_`): unpadded ones (Cp == C) with < 32 splits are read
+    in place, at most one other is reduced by extra blocks of the launch."""
     H = HEADER
     g = flat.grad if grad is None else grad
-    rng = None
+    rng, tail = None, None
     if slabs:
-        rng = sorted((flat.offsets[i] - H, flat.numels[i], t, k) for i, t, k in slabs)
+        rng = []
+        for i, t, k, cout, taps, cp, c in slabs:
+            off, n = flat.offsets[i] - H, flat.numels[i]
+            if n != cout * taps * c:
+                raise ValueError("flat_sgd_: slab layout does not match the leaf")
+            if cp == c and k < 32:
+                rng.append((off, n, t, k))
+            elif tail is None:
+                tail = (off, n, t, k, cout, taps, cp, c)
+            else:
+                raise ValueError("flat_sgd_: at most one channel-padded slab range")
+        rng.sort(key=lambda r: r[0])
     sgd_update_(flat.data[H:], g[H:], lr, slot=slot, mom=None if mom is None else mom[H:],
                 momentum=momentum, weight_decay=weight_decay,
-                shadow=None if flat.shadow is None else flat.shadow[H:], slabs=rng)
+                shadow=None if flat.shadow is None else flat.shadow[H:], slabs=rng, tail=tail)
 
 
 def scale_by_count_(x: torch.Tensor, slot: torch.Tensor) -> None:
