@@ -18,16 +18,22 @@ void add_inplace(uintptr_t y, uintptr_t x, int64_t n, uintptr_t stream);
 void fill_f32(uintptr_t x, float v, int64_t n, int64_t slot_index, float slot_value, uintptr_t stream);
 void cast_f32_bf16(uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream);
 void cast_bf16_f32(uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream);
+// the next streaming conv_fwd launch also runs the SGD of flat elements [lo, hi)
+// as nblk extra workgroups (conv_igemm.hip; flat_ops' update then skips them)
+void set_conv_side_sgd(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, uintptr_t slot, float lr,
+                       float momentum, float wd, int64_t lo, int64_t hi, std::vector<int64_t> offs,
+                       std::vector<int64_t> lens, std::vector<uintptr_t> slabs, std::vector<int> splits, int nblk);
 void sgd_update_g16(uintptr_t p, uintptr_t g16, uintptr_t mom, uintptr_t p16, uintptr_t slot, float lr,
                     float momentum, float wd, int64_t n, uintptr_t stream);
 // sgd_update whose gradient in up to 4 ranges [offs, offs+lens) is the sum of the
 // split-K slabs [splits][lens] at slabs[j], and in one optional channel-padded
 // "tail" range (offset, numel, splits, Cout, taps, Cp, C) the sum of tail_slab
-// (bitwise slab_reduce's sums)
+// (bitwise slab_reduce's sums); elements [skip_lo, skip_hi) are left alone (a
+// conv launch's side job updated them: set_conv_side_sgd)
 void sgd_update_slabs(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, uintptr_t slot, float lr,
                       float momentum, float wd, int64_t n, std::vector<int64_t> offs, std::vector<int64_t> lens,
                       std::vector<uintptr_t> slabs, std::vector<int> splits, std::vector<int64_t> tail,
-                      uintptr_t tail_slab, uintptr_t stream);
+                      uintptr_t tail_slab, int64_t skip_lo, int64_t skip_hi, uintptr_t stream);
 
 // metrics.hip ---------------------------------------------------------------
 // channels-last training BatchNorm (+ReLU, +residual) for the ResNet-50 path

@@ -27,6 +27,7 @@
 #include "dl_common.h"
 #include "dl_ops.h"
 #include "slab_reduce_dev.h"
+#include "sgd_dev.h"
 #include "wtrans_dev.h"
 
 #include <algorithm>
@@ -673,7 +674,16 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
                                                        bf16_t* __restrict__ y, float* __restrict__ stats,
                                                        float* __restrict__ slab, const ConvGeom g, int splits,
                                                        int kt_per_split, unsigned long long* dbg,
-                                                       const BnRedArgs br = BnRedArgs{}) {
+                                                       const BnRedArgs br = BnRedArgs{},
+                                                       const SgdJob side = SgdJob{}) {
+  // side job (set_conv_side_sgd): the last side.nblk workgroups run part of
+  // the step's SGD update on the CUs the convolution's one-workgroup-per-CU
+  // grid leaves free (its gradients are final by the time this conv runs)
+  const int conv_grid = (int)gridDim.x - side.nblk;
+  if ((int)blockIdx.x >= conv_grid) {
+    sgd_side_block(side, (int)blockIdx.x - conv_grid);
+    return;
+  }
   // x is the SPATIALLY ZERO-PADDED input [B][Hp][Wp][Cin]: every tap of every
   // output pixel is in bounds, so an activation load is (per-lane pixel base)
   // + (wave-uniform tap offset) with no bounds test.  Cout % BN == 0
@@ -704,7 +714,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   if (TAPU && g.posm && g.pm_kmax > 0) {
     // balanced position-major split-K: N tile tn owns pm_P workgroups; pixel
     // pos gets nbt * nsp(pos) of them, nsp(pos) = ceil(nk(pos) / pm_kmax)
-    const int id = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int id = xcd_swizzle(blockIdx.x, conv_grid);
     const int nbt = g.B / BM;
     tn = id / g.pm_P;
     int r = id - tn * g.pm_P, pos = 0, nsp = 1;
@@ -2173,6 +2183,7 @@ int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile,
   return (g.M + rpb - 1) / rpb;
 }
 
+static SgdJob g_side_sgd{};         // set_conv_side_sgd: side SGD job of the next conv_fwd launch
 static uintptr_t g_fwd_addend = 0;  // conv_fwd_add: bf16 [M][Cout] added in the epilogue
 static int g_fwd_slab_cap = 0;      // split-K slab capacity of the current conv_fwd call (FwdCfg)
 static int g_fwd_keep_slabs = 0;    // FwdCfg bit 20: leave the split-K slabs (the caller combines them)
@@ -2236,7 +2247,12 @@ static void launch_fwd_w(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uin
   plan_posm_balance(g, BM, ntn, splits, g_fwd_slab_cap);
   const int nkt = (g.Kch + 7) / 8;
   const int ktps = (nkt + splits - 1) / splits;
-  const int grid = g.pm_kmax > 0 ? ntn * g.pm_P : ntm * ntn * splits;
+  SgdJob side = g_side_sgd;  // one-shot: consumed by this launch
+  g_side_sgd.nblk = 0;
+  constexpr int kNT = 64 * WM * WN;
+  if (side.nblk < 0)  // auto: one float4 per thread (2048 x 512 measured best of 256..2048 workgroups)
+    side.nblk = (int)std::max<int64_t>(1, (side.hi4 - side.lo4 + kNT - 1) / kNT);
+  const int grid = (g.pm_kmax > 0 ? ntn * g.pm_P : ntm * ntn * splits) + side.nblk;
   constexpr int NT = 64 * WM * WN;
   constexpr bool kTR = (BN / WN / 16) % 2 == 0;
   g.swave = (g_fwd_swave_req && stats && splits == 1 && !g_red_atomic_host && g_fwd_tr && kTR && !g.posm) ? 1 : 0;
@@ -2250,31 +2266,31 @@ static void launch_fwd_w(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uin
       if (g_fwd_addend)
         conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, true, true, 3><<<grid, NT, 0, s>>>(
             (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, (float*)g_fwd_addend, g, 1, ktps, g_conv_dbg,
-            g_bnred2);
+            g_bnred2, side);
       else
         conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, false, true, 2><<<grid, NT, 0, s>>>(
-            (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, nullptr, g, 1, ktps, g_conv_dbg, g_bnred2);
+            (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, nullptr, g, 1, ktps, g_conv_dbg, g_bnred2, side);
     } else {
       throw std::runtime_error("conv BN reduce: tile without the transposed epilogue");
     }
   } else if (g_fwd_addend)
     conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, true><<<grid, NT, 0, s>>>(
-        (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, (float*)g_fwd_addend, g, 1, ktps, g_conv_dbg);
+        (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, (float*)g_fwd_addend, g, 1, ktps, g_conv_dbg, BnRedArgs{}, side);
   else if (splits > 1 && !g_fwd_tr)
     conv_fwd_kernel<BM, BN, false, true, TAPU, ST, WM, WN, false, false><<<grid, NT, 0, s>>>(
-        (const bf16_t*)x, (const bf16_t*)w, nullptr, nullptr, (float*)slab, g, splits, ktps, g_conv_dbg);
+        (const bf16_t*)x, (const bf16_t*)w, nullptr, nullptr, (float*)slab, g, splits, ktps, g_conv_dbg, BnRedArgs{}, side);
   else if (splits > 1)
     conv_fwd_kernel<BM, BN, false, true, TAPU, ST, WM, WN><<<grid, NT, 0, s>>>(
-        (const bf16_t*)x, (const bf16_t*)w, nullptr, nullptr, (float*)slab, g, splits, ktps, g_conv_dbg);
+        (const bf16_t*)x, (const bf16_t*)w, nullptr, nullptr, (float*)slab, g, splits, ktps, g_conv_dbg, BnRedArgs{}, side);
   else if (stats && !g_fwd_tr)
     conv_fwd_kernel<BM, BN, true, false, TAPU, ST, WM, WN, false, false><<<grid, NT, 0, s>>>(
-        (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)stats, nullptr, g, 1, ktps, g_conv_dbg);
+        (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)stats, nullptr, g, 1, ktps, g_conv_dbg, BnRedArgs{}, side);
   else if (stats)
     conv_fwd_kernel<BM, BN, true, false, TAPU, ST, WM, WN><<<grid, NT, 0, s>>>(
-        (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)stats, nullptr, g, 1, ktps, g_conv_dbg);
+        (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)stats, nullptr, g, 1, ktps, g_conv_dbg, BnRedArgs{}, side);
   else
     conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN><<<grid, NT, 0, s>>>(
-        (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, nullptr, g, 1, ktps, g_conv_dbg);
+        (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, nullptr, g, 1, ktps, g_conv_dbg, BnRedArgs{}, side);
 }
 
 static int g_fwd_waves = 8;
@@ -2555,6 +2571,10 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
   else if (tile == 2) launch_fwd<128, 64>(g, x, w, y, stats, slab, splits, s);
   else throw std::runtime_error("conv_fwd: bad tile id");
   DL_HIP_CHECK(hipGetLastError());
+  if (g_side_sgd.nblk != 0) {  // armed, but this call ran on the region / c8 kernel
+    g_side_sgd.nblk = 0;
+    throw std::runtime_error("set_conv_side_sgd: the next conv_fwd call must run on the streaming kernel");
+  }
   if (splits == 1) return (g.M + fwd_bm(tile) - 1) / fwd_bm(tile) * g_stat_rows_mult;
   if (g_fwd_keep_slabs) {
     if (stats || g.pm_kmax > 0) throw std::runtime_error("conv_fwd keep-slabs: no statistics / balanced split-K");
@@ -2571,6 +2591,19 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
                                                     g);
   DL_HIP_CHECK(hipGetLastError());
   return nb;
+}
+
+// The next streaming conv_fwd launch also runs the fused SGD update of the
+// elements [lo, hi) of the flat buffer p (gradient g, or the split-K slabs of
+// the given ranges; bf16 shadow p16 required) as nblk extra workgroups
+// (0: one float4 per thread).  One-shot; the caller's final update skips [lo, hi).
+void set_conv_side_sgd(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, uintptr_t slot, float lr,
+                       float momentum, float wd, int64_t lo, int64_t hi, std::vector<int64_t> offs,
+                       std::vector<int64_t> lens, std::vector<uintptr_t> slabs, std::vector<int> splits, int nblk) {
+  if (!p16) throw std::runtime_error("set_conv_side_sgd: needs the bf16 shadow");
+  SgdJob j = make_sgd_job(p, g, mom, p16, slot, lr, momentum, wd, lo, hi, offs, lens, slabs, splits, {}, 0);
+  j.nblk = nblk > 0 ? nblk : -1;  // -1: sized by the launch (one float4 per thread)
+  g_side_sgd = j;
 }
 
 // Arm (rows != 0) / disarm (rows == 0) the channels-last BatchNorm backward

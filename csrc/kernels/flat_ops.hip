@@ -14,58 +14,17 @@
 #include <vector>
 
 #include "dl_common.h"
-#include "slab_reduce_dev.h"
+#include "sgd_dev.h"
 
 namespace dl {
 
 // ---------------------------------------------------------------------------
 // helpers
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float participation_scale(const float* slot) {
-  if (slot == nullptr) return 1.0f;
-  float n = *slot;
-  return n > 1.0f ? 1.0f / n : 1.0f;  // reference: only divide when n > 1
-}
-
 // ---------------------------------------------------------------------------
 // SGD (+ optional momentum / weight decay), fused with 1/n normalisation and
 // the bf16 shadow-weight refresh used by the bf16 compute path.
 // ---------------------------------------------------------------------------
-// G16: the gradient is the bf16 all-reduced wire copy (grad_comm_dtype="bf16":
-// half the xGMI bytes; read here directly, never widened back to fp32).
-__device__ __forceinline__ float4 load_grad4(const float* g, int64_t i) {
-  return reinterpret_cast<const float4*>(g)[i];
-}
-__device__ __forceinline__ float4 load_grad4(const bf16_t* g, int64_t i) {
-  const uint2 u = reinterpret_cast<const uint2*>(g)[i];
-  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
-                     __uint_as_float(u.y & 0xffff0000u));
-}
-
-// One element of the fused update, with every rounding step explicit (fma
-// contraction left to the compiler differs between the float4 and the scalar
-// code paths; the slab-consuming update must match this kernel bit for bit).
-template <bool kMomentum>
-__device__ __forceinline__ float sgd_elem(float p, float g, float* m, float s, float wd, float lr, float momentum) {
-  float gx = __builtin_fmaf(g, s, wd * p);
-  if constexpr (kMomentum) {
-    const float mv = __builtin_fmaf(momentum, *m, gx);
-    *m = mv;
-    gx = mv;
-  }
-  return __builtin_fmaf(-lr, gx, p);
-}
-
-template <bool kMomentum>
-__device__ __forceinline__ float4 sgd_elem4(float4 p, const float4 g, float4& m, float s, float wd, float lr,
-                                            float momentum) {
-  p.x = sgd_elem<kMomentum>(p.x, g.x, &m.x, s, wd, lr, momentum);
-  p.y = sgd_elem<kMomentum>(p.y, g.y, &m.y, s, wd, lr, momentum);
-  p.z = sgd_elem<kMomentum>(p.z, g.z, &m.z, s, wd, lr, momentum);
-  p.w = sgd_elem<kMomentum>(p.w, g.w, &m.w, s, wd, lr, momentum);
-  return p;
-}
-
 template <bool kMomentum, bool kShadow, typename GT = float>
 __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, const GT* __restrict__ g,
                                                   float* __restrict__ mom, bf16_t* __restrict__ p16,
@@ -105,129 +64,14 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, const G
   }
 }
 
-// ---------------------------------------------------------------------------
-// SGD whose gradient for some ranges still lies in split-K weight-gradient
-// slabs (one GPU, nothing to all-reduce: the conv executor skips the slab
-// reduce launches and the update sums the slabs itself).  The sum per element
-// is bitwise the one slab_reduce_body<TPO> computes (slab_reduce_dev.h):
-// TPO lanes each add a strided subset of the splits in split order, then a
-// xor-shuffle tree -- so deferring the reduce changes no bit of the update.
-// ---------------------------------------------------------------------------
-constexpr int kSlabRanges = 4;
-constexpr int kSlabMaxSplits = 31;  // the stand-alone reduce uses 1 or 8 lanes per output up to here
-struct SlabRanges {
-  int n;
-  int64_t lo4[kSlabRanges], hi4[kSlabRanges];  // float4 index range in the updated buffer
-  const float* slab[kSlabRanges];               // [splits][len] fp32, len = (hi4 - lo4) * 4
-  int64_t stride4[kSlabRanges];                 // float4s per split
-  int splits[kSlabRanges], tpo[kSlabRanges];
-  // one "tail" range whose slabs are channel-padded (Cp > C) or have >= 32
-  // splits (the first conv layer: 3 -> 8 channels, 128 splits): reduced by
-  // extra blocks of the same launch with the stand-alone reduce's lane split
-  // (slab_reduce_each) and updated element by element
-  int tail_nblk;  // 0: none
-  int64_t tail_lo, tail_lo4, tail_hi4;  // element offset; float4 range the main blocks skip
-  const float* tail_slab;
-  int tail_splits, tail_cout, tail_taps, tail_cp, tail_c, tail_tpo;
-};
-
-template <int TPO>
-__device__ __forceinline__ void add4(float4 (&part)[TPO], int t, const float4& v) {
-  // t is a compile-time constant after unrolling (no dynamic register indexing)
-  float4& q = part[t];
-  q.x += v.x; q.y += v.y; q.z += v.z; q.w += v.w;
-}
-
-template <int TPO>
-__device__ __forceinline__ float4 slab_sum4(const float4* __restrict__ s, int64_t stride4, int splits) {
-  float4 part[TPO];
-#pragma unroll
-  for (int t = 0; t < TPO; ++t) part[t] = make_float4(0.f, 0.f, 0.f, 0.f);
-  // chunks of 4 splits, the chunk's loads in flight before its adds; lane t of
-  // the stand-alone reduce adds splits t, t+TPO, ... in order: same here
-  for (int sp0 = 0; sp0 < splits; sp0 += 4) {
-    float4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (sp0 + u < splits) v[u] = s[(int64_t)(sp0 + u) * stride4];
-    const bool hi = TPO == 8 && (sp0 & 4);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (sp0 + u >= splits) break;
-      if constexpr (TPO == 1) add4<TPO>(part, 0, v[u]);
-      else if (hi) add4<TPO>(part, 4 + u, v[u]);
-      else add4<TPO>(part, u, v[u]);
-    }
-  }
-#pragma unroll
-  for (int o = TPO / 2; o > 0; o >>= 1) {
-    float4 np[TPO];
-#pragma unroll
-    for (int t = 0; t < TPO; ++t) {
-      const float4 a = part[t], b = part[t ^ o];
-      np[t] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
-    }
-#pragma unroll
-    for (int t = 0; t < TPO; ++t) part[t] = np[t];
-  }
-  return part[0];
-}
-
-__device__ __forceinline__ float4 grad4_or_slabs(const float* __restrict__ g, const SlabRanges& r, int64_t i) {
-  for (int k = 0; k < r.n; ++k) {
-    if (i >= r.lo4[k] && i < r.hi4[k]) {
-      const float4* s = reinterpret_cast<const float4*>(r.slab[k]) + (i - r.lo4[k]);
-      return r.tpo[k] == 8 ? slab_sum4<8>(s, r.stride4[k], r.splits[k]) : slab_sum4<1>(s, r.stride4[k], r.splits[k]);
-    }
-  }
-  return load_grad4(g, i);
-}
-
 template <bool kMomentum, bool kShadow>
-__global__ void __launch_bounds__(256) sgd_slabs_kernel(float* __restrict__ p, const float* __restrict__ g,
-                                                        float* __restrict__ mom, bf16_t* __restrict__ p16,
-                                                        const float* __restrict__ slot, float lr, float momentum,
-                                                        float wd, int64_t n4, const SlabRanges r) {
-  const float s = participation_scale(slot);
-  const int nmain = (int)gridDim.x - r.tail_nblk;
+__global__ void __launch_bounds__(256) sgd_slabs_kernel(const SgdJob job) {
+  const int nmain = (int)gridDim.x - job.r.tail_nblk;
   if ((int)blockIdx.x >= nmain) {
-    auto upd = [&](int64_t i, int64_t, int, float gs) {
-      const int64_t e = r.tail_lo + i;  // KRSC weight: element i of the reduce's output order
-      float mv = kMomentum ? mom[e] : 0.f;
-      const float pv = sgd_elem<kMomentum>(p[e], gs, &mv, s, wd, lr, momentum);
-      if constexpr (kMomentum) mom[e] = mv;
-      p[e] = pv;
-      if constexpr (kShadow) p16[e] = f32_to_bf16(pv);
-    };
-    const int bid = (int)blockIdx.x - nmain;
-    if (r.tail_tpo == 32)
-      slab_reduce_each<32>(r.tail_slab, r.tail_splits, r.tail_cout, r.tail_taps, r.tail_cp, r.tail_c, bid,
-                           r.tail_nblk, upd);
-    else if (r.tail_tpo == 8)
-      slab_reduce_each<8>(r.tail_slab, r.tail_splits, r.tail_cout, r.tail_taps, r.tail_cp, r.tail_c, bid,
-                          r.tail_nblk, upd);
-    else
-      slab_reduce_each<1>(r.tail_slab, r.tail_splits, r.tail_cout, r.tail_taps, r.tail_cp, r.tail_c, bid,
-                          r.tail_nblk, upd);
+    sgd_tail_block<kMomentum, kShadow>(job, (int)blockIdx.x - nmain);
     return;
   }
-  const int64_t stride = (int64_t)nmain * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    if (i >= r.tail_lo4 && i < r.tail_hi4) continue;  // the tail blocks update these
-    float4 pv = reinterpret_cast<const float4*>(p)[i];
-    const float4 gv = grad4_or_slabs(g, r, i);
-    float4 mv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (kMomentum) mv = reinterpret_cast<const float4*>(mom)[i];
-    pv = sgd_elem4<kMomentum>(pv, gv, mv, s, wd, lr, momentum);
-    if constexpr (kMomentum) reinterpret_cast<float4*>(mom)[i] = mv;
-    reinterpret_cast<float4*>(p)[i] = pv;
-    if constexpr (kShadow) {
-      uint2 packed;
-      packed.x = pack_bf16x2(pv.x, pv.y);
-      packed.y = pack_bf16x2(pv.z, pv.w);
-      reinterpret_cast<uint2*>(p16)[i] = packed;
-    }
-  }
+  sgd_range_loop<kMomentum, kShadow>(job, (int)blockIdx.x, nmain);
 }
 
 // x *= 1/n (n read from the all-reduced participation slot)
@@ -350,55 +194,22 @@ void sgd_update(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, uintptr_
 void sgd_update_slabs(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, uintptr_t slot, float lr,
                       float momentum, float wd, int64_t n, std::vector<int64_t> offs, std::vector<int64_t> lens,
                       std::vector<uintptr_t> slabs, std::vector<int> splits, std::vector<int64_t> tail,
-                      uintptr_t tail_slab, uintptr_t stream) {
+                      uintptr_t tail_slab, int64_t skip_lo, int64_t skip_hi, uintptr_t stream) {
   check_vec4(n, "sgd_update_slabs");
-  const size_t k = offs.size();
-  if (k > (size_t)kSlabRanges || lens.size() != k || slabs.size() != k || splits.size() != k)
-    throw std::runtime_error("sgd_update_slabs: up to 4 consistent slab ranges");
-  SlabRanges r{};
-  r.n = (int)k;
-  for (size_t j = 0; j < k; ++j) {
-    if (offs[j] % 4 || lens[j] % 4 || offs[j] < 0 || offs[j] + lens[j] > n || slabs[j] % 16)
-      throw std::runtime_error("sgd_update_slabs: ranges must be 16-byte aligned and inside the buffer");
-    if (splits[j] < 1 || splits[j] > kSlabMaxSplits)
-      throw std::runtime_error("sgd_update_slabs: 1..31 splits per range");
-    if (j > 0 && offs[j] < offs[j - 1] + lens[j - 1]) throw std::runtime_error("sgd_update_slabs: ranges overlap");
-    r.lo4[j] = offs[j] / 4;
-    r.hi4[j] = (offs[j] + lens[j]) / 4;
-    r.slab[j] = (const float*)slabs[j];
-    r.stride4[j] = lens[j] / 4;
-    r.splits[j] = splits[j];
-    r.tpo[j] = slab_reduce_tpo(splits[j]) == 1 ? 1 : 8;  // the stand-alone slab_reduce's lane split
-  }
-  // tail = {offset, numel, splits, Cout, taps, Cp, C} or empty
-  r.tail_lo4 = r.tail_hi4 = -1;
-  if (!tail.empty()) {
-    if (tail.size() != 7) throw std::runtime_error("sgd_update_slabs: tail = (offset, numel, splits, Cout, taps, Cp, C)");
-    const int64_t off = tail[0], len = tail[1];
-    r.tail_splits = (int)tail[2]; r.tail_cout = (int)tail[3]; r.tail_taps = (int)tail[4];
-    r.tail_cp = (int)tail[5]; r.tail_c = (int)tail[6];
-    if (off % 4 || len % 4 || off < 0 || off + len > n || len != (int64_t)r.tail_cout * r.tail_taps * r.tail_c ||
-        r.tail_c > r.tail_cp || r.tail_splits < 1 || tail_slab == 0)
-      throw std::runtime_error("sgd_update_slabs: inconsistent tail range");
-    for (size_t j = 0; j < k; ++j)
-      if (offs[j] < off + len && off < offs[j] + lens[j]) throw std::runtime_error("sgd_update_slabs: tail overlaps");
-    r.tail_lo = off;
-    r.tail_lo4 = off / 4;
-    r.tail_hi4 = (off + len) / 4;
-    r.tail_slab = (const float*)tail_slab;
-    r.tail_tpo = slab_reduce_tpo(r.tail_splits);
-    r.tail_nblk = slab_reduce_grid(r.tail_splits, r.tail_cout, r.tail_taps, r.tail_c);
+  SgdJob job = make_sgd_job(p, g, mom, p16, slot, lr, momentum, wd, 0, n, offs, lens, slabs, splits, tail, tail_slab);
+  if (skip_hi > skip_lo) {
+    if (skip_lo % 4 || skip_hi % 4 || skip_lo < 0 || skip_hi > n) throw std::runtime_error("sgd_update_slabs: bad skip");
+    job.skip_lo4 = skip_lo / 4;
+    job.skip_hi4 = skip_hi / 4;
   }
   const int64_t n4 = n / 4;
   if (n4 == 0) return;
-  dim3 grid(stream_grid(n4) + r.tail_nblk), block(256);
+  dim3 grid(stream_grid(n4) + job.r.tail_nblk), block(256);
   auto s = as_stream(stream);
-  float* P = (float*)p; const float* G = (const float*)g; float* M = (float*)mom; bf16_t* P16 = (bf16_t*)p16;
-  const float* S = (const float*)slot;
-  if (mom && p16) sgd_slabs_kernel<true, true><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4, r);
-  else if (mom) sgd_slabs_kernel<true, false><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4, r);
-  else if (p16) sgd_slabs_kernel<false, true><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4, r);
-  else sgd_slabs_kernel<false, false><<<grid, block, 0, s>>>(P, G, M, P16, S, lr, momentum, wd, n4, r);
+  if (mom && p16) sgd_slabs_kernel<true, true><<<grid, block, 0, s>>>(job);
+  else if (mom) sgd_slabs_kernel<true, false><<<grid, block, 0, s>>>(job);
+  else if (p16) sgd_slabs_kernel<false, true><<<grid, block, 0, s>>>(job);
+  else sgd_slabs_kernel<false, false><<<grid, block, 0, s>>>(job);
   DL_HIP_CHECK(hipGetLastError());
 }
 

@@ -393,7 +393,9 @@ def test_deferred_slab_reduce_is_bitwise(dev, monkeypatch, momentum):
     parameters after unrolled-graph training are BITWISE those of the path with
     the stand-alone reduce (deterministic reduction mode; batch 128: 19 splits
     summed on 8 lanes + a shuffle tree, 5 sequentially, and the first layer's
-    channel-padded 128 splits on 32 lanes in extra blocks of the launch)."""
+    channel-padded 128 splits on 32 lanes in extra blocks of the launch);
+    with the side job, blocks 3-4 and the classifier are updated by extra
+    workgroups of block 3's dgrad launch -- still bitwise the same."""
     from torch_distlearn_amd import Tree
     from torch_distlearn_amd.data import DeviceLoader, PartitionedDataset, synthetic_cifar10
     from torch_distlearn_amd.engine import DataParallelTrainer
@@ -401,8 +403,9 @@ def test_deferred_slab_reduce_is_bitwise(dev, monkeypatch, momentum):
 
     imgs, labels = synthetic_cifar10(1024, seed=5)
     outs = []
-    for defer in ("0", "1"):
+    for defer, side in (("0", "0"), ("1", "0"), ("1", "1")):
         monkeypatch.setenv("DISTLEARN_DEFER_SLABS", defer)
+        monkeypatch.setenv("DISTLEARN_SIDE_SGD", side)
         tree = Tree(1, 1, host="127.0.0.1", port=29712, device=dev)
         model = CifarConvNet(seed=4).to(dev)
         tr = DataParallelTrainer(model, tree, lr=0.02, momentum=momentum, backend="hip",
@@ -413,13 +416,17 @@ def test_deferred_slab_reduce_is_bitwise(dev, monkeypatch, momentum):
             assert blocks == [0, 1, 2], blocks  # block 4's wgrad has no split
             ks = {e[0] // 4: e[2] for e in tr._slabs}
             assert ks[2] < 8 <= ks[1] < 32 <= ks[0], ks  # sequential, 8 lanes + tree, 32 lanes (padded tail)
+            # side == "1": blocks 3-4 + classifier updated inside block 3's dgrad launch
+            assert (tr._side is not None) == (side == "1")
+            if side == "1":
+                assert tr._side == (tr.flat.offsets[8], tr.flat.total)
         else:
-            assert tr._slabs is None
+            assert tr._slabs is None and tr._side is None
         ld = DeviceLoader(PartitionedDataset(imgs, labels, device=dev), "permutation", 128, seed=2)
         tr.run(ld, 7, unroll=4)
         torch.cuda.synchronize()
         outs.append(tr.flat.data.clone())
-    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
 
 def test_policy_selected_on_the_machine(dev, monkeypatch):

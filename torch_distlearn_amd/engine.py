@@ -134,6 +134,8 @@ class DataParallelTrainer:
                 and callable(getattr(self.executor, "defer_slab_reduce", None))
                 and os.environ.get("DISTLEARN_DEFER_SLABS", "1") == "1"):
             self._slabs = self.executor.defer_slab_reduce() or None
+        self._side = None
+        self._arm_side_update()
         # executor policy for the world > 1 overlap (select_policy): None until chosen
         self.policy: Optional[dict] = None
         self._policy_done = False
@@ -181,7 +183,7 @@ class DataParallelTrainer:
                 h(self.last_logits(), labels)
         if self.algo == "sgd":
             self.sgd.step(f, self.lr, momentum=self.momentum, weight_decay=self.weight_decay,
-                          momentum_buf=self.mom, slabs=self._slabs)
+                          momentum_buf=self.mom, slabs=self._slabs, skip=self._side)
         elif self.algo == "ea":
             self._local_update()
         return loss
@@ -190,7 +192,7 @@ class DataParallelTrainer:
         from .ops.flat import flat_sgd_
 
         flat_sgd_(self.flat, self.lr, slot=None, mom=self.mom, momentum=self.momentum,
-                  weight_decay=self.weight_decay, slabs=self._slabs)
+                  weight_decay=self.weight_decay, slabs=self._slabs, skip=self._side)
 
     def step(self, x, y: Optional[torch.Tensor] = None) -> torch.Tensor:
         """One training step on this node's mini-batch; returns the loss
@@ -363,10 +365,26 @@ class DataParallelTrainer:
                        "candidates": {n: dict(kw) for n, kw in cands.items()}}
         return self.policy
 
+    def _arm_side_update(self) -> None:
+        """One node, slabs deferred: the update of the last blocks' parameters
+        rides the dgrad launch of the block that produces them last (extra
+        workgroups on the CUs that conv leaves free, models/cifar_hip.py
+        side_update); the final update skips that range.
+        DISTLEARN_SIDE_SGD=0: off (A/B)."""
+        self._side = None
+        ex = self.executor
+        if (self._slabs is None or os.environ.get("DISTLEARN_SIDE_SGD", "1") != "1"
+                or not callable(getattr(ex, "side_update", None))):
+            return
+        rng = ex.side_update(lambda: self.lr, self.momentum, self.weight_decay, self.mom,
+                             self.flat.slot if self.algo == "sgd" else None)
+        self._side = rng
+
     def _set_policy(self, kw: dict) -> None:
         self.executor.set_policy(**kw)
         if self._slabs is not None:  # the re-planned workspaces have new slabs
             self._slabs = self.executor.defer_slab_reduce() or None
+            self._arm_side_update()
 
     def _time_step_graph(self, loader, reps: int) -> float:
         """ms per replay of a freshly captured one-step graph (state restored;

@@ -277,6 +277,7 @@ class CifarHIPExecutor:
         self.rows = {0: 0, 1: 1, 2: int(os.environ.get("DISTLEARN_REDUCE_ROWS", "16"))}[self.mode]
         self._alloc(self.B)
         self._deferred = ()  # blocks whose weight-gradient slab reduce the update performs (defer_slab_reduce)
+        self._side = None    # side SGD carried by a dgrad launch (side_update)
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self, B: int):
@@ -625,6 +626,8 @@ class CifarHIPExecutor:
                                                   h, h, cout, cin, KSIZE, dt, self.y[i - 1].data_ptr(),
                                                   self.coef[i - 1].data_ptr(), prt.data_ptr(), s)
                 else:
+                    if self._side is not None and i == self._side["block"]:
+                        self._arm_side()  # this launch also runs the update of blocks >= i
                     C.conv_fwd(dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), 0,
                                self.slabs.data_ptr(), B, h, h, cout, cin, KSIZE,
                                dt | _slab_cap_bits(ds) | ((1 << 20) if keep else 0), ds, s)
@@ -658,6 +661,51 @@ class CifarHIPExecutor:
         self.dgrad_stages, self.cu_reserve = int(dgrad_stages), int(cu_reserve)
         self._alloc(self.B)
         self._deferred = ()
+        self._side = None
+
+    def side_update(self, lr_fn, momentum: float, weight_decay: float, mom, slot, block: Optional[int] = None):
+        """Run the SGD update of every parameter from block ``block``'s conv
+        weight to the end of the flat buffer (blocks >= block, the
+        classifier) inside that block's dgrad launch, as extra workgroups on
+        the CUs its one-workgroup-per-CU grid leaves free (csrc
+        set_conv_side_sgd): their gradients are final by then (weight
+        gradients in the flat buffer or, deferred, in their slabs) and nothing
+        later in the step reads them.  One node only (after
+        :meth:`defer_slab_reduce`).  Returns the flat element range [lo, hi)
+        the final update must skip, or None when the block's dgrad is not a
+        streaming launch."""
+        nb = self.nb
+        if block is None:
+            block = int(os.environ.get("DISTLEARN_SIDE_SGD_BLOCK", str(nb - 2)))
+        if not (0 < block < nb) or self.flat.shadow is None or self._region_dgrad(block, self.B):
+            return None
+        dt, ds = self.dgrad_plan[block]
+        keep = self.fuse_combine and ds in (2, 4, 8)
+        if self.dgrad_bnred and ds == 1 and not keep:
+            return None  # (a region dgrad with the fused BN reduce)
+        f = self.flat
+        lo, hi = f.offsets[self._leaf(block, 0)], f.total
+        base = f.data.data_ptr()
+        slabs = [(f.offsets[self._leaf(i, 0)], f.numels[self._leaf(i, 0)], self.wslab_l[i].data_ptr(),
+                  self.wplan[i][1]) for i in self._deferred if i >= block]
+        if any(self.cins[i] != self.cins_real[i] for i in self._deferred if i >= block):
+            return None
+        slabs.sort()
+        self._side = {"block": block, "lr": lr_fn,
+                      "args": (base, f.grad.data_ptr(), 0 if mom is None else mom.data_ptr(), f.shadow.data_ptr(),
+                               0 if slot is None else slot.data_ptr()),
+                      "mw": (float(momentum), float(weight_decay)), "range": (lo, hi),
+                      "slabs": ([o for o, _, _, _ in slabs], [n for _, n, _, _ in slabs],
+                                [t for _, _, t, _ in slabs], [k for _, _, _, k in slabs])}
+        return lo, hi
+
+    def _arm_side(self) -> None:
+        sd = self._side
+        p, g, mom, p16, slot = sd["args"]
+        mo, wd = sd["mw"]
+        lo, hi = sd["range"]
+        self.C.set_conv_side_sgd(p, g, mom, p16, slot, float(sd["lr"]()), mo, wd, lo, hi, *sd["slabs"],
+                                 int(os.environ.get("DISTLEARN_SIDE_SGD_BLOCKS", "0")))  # 0: sized to the range
 
     def defer_slab_reduce(self):
         """Leave every split-K weight gradient in its slabs: the slab_reduce

@@ -178,7 +178,7 @@ def _scale_from_slot(slot):
 
 def sgd_update_(p: torch.Tensor, g: torch.Tensor, lr: float, slot: torch.Tensor | None = None,
                 mom: torch.Tensor | None = None, momentum: float = 0.0, weight_decay: float = 0.0,
-                shadow: torch.Tensor | None = None, slabs=None, tail=None) -> None:
+                shadow: torch.Tensor | None = None, slabs=None, tail=None, skip=None) -> None:
     """p -= lr * (g/n + wd*p) [with momentum buffer]; n from ``slot`` (device).
     ``g`` is fp32, or bf16 (the all-reduced wire copy of grad_comm_dtype="bf16").
     ``slabs``: [(offset into p, numel, slab tensor [splits * numel], splits)]:
@@ -186,8 +186,9 @@ def sgd_update_(p: torch.Tensor, g: torch.Tensor, lr: float, slot: torch.Tensor 
     ``g`` (one GPU: the conv executor's deferred slab reduce; bitwise the
     stand-alone reduce's sum).  ``tail``: one channel-padded range
     (offset, numel, slab tensor, splits, Cout, taps, Cp, C) reduced by extra
-    blocks of the same launch."""
-    if slabs or tail is not None:
+    blocks of the same launch.  ``skip``: elements [lo, hi) of p left alone
+    (updated inside the step by a conv launch's side job)."""
+    if slabs or tail is not None or skip is not None:
         if not p.is_cuda or g.dtype != torch.float32:
             raise ValueError("sgd_update_: slab gradients need an fp32 gradient on the GPU")
         slabs = slabs or []
@@ -198,7 +199,8 @@ def sgd_update_(p: torch.Tensor, g: torch.Tensor, lr: float, slot: torch.Tensor 
         native().sgd_update_slabs(p.data_ptr(), g.data_ptr(), _ptr(mom), _ptr(shadow), _ptr(slot), float(lr),
                                   float(momentum), float(weight_decay), p.numel(), [int(o) for o, _, _, _ in slabs],
                                   [int(n) for _, n, _, _ in slabs], [t.data_ptr() for _, _, t, _ in slabs],
-                                  [int(k) for _, _, _, k in slabs], tl, tptr, stream_handle())
+                                  [int(k) for _, _, _, k in slabs], tl, tptr,
+                                  int(skip[0]) if skip else 0, int(skip[1]) if skip else 0, stream_handle())
         return
     if p.is_cuda:
         fn = native().sgd_update_g16 if g.dtype == torch.bfloat16 else native().sgd_update
@@ -226,7 +228,7 @@ def _overlaps(x: torch.Tensor, y: torch.Tensor) -> bool:
 
 def flat_sgd_(flat: "FlatParams", lr: float, slot: torch.Tensor | None = None, mom: torch.Tensor | None = None,
               momentum: float = 0.0, weight_decay: float = 0.0, grad: torch.Tensor | None = None,
-              slabs=None) -> None:
+              slabs=None, skip=None) -> None:
     """The fused update over a FlatParams' parameter body: the 64-element
     header (whose gradient element is the participation count) is left out,
     so ``n`` never flows into the parameter buffer.  ``grad``: the gradient
@@ -234,7 +236,9 @@ def flat_sgd_(flat: "FlatParams", lr: float, slot: torch.Tensor | None = None, m
     ``slabs``: [(leaf index, slab tensor, splits, Cout, taps, Cp, C)] whose
     gradient is still in split-K slabs [splits][Cout][taps][Cp] (see
     :func:`sgd_update_`): unpadded ones (Cp == C) with < 32 splits are read
-    in place, at most one other is reduced by extra blocks of the launch."""
+    in place, at most one other is reduced by extra blocks of the launch.
+    ``skip``: a flat element range [lo, hi) (offsets into ``flat.data``)
+    already updated inside the step."""
     H = HEADER
     g = flat.grad if grad is None else grad
     rng, tail = None, None
@@ -253,7 +257,8 @@ def flat_sgd_(flat: "FlatParams", lr: float, slot: torch.Tensor | None = None, m
         rng.sort(key=lambda r: r[0])
     sgd_update_(flat.data[H:], g[H:], lr, slot=slot, mom=None if mom is None else mom[H:],
                 momentum=momentum, weight_decay=weight_decay,
-                shadow=None if flat.shadow is None else flat.shadow[H:], slabs=rng, tail=tail)
+                shadow=None if flat.shadow is None else flat.shadow[H:], slabs=rng, tail=tail,
+                skip=None if skip is None else (max(0, skip[0] - H), skip[1] - H))
 
 
 def scale_by_count_(x: torch.Tensor, slot: torch.Tensor) -> None:

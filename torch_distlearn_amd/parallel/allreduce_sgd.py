@@ -104,14 +104,17 @@ class AllReduceSGD:
         self._count_step()
 
     def step(self, flat: FlatParams, lr: float, momentum: float = 0.0, weight_decay: float = 0.0,
-             momentum_buf: Optional[torch.Tensor] = None, already_reduced: bool = False, slabs=None) -> None:
+             momentum_buf: Optional[torch.Tensor] = None, already_reduced: bool = False, slabs=None,
+             skip=None) -> None:
         """Fused ``sumAndNormalizeGradients`` + SGD update over a FlatParams:
         all-reduce (unless the bucketer already did), then ONE kernel
         ``p -= lr*(g/n + wd*p)`` (+momentum, + bf16 shadow refresh).  This is
         examples/cifar10.lua:184-191 in one launch.  ``slabs`` (one node
         only: nothing is all-reduced): leaves whose gradient the update sums
-        from split-K slabs itself (ops/flat.py flat_sgd_)."""
-        if slabs and self.tree.numNodes > 1:
+        from split-K slabs itself (ops/flat.py flat_sgd_); ``skip``: a flat
+        element range [lo, hi) already updated inside the step (a conv
+        launch's side job)."""
+        if (slabs or skip) and self.tree.numNodes > 1:
             raise ValueError("AllReduceSGD.step: slab gradients are never all-reduced (one node only)")
         g = None
         bk = self.bucketer if (self.bucketer is not None and flat is self.bucketer.flat) else None
@@ -127,7 +130,7 @@ class AllReduceSGD:
         if bk is not None and bk.wire16 and not already_reduced:
             g = flat.grad16
         flat_sgd_(flat, lr, slot=flat.slot, mom=momentum_buf, momentum=momentum, weight_decay=weight_decay, grad=g,
-                  slabs=slabs)
+                  slabs=slabs, skip=skip)
 
     def enable_bucket_updates(self, flat: FlatParams, lr_fn, momentum: float = 0.0, weight_decay: float = 0.0,
                               momentum_buf: Optional[torch.Tensor] = None) -> bool:
