@@ -65,7 +65,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("combine_bwd_reduce_blocks", &combine_bwd_reduce_blocks);
   m.def("conv_fwd_ex", &conv_fwd_ex);
   m.def("conv_fwd_bnred", &conv_fwd_bnred);
-  m.def("conv_region_ok", &conv_region_ok);
+  m.def("conv_region_ok", &conv_region_ok, py::arg("B"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"),
+        py::arg("KS"), py::arg("tile"), py::arg("splits") = 1);
   m.def("set_conv_wgrad_stage_store", &set_conv_wgrad_stage_store);
   m.def("set_conv_wgrad_order", &set_conv_wgrad_order);
   m.def("set_conv_fwd_pf", &set_conv_fwd_pf);

@@ -81,7 +81,7 @@ void set_head_stamps(uintptr_t buf);
 void set_bn_stamps(uintptr_t buf);
 void set_conv_wgrad_stamps(uintptr_t buf);
 void set_conv_bn_reduce(uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, uintptr_t rows, uintptr_t ym = 0);
-int conv_region_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile);
+int conv_region_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile, int splits = 1);
 int conv_fwd_bnred(uintptr_t x, uintptr_t w, uintptr_t y, int B, int H, int W, int Cin, int Cout, int KS, int tile,
                    uintptr_t y_prev, uintptr_t coef, uintptr_t rows, uintptr_t stream);
 int conv_fwd_ex(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab, int B, int Ho, int Wo, int Hp,

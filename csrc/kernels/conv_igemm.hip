@@ -2620,11 +2620,12 @@ void set_conv_bn_reduce(uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, u
 
 // Whether conv_fwd runs this unsplit shape on the region (tap-reuse) kernel --
 // the kernel that carries the fused BN backward reduce epilogue.
-int conv_region_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile) {
+int conv_region_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile, int splits) {
   ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
   RegionGeom rg{};
   const int t = tile & 15;
-  return (t == 2 && region_geom(g, 64, 1, rg)) || (t == 0 && region_geom(g, 128, 1, rg)) ? 1 : 0;
+  if (splits < 1) splits = 1;
+  return (t == 2 && region_geom(g, 64, splits, rg)) || (t == 0 && region_geom(g, 128, splits, rg)) ? 1 : 0;
 }
 
 // conv_fwd (a dgrad) with the previous block's BatchNorm backward reduce in its

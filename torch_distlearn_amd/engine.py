@@ -131,6 +131,7 @@ class DataParallelTrainer:
         # nothing is all-reduced at one node).  DISTLEARN_DEFER_SLABS=0: off (A/B).
         self._slabs = None
         if (tree.numNodes == 1 and algo in ("sgd", "ea") and not self.bucket_updates
+                and self.grad_comm_dtype == "fp32"  # a bf16 wire copy would be cast from the stale fp32 grads
                 and callable(getattr(self.executor, "defer_slab_reduce", None))
                 and os.environ.get("DISTLEARN_DEFER_SLABS", "1") == "1"):
             self._slabs = self.executor.defer_slab_reduce() or None

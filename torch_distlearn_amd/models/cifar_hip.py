@@ -677,9 +677,12 @@ class CifarHIPExecutor:
         nb = self.nb
         if block is None:
             block = int(os.environ.get("DISTLEARN_SIDE_SGD_BLOCK", str(nb - 2)))
-        if not (0 < block < nb) or self.flat.shadow is None or self._region_dgrad(block, self.B):
+        if not (0 < block < nb) or self.flat.shadow is None:
             return None
         dt, ds = self.dgrad_plan[block]
+        h, cout, cin = self.hs[block], self.couts[block], self.cins[block]
+        if self.C.conv_region_ok(self.B, h, h, cout, cin, KSIZE, dt, ds):
+            return None  # the dgrad runs on the region kernel (its LDS leaves no room beside it)
         keep = self.fuse_combine and ds in (2, 4, 8)
         if self.dgrad_bnred and ds == 1 and not keep:
             return None  # (a region dgrad with the fused BN reduce)
