@@ -32,11 +32,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_bn_tuning", &set_bn_tuning);
   m.def("set_bn_minw", &set_bn_minw);
   m.def("bn_rows_reduce", &bn_rows_reduce);
-  m.def("bn_nhwc_fwd_pad", &bn_nhwc_fwd_pad);
+  m.def("bn_nhwc_fwd_pad", &bn_nhwc_fwd_pad, py::arg("x"), py::arg("res"), py::arg("y"), py::arg("acc"), py::arg("w"),
+        py::arg("b"), py::arg("save"), py::arg("run_mean"), py::arg("run_var"), py::arg("M"), py::arg("C"),
+        py::arg("eps"), py::arg("momentum"), py::arg("relu"), py::arg("have_stats"), py::arg("H"), py::arg("W"),
+        py::arg("opad"), py::arg("stream"), py::arg("mbits") = 0);
   m.def("bn_nhwc_bwd_pad", &bn_nhwc_bwd_pad, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("save"),
         py::arg("w"), py::arg("b"), py::arg("acc"), py::arg("dx"), py::arg("dres"), py::arg("dw"), py::arg("db"),
         py::arg("M"), py::arg("C"), py::arg("relu"), py::arg("H"), py::arg("W"), py::arg("opad"), py::arg("stream"),
-        py::arg("have_sums") = 0);
+        py::arg("have_sums") = 0, py::arg("mbits") = 0);
   m.def("zero_border_nhwc", &zero_border_nhwc);
   m.def("gather_normalize", &gather_normalize);
 

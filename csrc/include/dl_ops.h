@@ -39,10 +39,11 @@ void sgd_update_slabs(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, ui
 // channels-last training BatchNorm (+ReLU, +residual) for the ResNet-50 path
 void bn_nhwc_fwd_pad(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b,
                      uintptr_t save, uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps,
-                     double momentum, int relu, int have_stats, int H, int W, int opad, uintptr_t stream);
+                     double momentum, int relu, int have_stats, int H, int W, int opad, uintptr_t stream,
+                     uintptr_t mbits = 0);
 void bn_nhwc_bwd_pad(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b,
                      uintptr_t acc, uintptr_t dx, uintptr_t dres, uintptr_t dw, uintptr_t db, int64_t M, int C,
-                     int relu, int H, int W, int opad, uintptr_t stream, int have_sums = 0);
+                     int relu, int H, int W, int opad, uintptr_t stream, int have_sums = 0, uintptr_t mbits = 0);
 void zero_border_nhwc(uintptr_t buf, int N, int H, int W, int C, int pad, uintptr_t stream);
 void bn_nhwc_fwd(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b, uintptr_t save,
                  uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps, double momentum, int relu, int have_stats,

@@ -142,11 +142,25 @@ __device__ __forceinline__ void stats8(const float* __restrict__ acc, int C, int
   }
 }
 
+// bit k = bf16 output channel k is nonzero (relu output >= 0: > 0 <=> nonzero,
+// the mask relu mode 1 derives from y)
+__device__ __forceinline__ uint8_t mask_byte(const u32x4& o) {
+  const uint32_t w[4] = {o[0], o[1], o[2], o[3]};
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    m |= (w[k] & 0x7fffu) ? (1u << (2 * k)) : 0u;
+    m |= (w[k] & 0x7fff0000u) ? (1u << (2 * k + 1)) : 0u;
+  }
+  return (uint8_t)m;
+}
+
 template <int U>
 __global__ void __launch_bounds__(kThreads) bn_nhwc_fwd_apply_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
     const float* __restrict__ acc, const float* __restrict__ w, const float* __restrict__ b, BnGeom g, float eps,
-    int relu, float* __restrict__ save, float* __restrict__ run_mean, float* __restrict__ run_var, float momentum) {
+    int relu, float* __restrict__ save, float* __restrict__ run_mean, float* __restrict__ run_var, float momentum,
+    uint8_t* __restrict__ mbits) {
   const int t = threadIdx.x, cv = t % g.CVB, r = t / g.CVB;
   const int c0 = blockIdx.y * g.CVB * 8;
   const int c = c0 + cv * 8;
@@ -174,7 +188,7 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_fwd_apply_kernel(
   const int64_t row0 = (int64_t)blockIdx.x * g.rows_per_block;
   const int64_t row1 = min(g.M, row0 + g.rows_per_block);
   const u32x4 z = {0u, 0u, 0u, 0u};
-  auto apply = [&](int64_t off, const u32x4& xr, const u32x4& rr) {
+  auto apply = [&](int64_t off, int64_t row, const u32x4& xr, const u32x4& rr) {
     float f[8];
     unpack8(xr, f);
 #pragma unroll
@@ -189,7 +203,9 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_fwd_apply_kernel(
 #pragma unroll
       for (int k = 0; k < 8; ++k) f[k] = fmaxf(f[k], 0.f);
     }
-    *(u32x4*)(y + off) = pack8(f);
+    const u32x4 o = pack8(f);
+    *(u32x4*)(y + off) = o;
+    if (mbits != nullptr) mbits[row * (g.C >> 3) + (c >> 3)] = mask_byte(o);  // relu mode 3
   };
   int64_t row = row0 + r;
   for (; row + (U - 1) * g.RPI < row1; row += U * g.RPI) {  // U rows' loads in flight
@@ -201,24 +217,27 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_fwd_apply_kernel(
       rv[u] = res != nullptr ? *(const u32x4*)(res + o) : z;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) apply(out_row(g, row + u * g.RPI) * g.C + c, xv[u], rv[u]);
+    for (int u = 0; u < U; ++u) apply(out_row(g, row + u * g.RPI) * g.C + c, row + u * g.RPI, xv[u], rv[u]);
   }
   for (; row < row1; row += g.RPI) {
     const int64_t o0 = row * g.C + c;
-    apply(out_row(g, row) * g.C + c, *(const u32x4*)(x + o0), res != nullptr ? *(const u32x4*)(res + o0) : z);
+    apply(out_row(g, row) * g.C + c, row, *(const u32x4*)(x + o0), res != nullptr ? *(const u32x4*)(res + o0) : z);
   }
 }
 
 // g = dy * relu'(.): relu 0 = identity, 1 = mask from the saved output y (BN
 // fused with a residual add), 2 = mask recomputed from x (x * sc + sh > 0,
 // bitwise the forward's pre-activation: same fp32 operands and fma), which
-// saves reading y in both backward passes (applied inline by the two kernels
-// below, after all of an iteration's loads are issued).
+// saves reading y in both backward passes, 3 = mask bits written by the forward
+// apply (BN + residual: one byte per 8 channels per row instead of re-reading
+// the 16 bytes of y in each backward pass; bit k = output channel k nonzero,
+// the same mask as mode 1) -- applied inline by the two kernels below, after
+// all of an iteration's loads are issued.
 template <int NT>
 __global__ void __launch_bounds__(NT) bn_nhwc_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ save, const float* __restrict__ w, const float* __restrict__ b, BnGeom g, int relu,
-    float* __restrict__ acc) {
+    float* __restrict__ acc, const uint8_t* __restrict__ mbits) {
   const int t = threadIdx.x, cv = t % g.CVB, r = t / g.CVB;
   const int c0 = blockIdx.y * g.CVB * 8;
   const int c = c0 + cv * 8;
@@ -233,11 +252,14 @@ __global__ void __launch_bounds__(NT) bn_nhwc_bwd_reduce_kernel(
   float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int64_t row0 = (int64_t)blockIdx.x * g.rows_per_block;
   const int64_t row1 = min(g.M, row0 + g.rows_per_block);
-  auto accum = [&](const u32x4& xr, const u32x4& dr, const u32x4& yr) {
+  auto accum = [&](const u32x4& xr, const u32x4& dr, const u32x4& yr, unsigned mb) {
     float gv[8], xv[8];
     unpack8(xr, xv);
     unpack8(dr, gv);
-    if (relu == 2) {
+    if (relu == 3) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gv[k] = (mb >> k) & 1u ? gv[k] : 0.f;
+    } else if (relu == 2) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) gv[k] = fmaf(xv[k], sc[k], sh[k]) > 0.f ? gv[k] : 0.f;
     } else if (relu) {
@@ -260,19 +282,22 @@ __global__ void __launch_bounds__(NT) bn_nhwc_bwd_reduce_kernel(
   const u32x4 z = {0u, 0u, 0u, 0u};
   for (; row + (U - 1) * g.RPI < row1; row += U * g.RPI) {
     u32x4 xr[U], dr[U], yr[U];
+    unsigned mb[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t off = (row + u * g.RPI) * g.C + c;
       xr[u] = *(const u32x4*)(x + off);
       dr[u] = *(const u32x4*)(dy + off);
       yr[u] = relu == 1 ? *(const u32x4*)(y + off) : z;
+      mb[u] = relu == 3 ? mbits[(row + u * g.RPI) * (g.C >> 3) + (c >> 3)] : 0u;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) accum(xr[u], dr[u], yr[u]);
+    for (int u = 0; u < U; ++u) accum(xr[u], dr[u], yr[u], mb[u]);
   }
   for (; row < row1; row += g.RPI) {
     const int64_t off = row * g.C + c;
-    accum(*(const u32x4*)(x + off), *(const u32x4*)(dy + off), relu == 1 ? *(const u32x4*)(y + off) : z);
+    accum(*(const u32x4*)(x + off), *(const u32x4*)(dy + off), relu == 1 ? *(const u32x4*)(y + off) : z,
+          relu == 3 ? mbits[row * (g.C >> 3) + (c >> 3)] : 0u);
   }
   block_reduce_atomic<NT>(sg, sgx, g, c0, acc);
 }
@@ -281,7 +306,8 @@ template <int U>
 __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ save, const float* __restrict__ w, const float* __restrict__ b,
-    const float* __restrict__ acc, BnGeom g, int relu, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, float* __restrict__ dw, float* __restrict__ db) {
+    const float* __restrict__ acc, BnGeom g, int relu, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, float* __restrict__ dw, float* __restrict__ db,
+    const uint8_t* __restrict__ mbits) {
   const int t = threadIdx.x, cv = t % g.CVB, r = t / g.CVB;
   const int c0 = blockIdx.y * g.CVB * 8;
   const int c = c0 + cv * 8;
@@ -306,11 +332,14 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
   const int64_t row0 = (int64_t)blockIdx.x * g.rows_per_block;
   const int64_t row1 = min(g.M, row0 + g.rows_per_block);
   const u32x4 z = {0u, 0u, 0u, 0u};
-  auto apply = [&](int64_t off, int64_t doff, const u32x4& xr, const u32x4& dr, const u32x4& yr) {
+  auto apply = [&](int64_t off, int64_t doff, const u32x4& xr, const u32x4& dr, const u32x4& yr, unsigned mb) {
     float gv[8], xv[8], o[8];
     unpack8(xr, xv);
     unpack8(dr, gv);
-    if (relu == 2) {
+    if (relu == 3) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gv[k] = (mb >> k) & 1u ? gv[k] : 0.f;
+    } else if (relu == 2) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) gv[k] = fmaf(xv[k], a[k], sh[k]) > 0.f ? gv[k] : 0.f;
     } else if (relu) {
@@ -330,21 +359,23 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
   int64_t row = row0 + r;
   for (; row + (U - 1) * g.RPI < row1; row += U * g.RPI) {  // U rows' loads in flight
     u32x4 xv[U], dv[U], yv[U];
+    unsigned mb[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t o = (row + u * g.RPI) * g.C + c;
       xv[u] = *(const u32x4*)(x + o);
       dv[u] = *(const u32x4*)(dy + o);
       yv[u] = relu == 1 ? *(const u32x4*)(y + o) : z;
+      mb[u] = relu == 3 ? mbits[(row + u * g.RPI) * (g.C >> 3) + (c >> 3)] : 0u;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      apply((row + u * g.RPI) * g.C + c, out_row(g, row + u * g.RPI) * g.C + c, xv[u], dv[u], yv[u]);
+      apply((row + u * g.RPI) * g.C + c, out_row(g, row + u * g.RPI) * g.C + c, xv[u], dv[u], yv[u], mb[u]);
   }
   for (; row < row1; row += g.RPI) {
     const int64_t o0 = row * g.C + c;
     apply(o0, out_row(g, row) * g.C + c, *(const u32x4*)(x + o0), *(const u32x4*)(dy + o0),
-          relu == 1 ? *(const u32x4*)(y + o0) : z);
+          relu == 1 ? *(const u32x4*)(y + o0) : z, relu == 3 ? mbits[row * (g.C >> 3) + (c >> 3)] : 0u);
   }
 }
 
@@ -506,13 +537,15 @@ void bn_nhwc_fwd(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr
                  uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps, double momentum, int relu,
                  int have_stats, uintptr_t stream) {
   bn_nhwc_fwd_pad(x, res, y, acc, w, b, save, run_mean, run_var, M, C, eps, momentum, relu, have_stats, 1, 1, 0,
-                  stream);
+                  stream, 0);
 }
 
 // y in the padded layout [N][H+2opad][W+2opad][C] (interior only; see zero_border_nhwc)
 void bn_nhwc_fwd_pad(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b,
                      uintptr_t save, uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps,
-                     double momentum, int relu, int have_stats, int H, int W, int opad, uintptr_t stream) {
+                     double momentum, int relu, int have_stats, int H, int W, int opad, uintptr_t stream,
+                     uintptr_t mbits) {
+  if (mbits && !relu) throw std::runtime_error("bn_nhwc_fwd: mask bits need the ReLU");
   dim3 grid, grid_r;
   BnGeom g = make_geom(M, C, &grid);
   set_out_pad(g, H, W, opad);
@@ -531,7 +564,7 @@ void bn_nhwc_fwd_pad(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uin
   auto fk = g_apply_rows == 4 ? bn_nhwc_fwd_apply_kernel<4> : bn_nhwc_fwd_apply_kernel<2>;
   fk<<<grid, kThreads, 0, s>>>((const bf16_t*)x, (const bf16_t*)res, (bf16_t*)y, (const float*)acc,
                                (const float*)w, (const float*)b, g, (float)eps, relu, (float*)save,
-                               (float*)run_mean, (float*)run_var, (float)momentum);
+                               (float*)run_mean, (float*)run_var, (float)momentum, (uint8_t*)mbits);
   DL_HIP_CHECK(hipGetLastError());
 }
 
@@ -540,7 +573,7 @@ void bn_nhwc_fwd_pad(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uin
 void bn_nhwc_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, uintptr_t acc,
                  uintptr_t dx,
                  uintptr_t dres, uintptr_t dw, uintptr_t db, int64_t M, int C, int relu, uintptr_t stream) {
-  bn_nhwc_bwd_pad(dy, y, x, save, w, b, acc, dx, dres, dw, db, M, C, relu, 1, 1, 0, stream);
+  bn_nhwc_bwd_pad(dy, y, x, save, w, b, acc, dx, dres, dw, db, M, C, relu, 1, 1, 0, stream, 0, 0);
 }
 
 // dx in the padded layout [N][H+2opad][W+2opad][C] (interior only).
@@ -549,7 +582,9 @@ void bn_nhwc_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr
 // ops/conv.py): the reduce pass over dy and x is skipped.
 void bn_nhwc_bwd_pad(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b,
                      uintptr_t acc, uintptr_t dx, uintptr_t dres, uintptr_t dw, uintptr_t db, int64_t M, int C,
-                     int relu, int H, int W, int opad, uintptr_t stream, int have_sums) {
+                     int relu, int H, int W, int opad, uintptr_t stream, int have_sums, uintptr_t mbits) {
+  if ((relu == 3) != (mbits != 0)) throw std::runtime_error("bn_nhwc_bwd: relu mode 3 reads the forward's mask bits");
+  if (relu == 1 && !y) throw std::runtime_error("bn_nhwc_bwd: relu mode 1 reads y");
   dim3 grid, grid_r;
   BnGeom g = make_geom(M, C, &grid);
   set_out_pad(g, H, W, opad);
@@ -560,13 +595,13 @@ void bn_nhwc_bwd_pad(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uin
     auto rk = nt == 1024 ? bn_nhwc_bwd_reduce_kernel<1024>
               : nt == 512 ? bn_nhwc_bwd_reduce_kernel<512> : bn_nhwc_bwd_reduce_kernel<256>;
     rk<<<grid_r, nt, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, (const float*)save,
-                             (const float*)w, (const float*)b, gr, relu, (float*)acc);
+                             (const float*)w, (const float*)b, gr, relu, (float*)acc, (const uint8_t*)mbits);
     DL_HIP_CHECK(hipGetLastError());
   }
   auto ak = g_apply_rows == 4 ? bn_nhwc_bwd_apply_kernel<4> : bn_nhwc_bwd_apply_kernel<2>;
   ak<<<grid, kThreads, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, (const float*)save,
                                (const float*)w, (const float*)b, (const float*)acc, g, relu, (bf16_t*)dx,
-                               (bf16_t*)dres, (float*)dw, (float*)db);
+                               (bf16_t*)dres, (float*)dw, (float*)db, (const uint8_t*)mbits);
   DL_HIP_CHECK(hipGetLastError());
 }
 

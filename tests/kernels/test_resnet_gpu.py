@@ -145,6 +145,40 @@ def test_bn_act_hip_matches_fp32(c, hw, relu, res):
         assert rel < 2e-2, (name, rel)
 
 
+@pytest.mark.parametrize("c,hw", [(256, 14), (2048, 7), (64, 56)])
+def test_bn_residual_mask_bits_bitwise(c, hw, monkeypatch):
+    """BN + residual + ReLU: the backward's ReLU mask from the forward's mask
+    bits (relu mode 3, 1/16 of y's bytes, y not kept) is exactly the mask of
+    the output y -- the residual gradient (the masked dy) equals
+    where(y > 0, dy, 0) bit for bit -- and mode 3 agrees with mode 1 (mask
+    read from y) to the run-to-run noise of the statistics' fp32 atomics."""
+    from torch_distlearn_amd import _native
+    from torch_distlearn_amd.ops import bn_nhwc
+
+    _native.native()
+    torch.manual_seed(c)
+    dev, n, cl = "cuda", 8, torch.channels_last
+    xb = (torch.randn(n, c, hw, hw, device=dev) * 2 + 0.3).to(torch.bfloat16).contiguous(memory_format=cl)
+    rb = torch.randn(n, c, hw, hw, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    w, b = torch.rand(c, device=dev) + 0.5, torch.randn(c, device=dev) * 0.2
+    go = torch.randn(n, c, hw, hw, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    outs = []
+    for bits in (False, True):
+        monkeypatch.setattr(bn_nhwc, "_MASK_BITS", bits)
+        x, r = xb.detach().requires_grad_(True), rb.detach().requires_grad_(True)
+        wi, bi = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        y = bn_nhwc.bn_act(x, wi, bi, torch.zeros(c, device=dev), torch.ones(c, device=dev), r, True)
+        assert y.grad_fn.__class__.__name__ == "_BnActBackward"
+        y.backward(go)
+        torch.cuda.synchronize()
+        outs.append([y, x.grad, r.grad, wi.grad, bi.grad])
+    (y0, dx0, dr0, dw0, db0), (y1, dx1, dr1, dw1, db1) = outs
+    assert torch.equal(dr1, torch.where(y1 > 0, go, torch.zeros_like(go)))  # mode 3: bits == y's mask
+    assert torch.equal(dr0, torch.where(y0 > 0, go, torch.zeros_like(go)))
+    for a, b_ in ((y0, y1), (dx0, dx1), (dw0, dw1), (db0, db1), (dr0, dr1)):
+        assert float((a.float() - b_.float()).norm() / (b_.float().norm() + 1e-12)) < 1e-2
+
+
 def test_resnet50_mixed_bn_train_step(monkeypatch):
     # the MIOpen BN path (DISTLEARN_RESNET_BN=mixed); the default is the HIP BN
     from torch_distlearn_amd.models import resnet

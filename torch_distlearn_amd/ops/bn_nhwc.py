@@ -23,6 +23,9 @@ from .._native import native, stream_handle
 # kernels' rows in flight / reduce block size; empty = the compiled defaults
 _TUNE = os.environ.get("DISTLEARN_BN_TUNE", "")
 _tuned = False
+# BN + residual + ReLU keeps its ReLU mask as bits for the backward (relu mode 3)
+# instead of re-reading the output y in both backward passes; 0 = mode 1 (A/B)
+_MASK_BITS = os.environ.get("DISTLEARN_BN_MASK_BITS", "1") == "1"
 
 
 def _bn():
@@ -84,11 +87,20 @@ class _BnAct(torch.autograd.Function):
         # (with out_pad the kernel writes y's padded buffer: its origin is y.data_ptr()
         # minus the interior offset)
         ybase = y.data_ptr() - (out_pad * (W + 2 * out_pad) + out_pad) * C * 2 if out_pad else y.data_ptr()
+        # BN + residual + ReLU: the backward needs the output's ReLU mask, which x
+        # alone does not give.  The apply writes it as bits (one byte per 8
+        # channels per row, 1/16 of y) so both backward passes read that instead
+        # of y (relu mode 3); y itself is then not kept for the backward.
+        # (bn_link -- the consuming dgrad computes the backward sums -- reads y.)
+        mbits = None
+        if relu and residual is not None and bn_link is None and _MASK_BITS:
+            mbits = torch.empty(M * C // 8, dtype=torch.uint8, device=x.device)
         _bn().bn_nhwc_fwd_pad(x.data_ptr(), res.data_ptr() if res is not None else 0, ybase, acc.data_ptr(),
                                  weight.data_ptr(), bias.data_ptr(), save.data_ptr(),
                                  running_mean.data_ptr() if running_mean is not None else 0,
                                  running_var.data_ptr() if running_var is not None else 0, M, C, float(eps),
-                                 float(momentum), int(relu), int(have_stats), H, W, int(out_pad), stream_handle())
+                                 float(momentum), int(relu), int(have_stats), H, W, int(out_pad), stream_handle(),
+                                 mbits.data_ptr() if mbits is not None else 0)
         ctx.has_res = residual is not None
         ctx.grads = grads
         ctx.res_sink = res_sink
@@ -97,8 +109,8 @@ class _BnAct(torch.autograd.Function):
         # relu mask: from the output when a residual was added (mode 1),
         # otherwise recomputed from x in the backward kernels (mode 2: y is
         # neither saved nor read)
-        ctx.relu = (1 if ctx.has_res else 2) if relu else 0
-        ctx.save_for_backward(x, y if ctx.relu == 1 else None, weight, bias, save, acc)
+        ctx.relu = (3 if mbits is not None else 1 if ctx.has_res else 2) if relu else 0
+        ctx.save_for_backward(x, y if ctx.relu == 1 else mbits, weight, bias, save, acc)
         ctx.bn_link = bn_link if ctx.relu else None
         if ctx.bn_link is not None:
             # what the consuming convolution's dgrad epilogue needs to compute this
@@ -128,10 +140,13 @@ class _BnAct(torch.autograd.Function):
         else:
             dw = torch.empty(C, device=x.device, dtype=torch.float32)
             db = torch.empty(C, device=x.device, dtype=torch.float32)
-        _bn().bn_nhwc_bwd_pad(dy.data_ptr(), y.data_ptr() if y is not None else 0, x.data_ptr(), save.data_ptr(),
+        ym = y if ctx.relu == 1 else None      # (the saved slot holds the mask bits in relu mode 3)
+        mb = y if ctx.relu == 3 else None
+        _bn().bn_nhwc_bwd_pad(dy.data_ptr(), ym.data_ptr() if ym is not None else 0, x.data_ptr(), save.data_ptr(),
                                  weight.data_ptr(), bias.data_ptr(), acc.data_ptr(), dxbase,
                                  dres.data_ptr() if dres is not None else 0, dw.data_ptr(), db.data_ptr(), M, C,
-                                 ctx.relu, H, W, int(p), stream_handle(), int(have_sums))
+                                 ctx.relu, H, W, int(p), stream_handle(), int(have_sums),
+                                 mb.data_ptr() if mb is not None else 0)
         if ctx.res_sink is not None and dres is not None and not ctx.res_sink.get("done"):
             # consumed by the conv whose input is the residual (ops/conv.py); if that
             # conv's backward already ran ("done"), autograd sums the gradients instead
