@@ -45,7 +45,9 @@ PYBIND11_MODULE(_C, m) {
 
   // ---- convnet kernels (MFMA implicit GEMM, BN/ReLU/pool, classifier head) ------
   m.def("conv_fwd", &conv_fwd);
-  m.def("conv_fwd_add", &conv_fwd_add);
+  m.def("conv_fwd_add", &conv_fwd_add, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("addend"), py::arg("B"),
+        py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"), py::arg("KS"), py::arg("tile"), py::arg("stream"),
+        py::arg("addend_mask") = 0);
   m.def("conv_fwd_stat_rows", &conv_fwd_stat_rows);
   m.def("set_conv_region", &set_conv_region);
   m.def("set_conv_region_stages", &set_conv_region_stages);

@@ -95,7 +95,7 @@ void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, i
                 int ldo, int tile, int atomic_creal, uintptr_t stream);
 void set_reduce_atomic_conv(int rows);
 void conv_fwd_add(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t addend, int B, int H, int W, int Cin, int Cout,
-                  int KS, int tile, uintptr_t stream);
+                  int KS, int tile, uintptr_t stream, uintptr_t addend_mask = 0);
 void set_conv_fwd_tr(int on);
 void set_conv_posm(int on);
 void set_conv_wgrad_xcd(int on);

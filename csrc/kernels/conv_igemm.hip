@@ -387,8 +387,11 @@ __device__ __forceinline__ void conv_fwd_epilogue(const f32x4 (&acc)[BM / WM / 1
           const int m = m0 + wm * TM + a * 16 + rq * 4 + r;
           float v0 = acc[a][b][r];
           const int64_t mo = (int64_t)phys(m) * g.Cout + n;
-          if constexpr (ADD) {
-            if (m < g.M && n < g.Cout) v0 += bf16_to_f32(reinterpret_cast<const bf16_t*>(slab)[mo]);
+          if constexpr (ADD) {  // (ADD: stats carries the addend's optional mask bits, see conv_fwd_add)
+            const uint8_t* mb = reinterpret_cast<const uint8_t*>(stats);
+            if (m < g.M && n < g.Cout &&
+                (mb == nullptr || ((mb[(int64_t)phys(m) * (g.Cout >> 3) + (n >> 3)] >> (n & 7)) & 1u)))
+              v0 += bf16_to_f32(reinterpret_cast<const bf16_t*>(slab)[mo]);
           }
           const bf16_t hv = f32_to_bf16(v0);
           if (m < g.M && n < g.Cout) y[mo] = hv;
@@ -513,8 +516,14 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
       if constexpr (ADD) {
         if (ok) {
           const uint4 ad = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(slab) + (int64_t)m * g.Cout + n);
-          v[0] += lo_bf16(ad.x); v[1] += hi_bf16(ad.x); v[2] += lo_bf16(ad.y); v[3] += hi_bf16(ad.y);
-          v[4] += lo_bf16(ad.z); v[5] += hi_bf16(ad.z); v[6] += lo_bf16(ad.w); v[7] += hi_bf16(ad.w);
+          // (ADD: stats carries the addend's optional mask bits, conv_fwd_add: the
+          // residual gradient = dy of the BN + residual + ReLU, masked here)
+          const uint8_t* mb = reinterpret_cast<const uint8_t*>(stats);
+          const unsigned bits = mb != nullptr ? mb[(int64_t)m * (g.Cout >> 3) + (n >> 3)] : 0xffu;
+          const float a8[8] = {lo_bf16(ad.x), hi_bf16(ad.x), lo_bf16(ad.y), hi_bf16(ad.y),
+                               lo_bf16(ad.z), hi_bf16(ad.z), lo_bf16(ad.w), hi_bf16(ad.w)};
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] += (bits >> k) & 1u ? a8[k] : 0.f;
         }
       }
       if constexpr (SLAB) {
@@ -2185,6 +2194,7 @@ int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile,
 
 static SgdJob g_side_sgd{};         // set_conv_side_sgd: side SGD job of the next conv_fwd launch
 static uintptr_t g_fwd_addend = 0;  // conv_fwd_add: bf16 [M][Cout] added in the epilogue
+static uintptr_t g_fwd_addend_mask = 0;  // conv_fwd_add: optional uint8 [M][Cout/8] mask bits of the addend
 static int g_fwd_slab_cap = 0;      // split-K slab capacity of the current conv_fwd call (FwdCfg)
 static int g_fwd_keep_slabs = 0;    // FwdCfg bit 20: leave the split-K slabs (the caller combines them)
 static int g_fwd_swave_req = 0;     // FwdCfg bit 21: per-wave-row BN statistics rows (ConvGeom::swave)
@@ -2265,8 +2275,8 @@ static void launch_fwd_w(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uin
     if constexpr ((BN / WN / 16) % 2 == 0) {  // the transposed epilogue (paired N fragments)
       if (g_fwd_addend)
         conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, true, true, 3><<<grid, NT, 0, s>>>(
-            (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, (float*)g_fwd_addend, g, 1, ktps, g_conv_dbg,
-            g_bnred2, side);
+            (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)g_fwd_addend_mask, (float*)g_fwd_addend, g, 1,
+            ktps, g_conv_dbg, g_bnred2, side);
       else
         conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, false, true, 2><<<grid, NT, 0, s>>>(
             (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, nullptr, g, 1, ktps, g_conv_dbg, g_bnred2, side);
@@ -2275,7 +2285,8 @@ static void launch_fwd_w(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uin
     }
   } else if (g_fwd_addend)
     conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, true><<<grid, NT, 0, s>>>(
-        (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, (float*)g_fwd_addend, g, 1, ktps, g_conv_dbg, BnRedArgs{}, side);
+        (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)g_fwd_addend_mask, (float*)g_fwd_addend, g, 1, ktps,
+        g_conv_dbg, BnRedArgs{}, side);
   else if (splits > 1 && !g_fwd_tr)
     conv_fwd_kernel<BM, BN, false, true, TAPU, ST, WM, WN, false, false><<<grid, NT, 0, s>>>(
         (const bf16_t*)x, (const bf16_t*)w, nullptr, nullptr, (float*)slab, g, splits, ktps, g_conv_dbg, BnRedArgs{}, side);
@@ -2654,24 +2665,27 @@ int conv_fwd_bnred(uintptr_t x, uintptr_t w, uintptr_t y, int B, int H, int W, i
 // y = conv(x, w) + addend (bf16, same layout as y), streaming kernel only
 // (KS = 1 or the region kernels disabled for the shape), no split-K / stats.
 void conv_fwd_add(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t addend, int B, int H, int W, int Cin, int Cout,
-                  int KS, int tile, uintptr_t stream) {
+                  int KS, int tile, uintptr_t stream, uintptr_t addend_mask) {
   const FwdCfg cfg(tile);
   ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
   hipStream_t s = as_stream(stream);
   if (!addend) throw std::runtime_error("conv_fwd_add: null addend");
   if (Cout % fwd_bn(tile) != 0) throw std::runtime_error("conv_fwd_add: Cout must be a multiple of the N tile");
   if (KS != 1 && g_region) throw std::runtime_error("conv_fwd_add: only the streaming kernel (KS = 1)");
+  if (addend_mask && g_bnred2.rows != nullptr)
+    throw std::runtime_error("conv_fwd_add: a masked addend does not combine with the fused BN reduce");
   g_fwd_addend = addend;
+  g_fwd_addend_mask = addend_mask;
   try {
     if (tile == 0) launch_fwd<128, 128>(g, x, w, y, 0, 0, 1, s);
     else if (tile == 1) launch_fwd<64, 64>(g, x, w, y, 0, 0, 1, s);
     else if (tile == 2) launch_fwd<128, 64>(g, x, w, y, 0, 0, 1, s);
     else throw std::runtime_error("conv_fwd_add: bad tile id");
   } catch (...) {
-    g_fwd_addend = 0;
+    g_fwd_addend = g_fwd_addend_mask = 0;
     throw;
   }
-  g_fwd_addend = 0;
+  g_fwd_addend = g_fwd_addend_mask = 0;
   DL_HIP_CHECK(hipGetLastError());
 }
 

@@ -150,3 +150,50 @@ def test_dgrad_add_epilogue_bn_residual_sums(dev, N, C, H, cout):
         assert _rel(a, b) < 2e-3
     for a, b in zip(res[0], ref):
         assert _rel(a, b) < 3e-2
+
+
+@pytest.mark.parametrize("N,C,H,mid", [(4, 256, 14, 64), (2, 512, 7, 128)])
+def test_masked_residual_gradient_in_c1_dgrad(dev, monkeypatch, N, C, H, mid):
+    """Identity bottleneck form: x -> c1 (1x1) -> c3 (1x1) -> BN + residual(x) +
+    ReLU.  With mask bits (relu mode 3) the BN's backward does not write the
+    residual gradient: it hands (dy, mask bits) to c1, whose dgrad epilogue
+    adds dy under the mask (conv_fwd_add with addend_mask).  x's gradient and
+    every parameter gradient match the path that writes dres (to the noise of
+    the BN reduce's fp32 atomics) and an fp32 PyTorch reference."""
+    from torch_distlearn_amd.ops import bn_nhwc
+    from torch_distlearn_amd.ops.conv import Conv1x1, ShadowBinding
+
+    def run(masked):
+        monkeypatch.setattr(bn_nhwc, "_MASKED_ADDEND", masked)
+        g = torch.Generator(device=dev).manual_seed(8)
+        mk = lambda *s: torch.randn(*s, device=dev, generator=g).to(BF).contiguous(memory_format=CL)  # noqa: E731
+        x = mk(N, C, H, H).requires_grad_(True)
+        w1 = (torch.randn(mid, C, 1, 1, device=dev, generator=g) * C ** -0.5).to(BF)
+        w3 = (torch.randn(C, mid, 1, 1, device=dev, generator=g) * mid ** -0.5).to(BF)
+        gamma = (torch.rand(C, device=dev, generator=g) + 0.5).requires_grad_(True)
+        beta = (torch.randn(C, device=dev, generator=g) * 0.3).requires_grad_(True)
+        go = mk(N, C, H, H)
+        b1 = ShadowBinding(w1.reshape(mid, C), torch.zeros(mid, C, device=dev), lambda: None)
+        b3 = ShadowBinding(w3.reshape(C, mid), torch.zeros(C, mid, device=dev), lambda: None)
+        link = {}
+        h = Conv1x1.apply(x, torch.nn.Parameter(w1.float()), b1, None, link, None, None)
+        y3 = Conv1x1.apply(h, torch.nn.Parameter(w3.float()), b3, None, None, None, None)
+        z = bn_nhwc.bn_act(y3, gamma, beta, None, None, residual=x, relu=True, acc=torch.zeros(4 * C, device=dev),
+                           have_stats=False, res_sink=link)
+        z.backward(go)
+        torch.cuda.synchronize()
+        assert ("gm" in link) is False and ("g" in link) is False  # consumed
+        # fp32 reference of the same chain
+        xr = x.detach().float().requires_grad_(True)
+        gr, br = gamma.detach().clone().requires_grad_(True), beta.detach().clone().requires_grad_(True)
+        hr = F.conv2d(xr, w1.float())
+        zr = F.relu(F.batch_norm(F.conv2d(hr, w3.float()), None, None, gr, br, True, 0.1, 1e-5) + xr)
+        zr.backward(go.float())
+        return [x.grad, gamma.grad, beta.grad, b1.g32, b3.g32], [xr.grad, gr.grad, br.grad]
+
+    on, ref = run(True)
+    off, _ = run(False)
+    for a, b in zip(on, off):
+        assert _rel(a, b) < 1e-2
+    for a, b in zip(on[:3], ref):
+        assert _rel(a, b) < 3e-2

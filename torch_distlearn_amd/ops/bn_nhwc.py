@@ -26,6 +26,18 @@ _tuned = False
 # BN + residual + ReLU keeps its ReLU mask as bits for the backward (relu mode 3)
 # instead of re-reading the output y in both backward passes; 0 = mode 1 (A/B)
 _MASK_BITS = os.environ.get("DISTLEARN_BN_MASK_BITS", "1") == "1"
+# ... and hands (dy, mask bits) to the residual's consumer instead of writing
+# the residual gradient (DISTLEARN_BN_MASKED_ADDEND=0: writes dres, A/B)
+_MASKED_ADDEND = os.environ.get("DISTLEARN_BN_MASKED_ADDEND", "1") == "1"
+
+
+def unpack_mask_bits(mbits: torch.Tensor, shape_like: torch.Tensor) -> torch.Tensor:
+    """bool [N, C, H, W] (channels-last) from relu mode 3's mask bits
+    (uint8 [M][C/8], bit k of byte (m, j) = channel 8j + k)."""
+    n, c, h, w = shape_like.shape
+    sh = torch.arange(8, device=mbits.device, dtype=torch.uint8)
+    bits = ((mbits.view(-1, c // 8, 1) >> sh) & 1).view(n, h, w, c).bool()
+    return bits.permute(0, 3, 1, 2)
 
 
 def _bn():
@@ -128,7 +140,13 @@ class _BnAct(torch.autograd.Function):
         p = ctx.dx_pad
         dx = padded_empty(N, C, H, W, p, x.device) if p else torch.empty_like(x, memory_format=torch.channels_last)
         dxbase = dx.data_ptr() - (p * (W + 2 * p) + p) * C * 2 if p else dx.data_ptr()
-        dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
+        # relu mode 3 with a waiting consumer (the conv whose input is the residual,
+        # ops/conv.py Conv1x1): the residual gradient dy * mask is not written
+        # here -- the consumer's dgrad epilogue adds dy under the mask bits itself
+        # (one full write + read of dres fewer)
+        park = (ctx.relu == 3 and ctx.res_sink is not None and _MASKED_ADDEND and ctx.has_res
+                and not ctx.res_sink.get("done"))
+        dres = torch.empty_like(x, memory_format=torch.channels_last) if (ctx.has_res and not park) else None
         acc = acc4[2 * C:]
         # the consumer's dgrad epilogue already reduced sum(g), sum(g*xhat) into acc
         have_sums = bool(ctx.bn_link is not None and ctx.bn_link.pop("sums", False))
@@ -147,7 +165,9 @@ class _BnAct(torch.autograd.Function):
                                  dres.data_ptr() if dres is not None else 0, dw.data_ptr(), db.data_ptr(), M, C,
                                  ctx.relu, H, W, int(p), stream_handle(), int(have_sums),
                                  mb.data_ptr() if mb is not None else 0)
-        if ctx.res_sink is not None and dres is not None and not ctx.res_sink.get("done"):
+        if park:
+            ctx.res_sink["gm"] = (dy, mb)
+        elif ctx.res_sink is not None and dres is not None and not ctx.res_sink.get("done"):
             # consumed by the conv whose input is the residual (ops/conv.py); if that
             # conv's backward already ran ("done"), autograd sums the gradients instead
             ctx.res_sink["g"] = dres

@@ -266,7 +266,7 @@ class Conv1x1(torch.autograd.Function):
         s = stream_handle()
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = None
-        add = s2 = None
+        add = s2 = add_mask = None
         link = ctx.res_link
         if link is not None and link.get("expect") and ctx.needs_input_grad[0]:
             # the same input also fed another branch (the identity residual's
@@ -275,6 +275,9 @@ class Conv1x1(torch.autograd.Function):
             # (a stride-2 downsample parks its deferred dgrad instead: "s2")
             add = link.pop("g", None)
             s2 = link.pop("s2", None)
+            gm = link.pop("gm", None)  # (dy, mask bits): the residual gradient still to be masked
+            if gm is not None:
+                add, add_mask = gm
             if add is None and s2 is None:
                 # autograd ran this branch first (no ordering guarantee): the other
                 # branch returns its gradient through autograd, which sums them
@@ -294,7 +297,7 @@ class Conv1x1(torch.autograd.Function):
                     if s2 is None else None
                 try:
                     C.conv_fwd_add(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), add.data_ptr(), M, 1, 1, cout, cin,
-                                   1, tile, s)
+                                   1, tile, s, 0 if add_mask is None else add_mask.data_ptr())
                 finally:
                     if bst is not None:
                         _bn_disarm(C)
@@ -315,10 +318,18 @@ class Conv1x1(torch.autograd.Function):
                 if bst is not None:
                     _bn_reduce_end(C, ctx.bn_link, bst, T, s)
             if add is not None:
+                if add_mask is not None:  # (split-K dgrad: the masked residual gradient the slow way)
+                    from .bn_nhwc import unpack_mask_bits
+
+                    add = add.masked_fill(~unpack_mask_bits(add_mask, add), 0)
                 dx.add_(add)
             if s2 is not None:  # dx[:, ::2, ::2] += the stride-2 downsample's dgrad (in place)
                 Conv1x1S2.deferred_dgrad(C, s2[0], s2[1], s2[2], dx, s)
         elif add is not None:
+            if add_mask is not None:
+                from .bn_nhwc import unpack_mask_bits
+
+                add = add.masked_fill(~unpack_mask_bits(add_mask, add), 0)
             dx = add
         # fp32 weight gradient added into the flat buffer: split-K partials in plain
         # slabs + one reduce-add (atomic split-K adds were 1.3-2.3x slower on every
