@@ -197,3 +197,50 @@ def test_masked_residual_gradient_in_c1_dgrad(dev, monkeypatch, N, C, H, mid):
         assert _rel(a, b) < 1e-2
     for a, b in zip(on[:3], ref):
         assert _rel(a, b) < 3e-2
+
+
+@pytest.mark.parametrize("branch", ["identity", "downsample_s2"])
+def test_c1_backward_first_hand_over(dev, branch):
+    """x feeds c1 (Conv1x1 with a residual link) and a second
+    branch that hands its gradient of x to c1's dgrad (the identity residual's
+    BatchNorm: res_sink; the stride-2 downsample conv: dx_sink).  Force c1's
+    backward to run FIRST (separate backward calls): c1 marks the link done and
+    the other branch must return its gradient through autograd -- x.grad
+    equals the one joint backward where the hand-over happens."""
+    from torch_distlearn_amd.ops.bn_nhwc import bn_act
+    from torch_distlearn_amd.ops.conv import Conv1x1, Conv1x1S2, ShadowBinding
+
+    N, C, H, mid = 4, 256, 14, 64
+
+    def run(split):
+        g = torch.Generator(device=dev).manual_seed(12)
+        mk = lambda *s: torch.randn(*s, device=dev, generator=g).to(BF).contiguous(memory_format=CL)  # noqa: E731
+        x = mk(N, C, H, H).requires_grad_(True)
+        w1 = (torch.randn(mid, C, 1, 1, device=dev, generator=g) * C ** -0.5).to(BF)
+        b1 = ShadowBinding(w1.reshape(mid, C), torch.zeros(mid, C, device=dev), lambda: None)
+        link = {}
+        a = Conv1x1.apply(x, torch.nn.Parameter(w1.float()), b1, None, link, None, None)
+        if branch == "identity":
+            y3 = mk(N, C, H, H).requires_grad_(True)
+            gamma = torch.rand(C, device=dev, generator=g) + 0.5
+            beta = torch.randn(C, device=dev, generator=g) * 0.3
+            b = bn_act(y3, gamma, beta, None, None, residual=x, relu=True, acc=torch.zeros(4 * C, device=dev),
+                       have_stats=False, res_sink=link)
+        else:
+            wd = (torch.randn(2 * C, C, 1, 1, device=dev, generator=g) * C ** -0.5).to(BF)
+            bd = ShadowBinding(wd.reshape(2 * C, C), torch.zeros(2 * C, C, device=dev), lambda: None)
+            bd.wt = None
+            b = Conv1x1S2.apply(x, torch.nn.Parameter(wd.float()), bd, None, link)
+        ga, gb = mk(*a.shape), mk(*b.shape)
+        if split:  # c1's backward first, then the other branch's
+            a.backward(ga, retain_graph=True)
+            b.backward(gb)
+        else:
+            torch.autograd.backward([b, a], [gb, ga])
+        torch.cuda.synchronize()
+        return x.grad.float(), link
+
+    joint, _ = run(False)
+    first, link = run(True)
+    assert link.get("done")
+    assert _rel(first, joint) < 1e-2

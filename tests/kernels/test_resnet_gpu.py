@@ -203,3 +203,43 @@ def test_zero_border_only_touches_the_border(N, H, W, C, p):
     ring = torch.ones(H + 2 * p, W + 2 * p, dtype=torch.bool, device="cuda")
     ring[p:p + H, p:p + W] = False
     assert (buf[:, ring] == 0).all()
+
+
+def test_resnet50_eval_bn_on_hip_kernel(monkeypatch):
+    """ResNet-50 eval / predict runs its BatchNorms on the
+    same HIP apply kernel as training, from the running statistics (no fp32
+    copy, no F.batch_norm), after a few training steps: log-probabilities match
+    the F.batch_norm eval path (fp32 BN on the same bf16 activations) and the
+    predicted classes agree."""
+    from torch_distlearn_amd import Tree
+    from torch_distlearn_amd.engine import DataParallelTrainer
+    from torch_distlearn_amd.models import ResNet50
+    from torch_distlearn_amd.models import resnet as R
+
+    dev = torch.device("cuda", 0)
+    tree = Tree(1, 1, host="127.0.0.1", port=29581, device=dev)
+    model = ResNet50(num_classes=100, seed=0).to(dev)
+    tr = DataParallelTrainer(model, tree, lr=0.02, backend="torch", compute_dtype=torch.bfloat16, max_batch=32)
+    tr.synchronize_parameters()
+    g = torch.Generator(device=dev).manual_seed(3)
+    xs = torch.randn(4, 32, 64, 64, 3, device=dev, generator=g).to(torch.bfloat16)
+    ys = torch.randint(0, 100, (4, 32), device=dev, generator=g)
+    for k in range(3):
+        tr.step(xs[k], ys[k])
+    torch.cuda.synchronize()
+    calls = []
+    orig = R._BN.act
+
+    def spy(self, x, *a, **kw):
+        calls.append(self.hip_eval_ok(x, kw.get("residual")))
+        return orig(self, x, *a, **kw)
+
+    monkeypatch.setattr(R._BN, "act", spy)
+    lp_hip = tr.predict(xs[3]).float()
+    assert calls and all(calls), "eval BatchNorms did not take the HIP kernel"
+    monkeypatch.setattr(R, "_BN_EVAL_HIP", False)
+    lp_ref = tr.predict(xs[3]).float()
+    torch.cuda.synchronize()
+    rel = float((lp_hip - lp_ref).norm() / lp_ref.norm())
+    assert rel < 2e-2, rel
+    assert float((lp_hip.argmax(1) == lp_ref.argmax(1)).float().mean()) >= 0.9

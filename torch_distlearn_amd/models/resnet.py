@@ -32,6 +32,9 @@ import torch.nn.functional as F
 # fused with its ReLU / residual add on the channels-last HIP kernels
 # (ops/bn_nhwc.py, csrc/kernels/bn_nhwc.hip; default: 43.7 -> 35.5 ms/step).
 _BN_MODE = os.environ.get("DISTLEARN_RESNET_BN", "hip")
+# eval-mode BatchNorm (predict) on the same HIP apply kernel from the running
+# statistics (0: F.batch_norm on an fp32 copy)
+_BN_EVAL_HIP = os.environ.get("DISTLEARN_RESNET_BN_EVAL", "hip") == "hip"
 
 
 class _BN(nn.Module):
@@ -60,12 +63,27 @@ class _BN(nn.Module):
         return supported(x) and self.weight.dtype == torch.float32 and (
             residual is None or (residual.dtype == x.dtype and residual.shape == x.shape))
 
+    def hip_eval_ok(self, x, residual=None) -> bool:
+        if not (_BN_MODE == "hip" and not self.training and x.is_cuda and _BN_EVAL_HIP):
+            return False
+        if torch.is_grad_enabled() and (x.requires_grad or self.weight.requires_grad):
+            return False  # differentiable eval forward: the torch op
+        from ..ops.bn_nhwc import supported
+
+        return supported(x) and self.weight.dtype == torch.float32 and (
+            residual is None or (residual.dtype == x.dtype and residual.shape == x.shape))
+
     def act(self, x, relu: bool = True, residual=None, acc=None, res_sink=None, have_stats: bool = False,
             out_pad: int = 0, dx_pad: int = 0, bn_link=None):
         """act(BN(x) [+ residual]); one fused HIP kernel pair in "hip" mode
         (``acc`` with ``have_stats``: statistics already accumulated by the
         producing conv; else the step's zeroed arena slice, if any;
         ``out_pad`` / ``dx_pad``: zero-bordered output / input gradient)."""
+        if self.hip_eval_ok(x, residual):  # eval / predict: the same HIP kernel from the running statistics
+            from ..ops.bn_nhwc import bn_act_eval
+
+            return bn_act_eval(x, self.weight, self.bias, self.running_mean, self.running_var, residual, relu,
+                               out_pad=out_pad)
         if self.hip_ok(x, residual):
             from ..ops.bn_nhwc import bn_act
 

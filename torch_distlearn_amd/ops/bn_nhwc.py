@@ -179,6 +179,30 @@ class _BnAct(torch.autograd.Function):
                 None, None, None)
 
 
+@torch.no_grad()
+def bn_act_eval(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_mean: torch.Tensor,
+                running_var: torch.Tensor, residual: Optional[torch.Tensor] = None, relu: bool = True,
+                eps: float = 1e-5, out_pad: int = 0) -> torch.Tensor:
+    """Eval-mode ``act(BN(x) [+ residual])`` from the running statistics on
+    the same HIP apply kernel as training (the ResNet-50 predict path; no
+    fp32 copy, no MIOpen): the kernel derives mean / variance from a [2C]
+    (sum, sum of squares) pair, so it is given M*mean and M*(var + mean^2)
+    of the running statistics and the statistics pass is skipped.  No
+    running-statistics update; not differentiable."""
+    M, C = _geom(x)
+    N, _, H, W = x.shape
+    rm, rv = running_mean.float(), running_var.float()
+    acc = torch.cat([rm * M, (rv + rm * rm) * M])
+    save = torch.empty(2 * C, device=x.device, dtype=torch.float32)
+    y = padded_empty(N, C, H, W, out_pad, x.device) if out_pad else torch.empty_like(x, memory_format=torch.channels_last)
+    ybase = y.data_ptr() - (out_pad * (W + 2 * out_pad) + out_pad) * C * 2 if out_pad else y.data_ptr()
+    res = residual.contiguous(memory_format=torch.channels_last) if residual is not None else None
+    _bn().bn_nhwc_fwd_pad(x.data_ptr(), res.data_ptr() if res is not None else 0, ybase, acc.data_ptr(),
+                          weight.contiguous().data_ptr(), bias.contiguous().data_ptr(), save.data_ptr(), 0, 0, M, C,
+                          float(eps), 0.0, int(relu), 1, H, W, int(out_pad), stream_handle())
+    return y
+
+
 def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_mean: Optional[torch.Tensor],
            running_var: Optional[torch.Tensor], residual: Optional[torch.Tensor] = None, relu: bool = True,
            eps: float = 1e-5, momentum: float = 0.1, acc: Optional[torch.Tensor] = None,

@@ -26,7 +26,14 @@ all-reduced -- half the xGMI bytes per step -- while the header (participation
 count) is all-reduced in fp32 beside it in the same group.  The fused SGD
 reads the bf16 result directly (``AllReduceSGD.step``); API callers that read
 ``flat.grad`` get it widened back to fp32 by :meth:`finish`.  At world 1 the
-all-reduce is the identity and the wire stays fp32.
+all-reduce is the identity and the wire stays fp32.  Accuracy trade-off: the
+collective reduces in its wire dtype, so the gradient SUM is accumulated in
+bf16 at every ring hop -- on top of rounding each rank's gradient to bf16 the
+sum picks up about one bf16 rounding per hop, i.e. its relative error grows
+with the world size (measured bound: tests/distributed/test_allreduce_sgd.py
+test_bf16_wire_matches_fp32_wire, worlds 2-8).  Replicas stay bitwise
+identical (every rank applies the same reduced bytes).  The headline bench
+keeps the fp32 wire.
 
 Per-bucket update (:meth:`set_early_update`, used by the native executors):
 the fused SGD of a bucket's parameters runs on the comm stream right after
