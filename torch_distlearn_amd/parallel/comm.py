@@ -378,8 +378,15 @@ def init_communicator(rank: Optional[int] = None, world_size: Optional[int] = No
     port = port or _env_int("MASTER_PORT", 29500)
     dev = torch.device(device) if device is not None else torch.device("cpu")
     if not dist.is_initialized():
-        dist.init_process_group("gloo", init_method=f"tcp://{host}:{port}", rank=rank, world_size=world_size,
-                                timeout=datetime.timedelta(seconds=timeout_s))
+        if world_size == 1:
+            # one process: an in-memory store, no TCP listener (a port another
+            # process grabbed between the launcher's probe and this bind used to
+            # fail a single-node run with EADDRINUSE)
+            dist.init_process_group("gloo", store=dist.HashStore(), rank=0, world_size=1,
+                                    timeout=datetime.timedelta(seconds=timeout_s))
+        else:
+            dist.init_process_group("gloo", init_method=f"tcp://{host}:{port}", rank=rank, world_size=world_size,
+                                    timeout=datetime.timedelta(seconds=timeout_s))
     ctrl = dist.group.WORLD
     if backend == "auto":
         backend = "rccl" if dev.type == "cuda" else "gloo"
