@@ -24,6 +24,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("cast_bf16_f32", &cast_bf16_f32);
   m.def("sgd_update_g16", &sgd_update_g16);
   m.def("sgd_update_slabs", &sgd_update_slabs);
+  m.def("arm_sgd_next_prep", &arm_sgd_next_prep);
+  m.def("sgd_next_prep_armed", &sgd_next_prep_armed);
+  m.def("disarm_sgd_next_prep", &disarm_sgd_next_prep);
   m.def("set_conv_side_sgd", &set_conv_side_sgd);
   m.def("confusion_update", &confusion_update);
   m.def("bn_nhwc_fwd", &bn_nhwc_fwd);

@@ -34,6 +34,15 @@ void sgd_update_slabs(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, ui
                       float momentum, float wd, int64_t n, std::vector<int64_t> offs, std::vector<int64_t> lens,
                       std::vector<uintptr_t> slabs, std::vector<int> splits, std::vector<int64_t> tail,
                       uintptr_t tail_slab, int64_t skip_lo, int64_t skip_hi, uintptr_t stream);
+// one-shot: the next sgd_update_slabs launch also prepares the next step of an
+// unrolled graph -- gathers its batch into xp, zeroes its accumulators (prep_dev.h)
+// and writes the tail (first layer) weights into the packed bf16 operand w1p
+void arm_sgd_next_prep(uintptr_t img, uintptr_t order, uintptr_t lab_all, uintptr_t lab_out, uintptr_t ctr,
+                       int n_order, int B, int C, std::vector<float> mean, std::vector<float> stdv, uintptr_t xp,
+                       int Cp, int H, int W, int sp, std::vector<uintptr_t> zp, std::vector<int64_t> zn,
+                       uintptr_t w1p, int w1_cp);
+bool sgd_next_prep_armed();
+void disarm_sgd_next_prep();
 
 // metrics.hip ---------------------------------------------------------------
 // channels-last training BatchNorm (+ReLU, +residual) for the ResNet-50 path

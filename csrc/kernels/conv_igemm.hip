@@ -27,6 +27,7 @@
 #include "dl_common.h"
 #include "dl_ops.h"
 #include "slab_reduce_dev.h"
+#include "prep_dev.h"
 #include "sgd_dev.h"
 #include "wtrans_dev.h"
 
@@ -1954,94 +1955,13 @@ __global__ void __launch_bounds__(256) pad_channels_kernel(const bf16_t* __restr
 // Job = blockIdx range; each transpose block moves one 32x32 (co, ci) tile of
 // one tap through LDS.
 // --------------------------------------------------------------------------
-struct PrepArgs {
-  const bf16_t* x; bf16_t* xp; int P; int C, Cp;                // input pad (channels + spatial)
-  int H, W, sp;                                                 // image dims, spatial zero pad
-  // device-side data path (img != nullptr): gather + normalise the step's
-  // batch straight from the HBM-resident uint8 dataset
-  const uint8_t* img; const int* order; const int64_t* lab_all; int64_t* lab_out;
-  const unsigned long long* ctr;  // [0] = step counter (advanced by head_wgrad)
-  int n_order, B;
-  float mean[3], inv_std[3];
-  const float* w1; bf16_t* w1p; int w1_cout, taps, w1_c, w1_cp;  // layer-1 pack
-  int nt;                                                        // transposes
-  const bf16_t* tw[4]; bf16_t* twt[4]; int tcout[4], tcin[4];
-  int nb_pad, nb_pack, nb_t[4];
-  int quad;  // fast gather/pad path: one block per image, 4 pixels per thread
-  // zero job: the step's atomic accumulators (BN statistics, BN parameter
-  // gradients, split-K weight gradients) -- float4 granularity
-  int nz, nb_zero;
-  float* zp[8];
-  int zn4[8];
-};
-
+// (PrepArgs and the pad / zero jobs: prep_dev.h, shared with the SGD launch
+// that prepares the next step of an unrolled graph.)
 __global__ void __launch_bounds__(256) prep_step_kernel(const PrepArgs a) {
   __shared__ bf16_t t[32][33];
   int blk = blockIdx.x;
-  if (blk < a.nb_pad && a.quad) {
-    // fast path (3 -> 8 channels, W % 4 == 0): block = one image, thread =
-    // 4 consecutive pixels of one row; every load of a thread is issued
-    // before the first use (one dependent round trip for the sample index,
-    // one for the pixels) and the 4 padded pixels go out as 64 contiguous B
-    const int HW = a.H * a.W, Hp = a.H + 2 * a.sp, Wp = a.W + 2 * a.sp;
-    const int b = blk;
-    int smp = 0;
-    if (a.img) {
-      const unsigned long long step = *a.ctr;  // advanced by head_wgrad later in the step
-      const int pos = (int)((step * (unsigned long long)a.B + (unsigned long long)b) % (unsigned)a.n_order);
-      smp = a.order[pos];
-      if (threadIdx.x == 0) a.lab_out[b] = a.lab_all[smp];
-    }
-    for (int q4 = threadIdx.x; q4 < HW / 4; q4 += 256) {
-      const int r = q4 * 4, h = r / a.W, w = r - h * a.W;
-      float f[12];
-      if (a.img) {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.img + ((int64_t)smp * HW + r) * 3);
-        const uint32_t d0 = src[0], d1 = src[1], d2 = src[2];
-        const uint32_t d[3] = {d0, d1, d2};
-#pragma unroll
-        for (int k = 0; k < 12; ++k) {
-          const float u = (float)((d[k >> 2] >> (8 * (k & 3))) & 0xffu);
-          f[k] = (u * (1.0f / 255.0f) - a.mean[k % 3]) * a.inv_std[k % 3];
-        }
-      } else {
-        const uint2* src = reinterpret_cast<const uint2*>(a.x + ((int64_t)b * HW + r) * 3);
-        const uint2 e0 = src[0], e1 = src[1], e2 = src[2];
-        const uint32_t d[6] = {e0.x, e0.y, e1.x, e1.y, e2.x, e2.y};
-#pragma unroll
-        for (int k = 0; k < 12; ++k) f[k] = (k & 1) ? hi_bf16(d[k >> 1]) : lo_bf16(d[k >> 1]);
-      }
-      uint4* dst = reinterpret_cast<uint4*>(a.xp + (((int64_t)b * Hp + h + a.sp) * Wp + w + a.sp) * 8);
-#pragma unroll
-      for (int px = 0; px < 4; ++px)
-        dst[px] = make_uint4(pack_bf16x2(f[3 * px], f[3 * px + 1]), pack_bf16x2(f[3 * px + 2], 0.f), 0u, 0u);
-    }
-    return;
-  }
   if (blk < a.nb_pad) {
-    const int HW = a.H * a.W, Hp = a.H + 2 * a.sp, Wp = a.W + 2 * a.sp;
-    // step counter: advanced by head_wgrad later in the same step (stream order)
-    const unsigned long long step = a.img ? *a.ctr : 0ull;
-    for (int p = blk * 256 + threadIdx.x; p < a.P; p += a.nb_pad * 256) {
-      const int b = p / HW;
-      const int r = p - b * HW, h = r / a.W, w = r - h * a.W;
-      bf16_t v[16];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) v[c] = 0;
-      if (a.img) {
-        // sample of this step = order[(step * B + b) mod n_order]
-        const int pos = (int)((step * (unsigned long long)a.B + (unsigned long long)b) % (unsigned)a.n_order);
-        const int smp = a.order[pos];
-        const uint8_t* src = a.img + ((int64_t)smp * HW + r) * a.C;
-        for (int c = 0; c < a.C && c < 3; ++c) v[c] = f32_to_bf16((src[c] * (1.0f / 255.0f) - a.mean[c]) * a.inv_std[c]);
-        if (r == 0) a.lab_out[b] = a.lab_all[smp];
-      } else {
-        for (int c = 0; c < a.C; ++c) v[c] = a.x[(int64_t)p * a.C + c];
-      }
-      const int64_t q = ((int64_t)b * Hp + h + a.sp) * Wp + w + a.sp;  // interior of the zero-bordered buffer
-      for (int c = 0; c < a.Cp; c += 8)
-        *reinterpret_cast<uint4*>(a.xp + q * a.Cp + c) = *reinterpret_cast<const uint4*>(v + c);
-    }
+    prep_pad_block(a, blk);
     return;
   }
   blk -= a.nb_pad;
@@ -2055,14 +1975,7 @@ __global__ void __launch_bounds__(256) prep_step_kernel(const PrepArgs a) {
   }
   blk -= a.nb_pack;
   if (blk < a.nb_zero) {
-    int64_t total = 0;
-    for (int j = 0; j < a.nz; ++j) total += a.zn4[j];
-    for (int64_t i = (int64_t)blk * 256 + threadIdx.x; i < total; i += (int64_t)a.nb_zero * 256) {
-      int64_t r = i;
-      int j = 0;
-      while (r >= a.zn4[j]) { r -= a.zn4[j]; ++j; }
-      reinterpret_cast<float4*>(a.zp[j])[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    prep_zero_block(a, blk);
     return;
   }
   blk -= a.nb_zero;
@@ -2101,27 +2014,12 @@ static void launch_prep(PrepArgs& a, int64_t P, uintptr_t w1, uintptr_t w1p, int
                         int w1_cp, const std::vector<uintptr_t>& tw, const std::vector<uintptr_t>& twt,
                         const std::vector<int>& tcout, const std::vector<int>& tcin,
                         const std::vector<uintptr_t>& zp, const std::vector<int64_t>& zn, uintptr_t stream) {
-  if (zp.size() != zn.size() || zp.size() > 8) throw std::runtime_error("prep_step: up to 8 zero ranges");
-  a.nz = (int)zp.size();
-  int64_t z4 = 0;
-  for (int j = 0; j < a.nz; ++j) {
-    if (zn[j] % 4 != 0 || zp[j] % 16 != 0 || zn[j] <= 0 || zn[j] / 4 >= (1ll << 31))
-      throw std::runtime_error("prep_step: zero ranges must be 16-byte aligned multiples of 4 floats");
-    a.zp[j] = (float*)zp[j];
-    a.zn4[j] = (int)(zn[j] / 4);
-    z4 += zn[j] / 4;
-  }
-  a.nb_zero = (int)std::min<int64_t>((z4 + 1023) / 1024, 256);
-  if (a.C > 16 || a.Cp > 16 || a.Cp % 8 != 0) throw std::runtime_error("prep_step: input channels must pad to 8 or 16");
-  if (P >= (1ll << 31)) throw std::runtime_error("prep_step: too many pixels");
-  if (P > 0 && (a.H <= 0 || a.W <= 0 || P % ((int64_t)a.H * a.W) != 0)) throw std::runtime_error("prep_step: P != B*H*W");
-  a.P = (int)P;
+  prep_set_zero(a, zp, zn);
+  prep_set_pad(a, P);
   a.w1 = (const float*)w1; a.w1p = (bf16_t*)w1p; a.w1_cout = w1_cout; a.taps = taps; a.w1_c = w1_c; a.w1_cp = w1_cp;
   a.nt = (int)tw.size();
   if (a.nt > 4 || twt.size() != tw.size() || tcout.size() != tw.size() || tcin.size() != tw.size())
     throw std::runtime_error("prep_step: up to 4 consistent transposes");
-  a.quad = (a.C == 3 && a.Cp == 8 && P > 0 && a.W % 4 == 0) ? 1 : 0;
-  a.nb_pad = a.quad ? (int)(P / ((int64_t)a.H * a.W)) : (int)std::min<int64_t>((P + 255) / 256, 1024);
   a.nb_pack = (int)std::min<int64_t>(((int64_t)w1_cout * taps * w1_cp + 255) / 256, 256);
   int total = a.nb_pad + a.nb_pack + a.nb_zero;
   for (int j = 0; j < a.nt; ++j) {
@@ -2156,16 +2054,9 @@ void prep_step_gather(uintptr_t img, uintptr_t order, uintptr_t lab_all, uintptr
                       int Cp, int H, int W, int sp, uintptr_t w1, uintptr_t w1p, int w1_cout, int taps, int w1_c,
                       int w1_cp, std::vector<uintptr_t> tw, std::vector<uintptr_t> twt, std::vector<int> tcout,
                       std::vector<int> tcin, std::vector<uintptr_t> zp, std::vector<int64_t> zn, uintptr_t stream) {
-  if (C > 3 || mean.size() < (size_t)C || stdv.size() < (size_t)C) throw std::runtime_error("prep_step_gather: C <= 3");
-  if (n_order <= 0 || B <= 0) throw std::runtime_error("prep_step_gather: empty order / batch");
   PrepArgs a{};
   a.xp = (bf16_t*)xp; a.C = C; a.Cp = Cp; a.H = H; a.W = W; a.sp = sp;
-  a.img = (const uint8_t*)img; a.order = (const int*)order; a.lab_all = (const int64_t*)lab_all;
-  a.lab_out = (int64_t*)lab_out; a.ctr = (const unsigned long long*)ctr; a.n_order = n_order; a.B = B;
-  for (int c = 0; c < 3; ++c) {
-    a.mean[c] = c < C ? mean[c] : 0.f;
-    a.inv_std[c] = c < C ? 1.0f / stdv[c] : 1.f;
-  }
+  prep_set_gather(a, img, order, lab_all, lab_out, ctr, n_order, B, C, mean, stdv);
   launch_prep(a, (int64_t)B * H * W, w1, w1p, w1_cout, taps, w1_c, w1_cp, tw, twt, tcout, tcin, zp, zn, stream);
 }
 

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "dl_common.h"
+#include "prep_dev.h"
 #include "sgd_dev.h"
 
 namespace dl {
@@ -64,14 +65,30 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, const G
   }
 }
 
+// Blocks: [next step's pad/gather | next step's zero job | update | tail].
+// `next` (nb_pad = nb_zero = 0: none) prepares the following step of an
+// unrolled graph in the same launch -- its input batch and zeroed
+// accumulators; the tail writes the first layer's packed operand -- so that
+// step runs without a prep launch of its own.
 template <bool kMomentum, bool kShadow>
-__global__ void __launch_bounds__(256) sgd_slabs_kernel(const SgdJob job) {
-  const int nmain = (int)gridDim.x - job.r.tail_nblk;
-  if ((int)blockIdx.x >= nmain) {
-    sgd_tail_block<kMomentum, kShadow>(job, (int)blockIdx.x - nmain);
+__global__ void __launch_bounds__(256) sgd_slabs_kernel(const SgdJob job, const PrepArgs next) {
+  int blk = (int)blockIdx.x;
+  if (blk < next.nb_pad) {
+    prep_pad_block(next, blk);
     return;
   }
-  sgd_range_loop<kMomentum, kShadow>(job, (int)blockIdx.x, nmain);
+  blk -= next.nb_pad;
+  if (blk < next.nb_zero) {
+    prep_zero_block(next, blk);
+    return;
+  }
+  blk -= next.nb_zero;
+  const int nmain = (int)gridDim.x - next.nb_pad - next.nb_zero - job.r.tail_nblk;
+  if (blk >= nmain) {
+    sgd_tail_block<kMomentum, kShadow>(job, blk - nmain);
+    return;
+  }
+  sgd_range_loop<kMomentum, kShadow>(job, blk, nmain);
 }
 
 // x *= 1/n (n read from the all-reduced participation slot)
@@ -191,6 +208,34 @@ void sgd_update(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, uintptr_
   DL_HIP_CHECK(hipGetLastError());
 }
 
+// One-shot: the next sgd_update_slabs launch also prepares the next step
+// (prep_dev.h jobs + the first layer's packed weights from its tail range).
+static PrepArgs g_next_prep{};
+static bool g_next_armed = false;
+static bf16_t* g_next_pack = nullptr;
+static int g_next_pack_cp = 0;
+
+void arm_sgd_next_prep(uintptr_t img, uintptr_t order, uintptr_t lab_all, uintptr_t lab_out, uintptr_t ctr,
+                       int n_order, int B, int C, std::vector<float> mean, std::vector<float> stdv, uintptr_t xp,
+                       int Cp, int H, int W, int sp, std::vector<uintptr_t> zp, std::vector<int64_t> zn,
+                       uintptr_t w1p, int w1_cp) {
+  if (g_next_armed) throw std::runtime_error("arm_sgd_next_prep: already armed (no sgd_update_slabs consumed it)");
+  if (!xp || !w1p || w1_cp < C) throw std::runtime_error("arm_sgd_next_prep: input buffer / packed weights");
+  PrepArgs a{};
+  a.xp = (bf16_t*)xp; a.C = C; a.Cp = Cp; a.H = H; a.W = W; a.sp = sp;
+  prep_set_gather(a, img, order, lab_all, lab_out, ctr, n_order, B, C, mean, stdv);
+  prep_set_pad(a, (int64_t)B * H * W);
+  prep_set_zero(a, zp, zn);
+  g_next_prep = a;
+  g_next_pack = (bf16_t*)w1p;
+  g_next_pack_cp = w1_cp;
+  g_next_armed = true;
+}
+
+bool sgd_next_prep_armed() { return g_next_armed; }
+
+void disarm_sgd_next_prep() { g_next_armed = false; }
+
 void sgd_update_slabs(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, uintptr_t slot, float lr,
                       float momentum, float wd, int64_t n, std::vector<int64_t> offs, std::vector<int64_t> lens,
                       std::vector<uintptr_t> slabs, std::vector<int> splits, std::vector<int64_t> tail,
@@ -203,13 +248,22 @@ void sgd_update_slabs(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, ui
     job.skip_hi4 = skip_hi / 4;
   }
   const int64_t n4 = n / 4;
+  PrepArgs next{};
+  if (g_next_armed) {
+    g_next_armed = false;
+    if (job.r.tail_nblk == 0 || job.r.tail_c != g_next_prep.C)
+      throw std::runtime_error("sgd_update_slabs: preparing the next step needs the first layer as the tail range");
+    next = g_next_prep;
+    job.tail_pack = g_next_pack;
+    job.tail_pack_cp = g_next_pack_cp;
+  }
   if (n4 == 0) return;
-  dim3 grid(stream_grid(n4) + job.r.tail_nblk), block(256);
+  dim3 grid(stream_grid(n4) + job.r.tail_nblk + next.nb_pad + next.nb_zero), block(256);
   auto s = as_stream(stream);
-  if (mom && p16) sgd_slabs_kernel<true, true><<<grid, block, 0, s>>>(job);
-  else if (mom) sgd_slabs_kernel<true, false><<<grid, block, 0, s>>>(job);
-  else if (p16) sgd_slabs_kernel<false, true><<<grid, block, 0, s>>>(job);
-  else sgd_slabs_kernel<false, false><<<grid, block, 0, s>>>(job);
+  if (mom && p16) sgd_slabs_kernel<true, true><<<grid, block, 0, s>>>(job, next);
+  else if (mom) sgd_slabs_kernel<true, false><<<grid, block, 0, s>>>(job, next);
+  else if (p16) sgd_slabs_kernel<false, true><<<grid, block, 0, s>>>(job, next);
+  else sgd_slabs_kernel<false, false><<<grid, block, 0, s>>>(job, next);
   DL_HIP_CHECK(hipGetLastError());
 }
 

@@ -395,7 +395,10 @@ def test_deferred_slab_reduce_is_bitwise(dev, monkeypatch, momentum):
     summed on 8 lanes + a shuffle tree, 5 sequentially, and the first layer's
     channel-padded 128 splits on 32 lanes in extra blocks of the launch);
     with the side job, blocks 3-4 and the classifier are updated by extra
-    workgroups of block 3's dgrad launch -- still bitwise the same."""
+    workgroups of block 3's dgrad launch -- still bitwise the same; and with
+    the update launch preparing the next step of the unrolled graph (its
+    batch gathered, accumulators zeroed, first-layer operand packed: the
+    executor's arm_next_prep) -- still bitwise, across an epoch boundary."""
     from torch_distlearn_amd import Tree
     from torch_distlearn_amd.data import DeviceLoader, PartitionedDataset, synthetic_cifar10
     from torch_distlearn_amd.engine import DataParallelTrainer
@@ -403,9 +406,10 @@ def test_deferred_slab_reduce_is_bitwise(dev, monkeypatch, momentum):
 
     imgs, labels = synthetic_cifar10(1024, seed=5)
     outs = []
-    for defer, side in (("0", "0"), ("1", "0"), ("1", "1")):
+    for defer, side, nxt in (("0", "0", "0"), ("1", "0", "0"), ("1", "1", "0"), ("1", "1", "1")):
         monkeypatch.setenv("DISTLEARN_DEFER_SLABS", defer)
         monkeypatch.setenv("DISTLEARN_SIDE_SGD", side)
+        monkeypatch.setenv("DISTLEARN_PREP_NEXT", nxt)
         tree = Tree(1, 1, host="127.0.0.1", port=29712, device=dev)
         model = CifarConvNet(seed=4).to(dev)
         tr = DataParallelTrainer(model, tree, lr=0.02, momentum=momentum, backend="hip",
@@ -423,10 +427,12 @@ def test_deferred_slab_reduce_is_bitwise(dev, monkeypatch, momentum):
         else:
             assert tr._slabs is None and tr._side is None
         ld = DeviceLoader(PartitionedDataset(imgs, labels, device=dev), "permutation", 128, seed=2)
-        tr.run(ld, 7, unroll=4)
+        tr.run(ld, 11, unroll=4)  # 8 steps per epoch: graphs of 4, 2, 1 steps, then a new epoch
         torch.cuda.synchronize()
+        assert (tr.executor.prepared_ahead > 0) == (nxt == "1")
+        assert not tr.executor.C.sgd_next_prep_armed()
         outs.append(tr.flat.data.clone())
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
 
 
 def test_policy_selected_on_the_machine(dev, monkeypatch):

@@ -168,10 +168,12 @@ class DataParallelTrainer:
         loss.backward()
         return loss.detach()
 
-    def _step_body(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    def _step_body(self, x: torch.Tensor, y: torch.Tensor, prep_next: bool = False) -> torch.Tensor:
         """The capturable part of a step: zero grads, forward, backward and
         the update (SGD: bucketed all-reduce + fused 1/n SGD; EA: the local
-        SGD step -- the elastic round every tau steps runs after it)."""
+        SGD step -- the elastic round every tau steps runs after it).
+        ``prep_next``: another step on the same DeviceLoader follows in the
+        same graph; the update launch prepares it (executor arm_next_prep)."""
         f = self.flat
         # zero grads, participation slot = 1 (this node contributes this round);
         # a native executor that overwrites every gradient sets the slot itself
@@ -182,6 +184,10 @@ class DataParallelTrainer:
             labels = x.labels_out if hasattr(x, "gather_args") else y
             for h in self.step_hooks:
                 h(self.last_logits(), labels)
+        if prep_next and self._slabs is not None and os.environ.get("DISTLEARN_PREP_NEXT", "1") == "1":
+            arm = getattr(self.executor, "arm_next_prep", None)
+            if arm is not None:
+                arm(x)
         if self.algo == "sgd":
             self.sgd.step(f, self.lr, momentum=self.momentum, weight_decay=self.weight_decay,
                           momentum_buf=self.mom, slabs=self._slabs, skip=self._side)
@@ -445,8 +451,8 @@ class DataParallelTrainer:
         n = k[1] if ea_round else k
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            for _ in range(n):
-                loss = self._step_body(loader, None)
+            for j in range(n):
+                loss = self._step_body(loader, None, prep_next=j + 1 < n)
             if ea_round:
                 self.ea.elastic_round()
         if self.sgd is not None:

@@ -277,6 +277,8 @@ class CifarHIPExecutor:
         self.rows = {0: 0, 1: 1, 2: int(os.environ.get("DISTLEARN_REDUCE_ROWS", "16"))}[self.mode]
         self._alloc(self.B)
         self._deferred = ()  # blocks whose weight-gradient slab reduce the update performs (defer_slab_reduce)
+        self._prefetched = False  # the coming step was prepared by the last update launch (arm_next_prep)
+        self.prepared_ahead = 0   # steps armed that way (counted at capture)
         self._side = None    # side SGD carried by a dgrad launch (side_update)
 
     # ------------------------------------------------------------------ buffers
@@ -471,7 +473,16 @@ class CifarHIPExecutor:
             ctr = x.ctr.data_ptr()  # advanced by head_wgrad after the gather read it
         if labels.dtype != torch.int64:
             raise ValueError("labels must be int64")
-        B = self._prep(x, s, with_transposes=not (self.fork_transposes or self.head_transposes))
+        if self._prefetched:  # the previous step's update launch prepared this one (arm_next_prep)
+            self._prefetched = False
+            if self.C.sgd_next_prep_armed():
+                self.C.disarm_sgd_next_prep()
+                raise RuntimeError("arm_next_prep: no update launch consumed the next-step preparation")
+            if not hasattr(x, "gather_args"):
+                raise RuntimeError("arm_next_prep: the prepared step must run on the same DeviceLoader")
+            B = x.batch
+        else:
+            B = self._prep(x, s, with_transposes=not (self.fork_transposes or self.head_transposes))
         self._last_b = B
         if self.fork_transposes:  # dgrad weight transposes overlap the forward
             side.wait_stream(main)
@@ -729,6 +740,31 @@ class CifarHIPExecutor:
         self._deferred = tuple(blocks)
         return [(self._leaf(i, 0), self.wslab_l[i], self.wplan[i][1], self.couts[i], taps, self.cins[i],
                  self.cins_real[i]) for i in blocks]
+
+    def arm_next_prep(self, loader) -> bool:
+        """Let the coming update launch (flat_sgd_ with the deferred slabs)
+        prepare the NEXT step on ``loader`` in extra workgroups: gather +
+        normalise its batch into the layer-1 buffer, zero its accumulators,
+        and write the updated first-layer weights straight into their packed
+        operand (the update's tail range) -- so the next :meth:`forward_backward`
+        skips its prep launch.  For consecutive steps of an unrolled graph
+        (engine.py _capture_multi); the step counter the gather reads was
+        advanced by this step's head kernel.  False (nothing armed) when the
+        update cannot carry it: the first layer's slab reduce not deferred,
+        the dgrad transposes in the prep launch, no device loader."""
+        if (not hasattr(loader, "gather_args") or 0 not in self._deferred or self.cins[0] == self.cins_real[0]
+                or self.fork_transposes or not self.head_transposes or loader.batch > self.cap):
+            return False
+        h = self.hs[0]
+        img, order, lab_all, lab_out, ctr, n_order, C, mean, std = loader.gather_args()
+        if (loader.H, loader.W, C) != (h, h, self.cins_real[0]):
+            return False
+        self.C.arm_sgd_next_prep(img, order, lab_all, lab_out, ctr, n_order, loader.batch, C, mean, std,
+                                 self.x8.data_ptr(), CIN_PAD, h, h, SPAD, *self._zero_args(True),
+                                 self.w1p.data_ptr(), CIN_PAD)
+        self._prefetched = True
+        self.prepared_ahead += 1
+        return True
 
     def _region_dgrad(self, i: int, B: int) -> bool:
         """Whether block i's (unsplit) dgrad runs on the region (tap-reuse)
