@@ -26,6 +26,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("sgd_update_slabs", &sgd_update_slabs);
   m.def("arm_sgd_next_prep", &arm_sgd_next_prep);
   m.def("sgd_next_prep_armed", &sgd_next_prep_armed);
+  m.def("set_sgd_trim", &set_sgd_trim);
   m.def("disarm_sgd_next_prep", &disarm_sgd_next_prep);
   m.def("set_conv_side_sgd", &set_conv_side_sgd);
   m.def("confusion_update", &confusion_update);

@@ -42,6 +42,7 @@ void arm_sgd_next_prep(uintptr_t img, uintptr_t order, uintptr_t lab_all, uintpt
                        int Cp, int H, int W, int sp, std::vector<uintptr_t> zp, std::vector<int64_t> zn,
                        uintptr_t w1p, int w1_cp);
 bool sgd_next_prep_armed();
+void set_sgd_trim(bool on);  // update grid sized to the elements before a skipped suffix (default on)
 void disarm_sgd_next_prep();
 
 // metrics.hip ---------------------------------------------------------------

@@ -208,6 +208,10 @@ void sgd_update(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, uintptr_
   DL_HIP_CHECK(hipGetLastError());
 }
 
+// size the update grid to the elements left after a skipped suffix (A/B)
+static bool g_sgd_trim = true;
+void set_sgd_trim(bool on) { g_sgd_trim = on; }
+
 // One-shot: the next sgd_update_slabs launch also prepares the next step
 // (prep_dev.h jobs + the first layer's packed weights from its tail range).
 static PrepArgs g_next_prep{};
@@ -246,6 +250,11 @@ void sgd_update_slabs(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, ui
     if (skip_lo % 4 || skip_hi % 4 || skip_lo < 0 || skip_hi > n) throw std::runtime_error("sgd_update_slabs: bad skip");
     job.skip_lo4 = skip_lo / 4;
     job.skip_hi4 = skip_hi / 4;
+    if (skip_hi == n && g_sgd_trim) {
+      // a skipped suffix (the side job's range): the grid covers only the rest
+      // (the tail blocks cover their own range)
+      job.hi4 = std::max(job.lo4, job.skip_lo4);
+    }
   }
   const int64_t n4 = n / 4;
   PrepArgs next{};
@@ -258,7 +267,7 @@ void sgd_update_slabs(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, ui
     job.tail_pack_cp = g_next_pack_cp;
   }
   if (n4 == 0) return;
-  dim3 grid(stream_grid(n4) + job.r.tail_nblk + next.nb_pad + next.nb_zero), block(256);
+  dim3 grid(stream_grid(job.hi4 - job.lo4) + job.r.tail_nblk + next.nb_pad + next.nb_zero), block(256);
   auto s = as_stream(stream);
   if (mom && p16) sgd_slabs_kernel<true, true><<<grid, block, 0, s>>>(job, next);
   else if (mom) sgd_slabs_kernel<true, false><<<grid, block, 0, s>>>(job, next);

@@ -1,14 +1,14 @@
 """Per-step kernel timeline from a rocprofv3 kernel-trace database: for one
 steady-state step (delimited by a marker kernel), list each kernel's duration
 and the idle gap before it; summarise busy vs. idle time per step.
-    python scripts/prof_timeline.py <db> [--marker prep_step] [--step -5]"""
+    python scripts/prof_timeline.py <db> [--marker conv_fwd_c8] [--step -5]"""
 import sqlite3
 import sys
 
 
 def main():
     db = sys.argv[1]
-    marker = sys.argv[sys.argv.index("--marker") + 1] if "--marker" in sys.argv else "prep_step"
+    marker = sys.argv[sys.argv.index("--marker") + 1] if "--marker" in sys.argv else "conv_fwd_c8"
     which = int(sys.argv[sys.argv.index("--step") + 1]) if "--step" in sys.argv else -5
     c = sqlite3.connect(db)
     rows = sorted(c.execute("select name, start, end from kernels"), key=lambda r: r[1])

@@ -206,6 +206,8 @@ class CifarHIPExecutor:
             self.C.set_conv_fwd_pf(int(os.environ["DISTLEARN_FWD_PF"]))
         if "DISTLEARN_WGRAD_ORDER" in os.environ:  # A/B: wgrad DMA before (1) or after (0) the fragment reads
             self.C.set_conv_wgrad_order(int(os.environ["DISTLEARN_WGRAD_ORDER"]))
+        if "DISTLEARN_SGD_TRIM" in os.environ:  # A/B: update grid sized to the range left after the side job's
+            self.C.set_sgd_trim(os.environ["DISTLEARN_SGD_TRIM"] == "1")
         if "DISTLEARN_WGRAD_PF" in os.environ:  # tuning: wgrad fragment prefetch (-1 auto, 0, 1)
             self.C.set_conv_wgrad_pf(int(os.environ["DISTLEARN_WGRAD_PF"]))
         # fuse the last block's BN/ReLU/pool into the head kernel (2048 pooled features)
