@@ -29,6 +29,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_sgd_trim", &set_sgd_trim);
   m.def("disarm_sgd_next_prep", &disarm_sgd_next_prep);
   m.def("set_conv_side_sgd", &set_conv_side_sgd);
+  m.def("set_conv_pool_load", &set_conv_pool_load);
+  m.def("conv_pool_load_ok", &conv_pool_load_ok);
   m.def("confusion_update", &confusion_update);
   m.def("bn_nhwc_fwd", &bn_nhwc_fwd);
   m.def("bn_nhwc_bwd", &bn_nhwc_bwd);

@@ -26,6 +26,39 @@ struct BnFin {
   int R;              // accumulated rows in sums
 };
 
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  f[0] = lo_bf16(v.x); f[1] = hi_bf16(v.x); f[2] = lo_bf16(v.y); f[3] = hi_bf16(v.y);
+  f[4] = lo_bf16(v.z); f[5] = hi_bf16(v.z); f[6] = lo_bf16(v.w); f[7] = hi_bf16(v.w);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]),
+                    pack_bf16x2(f[6], f[7]));
+}
+
+// The forward BN -> ReLU -> 2x2 max-pool of 8 channels: max over the window
+// v0..v3 of relu(sc*y + sh) (bf16 in / out).  Shared by the BN consumer
+// kernel (bn_pool.hip) and the conv that pools its input on load
+// (conv_igemm.hip, region kernel PL), so both produce the same bits.
+__device__ __forceinline__ uint4 bn_relu_pool8(const uint4& v0, const uint4& v1, const uint4& v2, const uint4& v3,
+                                               const float* sc_, const float* sh_) {
+  float sc[8], sh[8], f[8], mx[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { sc[k] = sc_[k]; sh[k] = sh_[k]; }
+  unpack8(v0, f);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) mx[k] = fmaf(sc[k], f[k], sh[k]);
+  unpack8(v1, f);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) mx[k] = fmaxf(mx[k], fmaf(sc[k], f[k], sh[k]));
+  unpack8(v2, f);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) mx[k] = fmaxf(mx[k], fmaf(sc[k], f[k], sh[k]));
+  unpack8(v3, f);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) mx[k] = fmaxf(fmaxf(mx[k], fmaf(sc[k], f[k], sh[k])), 0.f);
+  return pack8(mx);
+}
+
 constexpr int kFinMaxC = 1024;  // channels of the block-cooperative (LDS) coefficient tables
 constexpr int kMaxRows = 32;    // accumulated rows (set_reduce_atomic caps R at 64; the executors use <= 32)
 

@@ -80,14 +80,7 @@ void set_bn_minw(int fwd, int bwd) {
   g_bn_minw_bwd = bwd;
 }
 
-__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
-  f[0] = lo_bf16(v.x); f[1] = hi_bf16(v.x); f[2] = lo_bf16(v.y); f[3] = hi_bf16(v.y);
-  f[4] = lo_bf16(v.z); f[5] = hi_bf16(v.z); f[6] = lo_bf16(v.w); f[7] = hi_bf16(v.w);
-}
-__device__ __forceinline__ uint4 pack8(const float* f) {
-  return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]),
-                    pack_bf16x2(f[6], f[7]));
-}
+// (unpack8 / pack8 / bn_relu_pool8: bn_fin_dev.h)
 
 // Per-channel column sums of partial rows [T][2][C] (stat 0 at +0, stat 1 at
 // +C), one block per channel: every thread issues the loads of 4 rows before
@@ -245,21 +238,7 @@ __global__ void __launch_bounds__(256, MINW) bn_relu_pool_fwd_fin_kernel(const b
   bn_fin_block(fin, C, ssc, ssh);
   BN_STAMP(0, C, 1);
   for (; i < total;) {
-    float sc[8], sh[8], f[8], mx[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { sc[k] = ssc[c0 + k]; sh[k] = ssh[c0 + k]; }
-    unpack8(v[0], f);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) mx[k] = fmaf(sc[k], f[k], sh[k]);
-    unpack8(v[1], f);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) mx[k] = fmaxf(mx[k], fmaf(sc[k], f[k], sh[k]));
-    unpack8(v[2], f);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) mx[k] = fmaxf(mx[k], fmaf(sc[k], f[k], sh[k]));
-    unpack8(v[3], f);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) mx[k] = fmaxf(fmaxf(mx[k], fmaf(sc[k], f[k], sh[k])), 0.f);
+    const uint4 pooled = bn_relu_pool8(v[0], v[1], v[2], v[3], ssc + c0, ssh + c0);
     const int ow = (int)(pix % Wo);
     const int64_t t = pix / Wo;
     const int oh = (int)(t % Ho);
@@ -267,7 +246,7 @@ __global__ void __launch_bounds__(256, MINW) bn_relu_pool_fwd_fin_kernel(const b
     bf16_t* o = out + ((b * Hop + oh + opad) * Wop + ow + opad) * (int64_t)C + c0;
     i += stride;
     if (i < total) load4(item_base(i, c0, pix), v);
-    *reinterpret_cast<uint4*>(o) = pack8(mx);
+    *reinterpret_cast<uint4*>(o) = pooled;
   }
   BN_STAMP(0, C, 2);
 }

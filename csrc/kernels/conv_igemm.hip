@@ -27,6 +27,7 @@
 #include "dl_common.h"
 #include "dl_ops.h"
 #include "slab_reduce_dev.h"
+#include "bn_fin_dev.h"
 #include "prep_dev.h"
 #include "sgd_dev.h"
 #include "wtrans_dev.h"
@@ -85,6 +86,22 @@ struct BnRedArgs {
   const float* w;      // BNR 2: gamma
   const float* b;      // BNR 2: beta
   const bf16_t* ym;    // BNR 3: block output [M][C] (ReLU mask)
+};
+
+constexpr int kPlSlots = 5;  // region slots per thread of the pool-on-load fill (512 threads)
+
+// Pool-on-load source of the region kernel (PL): the previous block's
+// pre-BN conv output y [B][2H][2W][Cin] and its accumulated BN statistics
+// (fin: the coefficients are derived in the prologue, block 0 publishes coef
+// and the running statistics).  The region holds max_{2x2} relu(scale*y +
+// shift) (bn_relu_pool8, the BN consumer kernel's arithmetic) with the zero
+// border kept zero, and the tile's own interior rows of that pooled
+// activation go out to pout [B][Hp][Wp][Cin] (the backward's copy) -- the
+// separate BN/ReLU/pool launch and its read of y are gone.
+struct PoolLoad {
+  const bf16_t* y;
+  BnFin fin;
+  bf16_t* pout;
 };
 
 struct ConvGeom {
@@ -1089,13 +1106,13 @@ struct RegionGeom {
 };
 
 
-template <int BN, bool STATS, bool SLAB, int STAGES, int WM, int WN, bool BNRED = false>
+template <int BN, bool STATS, bool SLAB, int STAGES, int WM, int WN, bool BNRED = false, bool PL = false>
 __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf16_t* __restrict__ x,
                                                               const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
                                                               float* __restrict__ stats, float* __restrict__ slab,
                                                               const ConvGeom g, const RegionGeom rg, int splits,
                                                               unsigned long long* dbg, int ablate,
-                                                              const BnRedArgs br) {
+                                                              const BnRedArgs br, const PoolLoad pl = PoolLoad{}) {
   const unsigned long long t_start = dbg ? stamp() : 0ull;
   constexpr int BM = 128, BK = 64, CPR = 8, NW = WM * WN, PD = STAGES - 1;
   constexpr int B_BYTES = BN * BK * 2, B_INS = B_BYTES / 1024 / NW, LPS = B_INS;
@@ -1129,7 +1146,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf1
   const int cbase = split * rg.cpw;  // first 64-channel chunk of this workgroup
 
   // ---- region loads (once per chunk): lane-linear slots -> source pixel/chunk
-  {
+  if constexpr (!PL) {
     const int nq = rg.nslot >> 6;
     // slot -> (region row R, pixel in row, chunk): the region's image rows
     // are consecutive padded rows (rows mode: RH rows of one image; images
@@ -1209,6 +1226,63 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf1
 #pragma unroll
     for (int q = 0; q < LPS; ++q) issue_b(q, ld_k < nk);
     advance_ld();
+  }
+  if constexpr (PL) {
+    // ---- pool-on-load region fill (the weight stages above are in flight).
+    // One 64-channel chunk (cpw == 1, host-checked); every slot of a thread
+    // (<= kPlSlots) has its 4 window loads issued before the coefficient
+    // prologue and the first use: one memory round trip for the whole fill
+    // (a loop with one slot of lookahead paid one per slot).
+    constexpr int NT = 64 * NW;
+    __shared__ float ssc[64], ssh[64];
+    const int nrows = rg.nimg * rg.RH;
+    const int H2 = 2 * g.H, W2 = 2 * g.W;
+    const bool owner = tn == 0 && split == 0;  // one workgroup per M tile writes pout
+    const int own_lo = rg.rows_mode ? oh0 : 0, own_hi = rg.rows_mode ? oh0 + BM / g.W : g.H;
+    const int rowC = W2 * g.Cin;
+    int src[kPlSlots], dpix[kPlSlots];
+#pragma unroll
+    for (int k = 0; k < kPlSlots; ++k) {
+      // slot -> source element of y (-1: a zero slot) and the pout pixel (-1: none)
+      const int sl = tid + k * NT;
+      src[k] = -1;
+      dpix[k] = -1;
+      const int R = (int)(((float)sl + 0.5f) * rg.inv_RS);
+      const int r2 = sl - R * rg.RS;
+      const int col = (r2 * 6554) >> 16;  // r2 / 10 (S == 10)
+      const int ch = r2 - col * 10;
+      if (sl < rg.nslot && R < nrows && col < rg.RW && ch < 8) {
+        const int pix = start_pix + R * g.Wp + col;  // padded input pixel
+        const int img = pix / HpWp, rem = pix - img * HpWp;
+        const int pr = rem / g.Wp, ih = pr - g.pad, iw = rem - pr * g.Wp - g.pad;
+        if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) {
+          src[k] = ((img * H2 + 2 * ih) * W2 + 2 * iw) * g.Cin + cbase * 64 + ch * 8;
+          if (owner && ih >= own_lo && ih < own_hi) dpix[k] = pix;
+        }
+      }
+    }
+    uint4 v[kPlSlots][4];
+#pragma unroll
+    for (int k = 0; k < kPlSlots; ++k) {
+      const bf16_t* p = pl.y + (src[k] >= 0 ? src[k] : 0);
+      v[k][0] = *reinterpret_cast<const uint4*>(p);
+      v[k][1] = *reinterpret_cast<const uint4*>(p + g.Cin);
+      v[k][2] = *reinterpret_cast<const uint4*>(p + rowC);
+      v[k][3] = *reinterpret_cast<const uint4*>(p + rowC + g.Cin);
+    }
+    bn_fin_block(pl.fin, g.Cin, ssc, ssh);  // (rows summed behind the window loads; ends with a barrier)
+#pragma unroll
+    for (int k = 0; k < kPlSlots; ++k) {
+      const int sl = tid + k * NT;
+      if (sl >= rg.nslot) break;
+      uint4 o = make_uint4(0u, 0u, 0u, 0u);
+      if (src[k] >= 0) {
+        const int cc = src[k] & 63;  // first of the slot's 8 channels (Cin == 64)
+        o = bn_relu_pool8(v[k][0], v[k][1], v[k][2], v[k][3], ssc + cc, ssh + cc);
+        if (dpix[k] >= 0) *reinterpret_cast<uint4*>(pl.pout + (int64_t)dpix[k] * g.Cin + cc) = o;
+      }
+      *reinterpret_cast<uint4*>(sR + sl * 16) = o;
+    }
   }
   const unsigned long long t_issued = dbg ? stamp() : 0ull;
 
@@ -2092,6 +2166,7 @@ static int g_fwd_swave_req = 0;     // FwdCfg bit 21: per-wave-row BN statistics
 static int g_stat_rows_mult = 1;    // rows per M tile of the last streaming launch (WM when swave)
 static int g_red_atomic_host = 0;   // host mirror of g_red_atomic
 static BnRedArgs g_bnred{};         // conv_fwd_bnred: fused BN backward reduce (region dgrad only)
+static PoolLoad g_pool_load{};      // set_conv_pool_load: the next region conv pools its input on load
 static BnRedArgs g_bnred2{};        // set_conv_bn_reduce: NHWC BN backward reduce in the streaming epilogue
 // A/B knob: 0 = the untransposed accumulator layout for the split-K and BN-statistics
 // instances of the streaming kernel (set_conv_fwd_tr)
@@ -2373,8 +2448,27 @@ static void launch_fwd_region_st(const ConvGeom& g, const RegionGeom& rg, uintpt
       attr = true;
     }
     kern<<<grid, 64 * WM * WN, lds, s>>>((const bf16_t*)x, (const bf16_t*)w, yy, st, sl, g, rg, splits, g_conv_dbg,
-                                         g_region_ablate, g_bnred);
+                                         g_region_ablate, g_bnred, PoolLoad{});
   };
+  if (g_pool_load.y != nullptr) {
+    // (one instance: the layer-2 forward's tile / wave / ring shape)
+    if constexpr (BN == 128 && WM == 2 && WN == 4 && ST == 6) {
+      if (splits > 1 || !stats || g_bnred.rows != nullptr || g.Cin != 64 || rg.nslot > kPlSlots * 64 * WM * WN)
+        throw std::runtime_error("conv_pool_load: an unsplit forward with statistics, Cin == 64, a small region");
+      auto kern = conv_fwd_region_kernel<BN, true, false, ST, WM, WN, false, true>;
+      static bool attr = false;
+      if (!attr) {
+        DL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024));
+        attr = true;
+      }
+      kern<<<grid, 64 * WM * WN, lds, s>>>((const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)stats, nullptr, g,
+                                           rg, splits, g_conv_dbg, g_region_ablate, g_bnred, g_pool_load);
+      g_pool_load = PoolLoad{};
+      return;
+    } else {
+      throw std::runtime_error("conv_pool_load: this region shape has no pool-on-load instance");
+    }
+  }
   if (g_bnred.rows != nullptr) {
     if (splits > 1 || stats) throw std::runtime_error("conv_fwd_bnred: plain unsplit dgrad only");
     go(conv_fwd_region_kernel<BN, false, false, ST, WM, WN, true>, (bf16_t*)y, nullptr, nullptr);
@@ -2473,6 +2567,10 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
   else if (tile == 2) launch_fwd<128, 64>(g, x, w, y, stats, slab, splits, s);
   else throw std::runtime_error("conv_fwd: bad tile id");
   DL_HIP_CHECK(hipGetLastError());
+  if (g_pool_load.y != nullptr) {  // armed, but this call did not take the region kernel
+    g_pool_load = PoolLoad{};
+    throw std::runtime_error("set_conv_pool_load: the next conv_fwd call must run on the region kernel");
+  }
   if (g_side_sgd.nblk != 0) {  // armed, but this call ran on the region / c8 kernel
     g_side_sgd.nblk = 0;
     throw std::runtime_error("set_conv_side_sgd: the next conv_fwd call must run on the streaming kernel");
@@ -2518,6 +2616,36 @@ void set_conv_bn_reduce(uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, u
   g_bnred2 = rows ? BnRedArgs{(const bf16_t*)x, nullptr, (float*)rows, (const float*)save, (const float*)w,
                               (const float*)b, (const bf16_t*)ym}
                   : BnRedArgs{};
+}
+
+// The next conv_fwd call (a region-kernel forward with statistics) takes its
+// input as BN -> ReLU -> 2x2 max-pool of y_prev [B][2H][2W][Cin] on load: the
+// BN coefficients from the accumulated statistics (sums: R = reduce_rows()
+// rows, bn_fin_dev.h; block 0 publishes coef and the running statistics), the
+// pooled activation written into pout [B][H+2p][W+2p][Cin] (interior) for the
+// backward.  Replaces bn_relu_pool_fwd_fin on that edge.  One-shot.
+void set_conv_pool_load(uintptr_t y_prev, uintptr_t sums, int64_t M, uintptr_t gamma, uintptr_t beta, uintptr_t bias,
+                        uintptr_t rmean, uintptr_t rvar, float eps, float momentum, uintptr_t coef, uintptr_t pout) {
+  if (!y_prev || !sums || !gamma || !beta || !coef || !pout) throw std::runtime_error("set_conv_pool_load: null operand");
+  if (reduce_rows() < 1 || reduce_rows() > kMaxRows)
+    throw std::runtime_error("set_conv_pool_load: needs an atomic reduction mode with <= 32 rows");
+  g_pool_load = PoolLoad{(const bf16_t*)y_prev,
+                         make_bn_fin(sums, M, gamma, beta, bias, rmean, rvar, eps, momentum, coef, reduce_rows()),
+                         (bf16_t*)pout};
+}
+
+// Whether set_conv_pool_load can serve a conv_fwd of this shape (the
+// region kernel's pool-on-load instance: 128-wide tile, 8 waves, 6 stages).
+int conv_pool_load_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile) {
+  ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
+  RegionGeom rg{};
+  if ((tile & 15) != 0 || g_region_waves != 8 || Cin != 64 || Cout % 128 != 0 || !region_geom(g, 128, 1, rg) ||
+      rg.nslot > kPlSlots * 512)
+    return 0;
+  const int free_b = kRegionLdsCap - rg.cpw * rg.nslot * 16;
+  int st = std::min(8, free_b / (128 * 64 * 2));
+  if (g_region_stages > 0) st = std::min(st, g_region_stages);
+  return st >= 6 && st < 8 ? 1 : 0;  // launch_fwd_region's 6-stage instance
 }
 
 // Whether conv_fwd runs this unsplit shape on the region (tap-reuse) kernel --

@@ -902,3 +902,71 @@ def test_conv_c8_tiles_per_workgroup(C, B):
     assert torch.equal(outs[0][1], outs[1][1])
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=2).permute(0, 2, 3, 1)
     assert _rel(outs[1][0], ref) < 8e-3
+
+
+def test_pool_on_load_region_conv(C, monkeypatch):
+    """Block 2's region conv takes block 1's BN -> ReLU -> 2x2 pool on load
+    (set_conv_pool_load: coefficients derived in its prologue, the pooled
+    input computed into its LDS region, the pooled copy written for the
+    backward) instead of the bn_relu_pool_fwd_fin launch: the pooled
+    activation is bitwise the stand-alone pool of the same coefficients, the
+    block-2 output bitwise the plain region conv of it, the running
+    statistics updated once, and a step's loss / gradients match the
+    separate launch to the fp32-atomic statistics' noise."""
+    from torch_distlearn_amd import FlatParams
+    from torch_distlearn_amd.models import CifarConvNet
+    from torch_distlearn_amd.models.cifar_convnet import BN_EPS, BN_MOMENTUM
+    from torch_distlearn_amd.models.cifar_hip import KSIZE, SPAD, CifarHIPExecutor
+
+    monkeypatch.setenv("DISTLEARN_REDUCE_ATOMIC", "2")
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(11)
+    x = torch.randn(128, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)
+    y = torch.randint(0, 10, (128,), device=dev, generator=g)
+    res = []
+    for pl in ("0", "1", "1"):
+        monkeypatch.setenv("DISTLEARN_POOL_ON_LOAD", pl)
+        mdl = CifarConvNet(seed=4).to(dev)
+        flat = FlatParams(mdl, grads=True, shadow_bf16=True)
+        ex = CifarHIPExecutor(mdl, flat, max_batch=128)
+        assert ex._pool_on_load(1) == (pl == "1")
+        rm0, rv0 = ex.rm[0].clone(), ex.rv[0].clone()
+        # every interior element must be written: NaN inside, the zero border kept
+        interior = ex.p[0][:, SPAD:-SPAD, SPAD:-SPAD]
+        interior.fill_(float("nan"))
+        loss = float(ex.forward_backward(x.contiguous(), y))
+        torch.cuda.synchronize()
+        grads = torch.cat([v.flatten() for v in flat.views_of(flat.grad)])
+        res.append((loss, grads))
+        if pl == "1":
+            h0, c0 = ex.hs[0], ex.couts[0]
+            # the pooled input == the stand-alone pool with the coefficients block 0 published
+            ref = torch.zeros_like(ex.p[0])
+            C.bn_relu_pool_fwd(ex.y[0].data_ptr(), ex.coef[0].data_ptr(), ref.data_ptr(), 128, h0, h0, c0, SPAD,
+                               torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            assert torch.isfinite(ex.p[0].float()).all()
+            assert torch.equal(ex.p[0], ref)
+            # block 2's output == the plain region conv of that input
+            h1, ci1, co1 = ex.hs[1], ex.cins[1], ex.couts[1]
+            t1, sp1 = ex.fwd_plan[1]
+            y1 = torch.empty_like(ex.y[1])
+            C.conv_fwd(ex.p[0].data_ptr(), ex.p16[ex._leaf(1, 0)].data_ptr(), y1.data_ptr(), 0, 0, 128, h1, h1, ci1,
+                       co1, KSIZE, t1, 1, torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            assert torch.equal(ex.y[1], y1)
+            # running statistics: one momentum update with the batch statistics
+            coef = ex.coef[0].reshape(-1)  # [4][C]: mean, invstd, scale, shift
+            mean, istd = coef[:c0], coef[c0:2 * c0]
+            var = 1.0 / istd.double() ** 2 - BN_EPS
+            M = 128 * h0 * h0
+            bias = mdl.block_params(0)[1]
+            mo = BN_MOMENTUM
+            torch.testing.assert_close(ex.rm[0], (1 - mo) * rm0 + mo * (mean + bias), rtol=1e-4, atol=1e-5)
+            torch.testing.assert_close(ex.rv[0].double(), (1 - mo) * rv0.double() + mo * var * M / (M - 1), rtol=2e-3,
+                                       atol=1e-4)
+    (l0, g0), (l1, g1), (l2, g2) = res
+    rel = lambda a, b: float((a - b).norm() / b.norm())  # noqa: E731
+    assert abs(l0 - l1) < 1e-3 and abs(l0 - l2) < 1e-3
+    noise = rel(g1, g2)
+    assert min(rel(g1, g0), rel(g2, g0)) < max(3 * noise, 3e-2)

@@ -428,11 +428,16 @@ class CifarHIPExecutor:
         leaves the last block's pool to the head kernel (head_fwd_bwd_pool)."""
         C = self.C
         inp = self.x8
+        pooled = False  # block i-1's BN/ReLU/pool runs inside block i's conv (set_conv_pool_load)
         for i in range(self.nb):
             h, cin, cout = self.hs[i], self.cins[i], self.couts[i]
             M = B * h * h
             w = self.w1p if i == 0 else self.p16[self._leaf(i, 0)]
             t, sp = self.fwd_plan[i]
+            if pooled:
+                hp = self.hs[i - 1]
+                C.set_conv_pool_load(self.y[i - 1].data_ptr(), *self._fin_args(i - 1, B * hp * hp),
+                                     self.p[i - 1].data_ptr())
             ntm = C.conv_fwd(inp.data_ptr(), w.data_ptr(), self.y[i].data_ptr(),
                              self.stats[i].data_ptr() if train else 0, self.slabs.data_ptr(), B, h, h, cin, cout, KSIZE,
                              t | self.fwd_cfg | _slab_cap_bits(sp), sp, s)
@@ -442,7 +447,10 @@ class CifarHIPExecutor:
                               self.p32[self._leaf(i, 3)].data_ptr(), self.p32[self._leaf(i, 1)].data_ptr(),
                               self.rm[i].data_ptr(), self.rv[i].data_ptr(), BN_EPS, BN_MOMENTUM, 0 if train else 1,
                               self.coef[i].data_ptr(), s)
-            if pool_last or i + 1 < self.nb:
+            pooled = fused and i + 1 < self.nb and self._pool_on_load(i + 1)
+            if pooled:
+                pass  # the next conv derives the coefficients and pools on load
+            elif pool_last or i + 1 < self.nb:
                 opad = SPAD if i + 1 < self.nb else 0
                 if fused:
                     C.bn_relu_pool_fwd_fin(self.y[i].data_ptr(), *self._fin_args(i, M), self.p[i].data_ptr(), B, h,
@@ -451,6 +459,23 @@ class CifarHIPExecutor:
                     C.bn_relu_pool_fwd(self.y[i].data_ptr(), self.coef[i].data_ptr(), self.p[i].data_ptr(), B, h, h,
                                        cout, opad, s)
             inp = self.p[i]
+
+    def _pool_on_load(self, i: int) -> bool:
+        """Whether block i's conv takes block i-1's BN -> ReLU -> 2x2 pool on
+        load (csrc set_conv_pool_load: the region kernel derives the BN
+        coefficients, pools the pre-BN output of block i-1 into its LDS
+        region and writes the pooled copy the backward needs) instead of the
+        separate bn_relu_pool_fwd_fin launch.  Off by default (DISTLEARN_POOL_ON_LOAD=1:
+        on): the fused conv measured 25.9 us against 18.1 + 8.2 us for the two
+        launches, the step 0.3038 vs 0.3025 / 0.3107 vs 0.3107 ms -- both read
+        the pre-BN output once (the fused fill 1.5x with the halo rows), and
+        that read is what bounds them (profiles/r4_pool_on_load_ab.txt)."""
+        if os.environ.get("DISTLEARN_POOL_ON_LOAD", "0") != "1" or i < 1:
+            return False
+        t, sp = self.fwd_plan[i]
+        return (sp == 1 and self.hs[i - 1] == 2 * self.hs[i] and self.cins[i] == self.couts[i - 1]
+                and bool(self.C.conv_pool_load_ok(self.B, self.hs[i], self.hs[i], self.cins[i], self.couts[i], KSIZE,
+                                                  t)))
 
     def _fin_args(self, i: int, M: int):
         """(sums, M, gamma, beta, conv bias, running mean, running var, eps,
