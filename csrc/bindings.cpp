@@ -160,6 +160,7 @@ PYBIND11_MODULE(_C, m) {
       .def("group_start", &RcclCommunicator::group_start)
       .def("group_end", &RcclCommunicator::group_end)
       .def("track", &RcclCommunicator::track)
+      .def("set_paused", &RcclCommunicator::set_paused)
       .def("set_timeout", &RcclCommunicator::set_timeout)
       .def("timeout", &RcclCommunicator::timeout)
       .def("pending", &RcclCommunicator::pending)

@@ -232,6 +232,9 @@ class RcclCommunicator {
   }
 
   // Time the work enqueued so far on `stream` (no-op while it is being captured).
+  // pause (true) / resume the watchdog's polling, e.g. around a hipGraph capture
+  void set_paused(bool p) { paused_.store(p); }
+
   void track(uintptr_t stream) {
     std::lock_guard<std::mutex> g(mu_);
     live_locked();
@@ -353,6 +356,9 @@ class RcclCommunicator {
     while (!stop_) {
       cv_.wait_for(lk, std::chrono::milliseconds(poll_ms_));
       if (stop_ || !comm_.get()) continue;
+      // no HIP / RCCL query while the owner captures a hipGraph (set_paused):
+      // a query from this thread can invalidate the capture
+      if (paused_.load()) continue;
       ncclComm_t dead = nullptr;
       bool failed = false;
       // retire completed work (in order: events of one stream complete in order;
@@ -395,6 +401,7 @@ class RcclCommunicator {
   int rank_, world_, dev_;
   std::atomic<double> timeout_s_;
   int poll_ms_ = 50;
+  std::atomic<bool> paused_{false};
   int group_depth_ = 0;                    // guarded by call_mu_
   std::vector<uintptr_t> grouped_streams_;  // guarded by call_mu_
   std::mutex call_mu_;                      // serialises RCCL host calls

@@ -39,11 +39,15 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
 // v0..v3 of relu(sc*y + sh) (bf16 in / out).  Shared by the BN consumer
 // kernel (bn_pool.hip) and the conv that pools its input on load
 // (conv_igemm.hip, region kernel PL), so both produce the same bits.
+// sc_ / sh_: 8 consecutive LDS floats, 16-byte aligned, read as two 16-byte
+// vectors each (8 scalar pairs measured 6.06 vs 5.95 us per fwd-fin launch)
 __device__ __forceinline__ uint4 bn_relu_pool8(const uint4& v0, const uint4& v1, const uint4& v2, const uint4& v3,
                                                const float* sc_, const float* sh_) {
   float sc[8], sh[8], f[8], mx[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { sc[k] = sc_[k]; sh[k] = sh_[k]; }
+  const float4 a0 = reinterpret_cast<const float4*>(sc_)[0], a1 = reinterpret_cast<const float4*>(sc_)[1];
+  const float4 b0 = reinterpret_cast<const float4*>(sh_)[0], b1 = reinterpret_cast<const float4*>(sh_)[1];
+  sc[0] = a0.x; sc[1] = a0.y; sc[2] = a0.z; sc[3] = a0.w; sc[4] = a1.x; sc[5] = a1.y; sc[6] = a1.z; sc[7] = a1.w;
+  sh[0] = b0.x; sh[1] = b0.y; sh[2] = b0.z; sh[3] = b0.w; sh[4] = b1.x; sh[5] = b1.y; sh[6] = b1.z; sh[7] = b1.w;
   unpack8(v0, f);
 #pragma unroll
   for (int k = 0; k < 8; ++k) mx[k] = fmaf(sc[k], f[k], sh[k]);

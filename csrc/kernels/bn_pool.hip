@@ -208,7 +208,7 @@ template <int MINW = 1>  // (see bn_relu_pool_bwd_apply_kernel: uncapped 160 VGP
 __global__ void __launch_bounds__(256, MINW) bn_relu_pool_fwd_fin_kernel(const bf16_t* __restrict__ y, const BnFin fin,
                                                                    bf16_t* __restrict__ out, int B, int H, int W, int C,
                                                                    int opad) {
-  __shared__ float ssc[kFinMaxC], ssh[kFinMaxC];
+  __shared__ __attribute__((aligned(16))) float ssc[kFinMaxC], ssh[kFinMaxC];  // (bn_relu_pool8: 16-byte reads)
   const int C8 = C >> 3, Ho = H >> 1, Wo = W >> 1;
   const int Hop = Ho + 2 * opad, Wop = Wo + 2 * opad;
   const int64_t total = (int64_t)B * Ho * Wo * C8;

@@ -1234,7 +1234,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf1
     // prologue and the first use: one memory round trip for the whole fill
     // (a loop with one slot of lookahead paid one per slot).
     constexpr int NT = 64 * NW;
-    __shared__ float ssc[64], ssh[64];
+    __shared__ __attribute__((aligned(16))) float ssc[64], ssh[64];
     const int nrows = rg.nimg * rg.RH;
     const int H2 = 2 * g.H, W2 = 2 * g.W;
     const bool owner = tn == 0 && split == 0;  // one workgroup per M tile writes pout

@@ -55,6 +55,35 @@ def agree_on_policy(comm, local_ms: dict) -> tuple:
     return best, table
 
 
+# hipGraph capture mode: "thread_local" -- only this thread's unsafe HIP calls
+# may invalidate a capture (see _capturing for the other threads / finalizers)
+_CAPTURE_MODE = os.environ.get("DISTLEARN_CAPTURE_MODE", "thread_local")
+
+
+@contextlib.contextmanager
+def _capturing(comm):
+    """Around a hipGraph capture: the communicator's watchdog stops polling
+    (its hipEventQuery / RCCL async-error query from another thread) and the
+    cyclic garbage collector is off (a finaliser of an unreachable CUDA
+    object -- a stream, an event, another trainer's communicator -- would
+    issue HIP calls on this thread mid-capture).  Either invalidated captures
+    intermittently ("operation not permitted when stream is capturing")."""
+    import gc
+
+    pause = getattr(comm, "pause_watch", None)
+    if pause is not None:
+        pause(True)
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
+        if pause is not None:
+            pause(False)
+
+
 class DataParallelTrainer:
     def __init__(self, model: torch.nn.Module, tree: Tree, lr: float = 0.1, momentum: float = 0.0,
                  weight_decay: float = 0.0, algo: str = "sgd", tau: int = 10, alpha: float = 0.2,
@@ -450,7 +479,7 @@ class DataParallelTrainer:
         ea_round = isinstance(k, tuple)
         n = k[1] if ea_round else k
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with _capturing(self.tree.comm), torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
             for j in range(n):
                 loss = self._step_body(loader, None, prep_next=j + 1 < n)
             if ea_round:
@@ -508,7 +537,7 @@ class DataParallelTrainer:
         torch.cuda.current_stream().wait_stream(s)
         self._restore(saved, x)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with _capturing(self.tree.comm), torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
             loss = self._step_body(sx, sy)
         if self.sgd is not None:
             # the warm-up + capture bodies counted steps; undo (replay() counts itself)

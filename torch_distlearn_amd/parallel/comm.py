@@ -327,6 +327,13 @@ class RcclCommunicator(Communicator):
     def health(self) -> str:
         return "communicator closed" if self._c is None else self._c.async_error()
 
+    def pause_watch(self, paused: bool) -> None:
+        """Suspend (True) / resume the watchdog's event and async-error polling
+        -- around a hipGraph capture, where a HIP query from the watchdog
+        thread can invalidate the capture (engine.py _capturing)."""
+        if getattr(self, "_c", None) is not None:
+            self._c.set_paused(bool(paused))
+
     def track(self, stream=None) -> None:
         """Hand the work enqueued so far on ``stream`` to the watchdog (used
         after replaying a hipGraph that contains captured collectives)."""
