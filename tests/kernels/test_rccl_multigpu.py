@@ -349,8 +349,10 @@ def test_rccl_world1_p2p_inside_hipgraph(monkeypatch):
             comm.recv(r, 0)
     torch.cuda.current_stream().wait_stream(side)
     torch.cuda.synchronize()
+    from torch_distlearn_amd.engine import _capturing
+
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
+    with _capturing(comm), torch.cuda.graph(graph, capture_error_mode="thread_local"):  # (the trainer's guard)
         with comm.group():
             comm.send(s, 0)
             comm.recv(r, 0)
