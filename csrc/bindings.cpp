@@ -31,6 +31,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_conv_side_sgd", &set_conv_side_sgd);
   m.def("set_conv_pool_load", &set_conv_pool_load);
   m.def("conv_pool_load_ok", &conv_pool_load_ok);
+  m.def("set_conv_bn_on_load", &set_conv_bn_on_load);
   m.def("confusion_update", &confusion_update);
   m.def("bn_nhwc_fwd", &bn_nhwc_fwd);
   m.def("bn_nhwc_bwd", &bn_nhwc_bwd);

@@ -96,6 +96,8 @@ void set_conv_bn_reduce(uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, u
 // from the previous block's pre-BN output (BN coefficients from its accumulated sums)
 void set_conv_pool_load(uintptr_t y_prev, uintptr_t sums, int64_t M, uintptr_t gamma, uintptr_t beta, uintptr_t bias,
                         uintptr_t rmean, uintptr_t rvar, float eps, float momentum, uintptr_t coef, uintptr_t pout);
+void set_conv_bn_on_load(uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b, uintptr_t save, uintptr_t rmean,
+                         uintptr_t rvar, int64_t M, int C, double eps, double momentum, uintptr_t out);
 int conv_pool_load_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile);
 int conv_region_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile, int splits = 1);
 int conv_fwd_bnred(uintptr_t x, uintptr_t w, uintptr_t y, int B, int H, int W, int Cin, int Cout, int KS, int tile,

@@ -88,6 +88,29 @@ struct BnRedArgs {
   const bf16_t* ym;    // BNR 3: block output [M][C] (ReLU mask)
 };
 
+// BatchNorm -> ReLU applied to the A operand on load (OL: the ResNet-50 b2 ->
+// c3 edge, a stride-1 1x1 GEMM): the conv reads the BN's pre-activation input
+// y instead of its output, derives the per-channel scale / shift from the
+// accumulated statistics in its prologue (workgroup 0 publishes the saved
+// mean / invstd and updates the running statistics), applies
+// max(fma(y, scale, shift), 0) to every A fragment after its LDS read, and the
+// first N tile's workgroups write the activation out (the backward's copy) --
+// the BN apply launch and its read of y are gone.  Same arithmetic as
+// bn_nhwc_fwd_apply (bn_nhwc.hip), so the activation is the same bits.
+struct BnOnLoad {
+  const bf16_t* y;            // pre-BN input [M][C] (read instead of the conv's x)
+  const float* acc;           // [2C]: sum, sum of squares of y
+  const float* w;
+  const float* b;
+  float* save;                // [2C]: mean, invstd (for the BN backward)
+  float* rmean;
+  float* rvar;
+  float eps, momentum;
+  int M, C;
+  bf16_t* out;                // the activation [M][C] (== the conv's x argument)
+};
+constexpr int kOlMaxC = 512;
+
 constexpr int kPlSlots = 5;  // region slots per thread of the pool-on-load fill (512 threads)
 
 // Pool-on-load source of the region kernel (PL): the previous block's
@@ -696,13 +719,14 @@ __device__ __forceinline__ int b_frag_row(int b, int i) { return 32 * (b >> 1) +
 // 3-stage LDS ring filled by LDS-DMA, one barrier per K step.
 // --------------------------------------------------------------------------
 template <int BM, int BN, bool STATS, bool SLAB, bool TAPU, int STAGES, int WM = 2, int WN = 2, bool ADD = false,
-          bool TRP = true, int BNR = 0>
+          bool TRP = true, int BNR = 0, bool OL = false>
 __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                        bf16_t* __restrict__ y, float* __restrict__ stats,
                                                        float* __restrict__ slab, const ConvGeom g, int splits,
                                                        int kt_per_split, unsigned long long* dbg,
                                                        const BnRedArgs br = BnRedArgs{},
-                                                       const SgdJob side = SgdJob{}) {
+                                                       const SgdJob side = SgdJob{},
+                                                       const BnOnLoad ol = BnOnLoad{}) {
   // side job (set_conv_side_sgd): the last side.nblk workgroups run part of
   // the step's SGD update on the CUs the convolution's one-workgroup-per-CU
   // grid leaves free (its gradients are final by the time this conv runs)
@@ -727,7 +751,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   constexpr bool TR = TRP && FN % 2 == 0;
   static_assert(A_INS >= 1 && B_INS >= 1, "tile too small");
   static_assert(A_INS * NW * 1024 == A_BYTES && B_INS * NW * 1024 == B_BYTES, "DMA split");
-  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
+  // (OL: + the on-load scale / shift table past the ring)
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES + (OL ? 2 * kOlMaxC * 4 : 0)];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -888,6 +913,31 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  float* olt = reinterpret_cast<float*>(smem + STAGES * STAGE_BYTES);  // OL: scale [kOlMaxC], shift [kOlMaxC]
+  if constexpr (OL) {
+    // the BN coefficients (bn_nhwc.hip stats8 + fwd apply arithmetic); visible to
+    // every wave after the first K step's barrier
+    const float invM = 1.f / (float)ol.M;
+    for (int c = tid; c < ol.C; c += 64 * NW) {
+      const float m = ol.acc[c] * invM;
+      const float var = fmaxf(ol.acc[ol.C + c] * invM - m * m, 0.f);
+      const float is = rsqrtf(var + ol.eps);
+      const float sc = ol.w[c] * is;
+      olt[c] = sc;
+      olt[kOlMaxC + c] = fmaf(-m, sc, ol.b[c]);
+      if (blockIdx.x == 0) {
+        ol.save[c] = m;
+        ol.save[ol.C + c] = is;
+        if (ol.rmean != nullptr) {
+          const float unbias = ol.M > 1 ? (float)ol.M / (float)(ol.M - 1) : 1.f;
+          ol.rmean[c] = (1.f - ol.momentum) * ol.rmean[c] + ol.momentum * m;
+          ol.rvar[c] = (1.f - ol.momentum) * ol.rvar[c] + ol.momentum * var * unbias;
+        }
+      }
+    }
+  }
+  const bool ol_store = OL && tn == 0 && wn == 0;  // one writer per activation element
+
   const unsigned long long t_setup = dbg ? stamp() : 0ull;
   // Fragment-prefetch pipeline (g_fwd_pf, STAGES >= 3): every step issues one
   // stage unconditionally (zero-fill past nk keeps the vmcnt count constant),
@@ -1025,6 +1075,31 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
         for (int b = 0; b < FN; ++b) {
           const int row = wn * TN + (TR ? b_frag_row(b, lane & 15) : b * 16 + (lane & 15));
           bfr[kk][b] = __builtin_bit_cast(bf16x8, Bs[row * CPR + (ch ^ swz_b(row))]);
+        }
+      }
+      if constexpr (OL) {  // A = relu(scale * y + shift), 8 channels per fragment (1x1: step = 64 channels)
+        const int cstep = (kt_beg + i) * BK;
+#pragma unroll
+        for (int kk = 0; kk < BK / 32; ++kk) {
+          const int c = cstep + (kk * 4 + (lane >> 4)) * 8;
+          const float4 s0 = *reinterpret_cast<const float4*>(olt + c), s1 = *reinterpret_cast<const float4*>(olt + c + 4);
+          const float4 h0 = *reinterpret_cast<const float4*>(olt + kOlMaxC + c);
+          const float4 h1 = *reinterpret_cast<const float4*>(olt + kOlMaxC + c + 4);
+          const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+          const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+          for (int a = 0; a < FM; ++a) {
+            float f[8];
+            unpack8(__builtin_bit_cast(uint4, af[kk][a]), f);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], sc[k], sh[k]), 0.f);
+            const uint4 v = pack8(f);
+            af[kk][a] = __builtin_bit_cast(bf16x8, v);
+            if (ol_store) {
+              const int m = m0 + wm * TM + a * 16 + (lane & 15);
+              if (m < g.M) *reinterpret_cast<uint4*>(ol.out + (int64_t)m * ol.C + c) = v;
+            }
+          }
         }
       }
       // the next stage's LDS-DMA issues ride between the MFMAs (their issue cost
@@ -2167,6 +2242,7 @@ static int g_stat_rows_mult = 1;    // rows per M tile of the last streaming lau
 static int g_red_atomic_host = 0;   // host mirror of g_red_atomic
 static BnRedArgs g_bnred{};         // conv_fwd_bnred: fused BN backward reduce (region dgrad only)
 static PoolLoad g_pool_load{};      // set_conv_pool_load: the next region conv pools its input on load
+static BnOnLoad g_onload{};         // set_conv_bn_on_load: the next 1x1 GEMM applies a BN + ReLU on load
 static BnRedArgs g_bnred2{};        // set_conv_bn_reduce: NHWC BN backward reduce in the streaming epilogue
 // A/B knob: 0 = the untransposed accumulator layout for the split-K and BN-statistics
 // instances of the streaming kernel (set_conv_fwd_tr)
@@ -2233,6 +2309,20 @@ static void launch_fwd_w(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uin
   constexpr bool kTR = (BN / WN / 16) % 2 == 0;
   g.swave = (g_fwd_swave_req && stats && splits == 1 && !g_red_atomic_host && g_fwd_tr && kTR && !g.posm) ? 1 : 0;
   g_stat_rows_mult = g.swave ? WM : 1;
+  if (g_onload.y != nullptr) {
+    const BnOnLoad ol = g_onload;  // one-shot
+    g_onload = BnOnLoad{};
+    if constexpr (BM == 128 && BN == 128 && TAPU && WM == 2 && (WN == 2 || WN == 4) && ST <= 3) {
+      if (!stats || splits != 1 || g_fwd_addend || g_bnred2.rows != nullptr || g.posm || g.KS != 1 || g.S != 1 ||
+          g.Cin != ol.C || g.M != ol.M || (const bf16_t*)x != ol.out || side.nblk != 0 || !g_fwd_tr)
+        throw std::runtime_error("conv BN on load: a stride-1 1x1 forward with statistics on the activation's buffer");
+      conv_fwd_kernel<BM, BN, true, false, TAPU, ST, WM, WN, false, true, 0, true><<<grid, NT, 0, s>>>(
+          ol.y, (const bf16_t*)w, (bf16_t*)y, (float*)stats, nullptr, g, 1, ktps, g_conv_dbg, BnRedArgs{}, side, ol);
+      return;
+    } else {
+      throw std::runtime_error("conv BN on load: this tile / ring has no on-load instance (128x128, 4 or 8 waves, <= 3 stages)");
+    }
+  }
   if (g_fwd_addend && (splits > 1 || stats)) throw std::runtime_error("conv_fwd_add: no split-K / statistics");
   if (g_bnred2.rows != nullptr) {
     if (splits > 1 || stats) throw std::runtime_error("conv BN reduce: plain unsplit output only");
@@ -2567,6 +2657,10 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
   else if (tile == 2) launch_fwd<128, 64>(g, x, w, y, stats, slab, splits, s);
   else throw std::runtime_error("conv_fwd: bad tile id");
   DL_HIP_CHECK(hipGetLastError());
+  if (g_onload.y != nullptr) {  // armed, but this call did not take the streaming kernel
+    g_onload = BnOnLoad{};
+    throw std::runtime_error("set_conv_bn_on_load: the next conv_fwd call must be a streaming 1x1 GEMM");
+  }
   if (g_pool_load.y != nullptr) {  // armed, but this call did not take the region kernel
     g_pool_load = PoolLoad{};
     throw std::runtime_error("set_conv_pool_load: the next conv_fwd call must run on the region kernel");
@@ -2632,6 +2726,20 @@ void set_conv_pool_load(uintptr_t y_prev, uintptr_t sums, int64_t M, uintptr_t g
   g_pool_load = PoolLoad{(const bf16_t*)y_prev,
                          make_bn_fin(sums, M, gamma, beta, bias, rmean, rvar, eps, momentum, coef, reduce_rows()),
                          (bf16_t*)pout};
+}
+
+// The next conv_fwd (a stride-1 1x1 GEMM with statistics whose input buffer
+// is `out`) reads the BatchNorm input y instead and applies that BN + ReLU on
+// load (BnOnLoad); it also writes the activation into `out`, the saved
+// mean / invstd into save and updates the running statistics.  acc: [2C]
+// sum / sum of squares of y.  One-shot.
+void set_conv_bn_on_load(uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b, uintptr_t save, uintptr_t rmean,
+                         uintptr_t rvar, int64_t M, int C, double eps, double momentum, uintptr_t out) {
+  if (!y || !acc || !w || !b || !save || !out) throw std::runtime_error("set_conv_bn_on_load: null operand");
+  if (C < 64 || C > kOlMaxC || C % 64 != 0 || M <= 0 || M >= (1ll << 31))
+    throw std::runtime_error("set_conv_bn_on_load: 64 <= C <= 512, C % 64 == 0");
+  g_onload = BnOnLoad{(const bf16_t*)y, (const float*)acc, (const float*)w, (const float*)b, (float*)save,
+                      (float*)rmean, (float*)rvar, (float)eps, (float)momentum, (int)M, C, (bf16_t*)out};
 }
 
 // Whether set_conv_pool_load can serve a conv_fwd of this shape (the

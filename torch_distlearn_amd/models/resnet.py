@@ -74,7 +74,7 @@ class _BN(nn.Module):
             residual is None or (residual.dtype == x.dtype and residual.shape == x.shape))
 
     def act(self, x, relu: bool = True, residual=None, acc=None, res_sink=None, have_stats: bool = False,
-            out_pad: int = 0, dx_pad: int = 0, bn_link=None):
+            out_pad: int = 0, dx_pad: int = 0, bn_link=None, on_load: bool = False):
         """act(BN(x) [+ residual]); one fused HIP kernel pair in "hip" mode
         (``acc`` with ``have_stats``: statistics already accumulated by the
         producing conv; else the step's zeroed arena slice, if any;
@@ -91,7 +91,7 @@ class _BN(nn.Module):
                 acc, have_stats = self.acc, False
             return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual, relu, acc=acc,
                           grads=self.bind, res_sink=res_sink, have_stats=have_stats if acc is not None else None,
-                          out_pad=out_pad, dx_pad=dx_pad, bn_link=bn_link)
+                          out_pad=out_pad, dx_pad=dx_pad, bn_link=bn_link, on_load=on_load)
         y = self(x)
         if residual is not None:
             y = y + residual
@@ -135,6 +135,13 @@ _HEAD_HIP = os.environ.get("DISTLEARN_RESNET_HEAD", "hip") == "hip"
 # dgrads what the reduce pass saves -- every ResNet-50 BN kernel already streams at
 # ~5.5 TB/s, so a fusion only pays if it removes bytes (profiles/r3_resnet_bn_dgrad_ab.txt)
 _BN_DGRAD = os.environ.get("DISTLEARN_RESNET_BN_DGRAD", "0") == "1"
+# b2's BatchNorm + ReLU applied by c3's 1x1 GEMM to its A operand on load (csrc
+# set_conv_bn_on_load): the b2 apply launch and its read of c2's output are gone
+# (c3 writes the activation its backward needs).  Off: measured 25.43 vs 24.64
+# ms/step -- the per-fragment transform and the activation stores inside the
+# GEMM cost more than the apply pass they replace
+# (profiles/r4_resnet_bn_on_load_ab.txt).
+_BN_ON_LOAD = os.environ.get("DISTLEARN_RESNET_BN_ON_LOAD", "0") == "1"
 
 
 class _Conv(nn.Module):
@@ -220,14 +227,16 @@ class _Conv(nn.Module):
 
 
 def _conv_bn(conv: _Conv, bn: "_BN", x, relu: bool = True, residual=None, link=None, res_sink=None, dx_sink=None,
-             out_pad: int = 0, dx_pad: int = 0, in_link=None, out_link=None):
+             out_pad: int = 0, dx_pad: int = 0, in_link=None, out_link=None, into: Optional[_Conv] = None):
     """bn.act(conv(x)) with the BatchNorm statistics produced by the conv's
     epilogue when both run on the HIP kernels (one full read of the conv
     output fewer per BatchNorm).  ``out_pad`` / ``dx_pad``: the BatchNorm writes
     its output / input gradient zero-bordered (for a Conv3x3 neighbour).
     ``in_link``: the bn_link of the BatchNorm that produced ``x`` (the conv's
     dgrad epilogue computes its backward sums); ``out_link``: this
-    BatchNorm's own bn_link, for the next conv."""
+    BatchNorm's own bn_link, for the next conv.  ``into``: the 1x1 conv that
+    consumes the output -- with DISTLEARN_RESNET_BN_ON_LOAD=1 it applies this
+    BN + ReLU to its operand on load (no separate apply launch)."""
     kw = {"res_link": link, "dx_sink": dx_sink, "bn_link": in_link} if conv.bind is not None else {}
     pads = {"out_pad": out_pad, "dx_pad": dx_pad, "bn_link": out_link}
     if _FUSE_STATS and (conv.hip_gemm(x) or conv.hip_3x3(x) or conv.hip_strided(x)) and _BN_MODE == "hip" \
@@ -239,7 +248,9 @@ def _conv_bn(conv: _Conv, bn: "_BN", x, relu: bool = True, residual=None, link=N
             acc = bn.acc if bn.acc is not None else torch.zeros(4 * cout, device=x.device)
             y = conv(x, stats=acc[:2 * cout], **kw)
             if bn.hip_ok(y, residual):
-                return bn.act(y, relu, residual, acc=acc, res_sink=res_sink, have_stats=True, **pads)
+                ol = (_BN_ON_LOAD and into is not None and relu and residual is None and not out_pad
+                      and out_link is None and into.hip_gemm(y))
+                return bn.act(y, relu, residual, acc=acc, res_sink=res_sink, have_stats=True, on_load=ol, **pads)
             return bn.act(y, relu, residual)
     return bn.act(conv(x, **kw), relu, residual, res_sink=res_sink, **pads)
 
@@ -280,7 +291,7 @@ class _Bottleneck(nn.Module):
         l3 = {} if l1 is not None else None
         y = _conv_bn(self.c1, self.b1, x, link=link, out_pad=pad, out_link=l1,
                      in_link=in_link if self.down is None else None)
-        y = _conv_bn(self.c2, self.b2, y, dx_pad=pad, in_link=l1, out_link=l2)
+        y = _conv_bn(self.c2, self.b2, y, dx_pad=pad, in_link=l1, out_link=l2, into=self.c3)
         if self.down is None:
             return _conv_bn(self.c3, self.b3, y, residual=x, res_sink=link, in_link=l2, out_link=l3), l3
         s = _conv_bn(self.down[0], self.down[1], x, relu=False, dx_sink=link)

@@ -78,7 +78,7 @@ def supported(x: torch.Tensor) -> bool:
 class _BnAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, relu, eps, momentum, acc, grads, res_sink,
-                have_stats, out_pad, dx_pad, bn_link):
+                have_stats, out_pad, dx_pad, bn_link, on_load=False):
         M, C = _geom(x)
         N, _, H, W = x.shape
         if out_pad:
@@ -107,12 +107,18 @@ class _BnAct(torch.autograd.Function):
         mbits = None
         if relu and residual is not None and bn_link is None and _MASK_BITS:
             mbits = torch.empty(M * C // 8, dtype=torch.uint8, device=x.device)
-        _bn().bn_nhwc_fwd_pad(x.data_ptr(), res.data_ptr() if res is not None else 0, ybase, acc.data_ptr(),
-                                 weight.data_ptr(), bias.data_ptr(), save.data_ptr(),
-                                 running_mean.data_ptr() if running_mean is not None else 0,
-                                 running_var.data_ptr() if running_var is not None else 0, M, C, float(eps),
-                                 float(momentum), int(relu), int(have_stats), H, W, int(out_pad), stream_handle(),
-                                 mbits.data_ptr() if mbits is not None else 0)
+        apply = (x.data_ptr(), res.data_ptr() if res is not None else 0, ybase, acc.data_ptr(),
+                 weight.data_ptr(), bias.data_ptr(), save.data_ptr(),
+                 running_mean.data_ptr() if running_mean is not None else 0,
+                 running_var.data_ptr() if running_var is not None else 0, M, C, float(eps), float(momentum),
+                 int(relu), int(have_stats), H, W, int(out_pad))
+        if on_load and relu and residual is None and have_stats and not out_pad and mbits is None:
+            # y's content comes from the consuming 1x1 GEMM (ops/conv.py Conv1x1):
+            # it applies this BN + ReLU to its A operand on load and writes y, or
+            # runs this apply first when its tile has no on-load instance
+            y._dl_bn_on_load = apply
+        else:
+            _bn().bn_nhwc_fwd_pad(*apply, stream_handle(), mbits.data_ptr() if mbits is not None else 0)
         ctx.has_res = residual is not None
         ctx.grads = grads
         ctx.res_sink = res_sink
@@ -174,9 +180,9 @@ class _BnAct(torch.autograd.Function):
             dres = None
         if ctx.grads is not None:
             ready()
-            return dx, None, None, None, None, dres, None, None, None, None, None, None, None, None, None, None
+            return dx, None, None, None, None, dres, None, None, None, None, None, None, None, None, None, None, None
         return (dx, dw.to(weight.dtype), db.to(weight.dtype), None, None, dres, None, None, None, None, None, None, None,
-                None, None, None)
+                None, None, None, None)
 
 
 @torch.no_grad()
@@ -207,7 +213,7 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
            running_var: Optional[torch.Tensor], residual: Optional[torch.Tensor] = None, relu: bool = True,
            eps: float = 1e-5, momentum: float = 0.1, acc: Optional[torch.Tensor] = None,
            grads=None, res_sink: Optional[dict] = None, have_stats: Optional[bool] = None, out_pad: int = 0,
-           dx_pad: int = 0, bn_link: Optional[dict] = None) -> torch.Tensor:
+           dx_pad: int = 0, bn_link: Optional[dict] = None, on_load: bool = False) -> torch.Tensor:
     """``acc``: optional fp32 [4C] whose last 2C are zero; with ``have_stats``
     (the default when ``acc`` is given) its first 2C already hold the
     per-channel sum / sum of squares of x (see ops/conv.py Conv1x1), else they
@@ -226,7 +232,11 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
     epilogue adds the residual's gradient): the forward parks what that
     convolution's dgrad epilogue needs to produce the backward sums
     sum(g), sum(g*xhat) (ops/conv.py ``fused_bn_reduce``); the backward then
-    skips its own reduce pass over dy and x."""
+    skips its own reduce pass over dy and x.
+    ``on_load`` (ReLU, no residual, statistics given, unpadded output): the
+    returned tensor is filled by the 1x1 GEMM that consumes it, which applies
+    this BN + ReLU to its operand on load (ops/conv.py Conv1x1; csrc
+    set_conv_bn_on_load) -- the apply launch and its read of x are skipped."""
     if not supported(x):
         raise ValueError(f"bn_act: needs a channels-last bf16 CUDA tensor with a supported channel count, got "
                          f"{tuple(x.shape)} {x.dtype} {x.device}")
@@ -242,4 +252,4 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
         have_stats = acc is not None
     return _BnAct.apply(x, weight.contiguous(), bias.contiguous(), running_mean, running_var, residual, relu, eps,
                         momentum, acc, grads, res_sink, bool(have_stats), int(out_pad), int(dx_pad),
-                        bn_link if relu else None)
+                        bn_link if relu else None, bool(on_load))

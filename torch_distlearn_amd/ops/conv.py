@@ -220,6 +220,16 @@ class ChannelsLastWeights:
         native().weights_to_cl(self.table.data_ptr(), self.n, stream_handle())
 
 
+def _on_load_ok(tile: int, splits: int, cin: int, stats: bool) -> bool:
+    """Whether the 1x1 GEMM of this packed tile id has a BN-on-load instance
+    (csrc set_conv_bn_on_load): 128x128 tile, 4 or 8 waves, a 2- or 3-stage
+    ring (0: the global default, 3), one split, statistics, Cin % 64 == 0,
+    Cin <= 512."""
+    st, wv = (tile >> 4) & 15, (tile >> 8) & 15
+    return ((tile & 15) == 0 and splits == 1 and stats and st in (0, 2, 3) and wv in (0, 4, 8)
+            and cin % 64 == 0 and cin <= 512)
+
+
 class Conv1x1(torch.autograd.Function):
     """y = conv1x1(x, W) on the MFMA kernels; x channels-last bf16 [N, Cin, H, W]."""
 
@@ -231,6 +241,12 @@ class Conv1x1(torch.autograd.Function):
         ctx.dx_sink = dx_sink
         if dx_sink is not None:
             dx_sink["expect"] = True  # dx goes to the sink's consumer, not to autograd
+        ol = getattr(x, "_dl_bn_on_load", None)  # x: a BatchNorm output still to be computed (bn_act on_load)
+        if ol is not None:
+            del x._dl_bn_on_load
+            if not x.is_contiguous(memory_format=torch.channels_last):
+                native().bn_nhwc_fwd_pad(*ol, stream_handle(), 0)
+                ol = None
         x = x.contiguous(memory_format=torch.channels_last)
         N, cin, H, W = x.shape
         cout = weight.shape[0]
@@ -248,6 +264,13 @@ class Conv1x1(torch.autograd.Function):
             if splits == 1:
                 tile, nrows = _stats_cfg(tile, nrows)
             rows = torch.empty(max(nrows, 400 if splits > 1 else 1), 2, cout, device=x.device)
+        if ol is not None:
+            if _on_load_ok(tile, splits, cin, rows is not None):
+                # this GEMM reads the BN input, applies BN + ReLU on load and writes x
+                (xin, _, _, acc, w, b, save, rm, rv, Mx, Cx, eps, mom) = ol[:13]
+                C.set_conv_bn_on_load(xin, acc, w, b, save, rm, rv, Mx, Cx, eps, mom, x.data_ptr())
+            else:
+                C.bn_nhwc_fwd_pad(*ol, s, 0)
         T = C.conv_fwd(x.data_ptr(), bind.w16.data_ptr(), y.data_ptr(), 0 if rows is None else rows.data_ptr(),
                        0 if slab is None else slab.data_ptr(), M, 1, 1, cin, cout, 1, tile, splits, s)
         if rows is not None:  # ... -> sum / sum of squares per channel for the BatchNorm
