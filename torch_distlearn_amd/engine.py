@@ -213,15 +213,21 @@ class DataParallelTrainer:
             labels = x.labels_out if hasattr(x, "gather_args") else y
             for h in self.step_hooks:
                 h(self.last_logits(), labels)
+        armed = False
         if prep_next and self._slabs is not None and os.environ.get("DISTLEARN_PREP_NEXT", "1") == "1":
             arm = getattr(self.executor, "arm_next_prep", None)
-            if arm is not None:
-                arm(x)
-        if self.algo == "sgd":
-            self.sgd.step(f, self.lr, momentum=self.momentum, weight_decay=self.weight_decay,
-                          momentum_buf=self.mom, slabs=self._slabs, skip=self._side)
-        elif self.algo == "ea":
-            self._local_update()
+            armed = bool(arm(x)) if arm is not None else False
+        try:
+            if self.algo == "sgd":
+                self.sgd.step(f, self.lr, momentum=self.momentum, weight_decay=self.weight_decay,
+                              momentum_buf=self.mom, slabs=self._slabs, skip=self._side)
+            elif self.algo == "ea":
+                self._local_update()
+        except BaseException:
+            if armed:  # the update never consumed the next-step preparation
+                self.executor.C.disarm_sgd_next_prep()
+                self.executor._prefetched = False
+            raise
         return loss
 
     def _local_update(self) -> None:

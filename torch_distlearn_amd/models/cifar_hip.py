@@ -509,6 +509,8 @@ class CifarHIPExecutor:
                 raise RuntimeError("arm_next_prep: the prepared step must run on the same DeviceLoader")
             B = x.batch
         else:
+            if self.C.sgd_next_prep_armed():  # stale (an update that raised after arm_next_prep): drop it
+                self.C.disarm_sgd_next_prep()
             B = self._prep(x, s, with_transposes=not (self.fork_transposes or self.head_transposes))
         self._last_b = B
         if self.fork_transposes:  # dgrad weight transposes overlap the forward
