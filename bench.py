@@ -296,7 +296,12 @@ def main():
         sync()
         worker_barrier()
         sync()
+        probe = os.environ.get("DISTLEARN_BENCH_PROBE", "") == "1" and not cpu  # debug: where the window goes
+        if probe:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
+        if probe:
+            ev0.record()
         if step_args is None:
             loss = tr.run(loader, a.steps, unroll=unroll)
         else:
@@ -310,10 +315,18 @@ def main():
                     hist.append(loss.detach().clone())
             for i, l in enumerate(hist):
                 print(f"step {i} loss {float(l):.4f}", file=sys.stderr, flush=True)
+        if probe:
+            ev1.record()
+            t_sub = time.perf_counter() - t0
         sync()
+        if probe:
+            t_sync = time.perf_counter() - t0
         worker_barrier()
         sync()
         dt = time.perf_counter() - t0
+        if probe:
+            print(f"probe: window {dt * 1e3:.3f} ms, host enqueue {t_sub * 1e3:.3f} ms, first sync {t_sync * 1e3:.3f} ms, "
+                  f"GPU events {ev0.elapsed_time(ev1):.3f} ms", file=sys.stderr, flush=True)
         if tr.captures != captures0:
             raise RuntimeError(f"bench.py: {tr.captures - captures0} hipGraph capture(s) inside the timed region")
         tr.finish()
