@@ -274,9 +274,10 @@ def main():
             step_args = lambda i: (xs[i % nb], ys[i % nb])  # noqa: E731
         # steps per replayed graph: a timed window of at most 32 steps is ONE replay of a graph
         # holding exactly those steps (the driver's 20: 0.3307 vs 0.3335 ms/step as 16 + 4,
-        # = the 600-step figure 0.3305, profiles/r3_unroll_ab.txt); longer runs replay 16-step
-        # graphs (16 measured 1.3 % faster than 8, profiles/r2_unroll20_ab.txt)
-        unroll = int(os.environ.get("DISTLEARN_UNROLL", str(a.steps if 1 < a.steps <= 32 else 16)))
+        # = the 600-step figure 0.3305, profiles/r3_unroll_ab.txt); longer runs replay 32-step
+        # graphs (16 measured 1.3 % faster than 8, profiles/r2_unroll20_ab.txt; 32 vs 16:
+        # 0.2994 / 0.3008 / 0.3007 vs 0.3012 / 0.3035 / 0.3010 ms, profiles/r4_prep_next_ab.txt)
+        unroll = int(os.environ.get("DISTLEARN_UNROLL", str(a.steps if 1 < a.steps <= 32 else 32)))
         if step_args is None:  # device loader: unrolled graph replays of complete steps
             tr.run(loader, a.warmup, unroll=unroll)
         else:
