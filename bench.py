@@ -68,6 +68,16 @@ def parse():
     ap.add_argument("--grad-comm-dtype", default=os.environ.get("DISTLEARN_GRAD_COMM_DTYPE", "fp32"),
                     choices=["fp32", "bf16"],
                     help="gradient all-reduce wire dtype (bf16: half the xGMI bytes, count in an fp32 side slot)")
+    ap.add_argument("--nworld-path", type=int, default=0,
+                    help="1 = run the MULTI-NODE step configuration on one GPU (diagnostic, not the headline): the "
+                         "bucket all-reduces go through RCCL at world 1 (DISTLEARN_RCCL_WORLD1=1), so the trainer "
+                         "materialises every gradient for them (no one-node slab deferral / side SGD), the executor "
+                         "takes its overlap policy (both candidates timed and reported unless DISTLEARN_POLICY "
+                         "forces one)")
+    ap.add_argument("--hold-cus", type=int, default=0,
+                    help="with --nworld-path: hold R CUs during the timed region with workgroups of RCCL's "
+                         "all-reduce footprint (csrc/testing/diag.hip occupy_cus; the worst case of a collective "
+                         "overlapping the whole step); the time is then taken with GPU events")
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="self-launch (--gpus N > 1 without torch.distributed.run): seconds before the children "
                          "are killed and bench.py exits non-zero")
@@ -184,6 +194,12 @@ def main():
         print("bench.py: --algo async needs >= 2 ranks (1 server + clients)", file=sys.stderr)
         sys.exit(2)
     cpu = a.device == "cpu"
+    if a.nworld_path:
+        if world != 1 or cpu:
+            print("bench.py: --nworld-path rehearses the multi-node step on ONE GPU", file=sys.stderr)
+            sys.exit(2)
+        os.environ["DISTLEARN_RCCL_WORLD1"] = "1"
+        os.environ.setdefault("DISTLEARN_POLICY_SELECT", "1")
     if cpu:
         dev = torch.device("cpu")
         sync = lambda: None  # noqa: E731
@@ -294,9 +310,24 @@ def main():
             # bucket all-reduce, OUTSIDE the timed region; training state is restored after
             comm = tr.comm_profile(loader if step_args is None else step_args, steps=6)
         captures0 = tr.captures
-        sync()
+        hold = None
+        if a.hold_cus > 0 and not cpu:
+            from torch_distlearn_amd import _native
+
+            hold_stream = torch.cuda.Stream(device=dev)
+            sink = torch.zeros(4096, device=dev)
+            # outlasts the timed steps (<= 2 s); the window is timed with events on the step stream
+            _native.testing().occupy_cus(a.hold_cus, min(2_000_000, a.steps * 1500 + 50_000), sink.data_ptr(),
+                                         hold_stream.cuda_stream)
+            torch.cuda._sleep(2_000_000)  # the holding workgroups land first
+            hold = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        else:
+            sync()
         worker_barrier()
-        sync()
+        if hold is None:
+            sync()
+        else:
+            hold[0].record()
         probe = os.environ.get("DISTLEARN_BENCH_PROBE", "") == "1" and not cpu  # debug: where the window goes
         if probe:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -319,12 +350,16 @@ def main():
         if probe:
             ev1.record()
             t_sub = time.perf_counter() - t0
+        if hold is not None:
+            hold[1].record()
         sync()
         if probe:
             t_sync = time.perf_counter() - t0
         worker_barrier()
         sync()
         dt = time.perf_counter() - t0
+        if hold is not None:
+            dt = hold[0].elapsed_time(hold[1]) / 1e3  # the holding kernel outlives the window
         if probe:
             print(f"probe: window {dt * 1e3:.3f} ms, host enqueue {t_sub * 1e3:.3f} ms, first sync {t_sync * 1e3:.3f} ms, "
                   f"GPU events {ev0.elapsed_time(ev1):.3f} ms", file=sys.stderr, flush=True)
@@ -355,6 +390,11 @@ def main():
         # (engine.py select_policy: both candidates' ms per step, max over ranks)
         "policy": getattr(tr, "policy", None) if not is_server else None,
     }
+    if a.nworld_path:
+        policy["nworld_path"] = {
+            "what": "multi-node step configuration on one GPU: bucket all-reduces through RCCL at world 1, "
+                    "gradients materialised for them",
+            "fused_slab_reduce": getattr(tr, "_fused_reduce", None), "held_cus": a.hold_cus}
     ms = dt / a.steps * 1e3
     imgs = batch * len(workers) * a.steps / dt
     if rank == 0:

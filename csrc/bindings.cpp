@@ -29,6 +29,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_sgd_trim", &set_sgd_trim);
   m.def("disarm_sgd_next_prep", &disarm_sgd_next_prep);
   m.def("set_conv_side_sgd", &set_conv_side_sgd);
+  m.def("set_conv_side_reduce", &set_conv_side_reduce);
+  m.def("slab_reduce_multi", &slab_reduce_multi);
   m.def("set_conv_pool_load", &set_conv_pool_load);
   m.def("conv_pool_load_ok", &conv_pool_load_ok);
   m.def("set_conv_bn_on_load", &set_conv_bn_on_load);
@@ -161,7 +163,8 @@ PYBIND11_MODULE(_C, m) {
       .def("group_start", &RcclCommunicator::group_start)
       .def("group_end", &RcclCommunicator::group_end)
       .def("track", &RcclCommunicator::track)
-      .def("set_paused", &RcclCommunicator::set_paused)
+      .def("set_paused", &RcclCommunicator::set_paused, py::call_guard<py::gil_scoped_release>())
+      .def("polls", &RcclCommunicator::polls)
       .def("set_timeout", &RcclCommunicator::set_timeout)
       .def("timeout", &RcclCommunicator::timeout)
       .def("pending", &RcclCommunicator::pending)

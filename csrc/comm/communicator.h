@@ -15,6 +15,7 @@
 #pragma once
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -26,6 +27,7 @@
 #include <vector>
 
 #include "dl_common.h"
+#include "pause_gate.h"
 #include "retirable.h"
 
 #define DL_NCCL_CHECK(expr)                                                                                      \
@@ -231,9 +233,17 @@ class RcclCommunicator {
     return comm_.inflight();
   }
 
+  // pause (true) / resume the watchdog's polling, e.g. around a hipGraph
+  // capture: returns only once no poll is running (pause_gate.h), so no HIP /
+  // RCCL query from the watchdog thread can fall into the capture
+  void set_paused(bool p) { gate_.set(mu_, p); }
+  // watchdog polls run so far (tests: none may run while paused)
+  long long polls() {
+    std::lock_guard<std::mutex> g(mu_);
+    return gate_.polls();
+  }
+
   // Time the work enqueued so far on `stream` (no-op while it is being captured).
-  // pause (true) / resume the watchdog's polling, e.g. around a hipGraph capture
-  void set_paused(bool p) { paused_.store(p); }
 
   void track(uintptr_t stream) {
     std::lock_guard<std::mutex> g(mu_);
@@ -355,10 +365,43 @@ class RcclCommunicator {
     std::unique_lock<std::mutex> lk(mu_);
     while (!stop_) {
       cv_.wait_for(lk, std::chrono::milliseconds(poll_ms_));
-      if (stop_ || !comm_.get()) continue;
-      // no HIP / RCCL query while the owner captures a hipGraph (set_paused):
-      // a query from this thread can invalidate the capture
-      if (paused_.load()) continue;
+      if (stop_) continue;
+      // no HIP / RCCL query while the owner captures a hipGraph (set_paused
+      // waits for a running poll to finish; pause_gate.h)
+      if (!gate_.begin(lk)) continue;
+      ncclComm_t dead = poll_locked();
+      // dead == nullptr after a failure: a host call still holds the handle and
+      // aborts it on release (release_call) -- or this loop does, after the grace
+      if (dead) {  // abort outside the lock: the in-flight RCCL kernels see the abort flag and exit
+        lk.unlock();
+        ncclCommAbort(dead);
+        lk.lock();
+      }
+      gate_.end(lk);
+    }
+  }
+
+  // One watchdog poll (holding mu_): the handle to abort, or null.
+  ncclComm_t poll_locked() {
+    // A failed communicator whose handle a host call still holds is aborted by
+    // that call's release -- unless the call never returns (ncclGroupEnd stuck
+    // in connection setup with a dead peer, an outer group left open): after
+    // the grace period the handle is aborted from here anyway, the standard
+    // cross-thread abort that makes the blocked RCCL call return.
+    // Its release then finds nothing left to abort.
+    if (comm_.doomed()) {
+      const auto now = std::chrono::steady_clock::now();
+      if (!doomed_seen_) {
+        doomed_seen_ = true;
+        doomed_since_ = now;
+      } else if (std::chrono::duration<double>(now - doomed_since_).count() > abort_grace_s()) {
+        reason_ += " (a host call still held the communicator after the grace period: aborted from the watchdog)";
+        return comm_.take_doomed();
+      }
+      return nullptr;
+    }
+    if (!comm_.get()) return nullptr;
+    {
       ncclComm_t dead = nullptr;
       bool failed = false;
       // retire completed work (in order: events of one stream complete in order;
@@ -387,21 +430,21 @@ class RcclCommunicator {
           dead = detach_locked("collective on rank " + std::to_string(rank_) + " did not complete within " +
                                std::to_string(limit) + " s (dead or stuck peer?)");
       }
-      // dead == nullptr after a failure: a host call still holds the handle and
-      // aborts it on release (release_call)
-      if (dead) {  // abort outside the lock: the in-flight RCCL kernels see the abort flag and exit
-        lk.unlock();
-        ncclCommAbort(dead);
-        lk.lock();
-      }
+      return dead;
     }
   }
+
+  // seconds a doomed handle may stay held by a host call before the watchdog
+  // aborts it anyway: the collective timeout, at least 5 s
+  double abort_grace_s() const { return std::max(5.0, timeout_s_.load()); }
 
   Retirable<ncclComm_t> comm_;             // guarded by mu_
   int rank_, world_, dev_;
   std::atomic<double> timeout_s_;
   int poll_ms_ = 50;
-  std::atomic<bool> paused_{false};
+  PauseGate gate_;                          // guarded by mu_ (set() takes it)
+  bool doomed_seen_ = false;                // guarded by mu_
+  std::chrono::steady_clock::time_point doomed_since_;
   int group_depth_ = 0;                    // guarded by call_mu_
   std::vector<uintptr_t> grouped_streams_;  // guarded by call_mu_
   std::mutex call_mu_;                      // serialises RCCL host calls

@@ -23,6 +23,10 @@ void cast_bf16_f32(uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream);
 void set_conv_side_sgd(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, uintptr_t slot, float lr,
                        float momentum, float wd, int64_t lo, int64_t hi, std::vector<int64_t> offs,
                        std::vector<int64_t> lens, std::vector<uintptr_t> slabs, std::vector<int> splits, int nblk);
+// ... or sums split-K weight-gradient slabs into the gradient buffer g instead
+// (reduce-only side job: a multi-node step's gradients before the all-reduce)
+void set_conv_side_reduce(uintptr_t g, int64_t lo, int64_t hi, std::vector<int64_t> offs, std::vector<int64_t> lens,
+                          std::vector<uintptr_t> slabs, std::vector<int> splits, int nblk);
 void sgd_update_g16(uintptr_t p, uintptr_t g16, uintptr_t mom, uintptr_t p16, uintptr_t slot, float lr,
                     float momentum, float wd, int64_t n, uintptr_t stream);
 // sgd_update whose gradient in up to 4 ranges [offs, offs+lens) is the sum of the
@@ -36,12 +40,17 @@ void sgd_update_slabs(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, ui
                       uintptr_t tail_slab, int64_t skip_lo, int64_t skip_hi, uintptr_t stream);
 // one-shot: the next sgd_update_slabs launch also prepares the next step of an
 // unrolled graph -- gathers its batch into xp, zeroes its accumulators (prep_dev.h)
-// and writes the tail (first layer) weights into the packed bf16 operand w1p
+// and writes the first layer's updated weights into the packed bf16 operand w1p
+// (from the slab tail, or from the main loop's elements [pack_off, +pack_len))
 void arm_sgd_next_prep(uintptr_t img, uintptr_t order, uintptr_t lab_all, uintptr_t lab_out, uintptr_t ctr,
                        int n_order, int B, int C, std::vector<float> mean, std::vector<float> stdv, uintptr_t xp,
                        int Cp, int H, int W, int sp, std::vector<uintptr_t> zp, std::vector<int64_t> zn,
-                       uintptr_t w1p, int w1_cp);
+                       uintptr_t w1p, int w1_cp, int64_t pack_off, int64_t pack_len);
 bool sgd_next_prep_armed();
+// reduce-only launch: split-K slabs of up to 4 ranges + 1 padded tail summed into g
+void slab_reduce_multi(uintptr_t g, int64_t n, std::vector<int64_t> offs, std::vector<int64_t> lens,
+                       std::vector<uintptr_t> slabs, std::vector<int> splits, std::vector<int64_t> tail,
+                       uintptr_t tail_slab, uintptr_t stream);
 void set_sgd_trim(bool on);  // update grid sized to the elements before a skipped suffix (default on)
 void disarm_sgd_next_prep();
 

@@ -2700,6 +2700,20 @@ void set_conv_side_sgd(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, u
   g_side_sgd = j;
 }
 
+// The next streaming conv_fwd launch sums the split-K weight-gradient slabs of
+// the given in-place ranges into the gradient buffer g (a reduce-only side job,
+// sgd_dev.h: bitwise slab_reduce's sums) as nblk extra workgroups (0: one
+// float4 per thread): a multi-node step's weight gradient, materialised for
+// its all-reduce on the CUs the dgrad leaves free instead of in a launch of
+// its own.  One-shot.
+void set_conv_side_reduce(uintptr_t g, int64_t lo, int64_t hi, std::vector<int64_t> offs, std::vector<int64_t> lens,
+                          std::vector<uintptr_t> slabs, std::vector<int> splits, int nblk) {
+  if (offs.empty()) throw std::runtime_error("set_conv_side_reduce: no slab range");
+  SgdJob j = make_reduce_job(g, lo, hi, offs, lens, slabs, splits, {}, 0);
+  j.nblk = nblk > 0 ? nblk : -1;
+  g_side_sgd = j;
+}
+
 // Arm (rows != 0) / disarm (rows == 0) the channels-last BatchNorm backward
 // reduce (BnRedArgs, BNR 2) for the following conv_fwd / conv_fwd_ex calls on
 // the streaming kernel: x = the BN's input [M][C] (the conv output's layout),

@@ -88,7 +88,8 @@ __global__ void __launch_bounds__(256) sgd_slabs_kernel(const SgdJob job, const 
     sgd_tail_block<kMomentum, kShadow>(job, blk - nmain);
     return;
   }
-  sgd_range_loop<kMomentum, kShadow>(job, blk, nmain);
+  if (job.red) slab_reduce_range_loop(job, blk, nmain);  // reduce-only job (slab_reduce_multi)
+  else sgd_range_loop<kMomentum, kShadow>(job, blk, nmain);
 }
 
 // x *= 1/n (n read from the all-reduced participation slot)
@@ -218,13 +219,20 @@ static PrepArgs g_next_prep{};
 static bool g_next_armed = false;
 static bf16_t* g_next_pack = nullptr;
 static int g_next_pack_cp = 0;
+static int64_t g_next_pack_off = 0, g_next_pack_len = 0;  // the first layer's elements in the updated buffer
 
+// pack_off / pack_len: the first conv layer's weight [Cout][taps][C] as an
+// element range of the buffer the consuming update writes -- packed from the
+// main loop when the layer is not the update's slab tail (its gradient was
+// all-reduced at N > 1, so the update reads it from the flat gradient).
 void arm_sgd_next_prep(uintptr_t img, uintptr_t order, uintptr_t lab_all, uintptr_t lab_out, uintptr_t ctr,
                        int n_order, int B, int C, std::vector<float> mean, std::vector<float> stdv, uintptr_t xp,
                        int Cp, int H, int W, int sp, std::vector<uintptr_t> zp, std::vector<int64_t> zn,
-                       uintptr_t w1p, int w1_cp) {
+                       uintptr_t w1p, int w1_cp, int64_t pack_off, int64_t pack_len) {
   if (g_next_armed) throw std::runtime_error("arm_sgd_next_prep: already armed (no sgd_update_slabs consumed it)");
   if (!xp || !w1p || w1_cp < C) throw std::runtime_error("arm_sgd_next_prep: input buffer / packed weights");
+  if (pack_off % 4 || pack_len % 4 || pack_off < 0 || pack_len <= 0 || pack_len % C)
+    throw std::runtime_error("arm_sgd_next_prep: the first layer's element range must be 16-byte aligned");
   PrepArgs a{};
   a.xp = (bf16_t*)xp; a.C = C; a.Cp = Cp; a.H = H; a.W = W; a.sp = sp;
   prep_set_gather(a, img, order, lab_all, lab_out, ctr, n_order, B, C, mean, stdv);
@@ -233,6 +241,8 @@ void arm_sgd_next_prep(uintptr_t img, uintptr_t order, uintptr_t lab_all, uintpt
   g_next_prep = a;
   g_next_pack = (bf16_t*)w1p;
   g_next_pack_cp = w1_cp;
+  g_next_pack_off = pack_off;
+  g_next_pack_len = pack_len;
   g_next_armed = true;
 }
 
@@ -260,8 +270,20 @@ void sgd_update_slabs(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, ui
   PrepArgs next{};
   if (g_next_armed) {
     g_next_armed = false;
-    if (job.r.tail_nblk == 0 || job.r.tail_c != g_next_prep.C)
-      throw std::runtime_error("sgd_update_slabs: preparing the next step needs the first layer as the tail range");
+    if (job.r.tail_nblk > 0) {  // the first layer is the slab tail: its blocks write the packed operand
+      if (job.r.tail_c != g_next_prep.C || job.r.tail_lo != g_next_pack_off)
+        throw std::runtime_error("sgd_update_slabs: the slab tail is not the first layer the next step packs");
+    } else {  // the main loop packs the first layer's range
+      const int64_t lo4 = g_next_pack_off / 4, hi4 = (g_next_pack_off + g_next_pack_len) / 4;
+      if (lo4 < job.lo4 || hi4 > job.hi4 || (lo4 < job.skip_hi4 && job.skip_lo4 < hi4))
+        throw std::runtime_error("sgd_update_slabs: the first layer is not updated by this launch's main loop");
+      for (int k = 0; k < job.r.n; ++k)
+        if (lo4 < job.r.hi4[k] && job.r.lo4[k] < hi4)
+          throw std::runtime_error("sgd_update_slabs: the first layer overlaps a slab range");
+      job.pack_lo4 = lo4;
+      job.pack_hi4 = hi4;
+      job.pack_c = g_next_prep.C;
+    }
     next = g_next_prep;
     job.tail_pack = g_next_pack;
     job.tail_pack_cp = g_next_pack_cp;
@@ -273,6 +295,23 @@ void sgd_update_slabs(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p16, ui
   else if (mom) sgd_slabs_kernel<true, false><<<grid, block, 0, s>>>(job, next);
   else if (p16) sgd_slabs_kernel<false, true><<<grid, block, 0, s>>>(job, next);
   else sgd_slabs_kernel<false, false><<<grid, block, 0, s>>>(job, next);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+// Reduce-only launch (no update): the split-K weight-gradient slabs of up to
+// 4 in-place ranges and one channel-padded tail summed into the gradient
+// buffer g of n floats -- the weight gradients a multi-node step all-reduces,
+// bitwise the stand-alone slab_reduce's, several layers per launch.
+void slab_reduce_multi(uintptr_t g, int64_t n, std::vector<int64_t> offs, std::vector<int64_t> lens,
+                       std::vector<uintptr_t> slabs, std::vector<int> splits, std::vector<int64_t> tail,
+                       uintptr_t tail_slab, uintptr_t stream) {
+  check_vec4(n, "slab_reduce_multi");
+  SgdJob job = make_reduce_job(g, 0, n, offs, lens, slabs, splits, tail, tail_slab);
+  int64_t n4 = 0;
+  for (int k = 0; k < job.r.n; ++k) n4 = std::max(n4, job.r.hi4[k] - job.r.lo4[k]);
+  if (job.r.n == 0 && job.r.tail_nblk == 0) return;
+  const int nmain = job.r.n ? stream_grid(n4) : 0;
+  sgd_slabs_kernel<false, false><<<nmain + job.r.tail_nblk, 256, 0, as_stream(stream)>>>(job, PrepArgs{});
   DL_HIP_CHECK(hipGetLastError());
 }
 

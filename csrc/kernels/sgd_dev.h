@@ -150,7 +150,29 @@ struct SgdJob {
   // when the launch prepares the next step (flat_ops.hip, prep_dev.h)
   bf16_t* tail_pack;
   int tail_pack_cp;
+  // ... or, when the first layer is not a tail range (its gradient was
+  // all-reduced: no slabs), the updated elements [pack_lo4, pack_hi4) of the
+  // main loop ([Cout][taps][pack_c] weights) go to tail_pack the same way
+  int64_t pack_lo4, pack_hi4;
+  int pack_c;
+  // reduce-only job (red != null): no update -- the slab sums of the ranges
+  // (and of the tail) are written to red (same indexing as p), bitwise the
+  // stand-alone slab_reduce's: a multi-node step's weight gradients
+  // materialised for the all-reduce in extra workgroups of another launch
+  float* red;
 };
+
+// The first-layer pack of an element range the main loop updated (pack_c of
+// 3: a float4 straddles two output channels' tap rows).
+__device__ __forceinline__ void pack_range4(const SgdJob& j, int64_t i, const float4& pv) {
+  const float v[4] = {pv.x, pv.y, pv.z, pv.w};
+  const int64_t e0 = (i - j.pack_lo4) * 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t e = e0 + k;
+    j.tail_pack[(e / j.pack_c) * j.tail_pack_cp + e % j.pack_c] = f32_to_bf16(v[k]);
+  }
+}
 
 template <bool kMomentum, bool kShadow>
 __device__ __forceinline__ void sgd_range_loop(const SgdJob& j, int bid, int nblk) {
@@ -173,6 +195,21 @@ __device__ __forceinline__ void sgd_range_loop(const SgdJob& j, int bid, int nbl
       packed.y = pack_bf16x2(pv.z, pv.w);
       reinterpret_cast<uint2*>(j.p16)[i] = packed;
     }
+    if (i >= j.pack_lo4 && i < j.pack_hi4) pack_range4(j, i, pv);
+  }
+}
+
+// Reduce-only job: the slab sums of every in-place range into j.red.
+__device__ __forceinline__ void slab_reduce_range_loop(const SgdJob& j, int bid, int nblk) {
+  const SlabRanges& r = j.r;
+  const int64_t stride = (int64_t)nblk * blockDim.x;
+  for (int k = 0; k < r.n; ++k) {
+    const float4* s0 = reinterpret_cast<const float4*>(r.slab[k]);
+    for (int64_t i = r.lo4[k] + (int64_t)bid * blockDim.x + threadIdx.x; i < r.hi4[k]; i += stride) {
+      const float4* s = s0 + (i - r.lo4[k]);
+      reinterpret_cast<float4*>(j.red)[i] =
+          r.tpo[k] == 8 ? slab_sum4<8>(s, r.stride4[k], r.splits[k]) : slab_sum4<1>(s, r.stride4[k], r.splits[k]);
+    }
   }
 }
 
@@ -182,6 +219,10 @@ __device__ __forceinline__ void sgd_tail_block(const SgdJob& j, int bid) {
   const SlabRanges& r = j.r;
   auto upd = [&](int64_t i, int64_t, int, float gs) {
     const int64_t e = r.tail_lo + i;  // KRSC weight: element i of the reduce's output order
+    if (j.red) {  // reduce-only job
+      j.red[e] = gs;
+      return;
+    }
     float mv = kMomentum ? j.mom[e] : 0.f;
     const float pv = sgd_elem<kMomentum>(j.p[e], gs, &mv, s, j.wd, j.lr, j.momentum);
     if constexpr (kMomentum) j.mom[e] = mv;
@@ -252,12 +293,24 @@ inline SgdJob make_sgd_job(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p1
   return j;
 }
 
+// Host: a reduce-only job writing the slab sums of the ranges (and of the
+// tail) into the gradient buffer g (float index space of the job).
+inline SgdJob make_reduce_job(uintptr_t g, int64_t lo, int64_t hi, const std::vector<int64_t>& offs,
+                              const std::vector<int64_t>& lens, const std::vector<uintptr_t>& slabs,
+                              const std::vector<int>& splits, const std::vector<int64_t>& tail, uintptr_t tail_slab) {
+  if (!g) throw std::runtime_error("reduce job: null gradient buffer");
+  SgdJob j = make_sgd_job(g, g, 0, 0, 0, 0.f, 0.f, 0.f, lo, hi, offs, lens, slabs, splits, tail, tail_slab);
+  j.red = (float*)g;
+  return j;
+}
+
 // A side job run by workgroup `bid` of the job's nblk extra workgroups of a
 // host launch (conv_fwd_kernel): no tail range, always a bf16 shadow (the
 // conv executors' flat buffers have one; make_side_job checks), momentum at
-// run time.
+// run time -- or a reduce-only job (red).
 __device__ __forceinline__ void sgd_side_block(const SgdJob& j, int bid) {
-  if (j.mom) sgd_range_loop<true, true>(j, bid, j.nblk);
+  if (j.red) slab_reduce_range_loop(j, bid, j.nblk);
+  else if (j.mom) sgd_range_loop<true, true>(j, bid, j.nblk);
   else sgd_range_loop<false, true>(j, bid, j.nblk);
 }
 

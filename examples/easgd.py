@@ -9,11 +9,17 @@ reference's flags.
 
 * client: grads = df(params, x, y); ``syncClient`` every ``--communicationTime``
   steps (elastic move against the server's center); then the SGD step with the
-  pre-move grads (EASGD_client.lua:106-117).  Sends BYE when done.
+  pre-move grads (EASGD_client.lua:106-117).  Sends BYE when done.  On a GPU
+  (CIFAR-10) the client trains through ``DataParallelTrainer(algo="async",
+  backend="hip", graph=True)``: the hand-written kernels, a device-side
+  sampler, and the tau-1 local steps between two syncs replayed as ONE
+  hipGraph (engine.run); it prints its images/s.
 * server: ``syncServer`` until every client said BYE; every ``--testTime``
   syncs ``testNet`` hands the tester a center snapshot WITHOUT blocking on the
   tester's evaluation (reference defect fixed).
-* tester: evaluates each snapshot on the train/test partitions, appends
+* tester: evaluates each snapshot on the train/test partitions (the HIP
+  executor's forward on a GPU, BatchNorm on the batch statistics like the
+  reference's functional model, examples/Model.lua:56-66), appends
   "Training Error"/"Test Error" to ``Results/<save>/ErrorRate.log``, logs to
   ``Log.txt`` and writes the ``Net``/``optState`` checkpoint.
 
@@ -29,10 +35,10 @@ import torch  # noqa: E402
 
 from torch_distlearn_amd import AsyncEA, FlatParams, Tree  # noqa: E402
 from torch_distlearn_amd.checkpoint import load_checkpoint, results_dir, save_checkpoint  # noqa: E402
-from torch_distlearn_amd.data import Dataset  # noqa: E402
+from torch_distlearn_amd.data import Dataset, DeviceLoader  # noqa: E402
+from torch_distlearn_amd.engine import DataParallelTrainer, predict_module  # noqa: E402
 from torch_distlearn_amd.launch import device_of  # noqa: E402
-from torch_distlearn_amd.models import CifarConvNet, MnistConvNet  # noqa: E402
-from torch_distlearn_amd.ops.flat import flat_sgd_  # noqa: E402
+from torch_distlearn_amd.models import CifarConvNet, MnistConvNet, make_executor  # noqa: E402
 from torch_distlearn_amd.parallel.comm import CommError  # noqa: E402
 from torch_distlearn_amd.utils.color_print import set_verbose  # noqa: E402
 from torch_distlearn_amd.utils.metrics import ConfusionMatrix, Logger  # noqa: E402
@@ -59,6 +65,9 @@ def parse():
     ap.add_argument("--trainSize", type=int, default=50000)
     ap.add_argument("--testSize", type=int, default=10000)
     ap.add_argument("--cuda", action="store_true")
+    ap.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"],
+                    help="auto = the hand-written HIP executor for CIFAR-10 on a GPU, PyTorch ops otherwise")
+    ap.add_argument("--graph", type=int, default=1, help="hipGraph capture of the client's steps (GPU)")
     ap.add_argument("--gpu", type=int, default=None)
     ap.add_argument("--host", default=os.environ.get("MASTER_ADDR", "127.0.0.1"))
     ap.add_argument("--port", type=int, default=int(os.environ.get("MASTER_PORT", "8080")))
@@ -107,11 +116,14 @@ def run(opt):
 
     torch.manual_seed(0)
     model = (CifarConvNet(seed=0) if opt.dataset == "cifar10" else MnistConvNet(seed=0)).to(dev)
-    flat = FlatParams(model, grads=True, shadow_bf16=False)
     ea = AsyncEA(tree, None, None, None, None, None, N, rank, opt.communicationTime, opt.alpha)
     cd = torch.bfloat16 if dev.type == "cuda" else torch.float32
+    hip = opt.backend == "hip" or (opt.backend == "auto" and dev.type == "cuda" and opt.dataset == "cifar10")
+    if hip and (dev.type != "cuda" or opt.dataset != "cifar10"):
+        raise SystemExit("easgd: --backend hip needs --cuda and the CIFAR-10 convnet")
 
     if role == "server":
+        flat = FlatParams(model, grads=False, shadow_bf16=False)
         if opt.resume:
             st = load_checkpoint(results_dir(opt.save, opt.resultsRoot), model)  # Net = the last tested center
             ea.syncs = int(st.get("server_syncs", 0))
@@ -123,42 +135,60 @@ def run(opt):
         ea.shutdown()
         print(f"server: {ea.syncs} syncs")
     elif role == "client":
+        import time
+
         ds = Dataset(opt.dataset, rank, N, train=True, synthetic_size=opt.trainSize, device=dev)
-        b = ds.sampledBatcher("permutation", opt.batchSize, dtype=cd, seed=rank)
-        ea.initClient(flat)
-        model.train()
+        # grads -> syncClient (elastic move) -> SGD with the pre-move grads, every
+        # step (EASGD_client.lua:97-119): DataParallelTrainer(algo="async") does
+        # exactly that, on the HIP executor with unrolled hipGraphs on a GPU
+        tr = DataParallelTrainer(model, tree, lr=opt.learningRate, algo="async", tau=opt.communicationTime,
+                                 alpha=opt.alpha, backend="hip" if hip else "torch", compute_dtype=cd,
+                                 graph=bool(opt.graph) and dev.type == "cuda", max_batch=opt.batchSize, async_ea=ea)
+        fast = hip and tr.graph
+        b = (DeviceLoader(ds, "permutation", opt.batchSize, seed=rank) if fast
+             else ds.sampledBatcher("permutation", opt.batchSize, dtype=cd, seed=rank))
+        tr.synchronize_parameters()  # initClient: receive the server's center
+        die = [int(v) for v in opt.dieAfter.split(":")] if opt.dieAfter else None
+        loss, steps, t0 = None, 0, time.perf_counter()
         for _ in range(opt.numEpochs):
             nb = b.numBatches() if not opt.maxSteps else min(opt.maxSteps, b.numBatches())
-            for _ in range(nb):
-                x, y = b.getBatch()
-                flat.grad.zero_()
-                loss = model.loss(model(x, compute_dtype=cd), y)
-                loss.backward()
-                ea.syncClient(flat)                                  # EASGD_client.lua:109
-                if opt.dieAfter and [rank, ea.syncs] == [int(v) for v in opt.dieAfter.split(":")]:
+            done = 0
+            while done < nb:
+                # a syncing step at most every tau steps: run up to the next one
+                k = min(nb - done, opt.communicationTime - ea.step % opt.communicationTime) if fast else 1
+                loss = tr.run(b, k) if fast else tr.step(*b.getBatch())
+                done += k
+                if die and [rank, ea.syncs] == die:
                     os._exit(3)  # fault injection: this client dies without saying BYE
-                flat_sgd_(flat, opt.learningRate)  # :113-117 (pre-move grads)
-        ea.finishClient()
-        print(f"client {rank}: {ea.syncs} syncs, last loss {float(loss.detach()):.4f}")
+            steps += done
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        tr.finish()  # BYE
+        print(f"client {rank}: {ea.syncs} syncs, {steps} steps, {steps * opt.batchSize / max(dt, 1e-9):.1f} img/s, "
+              f"last loss {float(loss.detach()):.4f}")
     else:
         out = results_dir(opt.save, opt.resultsRoot)
         err_log = Logger(os.path.join(out, "ErrorRate.log"), ["Training Error", "Test Error"])
         txt = open(os.path.join(out, "Log.txt"), "a")
         txt.write(" ".join(sys.argv) + "\n")
-        tr = Dataset(opt.dataset, 1, 1, train=True, synthetic_size=min(opt.trainSize, 2048), device=dev)
+        trd = Dataset(opt.dataset, 1, 1, train=True, synthetic_size=min(opt.trainSize, 2048), device=dev)
         te = Dataset(opt.dataset, 1, 1, train=False, synthetic_size=min(opt.testSize, 2048), device=dev)
+        flat = FlatParams(model, grads=True, shadow_bf16=hip)
+        # the reference tester evaluates the snapshot with its training-mode
+        # functional model (batch statistics, EASGD_tester.lua:109-159)
+        ex = make_executor(model, flat, max_batch=256) if hip else None
         ea.initTester(flat)
         n = 0
         while ea.startTest(flat):
-            model.eval()
             errs = []
-            for ds in (tr, te):
+            for ds in (trd, te):
                 conf = ConfusionMatrix(10, device=dev)
                 b = ds.sampledBatcher("linear", 256, dtype=cd)
-                with torch.no_grad():
-                    for _ in range(b.numBatches()):
-                        x, y = b.getBatch()
-                        conf.add(model(x, compute_dtype=cd), y)
+                for _ in range(b.numBatches()):
+                    x, y = b.getBatch()
+                    conf.add(ex.predict(x, batch_stats=True) if ex is not None
+                             else predict_module(model, x, cd, batch_stats=True), y)
                 errs.append(1.0 - conf.totalValid)
             err_log.add({"Training Error": errs[0], "Test Error": errs[1]})
             txt.write(f"snapshot {n}: train error {errs[0]:.4f} test error {errs[1]:.4f}\n")

@@ -458,3 +458,62 @@ def test_policy_selected_on_the_machine(dev, monkeypatch):
     loss = tr.run(ld, 6, unroll=4)
     torch.cuda.synchronize()
     assert torch.isfinite(loss).all() and int(tr.sgd.stepsPerNode.sum()) == 6
+
+
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+def test_multinode_fused_reduce_is_bitwise(dev, monkeypatch, momentum):
+    """The multi-node step configuration (gradients all-reduced: world-1
+    collectives forced through RCCL, so no one-node slab deferral): the
+    split-K slab sums ride block 3's dgrad launch and ONE reduce-only launch
+    sums blocks 1-2 (executor fuse_slab_reduces), and the full-buffer update
+    launch prepares the next step of the unrolled graph (its batch, zeroed
+    accumulators, the first layer's packed operand from the main loop) --
+    parameters after unrolled training across an epoch boundary are BITWISE
+    those of the plain path (a slab_reduce launch per layer, a prep launch
+    per step)."""
+    from torch_distlearn_amd import Tree
+    from torch_distlearn_amd.data import DeviceLoader, PartitionedDataset, synthetic_cifar10
+    from torch_distlearn_amd.engine import DataParallelTrainer
+    from torch_distlearn_amd.models import CifarConvNet
+
+    monkeypatch.setenv("DISTLEARN_RCCL_WORLD1", "1")
+    imgs, labels = synthetic_cifar10(1024, seed=5)
+    outs = []
+    for fuse, nxt in (("0", "0"), ("1", "0"), ("1", "1")):
+        monkeypatch.setenv("DISTLEARN_FUSE_REDUCE", fuse)
+        monkeypatch.setenv("DISTLEARN_PREP_NEXT", nxt)
+        tree = Tree(1, 1, host="127.0.0.1", port=29716, device=dev)
+        model = CifarConvNet(seed=4).to(dev)
+        tr = DataParallelTrainer(model, tree, lr=0.02, momentum=momentum, backend="hip",
+                                 compute_dtype=torch.bfloat16, graph=True, max_batch=128)
+        tr.synchronize_parameters()
+        assert tr.reduces_grads and tr._slabs is None and tr._side is None
+        if fuse == "1":
+            assert tr._fused_reduce == {"ride": [2], "merged": [0, 1]}, tr._fused_reduce
+        else:
+            assert tr._fused_reduce is None
+        ld = DeviceLoader(PartitionedDataset(imgs, labels, device=dev), "permutation", 128, seed=2)
+        tr.run(ld, 11, unroll=4)
+        torch.cuda.synchronize()
+        assert (tr.executor.prepared_ahead > 0) == (nxt == "1")
+        assert not tr.executor.C.sgd_next_prep_armed()
+        outs.append(tr.flat.data.clone())
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
+
+
+def test_policy_change_drops_captured_graphs(dev, monkeypatch):
+    """a policy switch re-allocates the executor's workspaces, so
+    graphs captured before it (step() with graph=True) must never replay:
+    select_policy with a forced policy after a captured step drops them and
+    the next run() recaptures and trains on the new buffers."""
+    monkeypatch.setenv("DISTLEARN_POLICY", "reserve")
+    tr = _trainer(dev, "hip", True, 29717)
+    ld = _loader(dev)
+    tr.step(ld)
+    assert tr._graph is not None
+    old = tr._graph
+    tr.run(ld, 4, unroll=2)
+    torch.cuda.synchronize()
+    assert tr.policy["chosen"] == "reserve" and tr._graph is not old
+    assert (tr.executor.dgrad_stages, tr.executor.cu_reserve) == (2, tr.executor.policies()["reserve"]["cu_reserve"])
+    assert torch.isfinite(tr.flat.data).all() and int(tr.sgd.stepsPerNode.sum()) == 5

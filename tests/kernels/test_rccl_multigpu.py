@@ -447,3 +447,27 @@ def test_rccl_abort_waits_for_open_group(monkeypatch):
     with pytest.raises(CommError):
         comm.all_reduce(x)
     comm.close()
+
+
+def test_rccl_watchdog_pause_is_synchronous(monkeypatch):
+    """pause_watch(True) -- what every hipGraph capture
+    runs first (engine._capturing) -- returns only when no watchdog poll is in
+    progress, and no poll runs until resumed (csrc/comm/pause_gate.h; the
+    handshake itself is TSan-tested on the CPU, tests/unit/test_capture_guard.py)."""
+    import time
+
+    dev, comm = _world1(monkeypatch)
+    x = torch.ones(1024, device=dev)
+    comm.all_reduce(x)
+    time.sleep(0.3)  # the watchdog polls every 50 ms
+    assert comm._c.polls() > 0
+    for _ in range(5):
+        comm.pause_watch(True)
+        n = comm._c.polls()
+        time.sleep(0.2)
+        assert comm._c.polls() == n
+        comm.pause_watch(False)
+        time.sleep(0.2)
+        assert comm._c.polls() > n
+    assert _drained(comm) and comm.health() == ""
+    comm.close()

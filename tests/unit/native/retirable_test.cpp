@@ -49,6 +49,13 @@ static void state_machine() {
   Retirable<int> d(3);
   d.acquire();
   CHECK(d.release() == 0 && d.get() == 3);
+  // a call that never returns: after the grace period the watchdog takes the
+  // doomed handle and aborts it anyway; the late release finds nothing to abort
+  Retirable<int> f(6);
+  f.acquire();
+  CHECK(f.retire() == 0 && f.doomed());
+  CHECK(f.take_doomed() == 6);
+  CHECK(f.release() == 0 && !f.doomed() && f.inflight() == 0);
   // destroy path
   Retirable<int> e(4);
   e.acquire();

@@ -38,6 +38,7 @@ from .ops.flat import FlatParams, fill_
 from .parallel.allreduce_ea import AllReduceEA
 from .parallel.allreduce_sgd import AllReduceSGD
 from .parallel.buckets import GradBucketer
+from .parallel.comm import runs_collectives
 from .parallel.tree import Tree
 
 
@@ -82,6 +83,22 @@ def _capturing(comm):
             gc.enable()
         if pause is not None:
             pause(False)
+
+
+@torch.no_grad()
+def predict_module(model: torch.nn.Module, x: torch.Tensor, compute_dtype, batch_stats: bool = False):
+    """Forward of a PyTorch-path model without training side effects: eval
+    mode, or train-mode BatchNorm on the batch's statistics with the running
+    statistics restored afterwards."""
+    was = model.training
+    saved = [(b, b.detach().clone()) for b in model.buffers()] if batch_stats else []
+    model.train(batch_stats)
+    try:
+        return model(x, compute_dtype=compute_dtype)
+    finally:
+        for b, v in saved:
+            b.detach().copy_(v)
+        model.train(was)
 
 
 class DataParallelTrainer:
@@ -154,16 +171,27 @@ class DataParallelTrainer:
                 and os.environ.get("DISTLEARN_BUCKET_UPDATE", "0") == "1"):
             self.bucket_updates = self.sgd.enable_bucket_updates(
                 self.flat, lambda: self.lr, momentum=momentum, weight_decay=weight_decay, momentum_buf=self.mom)
-        # One node: the conv executor leaves the split-K weight gradients of the
-        # layers whose slabs the update can read in their slabs, and the fused SGD
-        # sums them itself (bitwise the same update, two launches fewer per step;
-        # nothing is all-reduced at one node).  DISTLEARN_DEFER_SLABS=0: off (A/B).
+        # Whether the gradients go through a collective: AllReduceSGD at N > 1
+        # (or at world 1 with the collectives forced through RCCL -- the
+        # multi-node configuration rehearsed on one GPU, bench.py --nworld-path).
+        # AllReduceEA all-reduces elastic deltas, never gradients.
+        self.reduces_grads = algo == "sgd" and runs_collectives(tree.comm)
+        # Gradients nobody all-reduces: the conv executor leaves the split-K
+        # weight gradients of the layers whose slabs the update can read in
+        # their slabs, and the fused SGD sums them itself (bitwise the same
+        # update, two launches fewer per step).  DISTLEARN_DEFER_SLABS=0: off (A/B).
+        # Gradients that are all-reduced: the slab sums ride the dgrad launches /
+        # one merged reduce launch (executor fuse_slab_reduces; DISTLEARN_FUSE_REDUCE=0: off).
         self._slabs = None
-        if (tree.numNodes == 1 and algo in ("sgd", "ea") and not self.bucket_updates
+        self._fused_reduce = None
+        if (not self.reduces_grads and algo in ("sgd", "ea", "async") and not self.bucket_updates
                 and self.grad_comm_dtype == "fp32"  # a bf16 wire copy would be cast from the stale fp32 grads
                 and callable(getattr(self.executor, "defer_slab_reduce", None))
                 and os.environ.get("DISTLEARN_DEFER_SLABS", "1") == "1"):
             self._slabs = self.executor.defer_slab_reduce() or None
+        elif (self.reduces_grads and callable(getattr(self.executor, "fuse_slab_reduces", None))
+              and os.environ.get("DISTLEARN_FUSE_REDUCE", "1") == "1"):
+            self._fused_reduce = self.executor.fuse_slab_reduces() or None
         self._side = None
         self._arm_side_update()
         # executor policy for the world > 1 overlap (select_policy): None until chosen
@@ -197,10 +225,13 @@ class DataParallelTrainer:
         loss.backward()
         return loss.detach()
 
-    def _step_body(self, x: torch.Tensor, y: torch.Tensor, prep_next: bool = False) -> torch.Tensor:
+    def _step_body(self, x: torch.Tensor, y: torch.Tensor, prep_next: bool = False,
+                   local: bool = False) -> torch.Tensor:
         """The capturable part of a step: zero grads, forward, backward and
         the update (SGD: bucketed all-reduce + fused 1/n SGD; EA: the local
-        SGD step -- the elastic round every tau steps runs after it).
+        SGD step -- the elastic round every tau steps runs after it; AsyncEA:
+        the local SGD step only when ``local`` -- a step that syncs with the
+        server runs its update after the sync, EASGD_client.lua:106-117).
         ``prep_next``: another step on the same DeviceLoader follows in the
         same graph; the update launch prepares it (executor arm_next_prep)."""
         f = self.flat
@@ -214,14 +245,14 @@ class DataParallelTrainer:
             for h in self.step_hooks:
                 h(self.last_logits(), labels)
         armed = False
-        if prep_next and self._slabs is not None and os.environ.get("DISTLEARN_PREP_NEXT", "1") == "1":
+        if prep_next and self._update_preps_next() and os.environ.get("DISTLEARN_PREP_NEXT", "1") == "1":
             arm = getattr(self.executor, "arm_next_prep", None)
             armed = bool(arm(x)) if arm is not None else False
         try:
             if self.algo == "sgd":
                 self.sgd.step(f, self.lr, momentum=self.momentum, weight_decay=self.weight_decay,
                               momentum_buf=self.mom, slabs=self._slabs, skip=self._side)
-            elif self.algo == "ea":
+            elif self.algo == "ea" or (self.algo == "async" and local):
                 self._local_update()
         except BaseException:
             if armed:  # the update never consumed the next-step preparation
@@ -229,6 +260,14 @@ class DataParallelTrainer:
                 self.executor._prefetched = False
             raise
         return loss
+
+    def _update_preps_next(self) -> bool:
+        """Whether the step's final update is ONE fused fp32 SGD launch that can
+        also prepare the next step of an unrolled graph (flat_sgd_ consumes an
+        armed arm_next_prep): not per-bucket updates, not the bf16 gradient
+        wire (its update reads the bf16 copy), not an AsyncEA client."""
+        return (self.algo in ("sgd", "ea", "async") and not self.bucket_updates and self.grad_comm_dtype == "fp32"
+                and (self._slabs is not None or self.reduces_grads or self.algo != "sgd"))
 
     def _local_update(self) -> None:
         from .ops.flat import flat_sgd_
@@ -250,8 +289,13 @@ class DataParallelTrainer:
             dev_loader = None
         else:
             dev_loader = loader
+        # AsyncEA: a step that does not sync with the server runs its local
+        # update in the step body; a syncing step updates after syncClient
+        # (EASGD_client.lua:106-117).  The single-step graph is the syncing
+        # step's body (run() replays the local steps as unrolled graphs).
+        local = self.aea is not None and (self.aea.step + 1) % self.aea.tau != 0
         if not self.graph:
-            loss = self._step_body(x, y)
+            loss = self._step_body(x, y, local=local)
         else:
             if self._graph is None:
                 self._capture(x, y)
@@ -272,8 +316,13 @@ class DataParallelTrainer:
             # every tau steps: fused elastic kernel + one all-reduce (lua/AllReduceEA.lua:25-47)
             self.ea.averageParameters(self.flat)
         elif self.aea is not None:
-            self.aea.syncClient(self.flat)   # EASGD_client.lua:109
-            self._local_update()             # :113-117 (pre-move grads)
+            if local:  # no sync this step (AsyncEA.lua:49-59)
+                self.aea.step += 1
+                if self.graph:
+                    self._local_update()
+            else:
+                self.aea.syncClient(self.flat)   # EASGD_client.lua:109
+                self._local_update()             # :113-117 (pre-move grads)
         if loader is not None:
             loader.step_done()
         self.last_loss = loss
@@ -312,13 +361,24 @@ class DataParallelTrainer:
                 if phase == 0 and cap >= self.ea.tau and self._ea_key() in self._multi:
                     key = self._ea_key()
                 cap = min(cap, self.ea.tau - 1 - phase)  # local steps before the round-triggering one
-            k = self.ea.tau if key is not None else (
-                max((u for u in self._multi if isinstance(u, int) and u <= cap), default=1) if fast else 1)
-            if k > 1:
+            elif fast and self.aea is not None:
+                # the local steps before the next syncing one: one graph of all
+                # tau - 1 of them when the cycle starts here, else the largest fitting
+                phase = self.aea.step % self.aea.tau
+                cap = min(cap, self.aea.tau - 1 - phase)
+                if phase == 0 and cap == self.aea.tau - 1 and self._async_key() in self._multi:
+                    key = self._async_key()
+            if key is not None:
+                k = key[1]
+            else:
+                k = max((u for u in self._multi if isinstance(u, int) and u <= cap), default=1) if fast else 1
+            if k > 1 or (key is not None and k >= 1):
                 g, loss = self._multi[key if key is not None else k]
                 g.replay()
                 if self.ea is not None:
                     self.ea.step += k  # the graph ran k local steps (+ the round when key is set)
+                elif self.aea is not None:
+                    self.aea.step += k  # k local steps (updates inside the graph), no sync
                 for _ in range(k):
                     if self.sgd is not None:
                         self.sgd._count_step()
@@ -333,10 +393,13 @@ class DataParallelTrainer:
         return loss
 
     def _unrolled(self, unroll: int) -> bool:
-        return self.graph and self.algo in ("sgd", "ea") and self.executor is not None and unroll > 1
+        return self.graph and self.algo in ("sgd", "ea", "async") and self.executor is not None and unroll > 1
 
     def _ea_key(self):
         return ("ea", self.ea.tau)
+
+    def _async_key(self):
+        return ("async", self.aea.tau - 1)
 
     @staticmethod
     def _unroll_sizes(unroll: int):
@@ -362,6 +425,8 @@ class DataParallelTrainer:
         new = [k for k in self._unroll_sizes(unroll) if k not in self._multi]
         if self.ea is not None and self.ea.tau > 1 and self._ea_key() not in self._multi:
             new.append(self._ea_key())
+        if self.aea is not None and self.aea.tau > 1 and self._async_key() not in self._multi:
+            new.append(self._async_key())
         for k in new:
             self._capture_multi(loader, k)
         if new:
@@ -416,6 +481,7 @@ class DataParallelTrainer:
         self._side = None
         ex = self.executor
         if (self._slabs is None or os.environ.get("DISTLEARN_SIDE_SGD", "1") != "1"
+                or self.algo == "async"  # a syncing step's update must follow the elastic move
                 or not callable(getattr(ex, "side_update", None))):
             return
         rng = ex.side_update(lambda: self.lr, self.momentum, self.weight_decay, self.mom,
@@ -423,10 +489,17 @@ class DataParallelTrainer:
         self._side = rng
 
     def _set_policy(self, kw: dict) -> None:
+        """Switch the executor's policy.  It re-allocates the workspaces, so
+        every graph captured before would replay on freed buffers: they are
+        dropped, and the slab plans are redone for the new slabs."""
         self.executor.set_policy(**kw)
+        self._graph, self._static = None, None
+        self._multi = {}
         if self._slabs is not None:  # the re-planned workspaces have new slabs
             self._slabs = self.executor.defer_slab_reduce() or None
             self._arm_side_update()
+        if self._fused_reduce is not None:
+            self._fused_reduce = self.executor.fuse_slab_reduces() or None
 
     def _time_step_graph(self, loader, reps: int) -> float:
         """ms per replay of a freshly captured one-step graph (state restored;
@@ -480,14 +553,17 @@ class DataParallelTrainer:
     def _capture_multi(self, loader, k):
         """Capture k consecutive step bodies on ``loader`` into one graph
         (capture records kernels without running them; replay counts the steps).
-        k = ("ea", tau): tau local steps followed by the AllReduceEA elastic round."""
+        k = ("ea", tau): tau local steps followed by the AllReduceEA elastic round;
+        ("async", n) or an int k for an AsyncEA client: k local steps (each with
+        its local update), no sync."""
         self.captures += 1
-        ea_round = isinstance(k, tuple)
-        n = k[1] if ea_round else k
+        ea_round = isinstance(k, tuple) and k[0] == "ea"
+        n = k[1] if isinstance(k, tuple) else k
+        local = self.aea is not None
         g = torch.cuda.CUDAGraph()
         with _capturing(self.tree.comm), torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
             for j in range(n):
-                loss = self._step_body(loader, None, prep_next=j + 1 < n)
+                loss = self._step_body(loader, None, prep_next=j + 1 < n, local=local)
             if ea_round:
                 self.ea.elastic_round()
         if self.sgd is not None:
@@ -584,11 +660,10 @@ class DataParallelTrainer:
         return self._last_logp
 
     @torch.no_grad()
-    def predict(self, x: torch.Tensor) -> torch.Tensor:
+    def predict(self, x: torch.Tensor, batch_stats: bool = False) -> torch.Tensor:
+        """Log-probabilities of ``x``: eval-mode BatchNorm (running
+        statistics), or ``batch_stats=True`` -- the batch's own statistics,
+        running statistics untouched (the reference AsyncEA tester's mode)."""
         if self.executor is not None:
-            return self.executor.predict(x)
-        self.model.eval()
-        try:
-            return self.model(x, compute_dtype=self.compute_dtype)
-        finally:
-            self.model.train()
+            return self.executor.predict(x, batch_stats=batch_stats)
+        return predict_module(self.model, x, self.compute_dtype, batch_stats)

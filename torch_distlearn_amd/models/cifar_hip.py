@@ -40,6 +40,8 @@ from typing import List, Optional
 import torch
 
 from .._native import native, stream_handle
+from ..ops.flat import HEADER
+from ..parallel.comm import runs_collectives
 from .cifar_convnet import BN_EPS, BN_MOMENTUM, KSIZE, CifarConvNet
 
 BF16 = torch.bfloat16
@@ -174,7 +176,7 @@ class CifarHIPExecutor:
         # two workgroups fit a CU) by 1 us; the region dgrad (layer 2) by 1 us.
         # With a real all-reduce (world > 1) the dgrads use the 2-stage ring.
         comm = getattr(bucketer, "comm", None)
-        overlapped = comm is not None and getattr(comm, "world_size", 1) > 1
+        overlapped = comm is not None and runs_collectives(comm)
         # 4 stages switch the streaming kernel to its fragment-prefetch loop (csrc
         # conv_fwd_kernel, g_fwd_pf; fwd via DISTLEARN_FWD_STAGES=4): measured -1.3 % on one
         # box and +0.7 % on the next (profiles/r3_fwd_prefetch_ab.txt), so 3 stays.
@@ -279,6 +281,11 @@ class CifarHIPExecutor:
         self.rows = {0: 0, 1: 1, 2: int(os.environ.get("DISTLEARN_REDUCE_ROWS", "16"))}[self.mode]
         self._alloc(self.B)
         self._deferred = ()  # blocks whose weight-gradient slab reduce the update performs (defer_slab_reduce)
+        # multi-node step (fuse_slab_reduces): blocks whose slabs are summed by
+        # extra workgroups of their own dgrad launch, and blocks summed together
+        # by one reduce-only launch after the last weight gradient
+        self._ride: dict = {}
+        self._merged: tuple = ()
         self._prefetched = False  # the coming step was prepared by the last update launch (arm_next_prep)
         self.prepared_ahead = 0   # steps armed that way (counted at capture)
         self._side = None    # side SGD carried by a dgrad launch (side_update)
@@ -636,6 +643,11 @@ class CifarHIPExecutor:
                     pending = (sargs, i)
                 elif i in self._deferred:
                     pass  # summed by the update kernel (defer_slab_reduce)
+                elif i in self._ride:
+                    pass  # summed by extra workgroups of this block's dgrad (fuse_slab_reduces)
+                elif i in self._merged:
+                    if i == self._merged[0]:  # the last merged block's wgrad: one launch sums them all
+                        self._reduce_merged(s)
                 else:
                     if self.side_reduce and i > 0:  # overlaps this block's dgrad (block 1 has none)
                         side.wait_stream(main)
@@ -649,10 +661,13 @@ class CifarHIPExecutor:
                 main.wait_stream(side)
                 side_pending = False
             side_pending |= rs is side
-            if pending is None or pending[1] != i:
+            if i in self._ride or (i in self._merged and i != self._merged[0]):
+                pass  # ready once the launch that sums its slabs is enqueued
+            elif pending is None or pending[1] != i:
                 with torch.cuda.stream(rs):
-                    for j in range(4):
-                        self._ready(self._leaf(i, j))
+                    for b in (self._merged if i in self._merged else (i,)):
+                        for j in range(4):
+                            self._ready(self._leaf(b, j))
             if i > 0:
                 dt, ds = self.dgrad_plan[i]
                 if self.dgrad_stages != 3:
@@ -668,9 +683,14 @@ class CifarHIPExecutor:
                 else:
                     if self._side is not None and i == self._side["block"]:
                         self._arm_side()  # this launch also runs the update of blocks >= i
+                    elif i in self._ride:
+                        C.set_conv_side_reduce(*self._ride[i])  # ... or sums this block's weight-gradient slabs
                     C.conv_fwd(dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), 0,
                                self.slabs.data_ptr(), B, h, h, cout, cin, KSIZE,
                                dt | _slab_cap_bits(ds) | ((1 << 20) if keep else 0), ds, s)
+                    if i in self._ride:
+                        for j in range(4):
+                            self._ready(self._leaf(i, j))
                 dp_splits = ds if keep else 0
                 if self.dgrad_stages != 3:
                     C.set_conv_stages(3, self._wgrad_stages)
@@ -702,6 +722,7 @@ class CifarHIPExecutor:
         self._alloc(self.B)
         self._deferred = ()
         self._side = None
+        self._ride, self._merged = {}, ()
 
     def side_update(self, lr_fn, momentum: float, weight_decay: float, mom, slot, block: Optional[int] = None):
         """Run the SGD update of every parameter from block ``block``'s conv
@@ -719,13 +740,8 @@ class CifarHIPExecutor:
             block = int(os.environ.get("DISTLEARN_SIDE_SGD_BLOCK", str(nb - 2)))
         if not (0 < block < nb) or self.flat.shadow is None:
             return None
-        dt, ds = self.dgrad_plan[block]
-        h, cout, cin = self.hs[block], self.couts[block], self.cins[block]
-        if self.C.conv_region_ok(self.B, h, h, cout, cin, KSIZE, dt, ds):
-            return None  # the dgrad runs on the region kernel (its LDS leaves no room beside it)
-        keep = self.fuse_combine and ds in (2, 4, 8)
-        if self.dgrad_bnred and ds == 1 and not keep:
-            return None  # (a region dgrad with the fused BN reduce)
+        if not self._dgrad_hosts_side_job(block):
+            return None
         f = self.flat
         lo, hi = f.offsets[self._leaf(block, 0)], f.total
         base = f.data.data_ptr()
@@ -741,6 +757,67 @@ class CifarHIPExecutor:
                       "slabs": ([o for o, _, _, _ in slabs], [n for _, n, _, _ in slabs],
                                 [t for _, _, t, _ in slabs], [k for _, _, _, k in slabs])}
         return lo, hi
+
+    def _dgrad_hosts_side_job(self, block: int) -> bool:
+        """Whether block ``block``'s dgrad is a streaming conv launch that can
+        carry extra workgroups (csrc SgdJob side job): not the region kernel
+        (its dynamic LDS leaves no room beside it) and not the region dgrad
+        with the fused BN reduce."""
+        if not 0 < block < self.nb:
+            return False
+        dt, ds = self.dgrad_plan[block]
+        h, cout, cin = self.hs[block], self.couts[block], self.cins[block]
+        if self.C.conv_region_ok(self.B, h, h, cout, cin, KSIZE, dt, ds):
+            return False
+        keep = self.fuse_combine and ds in (2, 4, 8)
+        return not (self.dgrad_bnred and ds == 1 and not keep)
+
+    def fuse_slab_reduces(self) -> dict:
+        """Multi-node step: the weight gradients are all-reduced, so their
+        split-K slabs must be summed before the bucket holding them launches
+        (the one-node update sums them itself instead: defer_slab_reduce).
+        Rather than one slab_reduce launch per layer, a layer whose dgrad is a
+        streaming launch has its slabs summed by extra workgroups of that
+        dgrad (csrc set_conv_side_reduce, on the CUs its grid leaves free),
+        and the other layers are summed together by ONE reduce-only launch
+        after the last of their weight gradients (slab_reduce_multi: up to 4
+        unpadded ranges + the first layer's channel-padded 128-way slabs).
+        Every sum is bitwise the stand-alone reduce's (sgd_dev.h).  A layer's
+        gradients are reported to the bucketer once the launch that sums them
+        is enqueued (CIFAR: blocks 1-2 share the last bucket, so merging them
+        delays no all-reduce).  Returns {"ride": [...], "merged": [...]}."""
+        self._ride, self._merged = {}, ()
+        if self.mode == 1 or self.side_wgrad or self.side_reduce or self.merge_slab:
+            return {}
+        f = self.flat
+        slab_blocks = [i for i in range(self.nb) if not self.wplan[i][2]]
+        unpadded = lambda i: self.cins[i] == self.cins_real[i] and self.wplan[i][1] < 32  # noqa: E731
+        ride = [i for i in slab_blocks if unpadded(i) and self._dgrad_hosts_side_job(i)]
+        rest = [i for i in slab_blocks if i not in ride]
+        inplace = [i for i in rest if unpadded(i)][:4]
+        padded = [i for i in rest if not unpadded(i)][:1]
+        for i in ride:
+            lf = self._leaf(i, 0)
+            off, n = f.offsets[lf], f.numels[lf]
+            self._ride[i] = (f.grad.data_ptr(), off, off + n, [off], [n], [self.wslab_l[i].data_ptr()],
+                             [self.wplan[i][1]], 0)
+        merged = sorted(inplace + padded)
+        if merged:
+            lfs = {i: self._leaf(i, 0) for i in merged}
+            tail, tslab = [], 0
+            if padded:
+                i = padded[0]
+                tail = [f.offsets[lfs[i]], f.numels[lfs[i]], self.wplan[i][1], self.couts[i], KSIZE * KSIZE,
+                        self.cins[i], self.cins_real[i]]
+                tslab = self.wslab_l[i].data_ptr()
+            self._merged_args = (f.grad.data_ptr(), f.total, [f.offsets[lfs[i]] for i in inplace],
+                                 [f.numels[lfs[i]] for i in inplace], [self.wslab_l[i].data_ptr() for i in inplace],
+                                 [self.wplan[i][1] for i in inplace], tail, tslab)
+            self._merged = tuple(merged)  # ascending: [0] is the last one the backward reaches
+        return {"ride": sorted(self._ride), "merged": list(self._merged)}
+
+    def _reduce_merged(self, s: int) -> None:
+        self.C.slab_reduce_multi(*self._merged_args, s)
 
     def _arm_side(self) -> None:
         sd = self._side
@@ -781,16 +858,17 @@ class CifarHIPExecutor:
         advanced by this step's head kernel.  False (nothing armed) when the
         update cannot carry it: the first layer's slab reduce not deferred,
         the dgrad transposes in the prep launch, no device loader."""
-        if (not hasattr(loader, "gather_args") or 0 not in self._deferred or self.cins[0] == self.cins_real[0]
+        if (not hasattr(loader, "gather_args") or self.cins[0] == self.cins_real[0]
                 or self.fork_transposes or not self.head_transposes or loader.batch > self.cap):
             return False
         h = self.hs[0]
         img, order, lab_all, lab_out, ctr, n_order, C, mean, std = loader.gather_args()
         if (loader.H, loader.W, C) != (h, h, self.cins_real[0]):
             return False
+        lf = self._leaf(0, 0)
         self.C.arm_sgd_next_prep(img, order, lab_all, lab_out, ctr, n_order, loader.batch, C, mean, std,
                                  self.x8.data_ptr(), CIN_PAD, h, h, SPAD, *self._zero_args(True),
-                                 self.w1p.data_ptr(), CIN_PAD)
+                                 self.w1p.data_ptr(), CIN_PAD, self.flat.offsets[lf] - HEADER, self.flat.numels[lf])
         self._prefetched = True
         self.prepared_ahead += 1
         return True
@@ -818,12 +896,23 @@ class CifarHIPExecutor:
             self.bucketer.mark_leaf_ready(leaf)
 
     @torch.no_grad()
-    def predict(self, x: torch.Tensor) -> torch.Tensor:
-        """Eval-mode forward (running BN statistics); returns log-probabilities
-        [B, classes] (fp32)."""
+    def predict(self, x: torch.Tensor, batch_stats: bool = False) -> torch.Tensor:
+        """Forward only; returns log-probabilities [B, classes] (fp32).  Eval
+        mode (running BN statistics) by default; ``batch_stats=True``
+        normalises with the batch's own statistics, the way the reference's
+        AsyncEA tester evaluates a center snapshot (its functional BN stays in
+        training mode: examples/Model.lua:56-66, EASGD_tester.lua:109-159) --
+        the running statistics are left as they were."""
         s = stream_handle()
-        B = self._prep(x, s, train=False)
-        self._forward(B, s, train=False)
+        if batch_stats:
+            self._set_mode()
+        B = self._prep(x, s, train=batch_stats)
+        if batch_stats:
+            saved = [(t, t.clone()) for t in self.rm + self.rv]
+        self._forward(B, s, train=batch_stats)
+        if batch_stats:
+            for t, v in saved:
+                t.copy_(v)
         nfc = 4 * self.nb
         self.C.head_fwd_bwd(self.p[-1].data_ptr(), self.p32[nfc].data_ptr(), self.p32[nfc + 1].data_ptr(), 0,
                             self.feat, B, self.nclass, self.logits.data_ptr(), 0, 0, 0, s)

@@ -188,9 +188,12 @@ def sgd_update_(p: torch.Tensor, g: torch.Tensor, lr: float, slot: torch.Tensor 
     (offset, numel, slab tensor, splits, Cout, taps, Cp, C) reduced by extra
     blocks of the same launch.  ``skip``: elements [lo, hi) of p left alone
     (updated inside the step by a conv launch's side job)."""
-    if slabs or tail is not None or skip is not None:
+    # an armed next-step preparation (executor arm_next_prep) rides the slab-capable launch
+    armed = p.is_cuda and native().sgd_next_prep_armed()
+    if slabs or tail is not None or skip is not None or armed:
         if not p.is_cuda or g.dtype != torch.float32:
-            raise ValueError("sgd_update_: slab gradients need an fp32 gradient on the GPU")
+            raise ValueError("sgd_update_: slab gradients / the next-step preparation need an fp32 gradient "
+                             "on the GPU")
         slabs = slabs or []
         tl, tptr = [], 0
         if tail is not None:

@@ -252,6 +252,14 @@ def rccl_channel_cap() -> int:
     return int(os.environ.get("NCCL_MAX_NCHANNELS", DEFAULT_RCCL_CHANNELS))
 
 
+def runs_collectives(comm) -> bool:
+    """Whether data-plane collectives on ``comm`` actually run: world > 1, or
+    an RCCL communicator at world 1 with the collectives forced through RCCL
+    (``DISTLEARN_RCCL_WORLD1=1``: the multi-node step configuration rehearsed
+    on one GPU)."""
+    return getattr(comm, "world_size", 1) > 1 or getattr(comm, "_skip1", True) is False
+
+
 class RcclCommunicator(Communicator):
     """Native RCCL data plane (C++), gloo control plane."""
 
@@ -260,7 +268,6 @@ class RcclCommunicator(Communicator):
         C = native()
         if world_size > 1:
             os.environ.setdefault("NCCL_MAX_NCHANNELS", str(DEFAULT_RCCL_CHANNELS))  # read at comm init
-        self.cu_reserve = rccl_channel_cap() if world_size > 1 else 0
         self.ctrl = ctrl_group
         self.rank, self.world_size = rank, world_size
         self.device = torch.device(device)
@@ -277,6 +284,8 @@ class RcclCommunicator(Communicator):
         # world 1 collectives are the identity and skipped; DISTLEARN_RCCL_WORLD1=1
         # issues them anyway (exercises RCCL inside hipGraph capture on one GPU)
         self._skip1 = world_size == 1 and os.environ.get("DISTLEARN_RCCL_WORLD1", "0") != "1"
+        # CUs a concurrent collective's workgroups hold (executor CU-reserve policy)
+        self.cu_reserve = rccl_channel_cap() if runs_collectives(self) else 0
 
     @staticmethod
     def _check(t):
