@@ -382,6 +382,9 @@ def main():
         "comm": type(tree.comm).__name__,
         "device_ids": sorted(set(int(d) for d in devs.tolist())),
         "nccl_max_nchannels": os.environ.get("NCCL_MAX_NCHANNELS"),
+        # RCCL channel cap (maxCTAs) of the gradient communicator: measured with the
+        # overlap policy at world > 1 (engine.py select_policy), 0 = no collective runs
+        "channel_cap": getattr(tree.comm, "channel_cap", None),
         "cu_reserve": getattr(ex, "cu_reserve", None),
         "dgrad_stages": getattr(ex, "dgrad_stages", None),
         # the wire dtype actually used (world 1: no collective, fp32)

@@ -144,12 +144,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   m.def("rccl_version", &rccl_version);
   py::class_<RcclCommunicator>(m, "RcclCommunicator")
-      .def(py::init([](py::bytes uid, int rank, int world, int device, double timeout_s) {
+      .def(py::init([](py::bytes uid, int rank, int world, int device, double timeout_s, int max_ctas) {
              std::string id(uid);  // copy while holding the GIL
              py::gil_scoped_release nogil;  // ncclCommInitRank blocks on the other ranks
-             return new RcclCommunicator(id, rank, world, device, timeout_s);
+             return new RcclCommunicator(id, rank, world, device, timeout_s, max_ctas);
            }),
-           py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("timeout_s") = 0.0)
+           py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("timeout_s") = 0.0,
+           py::arg("max_ctas") = 0)
+      .def_property_readonly("max_ctas", &RcclCommunicator::max_ctas)
       .def_property_readonly("rank", &RcclCommunicator::rank)
       .def_property_readonly("world", &RcclCommunicator::world)
       .def_property_readonly("device", &RcclCommunicator::device)

@@ -74,11 +74,26 @@ def _obj_for(src: str) -> str:
     return os.path.join(BUILD, rel + ".o")
 
 
+def _deps_mtime(obj: str, newest_header: float) -> float:
+    """Newest mtime among the headers ``obj`` was compiled from (its -MMD
+    dependency file); every header when there is no dependency file."""
+    dep = obj + ".d"
+    if not os.path.exists(dep):
+        return newest_header
+    try:
+        text = open(dep).read().replace("\\\n", " ")
+        files = text.split(":", 1)[1].split()
+        return max([os.path.getmtime(f) for f in files if f.endswith((".h", ".hpp", ".inc"))] + [0.0])
+    except (OSError, IndexError):
+        return newest_header
+
+
 def _compile(src: str, force: bool, verbose: bool, newest_header: float):
     obj = _obj_for(src)
-    if (not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), newest_header)):
+    if (not force and os.path.exists(obj)
+            and os.path.getmtime(obj) >= max(os.path.getmtime(src), _deps_mtime(obj, newest_header))):
         return obj, 0.0, False
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-c", src, "-o", obj] + COMMON + _includes()
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-c", src, "-o", obj, "-MMD", "-MF", obj + ".d"] + COMMON + _includes()
     cmd += os.environ.get("DISTLEARN_CFLAGS", "").split()  # A/B experiments (e.g. -DDL_FWD_SWAP=0)
     if "bindings" in src or "testing" in src:
         cmd += ["-fvisibility=hidden"]

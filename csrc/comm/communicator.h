@@ -97,14 +97,24 @@ inline int rccl_version() {
 // queries never invalidate a capture running on the main thread.
 class RcclCommunicator {
  public:
-  RcclCommunicator(const std::string& uid, int rank, int world, int device, double timeout_s)
-      : rank_(rank), world_(world), dev_(device), timeout_s_(timeout_s) {
+  // max_ctas > 0: at most that many channels (RCCL workgroups) per collective
+  // on THIS communicator (ncclConfig_t::maxCTAs) -- the channel cap is a
+  // per-communicator choice measured by the trainer (engine.py
+  // select_policy), not a process-wide NCCL_MAX_NCHANNELS guess.
+  RcclCommunicator(const std::string& uid, int rank, int world, int device, double timeout_s, int max_ctas = 0)
+      : rank_(rank), world_(world), dev_(device), max_ctas_(max_ctas), timeout_s_(timeout_s) {
     if ((int)uid.size() != (int)sizeof(ncclUniqueId)) throw std::runtime_error("bad ncclUniqueId size");
     ncclUniqueId id;
     std::memcpy(&id, uid.data(), sizeof(id));
     DL_HIP_CHECK(hipSetDevice(device));
     ncclComm_t c = nullptr;
-    DL_NCCL_CHECK(ncclCommInitRank(&c, world, id, rank));
+    if (max_ctas > 0) {
+      ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+      cfg.maxCTAs = max_ctas;
+      DL_NCCL_CHECK(ncclCommInitRankConfig(&c, world, id, rank, &cfg));
+    } else {
+      DL_NCCL_CHECK(ncclCommInitRank(&c, world, id, rank));
+    }
     comm_ = Retirable<ncclComm_t>(c);
     if (timeout_s_ > 0) watcher_ = std::thread([this] { watch_loop(); });
   }
@@ -140,6 +150,7 @@ class RcclCommunicator {
   int rank() const { return rank_; }
   int world() const { return world_; }
   int device() const { return dev_; }
+  int max_ctas() const { return max_ctas_; }
 
   // Every RCCL host call holds call_mu_ (RCCL calls on one communicator are not
   // thread-safe) but NOT mu_: mu_ guards only the watchdog's state (pending
@@ -439,7 +450,7 @@ class RcclCommunicator {
   double abort_grace_s() const { return std::max(5.0, timeout_s_.load()); }
 
   Retirable<ncclComm_t> comm_;             // guarded by mu_
-  int rank_, world_, dev_;
+  int rank_, world_, dev_, max_ctas_;
   std::atomic<double> timeout_s_;
   int poll_ms_ = 50;
   PauseGate gate_;                          // guarded by mu_ (set() takes it)

@@ -83,3 +83,57 @@ def _forced_worker(rank, world, port):
 def test_forced_policy_is_not_measured():
     for r in mp.run(_forced_worker, 2):
         assert r["policy"]["chosen"] == "full" and r["calls"] == [(3, 0)]
+
+
+def _cap_worker(rank, world, port):
+    import os
+
+    import torch
+
+    from torch_distlearn_amd import Tree
+    from torch_distlearn_amd.engine import DataParallelTrainer
+
+    os.environ.pop("DISTLEARN_CHANNEL_CAP", None)
+    os.environ["DISTLEARN_CHANNEL_CAPS"] = "16,32"
+    tree = Tree(rank + 1, world, host="127.0.0.1", port=port)
+    comm = tree.comm
+    rebuilt = []
+    comm.channel_cap = 32
+
+    def set_cap(c):  # stands in for the RCCL communicator's rebuild (collective)
+        rebuilt.append(c)
+        comm.channel_cap = c
+
+    comm.set_channel_cap = set_cap
+    tr = DataParallelTrainer(torch.nn.Linear(4, 2), tree, lr=0.1)
+    ex = _FakeExecutor()
+    tr.executor, tr.graph = ex, True
+    # rank-local ms per (policy, cap): the slowest rank makes reserve@16 the winner
+    table = {(3, 0, 16): 0.40, (3, 0, 32): 0.36 + 0.1 * rank, (2, 16, 16): 0.35 + 0.01 * rank, (2, 32, 32): 0.38}
+    seen = []
+
+    def fake_time(loader, reps):
+        key = ex.calls[-1] + (comm.channel_cap,)
+        seen.append(key)
+        return table[key]
+
+    tr._time_step_graph = fake_time
+    pol = tr.select_policy(None)
+    return {"policy": pol, "seen": seen, "rebuilt": rebuilt, "final": ex.calls[-1], "cap": comm.channel_cap}
+
+
+@pytest.mark.parametrize("world", [2])
+def test_channel_cap_is_measured_with_the_policy(world):
+    """the RCCL channel cap is not forced -- select_policy
+    crosses the overlap policies with the candidate caps, rebuilds the
+    communicator once per cap (caps outermost), the reserve policy leaves the
+    cap's CUs free, and every rank takes the pair whose slowest rank is fastest."""
+    res = mp.run(_cap_worker, world)
+    for r in res:
+        pol = r["policy"]
+        assert set(pol["ms_per_step"]) == {"full@16", "reserve@16", "full@32", "reserve@32"}
+        assert pol["chosen"] == "reserve@16" and pol["channel_cap"] == 16 and r["cap"] == 16
+        assert r["final"] == (2, 16)
+        assert r["seen"] == [(3, 0, 16), (2, 16, 16), (3, 0, 32), (2, 32, 32)]
+        assert r["rebuilt"] == [16, 32, 16]  # one rebuild per cap, then back to the winner's
+        assert pol["candidates"]["reserve@32"] == {"dgrad_stages": 2, "cu_reserve": 32, "channel_cap": 32}

@@ -426,6 +426,7 @@ def test_deferred_slab_reduce_is_bitwise(dev, monkeypatch, momentum):
                 assert tr._side == (tr.flat.offsets[8], tr.flat.total)
         else:
             assert tr._slabs is None and tr._side is None
+        assert tr.grads_materialized == (defer == "0")  # flat.grad is not written for deferred slabs
         ld = DeviceLoader(PartitionedDataset(imgs, labels, device=dev), "permutation", 128, seed=2)
         tr.run(ld, 11, unroll=4)  # 8 steps per epoch: graphs of 4, 2, 1 steps, then a new epoch
         torch.cuda.synchronize()
@@ -449,11 +450,14 @@ def test_policy_selected_on_the_machine(dev, monkeypatch):
     tr.prepare(ld, 4)
     torch.cuda.synchronize()
     pol = tr.policy
-    assert pol is not None and pol["chosen"] in ("full", "reserve"), pol
-    assert set(pol["ms_per_step"]) == {"full", "reserve"} and all(v > 0 for v in pol["ms_per_step"].values())
+    names = {f"{p}@{c}" for p in ("full", "reserve") for c in (16, 32)}  # x the measured channel caps
+    assert pol is not None and pol["chosen"] in names, pol
+    assert set(pol["ms_per_step"]) == names and all(v > 0 for v in pol["ms_per_step"].values())
     assert pol["chosen"] == min(pol["ms_per_step"], key=pol["ms_per_step"].get)
     want = pol["candidates"][pol["chosen"]]
     assert (tr.executor.dgrad_stages, tr.executor.cu_reserve) == (want["dgrad_stages"], want["cu_reserve"])
+    assert tr.tree.comm.channel_cap == want["channel_cap"] == pol["channel_cap"]
+    assert tr.tree.comm._c.max_ctas == want["channel_cap"]  # the communicator was rebuilt with the chosen cap
     assert torch.equal(tr.flat.data, p0) and int(ld.ctr[0]) == 0  # selection changed no training state
     loss = tr.run(ld, 6, unroll=4)
     torch.cuda.synchronize()
@@ -487,7 +491,7 @@ def test_multinode_fused_reduce_is_bitwise(dev, monkeypatch, momentum):
         tr = DataParallelTrainer(model, tree, lr=0.02, momentum=momentum, backend="hip",
                                  compute_dtype=torch.bfloat16, graph=True, max_batch=128)
         tr.synchronize_parameters()
-        assert tr.reduces_grads and tr._slabs is None and tr._side is None
+        assert tr.reduces_grads and tr._slabs is None and tr._side is None and tr.grads_materialized
         if fuse == "1":
             assert tr._fused_reduce == {"ride": [2], "merged": [0, 1]}, tr._fused_reduce
         else:

@@ -471,3 +471,57 @@ def test_rccl_watchdog_pause_is_synchronous(monkeypatch):
         assert comm._c.polls() > n
     assert _drained(comm) and comm.health() == ""
     comm.close()
+
+
+# ---------------------------------------------------------------------------
+def _async_hip_worker(rank, world, port, backend, unrolled):
+    os.environ["DISTLEARN_REDUCE_ATOMIC"] = "0"  # deterministic kernels: the two runs compare bitwise
+    dev, tree = _setup(rank, world, port, backend)
+    from torch_distlearn_amd import AsyncEA, FlatParams
+    from torch_distlearn_amd.data import DeviceLoader, PartitionedDataset
+    from torch_distlearn_amd.engine import DataParallelTrainer
+    from torch_distlearn_amd.models import CifarConvNet
+    from torch_distlearn_amd.utils.color_print import set_verbose
+
+    set_verbose(False)
+    model = CifarConvNet(seed=0).to(dev)
+    ea = AsyncEA(tree, None, None, None, None, None, world - 1, rank, 3, 0.3)
+    if rank == 0:
+        flat = FlatParams(model, grads=False)
+        ea.initServer(flat)
+        while ea.syncServer(flat):
+            pass
+        torch.cuda.synchronize()
+        return {"center": ea.center.cpu(), "syncs": ea.syncs}
+    tr = DataParallelTrainer(model, tree, lr=0.02, algo="async", tau=3, alpha=0.3, backend="hip",
+                             compute_dtype=torch.bfloat16, graph=True, max_batch=16, async_ea=ea)
+    tr.synchronize_parameters()
+    g = torch.Generator(device=dev).manual_seed(5)
+    imgs = torch.randint(0, 256, (16 * 8, 32, 32, 3), dtype=torch.uint8, device=dev, generator=g)
+    labs = torch.randint(0, 10, (16 * 8,), device=dev, generator=g)
+    loader = DeviceLoader(PartitionedDataset(imgs, labs, device=dev), "permutation", 16, seed=1)
+    if unrolled:
+        tr.run(loader, 11, unroll=4)
+    else:
+        for _ in range(11):
+            tr.step(loader)
+    tr.finish()
+    torch.cuda.synchronize()
+    return {"p": tr.flat.data.cpu(), "syncs": ea.syncs, "step": ea.step, "keys": sorted(str(k) for k in tr._multi),
+            "slabs": tr._slabs is not None, "side": tr._side is not None}
+
+
+def test_async_ea_hip_client_unrolled(monkeypatch):
+    """an AsyncEA client on the MI355X hot path --
+    DataParallelTrainer(algo="async", backend="hip", graph=True) with the
+    tau-1 local steps between two syncs replayed as ONE hipGraph (engine.run)
+    trains BITWISE like one captured step at a time (deterministic kernels),
+    against a real server rank (1 server + 1 client sharing the GPU, gloo
+    payloads: RCCL refuses two ranks on one GPU)."""
+    _need("gloo", 2)
+    outs = [mp.run(_async_hip_worker, 2, "gloo", u, timeout=600) for u in (False, True)]
+    (s0, c0), (s1, c1) = outs
+    assert c0["syncs"] == c1["syncs"] == 3 == s0["syncs"] == s1["syncs"] and c0["step"] == c1["step"] == 11
+    assert "('async', 2)" in c1["keys"] and c1["slabs"] and not c1["side"]
+    assert c0["p"].tobytes() == c1["p"].tobytes()
+    assert s0["center"].tobytes() == s1["center"].tobytes()

@@ -194,6 +194,12 @@ class DataParallelTrainer:
             self._fused_reduce = self.executor.fuse_slab_reduces() or None
         self._side = None
         self._arm_side_update()
+        # Whether flat.grad holds this step's gradients after a step:
+        # False while the one-node update sums split-K slabs itself (their
+        # weights' flat.grad entries are never written) or a conv launch's side
+        # job updates part of the parameters inside forward_backward -- gradient
+        # readers (norm logging, clipping, hooks) then need DISTLEARN_DEFER_SLABS=0.
+        self.grads_materialized = self._slabs is None and self._side is None
         # executor policy for the world > 1 overlap (select_policy): None until chosen
         self.policy: Optional[dict] = None
         self._policy_done = False
@@ -449,28 +455,75 @@ class DataParallelTrainer:
         whose slowest rank is fastest (:func:`agree_on_policy`).  Runs once;
         ``DISTLEARN_POLICY=<name>`` forces a candidate, one node keeps the
         executor default unless ``DISTLEARN_POLICY_SELECT=1``.  The choice
-        and both timings land in :attr:`policy` (bench.py's JSON config)."""
+        and both timings land in :attr:`policy` (bench.py's JSON config).
+
+        With an RCCL communicator whose collectives run, the candidates are
+        also crossed with the channel caps of
+        :func:`~torch_distlearn_amd.parallel.comm.channel_cap_candidates`
+        ("full@16", "reserve@32", ...: the communicator is rebuilt with each
+        cap, ``reserve`` leaves that many CUs): more channels move a bucket
+        faster, fewer leave more CUs to the backward -- the measured step
+        decides."""
         ex = self.executor
         if self._policy_done or not self.graph or ex is None or not callable(getattr(ex, "policies", None)):
             return self.policy
         self._policy_done = True
-        cands = ex.policies()
+        cands = self._policy_candidates()
         want = os.environ.get("DISTLEARN_POLICY", "auto")
         if want in cands:
-            self._set_policy(cands[want])
-            self.policy = {"chosen": want, "how": "forced (DISTLEARN_POLICY)"}
+            self._apply_candidate(*cands[want])
+            self.policy = {"chosen": want, "how": "forced (DISTLEARN_POLICY)", **self._cap_record()}
             return self.policy
-        if len(cands) < 2 or (self.tree.numNodes == 1 and os.environ.get("DISTLEARN_POLICY_SELECT", "0") != "1"):
+        # only a step whose gradient all-reduce overlaps the backward has a policy to
+        # choose (AllReduceEA / AsyncEA clients: no collective beside the backward; an
+        # AsyncEA server would never join the agreement collective)
+        if (len(cands) < 2 or not self.reduces_grads
+                or (self.tree.numNodes == 1 and os.environ.get("DISTLEARN_POLICY_SELECT", "0") != "1")):
+            if len(cands) == 1:  # a single candidate (pinned policy knobs / channel cap): nothing to measure
+                self._apply_candidate(*next(iter(cands.values())))
             return self.policy
         local = {}
-        for name, kw in sorted(cands.items()):
-            self._set_policy(kw)
+        # caps outermost: the communicator is rebuilt once per cap
+        for name, (kw, cap) in sorted(cands.items(), key=lambda it: (it[1][1] or 0, it[0])):
+            self._apply_candidate(kw, cap)
             local[name] = self._time_step_graph(loader, reps)
         name, table = agree_on_policy(self.tree.comm, local)
-        self._set_policy(cands[name])
+        self._apply_candidate(*cands[name])
         self.policy = {"chosen": name, "ms_per_step": table, "how": f"measured ({reps} graph replays per policy)",
-                       "candidates": {n: dict(kw) for n, kw in cands.items()}}
+                       "candidates": {n: dict(kw, **({"channel_cap": cap} if cap else {}))
+                                      for n, (kw, cap) in cands.items()}, **self._cap_record()}
         return self.policy
+
+    def _policy_candidates(self) -> dict:
+        """name -> (executor policy kwargs, channel cap or None)."""
+        from .parallel.comm import channel_cap_candidates
+
+        base = self.executor.policies()
+        comm = self.tree.comm
+        caps = [None]
+        if base and callable(getattr(comm, "set_channel_cap", None)) and runs_collectives(comm):
+            caps = channel_cap_candidates()
+        out = {}
+        for cap in caps:
+            for p, kw in base.items():
+                kw = dict(kw)
+                if cap is not None and kw.get("cu_reserve", 0) > 0:
+                    kw["cu_reserve"] = int(cap)  # the reserve policy leaves the cap's CUs free
+                out[p if len(caps) == 1 else f"{p}@{cap}"] = (kw, cap)
+        return out
+
+    def _apply_candidate(self, kw: dict, cap) -> None:
+        comm = self.tree.comm
+        if cap is not None and cap != getattr(comm, "channel_cap", None):
+            # graphs holding the old communicator's collectives go first
+            self._graph, self._static = None, None
+            self._multi = {}
+            comm.set_channel_cap(cap)
+        self._set_policy(kw)
+
+    def _cap_record(self) -> dict:
+        cap = getattr(self.tree.comm, "channel_cap", None)
+        return {"channel_cap": cap} if cap else {}
 
     def _arm_side_update(self) -> None:
         """One node, slabs deferred: the update of the last blocks' parameters
@@ -500,6 +553,7 @@ class DataParallelTrainer:
             self._arm_side_update()
         if self._fused_reduce is not None:
             self._fused_reduce = self.executor.fuse_slab_reduces() or None
+        self.grads_materialized = self._slabs is None and self._side is None
 
     def _time_step_graph(self, loader, reps: int) -> float:
         """ms per replay of a freshly captured one-step graph (state restored;

@@ -841,8 +841,10 @@ class CifarHIPExecutor:
         taps = KSIZE * KSIZE
         blocks = [i for i in range(self.nb) if not self.wplan[i][2]]
         padded = [i for i in blocks if not (self.cins[i] == self.cins_real[i] and self.wplan[i][1] < 32)]
-        if len(padded) > 1:  # the update reduces at most one such range
-            blocks = [i for i in blocks if i not in padded[1:]]
+        inplace = [i for i in blocks if i not in padded]
+        # the update reads at most 4 in-place ranges (csrc sgd_dev.h kSlabRanges) and
+        # reduces one padded tail; any further block keeps its stand-alone slab_reduce
+        blocks = sorted(inplace[:4] + padded[:1])
         self._deferred = tuple(blocks)
         return [(self._leaf(i, 0), self.wslab_l[i], self.wplan[i][1], self.couts[i], taps, self.cins[i],
                  self.cins_real[i]) for i in blocks]

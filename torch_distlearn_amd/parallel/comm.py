@@ -242,14 +242,33 @@ class ProcessGroupCommunicator(Communicator):
 # beside it (here: the 128x128 wgrad, 141 registers/wave, and the 3-stage streaming
 # conv) lose that CU for the collective's lifetime, and a grid sized to the whole chip
 # then needs a second round (measured per kernel with scripts/emulate_rccl.py and
-# bench_conv.py --occupy).  The channel count is therefore
-# capped (NCCL_MAX_NCHANNELS, unless the user set it) and the executor sizes the
-# grids of the kernels that overlap the bucketed all-reduce to leave that many CUs.
+# bench_conv.py --occupy).  More channels move a bucket faster over the 7 xGMI
+# links; fewer leave more CUs to the backward it overlaps.  The cap is therefore a
+# per-communicator setting (ncclConfig_t::maxCTAs, csrc/comm/communicator.h) that
+# the trainer MEASURES: DataParallelTrainer.select_policy times the step with every
+# candidate cap (DISTLEARN_CHANNEL_CAPS, default 16 and 32) x overlap policy at
+# world > 1 and keeps the fastest slowest-rank one.  A user's NCCL_MAX_NCHANNELS
+# (process-wide, read by RCCL at init) still applies on top and pins the cap.
 DEFAULT_RCCL_CHANNELS = 32
+DEFAULT_CHANNEL_CAPS = (16, 32)
 
 
 def rccl_channel_cap() -> int:
-    return int(os.environ.get("NCCL_MAX_NCHANNELS", DEFAULT_RCCL_CHANNELS))
+    """The cap a new communicator starts with (NCCL_MAX_NCHANNELS if the user
+    set it, else DISTLEARN_CHANNEL_CAP, else 32)."""
+    return int(os.environ.get("NCCL_MAX_NCHANNELS", os.environ.get("DISTLEARN_CHANNEL_CAP", DEFAULT_RCCL_CHANNELS)))
+
+
+def channel_cap_candidates() -> List[int]:
+    """The channel caps select_policy measures (one only when the user pinned
+    NCCL_MAX_NCHANNELS / DISTLEARN_CHANNEL_CAP)."""
+    if "NCCL_MAX_NCHANNELS" in os.environ or "DISTLEARN_CHANNEL_CAP" in os.environ:
+        return [rccl_channel_cap()]
+    v = os.environ.get("DISTLEARN_CHANNEL_CAPS")
+    caps = [int(c) for c in v.split(",") if c.strip()] if v else list(DEFAULT_CHANNEL_CAPS)
+    if any(c <= 0 or c > 256 for c in caps):
+        raise ValueError(f"DISTLEARN_CHANNEL_CAPS: caps must be in 1..256, got {caps}")
+    return sorted(set(caps))
 
 
 def runs_collectives(comm) -> bool:
@@ -265,27 +284,44 @@ class RcclCommunicator(Communicator):
 
     def __init__(self, rank: int, world_size: int, device: torch.device, ctrl_group=None,
                  timeout_s: Optional[float] = None):
-        C = native()
-        if world_size > 1:
-            os.environ.setdefault("NCCL_MAX_NCHANNELS", str(DEFAULT_RCCL_CHANNELS))  # read at comm init
         self.ctrl = ctrl_group
         self.rank, self.world_size = rank, world_size
         self.device = torch.device(device)
-        uid = C.rccl_unique_id() if rank == 0 else None
-        if world_size > 1:
-            lst = [uid]
-            dist.broadcast_object_list(lst, src=0, group=ctrl_group)
-            uid = lst[0]
-        # watchdog (csrc/comm/communicator.h): a collective older than timeout_s,
-        # or an RCCL async error, aborts the communicator instead of hanging
-        self.timeout_s = comm_timeout() if timeout_s is None else float(timeout_s)
-        self._c = C.RcclCommunicator(uid, rank, world_size, self.device.index or 0, self.timeout_s)
-        self._in_group = 0
         # world 1 collectives are the identity and skipped; DISTLEARN_RCCL_WORLD1=1
         # issues them anyway (exercises RCCL inside hipGraph capture on one GPU)
         self._skip1 = world_size == 1 and os.environ.get("DISTLEARN_RCCL_WORLD1", "0") != "1"
+        # watchdog (csrc/comm/communicator.h): a collective older than timeout_s,
+        # or an RCCL async error, aborts the communicator instead of hanging
+        self.timeout_s = comm_timeout() if timeout_s is None else float(timeout_s)
+        self._in_group = 0
+        self._c = None
+        # channel cap (maxCTAs) of this communicator; 0 = RCCL's own choice (nothing runs)
+        self.channel_cap = 0
+        self._init_native(rccl_channel_cap() if runs_collectives(self) else 0)
+
+    def _init_native(self, cap: int) -> None:
+        """(Re)create the native communicator with ``cap`` channels at most
+        (collective: every rank calls it with the same cap)."""
+        C = native()
+        uid = C.rccl_unique_id() if self.rank == 0 else None
+        if self.world_size > 1:
+            lst = [uid]
+            dist.broadcast_object_list(lst, src=0, group=self.ctrl)
+            uid = lst[0]
+        if self._c is not None:
+            self._c.destroy()
+        self._c = C.RcclCommunicator(uid, self.rank, self.world_size, self.device.index or 0, self.timeout_s,
+                                     int(cap))
+        self.channel_cap = int(cap)
         # CUs a concurrent collective's workgroups hold (executor CU-reserve policy)
-        self.cu_reserve = rccl_channel_cap() if runs_collectives(self) else 0
+        self.cu_reserve = int(cap)
+
+    def set_channel_cap(self, cap: int) -> None:
+        """Rebuild the communicator with another channel cap (collective).  No
+        hipGraph holding collectives of the old communicator may remain."""
+        if int(cap) != self.channel_cap:
+            torch.cuda.synchronize(self.device)
+            self._init_native(int(cap))
 
     @staticmethod
     def _check(t):
