@@ -59,6 +59,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("addend_mask") = 0);
   m.def("conv_fwd_stat_rows", &conv_fwd_stat_rows);
   m.def("set_conv_region", &set_conv_region);
+  m.def("set_conv_region_bd", &set_conv_region_bd);
   m.def("set_conv_region_stages", &set_conv_region_stages);
   m.def("set_conv_wgrad_pf", &set_conv_wgrad_pf);
   m.def("set_bn_bwd_items", &set_bn_bwd_items);

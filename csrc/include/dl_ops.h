@@ -86,6 +86,7 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
              int Cout, int KS, int tile, int splits, uintptr_t stream);
 int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile, int splits);
 void set_conv_region(int on);
+void set_conv_region_bd(int mode);  // direct-B region kernel: 0 off, 1 row tiles, 2 + whole images
 void set_conv_region_stages(int st);
 void set_conv_wgrad_pf(int pf);
 void set_bn_bwd_items(int n);

@@ -1450,6 +1450,203 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf1
   }
 }
 
+// s_waitcnt immediate (gfx9 encoding) for vmcnt(n), expcnt / lgkmcnt unconstrained
+constexpr int vmcnt_imm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x70 | 0xF00; }
+
+// --------------------------------------------------------------------------
+// Region kernel with the weight operand loaded straight into registers
+// ("direct B").  The region kernel above streams the weight tile through an
+// LDS ring: per k-step each wave issues LDS-DMA pieces (60-185 issue cycles
+// each among MFMAs, MI355X_MICROARCH.md), waits for the stage, joins a
+// workgroup barrier, and reads both operands back from LDS -- at 8 waves of
+// 32 x 32 (or 64 x 32) wave tiles the LDS traffic per k-step exceeds the
+// MFMA time (fwd2: ~1,700 cycles per k-step vs 512 of MFMA per SIMD).  Here
+// only the activation region lives in LDS (filled once, read-only after one
+// barrier): every wave loads ITS weight fragments (the MFMA A operand of the
+// transposed accumulator) with 16-byte buffer loads into a D-deep register
+// queue, D k-steps ahead, and reads its activation fragments from the region
+// one k-step ahead -- no barrier and no LDS-DMA in the k-loop, wider wave
+// tiles (4 waves: 128 x 32 or 64 x 32) so each LDS byte feeds more MFMAs.
+// Same arithmetic, fragment layouts and epilogue as the region kernel.
+// --------------------------------------------------------------------------
+template <int BN, int WM, int WN, int D, int NK, bool STATS, bool SLAB, bool BNRED = false>
+__global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_bd_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y, float* __restrict__ stats,
+    float* __restrict__ slab, const ConvGeom g, const RegionGeom rg, int splits, unsigned long long* dbg,
+    const BnRedArgs br) {
+  const unsigned long long t_start = dbg ? stamp() : 0ull;
+  constexpr int BM = 128, BK = 64, NW = WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int NB = (BK / 32) * FN;  // weight loads per k-step per lane
+  static_assert(FN % 2 == 0, "the 16-byte epilogue pairs N fragments");
+  static_assert(D * NB < 64, "vmcnt range");
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int region_bytes = rg.nslot * 16;
+  char* sR = smem;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int ntm = (g.M + BM - 1) / BM;
+  const int npanel = (g.Cout / BN) * splits;
+  const int id = xcd_swizzle(blockIdx.x, ntm * npanel);
+  const int tm = g.mmajor ? id / npanel : id % ntm;
+  const int panel = g.mmajor ? id - tm * npanel : id / ntm;
+  const int split = panel % splits, tn = panel / splits;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int HW = 1 << g.logHW, Wd = g.W;
+  const int taps = g.KS * g.KS;
+  // NK: the k-step count (cpw x taps) as a compile-time constant -- a static
+  // trip count and tail keep the accumulators in fixed registers
+  constexpr int nk = NK;
+  const int img0 = m0 >> g.logHW, oh0 = (m0 & (HW - 1)) >> g.logW;
+  const int start_pix = img0 * g.Hp * g.Wp + oh0 * g.Wp;
+  const int cbase = split * rg.cpw;
+
+  // ---- region fill (asm LDS-DMA: invisible to the compiler's LDS-DMA alias
+  // waits, which would otherwise drain the weight queue at every fragment read)
+  {
+    const i32x4 xr4 = make_rsrc4(x, (unsigned)((int64_t)g.B * g.Hp * g.Wp * g.Cin * 2));
+    const int nq = rg.nslot >> 6;
+    const int nrows = rg.nimg * rg.RH;
+    for (int q = wid; q < nq; q += NW) {
+      const int sl = q * 64 + lane;
+      const int R = (int)(((float)sl + 0.5f) * rg.inv_RS);
+      const int r2 = sl - R * rg.RS;
+      const int col = (r2 * 6554) >> 16;  // r2 / 10 (exact for r2 < 16384; S == 10)
+      const int ch = r2 - col * 10;
+      const bool ok = R < nrows && col < rg.RW && ch < 8;
+      const int pix = start_pix + R * g.Wp + col;
+      const unsigned voff = ok ? 2u * (unsigned)(pix * g.Cin + ch * 8) : kOOB;
+      for (int c = 0; c < rg.cpw; ++c)
+        blds16_asm(xr4, voff, 2u * (unsigned)((cbase + c) * 64), sR + c * region_bytes + q * 1024);
+    }
+  }
+
+  // ---- weight fragments: lane row n0 + wn*TN + b_frag_row(b, l&15), 8 channels
+  // at k = (step's k offset) + 8 * (4 kk + (l >> 4))
+  const rsrc_t wr = make_rsrc(w, (unsigned)((int64_t)g.Cout * g.K * 2));
+  unsigned bv[BK / 32][FN];
+#pragma unroll
+  for (int kk = 0; kk < BK / 32; ++kk)
+#pragma unroll
+    for (int b = 0; b < FN; ++b) {
+      const int row = n0 + wn * TN + b_frag_row(b, lane & 15);
+      bv[kk][b] = 2u * (unsigned)(row * g.K + (kk * 4 + (lane >> 4)) * 8);
+    }
+  int ld_s = 0, ld_c = 0, ld_t = 0;  // next k-step to load (wave-uniform)
+  bf16x8 bq[D][BK / 32][FN];
+  auto load_b = [&](bf16x8 (&dst)[BK / 32][FN]) {
+    const bool live = ld_s < nk;
+    const int soff = 2 * (ld_t * g.Cin + (cbase + ld_c) * 64);
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk)
+#pragma unroll
+      for (int b = 0; b < FN; ++b)
+        dst[kk][b] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    wr, live ? (int)bv[kk][b] : (int)kOOB, soff, 0));
+    ++ld_s;  // branch-free advance
+    ++ld_t;
+    const int wrap = ld_t == taps;
+    ld_t -= wrap * taps;
+    ld_c = min(ld_c + wrap, rg.cpw - 1);
+  };
+#pragma unroll
+  for (int q = 0; q < D; ++q) load_b(bq[q]);
+
+  // ---- activation fragment bases (slot of the tap-(0,0) pixel + lane chunk)
+  int a_base[FM];
+#pragma unroll
+  for (int a = 0; a < FM; ++a) {
+    const int m = min(m0 + wm * TM + a * 16 + (lane & 15), g.M - 1);
+    const int im = (m >> g.logHW) - img0;
+    const int oh = ((m & (HW - 1)) >> g.logW) - oh0;
+    const int ow = m & (Wd - 1);
+    a_base[a] = (im * rg.IS + oh * rg.RS + ow * rg.S + (lane >> 4)) * 16;
+  }
+  int rc = 0, rkh = 0, rkw = 0;  // k-step whose activation fragments are read next
+  auto read_a = [&](bf16x8 (&fa)[BK / 32][FM]) {
+    const char* As = sR + rc * region_bytes + (rkh * rg.RS + rkw * rg.S) * 16;  // wave-uniform tap offset
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk)
+#pragma unroll
+      for (int a = 0; a < FM; ++a) fa[kk][a] = *reinterpret_cast<const bf16x8*>(As + a_base[a] + kk * 64);
+    ++rkw;  // branch-free advance
+    const int ww = rkw == g.KS;
+    rkw -= ww * g.KS;
+    rkh += ww;
+    const int wh = rkh == g.KS;
+    rkh -= wh * g.KS;
+    rc = min(rc + wh, rg.cpw - 1);
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // the region (older than the D weight stages) landed for this wave, then for all
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(D * NB));
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned long long t_first = dbg ? stamp() : 0ull;
+  // activation fragments ping-pong between fa0 / fa1 (D is even: the parity
+  // of a step is static in the unrolled body, no register copies)
+  static_assert(D % 2 == 0, "even weight queue depth");
+  constexpr int NRD = (BK / 32) * FM;       // activation fragment reads per step
+  constexpr int NMF = (BK / 32) * FM * FN;  // MFMAs per step
+  bf16x8 fa0[BK / 32][FM], fa1[BK / 32][FM];
+  read_a(fa0);
+  auto step = [&](bf16x8 (&fc)[BK / 32][FM], bf16x8 (&fn)[BK / 32][FM], bf16x8 (&bs)[BK / 32][FN]) {
+    read_a(fn);  // the next k-step's activation fragments while this step's MFMAs run
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk)
+#pragma unroll
+      for (int a = 0; a < FM; ++a)
+#pragma unroll
+        for (int b = 0; b < FN; ++b) acc[a][b] = mfma16(bs[kk][b], fc[kk][a], acc[a][b]);
+    load_b(bs);  // k-step s + D into the slot just consumed
+    // issue order: (MFMA, fragment read) pairs, then (MFMA, weight load) pairs, the rest
+    constexpr int P1 = NRD < NMF ? NRD : NMF;
+    constexpr int P2 = NB < NMF - P1 ? NB : NMF - P1;
+#pragma unroll
+    for (int q = 0; q < P1; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    if constexpr (NRD > P1) __builtin_amdgcn_sched_group_barrier(0x100, NRD - P1, 0);
+#pragma unroll
+    for (int q = 0; q < P2; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    }
+    if constexpr (NB > P2) __builtin_amdgcn_sched_group_barrier(0x020, NB - P2, 0);
+    if constexpr (NMF - P1 - P2 > 0) __builtin_amdgcn_sched_group_barrier(0x008, NMF - P1 - P2, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int s0 = 0; s0 + D <= nk; s0 += D) {
+#pragma unroll
+    for (int q = 0; q < D; q += 2) {
+      step(fa0, fa1, bq[q]);
+      step(fa1, fa0, bq[q + 1]);
+    }
+  }
+  // the remaining nk % D steps (their weight stages are the first slots of the queue)
+  constexpr int R = nk % D;
+  if constexpr (R > 0) step(fa0, fa1, bq[0]);
+  if constexpr (R > 1) step(fa1, fa0, bq[1]);
+  if constexpr (R > 2) step(fa0, fa1, bq[2]);
+  static_assert(D <= 4, "the static tail covers up to 3 steps");
+  const unsigned long long t_loop = dbg ? stamp() : 0ull;
+  conv_fwd_epilogue_t<128, BN, STATS, SLAB, WM, WN, FM, FN, false, BNRED ? 1 : 0>(acc, g, y, stats, slab, split, tm,
+                                                                                 m0, n0, smem, 0, 0, br);
+  if (dbg && threadIdx.x == 0) {
+    unsigned long long* d = dbg + (size_t)blockIdx.x * 5;
+    d[0] = t_start; d[1] = t_start; d[2] = t_first; d[3] = t_loop; d[4] = stamp();
+  }
+}
+
 // --------------------------------------------------------------------------
 // First layer (Cin = 8 after the 3 -> 8 channel pad; K = KS*KS*8 = 200): the
 // whole problem of a workgroup fits in LDS at once -- its 128 output pixels'
@@ -2586,6 +2783,83 @@ static void launch_fwd_region(const ConvGeom& g, const RegionGeom& rg, uintptr_t
   else launch_fwd_region_st<BN, WM, WN, 3>(g, rg, x, w, y, stats, slab, splits, s);
 }
 
+// ---- direct-B region kernel (conv_fwd_region_bd_kernel) ---------------------
+// set_conv_region_bd: 0 = off, 1 = row tiles (H*W % 128 == 0), 2 = also
+// whole-image tiles (the 8x8 layer: 2 images per 128-row tile).  Without a
+// weight ring the region may take the whole LDS budget (still leaving room
+// for one RCCL workgroup, kRegionLdsCap).
+static int g_region_bd = 0;
+void set_conv_region_bd(int mode) {
+  if (mode < 0 || mode > 2) throw std::runtime_error("set_conv_region_bd: 0, 1 or 2");
+  g_region_bd = mode;
+}
+
+static bool region_geom_bd(const ConvGeom& g, int splits, RegionGeom& rg) {
+  constexpr int BM = 128;
+  if (!g_region_bd || g.KS != 5 || !g.pow2 || g.Cin % 64 != 0 || g.W > BM || BM % g.W != 0) return false;
+  const int HW = g.H * g.W;
+  const int chunks = g.Cin / 64;
+  if (chunks % splits != 0) return false;
+  rg.cpw = chunks / splits;
+  if (rg.cpw > 2) return false;
+  rg.S = 10;
+  rg.RW = g.Wp;
+  if (HW % BM == 0) {
+    rg.rows_mode = 1;
+    rg.nimg = 1;
+    rg.RH = BM / g.W + g.KS - 1;
+    rg.RS = rg.RW * rg.S;
+  } else if (BM % HW == 0 && g_region_bd >= 2) {
+    rg.rows_mode = 0;
+    rg.nimg = BM / HW;
+    rg.RH = g.Hp;
+    rg.RS = rg.RW * rg.S + 8;
+  } else {
+    return false;
+  }
+  rg.IS = rg.RH * rg.RS;
+  rg.nslot = (rg.nimg * rg.IS + 63) / 64 * 64;
+  if (rg.RS >= 16384 || rg.nslot >= (1 << 16)) return false;
+  rg.inv_S = 1.0f / rg.S;
+  rg.inv_RS = 1.0f / rg.RS;
+  rg.inv_IS = 1.0f / rg.IS;
+  return rg.cpw * rg.nslot * 16 <= kRegionLdsCap;
+}
+
+// either region kernel takes the shape (the streaming kernel otherwise)
+static bool any_region_geom(const ConvGeom& g, int tile, int splits, RegionGeom& rg) {
+  if ((tile == 0 || tile == 2) && region_geom_bd(g, splits, rg)) return true;
+  return (tile == 2 && region_geom(g, 64, splits, rg)) || (tile == 0 && region_geom(g, 128, splits, rg));
+}
+
+template <int BN, int WM, int WN, int NK>
+static void launch_fwd_region_bd(const ConvGeom& g, const RegionGeom& rg, uintptr_t x, uintptr_t w, uintptr_t y,
+                                 uintptr_t stats, uintptr_t slab, int splits, hipStream_t s) {
+  constexpr int D = 4;  // weight k-steps in flight per wave
+  const int ntm = (g.M + 127) / 128;
+  const int grid = ntm * (g.Cout / BN) * splits;
+  const size_t lds = std::max<size_t>((size_t)rg.cpw * rg.nslot * 16, (size_t)WM * 2 * BN * 4);
+  auto go = [&](auto kern, bf16_t* yy, float* st, float* sl) {
+    static bool attr = false;  // per instantiation: allow > 64 KiB of dynamic LDS
+    if (!attr) {
+      DL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      attr = true;
+    }
+    kern<<<grid, 64 * WM * WN, lds, s>>>((const bf16_t*)x, (const bf16_t*)w, yy, st, sl, g, rg, splits, g_conv_dbg,
+                                         g_bnred);
+  };
+  if (g_bnred.rows != nullptr) {
+    if (splits > 1 || stats) throw std::runtime_error("conv_fwd_bnred: plain unsplit dgrad only");
+    go(conv_fwd_region_bd_kernel<BN, WM, WN, D, NK, false, false, true>, (bf16_t*)y, nullptr, nullptr);
+  } else if (splits > 1) {
+    go(conv_fwd_region_bd_kernel<BN, WM, WN, D, NK, false, true>, nullptr, nullptr, (float*)slab);
+  } else if (stats) {
+    go(conv_fwd_region_bd_kernel<BN, WM, WN, D, NK, true, false>, (bf16_t*)y, (float*)stats, nullptr);
+  } else {
+    go(conv_fwd_region_bd_kernel<BN, WM, WN, D, NK, false, false>, (bf16_t*)y, nullptr, nullptr);
+  }
+}
+
 // tile: 0 = 128x128, 1 = 64x64, 2 = 128x64 (BM x BN, BK = 64).  splits > 1:
 // split-K into `slab` (fp32 [splits][M][Cout]) + combine (bf16 y, BN partials).
 // Returns the number of BN partial rows written to `stats` (if non-null).
@@ -2645,6 +2919,12 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
     };
     if (stats) go(conv_fwd_c8_kernel<true>);
     else go(conv_fwd_c8_kernel<false>);
+  } else if (!streaming_only && g_pool_load.y == nullptr && (tile == 0 || tile == 2) &&
+             region_geom_bd(g, splits, rg)) {
+    if (tile == 0 && rg.cpw == 1) launch_fwd_region_bd<128, 1, 4, 25>(g, rg, x, w, y, stats, slab, splits, s);
+    else if (tile == 0) launch_fwd_region_bd<128, 1, 4, 50>(g, rg, x, w, y, stats, slab, splits, s);
+    else if (rg.cpw == 1) launch_fwd_region_bd<64, 2, 2, 25>(g, rg, x, w, y, stats, slab, splits, s);
+    else launch_fwd_region_bd<64, 2, 2, 50>(g, rg, x, w, y, stats, slab, splits, s);
   } else if (!streaming_only && tile == 0 && region_geom(g, 128, splits, rg)) {
     if (g_region_waves == 4) launch_fwd_region<128, 2, 2>(g, rg, x, w, y, stats, slab, splits, s);
     else launch_fwd_region<128, 2, 4>(g, rg, x, w, y, stats, slab, splits, s);
@@ -2777,7 +3057,7 @@ int conv_region_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile, int
   RegionGeom rg{};
   const int t = tile & 15;
   if (splits < 1) splits = 1;
-  return (t == 2 && region_geom(g, 64, splits, rg)) || (t == 0 && region_geom(g, 128, splits, rg)) ? 1 : 0;
+  return any_region_geom(g, t, splits, rg) ? 1 : 0;
 }
 
 // conv_fwd (a dgrad) with the previous block's BatchNorm backward reduce in its
@@ -2788,7 +3068,7 @@ int conv_fwd_bnred(uintptr_t x, uintptr_t w, uintptr_t y, int B, int H, int W, i
   ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
   RegionGeom rg{};
   const int t = tile & 15;
-  if (!(t == 2 && region_geom(g, 64, 1, rg)) && !(t == 0 && region_geom(g, 128, 1, rg)))
+  if (!any_region_geom(g, t, 1, rg))
     throw std::runtime_error("conv_fwd_bnred: the shape does not take the region kernel");
   if (!rows || !coef || !y_prev) throw std::runtime_error("conv_fwd_bnred: null operand");
   g_bnred = BnRedArgs{(const bf16_t*)y_prev, (const float*)coef, (float*)rows};

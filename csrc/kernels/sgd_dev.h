@@ -174,10 +174,55 @@ __device__ __forceinline__ void pack_range4(const SgdJob& j, int64_t i, const fl
   }
 }
 
+// The update of a job without slab ranges (a multi-node step: every gradient
+// was all-reduced from the flat buffer): two items per thread per trip, every
+// load of both issued before the first update (flat_ops.hip sgd_kernel's
+// pattern) -- the per-item loop below pays one memory round trip per item.
+template <bool kMomentum, bool kShadow>
+__device__ __forceinline__ void sgd_plain_loop2(const SgdJob& j, int bid, int nblk) {
+  const float s = participation_scale(j.slot);
+  const int64_t stride = (int64_t)nblk * blockDim.x;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto live = [&](int64_t i) { return i < j.hi4 && !(i >= j.skip_lo4 && i < j.skip_hi4); };
+  auto finish = [&](int64_t i, float4 pv, const float4 gv, float4 mv) {
+    pv = sgd_elem4<kMomentum>(pv, gv, mv, s, j.wd, j.lr, j.momentum);
+    if constexpr (kMomentum) reinterpret_cast<float4*>(j.mom)[i] = mv;
+    reinterpret_cast<float4*>(j.p)[i] = pv;
+    if constexpr (kShadow) {
+      uint2 packed;
+      packed.x = pack_bf16x2(pv.x, pv.y);
+      packed.y = pack_bf16x2(pv.z, pv.w);
+      reinterpret_cast<uint2*>(j.p16)[i] = packed;
+    }
+    if (i >= j.pack_lo4 && i < j.pack_hi4) pack_range4(j, i, pv);
+  };
+  for (int64_t i = j.lo4 + (int64_t)bid * blockDim.x + threadIdx.x; i < j.hi4; i += 2 * stride) {
+    const int64_t i2 = i + stride;
+    const bool a = live(i), b = live(i2);
+    float4 pa = z4, ga = z4, ma = z4, pb = z4, gb = z4, mb = z4;
+    if (a) {
+      pa = reinterpret_cast<const float4*>(j.p)[i];
+      ga = load_grad4(j.g, i);
+      if constexpr (kMomentum) ma = reinterpret_cast<const float4*>(j.mom)[i];
+    }
+    if (b) {
+      pb = reinterpret_cast<const float4*>(j.p)[i2];
+      gb = load_grad4(j.g, i2);
+      if constexpr (kMomentum) mb = reinterpret_cast<const float4*>(j.mom)[i2];
+    }
+    if (a) finish(i, pa, ga, ma);
+    if (b) finish(i2, pb, gb, mb);
+  }
+}
+
 template <bool kMomentum, bool kShadow>
 __device__ __forceinline__ void sgd_range_loop(const SgdJob& j, int bid, int nblk) {
-  const float s = participation_scale(j.slot);
   const SlabRanges& r = j.r;
+  if (r.n == 0 && r.tail_hi4 <= r.tail_lo4) {  // (wave-uniform)
+    sgd_plain_loop2<kMomentum, kShadow>(j, bid, nblk);
+    return;
+  }
+  const float s = participation_scale(j.slot);
   const int64_t stride = (int64_t)nblk * blockDim.x;
   for (int64_t i = j.lo4 + (int64_t)bid * blockDim.x + threadIdx.x; i < j.hi4; i += stride) {
     if (i >= r.tail_lo4 && i < r.tail_hi4) continue;  // the tail blocks update these

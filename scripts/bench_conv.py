@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--wpf", type=int, default=-1, help="wgrad fragment prefetch: -1 by stages, 0 off, 1 on")
     ap.add_argument("--waves", type=int, default=8, help="waves per workgroup of the fwd/dgrad kernel (4 or 8)")
     ap.add_argument("--region", type=int, default=1, help="1: tap-reuse (LDS-resident region) fwd/dgrad kernel")
+    ap.add_argument("--region-bd", type=int, default=0,
+                    help="direct-B region kernel (weights into registers): 0 off, 1 row tiles, 2 + whole images")
     ap.add_argument("--rstages", type=int, default=0, help="region kernel B-ring stages (0 = max that fits)")
     ap.add_argument("--rwaves", type=int, default=8, help="region kernel waves per workgroup (4 or 8)")
     ap.add_argument("--wstage", type=int, default=1, help="wgrad slab stores staged through LDS as whole rows")
@@ -47,10 +49,11 @@ def main():
     C.set_conv_waves(a.waves)
     C.set_conv_wgrad_pf(a.wpf)
     C.set_conv_region(a.region)
+    C.set_conv_region_bd(a.region_bd)
     C.set_conv_region_stages(a.rstages)
     C.set_conv_region_waves(a.rwaves)
     C.set_conv_wgrad_stage_store(a.wstage)
-    print(f"# stages fwd={fs} wgrad={ws} region={a.region}")
+    print(f"# stages fwd={fs} wgrad={ws} region={a.region} region_bd={a.region_bd}")
     dev = torch.device("cuda")
     def cur():  # current-stream handle at call time (graph capture switches streams)
         return torch.cuda.current_stream().cuda_stream

@@ -973,3 +973,92 @@ def test_pool_on_load_region_conv(C, monkeypatch):
     # the block-2 output above are the bitwise oracle
     noise = rel(g1, g2)
     assert min(rel(g1, g0), rel(g2, g0)) < max(3 * noise, 6e-2)
+
+
+@pytest.mark.parametrize("shape", [(8, 16, 64, 128), (8, 8, 128, 256), (3, 16, 64, 128), (3, 8, 128, 64),
+                                   (4, 16, 128, 64), (5, 8, 256, 128)])
+@pytest.mark.parametrize("tile", [0, 2])
+@pytest.mark.parametrize("splits", [1, 2])
+def test_region_direct_b_bitwise(C, shape, tile, splits):
+    """The direct-B region kernel (conv_fwd_region_bd_kernel: weights loaded
+    straight into a register queue, no LDS ring, no barrier in the k-loop)
+    accumulates every output in the region kernel's k order: forward output
+    and split-K slabs are BITWISE those of the LDS-ring region kernel (images
+    mode on both), the BN statistics equal to float rounding, and all within
+    bf16 error of fp32 conv2d."""
+    B, H, cin, cout = shape
+    if cout % _TILE_BN[tile] != 0 or (cin // 64) % splits != 0 or (cin // 64) // splits > 2:
+        pytest.skip("shape outside the region kernels")
+    if splits > 1 and 256 % (cout // 8) != 0:
+        pytest.skip("split-K combine needs Cout/8 | 256")
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(101 + B * H + cin + tile)
+    x = torch.randn(B, H, H, cin, device=dev, generator=g).to(torch.bfloat16)
+    w = (torch.randn(cout, 5, 5, cin, device=dev, generator=g) * 0.05).to(torch.bfloat16)
+    xp = _pad(x)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=2).permute(0, 2, 3, 1)
+    rows = C.conv_fwd_stat_rows(B, H, H, cin, cout, 5, tile, splits)
+    C.set_conv_region(2)
+    try:
+        ring_ok = C.conv_region_ok(B, H, H, cin, cout, 5, tile, splits)  # the LDS-ring kernel fits too
+    finally:
+        C.set_conv_region(1)
+    outs = []
+    for bd in ((0, 2) if ring_ok else (2,)):
+        C.set_conv_region(2)
+        C.set_conv_region_bd(bd)
+        try:
+            assert C.conv_region_ok(B, H, H, cin, cout, 5, tile, splits)
+            y = torch.empty(B, H, H, cout, dtype=torch.bfloat16, device=dev)
+            stats = torch.full((rows, 2, cout), float("nan"), device=dev)
+            slab = torch.full((splits * B * H * H * cout,), float("nan"), device=dev)
+            # keep the split-K slabs (FwdCfg bit 20): compare them, not only the combine
+            C.conv_fwd(xp.data_ptr(), w.data_ptr(), y.data_ptr(), stats.data_ptr() if splits == 1 else 0,
+                       slab.data_ptr(), B, H, H, cin, cout, 5, tile | ((1 << 20) if splits > 1 else 0), splits, _s())
+        finally:
+            C.set_conv_region(1)
+            C.set_conv_region_bd(0)
+        torch.cuda.synchronize()
+        if splits == 1:
+            assert _rel(y, ref) < 8e-3, bd
+            outs.append((y, stats))
+        else:
+            part = slab.view(splits, B, H, H, cout).sum(0)
+            assert _rel(part, ref) < 1e-3, bd
+            outs.append((slab,))
+    if len(outs) == 2:
+        # outputs / slabs bitwise; the BN statistics sum the wave rows of a tile in a
+        # different grouping (1 or 2 wave rows vs 2 or 4): equal to float rounding
+        assert torch.equal(outs[0][0], outs[1][0])
+        if splits == 1:
+            torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-3)
+
+
+def test_region_direct_b_dgrad_bn_reduce(C):
+    """The direct-B region kernel as the layer-2 dgrad with the previous
+    block's BN backward reduce in its epilogue (conv_fwd_bnred): dx bitwise
+    the LDS-ring region kernel's, the partial rows to float rounding."""
+    B, H, cin, cout = 8, 16, 64, 128  # the dgrad of block 2: dy [B,16,16,128] -> dP [B,16,16,64]
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(5)
+    dy = torch.randn(B, H, H, cout, device=dev, generator=g).to(torch.bfloat16)
+    wt = (torch.randn(cin, 5, 5, cout, device=dev, generator=g) * 0.05).to(torch.bfloat16)
+    yprev = torch.randn(B, 2 * H, 2 * H, cin, device=dev, generator=g).to(torch.bfloat16)
+    coef = torch.stack([torch.randn(cin, device=dev, generator=g) * 0.1, torch.rand(cin, device=dev, generator=g) + 0.5,
+                        torch.rand(cin, device=dev, generator=g) + 0.5, torch.randn(cin, device=dev, generator=g) * 0.1])
+    dyp = _pad(dy)
+    outs = []
+    for bd in (0, 1):
+        C.set_conv_region_bd(bd)
+        try:
+            dx = torch.empty(B, H, H, cin, dtype=torch.bfloat16, device=dev)
+            rows = torch.full(((B * H * H + 127) // 128, 2, cin), float("nan"), device=dev)
+            T = C.conv_fwd_bnred(dyp.data_ptr(), wt.data_ptr(), dx.data_ptr(), B, H, H, cout, cin, 5, 2,
+                                 yprev.data_ptr(), coef.data_ptr(), rows.data_ptr(), _s())
+        finally:
+            C.set_conv_region_bd(0)
+        torch.cuda.synchronize()
+        outs.append((dx, rows[:T]))
+    assert torch.isfinite(outs[0][1]).all()
+    assert torch.equal(outs[0][0], outs[1][0])  # dx bitwise; the rows group the wave rows differently
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-3)

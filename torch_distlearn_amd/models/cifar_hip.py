@@ -221,6 +221,10 @@ class CifarHIPExecutor:
         # bwd_reduce_head's launch is gone (DISTLEARN_HEAD_REDUCE=0: A/B)
         if "DISTLEARN_REGION" in os.environ:  # tuning: tap-reuse region conv kernel (0 off, 1 rows, 2 + images)
             self.C.set_conv_region(int(os.environ["DISTLEARN_REGION"]))
+        # direct-B region kernel (weights straight into registers, no LDS ring or
+        # barrier in the k-loop; csrc conv_fwd_region_bd_kernel): 0 off, 1 row
+        # tiles (layer 2 fwd / dgrad), 2 + whole-image tiles (layer 3)
+        self.C.set_conv_region_bd(int(os.environ.get("DISTLEARN_REGION_BD", "0")))
         if "DISTLEARN_BN_BWD_ITEMS" in os.environ:  # tuning: pooled pixels per thread of the BN backward reduce
             self.C.set_bn_bwd_items(int(os.environ["DISTLEARN_BN_BWD_ITEMS"]))
         self.side = torch.cuda.Stream(device=self.dev, priority=int(os.environ.get("DISTLEARN_SIDE_PRIORITY", "0"))) \
