@@ -470,6 +470,10 @@ class DataParallelTrainer:
         self._policy_done = True
         cands = self._policy_candidates()
         want = os.environ.get("DISTLEARN_POLICY", "auto")
+        if want not in cands and "@" not in want:
+            # a base policy name ("full" / "reserve") forces it at the communicator's current cap
+            cap = getattr(self.tree.comm, "channel_cap", None)
+            want = f"{want}@{cap}" if f"{want}@{cap}" in cands else want
         if want in cands:
             self._apply_candidate(*cands[want])
             self.policy = {"chosen": want, "how": "forced (DISTLEARN_POLICY)", **self._cap_record()}

@@ -219,8 +219,15 @@ class CifarHIPExecutor:
         # (atomic-rows mode 2) the last block's BN backward reduce runs inside the head
         # kernel and the classifier weight gradient rides the BN backward apply launch:
         # bwd_reduce_head's launch is gone (DISTLEARN_HEAD_REDUCE=0: A/B)
+        self._region_mode = int(os.environ.get("DISTLEARN_REGION", "1"))
         if "DISTLEARN_REGION" in os.environ:  # tuning: tap-reuse region conv kernel (0 off, 1 rows, 2 + images)
-            self.C.set_conv_region(int(os.environ["DISTLEARN_REGION"]))
+            self.C.set_conv_region(self._region_mode)
+        # the FORWARD conv of an image smaller than a 128-row tile (layer 3: 8x8, two
+        # images per tile) on the region kernel's whole-image tiles: 20.5 vs 24.6 us
+        # (scripts/bench_conv.py), 0.2981 vs 0.3021 ms/step (profiles/r5_fwd3_region_ab.txt);
+        # the dgrad of that layer stays on the streaming kernel, which hosts the side SGD
+        self.fwd_region_images = (os.environ.get("DISTLEARN_FWD_REGION_IMAGES", "1") == "1"
+                                  and self._region_mode == 1)
         # direct-B region kernel (weights straight into registers, no LDS ring or
         # barrier in the k-loop; csrc conv_fwd_region_bd_kernel): 0 off, 1 row
         # tiles (layer 2 fwd / dgrad), 2 + whole-image tiles (layer 3)
@@ -449,9 +456,16 @@ class CifarHIPExecutor:
                 hp = self.hs[i - 1]
                 C.set_conv_pool_load(self.y[i - 1].data_ptr(), *self._fin_args(i - 1, B * hp * hp),
                                      self.p[i - 1].data_ptr())
-            ntm = C.conv_fwd(inp.data_ptr(), w.data_ptr(), self.y[i].data_ptr(),
-                             self.stats[i].data_ptr() if train else 0, self.slabs.data_ptr(), B, h, h, cin, cout, KSIZE,
-                             t | self.fwd_cfg | _slab_cap_bits(sp), sp, s)
+            img = self.fwd_region_images and h * h < 128 and 128 % (h * h) == 0
+            if img:
+                C.set_conv_region(2)
+            try:
+                ntm = C.conv_fwd(inp.data_ptr(), w.data_ptr(), self.y[i].data_ptr(),
+                                 self.stats[i].data_ptr() if train else 0, self.slabs.data_ptr(), B, h, h, cin, cout,
+                                 KSIZE, t | self.fwd_cfg | _slab_cap_bits(sp), sp, s)
+            finally:
+                if img:
+                    C.set_conv_region(self._region_mode)
             fused = train and self.atomic  # coefficients derived by the consumer kernel
             if not fused:
                 C.bn_finalize(self.stats[i].data_ptr(), ntm, cout, M, self.p32[self._leaf(i, 2)].data_ptr(),
