@@ -69,6 +69,8 @@ def parse():
                     help="auto = the hand-written HIP executor for CIFAR-10 on a GPU, PyTorch ops otherwise")
     ap.add_argument("--graph", type=int, default=1, help="hipGraph capture of the client's steps (GPU)")
     ap.add_argument("--gpu", type=int, default=None)
+    ap.add_argument("--commBackend", default="auto", choices=["auto", "rccl", "gloo"],
+                    help="data plane (auto: RCCL on GPUs); gloo lets several roles share one GPU")
     ap.add_argument("--host", default=os.environ.get("MASTER_ADDR", "127.0.0.1"))
     ap.add_argument("--port", type=int, default=int(os.environ.get("MASTER_PORT", "8080")))
     ap.add_argument("--verbose", action="store_true")
@@ -112,7 +114,7 @@ def run(opt):
         opt.gpu = rank + 1
     dev = device_of(opt)
     set_verbose(opt.verbose)
-    tree = Tree(rank + 1, world, host=opt.host, port=opt.port, device=dev)
+    tree = Tree(rank + 1, world, host=opt.host, port=opt.port, device=dev, backend=opt.commBackend)
 
     torch.manual_seed(0)
     model = (CifarConvNet(seed=0) if opt.dataset == "cifar10" else MnistConvNet(seed=0)).to(dev)

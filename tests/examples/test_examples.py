@@ -114,7 +114,8 @@ def test_bench_contract_cpu(algo):
     assert out["n_gpus"] == 3 and out["steps"] == 3 and out["warmup"] == 1 and out["higher_is_better"]
     workers = 2 if algo == "async" else 3
     assert out["config"]["global_batch"] == 4 * workers
-    assert abs(out["value"] - 4 * workers * 1000.0 / out["ms_per_step"]) / out["value"] < 1e-3
+    # (value is rounded to 0.1 img/s: at CPU speed that alone can exceed 1e-3 relative)
+    assert abs(out["value"] - 4 * workers * 1000.0 / out["ms_per_step"]) <= max(1e-3 * out["value"], 0.051)
 
 
 def test_bench_self_launch_cpu():
