@@ -89,8 +89,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_bn_stamps", &set_bn_stamps);
   m.def("set_conv_wgrad_stamps", &set_conv_wgrad_stamps);
   m.def("set_conv_bn_reduce", &set_conv_bn_reduce, py::arg("x"), py::arg("save"), py::arg("w"), py::arg("b"),
-        py::arg("rows"), py::arg("ym") = 0);
+        py::arg("rows"), py::arg("ym") = 0, py::arg("mb") = 0);
   m.def("conv_wgrad_ex", &conv_wgrad_ex);
+  m.def("wgrad_posm_plan", &wgrad_posm_plan);
   // ---- ResNet-50 glue (resnet_glue.hip) ------------------------------------------
   m.def("s2d_stem_input", &s2d_stem_input);
   m.def("stem_weight_pack", &stem_weight_pack);

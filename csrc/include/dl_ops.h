@@ -101,7 +101,8 @@ void set_conv_fwd_pf(int on);
 void set_head_stamps(uintptr_t buf);
 void set_bn_stamps(uintptr_t buf);
 void set_conv_wgrad_stamps(uintptr_t buf);
-void set_conv_bn_reduce(uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, uintptr_t rows, uintptr_t ym = 0);
+void set_conv_bn_reduce(uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, uintptr_t rows, uintptr_t ym = 0,
+                        uintptr_t mb = 0);
 // the next conv_fwd (region kernel, forward with statistics) pools its input on load
 // from the previous block's pre-BN output (BN coefficients from its accumulated sums)
 void set_conv_pool_load(uintptr_t y_prev, uintptr_t sums, int64_t M, uintptr_t gamma, uintptr_t beta, uintptr_t bias,
@@ -118,6 +119,9 @@ int conv_fwd_ex(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_
 void conv_wgrad_ex(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int Ho, int Wo, int Hp, int Wp, int dHp, int dWp,
                    int dpad, int Cin, int Cout, int KH, int KW, int S, int splits, int ldo, int tile,
                    uintptr_t stream);
+// position-major wgrad plan at `steps` K steps per workgroup: {max splits a
+// column tile needs, workgroups with work} ({0, 0}: B does not take it)
+std::vector<int> wgrad_posm_plan(int B, int H, int W, int Cin, int Cout, int KS, int tile, int steps);
 void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, int Cin, int Cout, int KS, int splits,
                 int ldo, int tile, int atomic_creal, uintptr_t stream);
 void set_reduce_atomic_conv(int rows);

@@ -75,9 +75,10 @@ __device__ __forceinline__ void put_stats(float* __restrict__ stats, int64_t row
 // deterministic partial rows [T][sum g (C); sum g*xhat (C)] (one per M tile,
 // reduced by bn_rows_reduce into the BatchNorm's backward accumulator) --
 // bn_nhwc_bwd_reduce_kernel's arithmetic (relu mode 2), fused.
-// BNR == 3: the same for a BN + residual + ReLU output (relu mode 1: the mask
-// is out > 0 of the saved block output `ym`); the dgrad is the next block's c1
-// with the residual gradient added in the epilogue (ADD), so dz is complete.
+// BNR == 3: the same for a BN + residual + ReLU output (the mask is out > 0:
+// its bits `mb`, one byte per 8 channels as bn_nhwc's relu mode 3 writes them,
+// or else the saved block output `ym`); the dgrad is the next block's c1 with
+// the residual gradient added in the epilogue (ADD), so dz is complete.
 struct BnRedArgs {
   const bf16_t* y;     // BNR 1: [B][2Ho][2Wo][C] pre-BN output of the previous block; BNR 2: x [M][C]
   const float* coef;   // BNR 1: [4][C] mean, invstd, scale, shift
@@ -85,7 +86,8 @@ struct BnRedArgs {
   const float* save;   // BNR 2: [2][C] mean, invstd
   const float* w;      // BNR 2: gamma
   const float* b;      // BNR 2: beta
-  const bf16_t* ym;    // BNR 3: block output [M][C] (ReLU mask)
+  const bf16_t* ym;    // BNR 3: block output [M][C] (ReLU mask) ...
+  const uint8_t* mb;   // ... or its mask bits [M][C/8] (bit k of byte n/8: channel n + k)
 };
 
 // BatchNorm -> ReLU applied to the A operand on load (OL: the ResNet-50 b2 ->
@@ -153,7 +155,34 @@ struct ConvGeom {
   // (M tile, wave row) written straight from the lanes -- no LDS round and no
   // barriers in the epilogue (FwdCfg bit 21; T = M tiles x WM rows)
   int swave;
+  // position-major weight gradient (conv_wgrad tile bits 8-16): a K step is BK
+  // images at ONE output pixel, and a column tile only visits the pixels where
+  // one of its taps reads inside the image (wgrad_posm_steps); wposm = steps per
+  // workgroup (the tile's steps are split over ceil(steps / wposm) workgroups),
+  // wlognbc = log2(B / BK), wskip: splits a tile does not need write nothing
+  // (their slabs stay zero from allocation) instead of zeros
+  int wposm, wlognbc, wskip;
 };
+
+// Position-major wgrad steps of the column tile [k0, k0 + BN): output pixels
+// (ph0 + i, pw0 + j), i < nph, j < npw, where a tap of the tile reads inside
+// the image (padded row ph + kh is interior: pad <= ph + kh < H + pad), times
+// B / BK image chunks.  The ResNet-free CIFAR layers 3 / 4 (8x8 / 4x4, 5x5
+// kernels) visit 72 % / 49 % of the pixel-major steps.
+__host__ __device__ inline int wgrad_posm_steps(const ConvGeom& g, int k0, int BN, int& ph0, int& pw0, int& npw) {
+  const int kc_lo = k0 / 8, kc_hi = (k0 + BN) / 8 < g.Kch ? (k0 + BN) / 8 - 1 : g.Kch - 1;
+  const int kp_lo = kc_lo >> g.logC8, kp_hi = kc_hi >> g.logC8;
+  const int kh_lo = kp_lo / g.KW, kh_hi = kp_hi / g.KW;
+  int kw_lo = kp_lo - kh_lo * g.KW, kw_hi = kp_hi - kh_hi * g.KW;
+  if (kh_lo != kh_hi) { kw_lo = 0; kw_hi = g.KW - 1; }  // the tile spans a tap row boundary
+  ph0 = g.pad - kh_hi > 0 ? g.pad - kh_hi : 0;
+  pw0 = g.pad - kw_hi > 0 ? g.pad - kw_hi : 0;
+  const int ph1 = g.H + g.pad - kh_lo < g.H ? g.H + g.pad - kh_lo : g.H;
+  const int pw1 = g.W + g.pad - kw_lo < g.W ? g.W + g.pad - kw_lo : g.W;
+  const int nph = ph1 > ph0 ? ph1 - ph0 : 0;
+  npw = pw1 > pw0 ? pw1 - pw0 : 0;
+  return (nph * npw) << g.wlognbc;
+}
 
 // q = n / d, r = n - q*d for 0 <= n < 2^24 via a float reciprocal and one
 // correction step (the ResNet-50 spatial sizes 56/28/14/7 are not powers of two)
@@ -581,7 +610,11 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
           if (ok) {
             const uint4 xv4 = *reinterpret_cast<const uint4*>(br.y + (int64_t)m * g.Cout + n);
             uint4 mv4 = xv4;
-            if constexpr (BNR == 3) mv4 = *reinterpret_cast<const uint4*>(br.ym + (int64_t)m * g.Cout + n);
+            unsigned mbits = 0xffu;
+            if constexpr (BNR == 3) {
+              if (br.mb != nullptr) mbits = br.mb[(int64_t)m * (g.Cout >> 3) + (n >> 3)];
+              else mv4 = *reinterpret_cast<const uint4*>(br.ym + (int64_t)m * g.Cout + n);
+            }
             const float mv[8] = {lo_bf16(mv4.x), hi_bf16(mv4.x), lo_bf16(mv4.y), hi_bf16(mv4.y),
                                  lo_bf16(mv4.z), hi_bf16(mv4.z), lo_bf16(mv4.w), hi_bf16(mv4.w)};
             const float gd[8] = {lo_bf16(pk.x), hi_bf16(pk.x), lo_bf16(pk.y), hi_bf16(pk.y),
@@ -590,7 +623,8 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
                                  lo_bf16(xv4.z), hi_bf16(xv4.z), lo_bf16(xv4.w), hi_bf16(xv4.w)};
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-              const bool pos = BNR == 3 ? mv[k] > 0.f : fmaf(xv[k], rsc[q][k], rsh[q][k]) > 0.f;
+              const bool pos = BNR == 3 ? (br.mb != nullptr ? ((mbits >> k) & 1u) != 0u : mv[k] > 0.f)
+                                        : fmaf(xv[k], rsc[q][k], rsh[q][k]) > 0.f;
               const float gk = pos ? gd[k] : 0.f;
               s1[q][k] += gk;
               s2[q][k] = fmaf(gk, (xv[k] - rmu[q][k]) * ris[q][k], s2[q][k]);
@@ -1885,10 +1919,26 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
   const int mend = min(g.M, mbeg + m_per_split);
   const int HW = 1 << g.logHW, Wd = g.W, C8 = 1 << g.logC8;
   const int HpWp = g.Hp * g.Wp;
+  // position-major steps (g.wposm): this tile's steps, balanced over the
+  // ceil(steps / wposm) workgroups it needs; a split past those has no work
+  int pm_beg = 0, pm_nk = 0, pm_ph0 = 0, pm_pw0 = 0, pm_npw = 1;
+  if (g.wposm) {
+    const int ntot = wgrad_posm_steps(g, k0, BN, pm_ph0, pm_pw0, pm_npw);
+    const int st = (ntot + g.wposm - 1) / g.wposm;
+    if (split < st) {
+      pm_beg = split * ntot / st;
+      pm_nk = (split + 1) * ntot / st - pm_beg;
+    } else if (g.wskip) {
+      return;  // nothing issued yet; its slab stays zero from allocation
+    }
+    if (pm_npw == 0) pm_npw = 1;  // (no steps: only the divisor below)
+  }
   // padded pixel offset of row r inside a 64-aligned step (pow2 H, W: the step's
   // pixel decomposes as wave-uniform step base + per-lane row part; otherwise
-  // every lane decomposes its own pixel each step, out_pix)
+  // every lane decomposes its own pixel each step, out_pix); position-major:
+  // row r is image r of the step's chunk
   auto lane_pix = [&](int r) {
+    if (g.wposm) return r * HpWp;
     return g.pow2 ? (r >> g.logHW) * HpWp + ((r & (HW - 1)) >> g.logW) * g.Wp + (r & (Wd - 1)) : 0;
   };
 
@@ -1931,7 +1981,19 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
     char* sB = sA + A_BYTES;
     const int ms = mbeg + kt * BK;  // 64-aligned first row of the step
     const int left = mend - ms;     // rows left (uniform)
-    if (g.pow2) {
+    if (g.wposm) {
+      // step kt of this workgroup: pixel q, image chunk c (chunk-minor)
+      const bool ok = kt < pm_nk;
+      const int idx = pm_beg + (ok ? kt : 0);
+      const int q = idx >> g.wlognbc, c = idx & ((1 << g.wlognbc) - 1);
+      const int qh = q / pm_npw;
+      const int u = c * BK * HpWp + (pm_ph0 + qh) * g.Wp + pm_pw0 + (q - qh * pm_npw);  // wave-uniform
+      const unsigned ua = 2u * (unsigned)(u * g.Cout), ub = 2u * (unsigned)(u * g.Cin);
+#pragma unroll
+      for (int j = 0; j < A_INS; ++j) blds16_asm(dyr, ok ? a_v[j] : kOOB, ua, sA + (wid * A_INS + j) * 1024);
+#pragma unroll
+      for (int j = 0; j < B_INS; ++j) blds16_asm(xr, ok ? b_v[j] : kOOB, ub, sB + (wid * B_INS + j) * 1024);
+    } else if (g.pow2) {
       const int u = (ms >> g.logHW) * HpWp + ((ms & (HW - 1)) >> g.logW) * g.Wp;  // wave-uniform
       const unsigned ua = 2u * (unsigned)(u * g.Cout), ub = 2u * (unsigned)(u * g.Cin);
 #pragma unroll
@@ -1965,7 +2027,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int gq = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
-  const int nk = max(0, (mend - mbeg + BK - 1) / BK);
+  const int nk = g.wposm ? pm_nk : max(0, (mend - mbeg + BK - 1) / BK);
   // PF: (as conv_fwd_region_kernel) every step issues one stage
   // unconditionally, fragments of step i+1 are read (transposed LDS reads)
   // while the MFMAs of step i run, interleaved 1:1 -- needs >= 4 stages to
@@ -2523,7 +2585,7 @@ static void launch_fwd_w(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uin
   if (g_fwd_addend && (splits > 1 || stats)) throw std::runtime_error("conv_fwd_add: no split-K / statistics");
   if (g_bnred2.rows != nullptr) {
     if (splits > 1 || stats) throw std::runtime_error("conv BN reduce: plain unsplit output only");
-    if ((g_bnred2.ym != nullptr) != (g_fwd_addend != 0))
+    if ((g_bnred2.ym != nullptr || g_bnred2.mb != nullptr) != (g_fwd_addend != 0))
       throw std::runtime_error("conv BN reduce: the output-mask form (relu 1) goes with the residual addend");
     if constexpr ((BN / WN / 16) % 2 == 0) {  // the transposed epilogue (paired N fragments)
       if (g_fwd_addend)
@@ -2998,11 +3060,14 @@ void set_conv_side_reduce(uintptr_t g, int64_t lo, int64_t hi, std::vector<int64
 // reduce (BnRedArgs, BNR 2) for the following conv_fwd / conv_fwd_ex calls on
 // the streaming kernel: x = the BN's input [M][C] (the conv output's layout),
 // save = its [mean; invstd], w / b = gamma / beta, rows = [T][2][C] partials;
-// ym != 0: the ReLU mask is ym > 0 (BN + residual + ReLU, BNR 3; the call
-// must be a conv_fwd_add, whose addend completes the gradient).
-void set_conv_bn_reduce(uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, uintptr_t rows, uintptr_t ym) {
+// ym != 0: the ReLU mask is ym > 0, mb != 0: the mask is those bits (BN +
+// residual + ReLU, BNR 3; the call must be a conv_fwd_add, whose addend
+// completes the gradient).
+void set_conv_bn_reduce(uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, uintptr_t rows, uintptr_t ym,
+                        uintptr_t mb) {
+  if (ym && mb) throw std::runtime_error("set_conv_bn_reduce: ReLU mask from ym or from mask bits, not both");
   g_bnred2 = rows ? BnRedArgs{(const bf16_t*)x, nullptr, (float*)rows, (const float*)save, (const float*)w,
-                              (const float*)b, (const bf16_t*)ym}
+                              (const float*)b, (const bf16_t*)ym, (const uint8_t*)mb}
                   : BnRedArgs{};
 }
 
@@ -3093,8 +3158,6 @@ void conv_fwd_add(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t addend, int B
   if (!addend) throw std::runtime_error("conv_fwd_add: null addend");
   if (Cout % fwd_bn(tile) != 0) throw std::runtime_error("conv_fwd_add: Cout must be a multiple of the N tile");
   if (KS != 1 && g_region) throw std::runtime_error("conv_fwd_add: only the streaming kernel (KS = 1)");
-  if (addend_mask && g_bnred2.rows != nullptr)
-    throw std::runtime_error("conv_fwd_add: a masked addend does not combine with the fused BN reduce");
   g_fwd_addend = addend;
   g_fwd_addend_mask = addend_mask;
   try {
@@ -3208,8 +3271,46 @@ void conv_wgrad_ex(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int Ho, int 
   conv_wgrad_g(g, dy, x, out, splits, ldo, tile, 0, stream);
 }
 
-static void conv_wgrad_g(const ConvGeom& g, uintptr_t dy, uintptr_t x, uintptr_t out, int splits, int ldo, int tile,
+// Position-major wgrad plan (see ConvGeom::wposm): (max splits a column tile
+// needs, total workgroups with work) at `steps` K steps per workgroup
+static std::pair<int, int> wgrad_posm_need(const ConvGeom& g, int bm, int bn, int steps) {
+  int smax = 0, total = 0, ph0, pw0, npw;
+  for (int k0 = 0; k0 < g.K; k0 += bn) {
+    const int st = (wgrad_posm_steps(g, k0, bn, ph0, pw0, npw) + steps - 1) / steps;
+    smax = std::max(smax, st);
+    total += st;
+  }
+  return {smax, total * (g.Cout / bm)};
+}
+
+std::vector<int> wgrad_posm_plan(int B, int H, int W, int Cin, int Cout, int KS, int tile, int steps) {
+  ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
+  const int bk = tile == 4 ? 32 : 64;
+  if (B % bk != 0 || !is_pow2(B / bk)) return {0, 0};
+  g.wposm = steps;
+  g.wlognbc = ilog2_exact(B / bk, "B/BK");
+  const int bm = tile == 1 ? 64 : (tile >= 3 ? 256 : 128), bn = tile == 1 || tile == 0 ? 64 : 128;
+  const auto r = wgrad_posm_need(g, bm, bn, steps);
+  return {r.first, r.second};
+}
+
+static void conv_wgrad_g(const ConvGeom& g0, uintptr_t dy, uintptr_t x, uintptr_t out, int splits, int ldo, int tile,
                          int atomic_creal, uintptr_t stream) {
+  ConvGeom g = g0;
+  // tile bits 8-15: position-major steps per workgroup (0 = pixel-major), bit 16: idle splits write nothing
+  const int posm_steps = (tile >> 8) & 255, posm_skip = (tile >> 16) & 1;
+  tile &= 255;
+  if (posm_steps) {
+    const int bk = tile == 4 ? 32 : 64;
+    if (atomic_creal > 0 || g.dsep || !g.pow2 || g.S != 1 || g.B % bk != 0 || !is_pow2(g.B / bk))
+      throw std::runtime_error("conv_wgrad: position-major steps need pow2 H, W, B % BK == 0, B / BK a power of two");
+    g.wposm = posm_steps;
+    g.wlognbc = ilog2_exact(g.B / bk, "B/BK");
+    g.wskip = posm_skip;
+    const int bm = tile == 1 ? 64 : (tile >= 3 ? 256 : 128), bn = tile == 1 || tile == 0 ? 64 : 128;
+    if (wgrad_posm_need(g, bm, bn, posm_steps).first > std::max(1, splits))
+      throw std::runtime_error("conv_wgrad: a column tile needs more position-major splits than given");
+  }
   const int Cin = g.Cin, Cout = g.Cout, W = g.W;
   if (ldo < g.K) throw std::runtime_error("conv_wgrad: ldo < K");
   if (ldo % 4 != 0) throw std::runtime_error("conv_wgrad: ldo % 4 != 0 (16-byte slab stores)");

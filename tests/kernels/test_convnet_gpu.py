@@ -94,6 +94,51 @@ def test_conv_fwd_and_stats(C, shape, tile, splits, region):
     torch.testing.assert_close(stats[:, 1].sum(0), (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
 
 
+# (B, H, Cin, Cout) of the position-major wgrad: the executor's layers 3 / 4 at batch 128
+# and 64 (B / 64 image chunks), plus layer 2's 64-channel taps (a column tile spans two taps)
+WPOSM_SHAPES = [(128, 4, 256, 256), (128, 8, 128, 256), (64, 8, 128, 128), (64, 16, 64, 128)]
+
+
+@pytest.mark.parametrize("shape", WPOSM_SHAPES)
+@pytest.mark.parametrize("tile", [2, 0])
+def test_wgrad_position_major(C, shape, tile):
+    """Position-major weight gradient (ConvGeom::wposm, conv_wgrad tile bits
+    8-16): a K step is 64 images at one output pixel, a column tile visits
+    only the pixels where one of its taps reads inside the image, and its
+    steps are balanced over ceil(steps / L) workgroups.  The slab sum equals
+    an fp64 reference, with idle splits writing zeros (bit 16 off: slabs
+    start as NaN) or nothing (bit 16 on: slabs pre-zeroed), and the plan
+    helper agrees with the kernel (it refuses too few splits)."""
+    B, H, cin, cout = shape
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(31 + H + cin)
+    x = torch.randn(B, H, H, cin, device=dev, generator=g).to(torch.bfloat16)
+    dy = torch.randn(B, H, H, cout, device=dev, generator=g).to(torch.bfloat16)
+    xr = x.double().cpu().permute(0, 3, 1, 2)
+    wr = torch.zeros(cout, cin, 5, 5, dtype=torch.float64, requires_grad=True)
+    F.conv2d(xr, wr, padding=2).backward(dy.double().cpu().permute(0, 3, 1, 2))
+    dw_ref = wr.grad.permute(0, 2, 3, 1).float().to(dev)
+    K = 25 * cin
+    xp, dyp = _pad(x), _pad(dy)
+    full = B * H * H // 64
+    for steps in (max(1, full // 4), max(1, full // 2), full):
+        smax, total = C.wgrad_posm_plan(B, H, H, cin, cout, 5, tile, steps)
+        assert 1 <= smax <= (full + steps - 1) // steps and total >= smax
+        for skip in (0, 1):
+            slabs = (torch.zeros if skip else lambda *s, **k: torch.full(s, float("nan"), **k))(
+                smax, cout, K, device=dev)
+            C.conv_wgrad(dyp.data_ptr(), xp.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, smax, K,
+                         tile | (steps << 8) | (skip << 16), 0, _s())
+            dw = torch.empty(cout, 5, 5, cin, device=dev)
+            C.slab_reduce(slabs.data_ptr(), dw.data_ptr(), smax, cout, 25, cin, cin, _s())
+            torch.cuda.synchronize()
+            assert _rel(dw, dw_ref) < 1e-4, (steps, skip, _rel(dw, dw_ref))
+        if smax > 1:
+            with pytest.raises(RuntimeError, match="position-major splits"):
+                C.conv_wgrad(dyp.data_ptr(), xp.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, smax - 1, K,
+                             tile | (steps << 8), 0, _s())
+
+
 @pytest.mark.parametrize("shape", CONV_SHAPES)
 def test_conv_fwd_prefetch_pipeline_bitwise(C, shape):
     """The streaming kernel's fragment-prefetch main loop (set_conv_fwd_pf 1,

@@ -113,14 +113,18 @@ def test_resnet50_step_bn_dgrad_on_off(dev, monkeypatch):
     assert _rel(out[1][1], out[0][1]) < 2e-2
 
 
+@pytest.mark.parametrize("mask_bits", [True, False])
 @pytest.mark.parametrize("N,C,H,cout", [(4, 256, 14, 64), (2, 512, 14, 128), (2, 1024, 7, 256)])
-def test_dgrad_add_epilogue_bn_residual_sums(dev, N, C, H, cout):
+def test_dgrad_add_epilogue_bn_residual_sums(dev, monkeypatch, N, C, H, cout, mask_bits):
     """b3 form (BN + residual + ReLU, mask from the output): the next block's
     c1 dgrad with the residual gradient added in its epilogue (conv_fwd_add)
-    produces the BatchNorm's backward sums (BNR 3)."""
+    produces the BatchNorm's backward sums (BNR 3) -- the ReLU mask read from
+    the mask bits the forward apply wrote (relu mode 3) or from the output."""
+    from torch_distlearn_amd.ops import bn_nhwc
     from torch_distlearn_amd.ops.bn_nhwc import bn_act
     from torch_distlearn_amd.ops.conv import Conv1x1, ShadowBinding
 
+    monkeypatch.setattr(bn_nhwc, "_MASK_BITS", mask_bits)
     res = []
     for linked in (True, False):
         g = torch.Generator(device=dev).manual_seed(21)
@@ -139,6 +143,7 @@ def test_dgrad_add_epilogue_bn_residual_sums(dev, N, C, H, cout):
         torch.cuda.synchronize()
         if linked:
             assert L.get("nbwd") == 1 and "sums" not in L
+            assert (L["fwd"][7] is not None) == mask_bits and (L["fwd"][6] is None) == mask_bits
         res.append((x3.grad, r.grad, gamma.grad, beta.grad))
         if linked:  # fp32 reference of the chain
             xr, rr = x3.detach().float().requires_grad_(True), r.detach().float().requires_grad_(True)

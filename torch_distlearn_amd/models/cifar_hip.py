@@ -126,6 +126,38 @@ def _wgrad_plan(cout: int, K: int, M: int, reserve: int = 0, wide: Optional[bool
     return tile, splits
 
 
+# Position-major weight gradients for feature maps of at most this size (0 = off):
+# a K step is 64 images at ONE output pixel, and a column tile (one tap of a
+# 5x5 kernel) skips the pixels where it only reads the zero border -- layer 4
+# (4x4) visits 49 % of the pixel-major steps, layer 3 (8x8) 72 % -- with each
+# tile's steps balanced over as many workgroups as it needs (csrc ConvGeom::wposm).
+# Off: a position-major step gathers 64 rows 32 KB apart (one per image) where a
+# pixel-major step reads 64 adjacent pixels, and costs ~1.8x the time: wgrad3
+# 19.8 -> 27.5 us with 20 instead of 26 steps per workgroup, wgrad4 22.6 -> 26.0,
+# plus the extra slabs' sums; 0.312-0.314 vs 0.298-0.300 ms/step
+# (profiles/r5_wgrad_posm_ab.txt).  Tested option (test_wgrad_position_major).
+_WGRAD_POSM_MAX_HW = int(os.environ.get("DISTLEARN_WGRAD_POSM", "0"))
+
+
+def _wgrad_posm(C, B: int, h: int, cin: int, cout: int, tile: int, splits: int, reserve: int = 0):
+    """(tile id, splits) of a position-major weight gradient, or the pixel-major
+    plan unchanged: the fewest K steps per workgroup whose workgroups still fit
+    one round of the chip, when that beats the pixel-major steps per workgroup.
+    The tile id carries the steps (bits 8-15) and bit 16: splits a column tile
+    does not need write nothing (the executor's slabs are zero from allocation)."""
+    if h > _WGRAD_POSM_MAX_HW or tile not in (0, 2) or B % 64 != 0:
+        return tile, splits
+    slots = 256 - reserve
+    cur = -(-B * h * h // (64 * splits))  # pixel-major steps per workgroup
+    for steps in range(1, cur):
+        smax, total = C.wgrad_posm_plan(B, h, h, cin, cout, KSIZE, tile, steps)
+        if smax <= 1:
+            return tile, splits
+        if total <= slots:
+            return tile | (steps << 8) | (1 << 16), smax
+    return tile, splits
+
+
 class CifarHIPExecutor:
     takes_loader = True  # gathers DeviceLoader batches on the device inside the step
 
@@ -360,11 +392,15 @@ class CifarHIPExecutor:
                 if i + 1 < self.nb else g
             self.bwd_part.append(None if self.atomic else torch.empty(gp, 2, cout, device=d))
             tile_w, splits_w = _wgrad_plan(cout, K, M, self.cu_reserve)
+            if not self.atomic_wgrad:
+                tile_w, splits_w = _wgrad_posm(C, B, h, cin, cout, tile_w, splits_w, self.cu_reserve)
             direct = splits_w == 1 and cin == self.cins_real[i]
             self.wplan.append((tile_w, splits_w, direct))
             if not direct and not self.atomic_wgrad:
                 wslab_elems = max(wslab_elems, splits_w * cout * K)
-            self.wslab_l.append(None if (direct or self.atomic_wgrad) else torch.empty(splits_w * cout * K, device=d))
+            # (position-major plans: the slabs of splits a tile does not need stay zero)
+            alloc = torch.zeros if (tile_w >> 16) & 1 else torch.empty
+            self.wslab_l.append(None if (direct or self.atomic_wgrad) else alloc(splits_w * cout * K, device=d))
             if i > 0:
                 dt, ds = _fwd_plan(M, cin, KSIZE * KSIZE * cout)
                 self.dgrad_plan[i] = (dt, ds)

@@ -102,10 +102,10 @@ class _BnAct(torch.autograd.Function):
         # BN + residual + ReLU: the backward needs the output's ReLU mask, which x
         # alone does not give.  The apply writes it as bits (one byte per 8
         # channels per row, 1/16 of y) so both backward passes read that instead
-        # of y (relu mode 3); y itself is then not kept for the backward.
-        # (bn_link -- the consuming dgrad computes the backward sums -- reads y.)
+        # of y (relu mode 3); y itself is then not kept for the backward (a
+        # consuming dgrad that computes the backward sums, bn_link, reads the bits too).
         mbits = None
-        if relu and residual is not None and bn_link is None and _MASK_BITS:
+        if relu and residual is not None and _MASK_BITS:
             mbits = torch.empty(M * C // 8, dtype=torch.uint8, device=x.device)
         apply = (x.data_ptr(), res.data_ptr() if res is not None else 0, ybase, acc.data_ptr(),
                  weight.data_ptr(), bias.data_ptr(), save.data_ptr(),
@@ -133,8 +133,9 @@ class _BnAct(torch.autograd.Function):
         if ctx.bn_link is not None:
             # what the consuming convolution's dgrad epilogue needs to compute this
             # BatchNorm's backward sums itself (ops/conv.py _bn_reduce_begin); with a
-            # residual the ReLU mask is the output's sign (relu mode 1)
-            bn_link["fwd"] = (x, save, weight, bias, acc, C, y if ctx.relu == 1 else None)
+            # residual the ReLU mask is the output's sign: its bits (relu mode 3) or y (1)
+            bn_link["fwd"] = (x, save, weight, bias, acc, C, y if ctx.relu == 1 else None,
+                              mbits if ctx.relu == 3 else None)
         return y
 
     @staticmethod

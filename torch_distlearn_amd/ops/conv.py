@@ -155,16 +155,18 @@ def _bn_reduce_begin(C, link, M: int, cin: int, nrows: int, residual_add: bool =
     f = link.get("fwd") if link is not None else None
     if f is None:
         return None
-    x, save, w, b, acc4, cc, ym = f
-    if (ym is not None) != residual_add:
+    x, save, w, b, acc4, cc, ym, mb = f
+    if (ym is not None or mb is not None) != residual_add:
         return None
     if cc != cin or x.numel() != M * cin or not x.is_contiguous(memory_format=torch.channels_last):
         return None
     if ym is not None and (ym.numel() != M * cin or not ym.is_contiguous(memory_format=torch.channels_last)):
         return None
+    if mb is not None and mb.numel() * 8 != M * cin:
+        return None
     rows = torch.empty(max(1, nrows), 2, cc, device=x.device)
     C.set_conv_bn_reduce(x.data_ptr(), save.data_ptr(), w.data_ptr(), b.data_ptr(), rows.data_ptr(),
-                         0 if ym is None else ym.data_ptr())
+                         0 if ym is None else ym.data_ptr(), 0 if mb is None else mb.data_ptr())
     return rows, f
 
 
@@ -172,7 +174,7 @@ def _bn_reduce_end(C, link, st, T: int, s) -> None:
     """Disarm, then column-sum the partial rows into the BatchNorm's backward
     half of its sums buffer and tell its backward (``link["sums"]``)."""
     C.set_conv_bn_reduce(0, 0, 0, 0, 0)
-    rows, (x, save, w, b, acc4, cc, _) = st
+    rows, (x, save, w, b, acc4, cc, _, _) = st
     accb = acc4[2 * cc:]
     if link.get("nbwd", 0):  # a second backward (retain_graph): start from 0 again
         accb.zero_()
