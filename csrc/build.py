@@ -103,6 +103,9 @@ def _compile(src: str, force: bool, verbose: bool, newest_header: float):
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+    # the object is as old as the sources it was compiled from: a source edited
+    # while hipcc ran (minutes for conv_igemm.hip) is newer and rebuilds next time
+    os.utime(obj, (t0 - 1.0, t0 - 1.0))
     return obj, time.time() - t0, True
 
 

@@ -571,12 +571,47 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
       }
     }
   }
+  // the stored row of fragment a (position-major tiles hold image pm_b0 + r at
+  // output pixel pm_pos)
+  auto row_of = [&](int a, bool& ok) {
+    const int ml = m0 + wm * TM + a * 16 + (lane & 15);
+    ok = ml < g.M;
+    return g.posm ? (pm_b0 + ml - m0) * (g.H * g.W) + pm_pos : (g.om && ok ? om_row(g, ml) : ml);
+  };
+  // ADD (plain): every fragment's addend (and mask byte) loaded before the
+  // first store -- y may alias it as far as the compiler knows, so a load left
+  // in the loop below waits behind each store, one memory latency per
+  // fragment: ResNet-50 c1 dgrads with the residual addend 827 vs 956 / 538 vs
+  // 575 us per step (profiles/r5_resnet_bn_dgrad_ab.txt).  Not for BNR 2 / 3
+  // (the ResNet BN-dgrad fusion: with the BN input preloaded as well its c1
+  // dgrad took 2122 instead of 1576 us per step, register pressure) nor BNR 1
+  // (the CIFAR region dgrad's pool windows: 24.3 vs 23.7-24.0 us)
+  constexpr bool PA = ADD && BNR == 0;
+  uint4 pad_[PA ? FM : 1][PA ? NP : 1];
+  unsigned padm_[PA ? FM : 1][PA ? NP : 1];
+  if constexpr (PA) {
+#pragma unroll
+    for (int a = 0; a < FM; ++a) {
+      bool ok;
+      const int m = row_of(a, ok);
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        const int n = n0 + nl + 32 * q;
+        const int64_t o = (int64_t)(ok ? m : 0) * g.Cout + n, ob = (int64_t)(ok ? m : 0) * (g.Cout >> 3) + (n >> 3);
+        {
+          // (ADD: stats carries the addend's optional mask bits, conv_fwd_add: the
+          // residual gradient = dy of the BN + residual + ReLU, masked here)
+          const uint8_t* mb = reinterpret_cast<const uint8_t*>(stats);
+          pad_[a][q] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(slab) + o);
+          padm_[a][q] = mb != nullptr ? mb[ob] : 0xffu;
+        }
+      }
+    }
+  }
 #pragma unroll
   for (int a = 0; a < FM; ++a) {
-    const int ml = m0 + wm * TM + a * 16 + (lane & 15);
-    const bool ok = ml < g.M;
-    // stored row: position-major tiles hold image pm_b0 + r at output pixel pm_pos
-    const int m = g.posm ? (pm_b0 + ml - m0) * (g.H * g.W) + pm_pos : (g.om && ok ? om_row(g, ml) : ml);
+    bool ok;
+    const int m = row_of(a, ok);
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
       const int n = n0 + nl + 32 * q;
@@ -585,11 +620,11 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
       for (int j = 0; j < 4; ++j) { v[j] = acc[a][2 * q][j]; v[4 + j] = acc[a][2 * q + 1][j]; }
       if constexpr (ADD) {
         if (ok) {
-          const uint4 ad = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(slab) + (int64_t)m * g.Cout + n);
-          // (ADD: stats carries the addend's optional mask bits, conv_fwd_add: the
-          // residual gradient = dy of the BN + residual + ReLU, masked here)
           const uint8_t* mb = reinterpret_cast<const uint8_t*>(stats);
-          const unsigned bits = mb != nullptr ? mb[(int64_t)m * (g.Cout >> 3) + (n >> 3)] : 0xffu;
+          const uint4 ad = PA ? pad_[a][q]
+                                    : *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(slab) +
+                                                                      (int64_t)m * g.Cout + n);
+          const unsigned bits = PA ? padm_[a][q] : (mb != nullptr ? mb[(int64_t)m * (g.Cout >> 3) + (n >> 3)] : 0xffu);
           const float a8[8] = {lo_bf16(ad.x), hi_bf16(ad.x), lo_bf16(ad.y), hi_bf16(ad.y),
                                lo_bf16(ad.z), hi_bf16(ad.z), lo_bf16(ad.w), hi_bf16(ad.w)};
 #pragma unroll

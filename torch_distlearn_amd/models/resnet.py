@@ -131,9 +131,11 @@ _HEAD_HIP = os.environ.get("DISTLEARN_RESNET_HEAD", "hip") == "hip"
 # the BatchNorm backward sums (sum g, sum g*xhat) from the epilogue of the dgrad that
 # produces the BN's output gradient (b1 / b2: the c2 / c3 dgrads; b3: the next block's
 # c1 dgrad, which adds the residual gradient) instead of the BN's reduce pass over dz
-# and x (ops/conv.py _bn_reduce_begin).  Off: the epilogue's extra read of x costs the
-# dgrads what the reduce pass saves -- every ResNet-50 BN kernel already streams at
-# ~5.5 TB/s, so a fusion only pays if it removes bytes (profiles/r3_resnet_bn_dgrad_ab.txt)
+# and x (ops/conv.py _bn_reduce_begin); the b3 form reads the ReLU mask bits the forward
+# apply wrote.  Off: the reduce pass goes (-1.64 ms/step) but every fused epilogue
+# re-reads the BN input x, as many bytes as the dgrad writes, and the one-round dgrad
+# grids expose that latency (+2.0 ms): 24.53 vs 24.21 ms/step
+# (profiles/r5_resnet_bn_dgrad_ab.txt; round 3: r3_resnet_bn_dgrad_ab.txt)
 _BN_DGRAD = os.environ.get("DISTLEARN_RESNET_BN_DGRAD", "0") == "1"
 # b2's BatchNorm + ReLU applied by c3's 1x1 GEMM to its A operand on load (csrc
 # set_conv_bn_on_load): the b2 apply launch and its read of c2's output are gone
