@@ -46,7 +46,19 @@ def run(fn, world: int, *args, timeout: float = 240.0, dead=()):
     """Run ``fn(rank, world, port, *args)`` in ``world`` processes; return the
     per-rank results (raises on any worker failure or timeout).  Ranks in
     ``dead`` are expected to die without reporting (fault-injection tests):
-    their result is None."""
+    their result is None.  The ephemeral port is probed, then bound by rank 0's
+    store a moment later; if another process took it in between (EADDRINUSE
+    at rendezvous, seen once on a busy box) the whole run starts again on a
+    fresh port, once."""
+    try:
+        return _run(fn, world, *args, timeout=timeout, dead=dead)
+    except RuntimeError as e:
+        if "EADDRINUSE" not in str(e):
+            raise
+        return _run(fn, world, *args, timeout=timeout, dead=dead)
+
+
+def _run(fn, world: int, *args, timeout: float = 240.0, dead=()):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
