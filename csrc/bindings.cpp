@@ -92,6 +92,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("rows"), py::arg("ym") = 0, py::arg("mb") = 0);
   m.def("conv_wgrad_ex", &conv_wgrad_ex);
   m.def("wgrad_posm_plan", &wgrad_posm_plan);
+  m.def("conv_wgrad_c8", &conv_wgrad_c8);
   // ---- ResNet-50 glue (resnet_glue.hip) ------------------------------------------
   m.def("s2d_stem_input", &s2d_stem_input);
   m.def("stem_weight_pack", &stem_weight_pack);

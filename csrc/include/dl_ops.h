@@ -119,6 +119,10 @@ int conv_fwd_ex(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_
 void conv_wgrad_ex(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int Ho, int Wo, int Hp, int Wp, int dHp, int dWp,
                    int dpad, int Cin, int Cout, int KH, int KW, int S, int splits, int ldo, int tile,
                    uintptr_t stream);
+// first-layer weight gradient from an LDS-resident input region (Cin 8, Cout 64):
+// fp32 slabs [B * H / R][64][ldo]; returns the split count
+int conv_wgrad_c8(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, int Cin, int Cout, int KS, int R,
+                  int ldo, uintptr_t stream);
 // position-major wgrad plan at `steps` K steps per workgroup: {max splits a
 // column tile needs, workgroups with work} ({0, 0}: B does not take it)
 std::vector<int> wgrad_posm_plan(int B, int H, int W, int Cin, int Cout, int KS, int tile, int steps);

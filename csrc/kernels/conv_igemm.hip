@@ -1809,6 +1809,117 @@ __global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restri
   }
 }
 
+// --------------------------------------------------------------------------
+// First-layer weight gradient (Cin = 8, K = taps * 8 <= 208) from an LDS-
+// resident input region.  The generic wgrad gathers the im2col rows of x
+// through the L2 for every 64-column K tile: for the reference's layer 1 that
+// is 4 tiles x (8 KB dy + 8 KB im2col) per 64-pixel step, and every conv loop
+// here runs at the L2->CU rate.  A workgroup of this kernel owns a band of R
+// output rows of one image and the WHOLE 64 x 208 weight-gradient tile:
+//   * its padded input rows (R + KS - 1 rows x Wp pixels x 16 B) are DMA'd
+//     into LDS once, and every tap's B fragment is read from there with
+//     ds_read_b64_tr_b16 at the tap's pixel offset (no im2col in memory);
+//   * only dy streams, 64 pixels (8 KB) per step through a 3-stage ring,
+//     read as the other operand with the same transposed reads;
+// so a step moves 8 KB of dy instead of 64 KB, and x is read ~1.25x in total.
+// Waves: wm = wid & 3 owns 16 output channels, wk = wid >> 2 the K fragments
+// wk, wk + 2, ... (fragment j = taps 2j, 2j + 1; taps past KS*KS read a zero
+// slot).  Output: fp32 slab [band][Cout][ldo] (one split per band), the
+// layout of conv_wgrad's slabs.
+// --------------------------------------------------------------------------
+template <int ST>
+__global__ void __launch_bounds__(512) conv_wgrad_c8r_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                             float* __restrict__ out, const ConvGeom g, int R, int ldo) {
+  constexpr int NW = 8, BK = 64, NKF = 7;  // 13 K fragments over 2 wave columns
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid & 3, wk = wid >> 2;
+  const int taps = g.KS * g.KS, nkf = (taps + 1) / 2;
+  const int bands = g.H / R;
+  const int img = blockIdx.x / bands, R0 = (blockIdx.x - img * bands) * R;
+  const int rrows = R + g.KS - 1;
+  const int rslots = rrows * g.Wp;                   // region pixels (16 B each)
+  const int rslots_p = (rslots + 1 + 63) / 64 * 64;  // + >= 1 zero slot, whole DMA pieces
+  char* sR = smem;
+  char* sD = smem + rslots_p * 16;  // dy ring: ST x [64 px][8 chunks] (swz_tr<8>)
+  // (all LDS-DMA from asm: a builtin one in flight makes hipcc drain vmcnt before every tr read)
+  const i32x4 xr = make_rsrc4(x, (unsigned)((int64_t)g.B * g.Hp * g.Wp * 16));
+  const i32x4 dyr = make_rsrc4(dy, (unsigned)((int64_t)g.B * g.Hp * g.Wp * g.Cout * 2));
+  const int start_pix = (img * g.Hp + R0) * g.Wp;
+  const int npieces = rslots_p / 64;  // region DMA pieces: waves 0 .. npieces % NW - 1 issue one more
+  for (int q = wid; q < npieces; q += NW) {
+    const int sl = q * 64 + lane;
+    blds16_asm(xr, sl < rslots ? 16u * (unsigned)(start_pix + sl) : kOOB, 0u, sR + q * 1024);
+  }
+  // dy lanes: 8 rows (pixels) x 8 chunks per wave instruction, one per wave per step
+  const int drow = 8 * wid + lane / 8;
+  const int dch = swz_tr<8>(drow, lane % 8) - drow * 8;  // logical chunk of this LDS slot (involution)
+  const int nsteps = R * g.W / BK;
+  auto issue = [&](int s, int slot) {
+    const int px = s * BK + drow;  // band-local output pixel
+    const int oh = R0 + (px >> g.logW), ow = px & (g.W - 1);
+    const unsigned v = s < nsteps ? 2u * (unsigned)(((img * g.Hp + oh + g.pad) * g.Wp + ow + g.pad) * g.Cout + dch * 8)
+                                  : kOOB;
+    blds16_asm(dyr, v, 0u, sD + slot * (BK * 128) + wid * 1024);
+  };
+#pragma unroll
+  for (int p = 0; p < ST - 1; ++p) issue(p, p);
+  f32x4 acc[NKF];
+#pragma unroll
+  for (int t = 0; t < NKF; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int gq = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  // per K fragment: this lane's tap offset (region slots) and byte offset in the 16-B pixel
+  int toff[NKF], tsub[NKF];
+#pragma unroll
+  for (int t = 0; t < NKF; ++t) {
+    const int jf = wk + 2 * t, k = jf * 16 + 4 * p4, tap = k >> 3;
+    const int kh = tap / g.KS, kw = tap - kh * g.KS;
+    toff[t] = (jf < nkf && tap < taps) ? kh * g.Wp + kw : -1;
+    tsub[t] = (k & 7) * 2;
+  }
+  const int zero_byte = rslots * 16;
+  int slot = 0;
+  for (int s = 0; s < nsteps; ++s) {
+    wait_vmcnt<ST - 2>();  // stage s landed (and, at s = 0, the region: issued before every stage)
+    block_sync_lds();
+    issue(s + ST - 1, (slot + ST - 1) % ST);
+    const char* D = sD + slot * (BK * 128);
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int r0 = kk * 32 + gq * 8 + q4;
+      const int col = wm * 16 + 4 * p4, ch = col >> 3, sub = (col & 7) * 2;
+      const s16x4 alo = ds_read_tr16(D + swz_tr<8>(r0, ch) * 16 + sub);
+      const s16x4 ahi = ds_read_tr16(D + swz_tr<8>(r0 + 4, ch) * 16 + sub);
+      const bf16x8 fa = bf16x8{alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]};
+      // band-local pixels s*64 + r0 (lo) and + 4 (hi): region slot of tap (0, 0)
+      const int plo = s * BK + r0, phi = plo + 4;
+      const int slo = (plo >> g.logW) * g.Wp + (plo & (g.W - 1)), shi = (phi >> g.logW) * g.Wp + (phi & (g.W - 1));
+#pragma unroll
+      for (int t = 0; t < NKF; ++t) {
+        if (wk + 2 * t >= nkf) break;
+        const int blo = toff[t] >= 0 ? (slo + toff[t]) * 16 + tsub[t] : zero_byte;
+        const int bhi = toff[t] >= 0 ? (shi + toff[t]) * 16 + tsub[t] : zero_byte;
+        const s16x4 lo = ds_read_tr16(sR + blo), hi = ds_read_tr16(sR + bhi);
+        const bf16x8 fb = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc[t] = mfma16(fb, fa, acc[t]);  // C^T: lane holds 4 consecutive k of one co
+      }
+    }
+    slot = slot + 1 == ST ? 0 : slot + 1;
+  }
+  wait_vmcnt<0>();  // the trailing zero-fill DMAs target the ring
+  // slab[band][co][k]: lane (rq, col_l) holds k = 16 jf + 4 rq + 0..3 of co = 16 wm + col_l
+  float* o = out + (int64_t)blockIdx.x * g.Cout * ldo;
+  const int col_l = lane & 15, rq = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < NKF; ++t) {
+    const int jf = wk + 2 * t;
+    const int k = jf * 16 + rq * 4, co = wm * 16 + col_l;
+    if (jf < nkf && k < g.K)
+      *reinterpret_cast<float4*>(o + (int64_t)co * ldo + k) = make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
+  }
+}
+
 // split-K combine: y = bf16(sum_s slab[s]) (+ BN partial sums, one row per block)
 template <bool STATS>
 __global__ void __launch_bounds__(256) splitk_combine_kernel(const float* __restrict__ slab, bf16_t* __restrict__ y,
@@ -3430,6 +3541,35 @@ static void conv_wgrad_g(const ConvGeom& g0, uintptr_t dy, uintptr_t x, uintptr_
 #undef DL_WGX
 #undef DL_WGXK
   DL_HIP_CHECK(hipGetLastError());
+}
+
+// First-layer weight gradient from an LDS-resident input region
+// (conv_wgrad_c8r_kernel): x = [B][Hp][Wp][8] zero-bordered, dy = [B][Hp][Wp][64]
+// with the output interior at (pad, pad) (conv_wgrad's operands), R output rows
+// per workgroup; out = fp32 slabs [B * H / R][64][ldo].  Returns the split count.
+int conv_wgrad_c8(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, int Cin, int Cout, int KS, int R,
+                  int ldo, uintptr_t stream) {
+  const ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
+  if (Cin != 8 || Cout != 64) throw std::runtime_error("conv_wgrad_c8: Cin = 8, Cout = 64 only");
+  if (KS * KS > 26) throw std::runtime_error("conv_wgrad_c8: at most 26 taps (13 K fragments)");
+  if (!g.pow2 || W % 8 != 0 || 64 % W != 0) throw std::runtime_error("conv_wgrad_c8: W must be 8, 16, 32 or 64");
+  if (R < 1 || H % R != 0 || (R * W) % 64 != 0) throw std::runtime_error("conv_wgrad_c8: R | H and 64 | R * W");
+  if (ldo < g.K || ldo % 4 != 0) throw std::runtime_error("conv_wgrad_c8: ldo >= K, ldo % 4 == 0");
+  constexpr int ST = 3;
+  const int rslots_p = ((R + KS - 1) * g.Wp + 1 + 63) / 64 * 64;
+  const size_t lds = (size_t)rslots_p * 16 + ST * 64 * 128;
+  if (lds > 160 * 1024) throw std::runtime_error("conv_wgrad_c8: region too large for LDS");
+  static bool attr = false;
+  if (!attr) {
+    DL_HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_c8r_kernel<ST>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  const int grid = B * (H / R);
+  conv_wgrad_c8r_kernel<ST><<<grid, 512, lds, as_stream(stream)>>>((const bf16_t*)dy, (const bf16_t*)x, (float*)out, g,
+                                                                    R, ldo);
+  DL_HIP_CHECK(hipGetLastError());
+  return grid;
 }
 
 void set_reduce_atomic_conv(int rows) {

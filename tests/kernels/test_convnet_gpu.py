@@ -94,6 +94,51 @@ def test_conv_fwd_and_stats(C, shape, tile, splits, region):
     torch.testing.assert_close(stats[:, 1].sum(0), (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
 
 
+@pytest.mark.parametrize("B,H,R", [(8, 32, 2), (8, 32, 16), (4, 32, 32), (4, 16, 4), (4, 16, 16), (2, 8, 8)])
+def test_wgrad_first_layer_region(C, B, H, R):
+    """First-layer weight gradient from an LDS-resident input region
+    (conv_wgrad_c8r_kernel: Cin 8, Cout 64, a workgroup per band of R output
+    rows owns the whole 64 x 200 tile, B fragments read per tap from the
+    region with ds_read_b64_tr_b16): one slab per band, whose sum equals an
+    fp64 reference and the generic split-K wgrad."""
+    cin, cout = 8, 64
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(41 + B * H + R)
+    x = torch.randn(B, H, H, cin, device=dev, generator=g).to(torch.bfloat16)
+    x[..., 3:] = 0  # the executor's 3 -> 8 channel pad (any values are fine for the kernel)
+    dy = torch.randn(B, H, H, cout, device=dev, generator=g).to(torch.bfloat16)
+    xr = x.double().cpu().permute(0, 3, 1, 2)
+    wr = torch.zeros(cout, cin, 5, 5, dtype=torch.float64, requires_grad=True)
+    F.conv2d(xr, wr, padding=2).backward(dy.double().cpu().permute(0, 3, 1, 2))
+    dw_ref = wr.grad.permute(0, 2, 3, 1).float().to(dev)
+    K = 25 * cin
+    xp, dyp = _pad(x), _pad(dy)
+    nb = B * H // R
+    slabs = torch.full((nb, cout, K), float("nan"), device=dev)
+    assert C.conv_wgrad_c8(dyp.data_ptr(), xp.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, R, K, _s()) == nb
+    dw = torch.empty(cout, 5, 5, cin, device=dev)
+    C.slab_reduce(slabs.data_ptr(), dw.data_ptr(), nb, cout, 25, cin, cin, _s())
+    gen = torch.full((4, cout, K), float("nan"), device=dev)
+    C.conv_wgrad(dyp.data_ptr(), xp.data_ptr(), gen.data_ptr(), B, H, H, cin, cout, 5, 4, K, 1, 0, _s())
+    dwg = torch.empty(cout, 5, 5, cin, device=dev)
+    C.slab_reduce(gen.data_ptr(), dwg.data_ptr(), 4, cout, 25, cin, cin, _s())
+    torch.cuda.synchronize()
+    assert not torch.isnan(slabs).any()
+    assert _rel(dw, dw_ref) < 1e-4, _rel(dw, dw_ref)
+    assert _rel(dw, dwg) < 1e-4
+    # one band alone: slab b is the gradient of the rows it owns
+    b = nb // 2
+    img, r0 = b // (H // R), (b % (H // R)) * R
+    dyb = torch.zeros_like(dy)
+    dyb[img, r0:r0 + R] = dy[img, r0:r0 + R]
+    wr2 = torch.zeros(cout, cin, 5, 5, dtype=torch.float64, requires_grad=True)
+    F.conv2d(xr, wr2, padding=2).backward(dyb.double().cpu().permute(0, 3, 1, 2))
+    ref_b = wr2.grad.permute(0, 2, 3, 1).reshape(cout, K).float().to(dev)
+    assert _rel(slabs[b], ref_b) < 1e-4
+    with pytest.raises(RuntimeError, match="R \\| H"):
+        C.conv_wgrad_c8(dyp.data_ptr(), xp.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, 3, K, _s())
+
+
 # (B, H, Cin, Cout) of the position-major wgrad: the executor's layers 3 / 4 at batch 128
 # and 64 (B / 64 image chunks), plus layer 2's 64-channel taps (a column tile spans two taps)
 WPOSM_SHAPES = [(128, 4, 256, 256), (128, 8, 128, 256), (64, 8, 128, 128), (64, 16, 64, 128)]

@@ -158,6 +158,18 @@ def _wgrad_posm(C, B: int, h: int, cin: int, cout: int, tile: int, splits: int, 
     return tile, splits
 
 
+# First-layer weight gradient from an LDS-resident input region (csrc
+# conv_wgrad_c8r_kernel): one workgroup per band of this many output rows owns
+# the whole 64 x 200 tile, reads its padded input rows once and streams only dy
+# (8 KB per 64-pixel step instead of 4 K tiles x 16 KB through the L2); one
+# slab per band.  0 = the generic split-K wgrad (default): the region kernel ran
+# 13.2 vs 11.7 us and its 256 slabs cost the update 1 us more -- 0.3052-0.3069 vs
+# 0.3020-0.3038 ms/step at 16 rows, 0.310-0.312 at 32 (profiles/r5_wgrad_c8r_ab.txt):
+# with one workgroup per CU its 16 transposed LDS reads per 7 MFMAs and the barrier
+# per 64-pixel step are exposed latency, so the L2 bytes it saves were not the bound.
+_WGRAD_C8R_ROWS = int(os.environ.get("DISTLEARN_WGRAD_C8R", "0"))
+
+
 class CifarHIPExecutor:
     takes_loader = True  # gathers DeviceLoader batches on the device inside the step
 
@@ -394,12 +406,16 @@ class CifarHIPExecutor:
             tile_w, splits_w = _wgrad_plan(cout, K, M, self.cu_reserve)
             if not self.atomic_wgrad:
                 tile_w, splits_w = _wgrad_posm(C, B, h, cin, cout, tile_w, splits_w, self.cu_reserve)
+            rb = _WGRAD_C8R_ROWS
+            if (not self.atomic_wgrad and i == 0 and rb > 0 and cin == 8 and cout == 64 and KSIZE * KSIZE <= 26
+                    and h in (8, 16, 32, 64) and h % rb == 0 and (rb * h) % 64 == 0):
+                tile_w, splits_w = -rb, B * h // rb  # tile < 0: conv_wgrad_c8 with -tile output rows per band
             direct = splits_w == 1 and cin == self.cins_real[i]
             self.wplan.append((tile_w, splits_w, direct))
             if not direct and not self.atomic_wgrad:
                 wslab_elems = max(wslab_elems, splits_w * cout * K)
             # (position-major plans: the slabs of splits a tile does not need stay zero)
-            alloc = torch.zeros if (tile_w >> 16) & 1 else torch.empty
+            alloc = torch.zeros if tile_w > 0 and (tile_w >> 16) & 1 else torch.empty
             self.wslab_l.append(None if (direct or self.atomic_wgrad) else alloc(splits_w * cout * K, device=d))
             if i > 0:
                 dt, ds = _fwd_plan(M, cin, KSIZE * KSIZE * cout)
@@ -690,8 +706,12 @@ class CifarHIPExecutor:
             rs = ws  # the stream that writes this block's weight gradient last
             if not direct and not self.atomic_wgrad:
                 slab = self.wslab_l[i]
-                C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), slab.data_ptr(), B, h, h, cin, cout, KSIZE,
-                             splits, K, tile, 0, wss)
+                if tile < 0:  # the first layer from an LDS-resident input region, one slab per band
+                    C.conv_wgrad_c8(dY.data_ptr(), xin.data_ptr(), slab.data_ptr(), B, h, h, cin, cout, KSIZE, -tile,
+                                    K, wss)
+                else:
+                    C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), slab.data_ptr(), B, h, h, cin, cout, KSIZE,
+                                 splits, K, tile, 0, wss)
                 sargs = (slab.data_ptr(), gw.data_ptr(), splits, cout, KSIZE * KSIZE, cin, self.cins_real[i])
                 if merge and i > 0:  # reduced by block i-1's BN backward reduce launch
                     pending = (sargs, i)
