@@ -44,11 +44,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_nhwc_fwd_pad", &bn_nhwc_fwd_pad, py::arg("x"), py::arg("res"), py::arg("y"), py::arg("acc"), py::arg("w"),
         py::arg("b"), py::arg("save"), py::arg("run_mean"), py::arg("run_var"), py::arg("M"), py::arg("C"),
         py::arg("eps"), py::arg("momentum"), py::arg("relu"), py::arg("have_stats"), py::arg("H"), py::arg("W"),
-        py::arg("opad"), py::arg("stream"), py::arg("mbits") = 0);
+        py::arg("opad"), py::arg("stream"), py::arg("mbits") = 0, py::arg("rbn_acc") = 0, py::arg("rbn_w") = 0,
+        py::arg("rbn_b") = 0, py::arg("rbn_save") = 0, py::arg("rbn_rm") = 0, py::arg("rbn_rv") = 0,
+        py::arg("rbn_eps") = 1e-5, py::arg("rbn_momentum") = 0.1);
   m.def("bn_nhwc_bwd_pad", &bn_nhwc_bwd_pad, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("save"),
         py::arg("w"), py::arg("b"), py::arg("acc"), py::arg("dx"), py::arg("dres"), py::arg("dw"), py::arg("db"),
         py::arg("M"), py::arg("C"), py::arg("relu"), py::arg("H"), py::arg("W"), py::arg("opad"), py::arg("stream"),
-        py::arg("have_sums") = 0, py::arg("mbits") = 0);
+        py::arg("have_sums") = 0, py::arg("mbits") = 0, py::arg("rbn_x") = 0, py::arg("rbn_save") = 0,
+        py::arg("rbn_w") = 0, py::arg("rbn_acc") = 0, py::arg("rbn_dw") = 0, py::arg("rbn_db") = 0);
   m.def("zero_border_nhwc", &zero_border_nhwc);
   m.def("gather_normalize", &gather_normalize);
 
@@ -140,7 +143,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_wgrad", &head_wgrad);
   m.def("mnist_step", &mnist_step);
   m.def("mnist_scratch_bytes", &mnist_scratch_bytes);
-  m.def("maxpool_nhwc_fwd", &maxpool_nhwc_fwd);
+  m.def("maxpool_nhwc_fwd", &maxpool_nhwc_fwd, py::arg("x"), py::arg("y"), py::arg("idx"), py::arg("N"), py::arg("H"),
+        py::arg("W"), py::arg("C"), py::arg("K"), py::arg("S"), py::arg("P"), py::arg("stream"), py::arg("bn_acc") = 0,
+        py::arg("bn_w") = 0, py::arg("bn_b") = 0, py::arg("bn_save") = 0, py::arg("bn_rm") = 0, py::arg("bn_rv") = 0,
+        py::arg("bn_eps") = 1e-5, py::arg("bn_momentum") = 0.1);
   m.def("maxpool_nhwc_bwd", &maxpool_nhwc_bwd);
 
   // ---- RCCL communicator ------------------------------------------------------

@@ -59,10 +59,14 @@ void disarm_sgd_next_prep();
 void bn_nhwc_fwd_pad(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b,
                      uintptr_t save, uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps,
                      double momentum, int relu, int have_stats, int H, int W, int opad, uintptr_t stream,
-                     uintptr_t mbits = 0);
+                     uintptr_t mbits = 0, uintptr_t rbn_acc = 0, uintptr_t rbn_w = 0, uintptr_t rbn_b = 0,
+                     uintptr_t rbn_save = 0, uintptr_t rbn_rm = 0, uintptr_t rbn_rv = 0, double rbn_eps = 1e-5,
+                     double rbn_momentum = 0.1);
 void bn_nhwc_bwd_pad(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b,
                      uintptr_t acc, uintptr_t dx, uintptr_t dres, uintptr_t dw, uintptr_t db, int64_t M, int C,
-                     int relu, int H, int W, int opad, uintptr_t stream, int have_sums = 0, uintptr_t mbits = 0);
+                     int relu, int H, int W, int opad, uintptr_t stream, int have_sums = 0, uintptr_t mbits = 0,
+                     uintptr_t rbn_x = 0, uintptr_t rbn_save = 0, uintptr_t rbn_w = 0, uintptr_t rbn_acc = 0,
+                     uintptr_t rbn_dw = 0, uintptr_t rbn_db = 0);
 void zero_border_nhwc(uintptr_t buf, int N, int H, int W, int C, int pad, uintptr_t stream);
 void bn_nhwc_fwd(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b, uintptr_t save,
                  uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps, double momentum, int relu, int have_stats,
@@ -213,7 +217,9 @@ void head_wgrad(uintptr_t h, uintptr_t dlogits, uintptr_t loss_b, int F, int B, 
 
 // pool_nhwc.hip ----------------------------------------------------------------
 void maxpool_nhwc_fwd(uintptr_t x, uintptr_t y, uintptr_t idx, int N, int H, int W, int C, int K, int S, int P,
-                      uintptr_t stream);
+                      uintptr_t stream, uintptr_t bn_acc = 0, uintptr_t bn_w = 0, uintptr_t bn_b = 0,
+                      uintptr_t bn_save = 0, uintptr_t bn_rm = 0, uintptr_t bn_rv = 0, double bn_eps = 1e-5,
+                      double bn_momentum = 0.1);
 void maxpool_nhwc_bwd(uintptr_t dy, uintptr_t idx, uintptr_t dx, int N, int H, int W, int C, int K, int S, int P,
                       uintptr_t stream);
 

@@ -19,6 +19,7 @@
 // The apply kernels recompute mean / invstd from the sums; block (0, g) writes
 // the saved statistics (and running stats / weight gradients) of its channels.
 #include "dl_common.h"
+#include "bn_coef_dev.h"
 #include "dl_ops.h"
 
 namespace dl {
@@ -131,17 +132,6 @@ __global__ void __launch_bounds__(NT) bn_nhwc_stats_kernel(const bf16_t* __restr
   block_reduce_atomic<NT>(s, q, g, c0, acc);
 }
 
-__device__ __forceinline__ void stats8(const float* __restrict__ acc, int C, int c, float invM, float eps,
-                                       float* mean, float* invstd) {
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const float m = acc[c + k] * invM;
-    const float var = fmaxf(acc[C + c + k] * invM - m * m, 0.f);
-    mean[k] = m;
-    invstd[k] = rsqrtf(var + eps);
-  }
-}
-
 // bit k = bf16 output channel k is nonzero (relu output >= 0: > 0 <=> nonzero,
 // the mask relu mode 1 derives from y)
 __device__ __forceinline__ uint8_t mask_byte(const u32x4& o) {
@@ -155,36 +145,37 @@ __device__ __forceinline__ uint8_t mask_byte(const u32x4& o) {
   return (uint8_t)m;
 }
 
+// The BatchNorm of the residual branch applied on load (ResBn; the ResNet-50
+// downsample BN feeding a block's b3): `res` is then that BN's INPUT, the
+// residual added is bf16(res * rsc + rsh) -- bitwise what its own apply launch
+// would have written -- and block 0 publishes its saved mean / invstd and
+// running statistics.  Its apply launch and the write + read of its output go.
+struct ResBn {
+  const float* acc;  // [2C] sum, sum of squares of the residual BN's input (null: plain residual)
+  const float* w;
+  const float* b;
+  float* save;  // [2C] mean, invstd (its backward's)
+  float* run_mean;
+  float* run_var;
+  float eps, momentum;
+};
+
 template <int U>
 __global__ void __launch_bounds__(kThreads) bn_nhwc_fwd_apply_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
     const float* __restrict__ acc, const float* __restrict__ w, const float* __restrict__ b, BnGeom g, float eps,
     int relu, float* __restrict__ save, float* __restrict__ run_mean, float* __restrict__ run_var, float momentum,
-    uint8_t* __restrict__ mbits) {
+    uint8_t* __restrict__ mbits, const ResBn rbn) {
   const int t = threadIdx.x, cv = t % g.CVB, r = t / g.CVB;
   const int c0 = blockIdx.y * g.CVB * 8;
   const int c = c0 + cv * 8;
-  const float invM = 1.f / (float)g.M;
-  float mean[8], invstd[8], sc[8], sh[8];
-  stats8(acc, g.C, c, invM, eps, mean, invstd);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    sc[k] = w[c + k] * invstd[k];
-    sh[k] = fmaf(-mean[k], sc[k], b[c + k]);
-  }
-  if (blockIdx.x == 0 && r == 0) {
-    const float unbias = g.M > 1 ? (float)g.M / (float)(g.M - 1) : 1.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      save[c + k] = mean[k];
-      save[g.C + c + k] = invstd[k];
-      if (run_mean != nullptr) {
-        const float var = fmaxf(acc[g.C + c + k] * invM - mean[k] * mean[k], 0.f);
-        run_mean[c + k] = (1.f - momentum) * run_mean[c + k] + momentum * mean[k];
-        run_var[c + k] = (1.f - momentum) * run_var[c + k] + momentum * var * unbias;
-      }
-    }
-  }
+  const bool publish = blockIdx.x == 0 && r == 0;
+  float sc[8], sh[8], rsc[8], rsh[8];
+  bn_coef8(acc, w, b, g.C, c, g.M, eps, momentum, publish, save, run_mean, run_var, sc, sh);
+  const bool rbn_on = rbn.acc != nullptr;
+  if (rbn_on)
+    bn_coef8(rbn.acc, rbn.w, rbn.b, g.C, c, g.M, rbn.eps, rbn.momentum, publish, rbn.save, rbn.run_mean,
+             rbn.run_var, rsc, rsh);
   const int64_t row0 = (int64_t)blockIdx.x * g.rows_per_block;
   const int64_t row1 = min(g.M, row0 + g.rows_per_block);
   const u32x4 z = {0u, 0u, 0u, 0u};
@@ -196,6 +187,10 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_fwd_apply_kernel(
     if (res != nullptr) {
       float q[8];
       unpack8(rr, q);
+      if (rbn_on) {  // the residual BN's output as its own apply would store it (bf16)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) q[k] = __uint_as_float((uint32_t)f32_to_bf16(fmaf(q[k], rsc[k], rsh[k])) << 16);
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) f[k] += q[k];
     }
@@ -233,11 +228,27 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_fwd_apply_kernel(
 // the 16 bytes of y in each backward pass; bit k = output channel k nonzero,
 // the same mask as mode 1) -- applied inline by the two kernels below, after
 // all of an iteration's loads are issued.
+// The backward of the residual branch's BatchNorm fused into the BN + residual
+// + ReLU's backward (ResNet-50 downsample blocks): the residual's gradient IS
+// g = dy * mask, so the reduce also sums g * xhat_r over the residual BN's
+// input x_r (its sum(g) is the same as ours), and the apply writes that BN's
+// input gradient a_r (g - mean g - xhat_r mean(g xhat_r)) where it would have
+// written g -- the residual BN's own reduce and apply passes, and the write +
+// two reads of g, go.
+struct ResBnBwd {
+  const bf16_t* x;   // the residual BN's input (null: plain residual gradient)
+  const float* save;  // its [2C] mean, invstd
+  const float* w;
+  float* acc;         // its [2C] backward sums (zeroed), filled by the reduce
+  float* dw;
+  float* db;
+};
+
 template <int NT>
 __global__ void __launch_bounds__(NT) bn_nhwc_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ save, const float* __restrict__ w, const float* __restrict__ b, BnGeom g, int relu,
-    float* __restrict__ acc, const uint8_t* __restrict__ mbits) {
+    float* __restrict__ acc, const uint8_t* __restrict__ mbits, const ResBnBwd rb) {
   const int t = threadIdx.x, cv = t % g.CVB, r = t / g.CVB;
   const int c0 = blockIdx.y * g.CVB * 8;
   const int c = c0 + cv * 8;
@@ -249,10 +260,17 @@ __global__ void __launch_bounds__(NT) bn_nhwc_bwd_reduce_kernel(
     sc[k] = w[c + k] * invstd[k];
     sh[k] = fmaf(-mean[k], sc[k], b[c + k]);
   }
-  float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bool fr = rb.x != nullptr;
+  float rmean[8], rinv[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    rmean[k] = fr ? rb.save[c + k] : 0.f;
+    rinv[k] = fr ? rb.save[g.C + c + k] : 0.f;
+  }
+  float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int64_t row0 = (int64_t)blockIdx.x * g.rows_per_block;
   const int64_t row1 = min(g.M, row0 + g.rows_per_block);
-  auto accum = [&](const u32x4& xr, const u32x4& dr, const u32x4& yr, unsigned mb) {
+  auto accum = [&](const u32x4& xr, const u32x4& dr, const u32x4& yr, unsigned mb, const u32x4& rr) {
     float gv[8], xv[8];
     unpack8(xr, xv);
     unpack8(dr, gv);
@@ -273,6 +291,12 @@ __global__ void __launch_bounds__(NT) bn_nhwc_bwd_reduce_kernel(
       sg[k] += gv[k];
       sgx[k] = fmaf(gv[k], (xv[k] - mean[k]) * invstd[k], sgx[k]);
     }
+    if (fr) {
+      float xrv[8];
+      unpack8(rr, xrv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sgr[k] = fmaf(gv[k], (xrv[k] - rmean[k]) * rinv[k], sgr[k]);
+    }
   };
   // four rows per iteration: every load of the group is issued before any is
   // consumed (8-12 16-byte loads in flight per lane; the single-row loop ran at
@@ -281,7 +305,7 @@ __global__ void __launch_bounds__(NT) bn_nhwc_bwd_reduce_kernel(
   int64_t row = row0 + r;
   const u32x4 z = {0u, 0u, 0u, 0u};
   for (; row + (U - 1) * g.RPI < row1; row += U * g.RPI) {
-    u32x4 xr[U], dr[U], yr[U];
+    u32x4 xr[U], dr[U], yr[U], rr[U];
     unsigned mb[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -290,16 +314,21 @@ __global__ void __launch_bounds__(NT) bn_nhwc_bwd_reduce_kernel(
       dr[u] = *(const u32x4*)(dy + off);
       yr[u] = relu == 1 ? *(const u32x4*)(y + off) : z;
       mb[u] = relu == 3 ? mbits[(row + u * g.RPI) * (g.C >> 3) + (c >> 3)] : 0u;
+      rr[u] = fr ? *(const u32x4*)(rb.x + off) : z;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) accum(xr[u], dr[u], yr[u], mb[u]);
+    for (int u = 0; u < U; ++u) accum(xr[u], dr[u], yr[u], mb[u], rr[u]);
   }
   for (; row < row1; row += g.RPI) {
     const int64_t off = row * g.C + c;
     accum(*(const u32x4*)(x + off), *(const u32x4*)(dy + off), relu == 1 ? *(const u32x4*)(y + off) : z,
-          relu == 3 ? mbits[row * (g.C >> 3) + (c >> 3)] : 0u);
+          relu == 3 ? mbits[row * (g.C >> 3) + (c >> 3)] : 0u, fr ? *(const u32x4*)(rb.x + off) : z);
   }
   block_reduce_atomic<NT>(sg, sgx, g, c0, acc);
+  if (fr) {
+    __syncthreads();  // (block_reduce_atomic's LDS is reused)
+    block_reduce_atomic<NT>(sg, sgr, g, c0, rb.acc);
+  }
 }
 
 template <int U>
@@ -307,7 +336,7 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ save, const float* __restrict__ w, const float* __restrict__ b,
     const float* __restrict__ acc, BnGeom g, int relu, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, float* __restrict__ dw, float* __restrict__ db,
-    const uint8_t* __restrict__ mbits) {
+    const uint8_t* __restrict__ mbits, const ResBnBwd rb) {
   const int t = threadIdx.x, cv = t % g.CVB, r = t / g.CVB;
   const int c0 = blockIdx.y * g.CVB * 8;
   const int c = c0 + cv * 8;
@@ -322,17 +351,33 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
     mg[k] = acc[c + k] * invM;
     mgx[k] = acc[g.C + c + k] * invM;
   }
+  // the residual BN's coefficients (ResBnBwd): dres <- its input gradient
+  const bool fr = rb.x != nullptr;
+  float rmean[8], rinv[8], ra[8], rmg[8], rmgx[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    rmean[k] = fr ? rb.save[c + k] : 0.f;
+    rinv[k] = fr ? rb.save[g.C + c + k] : 0.f;
+    ra[k] = fr ? rb.w[c + k] * rinv[k] : 0.f;
+    rmg[k] = fr ? rb.acc[c + k] * invM : 0.f;
+    rmgx[k] = fr ? rb.acc[g.C + c + k] * invM : 0.f;
+  }
   if (blockIdx.x == 0 && r == 0) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       db[c + k] = acc[c + k];
       dw[c + k] = acc[g.C + c + k];
+      if (fr) {
+        rb.db[c + k] = rb.acc[c + k];
+        rb.dw[c + k] = rb.acc[g.C + c + k];
+      }
     }
   }
   const int64_t row0 = (int64_t)blockIdx.x * g.rows_per_block;
   const int64_t row1 = min(g.M, row0 + g.rows_per_block);
   const u32x4 z = {0u, 0u, 0u, 0u};
-  auto apply = [&](int64_t off, int64_t doff, const u32x4& xr, const u32x4& dr, const u32x4& yr, unsigned mb) {
+  auto apply = [&](int64_t off, int64_t doff, const u32x4& xr, const u32x4& dr, const u32x4& yr, unsigned mb,
+                   const u32x4& rr) {
     float gv[8], xv[8], o[8];
     unpack8(xr, xv);
     unpack8(dr, gv);
@@ -354,11 +399,22 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
       o[k] = a[k] * (gv[k] - mg[k] - xh * mgx[k]);
     }
     *(u32x4*)(dx + doff) = pack8(o);
-    if (dres != nullptr) *(u32x4*)(dres + off) = pack8(gv);
+    if (fr) {  // the residual BN's input gradient in place of g
+      float xrv[8], orr[8];
+      unpack8(rr, xrv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float xh = (xrv[k] - rmean[k]) * rinv[k];
+        orr[k] = ra[k] * (gv[k] - rmg[k] - xh * rmgx[k]);
+      }
+      *(u32x4*)(dres + off) = pack8(orr);
+    } else if (dres != nullptr) {
+      *(u32x4*)(dres + off) = pack8(gv);
+    }
   };
   int64_t row = row0 + r;
   for (; row + (U - 1) * g.RPI < row1; row += U * g.RPI) {  // U rows' loads in flight
-    u32x4 xv[U], dv[U], yv[U];
+    u32x4 xv[U], dv[U], yv[U], rv[U];
     unsigned mb[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -367,15 +423,17 @@ __global__ void __launch_bounds__(kThreads) bn_nhwc_bwd_apply_kernel(
       dv[u] = *(const u32x4*)(dy + o);
       yv[u] = relu == 1 ? *(const u32x4*)(y + o) : z;
       mb[u] = relu == 3 ? mbits[(row + u * g.RPI) * (g.C >> 3) + (c >> 3)] : 0u;
+      rv[u] = fr ? *(const u32x4*)(rb.x + o) : z;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      apply((row + u * g.RPI) * g.C + c, out_row(g, row + u * g.RPI) * g.C + c, xv[u], dv[u], yv[u], mb[u]);
+      apply((row + u * g.RPI) * g.C + c, out_row(g, row + u * g.RPI) * g.C + c, xv[u], dv[u], yv[u], mb[u], rv[u]);
   }
   for (; row < row1; row += g.RPI) {
     const int64_t o0 = row * g.C + c;
     apply(o0, out_row(g, row) * g.C + c, *(const u32x4*)(x + o0), *(const u32x4*)(dy + o0),
-          relu == 1 ? *(const u32x4*)(y + o0) : z, relu == 3 ? mbits[row * (g.C >> 3) + (c >> 3)] : 0u);
+          relu == 1 ? *(const u32x4*)(y + o0) : z, relu == 3 ? mbits[row * (g.C >> 3) + (c >> 3)] : 0u,
+          fr ? *(const u32x4*)(rb.x + o0) : z);
   }
 }
 
@@ -541,11 +599,19 @@ void bn_nhwc_fwd(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr
 }
 
 // y in the padded layout [N][H+2opad][W+2opad][C] (interior only; see zero_border_nhwc)
+// rbn_acc != 0: `res` is the input of the residual branch's BatchNorm, applied
+// on load (ResBn: rbn_acc = its [2C] sums, complete; rbn_w / rbn_b its affine
+// parameters; rbn_save / rbn_rm / rbn_rv what its own apply would write)
 void bn_nhwc_fwd_pad(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b,
                      uintptr_t save, uintptr_t run_mean, uintptr_t run_var, int64_t M, int C, double eps,
                      double momentum, int relu, int have_stats, int H, int W, int opad, uintptr_t stream,
-                     uintptr_t mbits) {
+                     uintptr_t mbits, uintptr_t rbn_acc, uintptr_t rbn_w, uintptr_t rbn_b, uintptr_t rbn_save,
+                     uintptr_t rbn_rm, uintptr_t rbn_rv, double rbn_eps, double rbn_momentum) {
   if (mbits && !relu) throw std::runtime_error("bn_nhwc_fwd: mask bits need the ReLU");
+  if (rbn_acc && (!res || !rbn_w || !rbn_b || !rbn_save))
+    throw std::runtime_error("bn_nhwc_fwd: the residual BN needs its input, affine parameters and save buffer");
+  const ResBn rbn{(const float*)rbn_acc, (const float*)rbn_w, (const float*)rbn_b, (float*)rbn_save,
+                  (float*)rbn_rm, (float*)rbn_rv, (float)rbn_eps, (float)rbn_momentum};
   dim3 grid, grid_r;
   BnGeom g = make_geom(M, C, &grid);
   set_out_pad(g, H, W, opad);
@@ -564,7 +630,7 @@ void bn_nhwc_fwd_pad(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uin
   auto fk = g_apply_rows == 4 ? bn_nhwc_fwd_apply_kernel<4> : bn_nhwc_fwd_apply_kernel<2>;
   fk<<<grid, kThreads, 0, s>>>((const bf16_t*)x, (const bf16_t*)res, (bf16_t*)y, (const float*)acc,
                                (const float*)w, (const float*)b, g, (float)eps, relu, (float*)save,
-                               (float*)run_mean, (float*)run_var, (float)momentum, (uint8_t*)mbits);
+                               (float*)run_mean, (float*)run_var, (float)momentum, (uint8_t*)mbits, rbn);
   DL_HIP_CHECK(hipGetLastError());
 }
 
@@ -573,18 +639,27 @@ void bn_nhwc_fwd_pad(uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t acc, uin
 void bn_nhwc_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, uintptr_t acc,
                  uintptr_t dx,
                  uintptr_t dres, uintptr_t dw, uintptr_t db, int64_t M, int C, int relu, uintptr_t stream) {
-  bn_nhwc_bwd_pad(dy, y, x, save, w, b, acc, dx, dres, dw, db, M, C, relu, 1, 1, 0, stream, 0, 0);
+  bn_nhwc_bwd_pad(dy, y, x, save, w, b, acc, dx, dres, dw, db, M, C, relu, 1, 1, 0, stream, 0, 0, 0, 0, 0, 0, 0, 0);
 }
 
 // dx in the padded layout [N][H+2opad][W+2opad][C] (interior only).
 // have_sums: acc already holds sum(g), sum(g*xhat) -- computed by the epilogue
 // of the convolution that produced dy (conv_igemm.hip set_conv_bn_reduce,
 // ops/conv.py): the reduce pass over dy and x is skipped.
+// rbn_x != 0: dres receives the input gradient of the residual branch's
+// BatchNorm (ResBnBwd: its input rbn_x, saved mean / invstd, gamma, zeroed
+// [2C] backward sums and dgamma / dbeta outputs) instead of g.
 void bn_nhwc_bwd_pad(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b,
                      uintptr_t acc, uintptr_t dx, uintptr_t dres, uintptr_t dw, uintptr_t db, int64_t M, int C,
-                     int relu, int H, int W, int opad, uintptr_t stream, int have_sums, uintptr_t mbits) {
+                     int relu, int H, int W, int opad, uintptr_t stream, int have_sums, uintptr_t mbits,
+                     uintptr_t rbn_x, uintptr_t rbn_save, uintptr_t rbn_w, uintptr_t rbn_acc, uintptr_t rbn_dw,
+                     uintptr_t rbn_db) {
   if ((relu == 3) != (mbits != 0)) throw std::runtime_error("bn_nhwc_bwd: relu mode 3 reads the forward's mask bits");
   if (relu == 1 && !y) throw std::runtime_error("bn_nhwc_bwd: relu mode 1 reads y");
+  if (rbn_x && (have_sums || !dres || !rbn_save || !rbn_w || !rbn_acc || !rbn_dw || !rbn_db))
+    throw std::runtime_error("bn_nhwc_bwd: the fused residual BN needs this reduce pass, dres and all its operands");
+  const ResBnBwd rb{(const bf16_t*)rbn_x, (const float*)rbn_save, (const float*)rbn_w, (float*)rbn_acc,
+                    (float*)rbn_dw, (float*)rbn_db};
   dim3 grid, grid_r;
   BnGeom g = make_geom(M, C, &grid);
   set_out_pad(g, H, W, opad);
@@ -595,13 +670,13 @@ void bn_nhwc_bwd_pad(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save, uin
     auto rk = nt == 1024 ? bn_nhwc_bwd_reduce_kernel<1024>
               : nt == 512 ? bn_nhwc_bwd_reduce_kernel<512> : bn_nhwc_bwd_reduce_kernel<256>;
     rk<<<grid_r, nt, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, (const float*)save,
-                             (const float*)w, (const float*)b, gr, relu, (float*)acc, (const uint8_t*)mbits);
+                             (const float*)w, (const float*)b, gr, relu, (float*)acc, (const uint8_t*)mbits, rb);
     DL_HIP_CHECK(hipGetLastError());
   }
   auto ak = g_apply_rows == 4 ? bn_nhwc_bwd_apply_kernel<4> : bn_nhwc_bwd_apply_kernel<2>;
   ak<<<grid, kThreads, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, (const float*)save,
                                (const float*)w, (const float*)b, (const float*)acc, g, relu, (bf16_t*)dx,
-                               (bf16_t*)dres, (float*)dw, (float*)db, (const uint8_t*)mbits);
+                               (bf16_t*)dres, (float*)dw, (float*)db, (const uint8_t*)mbits, rb);
   DL_HIP_CHECK(hipGetLastError());
 }
 

@@ -989,7 +989,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
     const float invM = 1.f / (float)ol.M;
     for (int c = tid; c < ol.C; c += 64 * NW) {
       const float m = ol.acc[c] * invM;
-      const float var = fmaxf(ol.acc[ol.C + c] * invM - m * m, 0.f);
+      const float var = fmaxf(fmaf(-m, m, ol.acc[ol.C + c] * invM), 0.f);  // (as bn_nhwc.hip var_of)
       const float is = rsqrtf(var + ol.eps);
       const float sc = ol.w[c] * is;
       olt[c] = sc;
@@ -999,8 +999,10 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
         ol.save[ol.C + c] = is;
         if (ol.rmean != nullptr) {
           const float unbias = ol.M > 1 ? (float)ol.M / (float)(ol.M - 1) : 1.f;
-          ol.rmean[c] = (1.f - ol.momentum) * ol.rmean[c] + ol.momentum * m;
-          ol.rvar[c] = (1.f - ol.momentum) * ol.rvar[c] + ol.momentum * var * unbias;
+          // (explicit fmas, as bn_nhwc.hip bn_coef8)
+          const float keep_m = (1.f - ol.momentum) * ol.rmean[c], keep_v = (1.f - ol.momentum) * ol.rvar[c];
+          ol.rmean[c] = fmaf(ol.momentum, m, keep_m);
+          ol.rvar[c] = fmaf(ol.momentum, var * unbias, keep_v);
         }
       }
     }

@@ -6,6 +6,7 @@
 // took 0.62 ms per ResNet-50 step (profiles/r2_resnet50_hip1x1_kernels.txt).
 // Ties resolve to the first maximum in row-major window order (torch's rule).
 #include "dl_common.h"
+#include "bn_coef_dev.h"
 #include "dl_ops.h"
 
 namespace dl {
@@ -106,10 +107,35 @@ __global__ void __launch_bounds__(256) maxpool_nhwc_bwd_kernel(const bf16_t* __r
 // run a dependent load chain per window position with 64-bit divisions and
 // measured 154 us (forward) / 256 us (backward) per batch-256 step, about
 // 3.7 / 2.2 TB/s.  Out-of-image taps load a valid pixel and are masked.
+// The training BatchNorm + ReLU that produced the pooled tensor, applied on
+// load (PoolBn; the ResNet-50 stem BN): x is then the BN's INPUT, each window
+// element is bf16(relu(x * sc + sh)) -- bitwise what the BN's own apply would
+// have stored -- and the threads of workgroup 0 publish its saved mean /
+// invstd and running statistics: the BN's apply launch and the write + read of
+// its 112x112 output go.
+struct PoolBn {
+  const float* acc;  // [2C] sum, sum of squares of the BN input (null: plain pooling)
+  const float* w;
+  const float* b;
+  float* save;
+  float* run_mean;
+  float* run_var;
+  float eps, momentum;
+};
+
 __global__ void __launch_bounds__(256) maxpool3s2_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
-                                                             uint8_t* __restrict__ idx, const PoolGeom g) {
+                                                             uint8_t* __restrict__ idx, const PoolGeom g,
+                                                             const PoolBn pb) {
   const int C8 = g.C >> 3;
   const int total = g.N * g.Ho * g.Wo * C8;
+  // (the grid stride is a multiple of C8: a thread keeps its 8 channels)
+  float sc[8], sh[8];
+  const bool bn = pb.acc != nullptr;
+  if (bn) {
+    const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    bn_coef8(pb.acc, pb.w, pb.b, g.C, (i0 % C8) * 8, (int64_t)g.N * g.H * g.W, pb.eps, pb.momentum,
+             blockIdx.x == 0 && (int)threadIdx.x < C8, pb.save, pb.run_mean, pb.run_var, sc, sh);
+  }
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int c8 = i % C8, pix = i / C8;
     const int ow = pix % g.Wo, t = pix / g.Wo;
@@ -135,6 +161,10 @@ __global__ void __launch_bounds__(256) maxpool3s2_fwd_kernel(const bf16_t* __res
       if (!ok[p]) continue;
       float f[8];
       unpack8p(v[p], f);
+      if (bn) {  // the stored BN + ReLU output (bf16), as the apply would write it
+#pragma unroll
+        for (int k = 0; k < 8; ++k) f[k] = __uint_as_float((uint32_t)f32_to_bf16(fmaxf(fmaf(f[k], sc[k], sh[k]), 0.f)) << 16);
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k)
         if (f[k] > best[k]) { best[k] = f[k]; arg[k] = (uint8_t)p; }
@@ -201,13 +231,22 @@ PoolGeom pool_geom(int N, int H, int W, int C, int K, int S, int P) {
 
 }  // namespace
 
+// bn_acc != 0: x is the input of a training BatchNorm + ReLU applied on load
+// (PoolBn: its complete [2C] sums, gamma / beta, and the save / running
+// statistics its own apply would write); 3x3 / stride 2 / pad 1 only.
 void maxpool_nhwc_fwd(uintptr_t x, uintptr_t y, uintptr_t idx, int N, int H, int W, int C, int K, int S, int P,
-                      uintptr_t stream) {
+                      uintptr_t stream, uintptr_t bn_acc, uintptr_t bn_w, uintptr_t bn_b, uintptr_t bn_save,
+                      uintptr_t bn_rm, uintptr_t bn_rv, double bn_eps, double bn_momentum) {
   const PoolGeom g = pool_geom(N, H, W, C, K, S, P);
   const int64_t total = (int64_t)N * g.Ho * g.Wo * (C / 8);
-  if (stem_window(g, (int64_t)N * H * W * (C / 8)))
+  const bool stem = stem_window(g, (int64_t)N * H * W * (C / 8));
+  if (bn_acc && (!stem || !bn_w || !bn_b || !bn_save || 256 % (C / 8) != 0))
+    throw std::runtime_error("maxpool_nhwc_fwd: BN on load needs the 3x3/2 window, its parameters and C/8 | 256");
+  const PoolBn pb{(const float*)bn_acc, (const float*)bn_w, (const float*)bn_b, (float*)bn_save, (float*)bn_rm,
+                  (float*)bn_rv, (float)bn_eps, (float)bn_momentum};
+  if (stem)
     maxpool3s2_fwd_kernel<<<(int)std::min<int64_t>((total + 255) / 256, 8192), 256, 0, as_stream(stream)>>>(
-        (const bf16_t*)x, (bf16_t*)y, (uint8_t*)idx, g);
+        (const bf16_t*)x, (bf16_t*)y, (uint8_t*)idx, g, pb);
   else
     maxpool_nhwc_fwd_kernel<<<stream_grid(total), 256, 0, as_stream(stream)>>>((const bf16_t*)x, (bf16_t*)y,
                                                                                 (uint8_t*)idx, g);

@@ -249,3 +249,141 @@ def test_c1_backward_first_hand_over(dev, branch):
     first, link = run(True)
     assert link.get("done")
     assert _rel(first, joint) < 1e-2
+
+
+@pytest.mark.parametrize("N,C,H", [(4, 256, 14), (2, 512, 7)])
+def test_deferred_residual_bn_apply(dev, N, C, H):
+    """The downsample branch's BN (no ReLU) deferred into the BN + residual +
+    ReLU that consumes it (bn_act defer_apply; csrc bn_nhwc.hip ResBn) and its
+    backward fused into that BN's backward (ResBnBwd: the residual BN's sums
+    ride the reduce pass, its input gradient is written where g was): the
+    block output and the running statistics are BITWISE those of the path that
+    runs the downsample BN on its own (statistics given), every gradient equal
+    to the noise of the backward sums' fp32 atomics, and materialize() runs
+    the deferred apply for another consumer."""
+    from torch_distlearn_amd.ops.bn_nhwc import bn_act, materialize
+
+    def run(defer):
+        g = torch.Generator(device=dev).manual_seed(17)
+        mk = lambda *s: torch.randn(*s, device=dev, generator=g).to(BF).contiguous(memory_format=CL)  # noqa: E731
+        y3, yd = mk(N, C, H, H).requires_grad_(True), mk(N, C, H, H).requires_grad_(True)
+        p = [(torch.rand(C, device=dev, generator=g) + 0.5).requires_grad_(True) for _ in range(2)]
+        q = [(torch.randn(C, device=dev, generator=g) * 0.3).requires_grad_(True) for _ in range(2)]
+        rs = [(torch.zeros(C, device=dev), torch.ones(C, device=dev)) for _ in range(2)]
+
+        def acc_of(t):
+            tf = t.detach().float().permute(0, 2, 3, 1).reshape(-1, C)
+            return torch.cat([tf.sum(0), (tf * tf).sum(0), torch.zeros(2 * C, device=dev)])
+
+        s = bn_act(yd, p[1], q[1], *rs[1], relu=False, acc=acc_of(yd), have_stats=True, defer_apply=defer)
+        if defer:
+            assert getattr(s, "_dl_res_bn", None) is not None
+        z = bn_act(y3, p[0], q[0], *rs[0], residual=s, relu=True, acc=acc_of(y3), have_stats=True)
+        go = mk(N, C, H, H)
+        z.backward(go)
+        torch.cuda.synchronize()
+        return [z, y3.grad, yd.grad, p[0].grad, p[1].grad, q[0].grad, q[1].grad, *rs[0], *rs[1]]
+
+    a, b = run(False), run(True)
+    for i in (0, 7, 8, 9, 10):  # output, running statistics
+        assert torch.equal(a[i], b[i]), i
+    for i in range(1, 7):  # input and parameter gradients
+        assert _rel(b[i], a[i]) < 1e-3, (i, _rel(b[i], a[i]))
+    # materialize(): the deferred output written as the plain apply writes it
+    g = torch.Generator(device=dev).manual_seed(3)
+    yd = torch.randn(N, C, H, H, device=dev, generator=g).to(BF).contiguous(memory_format=CL)
+    w, bb = torch.rand(C, device=dev, generator=g) + 0.5, torch.randn(C, device=dev, generator=g)
+    tf = yd.float().permute(0, 2, 3, 1).reshape(-1, C)
+    acc = torch.cat([tf.sum(0), (tf * tf).sum(0), torch.zeros(2 * C, device=dev)])
+    with torch.no_grad():
+        ref = bn_act(yd, w, bb, None, None, relu=False, acc=acc.clone(), have_stats=True)
+        d = bn_act(yd, w, bb, None, None, relu=False, acc=acc.clone(), have_stats=True, defer_apply=True)
+        materialize(d)
+    torch.cuda.synchronize()
+    assert torch.equal(ref, d)
+
+
+def test_resnet50_step_deferred_down_bn(dev, monkeypatch):
+    """The whole ResNet-50 step with the downsample BNs applied on load by the
+    blocks' b3 against the separate apply: same loss and gradients (to the
+    run-to-run noise of the fp32 statistics atomics)."""
+    from torch_distlearn_amd import FlatParams
+    from torch_distlearn_amd.models import ResNet50
+    from torch_distlearn_amd.models import resnet as R
+
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(16, 3, 64, 64, device=dev, generator=g).to(BF).contiguous(memory_format=CL)
+    y = torch.randint(0, 1000, (16,), device=dev, generator=g)
+    out = []
+    for on in (False, True):
+        monkeypatch.setattr(R, "_DEFER_DOWN_BN", on)
+        model = ResNet50(num_classes=1000, seed=0).to(dev)
+        flat = FlatParams(model, grads=True, shadow_bf16=True)
+        model.attach_flat(flat)
+        flat.grad.zero_()
+        loss, _ = model.forward_loss(x, y, BF)
+        loss.backward()
+        torch.cuda.synchronize()
+        rm = torch.cat([blk.down[1].running_mean for blk in model.blocks if blk.down is not None])
+        out.append((float(loss), flat.grad.clone(), rm))
+    assert abs(out[0][0] - out[1][0]) < 1e-6
+    assert _rel(out[1][1], out[0][1]) < 2e-2
+    assert _rel(out[1][2], out[0][2]) < 1e-5
+
+
+@pytest.mark.parametrize("N,C,H", [(4, 64, 56), (2, 64, 112)])
+def test_stem_pool_applies_bn_on_load(dev, N, C, H):
+    """The stem BN + ReLU applied by the 3x3/2 max-pool on load (bn_act
+    defer_pool; csrc pool_nhwc.hip PoolBn): pooled output, argmax choice and
+    the BN's running statistics BITWISE those of the BN apply + pool path,
+    gradients to the noise of the backward sums' fp32 atomics."""
+    from torch_distlearn_amd.ops.bn_nhwc import bn_act
+    from torch_distlearn_amd.ops.pool import max_pool2d_nhwc
+
+    def run(defer):
+        g = torch.Generator(device=dev).manual_seed(23)
+        x = torch.randn(N, C, H, H, device=dev, generator=g).to(BF).contiguous(memory_format=CL).requires_grad_(True)
+        w = (torch.rand(C, device=dev, generator=g) + 0.5).requires_grad_(True)
+        b = (torch.randn(C, device=dev, generator=g) * 0.3).requires_grad_(True)
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        tf = x.detach().float().permute(0, 2, 3, 1).reshape(-1, C)
+        acc = torch.cat([tf.sum(0), (tf * tf).sum(0), torch.zeros(2 * C, device=dev)])
+        z = bn_act(x, w, b, rm, rv, relu=True, acc=acc, have_stats=True, defer_pool=defer)
+        assert (getattr(z, "_dl_pool_bn", None) is not None) == defer
+        p = max_pool2d_nhwc(z, 3, 2, 1)
+        go = torch.randn(p.shape, device=dev, generator=g).to(BF).contiguous(memory_format=CL)
+        p.backward(go)
+        torch.cuda.synchronize()
+        return [p, rm, rv], [x.grad, w.grad, b.grad]
+
+    (ea, ga), (eb, gb) = run(False), run(True)
+    for u, v in zip(ea, eb):
+        assert torch.equal(u, v)
+    for u, v in zip(ga, gb):
+        assert _rel(v, u) < 1e-3
+
+
+def test_resnet50_step_deferred_stem_bn(dev, monkeypatch):
+    """The whole ResNet-50 step with the stem BN applied by the max-pool on load
+    against the separate apply: same loss, gradients to atomics noise."""
+    from torch_distlearn_amd import FlatParams
+    from torch_distlearn_amd.models import ResNet50
+    from torch_distlearn_amd.models import resnet as R
+
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(16, 3, 64, 64, device=dev, generator=g).to(BF).contiguous(memory_format=CL)
+    y = torch.randint(0, 1000, (16,), device=dev, generator=g)
+    out = []
+    for on in (False, True):
+        monkeypatch.setattr(R, "_DEFER_STEM_BN", on)
+        model = ResNet50(num_classes=1000, seed=0).to(dev)
+        flat = FlatParams(model, grads=True, shadow_bf16=True)
+        model.attach_flat(flat)
+        flat.grad.zero_()
+        loss, _ = model.forward_loss(x, y, BF)
+        loss.backward()
+        torch.cuda.synchronize()
+        out.append((float(loss), flat.grad.clone(), model.stem_bn.running_var.clone()))
+    assert abs(out[0][0] - out[1][0]) < 1e-6
+    assert _rel(out[1][1], out[0][1]) < 2e-2
+    assert torch.equal(out[1][2], out[0][2])

@@ -74,11 +74,18 @@ class _BN(nn.Module):
             residual is None or (residual.dtype == x.dtype and residual.shape == x.shape))
 
     def act(self, x, relu: bool = True, residual=None, acc=None, res_sink=None, have_stats: bool = False,
-            out_pad: int = 0, dx_pad: int = 0, bn_link=None, on_load: bool = False):
+            out_pad: int = 0, dx_pad: int = 0, bn_link=None, on_load: bool = False, defer: bool = False,
+            defer_pool: bool = False):
         """act(BN(x) [+ residual]); one fused HIP kernel pair in "hip" mode
         (``acc`` with ``have_stats``: statistics already accumulated by the
         producing conv; else the step's zeroed arena slice, if any;
-        ``out_pad`` / ``dx_pad``: zero-bordered output / input gradient)."""
+        ``out_pad`` / ``dx_pad``: zero-bordered output / input gradient;
+        ``defer``: no ReLU / residual -- the output is a handle the consuming
+        BN + residual + ReLU applies on load, ops/bn_nhwc.py defer_apply)."""
+        if residual is not None and getattr(residual, "_dl_res_bn", None) is not None and not self.hip_ok(x, residual):
+            from ..ops.bn_nhwc import materialize
+
+            materialize(residual)  # this BN cannot apply the deferred residual BN on load
         if self.hip_eval_ok(x, residual):  # eval / predict: the same HIP kernel from the running statistics
             from ..ops.bn_nhwc import bn_act_eval
 
@@ -91,7 +98,10 @@ class _BN(nn.Module):
                 acc, have_stats = self.acc, False
             return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual, relu, acc=acc,
                           grads=self.bind, res_sink=res_sink, have_stats=have_stats if acc is not None else None,
-                          out_pad=out_pad, dx_pad=dx_pad, bn_link=bn_link, on_load=on_load)
+                          out_pad=out_pad, dx_pad=dx_pad, bn_link=bn_link, on_load=on_load,
+                          defer_apply=defer and not relu and residual is None and have_stats and acc is not None,
+                          defer_pool=defer_pool and relu and residual is None and have_stats and acc is not None
+                          and not out_pad)
         y = self(x)
         if residual is not None:
             y = y + residual
@@ -144,6 +154,14 @@ _BN_DGRAD = os.environ.get("DISTLEARN_RESNET_BN_DGRAD", "0") == "1"
 # GEMM cost more than the apply pass they replace
 # (profiles/r4_resnet_bn_on_load_ab.txt).
 _BN_ON_LOAD = os.environ.get("DISTLEARN_RESNET_BN_ON_LOAD", "0") == "1"
+# the downsample branch's BatchNorm applied on load by the block's b3 apply (csrc
+# bn_nhwc.hip ResBn): b3 reads the downsample conv's output and applies that BN
+# itself, so the downsample BN's apply launch and the write + read of its output
+# go (4 per step, ~0.28 ms at batch 256)
+_DEFER_DOWN_BN = os.environ.get("DISTLEARN_RESNET_DEFER_DOWN_BN", "1") == "1"
+# the stem BatchNorm + ReLU applied on load by the stem max-pool (csrc pool_nhwc.hip
+# PoolBn): the apply launch and the write + read of its 112x112x64 output go
+_DEFER_STEM_BN = os.environ.get("DISTLEARN_RESNET_DEFER_STEM_BN", "1") == "1"
 
 
 class _Conv(nn.Module):
@@ -229,7 +247,8 @@ class _Conv(nn.Module):
 
 
 def _conv_bn(conv: _Conv, bn: "_BN", x, relu: bool = True, residual=None, link=None, res_sink=None, dx_sink=None,
-             out_pad: int = 0, dx_pad: int = 0, in_link=None, out_link=None, into: Optional[_Conv] = None):
+             out_pad: int = 0, dx_pad: int = 0, in_link=None, out_link=None, into: Optional[_Conv] = None,
+             defer: bool = False, defer_pool: bool = False):
     """bn.act(conv(x)) with the BatchNorm statistics produced by the conv's
     epilogue when both run on the HIP kernels (one full read of the conv
     output fewer per BatchNorm).  ``out_pad`` / ``dx_pad``: the BatchNorm writes
@@ -252,7 +271,8 @@ def _conv_bn(conv: _Conv, bn: "_BN", x, relu: bool = True, residual=None, link=N
             if bn.hip_ok(y, residual):
                 ol = (_BN_ON_LOAD and into is not None and relu and residual is None and not out_pad
                       and out_link is None and into.hip_gemm(y))
-                return bn.act(y, relu, residual, acc=acc, res_sink=res_sink, have_stats=True, on_load=ol, **pads)
+                return bn.act(y, relu, residual, acc=acc, res_sink=res_sink, have_stats=True, on_load=ol, defer=defer,
+                              defer_pool=defer_pool, **pads)
             return bn.act(y, relu, residual)
     return bn.act(conv(x, **kw), relu, residual, res_sink=res_sink, **pads)
 
@@ -296,7 +316,8 @@ class _Bottleneck(nn.Module):
         y = _conv_bn(self.c2, self.b2, y, dx_pad=pad, in_link=l1, out_link=l2, into=self.c3)
         if self.down is None:
             return _conv_bn(self.c3, self.b3, y, residual=x, res_sink=link, in_link=l2, out_link=l3), l3
-        s = _conv_bn(self.down[0], self.down[1], x, relu=False, dx_sink=link)
+        # (the downsample BN's apply deferred into b3's: csrc ResBn)
+        s = _conv_bn(self.down[0], self.down[1], x, relu=False, dx_sink=link, defer=_DEFER_DOWN_BN)
         return _conv_bn(self.c3, self.b3, y, residual=s, in_link=l2, out_link=l3), l3
 
 
@@ -325,10 +346,12 @@ class ResNet50(nn.Module):
         if h.is_cuda:
             h = h.contiguous(memory_format=torch.channels_last)
         self._begin_step(h)
-        h = _conv_bn(self.stem, self.stem_bn, h)
+        # (with the HIP pool, the stem BN + ReLU is applied by the pool on load: PoolBn)
+        h = _conv_bn(self.stem, self.stem_bn, h, defer_pool=_POOL_HIP and _DEFER_STEM_BN)
+        from ..ops.bn_nhwc import materialize
         from ..ops.pool import max_pool2d_nhwc, supported
 
-        h = max_pool2d_nhwc(h, 3, 2, 1) if (_POOL_HIP and supported(h)) else F.max_pool2d(h, 3, 2, 1)
+        h = max_pool2d_nhwc(h, 3, 2, 1) if (_POOL_HIP and supported(h)) else F.max_pool2d(materialize(h), 3, 2, 1)
         link = None
         for b in self.blocks:
             h, link = b.forward_linked(h, link)

@@ -75,10 +75,21 @@ def supported(x: torch.Tensor) -> bool:
             and x.is_contiguous(memory_format=torch.channels_last))
 
 
+def materialize(t: torch.Tensor) -> torch.Tensor:
+    """Run the deferred apply of a BatchNorm output made with ``defer_apply``
+    or ``defer_pool`` (for a consumer that cannot apply it on load); returns ``t``."""
+    for key in ("_dl_res_bn", "_dl_pool_bn"):
+        args = getattr(t, key, None)
+        if args is not None:
+            delattr(t, key)
+            _bn().bn_nhwc_fwd_pad(*args[0], stream_handle(), 0)
+    return t
+
+
 class _BnAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, relu, eps, momentum, acc, grads, res_sink,
-                have_stats, out_pad, dx_pad, bn_link, on_load=False):
+                have_stats, out_pad, dx_pad, bn_link, on_load=False, defer_apply=False, defer_pool=False):
         M, C = _geom(x)
         N, _, H, W = x.shape
         if out_pad:
@@ -95,7 +106,14 @@ class _BnAct(torch.autograd.Function):
             have_stats = False
         ctx.backwards = 0
         save = torch.empty(2 * C, device=x.device, dtype=torch.float32)
-        res = residual.contiguous(memory_format=torch.channels_last) if residual is not None else None
+        # a residual that is a deferred BatchNorm output (the downsample branch's BN,
+        # defer_apply): this apply reads that BN's input and applies it on load
+        rbn = getattr(residual, "_dl_res_bn", None) if residual is not None else None
+        if rbn is not None:
+            del residual._dl_res_bn
+            res = rbn[1][0]
+        else:
+            res = residual.contiguous(memory_format=torch.channels_last) if residual is not None else None
         # (with out_pad the kernel writes y's padded buffer: its origin is y.data_ptr()
         # minus the interior offset)
         ybase = y.data_ptr() - (out_pad * (W + 2 * out_pad) + out_pad) * C * 2 if out_pad else y.data_ptr()
@@ -117,9 +135,35 @@ class _BnAct(torch.autograd.Function):
             # it applies this BN + ReLU to its A operand on load and writes y, or
             # runs this apply first when its tile has no on-load instance
             y._dl_bn_on_load = apply
+        elif defer_pool and relu and residual is None and have_stats and not out_pad and mbits is None:
+            # y feeds the stem max-pool, which applies this BN + ReLU on load (csrc
+            # pool_nhwc.hip PoolBn); the backward needs neither y nor its mask (relu 2)
+            y._dl_pool_bn = (apply, (x, acc, weight, bias, save, running_mean, running_var, eps, momentum))
+        elif defer_apply and not relu and residual is None and have_stats and not out_pad:
+            # y is the residual of a BN + residual + ReLU whose apply applies this BN
+            # on load (its kernel publishes save and the running statistics); y stays
+            # unwritten unless a consumer calls materialize()
+            y._dl_res_bn = (apply, (x, acc, weight, bias, save, running_mean, running_var, eps, momentum))
         else:
-            _bn().bn_nhwc_fwd_pad(*apply, stream_handle(), mbits.data_ptr() if mbits is not None else 0)
+            rargs = {}
+            if rbn is not None:
+                _, racc, rw, rb, rsave, rrm, rrv, reps, rmom = rbn[1]
+                rargs = dict(rbn_acc=racc.data_ptr(), rbn_w=rw.data_ptr(), rbn_b=rb.data_ptr(),
+                             rbn_save=rsave.data_ptr(), rbn_rm=rrm.data_ptr() if rrm is not None else 0,
+                             rbn_rv=rrv.data_ptr() if rrv is not None else 0, rbn_eps=float(reps),
+                             rbn_momentum=float(rmom))
+            _bn().bn_nhwc_fwd_pad(*apply, stream_handle(), mbits.data_ptr() if mbits is not None else 0, **rargs)
         ctx.has_res = residual is not None
+        # the residual branch's BN backward fused into this backward (csrc ResBnBwd):
+        # a BN + residual + ReLU takes it over from a defer_apply BN that made its residual
+        ctx.rbn_bwd = None
+        if residual is not None and getattr(residual, "_dl_res_bwd", None) is not None:
+            ctx.rbn_bwd = residual._dl_res_bwd
+            del residual._dl_res_bwd
+        ctx.own_link = None
+        if defer_apply and not relu and residual is None and not out_pad:
+            ctx.own_link = {"fwd": (x, save, weight, acc, grads)}
+            y._dl_res_bwd = ctx.own_link
         ctx.grads = grads
         ctx.res_sink = res_sink
         if res_sink is not None and residual is not None:
@@ -142,6 +186,16 @@ class _BnAct(torch.autograd.Function):
     def backward(ctx, dy):
         x, y, weight, bias, save, acc4 = ctx.saved_tensors
         M, C = _geom(x)
+        if ctx.own_link is not None and ctx.own_link.pop("fused", None):
+            # the consuming BN + residual + ReLU's backward already computed this BN's
+            # input gradient (it arrives as dy) and its dgamma / dbeta
+            dw, db = ctx.own_link.pop("dwdb")
+            if ctx.grads is not None:
+                ctx.grads[2]()
+                return (dy, None, None, None, None, None, None, None, None, None, None, None, None, None, None, None,
+                        None, None, None)
+            return (dy, dw.to(weight.dtype), db.to(weight.dtype), None, None, None, None, None, None, None, None, None,
+                    None, None, None, None, None, None, None)
         dy = dy.contiguous(memory_format=torch.channels_last)
         N, _, H, W = x.shape
         p = ctx.dx_pad
@@ -167,11 +221,29 @@ class _BnAct(torch.autograd.Function):
             db = torch.empty(C, device=x.device, dtype=torch.float32)
         ym = y if ctx.relu == 1 else None      # (the saved slot holds the mask bits in relu mode 3)
         mb = y if ctx.relu == 3 else None
+        rargs = {}
+        rl = ctx.rbn_bwd
+        if rl is not None and dres is not None and not have_sums and "fwd" in rl:
+            # dres <- the residual BN's input gradient (its reduce sums ride our reduce pass)
+            rx, rsave, rw, racc4, rgrads = rl["fwd"]
+            rC = rx.shape[1]
+            racc = racc4[2 * rC:]
+            if ctx.backwards > 1:
+                racc.zero_()
+            if rgrads is not None:
+                rdw, rdb = rgrads[0], rgrads[1]
+            else:
+                rdw = torch.empty(rC, device=x.device, dtype=torch.float32)
+                rdb = torch.empty(rC, device=x.device, dtype=torch.float32)
+            rargs = dict(rbn_x=rx.data_ptr(), rbn_save=rsave.data_ptr(), rbn_w=rw.data_ptr(), rbn_acc=racc.data_ptr(),
+                         rbn_dw=rdw.data_ptr(), rbn_db=rdb.data_ptr())
+            rl["fused"] = True
+            rl["dwdb"] = (rdw, rdb)
         _bn().bn_nhwc_bwd_pad(dy.data_ptr(), ym.data_ptr() if ym is not None else 0, x.data_ptr(), save.data_ptr(),
                                  weight.data_ptr(), bias.data_ptr(), acc.data_ptr(), dxbase,
                                  dres.data_ptr() if dres is not None else 0, dw.data_ptr(), db.data_ptr(), M, C,
                                  ctx.relu, H, W, int(p), stream_handle(), int(have_sums),
-                                 mb.data_ptr() if mb is not None else 0)
+                                 mb.data_ptr() if mb is not None else 0, **rargs)
         if park:
             ctx.res_sink["gm"] = (dy, mb)
         elif ctx.res_sink is not None and dres is not None and not ctx.res_sink.get("done"):
@@ -181,9 +253,10 @@ class _BnAct(torch.autograd.Function):
             dres = None
         if ctx.grads is not None:
             ready()
-            return dx, None, None, None, None, dres, None, None, None, None, None, None, None, None, None, None, None
+            return (dx, None, None, None, None, dres, None, None, None, None, None, None, None, None, None, None, None,
+                    None, None)
         return (dx, dw.to(weight.dtype), db.to(weight.dtype), None, None, dres, None, None, None, None, None, None, None,
-                None, None, None, None)
+                None, None, None, None, None, None)
 
 
 @torch.no_grad()
@@ -214,7 +287,8 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
            running_var: Optional[torch.Tensor], residual: Optional[torch.Tensor] = None, relu: bool = True,
            eps: float = 1e-5, momentum: float = 0.1, acc: Optional[torch.Tensor] = None,
            grads=None, res_sink: Optional[dict] = None, have_stats: Optional[bool] = None, out_pad: int = 0,
-           dx_pad: int = 0, bn_link: Optional[dict] = None, on_load: bool = False) -> torch.Tensor:
+           dx_pad: int = 0, bn_link: Optional[dict] = None, on_load: bool = False,
+           defer_apply: bool = False, defer_pool: bool = False) -> torch.Tensor:
     """``acc``: optional fp32 [4C] whose last 2C are zero; with ``have_stats``
     (the default when ``acc`` is given) its first 2C already hold the
     per-channel sum / sum of squares of x (see ops/conv.py Conv1x1), else they
@@ -237,12 +311,22 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
     ``on_load`` (ReLU, no residual, statistics given, unpadded output): the
     returned tensor is filled by the 1x1 GEMM that consumes it, which applies
     this BN + ReLU to its operand on load (ops/conv.py Conv1x1; csrc
-    set_conv_bn_on_load) -- the apply launch and its read of x are skipped."""
+    set_conv_bn_on_load) -- the apply launch and its read of x are skipped.
+    ``defer_apply`` (no ReLU, no residual, statistics given, unpadded): the
+    returned tensor is only a handle for the BN + residual + ReLU that takes it
+    as its residual -- that apply reads this BN's input and applies it on load
+    (csrc ResBn), so this apply launch and the write + read of its output go;
+    :func:`materialize` runs it for any other consumer.
+    ``defer_pool`` (ReLU, no residual, statistics given, unpadded): the same
+    for the stem max-pool (ops/pool.py), which applies this BN + ReLU to the
+    window elements it loads (csrc pool_nhwc.hip PoolBn)."""
     if not supported(x):
         raise ValueError(f"bn_act: needs a channels-last bf16 CUDA tensor with a supported channel count, got "
                          f"{tuple(x.shape)} {x.dtype} {x.device}")
     if residual is not None and (residual.shape != x.shape or residual.dtype != x.dtype):
         raise ValueError("bn_act: residual must match x in shape and dtype")
+    if residual is not None and getattr(residual, "_dl_res_bn", None) is not None and out_pad:
+        materialize(residual)
     if weight.dtype != torch.float32 or bias.dtype != torch.float32:
         raise ValueError("bn_act: weight / bias must be fp32")
     if acc is not None and (acc.numel() != 4 * x.shape[1] or acc.dtype != torch.float32):
@@ -253,4 +337,4 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
         have_stats = acc is not None
     return _BnAct.apply(x, weight.contiguous(), bias.contiguous(), running_mean, running_var, residual, relu, eps,
                         momentum, acc, grads, res_sink, bool(have_stats), int(out_pad), int(dx_pad),
-                        bn_link if relu else None, bool(on_load))
+                        bn_link if relu else None, bool(on_load), bool(defer_apply), bool(defer_pool))

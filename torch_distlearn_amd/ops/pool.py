@@ -20,7 +20,19 @@ class _MaxPool(torch.autograd.Function):
         Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         y = torch.empty((N, C, Ho, Wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
         idx = torch.empty((N, Ho, Wo, C), dtype=torch.uint8, device=x.device)
-        native().maxpool_nhwc_fwd(x.data_ptr(), y.data_ptr(), idx.data_ptr(), N, H, W, C, k, s, p, stream_handle())
+        # x may be a deferred BN + ReLU output (ops/bn_nhwc.py defer_pool): pool its
+        # input with the BN applied on load (csrc pool_nhwc.hip PoolBn)
+        pb = getattr(x, "_dl_pool_bn", None)
+        kw, src = {}, x
+        if pb is not None:
+            del x._dl_pool_bn
+            xin, acc, w, b, save, rm, rv, eps, mom = pb[1]
+            src = xin
+            kw = dict(bn_acc=acc.data_ptr(), bn_w=w.data_ptr(), bn_b=b.data_ptr(), bn_save=save.data_ptr(),
+                      bn_rm=rm.data_ptr() if rm is not None else 0, bn_rv=rv.data_ptr() if rv is not None else 0,
+                      bn_eps=float(eps), bn_momentum=float(mom))
+        native().maxpool_nhwc_fwd(src.data_ptr(), y.data_ptr(), idx.data_ptr(), N, H, W, C, k, s, p, stream_handle(),
+                                  **kw)
         ctx.save_for_backward(idx)
         ctx.geom = (N, C, H, W, k, s, p)
         return y
@@ -38,4 +50,8 @@ class _MaxPool(torch.autograd.Function):
 def max_pool2d_nhwc(x: torch.Tensor, k: int, s: int, p: int) -> torch.Tensor:
     if not supported(x):
         raise ValueError("max_pool2d_nhwc: needs a channels-last bf16 CUDA tensor with C % 8 == 0")
+    if getattr(x, "_dl_pool_bn", None) is not None and not (k == 3 and s == 2 and p == 1 and 256 % (x.shape[1] // 8) == 0):
+        from .bn_nhwc import materialize
+
+        materialize(x)  # this window cannot apply the deferred BN on load
     return _MaxPool.apply(x, k, s, p)
