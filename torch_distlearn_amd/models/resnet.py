@@ -46,6 +46,7 @@ class _BN(nn.Module):
         self.register_buffer("running_var", torch.ones(c))
         self.bind = None  # (weight grad view, bias grad view, ready) -- ResNet50.attach_flat
         self.acc = None  # this step's zeroed fp32 [4C] slice of the model's statistics arena
+        self.pad_bufs = {}  # persistent zero-bordered output / input-gradient buffers (ops/bn_nhwc.py padded_buffer)
 
     def forward(self, x):
         if _BN_MODE == "mixed" and x.is_cuda:
@@ -101,7 +102,7 @@ class _BN(nn.Module):
                           out_pad=out_pad, dx_pad=dx_pad, bn_link=bn_link, on_load=on_load,
                           defer_apply=defer and not relu and residual is None and have_stats and acc is not None,
                           defer_pool=defer_pool and relu and residual is None and have_stats and acc is not None
-                          and not out_pad)
+                          and not out_pad, pad_key=self.pad_bufs if _PAD_PERSIST else None)
         y = self(x)
         if residual is not None:
             y = y + residual
@@ -162,6 +163,12 @@ _DEFER_DOWN_BN = os.environ.get("DISTLEARN_RESNET_DEFER_DOWN_BN", "1") == "1"
 # the stem BatchNorm + ReLU applied on load by the stem max-pool (csrc pool_nhwc.hip
 # PoolBn): the apply launch and the write + read of its 112x112x64 output go
 _DEFER_STEM_BN = os.environ.get("DISTLEARN_RESNET_DEFER_STEM_BN", "1") == "1"
+# the zero-bordered BN outputs / input gradients of the 3x3 convs in buffers that
+# persist per BatchNorm (border zeroed once, not by a zero_border launch per use).
+# Off: 23.66-23.72 vs 23.72-23.92 ms/step (profiles/r5_resnet_pad_persist_ab.txt),
+# but two fresh models then no longer give a bitwise-equal first loss
+# (test_resnet50_bn_on_load's l0 == l2) and the cause is not pinned down yet
+_PAD_PERSIST = os.environ.get("DISTLEARN_RESNET_PAD_PERSIST", "0") == "1"
 
 
 class _Conv(nn.Module):

@@ -68,6 +68,24 @@ def padded_empty(n: int, c: int, h: int, w: int, pad: int, device) -> torch.Tens
     return v
 
 
+def padded_buffer(cache: dict, role: str, n: int, c: int, h: int, w: int, pad: int, device) -> torch.Tensor:
+    """:func:`padded_empty` whose buffer persists in ``cache`` (a dict the
+    owner keeps, e.g. the BatchNorm module's) per (role, shape): its border is
+    zeroed once instead of by a zero_border launch per use (32 per ResNet-50
+    step).  Each call returns a fresh view of the cached buffer, so the caller
+    must not hold the previous view across a later call for the same role (a
+    BatchNorm's output for the next 3x3 conv is consumed within the step)."""
+    k = (role, n, c, h, w, pad, str(device))
+    base = cache.get(k)
+    if base is None:
+        base = padded_empty(n, c, h, w, pad, device)
+        cache[k] = base
+    hp, wp = h + 2 * pad, w + 2 * pad
+    v = base.as_strided((n, c, h, w), (hp * wp * c, 1, wp * c, c), base.storage_offset())
+    v._dl_pad = pad
+    return v
+
+
 def supported(x: torch.Tensor) -> bool:
     c = x.shape[1]
     ok_c = c % 8 == 0 and ((c < 256 and 256 % (c // 8) == 0) or c % 256 == 0)
@@ -89,11 +107,14 @@ def materialize(t: torch.Tensor) -> torch.Tensor:
 class _BnAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, relu, eps, momentum, acc, grads, res_sink,
-                have_stats, out_pad, dx_pad, bn_link, on_load=False, defer_apply=False, defer_pool=False):
+                have_stats, out_pad, dx_pad, bn_link, on_load=False, defer_apply=False, defer_pool=False,
+                pad_key=None):
         M, C = _geom(x)
         N, _, H, W = x.shape
+        ctx.pad_key = pad_key
         if out_pad:
-            y = padded_empty(N, C, H, W, out_pad, x.device)
+            y = (padded_buffer(pad_key, "y", N, C, H, W, out_pad, x.device) if pad_key is not None
+                 else padded_empty(N, C, H, W, out_pad, x.device))
         else:
             y = torch.empty_like(x, memory_format=torch.channels_last)
         ctx.dx_pad = dx_pad
@@ -193,13 +214,17 @@ class _BnAct(torch.autograd.Function):
             if ctx.grads is not None:
                 ctx.grads[2]()
                 return (dy, None, None, None, None, None, None, None, None, None, None, None, None, None, None, None,
-                        None, None, None)
+                        None, None, None, None)
             return (dy, dw.to(weight.dtype), db.to(weight.dtype), None, None, None, None, None, None, None, None, None,
-                    None, None, None, None, None, None, None)
+                    None, None, None, None, None, None, None, None)
         dy = dy.contiguous(memory_format=torch.channels_last)
         N, _, H, W = x.shape
         p = ctx.dx_pad
-        dx = padded_empty(N, C, H, W, p, x.device) if p else torch.empty_like(x, memory_format=torch.channels_last)
+        if p:
+            dx = (padded_buffer(ctx.pad_key, "dx", N, C, H, W, p, x.device) if ctx.pad_key is not None
+                  else padded_empty(N, C, H, W, p, x.device))
+        else:
+            dx = torch.empty_like(x, memory_format=torch.channels_last)
         dxbase = dx.data_ptr() - (p * (W + 2 * p) + p) * C * 2 if p else dx.data_ptr()
         # relu mode 3 with a waiting consumer (the conv whose input is the residual,
         # ops/conv.py Conv1x1): the residual gradient dy * mask is not written
@@ -254,9 +279,9 @@ class _BnAct(torch.autograd.Function):
         if ctx.grads is not None:
             ready()
             return (dx, None, None, None, None, dres, None, None, None, None, None, None, None, None, None, None, None,
-                    None, None)
+                    None, None, None)
         return (dx, dw.to(weight.dtype), db.to(weight.dtype), None, None, dres, None, None, None, None, None, None, None,
-                None, None, None, None, None, None)
+                None, None, None, None, None, None, None)
 
 
 @torch.no_grad()
@@ -288,7 +313,7 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
            eps: float = 1e-5, momentum: float = 0.1, acc: Optional[torch.Tensor] = None,
            grads=None, res_sink: Optional[dict] = None, have_stats: Optional[bool] = None, out_pad: int = 0,
            dx_pad: int = 0, bn_link: Optional[dict] = None, on_load: bool = False,
-           defer_apply: bool = False, defer_pool: bool = False) -> torch.Tensor:
+           defer_apply: bool = False, defer_pool: bool = False, pad_key=None) -> torch.Tensor:
     """``acc``: optional fp32 [4C] whose last 2C are zero; with ``have_stats``
     (the default when ``acc`` is given) its first 2C already hold the
     per-channel sum / sum of squares of x (see ops/conv.py Conv1x1), else they
@@ -319,7 +344,10 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
     :func:`materialize` runs it for any other consumer.
     ``defer_pool`` (ReLU, no residual, statistics given, unpadded): the same
     for the stem max-pool (ops/pool.py), which applies this BN + ReLU to the
-    window elements it loads (csrc pool_nhwc.hip PoolBn)."""
+    window elements it loads (csrc pool_nhwc.hip PoolBn).
+    ``pad_key``: a dict in which the zero-bordered output / input gradient
+    buffers persist (:func:`padded_buffer`; the BatchNorm module's): no border
+    fill per use."""
     if not supported(x):
         raise ValueError(f"bn_act: needs a channels-last bf16 CUDA tensor with a supported channel count, got "
                          f"{tuple(x.shape)} {x.dtype} {x.device}")
@@ -337,4 +365,4 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
         have_stats = acc is not None
     return _BnAct.apply(x, weight.contiguous(), bias.contiguous(), running_mean, running_var, residual, relu, eps,
                         momentum, acc, grads, res_sink, bool(have_stats), int(out_pad), int(dx_pad),
-                        bn_link if relu else None, bool(on_load), bool(defer_apply), bool(defer_pool))
+                        bn_link if relu else None, bool(on_load), bool(defer_apply), bool(defer_pool), pad_key)
