@@ -143,6 +143,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_wgrad", &head_wgrad);
   m.def("mnist_step", &mnist_step);
   m.def("mnist_scratch_bytes", &mnist_scratch_bytes);
+  m.def("maxpool_bn_bwd", &maxpool_bn_bwd);
   m.def("maxpool_nhwc_fwd", &maxpool_nhwc_fwd, py::arg("x"), py::arg("y"), py::arg("idx"), py::arg("N"), py::arg("H"),
         py::arg("W"), py::arg("C"), py::arg("K"), py::arg("S"), py::arg("P"), py::arg("stream"), py::arg("bn_acc") = 0,
         py::arg("bn_w") = 0, py::arg("bn_b") = 0, py::arg("bn_save") = 0, py::arg("bn_rm") = 0, py::arg("bn_rv") = 0,

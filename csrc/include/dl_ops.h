@@ -216,6 +216,10 @@ void head_wgrad(uintptr_t h, uintptr_t dlogits, uintptr_t loss_b, int F, int B, 
                 uintptr_t loss, uintptr_t slot, uintptr_t step_ctr, uintptr_t stream);
 
 // pool_nhwc.hip ----------------------------------------------------------------
+// stem max-pool backward fused with its input BN + ReLU's backward (pool_nhwc.hip)
+void maxpool_bn_bwd(uintptr_t dy, uintptr_t idx, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b,
+                    uintptr_t acc, uintptr_t dx, uintptr_t dw, uintptr_t db, int N, int H, int W, int C,
+                    uintptr_t stream);
 void maxpool_nhwc_fwd(uintptr_t x, uintptr_t y, uintptr_t idx, int N, int H, int W, int C, int K, int S, int P,
                       uintptr_t stream, uintptr_t bn_acc = 0, uintptr_t bn_w = 0, uintptr_t bn_b = 0,
                       uintptr_t bn_save = 0, uintptr_t bn_rm = 0, uintptr_t bn_rv = 0, double bn_eps = 1e-5,

@@ -218,6 +218,116 @@ __global__ void __launch_bounds__(256) maxpool3s2_bwd_kernel(const bf16_t* __res
   }
 }
 
+// The stem max-pool backward fused with the backward of the BN + ReLU that
+// produced its input (relu mode 2: mask recomputed from the BN input x): every
+// input pixel gathers its dz (rounded to bf16, as the plain backward stores
+// it), g = dz * (x * sc + sh > 0), and
+//   PASS 0: per-channel sum(g), sum(g * xhat) -> acc (zeroed; one fp32 atomic
+//           per channel per block, grid capped like bn_nhwc's reduce);
+//   PASS 1: dx = w * invstd * (g - mean(g) - xhat * mean(g xhat)) and, block 0,
+//           dgamma / dbeta -- bn_nhwc.hip's arithmetic (relu mode 2).
+// The 112x112 dz is never written, and the BN's two passes re-read the small
+// pooled gradient and argmax bytes instead of it.
+template <int PASS>
+__global__ void __launch_bounds__(256) maxpool3s2_bwd_bn_kernel(const bf16_t* __restrict__ dy,
+                                                                const uint8_t* __restrict__ idx,
+                                                                const bf16_t* __restrict__ x,
+                                                                const float* __restrict__ save,
+                                                                const float* __restrict__ w,
+                                                                const float* __restrict__ b, float* __restrict__ acc,
+                                                                bf16_t* __restrict__ dx, float* __restrict__ dw,
+                                                                float* __restrict__ db, const PoolGeom g) {
+  const int C8 = g.C >> 3;
+  const int total = g.N * g.H * g.W * C8;
+  const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (t0 % C8) * 8;  // (the grid stride is a multiple of C8: fixed channels per thread)
+  const float invM = 1.f / (float)((int64_t)g.N * g.H * g.W);
+  float mean[8], invstd[8], sc[8], sh[8], mg[8], mgx[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    mean[k] = save[c0 + k];
+    invstd[k] = save[g.C + c0 + k];
+    sc[k] = w[c0 + k] * invstd[k];
+    sh[k] = fmaf(-mean[k], sc[k], b[c0 + k]);
+    mg[k] = PASS == 1 ? acc[c0 + k] * invM : 0.f;
+    mgx[k] = PASS == 1 ? acc[g.C + c0 + k] * invM : 0.f;
+  }
+  if (PASS == 1 && blockIdx.x == 0 && (int)threadIdx.x < C8) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      db[c0 + k] = acc[c0 + k];
+      dw[c0 + k] = acc[g.C + c0 + k];
+    }
+  }
+  float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int i = t0; i < total; i += gridDim.x * blockDim.x) {
+    const int c8 = i % C8, pix = i / C8;
+    const int ww = pix % g.W, t = pix / g.W;
+    const int h = t % g.H, n = t / g.H;
+    const int ohs[2] = {h >> 1, min(g.Ho - 1, (h + 1) >> 1)};
+    const int ows[2] = {ww >> 1, min(g.Wo - 1, (ww + 1) >> 1)};
+    uint4 d[4];
+    uint2 a[4];
+    bool ok[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int oh = ohs[j >> 1], ow = ows[j & 1];
+      ok[j] = (j < 2 || ohs[1] != ohs[0]) && ((j & 1) == 0 || ows[1] != ows[0]);
+      const int64_t o = ((int64_t)(n * g.Ho + oh) * g.Wo + ow) * g.C + c8 * 8;
+      d[j] = *reinterpret_cast<const uint4*>(dy + o);
+      a[j] = *reinterpret_cast<const uint2*>(idx + o);
+    }
+    const int64_t xo = (int64_t)pix * g.C + c8 * 8;
+    const uint4 xr = *reinterpret_cast<const uint4*>(x + xo);
+    float dz[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!ok[j]) continue;
+      const int oh = ohs[j >> 1], ow = ows[j & 1];
+      const uint32_t pos = (uint32_t)((h - (2 * oh - 1)) * 3 + (ww - (2 * ow - 1)));
+      float f[8];
+      unpack8p(d[j], f);
+      const uint32_t aw[2] = {a[j].x, a[j].y};
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (((aw[k >> 2] >> (8 * (k & 3))) & 0xffu) == pos) dz[k] += f[k];
+    }
+    float xv[8], gv[8];
+    unpack8p(pack8p(dz), gv);  // the stored dz's bf16 values
+    unpack8p(xr, xv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gv[k] = fmaf(xv[k], sc[k], sh[k]) > 0.f ? gv[k] : 0.f;
+    if (PASS == 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s1[k] += gv[k];
+        s2[k] = fmaf(gv[k], (xv[k] - mean[k]) * invstd[k], s2[k]);
+      }
+    } else {
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float xh = (xv[k] - mean[k]) * invstd[k];
+        o[k] = sc[k] * (gv[k] - mg[k] - xh * mgx[k]);
+      }
+      *reinterpret_cast<uint4*>(dx + xo) = pack8p(o);
+    }
+  }
+  if (PASS == 0) {  // threads t and t + C8, t + 2 C8, ... share channels: sum them, one atomic per channel
+    __shared__ float red[256 * 16];
+    const int tt = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { red[tt * 16 + k] = s1[k]; red[tt * 16 + 8 + k] = s2[k]; }
+    __syncthreads();
+    for (int j = tt; j < 2 * g.C; j += 256) {
+      const int which = j / g.C, ch = j - which * g.C;
+      float sum = 0.f;
+      for (int r = ch >> 3; r < 256; r += C8) sum += red[r * 16 + which * 8 + (ch & 7)];
+      atomicAdd(&acc[which * g.C + ch], sum);
+    }
+  }
+}
+
 static bool stem_window(const PoolGeom& g, int64_t in_items) {
   return g.K == 3 && g.S == 2 && g.P == 1 && in_items < (1ll << 31);
 }
@@ -263,6 +373,32 @@ void maxpool_nhwc_bwd(uintptr_t dy, uintptr_t idx, uintptr_t dx, int N, int H, i
   else
     maxpool_nhwc_bwd_kernel<<<stream_grid(total), 256, 0, as_stream(stream)>>>((const bf16_t*)dy, (const uint8_t*)idx,
                                                                                 (bf16_t*)dx, g);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+// The stem max-pool backward fused with its input BN + ReLU's backward
+// (maxpool3s2_bwd_bn_kernel): dy / idx the pooled gradient and argmax bytes,
+// x the BN input, save its [2C] mean / invstd, w / b its affine parameters,
+// acc its [2C] backward sums (zeroed), dx the BN input gradient, dw / db its
+// parameter gradients.
+void maxpool_bn_bwd(uintptr_t dy, uintptr_t idx, uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b,
+                    uintptr_t acc, uintptr_t dx, uintptr_t dw, uintptr_t db, int N, int H, int W, int C,
+                    uintptr_t stream) {
+  const PoolGeom g = pool_geom(N, H, W, C, 3, 2, 1);
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  if (!stem_window(g, total) || 256 % (C / 8) != 0)
+    throw std::runtime_error("maxpool_bn_bwd: the 3x3/2 window, C/8 | 256");
+  if (!dy || !idx || !x || !save || !w || !b || !acc || !dx || !dw || !db)
+    throw std::runtime_error("maxpool_bn_bwd: null operand");
+  hipStream_t s = as_stream(stream);
+  // (the sums pass: 2048 blocks -- at 256, one 4-wave block per CU left its gather loads exposed: 456 us)
+  maxpool3s2_bwd_bn_kernel<0><<<(int)std::min<int64_t>((total + 255) / 256, 2048), 256, 0, s>>>(
+      (const bf16_t*)dy, (const uint8_t*)idx, (const bf16_t*)x, (const float*)save, (const float*)w,
+      (const float*)b, (float*)acc, nullptr, nullptr, nullptr, g);
+  DL_HIP_CHECK(hipGetLastError());
+  maxpool3s2_bwd_bn_kernel<1><<<(int)std::min<int64_t>((total + 255) / 256, 8192), 256, 0, s>>>(
+      (const bf16_t*)dy, (const uint8_t*)idx, (const bf16_t*)x, (const float*)save, (const float*)w,
+      (const float*)b, (float*)acc, (bf16_t*)dx, (float*)dw, (float*)db, g);
   DL_HIP_CHECK(hipGetLastError());
 }
 

@@ -183,8 +183,13 @@ class _BnAct(torch.autograd.Function):
             del residual._dl_res_bwd
         ctx.own_link = None
         if defer_apply and not relu and residual is None and not out_pad:
-            ctx.own_link = {"fwd": (x, save, weight, acc, grads)}
+            ctx.own_link = {"fwd": (x, save, weight, bias, acc, grads)}
             y._dl_res_bwd = ctx.own_link
+        elif getattr(y, "_dl_pool_bn", None) is not None:
+            # ... and the stem max-pool's backward computes this BN's backward too
+            # (csrc pool_nhwc.hip maxpool3s2_bwd_bn_kernel; relu mode 2)
+            ctx.own_link = {"fwd": (x, save, weight, bias, acc, grads)}
+            y._dl_pool_bwd = ctx.own_link
         ctx.grads = grads
         ctx.res_sink = res_sink
         if res_sink is not None and residual is not None:
@@ -250,7 +255,7 @@ class _BnAct(torch.autograd.Function):
         rl = ctx.rbn_bwd
         if rl is not None and dres is not None and not have_sums and "fwd" in rl:
             # dres <- the residual BN's input gradient (its reduce sums ride our reduce pass)
-            rx, rsave, rw, racc4, rgrads = rl["fwd"]
+            rx, rsave, rw, _, racc4, rgrads = rl["fwd"]
             rC = rx.shape[1]
             racc = racc4[2 * rC:]
             if ctx.backwards > 1:

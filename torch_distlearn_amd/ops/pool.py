@@ -33,6 +33,11 @@ class _MaxPool(torch.autograd.Function):
                       bn_eps=float(eps), bn_momentum=float(mom))
         native().maxpool_nhwc_fwd(src.data_ptr(), y.data_ptr(), idx.data_ptr(), N, H, W, C, k, s, p, stream_handle(),
                                   **kw)
+        # ... and its backward then runs the BN's backward too (maxpool_bn_bwd)
+        ctx.bn_link = getattr(x, "_dl_pool_bwd", None) if pb is not None else None
+        if ctx.bn_link is not None:
+            del x._dl_pool_bwd
+        ctx.backwards = 0
         ctx.save_for_backward(idx)
         ctx.geom = (N, C, H, W, k, s, p)
         return y
@@ -43,6 +48,23 @@ class _MaxPool(torch.autograd.Function):
         N, C, H, W, k, s, p = ctx.geom
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
+        link = ctx.bn_link
+        ctx.backwards += 1
+        if link is not None and "fwd" in link:
+            # dx = the input gradient of the BN + ReLU before the pool (its sums and
+            # dgamma / dbeta too): that BN's backward passes it through
+            xb, save, w, b, acc4, grads = link["fwd"]
+            accb = acc4[2 * C:]
+            if ctx.backwards > 1:
+                accb.zero_()
+            dw, db = (grads[0], grads[1]) if grads is not None else (
+                torch.empty(C, device=dy.device), torch.empty(C, device=dy.device))
+            native().maxpool_bn_bwd(dy.data_ptr(), idx.data_ptr(), xb.data_ptr(), save.data_ptr(), w.data_ptr(),
+                                    b.data_ptr(), accb.data_ptr(), dx.data_ptr(), dw.data_ptr(), db.data_ptr(), N, H,
+                                    W, C, stream_handle())
+            link["fused"] = True
+            link["dwdb"] = (dw, db)
+            return dx, None, None, None
         native().maxpool_nhwc_bwd(dy.data_ptr(), idx.data_ptr(), dx.data_ptr(), N, H, W, C, k, s, p, stream_handle())
         return dx, None, None, None
 
