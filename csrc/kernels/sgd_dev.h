@@ -87,25 +87,31 @@ __device__ __forceinline__ void add4(float4 (&part)[TPO], int t, const float4& v
   q.x += v.x; q.y += v.y; q.z += v.z; q.w += v.w;
 }
 
+#ifndef DL_SLAB_CHUNK
+#define DL_SLAB_CHUNK 8
+#endif
+constexpr int kSlabChunk = DL_SLAB_CHUNK;  // splits' loads in flight per chunk (build A/B: -DDL_SLAB_CHUNK=16)
+
 template <int TPO>
 __device__ __forceinline__ float4 slab_sum4(const float4* __restrict__ s, int64_t stride4, int splits) {
   float4 part[TPO];
 #pragma unroll
   for (int t = 0; t < TPO; ++t) part[t] = make_float4(0.f, 0.f, 0.f, 0.f);
-  // chunks of 4 splits, the chunk's loads in flight before its adds; lane t of
-  // the stand-alone reduce adds splits t, t+TPO, ... in order: same here
-  for (int sp0 = 0; sp0 < splits; sp0 += 4) {
-    float4 v[4];
+  // chunks of kSlabChunk splits, the chunk's loads in flight before its adds
+  // (a chain of dependent 4-load chunks left the 19-split sums latency-bound);
+  // lane t of the stand-alone reduce adds splits t, t+TPO, ... in order: same
+  // here (kSlabChunk is a multiple of TPO, so split sp0 + u lands in part[u % TPO])
+  static_assert(kSlabChunk % 8 == 0, "chunk of whole 8-split groups");
+  for (int sp0 = 0; sp0 < splits; sp0 += kSlabChunk) {
+    float4 v[kSlabChunk];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < kSlabChunk; ++u)
       if (sp0 + u < splits) v[u] = s[(int64_t)(sp0 + u) * stride4];
-    const bool hi = TPO == 8 && (sp0 & 4);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kSlabChunk; ++u) {
       if (sp0 + u >= splits) break;
       if constexpr (TPO == 1) add4<TPO>(part, 0, v[u]);
-      else if (hi) add4<TPO>(part, 4 + u, v[u]);
-      else add4<TPO>(part, u, v[u]);
+      else add4<TPO>(part, u % TPO, v[u]);
     }
   }
 #pragma unroll

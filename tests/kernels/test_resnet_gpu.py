@@ -266,6 +266,7 @@ def test_resnet50_bn_on_load(monkeypatch):
     x = torch.randn(B, 64, 64, 3, device=dev, generator=g).to(torch.bfloat16)
     y = torch.randint(0, 100, (B,), device=dev, generator=g)
     C = _native.native()
+    C.set_reduce_atomic(0)  # deterministic partial-row BN statistics
     real = C.set_conv_bn_on_load
     calls = []
     monkeypatch.setattr(C, "set_conv_bn_on_load", lambda *a: (calls.append(a[9]), real(*a))[1])
@@ -284,7 +285,9 @@ def test_resnet50_bn_on_load(monkeypatch):
         out.append((loss, tr.flat.grad.clone(), [b.clone() for b in model.buffers()]))
         tr.finish()
     (l0, g0, b0), (l1, g1, b1), (l2, g2, b2) = out
-    assert abs(l1 - l0) < 1e-4 * abs(l0) and l0 == l2
+    # (l0 vs l2: the same path twice; the head adds the per-sample losses with fp32
+    # atomics, so the mean may differ in its last bit -- 4.852560997 vs 4.852560520)
+    assert abs(l1 - l0) < 1e-4 * abs(l0) and abs(l2 - l0) <= 4e-7 * abs(l0)
     # the two kernels' variance expressions contract to different fmas: last-bit
     # differences in invstd propagate to the later blocks' statistics
     for a, b in zip(b1, b0):

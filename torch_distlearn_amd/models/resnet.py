@@ -164,11 +164,11 @@ _DEFER_DOWN_BN = os.environ.get("DISTLEARN_RESNET_DEFER_DOWN_BN", "1") == "1"
 # PoolBn): the apply launch and the write + read of its 112x112x64 output go
 _DEFER_STEM_BN = os.environ.get("DISTLEARN_RESNET_DEFER_STEM_BN", "1") == "1"
 # the zero-bordered BN outputs / input gradients of the 3x3 convs in buffers that
-# persist per BatchNorm (border zeroed once, not by a zero_border launch per use).
-# Off: 23.66-23.72 vs 23.72-23.92 ms/step (profiles/r5_resnet_pad_persist_ab.txt),
-# but two fresh models then no longer give a bitwise-equal first loss
-# (test_resnet50_bn_on_load's l0 == l2) and the cause is not pinned down yet
-_PAD_PERSIST = os.environ.get("DISTLEARN_RESNET_PAD_PERSIST", "0") == "1"
+# persist per BatchNorm (border zeroed once, not by a zero_border launch per use):
+# 23.66-23.72 vs 23.72-23.92 ms/step (profiles/r5_resnet_pad_persist_ab.txt).  (The
+# first-loss mismatch seen with it was the head's atomic loss sum, which flips the
+# last bit of the mean run to run with or without it.)
+_PAD_PERSIST = os.environ.get("DISTLEARN_RESNET_PAD_PERSIST", "1") == "1"
 
 
 class _Conv(nn.Module):
