@@ -387,3 +387,48 @@ def test_resnet50_step_deferred_stem_bn(dev, monkeypatch):
     assert abs(out[0][0] - out[1][0]) < 1e-6
     assert _rel(out[1][1], out[0][1]) < 2e-2
     assert torch.equal(out[1][2], out[0][2])
+
+
+def test_persistent_pad_buffers_reused_and_guarded(dev, monkeypatch):
+    """Persistent zero-bordered BN buffers (ops/bn_nhwc.py padded_buffer): a
+    training step releases every view, so the next step reuses the same memory;
+    a second forward while the first one's views are still saved gets buffers
+    of its own, so the first forward's backward is unaffected."""
+    from torch_distlearn_amd import FlatParams
+    from torch_distlearn_amd.models import ResNet50
+    from torch_distlearn_amd.models import resnet as R
+
+    monkeypatch.setattr(R, "_PAD_PERSIST", True)
+    g = torch.Generator(device=dev).manual_seed(8)
+    xs = [torch.randn(8, 3, 64, 64, device=dev, generator=g).to(BF).contiguous(memory_format=CL) for _ in range(2)]
+    ys = [torch.randint(0, 1000, (8,), device=dev, generator=g) for _ in range(2)]
+    model = ResNet50(num_classes=1000, seed=0).to(dev)
+    flat = FlatParams(model, grads=True, shadow_bf16=True)
+    model.attach_flat(flat)
+    caches = [m.pad_bufs for m in model.modules() if hasattr(m, "pad_bufs")]
+
+    def bases():
+        return {(id(c), k): e[0].data_ptr() for c in caches for k, e in c.items()}
+
+    grads = []
+    for i in range(2):
+        flat.grad.zero_()
+        loss, _ = model.forward_loss(xs[i], ys[i], BF)
+        loss.backward()
+        torch.cuda.synchronize()
+        grads.append(flat.grad.clone())
+        if i == 0:
+            first = bases()
+    assert first, "no persistent pad buffers were used"
+    assert all(e[1]() is None for c in caches for e in c.values()), "a pad-buffer view outlived its step"
+    assert bases() == first
+    # two forwards, then the first one's backward: the second forward must not
+    # overwrite the views the first saved (the flat gradient is overwritten per
+    # backward, not accumulated, so only one backward runs)
+    flat.grad.zero_()
+    l0, _ = model.forward_loss(xs[0], ys[0], BF)
+    l1, _ = model.forward_loss(xs[1], ys[1], BF)
+    l0.backward()
+    torch.cuda.synchronize()
+    assert _rel(flat.grad, grads[0]) < 2e-2
+    del l1

@@ -13,6 +13,7 @@ op (tests/kernels/test_resnet_gpu.py).
 from __future__ import annotations
 
 import os
+import weakref
 from typing import Optional
 
 import torch
@@ -72,17 +73,23 @@ def padded_buffer(cache: dict, role: str, n: int, c: int, h: int, w: int, pad: i
     """:func:`padded_empty` whose buffer persists in ``cache`` (a dict the
     owner keeps, e.g. the BatchNorm module's) per (role, shape): its border is
     zeroed once instead of by a zero_border launch per use (32 per ResNet-50
-    step).  Each call returns a fresh view of the cached buffer, so the caller
-    must not hold the previous view across a later call for the same role (a
-    BatchNorm's output for the next 3x3 conv is consumed within the step)."""
+    step).  Each call returns a fresh view of the cached buffer -- unless the
+    previous view is still alive (weakref), e.g. saved by a backward that has
+    not run yet, in which case the call gets a fresh buffer of its own."""
     k = (role, n, c, h, w, pad, str(device))
-    base = cache.get(k)
-    if base is None:
-        base = padded_empty(n, c, h, w, pad, device)
-        cache[k] = base
+    ent = cache.get(k)
+    if ent is not None and ent[1]() is not None:
+        # the previous view is still referenced (e.g. saved for a backward that
+        # has not run: two forwards before one backward): a fresh buffer this time
+        return padded_empty(n, c, h, w, pad, device)
+    if ent is None:
+        ent = [padded_empty(n, c, h, w, pad, device), lambda: None]
+        cache[k] = ent
+    base = ent[0]
     hp, wp = h + 2 * pad, w + 2 * pad
     v = base.as_strided((n, c, h, w), (hp * wp * c, 1, wp * c, c), base.storage_offset())
     v._dl_pad = pad
+    ent[1] = weakref.ref(v)
     return v
 
 
