@@ -399,9 +399,15 @@ def _plan_3x3(M: int, N: int, K: int):
     """Forward / dgrad plan of a 3x3 GEMM (packed tile id, splits): 2-stage
     ring, 8 waves, no split -- the best of a stage/wave/tile/split sweep on
     every ResNet-50 stride-1 3x3 shape (scripts/bench_conv3x3.py SWEEP=1,
-    profiles/r2_conv3x3_sweep.jsonl): 71-88 us vs MIOpen's 74-119 us forward."""
+    profiles/r2_conv3x3_sweep.jsonl): 71-88 us vs MIOpen's 74-119 us forward.
+    The 64-channel GEMMs (the 56x56 stage) run 4 waves since round 5: 93.8 vs
+    114.4 us with 8 (profiles/r5_conv3x3_sweep.jsonl)."""
     tile = 0 if N % 128 == 0 else 2
-    return tile | (2 << 4) | (8 << 8), 1
+    waves = 4 if (N == 64 and _W4_C64) else 8
+    return tile | (2 << 4) | (waves << 8), 1
+
+
+_W4_C64 = os.environ.get("DISTLEARN_RESNET_3X3_W4", "1") == "1"
 
 
 def _wgrad_plan_3x3(cout: int, K: int, M: int):
