@@ -45,7 +45,7 @@ def main():
         y = torch.empty_like(dy)
         dx = torch.empty_like(x)
         gw = torch.zeros(cout, cin, device=dev)
-        rows = torch.empty(max(1, (M + 127) // 128), 2, cout, device=dev)
+        rows = torch.empty(4 * max(1, (M + 127) // 128), 2, cout, device=dev)  # 4x: per-wave-row rows (bit 21)
         ft, fs = _fwd_plan(M, cout, cin)
         dt, ds = _fwd_plan(M, cin, cout)
         wtile, wsp = _wgrad_plan(cout, cin, M)
@@ -56,6 +56,12 @@ def main():
                                              cout, 1, ft, fs, s)),
             "fwd_stats": timeit(lambda: C.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), rows.data_ptr(),
                                                    slab.data_ptr(), M, 1, 1, cin, cout, 1, ft, fs, s)),
+            "fwd_stats_swave": timeit(lambda: C.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), rows.data_ptr(),
+                                                         slab.data_ptr(), M, 1, 1, cin, cout, 1, ft | (1 << 21), fs, s)),
+            "fwd_stats_rows_reduce": timeit(lambda: C.bn_rows_reduce(rows.data_ptr(), (M + 127) // 128, cout,
+                                                                     gw.data_ptr(), s)),
+            "fwd_stats_swave_rows_reduce": timeit(lambda: C.bn_rows_reduce(rows.data_ptr(), 4 * ((M + 127) // 128), cout,
+                                                                           gw.data_ptr(), s)),
             "dgrad": timeit(lambda: C.conv_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, slab.data_ptr(), M, 1, 1,
                                                cout, cin, 1, dt, ds, s)),
             "wgrad_atomic": timeit(lambda: (gw.zero_(), C.conv_wgrad(dy.data_ptr(), x.data_ptr(), gw.data_ptr(), M, 1, 1,
