@@ -544,6 +544,10 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
   for (int q = 0; q < NP; ++q)
 #pragma unroll
     for (int k = 0; k < 8; ++k) { s1[q][k] = 0.f; s2[q][k] = 0.f; }
+  // vmcnt(0) before any output store: the k loop's trailing LDS-DMA (zero-fill
+  // past nk, inline asm the compiler does not track) has landed, so the LDS-only
+  // barriers of the statistics below need not wait for this tile's stores
+  if constexpr ((STATS || BNRED) && !SLAB) __builtin_amdgcn_s_waitcnt(0x0F70);
   // BNRED: the lane's channels are fixed per q -- their BN coefficients once
   float rmu[BNRED ? NP : 1][8], ris[BNRED ? NP : 1][8], rsc[BNRED ? NP : 1][8], rsh[BNRED ? NP : 1][8];
   if constexpr (BNR == 1) {
@@ -740,7 +744,11 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
         return;
       }
     }
-    __syncthreads();  // every wave done with the LDS ring and region
+    // LDS-only barriers: __syncthreads() would also wait for this wave's output
+    // stores (vmcnt(0)) before the tile's statistics, exposing their latency per
+    // tile.  No LDS-DMA is in flight (waited above); the ring's reads are lgkm.
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every wave done with the LDS ring and region
+    __builtin_amdgcn_s_barrier();
     float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]
     if ((lane & 15) == 15) {
 #pragma unroll
@@ -751,7 +759,8 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
           red[(wm * 2 + 1) * BN + nl + 32 * q + k] = s2[q][k];
         }
     }
-    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
     for (int c = tid; c < BN; c += NT) {
       float sa = 0.f, sb = 0.f;
 #pragma unroll
