@@ -82,7 +82,7 @@ def test_async_easgd_dead_client_exits_nonzero(tmp_path):
     non-zero with a communication error within --commTimeout (no hang)."""
     cmd = [sys.executable, "-m", "torch_distlearn_amd.launch", "--nproc", "4", "--no-node-flags",
            os.path.join(ROOT, "examples", "easgd.py"), "--numNodes", "2", "--dataset", "mnist", "--trainSize", "4096",
-           "--batchSize", "16", "--communicationTime", "2", "--testTime", "2", "--numEpochs", "50",
+           "--batchSize", "16", "--communicationTime", "2", "--testTime", "2", "--numEpochs", "20",
            "--commTimeout", "5", "--dieAfter", "2:3", "--resultsRoot", str(tmp_path / "Results")]
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
