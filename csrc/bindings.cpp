@@ -83,6 +83,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("combine_bwd_reduce_blocks", &combine_bwd_reduce_blocks);
   m.def("conv_fwd_ex", &conv_fwd_ex);
   m.def("conv_fwd_bnred", &conv_fwd_bnred);
+  m.def("conv_fwd_fix", &conv_fwd_fix);
+  m.def("conv_fix_ok", &conv_fix_ok);
   m.def("conv_region_ok", &conv_region_ok, py::arg("B"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"),
         py::arg("KS"), py::arg("tile"), py::arg("splits") = 1);
   m.def("set_conv_wgrad_stage_store", &set_conv_wgrad_stage_store);

@@ -400,6 +400,14 @@ class RcclCommunicator {
     // the grace period the handle is aborted from here anyway, the standard
     // cross-thread abort that makes the blocked RCCL call return.
     // Its release then finds nothing left to abort.
+    // Assumption: a host call still holding the handle after the
+    // grace is BLOCKED inside RCCL on a peer (connection setup, proxy progress),
+    // and RCCL's blocking loops poll the communicator's abort flag and return
+    // ncclInternalError/ncclRemoteError without touching the communicator again
+    // -- the contract NCCL documents for aborting from another thread.  A call
+    // that is merely slow (not blocked) would race the free, so the grace is
+    // max(5 s, the collective timeout): far longer than any RCCL host call that
+    // makes progress takes (group launches and comm init: milliseconds).
     if (comm_.doomed()) {
       const auto now = std::chrono::steady_clock::now();
       if (!doomed_seen_) {

@@ -115,6 +115,10 @@ void set_conv_bn_on_load(uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b, u
                          uintptr_t rvar, int64_t M, int C, double eps, double momentum, uintptr_t out);
 int conv_pool_load_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile);
 int conv_region_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile, int splits = 1);
+int conv_fwd_fix(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab, int B, int H, int W, int Cin,
+                 int Cout, int KS, int tile, int splits, uintptr_t y_prev, uintptr_t coef, uintptr_t rows,
+                 uintptr_t stream);
+int conv_fix_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile, int splits);
 int conv_fwd_bnred(uintptr_t x, uintptr_t w, uintptr_t y, int B, int H, int W, int Cin, int Cout, int KS, int tile,
                    uintptr_t y_prev, uintptr_t coef, uintptr_t rows, uintptr_t stream);
 int conv_fwd_ex(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab, int B, int Ho, int Wo, int Hp,

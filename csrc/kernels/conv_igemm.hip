@@ -747,8 +747,7 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
     // LDS-only barriers: __syncthreads() would also wait for this wave's output
     // stores (vmcnt(0)) before the tile's statistics, exposing their latency per
     // tile.  No LDS-DMA is in flight (waited above); the ring's reads are lgkm.
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every wave done with the LDS ring and region
-    __builtin_amdgcn_s_barrier();
+    block_sync_lds();  // lgkmcnt(0) (a compiler memory fence) + barrier: every wave done with the ring
     float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]
     if ((lane & 15) == 15) {
 #pragma unroll
@@ -759,8 +758,7 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
           red[(wm * 2 + 1) * BN + nl + 32 * q + k] = s2[q][k];
         }
     }
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
+    block_sync_lds();
     for (int c = tid; c < BN; c += NT) {
       float sa = 0.f, sb = 0.f;
 #pragma unroll
@@ -789,6 +787,143 @@ __device__ __forceinline__ int swz_b(int row) { return ((row >> 1) ^ (row >> 3))
 // output row 4(l>>4)+r holds channel 32p + 8(l>>4) + 4(b&1) + r.
 __device__ __forceinline__ int b_frag_row(int b, int i) { return 32 * (b >> 1) + 8 * (i >> 2) + 4 * (b & 1) + (i & 3); }
 
+// In-launch split-K combine (FIX, conv_fwd_fix).  Every K slice of a tile
+// publishes its fp32 partial tile write-through (sc1 16-byte buffer stores),
+// drains its stores (every wave: s_waitcnt vmcnt(0)), and after a workgroup
+// barrier one lane adds to the tile's arrival counter (relaxed, agent scope).
+// The slice whose add returns splits - 1 is the reducer: it reads EVERY slice
+// (its own included) with sc1 loads -- which bypass the CU's L1, so no acquire
+// fence is needed -- and sums them in slice order, bitwise the sums of
+// splitk_combine / combine_bwd_reduce; it then runs the plain bf16 epilogue
+// (BN statistics, or the BN backward reduce of the block below).  The other
+// slices exit.  Correct for any placement of a tile's slices over CUs and
+// XCDs (cdna_hip_programming.md §5 "in-launch split-K reduction", §6
+// Guideline 16: sc1 payload + drained stores + counter, sc1 loads): the
+// separate combine launch and its ~1.5-2 us kernel boundary are gone.  The
+// reducer resets the counter for the next launch (the counters start zeroed:
+// a __device__ array).
+__device__ int g_fix_cnt[1 << 16];
+constexpr int kFixCnt = 1 << 16;
+
+template <int BM, int BN, int WM, int WN, int FM, int FN>
+__device__ __forceinline__ bool splitk_fixup(f32x4 (&acc)[FM][FN], const ConvGeom& g, float* __restrict__ slab,
+                                             int split, int splits, int m0, int n0, int pm_b0, int pm_pos, int* cnt,
+                                             char* smem) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  constexpr int TM = BM / WM, TN = BN / WN, NP = FN / 2;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = tid >> 6, wm = wid / WN, wn = wid % WN;
+  const int nl = wn * TN + 8 * (lane >> 4);
+  const rsrc_t sr = make_rsrc(slab, (unsigned)((int64_t)splits * g.M * g.Cout * 4));
+  unsigned off[FM][NP];  // byte offset of the lane's 8 channels in slice 0 (or kOOB: M tail)
+#pragma unroll
+  for (int a = 0; a < FM; ++a) {
+    const int ml = m0 + wm * TM + a * 16 + (lane & 15);
+    const int row = g.posm ? (pm_b0 + ml - m0) * (g.H * g.W) + pm_pos : ml;
+#pragma unroll
+    for (int q = 0; q < NP; ++q)
+      off[a][q] = ml < g.M ? (unsigned)(((int64_t)row * g.Cout + n0 + nl + 32 * q) * 4) : kOOB;
+  }
+  const unsigned sstride = (unsigned)((int64_t)g.M * g.Cout * 4);
+#pragma unroll
+  for (int a = 0; a < FM; ++a)
+#pragma unroll
+    for (int q = 0; q < NP; ++q)
+      if (off[a][q] != kOOB) {
+        const unsigned o = off[a][q] + (unsigned)split * sstride;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[a][2 * q]), sr, (int)o, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[a][2 * q + 1]), sr, (int)(o + 16), 0, 16);
+      }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its slice is out of the CU
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem);  // the k loop is done with the ring (barrier above)
+  if (tid == 0) {
+    const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == splits - 1 ? 1 : 0;
+    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = last;
+  }
+  __syncthreads();
+  const int last = flag[0];
+  __syncthreads();  // flag read by every wave before the epilogue reuses the LDS
+  if (!last) return false;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction) keep the loads below the counter
+  if (splits <= 4) {
+    // the other slices only (the reducer's own is in registers): up to 3 loads
+    // per fragment half, all in flight; unconditional (a slice index past the
+    // others re-reads the last one and is not used)
+    u32x4 ld[3][FM][NP][2];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int o_s = min(u < split ? u : u + 1, splits - 1);  // u-th slice other than `split`
+      const unsigned so = (unsigned)o_s * sstride;
+#pragma unroll
+      for (int a = 0; a < FM; ++a)
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+          const unsigned o = off[a][q] == kOOB ? kOOB : off[a][q] + so;
+          ld[u][a][q][0] = __builtin_amdgcn_raw_buffer_load_b128(sr, (int)o, 0, 16);
+          ld[u][a][q][1] = __builtin_amdgcn_raw_buffer_load_b128(sr, (int)(o + 16), 0, 16);
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < FM; ++a)
+#pragma unroll
+      for (int q = 0; q < NP; ++q)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4 own = acc[a][2 * q + h];
+          f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {  // slice order; selects on values, never on loads
+            const f32x4 lo = __builtin_bit_cast(f32x4, ld[s < 3 ? s : 2][a][q][h]);
+            const f32x4 hi = __builtin_bit_cast(f32x4, ld[s > 0 ? s - 1 : 0][a][q][h]);
+            const f32x4 x = s < split ? lo : (s == split ? own : hi);
+            if (s == 0) d = x;  // (0 + x would turn -0 into +0)
+            else if (s < splits) d = f32x4{d[0] + x[0], d[1] + x[1], d[2] + x[2], d[3] + x[3]};
+          }
+          acc[a][2 * q + h] = d;
+        }
+    return true;
+  }
+  // more slices: every slice (its own re-read), 4 at a time with all their loads in flight
+#pragma unroll
+  for (int a = 0; a < FM; ++a)
+#pragma unroll
+    for (int b = 0; b < FN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int s0 = 0; s0 < splits; s0 += 4) {
+    u32x4 ld[4][FM][NP][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const unsigned so = (unsigned)min(s0 + u, splits - 1) * sstride;
+#pragma unroll
+      for (int a = 0; a < FM; ++a)
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+          const unsigned o = off[a][q] == kOOB ? kOOB : off[a][q] + so;
+          ld[u][a][q][0] = __builtin_amdgcn_raw_buffer_load_b128(sr, (int)o, 0, 16);
+          ld[u][a][q][1] = __builtin_amdgcn_raw_buffer_load_b128(sr, (int)(o + 16), 0, 16);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool use = s0 + u < splits;
+#pragma unroll
+      for (int a = 0; a < FM; ++a)
+#pragma unroll
+        for (int q = 0; q < NP; ++q)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const f32x4 v = __builtin_bit_cast(f32x4, ld[u][a][q][h]);
+            f32x4& d = acc[a][2 * q + h];
+            if (s0 + u == 0) d = v;
+            else if (use) d = f32x4{d[0] + v[0], d[1] + v[1], d[2] + v[2], d[3] + v[3]};
+          }
+    }
+  }
+  return true;
+}
+
 // --------------------------------------------------------------------------
 // forward / dgrad implicit GEMM, split-K capable
 //   C[m][n] = sum_{k in split} im2col(x)[m][k] * w[n][k]
@@ -796,15 +931,19 @@ __device__ __forceinline__ int b_frag_row(int b, int i) { return 32 * (b >> 1) +
 // 256 threads = 4 waves (2 x 2), wave tile (BM/2) x (BN/2), BK = 64,
 // 3-stage LDS ring filled by LDS-DMA, one barrier per K step.
 // --------------------------------------------------------------------------
+// FIX: split-K with the in-launch combine (splitk_fixup): `slab` holds the
+// slices, the reducer of each tile runs the plain (STATS / BNR) epilogue;
+// fixcnt = the launch's per-tile arrival counters.
 template <int BM, int BN, bool STATS, bool SLAB, bool TAPU, int STAGES, int WM = 2, int WN = 2, bool ADD = false,
-          bool TRP = true, int BNR = 0, bool OL = false>
+          bool TRP = true, int BNR = 0, bool OL = false, bool FIX = false>
 __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                        bf16_t* __restrict__ y, float* __restrict__ stats,
                                                        float* __restrict__ slab, const ConvGeom g, int splits,
                                                        int kt_per_split, unsigned long long* dbg,
                                                        const BnRedArgs br = BnRedArgs{},
                                                        const SgdJob side = SgdJob{},
-                                                       const BnOnLoad ol = BnOnLoad{}) {
+                                                       const BnOnLoad ol = BnOnLoad{},
+                                                       int* __restrict__ fixcnt = nullptr) {
   // side job (set_conv_side_sgd): the last side.nblk workgroups run part of
   // the step's SGD update on the CUs the convolution's one-workgroup-per-CU
   // grid leaves free (its gradients are final by the time this conv runs)
@@ -1222,6 +1361,14 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
     }
   };
   static_assert(BNR == 0 || TR, "the fused BN reduce needs the transposed epilogue");
+  if constexpr (FIX) {
+    static_assert(TR && !SLAB && !ADD && !OL, "FIX: transposed plain epilogue after the in-launch combine");
+    if (!splitk_fixup<BM, BN, WM, WN, FM, FN>(acc, g, slab, split, splits, m0, n0, pm_b0, pm_pos, fixcnt + tn * ntm + tm,
+                                              smem)) {
+      dbg_out();
+      return;
+    }
+  }
   if constexpr (TR)
     conv_fwd_epilogue_t<BM, BN, STATS, SLAB, WM, WN, FM, FN, ADD, BNR>(acc, g, y, stats, slab, split, tm, m0, n0, smem,
                                                                        pm_b0, pm_pos, br);
@@ -2660,6 +2807,15 @@ static BnRedArgs g_bnred{};         // conv_fwd_bnred: fused BN backward reduce 
 static PoolLoad g_pool_load{};      // set_conv_pool_load: the next region conv pools its input on load
 static BnOnLoad g_onload{};         // set_conv_bn_on_load: the next 1x1 GEMM applies a BN + ReLU on load
 static BnRedArgs g_bnred2{};        // set_conv_bn_reduce: NHWC BN backward reduce in the streaming epilogue
+// conv_fwd_fix: the current conv_fwd call combines its split-K slices in-launch
+// (FIX); bnred.rows != nullptr: its epilogue is the BN backward reduce of the
+// block below (BNR 1) instead of the BN statistics
+struct FixState {
+  bool on = false;
+  BnRedArgs bnred{};
+};
+static FixState g_fix{};
+static int g_fix_next = 0;  // next free arrival counter (round robin over g_fix_cnt)
 // A/B knob: 0 = the untransposed accumulator layout for the split-K and BN-statistics
 // instances of the streaming kernel (set_conv_fwd_tr)
 static int g_fwd_tr = 1;
@@ -2737,6 +2893,36 @@ static void launch_fwd_w(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uin
       return;
     } else {
       throw std::runtime_error("conv BN on load: this tile / ring has no on-load instance (128x128, 4 or 8 waves, <= 3 stages)");
+    }
+  }
+  if (g_fix.on) {
+    if constexpr (kTR && TAPU && BM == 128 && BN == 64 && WM == 4 && WN == 2) {
+      if (splits < 2 || g.pm_kmax > 0 || g.om || g_fwd_addend || g_bnred2.rows != nullptr)
+        throw std::runtime_error("conv_fwd_fix: split-K without balanced plans / output maps / addends");
+      const int ntiles = ntm * ntn;
+      if (ntiles > kFixCnt) throw std::runtime_error("conv_fwd_fix: too many tiles");
+      static int* cnt0 = nullptr;
+      if (!cnt0) DL_HIP_CHECK(hipGetSymbolAddress((void**)&cnt0, HIP_SYMBOL(g_fix_cnt)));
+      if (g_fix_next + ntiles > kFixCnt) g_fix_next = 0;
+      int* cnt = cnt0 + g_fix_next;  // distinct counters per call site (graph replays reuse them in order)
+      g_fix_next += ntiles;
+      if (g_fix.bnred.rows != nullptr) {
+        if (stats) throw std::runtime_error("conv_fwd_fix: BN reduce epilogue has no statistics");
+        conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, false, true, 1, false, true><<<grid, NT, 0, s>>>(
+            (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, (float*)slab, g, splits, ktps, g_conv_dbg,
+            g_fix.bnred, side, BnOnLoad{}, cnt);
+      } else if (stats) {
+        conv_fwd_kernel<BM, BN, true, false, TAPU, ST, WM, WN, false, true, 0, false, true><<<grid, NT, 0, s>>>(
+            (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)stats, (float*)slab, g, splits, ktps, g_conv_dbg,
+            BnRedArgs{}, side, BnOnLoad{}, cnt);
+      } else {
+        conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, false, true, 0, false, true><<<grid, NT, 0, s>>>(
+            (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, (float*)slab, g, splits, ktps, g_conv_dbg,
+            BnRedArgs{}, side, BnOnLoad{}, cnt);
+      }
+      return;
+    } else {
+      throw std::runtime_error("conv_fwd_fix: only the 128x64 streaming tile (8 waves) combines in-launch");
     }
   }
   if (g_fwd_addend && (splits > 1 || stats)) throw std::runtime_error("conv_fwd_add: no split-K / statistics");
@@ -3123,7 +3309,8 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
   const int c8_rows = c8_mt * 128 / std::max(1, W) + KS - 1;
   const size_t c8_lds =
       (size_t)((c8_rows * g.Wp + 1 + 63) / 64 * 64 + (64 * KS * KS + 63) / 64 * 64) * 16 + 4 * 2 * 64 * 4;
-  const bool streaming_only = g_bnred2.rows != nullptr;  // the NHWC BN reduce epilogue is on the streaming kernel
+  // the NHWC BN reduce epilogue and the in-launch split-K combine are on the streaming kernel
+  const bool streaming_only = g_bnred2.rows != nullptr || g_fix.on;
   if (!streaming_only && tile == 2 && splits == 1 && g_region && g.pow2 && Cin == 8 && W <= 128 && 128 % W == 0 && (H * W) % 128 == 0 &&
       Cout % 64 == 0 && c8_lds <= 160 * 1024) {
     const int grid = (g.M / 128 / c8_mt) * (Cout / 64);
@@ -3168,7 +3355,7 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
     g_side_sgd.nblk = 0;
     throw std::runtime_error("set_conv_side_sgd: the next conv_fwd call must run on the streaming kernel");
   }
-  if (splits == 1) return (g.M + fwd_bm(tile) - 1) / fwd_bm(tile) * g_stat_rows_mult;
+  if (splits == 1 || g_fix.on) return (g.M + fwd_bm(tile) - 1) / fwd_bm(tile) * g_stat_rows_mult;
   if (g_fwd_keep_slabs) {
     if (stats || g.pm_kmax > 0) throw std::runtime_error("conv_fwd keep-slabs: no statistics / balanced split-K");
     return 0;
@@ -3303,6 +3490,41 @@ int conv_fwd_bnred(uintptr_t x, uintptr_t w, uintptr_t y, int B, int H, int W, i
   }
   g_bnred = BnRedArgs{};
   return T;
+}
+
+// conv_fwd of a split-K plan whose slices are combined inside the launch
+// (FIX, splitk_fixup) instead of by splitk_combine / combine_bwd_reduce: the
+// reducer of each tile writes bf16 y and either the BN statistics (stats) or,
+// y_prev != 0 (a dgrad), the BatchNorm backward reduce of the block below
+// into rows (conv_fwd_bnred's epilogue, BNR 1).  128x64 streaming tiles only
+// (conv_fix_ok).  Returns the rows written (M tiles).
+int conv_fwd_fix(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab, int B, int H, int W, int Cin,
+                 int Cout, int KS, int tile, int splits, uintptr_t y_prev, uintptr_t coef, uintptr_t rows,
+                 uintptr_t stream) {
+  if (splits < 2 || !slab) throw std::runtime_error("conv_fwd_fix: a split-K plan with a slab");
+  if ((y_prev != 0) != (rows != 0) || (y_prev && !coef)) throw std::runtime_error("conv_fwd_fix: BN reduce operands");
+  g_fix.on = true;
+  g_fix.bnred = y_prev ? BnRedArgs{(const bf16_t*)y_prev, (const float*)coef, (float*)rows} : BnRedArgs{};
+  int T;
+  try {
+    T = conv_fwd(x, w, y, stats, slab, B, H, W, Cin, Cout, KS, tile, splits, stream);
+  } catch (...) {
+    g_fix = FixState{};
+    throw;
+  }
+  g_fix = FixState{};
+  return T;
+}
+
+// Whether conv_fwd_fix serves this plan (the 128x64 streaming tile, 8 waves,
+// the transposed epilogue; no balanced position-major split).
+int conv_fix_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile, int splits) {
+  (void)B; (void)H; (void)W;
+  const int t = tile & 15, wv = (tile >> 8) & 15;
+  return (t == 2 && splits >= 2 && Cin >= 64 && Cout % 64 == 0 && KS >= 1 && (wv == 0 ? g_fwd_waves : wv) == 8 &&
+          g_fwd_tr && !g_posm_balance)
+             ? 1
+             : 0;
 }
 
 // y = conv(x, w) + addend (bf16, same layout as y), streaming kernel only

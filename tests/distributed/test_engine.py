@@ -98,3 +98,86 @@ def _debug_worker(rank, world, port, perturb):
 def test_replica_divergence_detection():
     assert mp.run(_debug_worker, 2, False) == ["ok", "ok"]
     assert mp.run(_debug_worker, 2, True) == ["diverged", "diverged"]
+
+
+def _seq_worker(rank, world, port, algo, inject):
+    """Uneven epochs through the trainer with DISTLEARN_DEBUG_SYNC=1: the
+    collective-sequence hashes agree at every epoch synchronisation (after the
+    drain).  ``inject``: in epoch 2 node 2 issues one all-reduce with another
+    op than the others' (gloo runs it without hanging -- the silent kind of
+    divergence); the next synchronisation must raise CommError."""
+    import os
+
+    os.environ["DISTLEARN_DEBUG_SYNC"] = "1"
+    from torch_distlearn_amd import Tree
+    from torch_distlearn_amd.engine import DataParallelTrainer
+    from torch_distlearn_amd.models import MnistConvNet
+    from torch_distlearn_amd.parallel.comm import CommError
+
+    tree = Tree(rank + 1, world, host="127.0.0.1", port=port)
+    tr = DataParallelTrainer(MnistConvNet(seed=0), tree, lr=0.05, algo=algo, tau=2, alpha=0.3,
+                             compute_dtype=torch.float32, bucket_bytes=8 << 10)
+    tr.synchronize_parameters()
+    g = torch.Generator().manual_seed(rank)
+    seen = []
+    for epoch in range(3):
+        if inject and epoch == 1:  # (aligned: every rank is at the same collective after a sync)
+            t = torch.ones(16)
+            tree.comm.all_reduce(t, "max" if rank == 1 else "sum")
+        for _ in range(3 + (rank + epoch) % world):  # uneven per node and per epoch
+            tr.step(torch.randn(4, 1024, generator=g), torch.randint(0, 10, (4,), generator=g))
+        try:
+            tr.synchronize()
+        except CommError as e:
+            return {"raised": str(e), "epoch": epoch, "seen": seen}
+        seen.append(tree.comm.seq_state()[1])
+    return {"raised": None, "seen": seen}
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("algo", ["sgd", "ea"])
+def test_collective_sequence_hash_agrees_on_uneven_epochs(world, algo):
+    """every rank's hash of the collectives it issued
+    (graph replays included) agrees at the epoch synchronisation, uneven
+    epochs and drains notwithstanding."""
+    res = mp.run(_seq_worker, world, algo, False)
+    for r in res:
+        assert r["raised"] is None and len(r["seen"]) == 3
+        assert r["seen"] == res[0]["seen"] and r["seen"][0] > 0
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_collective_sequence_divergence_raises(world):
+    """An injected collective that differs on one rank raises CommError on
+    every rank at the next synchronisation, naming the nodes."""
+    res = mp.run(_seq_worker, world, "sgd", True)
+    for r in res:
+        assert r["raised"] is not None and r["epoch"] == 1, r
+        assert "collective sequence diverged" in r["raised"] and "nodes [2]" in r["raised"]
+
+
+def test_sequence_record_and_replay():
+    """A captured graph's collectives are recorded, not counted; each replay
+    counts them (the engine's _seq_record / _replay)."""
+    import os
+
+    from torch_distlearn_amd.parallel.comm import Communicator
+
+    os.environ["DISTLEARN_DEBUG_SYNC"] = "1"
+    try:
+        a, b = Communicator(), Communicator()
+        t = torch.zeros(8)
+        with a.seq_record() as rec:
+            a._note("all_reduce", t, 0)
+            a._note("broadcast", t, 1)
+        assert a.seq_state()[1] == 0 and len(rec) == 2
+        a.seq_replay(rec, times=3)
+        for _ in range(3):
+            b._note("all_reduce", t, 0)
+            b._note("broadcast", t, 1)
+        assert a.seq_state() == b.seq_state()
+        b._note("broadcast", t, 0)  # another root: another hash
+        a._note("broadcast", t, 1)
+        assert a.seq_state()[1] == b.seq_state()[1] and a.seq_state()[0] != b.seq_state()[0]
+    finally:
+        os.environ.pop("DISTLEARN_DEBUG_SYNC", None)

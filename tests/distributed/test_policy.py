@@ -137,3 +137,32 @@ def test_channel_cap_is_measured_with_the_policy(world):
         assert r["seen"] == [(3, 0, 16), (2, 16, 16), (3, 0, 32), (2, 32, 32)]
         assert r["rebuilt"] == [16, 32, 16]  # one rebuild per cap, then back to the winner's
         assert pol["candidates"]["reserve@32"] == {"dgrad_stages": 2, "cu_reserve": 32, "channel_cap": 32}
+
+
+def _cap_mismatch_worker(rank, world, port):
+    import os
+
+    import torch
+
+    from torch_distlearn_amd import Tree
+    from torch_distlearn_amd.engine import DataParallelTrainer
+
+    os.environ.pop("DISTLEARN_CHANNEL_CAP", None)
+    os.environ["DISTLEARN_CHANNEL_CAPS"] = "16,32" if rank == 0 else "16,64"
+    tree = Tree(rank + 1, world, host="127.0.0.1", port=port)
+    tree.comm.set_channel_cap = lambda c: (_ for _ in ()).throw(AssertionError("rebuilt before agreeing"))
+    tr = DataParallelTrainer(torch.nn.Linear(4, 2), tree, lr=0.1)
+    tr.executor, tr.graph = _FakeExecutor(), True
+    tr._time_step_graph = lambda loader, reps: 0.3
+    try:
+        tr.select_policy(None)
+    except ValueError as e:
+        return str(e)
+    return "no error"
+
+
+def test_channel_cap_lists_must_agree():
+    """ranks whose environments give different cap lists fail with
+    a clear error on every rank before any communicator rebuild."""
+    for msg in mp.run(_cap_mismatch_worker, 2):
+        assert "disagree on the channel caps" in msg

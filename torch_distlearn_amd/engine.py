@@ -207,6 +207,7 @@ class DataParallelTrainer:
         self._graph = None
         self._static = None
         self._multi = {}     # unroll -> (graph, loss) (run())
+        self._seqs = {}      # id(graph) -> collectives recorded at its capture (DISTLEARN_DEBUG_SYNC)
         self.captures = 0    # hipGraph captures so far (none may happen in a timed region)
         self.last_loss: Optional[torch.Tensor] = None
         self.steps = 0
@@ -271,7 +272,9 @@ class DataParallelTrainer:
         """Whether the step's final update is ONE fused fp32 SGD launch that can
         also prepare the next step of an unrolled graph (flat_sgd_ consumes an
         armed arm_next_prep): not per-bucket updates, not the bf16 gradient
-        wire (its update reads the bf16 copy), not an AsyncEA client."""
+        wire (its update reads the bf16 copy).  An AsyncEA client's local-step
+        updates inside its unrolled graph consume the preparation too; a
+        syncing step (update after syncClient, outside the graph) never arms it."""
         return (self.algo in ("sgd", "ea", "async") and not self.bucket_updates and self.grad_comm_dtype == "fp32"
                 and (self._slabs is not None or self.reduces_grads or self.algo != "sgd"))
 
@@ -312,7 +315,7 @@ class DataParallelTrainer:
                     self._static[1].copy_(y, non_blocking=True)
             elif self._static[0] is not dev_loader:
                 raise ValueError("the captured step is bound to another DeviceLoader")
-            self._graph.replay()
+            self._replay(self._graph)
             self._track()
             if self.sgd is not None:
                 # the captured body counted one step at capture time only
@@ -380,7 +383,7 @@ class DataParallelTrainer:
                 k = max((u for u in self._multi if isinstance(u, int) and u <= cap), default=1) if fast else 1
             if k > 1 or (key is not None and k >= 1):
                 g, loss = self._multi[key if key is not None else k]
-                g.replay()
+                self._replay(g)
                 if self.ea is not None:
                     self.ea.step += k  # the graph ran k local steps (+ the round when key is set)
                 elif self.aea is not None:
@@ -437,9 +440,9 @@ class DataParallelTrainer:
             self._capture_multi(loader, k)
         if new:
             saved = self._snapshot(loader)
-            self._graph.replay()
+            self._replay(self._graph)
             for k in new:
-                self._multi[k][0].replay()
+                self._replay(self._multi[k][0])
             self._restore(saved, loader)
             torch.cuda.current_stream().synchronize()
 
@@ -500,13 +503,13 @@ class DataParallelTrainer:
 
     def _policy_candidates(self) -> dict:
         """name -> (executor policy kwargs, channel cap or None)."""
-        from .parallel.comm import channel_cap_candidates
+        from .parallel.comm import agree_channel_caps, channel_cap_candidates
 
         base = self.executor.policies()
         comm = self.tree.comm
         caps = [None]
         if base and callable(getattr(comm, "set_channel_cap", None)) and runs_collectives(comm):
-            caps = channel_cap_candidates()
+            caps = agree_channel_caps(comm, channel_cap_candidates())
         out = {}
         for cap in caps:
             for p, kw in base.items():
@@ -565,13 +568,13 @@ class DataParallelTrainer:
         saved = self._snapshot(loader)
         self._capture(loader, None)
         g = self._graph
-        g.replay()
+        self._replay(g)
         torch.cuda.synchronize()
         self.tree.comm.barrier()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(reps):
-            g.replay()
+            self._replay(g)
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / reps
@@ -601,6 +604,26 @@ class DataParallelTrainer:
         if ctr is not None:
             loader.ctr.copy_(ctr)
 
+    @contextlib.contextmanager
+    def _seq_record(self, g):
+        """Record the collectives a capture of ``g`` issues (every replay
+        counts them: Communicator.seq_replay, DISTLEARN_DEBUG_SYNC)."""
+        rec_fn = getattr(self.tree.comm, "seq_record", None)
+        if rec_fn is None:
+            yield
+            return
+        with rec_fn() as rec:
+            yield
+        # keyed by id (no reference: a dropped graph must be freed); every graph
+        # this engine replays was recorded here, so a reused id is overwritten
+        self._seqs[id(g)] = rec
+
+    def _replay(self, g) -> None:
+        g.replay()
+        rec = self._seqs.get(id(g))
+        if rec:
+            self.tree.comm.seq_replay(rec)
+
     def _track(self) -> None:
         """Let the communicator's watchdog time the collectives of the work
         just enqueued (a replayed graph's collectives are invisible to it)."""
@@ -619,7 +642,7 @@ class DataParallelTrainer:
         n = k[1] if isinstance(k, tuple) else k
         local = self.aea is not None
         g = torch.cuda.CUDAGraph()
-        with _capturing(self.tree.comm), torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
+        with _capturing(self.tree.comm), self._seq_record(g), torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
             for j in range(n):
                 loss = self._step_body(loader, None, prep_next=j + 1 < n, local=local)
             if ea_round:
@@ -677,7 +700,7 @@ class DataParallelTrainer:
         torch.cuda.current_stream().wait_stream(s)
         self._restore(saved, x)
         g = torch.cuda.CUDAGraph()
-        with _capturing(self.tree.comm), torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
+        with _capturing(self.tree.comm), self._seq_record(g), torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
             loss = self._step_body(sx, sy)
         if self.sgd is not None:
             # the warm-up + capture bodies counted steps; undo (replay() counts itself)

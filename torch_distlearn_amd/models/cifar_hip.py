@@ -329,6 +329,14 @@ class CifarHIPExecutor:
         # an unsplit (region-kernel) dgrad runs the BN backward reduce of the block
         # below in its epilogue (csrc conv_fwd_bnred; DISTLEARN_DGRAD_BNRED=0: A/B)
         self.dgrad_bnred = os.environ.get("DISTLEARN_DGRAD_BNRED", "1") == "1"
+        # split-K forwards combine their slices in-launch (csrc splitk_fixup): the
+        # splitk_combine launch is gone (layer-4 forward 18.2 + 5.4 -> 22.6 us).
+        # DISTLEARN_FIX=2: the split-K dgrads too, their reducers running the BN
+        # backward reduce of the block below -- measured slower than the
+        # combine_bwd_reduce launch (dgrad4 22.9 -> 27.3, dgrad3 33.5 -> 36.6 us:
+        # the reducer's chain of slice drain, counter, slice loads and pool-window
+        # loads is serial latency at the kernel's tail), 0: off
+        self.fix = int(os.environ.get("DISTLEARN_FIX", "1"))
         self.atomic = self.mode > 0             # BN statistics / gradients by atomics, no finalize kernels
         self.head_reduce = (os.environ.get("DISTLEARN_HEAD_REDUCE", "1") == "1" and self.mode == 2 and self.head_pool
                             and self.head_wgrad_fused and self.couts[-1] == 512)
@@ -512,9 +520,14 @@ class CifarHIPExecutor:
             if img:
                 C.set_conv_region(2)
             try:
-                ntm = C.conv_fwd(inp.data_ptr(), w.data_ptr(), self.y[i].data_ptr(),
-                                 self.stats[i].data_ptr() if train else 0, self.slabs.data_ptr(), B, h, h, cin, cout,
-                                 KSIZE, t | self.fwd_cfg | _slab_cap_bits(sp), sp, s)
+                if self._fix_ok(B, h, cin, cout, t | self.fwd_cfg, sp):
+                    ntm = C.conv_fwd_fix(inp.data_ptr(), w.data_ptr(), self.y[i].data_ptr(),
+                                         self.stats[i].data_ptr() if train else 0, self.slabs.data_ptr(), B, h, h,
+                                         cin, cout, KSIZE, t | self.fwd_cfg, sp, 0, 0, 0, s)
+                else:
+                    ntm = C.conv_fwd(inp.data_ptr(), w.data_ptr(), self.y[i].data_ptr(),
+                                     self.stats[i].data_ptr() if train else 0, self.slabs.data_ptr(), B, h, h, cin,
+                                     cout, KSIZE, t | self.fwd_cfg | _slab_cap_bits(sp), sp, s)
             finally:
                 if img:
                     C.set_conv_region(self._region_mode)
@@ -536,6 +549,12 @@ class CifarHIPExecutor:
                     C.bn_relu_pool_fwd(self.y[i].data_ptr(), self.coef[i].data_ptr(), self.p[i].data_ptr(), B, h, h,
                                        cout, opad, s)
             inp = self.p[i]
+
+    def _fix_ok(self, B: int, h: int, cin: int, cout: int, tile: int, splits: int) -> bool:
+        """Whether a split-K conv of this plan combines its slices inside the
+        launch (csrc conv_fwd_fix: the tile's last-arriving slice sums them and
+        runs the epilogue) instead of a combine launch.  DISTLEARN_FIX=0: off."""
+        return (self.fix > 0 and splits > 1 and self.C.conv_fix_ok(B, h, h, cin, cout, KSIZE, tile, splits) == 1)
 
     def _pool_on_load(self, i: int) -> bool:
         """Whether block i's conv takes block i-1's BN -> ReLU -> 2x2 pool on
@@ -746,10 +765,25 @@ class CifarHIPExecutor:
                 dt, ds = self.dgrad_plan[i]
                 if self.dgrad_stages != 3:
                     C.set_conv_stages(self.dgrad_stages, self._wgrad_stages)
-                keep = self.fuse_combine and ds in (2, 4, 8) and not (merge and pending is not None)
+                fix = self.fix >= 2 and self._fix_ok(B, h, cout, cin, dt, ds) and not (merge and pending is not None)
+                keep = self.fuse_combine and ds in (2, 4, 8) and not (merge and pending is not None) and not fix
                 bnred = (self.dgrad_bnred and ds == 1 and not keep and self._region_dgrad(i, B)
                          and not (merge and pending is not None))
-                if bnred:
+                if fix:
+                    # split-K slices combined inside the launch, whose reducers also
+                    # run block i-1's BN backward reduce (no combine_bwd_reduce launch)
+                    prt = {0: self.bwd_part[i - 1], 1: self.g32[self._leaf(i - 1, 2)], 2: self.bwd_rows[i - 1]}[self.mode]
+                    if self._side is not None and i == self._side["block"]:
+                        self._arm_side()
+                    elif i in self._ride:
+                        C.set_conv_side_reduce(*self._ride[i])
+                    dp_reduced = C.conv_fwd_fix(dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), 0,
+                                                self.slabs.data_ptr(), B, h, h, cout, cin, KSIZE, dt, ds,
+                                                self.y[i - 1].data_ptr(), self.coef[i - 1].data_ptr(), prt.data_ptr(), s)
+                    if i in self._ride:
+                        for j in range(4):
+                            self._ready(self._leaf(i, j))
+                elif bnred:
                     prt = {0: self.bwd_part[i - 1], 1: self.g32[self._leaf(i - 1, 2)], 2: self.bwd_rows[i - 1]}[self.mode]
                     dp_reduced = C.conv_fwd_bnred(dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), B,
                                                   h, h, cout, cin, KSIZE, dt, self.y[i - 1].data_ptr(),

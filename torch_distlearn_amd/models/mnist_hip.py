@@ -74,6 +74,10 @@ class MnistHIPExecutor:
         return self.logp[:self._last_b]
 
     @torch.no_grad()
-    def predict(self, x: torch.Tensor) -> torch.Tensor:
+    def predict(self, x: torch.Tensor, batch_stats: bool = False) -> torch.Tensor:
+        """Log-probabilities of ``x``.  The MNIST net has no BatchNorm, so
+        ``batch_stats`` (the trainer's train-mode-statistics flag) changes
+        nothing; it is accepted so ``DataParallelTrainer.predict`` works on
+        every executor."""
         B = self._launch(x, None)
         return self.logp[:B].clone()

@@ -135,6 +135,9 @@ class AllReduceEA:
 
         self.tree.allReduce(FlatBuffer(self.delta), "sum", drain_step)
         self.step = 0
+        from ..utils.debug import check_collective_sequence
+
+        check_collective_sequence(self.tree, "the AllReduceEA epoch synchronisation")  # DISTLEARN_DEBUG_SYNC=1
 
     def synchronizeCenter(self, params: Any) -> Any:  # noqa: N802  (:77-84)
         self._one_time_init(params)

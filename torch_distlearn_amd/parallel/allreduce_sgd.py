@@ -179,6 +179,9 @@ class AllReduceSGD:
     def synchronizeParameters(self, params: Any) -> Any:  # noqa: N802  (:33-54)
         # 1. drain (all nodes, deadlock-free even with zero-step nodes)
         self._drain(params)
+        from ..utils.debug import check_collective_sequence
+
+        check_collective_sequence(self.tree, "synchronizeParameters")  # DISTLEARN_DEBUG_SYNC=1
         # 2. everybody learns everybody's step count (:39); control plane
         steps = self.stepsPerNode.clone()
         self.tree.comm.all_reduce_host(steps, "sum")

@@ -54,12 +54,75 @@ class CommError(RuntimeError):
     longer usable."""
 
 
+# collective-sequence tracking (DISTLEARN_DEBUG_SYNC=1): every data-plane
+# collective a rank issues is folded into a running 64-bit FNV-1a hash of
+# (op, dtype, count, op / root); see Communicator.seq_*
+SEQ_KINDS = {"all_reduce": 1, "broadcast": 2, "all_gather": 3, "reduce_scatter": 4}
+_FNV_OFFSET, _FNV_PRIME, _M64 = 0xCBF29CE484222325, 0x100000001B3, (1 << 64) - 1
+
+
+def seq_tracking() -> bool:
+    return os.environ.get("DISTLEARN_DEBUG_SYNC", "0") == "1"
+
+
 class Communicator:
     """Interface shared by the RCCL and process-group communicators."""
 
     rank: int
     world_size: int
     ctrl: Optional[dist.ProcessGroup]
+    # collective-sequence state (class defaults; per instance once written)
+    _seq_h = _FNV_OFFSET
+    _seq_n = 0
+    _seq_rec: Optional[list] = None
+
+    # ---------------- collective-sequence tracking ----------------
+    # RCCL hangs -- it does not fail -- when ranks issue different collective
+    # sequences (the likely failure of uneven epochs with unrolled hipGraphs and
+    # drains).  With DISTLEARN_DEBUG_SYNC=1 each rank hashes every collective it
+    # issues; a hipGraph capture RECORDS its collectives (seq_record) and every
+    # replay folds that record in (seq_replay), so the hash follows what ran.
+    # The algorithms compare the hashes over the control plane at their epoch
+    # synchronisation (utils/debug.check_collective_sequence) and raise
+    # CommError naming the ranks that differ.  Point-to-point traffic (AsyncEA)
+    # is asymmetric by design and not hashed.
+    def _note(self, kind: str, t: torch.Tensor, arg: int = 0) -> None:
+        if not seq_tracking():
+            return
+        item = (SEQ_KINDS[kind], DTYPE_CODES.get(t.dtype, 99), int(t.numel()), int(arg))
+        if self._seq_rec is not None:  # inside a capture: it runs at every replay
+            self._seq_rec.append(item)
+        else:
+            self._seq_fold((item,))
+
+    def _seq_fold(self, items) -> None:
+        h = self._seq_h
+        for it in items:
+            for v in it:
+                h = ((h ^ (v & _M64)) * _FNV_PRIME) & _M64
+        self._seq_h = h
+        self._seq_n += len(items)
+
+    @contextlib.contextmanager
+    def seq_record(self):
+        """Record (instead of count) the collectives issued inside the block --
+        a hipGraph capture; yields the list to hand to :meth:`seq_replay`."""
+        prev, rec = self._seq_rec, []
+        self._seq_rec = rec
+        try:
+            yield rec
+        finally:
+            self._seq_rec = prev
+
+    def seq_replay(self, rec: Optional[list], times: int = 1) -> None:
+        """Count a recorded sequence as issued ``times`` times (graph replays)."""
+        if rec:
+            for _ in range(times):
+                self._seq_fold(rec)
+
+    def seq_state(self) -> Tuple[int, int]:
+        """(hash, number of collectives) of what this rank issued so far."""
+        return self._seq_h, self._seq_n
 
     # ---------------- data plane (in-place, stream ordered) ----------------
     def all_reduce(self, t: torch.Tensor, op: str = "sum", stream=None) -> None:
@@ -124,6 +187,15 @@ class Communicator:
             with _ctrl_errors("host all-reduce"):
                 dist.all_reduce(t, op=_DIST_OPS[op], group=self.ctrl)
 
+    def all_gather_host(self, t: torch.Tensor) -> List[torch.Tensor]:
+        """Small CPU all-gather on the control plane: every rank's ``t``."""
+        if self.world_size == 1:
+            return [t.clone()]
+        out = [torch.empty_like(t) for _ in range(self.world_size)]
+        with _ctrl_errors("host all-gather"):
+            dist.all_gather(out, t, group=self.ctrl)
+        return out
+
     def broadcast_object(self, obj, root: int = 0):
         lst = [obj]
         if self.world_size > 1:
@@ -166,6 +238,7 @@ class ProcessGroupCommunicator(Communicator):
         self._unstage = []
 
     def all_reduce(self, t, op="sum", stream=None):
+        self._note("all_reduce", t, OP_CODES[op])
         if self.world_size == 1:
             return
         with _ctrl_errors("all-reduce"):
@@ -176,11 +249,13 @@ class ProcessGroupCommunicator(Communicator):
                 dist.all_reduce(t, op=_DIST_OPS[op], group=self.data)
 
     def broadcast(self, t, root=0, stream=None):
+        self._note("broadcast", t, root)
         if self.world_size > 1:
             with _ctrl_errors("broadcast"):
                 dist.broadcast(t, src=root, group=self.data)
 
     def all_gather(self, out, t, stream=None):
+        self._note("all_gather", t)
         if self.world_size == 1:
             out.view(-1).copy_(t.view(-1))
             return
@@ -271,6 +346,30 @@ def channel_cap_candidates() -> List[int]:
     return sorted(set(caps))
 
 
+def agree_channel_caps(comm, caps: List[int]) -> List[int]:
+    """Check that every rank measures the same channel-cap list.
+    Each rank derives it from its own environment; a rank whose list differs
+    would rebuild its communicator at another cap and the ranks would hang in
+    comm init or the policy broadcast.  Collective over the control plane:
+    raises ``ValueError`` naming the disagreement instead."""
+    if getattr(comm, "world_size", 1) <= 1:
+        return caps
+    n = 17  # count + up to 16 caps
+    if len(caps) > n - 1:
+        raise ValueError(f"at most {n - 1} channel caps, got {caps}")
+    mine = torch.zeros(n, dtype=torch.float64)
+    mine[0] = len(caps)
+    mine[1:1 + len(caps)] = torch.tensor([float(c) for c in caps], dtype=torch.float64)
+    hi, lo = mine.clone(), -mine
+    comm.all_reduce_host(hi, "max")
+    comm.all_reduce_host(lo, "max")
+    if not torch.equal(hi, -lo):
+        raise ValueError(
+            f"ranks disagree on the channel caps to measure (rank {comm.rank}: {caps}); set the same "
+            "NCCL_MAX_NCHANNELS / DISTLEARN_CHANNEL_CAP / DISTLEARN_CHANNEL_CAPS on every rank")
+    return caps
+
+
 def runs_collectives(comm) -> bool:
     """Whether data-plane collectives on ``comm`` actually run: world > 1, or
     an RCCL communicator at world 1 with the collectives forced through RCCL
@@ -332,6 +431,7 @@ class RcclCommunicator(Communicator):
 
     def all_reduce(self, t, op="sum", stream=None):
         self._check(t)
+        self._note("all_reduce", t, OP_CODES[op])
         if self._skip1:  # identity (in place); skips RCCL's self-copy
             return
         self._call(self._c.all_reduce, t.data_ptr(), t.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], OP_CODES[op],
@@ -339,6 +439,7 @@ class RcclCommunicator(Communicator):
 
     def broadcast(self, t, root=0, stream=None):
         self._check(t)
+        self._note("broadcast", t, root)
         if self._skip1:
             return
         self._call(self._c.broadcast, t.data_ptr(), t.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], root, stream_handle(stream))
@@ -346,10 +447,12 @@ class RcclCommunicator(Communicator):
     def all_gather(self, out, t, stream=None):
         self._check(t)
         self._check(out)
+        self._note("all_gather", t)
         self._call(self._c.all_gather, t.data_ptr(), out.data_ptr(), t.numel(), DTYPE_CODES[t.dtype], stream_handle(stream))
 
     def reduce_scatter(self, out, t, op="sum", stream=None):
         self._check(t)
+        self._note("reduce_scatter", t, OP_CODES[op])
         self._call(self._c.reduce_scatter, t.data_ptr(), out.data_ptr(), out.numel(), DTYPE_CODES[t.dtype], OP_CODES[op],
                                stream_handle(stream))
 

@@ -7,6 +7,13 @@ the replicas disagree -- the cheap end-to-end check that the collective
 sequence, the uneven-step drain and the RCCL reductions kept every node
 bitwise identical.  ``DISTLEARN_DEBUG_SYNC=1`` makes
 ``AllReduceSGD.synchronizeParameters`` run it automatically.
+
+:func:`check_collective_sequence` (also under ``DISTLEARN_DEBUG_SYNC=1``)
+compares the hash of every rank's issued collective sequence
+(``Communicator.seq_state``, graph replays included) at the algorithms' epoch
+synchronisation, after the drain -- RCCL hangs or silently mixes buffers when
+ranks issue different sequences; this turns that into a ``CommError`` naming
+the ranks.
 """
 from __future__ import annotations
 
@@ -33,3 +40,26 @@ def assert_replicas_in_sync(tree, buf: torch.Tensor, what: str = "parameters") -
 
 def debug_sync_enabled() -> bool:
     return os.environ.get("DISTLEARN_DEBUG_SYNC", "0") == "1"
+
+
+def check_collective_sequence(tree, what: str) -> None:
+    """Raise :class:`~torch_distlearn_amd.parallel.comm.CommError` when the
+    ranks' collective sequences (op, dtype, count, op / root of every
+    collective issued so far) differ.  Collective (control plane); a no-op
+    unless ``DISTLEARN_DEBUG_SYNC=1``."""
+    from ..parallel.comm import CommError, seq_tracking
+
+    comm = tree.comm
+    if comm.world_size <= 1 or not seq_tracking():
+        return
+    h, n = comm.seq_state()
+    mine = torch.tensor([h >> 32, h & 0xFFFFFFFF, n], dtype=torch.int64)
+    every = [tuple(int(v) for v in t.tolist()) for t in comm.all_gather_host(mine)]
+    if len(set(every)) == 1:
+        return
+    groups = {}
+    for r, v in enumerate(every):
+        groups.setdefault(v, []).append(r + 1)
+    desc = "; ".join(f"nodes {nodes}: {v[2]} collectives, hash {(v[0] << 32) | v[1]:016x}"
+                     for v, nodes in sorted(groups.items(), key=lambda kv: kv[1]))
+    raise CommError(f"collective sequence diverged before {what} (seen on node {tree.nodeIndex}): {desc}")
