@@ -305,10 +305,12 @@ def main():
         if step_args is None:
             tr.prepare(loader, unroll)  # (run() already did; explicit: no capture may fall in the timed region)
         comm = {}
-        if len(workers) > 1 and a.algo == "sgd" and not cpu:
-            # communication profile: eager calibration steps with HIP events around every
-            # bucket all-reduce, OUTSIDE the timed region; training state is restored after
-            comm = tr.comm_profile(loader if step_args is None else step_args, steps=6)
+        if (len(workers) > 1 or a.nworld_path) and a.algo == "sgd" and not cpu:
+            # communication profile: HIP events around every bucket all-reduce, read from
+            # replays of a captured one-step graph (the timed schedule; eager steps when
+            # the model has no device loader), OUTSIDE the timed region; training state
+            # is restored after
+            comm = tr.comm_profile(loader if step_args is None else step_args, steps=6, replay=True)
         captures0 = tr.captures
         hold = None
         if a.hold_cus > 0 and not cpu:
@@ -426,7 +428,8 @@ def main():
             "final_loss": round(lval, 4),
         }
         if comm:
-            out["comm"] = {**comm, "method": "rank-0 HIP events, 6 eager calibration steps outside the timed region"}
+            out["comm"] = {**comm, "method": f"rank-0 HIP events, {comm.get('source', 'eager steps')}, "
+                                             "6 calibration steps outside the timed region"}
         print(json.dumps(out), flush=True)
     tree.comm.barrier()
 

@@ -31,9 +31,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_conv_side_sgd", &set_conv_side_sgd);
   m.def("set_conv_side_reduce", &set_conv_side_reduce);
   m.def("slab_reduce_multi", &slab_reduce_multi);
-  m.def("set_conv_pool_load", &set_conv_pool_load);
-  m.def("conv_pool_load_ok", &conv_pool_load_ok);
-  m.def("set_conv_bn_on_load", &set_conv_bn_on_load);
   m.def("confusion_update", &confusion_update);
   m.def("bn_nhwc_fwd", &bn_nhwc_fwd);
   m.def("bn_nhwc_bwd", &bn_nhwc_bwd);
@@ -62,19 +59,13 @@ PYBIND11_MODULE(_C, m) {
         py::arg("addend_mask") = 0);
   m.def("conv_fwd_stat_rows", &conv_fwd_stat_rows);
   m.def("set_conv_region", &set_conv_region);
-  m.def("set_conv_region_bd", &set_conv_region_bd);
   m.def("set_conv_region_stages", &set_conv_region_stages);
-  m.def("set_conv_wgrad_pf", &set_conv_wgrad_pf);
   m.def("set_bn_bwd_items", &set_bn_bwd_items);
   m.def("set_conv_region_ablate", &set_conv_region_ablate);
   m.def("set_conv_region_waves", &set_conv_region_waves);
   m.def("set_conv_stages", &set_conv_stages);
-  m.def("set_conv_fwd_tr", &set_conv_fwd_tr);
   m.def("set_conv_posm", &set_conv_posm);
-  m.def("set_conv_wgrad_xcd", &set_conv_wgrad_xcd);
-  m.def("set_conv_fwd_order", &set_conv_fwd_order);
   m.def("set_conv_c8_mt", &set_conv_c8_mt);
-  m.def("set_conv_posm_balance", &set_conv_posm_balance);
   m.def("set_conv_waves", &set_conv_waves);
   m.def("set_conv_debug", &set_conv_debug);
   m.def("conv_wgrad", &conv_wgrad);
@@ -87,17 +78,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_fix_ok", &conv_fix_ok);
   m.def("conv_region_ok", &conv_region_ok, py::arg("B"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"),
         py::arg("KS"), py::arg("tile"), py::arg("splits") = 1);
-  m.def("set_conv_wgrad_stage_store", &set_conv_wgrad_stage_store);
-  m.def("set_conv_wgrad_order", &set_conv_wgrad_order);
   m.def("set_conv_fwd_pf", &set_conv_fwd_pf);
   m.def("set_head_stamps", &set_head_stamps);
   m.def("set_bn_stamps", &set_bn_stamps);
   m.def("set_conv_wgrad_stamps", &set_conv_wgrad_stamps);
-  m.def("set_conv_bn_reduce", &set_conv_bn_reduce, py::arg("x"), py::arg("save"), py::arg("w"), py::arg("b"),
-        py::arg("rows"), py::arg("ym") = 0, py::arg("mb") = 0);
   m.def("conv_wgrad_ex", &conv_wgrad_ex);
-  m.def("wgrad_posm_plan", &wgrad_posm_plan);
-  m.def("conv_wgrad_c8", &conv_wgrad_c8);
   // ---- ResNet-50 glue (resnet_glue.hip) ------------------------------------------
   m.def("s2d_stem_input", &s2d_stem_input);
   m.def("stem_weight_pack", &stem_weight_pack);

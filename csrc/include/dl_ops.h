@@ -90,30 +90,19 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
              int Cout, int KS, int tile, int splits, uintptr_t stream);
 int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile, int splits);
 void set_conv_region(int on);
-void set_conv_region_bd(int mode);  // direct-B region kernel: 0 off, 1 row tiles, 2 + whole images
-void set_conv_region_stages(int st);
-void set_conv_wgrad_pf(int pf);
 void set_bn_bwd_items(int n);
 void set_conv_region_ablate(int a);
 void set_conv_region_waves(int w);
+void set_conv_region_stages(int st);
 void set_conv_stages(int fwd, int wgrad);
 void set_conv_waves(int waves);
 void set_conv_debug(uintptr_t buf);
-void set_conv_wgrad_stage_store(int on);
-void set_conv_wgrad_order(int dma_first);
 void set_conv_fwd_pf(int on);
 void set_head_stamps(uintptr_t buf);
 void set_bn_stamps(uintptr_t buf);
 void set_conv_wgrad_stamps(uintptr_t buf);
-void set_conv_bn_reduce(uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, uintptr_t rows, uintptr_t ym = 0,
-                        uintptr_t mb = 0);
 // the next conv_fwd (region kernel, forward with statistics) pools its input on load
 // from the previous block's pre-BN output (BN coefficients from its accumulated sums)
-void set_conv_pool_load(uintptr_t y_prev, uintptr_t sums, int64_t M, uintptr_t gamma, uintptr_t beta, uintptr_t bias,
-                        uintptr_t rmean, uintptr_t rvar, float eps, float momentum, uintptr_t coef, uintptr_t pout);
-void set_conv_bn_on_load(uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b, uintptr_t save, uintptr_t rmean,
-                         uintptr_t rvar, int64_t M, int C, double eps, double momentum, uintptr_t out);
-int conv_pool_load_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile);
 int conv_region_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile, int splits = 1);
 int conv_fwd_fix(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab, int B, int H, int W, int Cin,
                  int Cout, int KS, int tile, int splits, uintptr_t y_prev, uintptr_t coef, uintptr_t rows,
@@ -129,22 +118,15 @@ void conv_wgrad_ex(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int Ho, int 
                    uintptr_t stream);
 // first-layer weight gradient from an LDS-resident input region (Cin 8, Cout 64):
 // fp32 slabs [B * H / R][64][ldo]; returns the split count
-int conv_wgrad_c8(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, int Cin, int Cout, int KS, int R,
-                  int ldo, uintptr_t stream);
 // position-major wgrad plan at `steps` K steps per workgroup: {max splits a
 // column tile needs, workgroups with work} ({0, 0}: B does not take it)
-std::vector<int> wgrad_posm_plan(int B, int H, int W, int Cin, int Cout, int KS, int tile, int steps);
 void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, int Cin, int Cout, int KS, int splits,
                 int ldo, int tile, int atomic_creal, uintptr_t stream);
 void set_reduce_atomic_conv(int rows);
 void conv_fwd_add(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t addend, int B, int H, int W, int Cin, int Cout,
                   int KS, int tile, uintptr_t stream, uintptr_t addend_mask = 0);
-void set_conv_fwd_tr(int on);
 void set_conv_posm(int on);
-void set_conv_wgrad_xcd(int on);
-void set_conv_fwd_order(int mmajor);
 void set_conv_c8_mt(int mt);
-void set_conv_posm_balance(int on);
 void slab_reduce(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream);
 void slab_reduce_add(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C, uintptr_t stream);
 void slab_reduce_add_oihw(uintptr_t slabs, uintptr_t dst, int splits, int Cout, int taps, int Cp, int C,

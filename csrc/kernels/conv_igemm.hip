@@ -69,65 +69,19 @@ __device__ __forceinline__ void put_stats(float* __restrict__ stats, int64_t row
 // re-read of dP, are gone.  rows: mode 0 = one partial row per M tile
 // [T][sum dz (C); sum dz*xhat (C)], atomic modes = R striped rows
 // [R][dgamma = sum dz*xhat (C); dbeta = sum dz (C)] (the layouts of the reduce).
-// BNR == 2 (ResNet-50 channels-last BatchNorm, no pool): the dgrad output is
-// the gradient dz of a BN(+ReLU) output whose input x has the output's layout;
-// g = dz * (x*scale + shift > 0) and sum(g), sum(g * xhat) per channel go to
-// deterministic partial rows [T][sum g (C); sum g*xhat (C)] (one per M tile,
-// reduced by bn_rows_reduce into the BatchNorm's backward accumulator) --
-// bn_nhwc_bwd_reduce_kernel's arithmetic (relu mode 2), fused.
-// BNR == 3: the same for a BN + residual + ReLU output (the mask is out > 0:
-// its bits `mb`, one byte per 8 channels as bn_nhwc's relu mode 3 writes them,
-// or else the saved block output `ym`); the dgrad is the next block's c1 with
-// the residual gradient added in the epilogue (ADD), so dz is complete.
+// (BNR 2 / 3, the same reduce for the ResNet-50 channels-last BatchNorms in
+// the 1x1 dgrad epilogues, measured slower than the reduce pass -- the
+// epilogue's re-read of the BN input costs more than it saves,
+// profiles/r5_resnet_bn_dgrad_ab.txt -- and was removed in round 6.)
 struct BnRedArgs {
-  const bf16_t* y;     // BNR 1: [B][2Ho][2Wo][C] pre-BN output of the previous block; BNR 2: x [M][C]
-  const float* coef;   // BNR 1: [4][C] mean, invstd, scale, shift
+  const bf16_t* y;     // [B][2Ho][2Wo][C] pre-BN output of the previous block
+  const float* coef;   // [4][C] mean, invstd, scale, shift
   float* rows;
-  const float* save;   // BNR 2: [2][C] mean, invstd
-  const float* w;      // BNR 2: gamma
-  const float* b;      // BNR 2: beta
-  const bf16_t* ym;    // BNR 3: block output [M][C] (ReLU mask) ...
-  const uint8_t* mb;   // ... or its mask bits [M][C/8] (bit k of byte n/8: channel n + k)
 };
 
-// BatchNorm -> ReLU applied to the A operand on load (OL: the ResNet-50 b2 ->
-// c3 edge, a stride-1 1x1 GEMM): the conv reads the BN's pre-activation input
-// y instead of its output, derives the per-channel scale / shift from the
-// accumulated statistics in its prologue (workgroup 0 publishes the saved
-// mean / invstd and updates the running statistics), applies
-// max(fma(y, scale, shift), 0) to every A fragment after its LDS read, and the
-// first N tile's workgroups write the activation out (the backward's copy) --
-// the BN apply launch and its read of y are gone.  Same arithmetic as
-// bn_nhwc_fwd_apply (bn_nhwc.hip), so the activation is the same bits.
-struct BnOnLoad {
-  const bf16_t* y;            // pre-BN input [M][C] (read instead of the conv's x)
-  const float* acc;           // [2C]: sum, sum of squares of y
-  const float* w;
-  const float* b;
-  float* save;                // [2C]: mean, invstd (for the BN backward)
-  float* rmean;
-  float* rvar;
-  float eps, momentum;
-  int M, C;
-  bf16_t* out;                // the activation [M][C] (== the conv's x argument)
-};
-constexpr int kOlMaxC = 512;
-
-constexpr int kPlSlots = 5;  // region slots per thread of the pool-on-load fill (512 threads)
-
-// Pool-on-load source of the region kernel (PL): the previous block's
-// pre-BN conv output y [B][2H][2W][Cin] and its accumulated BN statistics
-// (fin: the coefficients are derived in the prologue, block 0 publishes coef
-// and the running statistics).  The region holds max_{2x2} relu(scale*y +
-// shift) (bn_relu_pool8, the BN consumer kernel's arithmetic) with the zero
-// border kept zero, and the tile's own interior rows of that pooled
-// activation go out to pout [B][Hp][Wp][Cin] (the backward's copy) -- the
-// separate BN/ReLU/pool launch and its read of y are gone.
-struct PoolLoad {
-  const bf16_t* y;
-  BnFin fin;
-  bf16_t* pout;
-};
+// (A BatchNorm -> ReLU applied to the A operand on load of the ResNet-50
+// b2 -> c3 1x1 GEMM measured slower than the apply pass it removed, 25.43 vs
+// 24.64 ms/step, profiles/r4_resnet_bn_on_load_ab.txt; removed in round 6.)
 
 struct ConvGeom {
   int B, H, W;
@@ -138,8 +92,6 @@ struct ConvGeom {
   int M, K, Kch;           // M = B*H*W, K = KS*KS*Cin, Kch = K/8
   int pow2;                // H and W powers of two (the region / c8 kernels and the shift addressing)
   int posm;                // streaming kernel: position-major M tiles with padding taps skipped (fwd_posm)
-  int mmajor;              // fwd/dgrad tile order after the XCD swizzle: 0 panel-major, 1 M-tile-major
-  int pm_kmax, pm_P;       // balanced position-major split-K: max K steps per workgroup, workgroups per N tile
   float inv_HW, inv_W;     // reciprocals for the non-pow2 pixel decomposition (fdivmod)
   // Generalised geometry (make_geom_ex; the streaming forward and the wgrad
   // kernels only, non-pow2 addressing): tap (kh, kw) of output pixel (oh, ow)
@@ -151,38 +103,7 @@ struct ConvGeom {
   // row b*omHW + (omS*oh + omH0)*omW + omS*ow + omW0 (the phases of a strided
   // convolution's input gradient, written interleaved into the full tensor)
   int om, omS, omH0, omW0, omW, omHW;
-  // BN statistics (reduction mode 0, transposed epilogue): one partial row per
-  // (M tile, wave row) written straight from the lanes -- no LDS round and no
-  // barriers in the epilogue (FwdCfg bit 21; T = M tiles x WM rows)
-  int swave;
-  // position-major weight gradient (conv_wgrad tile bits 8-16): a K step is BK
-  // images at ONE output pixel, and a column tile only visits the pixels where
-  // one of its taps reads inside the image (wgrad_posm_steps); wposm = steps per
-  // workgroup (the tile's steps are split over ceil(steps / wposm) workgroups),
-  // wlognbc = log2(B / BK), wskip: splits a tile does not need write nothing
-  // (their slabs stay zero from allocation) instead of zeros
-  int wposm, wlognbc, wskip;
 };
-
-// Position-major wgrad steps of the column tile [k0, k0 + BN): output pixels
-// (ph0 + i, pw0 + j), i < nph, j < npw, where a tap of the tile reads inside
-// the image (padded row ph + kh is interior: pad <= ph + kh < H + pad), times
-// B / BK image chunks.  The ResNet-free CIFAR layers 3 / 4 (8x8 / 4x4, 5x5
-// kernels) visit 72 % / 49 % of the pixel-major steps.
-__host__ __device__ inline int wgrad_posm_steps(const ConvGeom& g, int k0, int BN, int& ph0, int& pw0, int& npw) {
-  const int kc_lo = k0 / 8, kc_hi = (k0 + BN) / 8 < g.Kch ? (k0 + BN) / 8 - 1 : g.Kch - 1;
-  const int kp_lo = kc_lo >> g.logC8, kp_hi = kc_hi >> g.logC8;
-  const int kh_lo = kp_lo / g.KW, kh_hi = kp_hi / g.KW;
-  int kw_lo = kp_lo - kh_lo * g.KW, kw_hi = kp_hi - kh_hi * g.KW;
-  if (kh_lo != kh_hi) { kw_lo = 0; kw_hi = g.KW - 1; }  // the tile spans a tap row boundary
-  ph0 = g.pad - kh_hi > 0 ? g.pad - kh_hi : 0;
-  pw0 = g.pad - kw_hi > 0 ? g.pad - kw_hi : 0;
-  const int ph1 = g.H + g.pad - kh_lo < g.H ? g.H + g.pad - kh_lo : g.H;
-  const int pw1 = g.W + g.pad - kw_lo < g.W ? g.W + g.pad - kw_lo : g.W;
-  const int nph = ph1 > ph0 ? ph1 - ph0 : 0;
-  npw = pw1 > pw0 ? pw1 - pw0 : 0;
-  return (nph * npw) << g.wlognbc;
-}
 
 // q = n / d, r = n - q*d for 0 <= n < 2^24 via a float reciprocal and one
 // correction step (the ResNet-50 spatial sizes 56/28/14/7 are not powers of two)
@@ -242,20 +163,16 @@ static int ilog2_exact(int v, const char* what) {
 static bool is_pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
 
 static ConvGeom make_geom(int B, int H, int W, int Cin, int Cout, int KS) {
-  ConvGeom g{};  // value-initialised: a field added later (e.g. swave) must not read stack garbage
+  ConvGeom g{};  // value-initialised: a field added later must not read stack garbage
   g.B = B; g.H = H; g.W = W; g.Cin = Cin; g.Cout = Cout; g.KS = KS; g.pad = KS / 2;
   g.Hp = H + 2 * g.pad; g.Wp = W + 2 * g.pad;
   if (KS % 2 != 1) throw std::runtime_error("conv: odd kernel size required");
   if (Cin < 8) throw std::runtime_error("conv: Cin must be >= 8 (pad the input channels)");
   g.pow2 = is_pow2(W) && is_pow2(H) ? 1 : 0;
   g.posm = 0;
-  g.mmajor = 0;
-  g.pm_kmax = 0;
-  g.pm_P = 0;
   g.S = 1; g.KH = KS; g.KW = KS;
   g.dsep = 0; g.dHp = g.Hp; g.dWp = g.Wp; g.dpad = g.pad;
   g.om = 0; g.omS = 1; g.omH0 = 0; g.omW0 = 0; g.omW = W; g.omHW = H * W;
-  g.swave = 0;
   g.logW = g.pow2 ? ilog2_exact(W, "W") : 0;
   g.logHW = g.pow2 ? ilog2_exact(H * W, "H*W") : 0;
   g.inv_HW = 1.0f / (float)(H * W);
@@ -533,8 +450,8 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
   constexpr int NT = 64 * WM * WN, TM = BM / WM, TN = BN / WN, NP = FN / 2;
   static_assert(!(ADD && (SLAB || STATS)), "ADD: plain bf16 output only");
   constexpr bool BNRED = BNR != 0;
-  static_assert(!(BNRED && (SLAB || STATS)) && !(BNR == 1 && ADD) && !(BNR == 3 && !ADD),
-                "BNRED: plain bf16 output (BNR 3: with the residual addend)");
+  static_assert(BNR == 0 || BNR == 1, "BNR 1: the pooled BN backward reduce");
+  static_assert(!(BNRED && (SLAB || STATS || ADD)), "BNRED: plain bf16 output");
   static_assert(FN % 2 == 0, "N fragments pair up");
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = tid >> 6, wm = wid / WN, wn = wid % WN;
@@ -562,18 +479,6 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
         rsh[q][k] = br.coef[3 * g.Cout + n + k];
       }
     }
-  } else if constexpr (BNR == 2 || BNR == 3) {
-#pragma unroll
-    for (int q = 0; q < NP; ++q) {
-      const int n = n0 + nl + 32 * q;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {  // bn_nhwc: sc = w*invstd, sh = fma(-mean, sc, b)
-        rmu[q][k] = br.save[n + k];
-        ris[q][k] = br.save[g.Cout + n + k];
-        rsc[q][k] = br.w[n + k] * ris[q][k];
-        rsh[q][k] = fmaf(-rmu[q][k], rsc[q][k], br.b[n + k]);
-      }
-    }
   }
   // the stored row of fragment a (position-major tiles hold image pm_b0 + r at
   // output pixel pm_pos)
@@ -586,9 +491,7 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
   // first store -- y may alias it as far as the compiler knows, so a load left
   // in the loop below waits behind each store, one memory latency per
   // fragment: ResNet-50 c1 dgrads with the residual addend 827 vs 956 / 538 vs
-  // 575 us per step (profiles/r5_resnet_bn_dgrad_ab.txt).  Not for BNR 2 / 3
-  // (the ResNet BN-dgrad fusion: with the BN input preloaded as well its c1
-  // dgrad took 2122 instead of 1576 us per step, register pressure) nor BNR 1
+  // 575 us per step (profiles/r5_resnet_bn_dgrad_ab.txt).  Not for BNR 1
   // (the CIFAR region dgrad's pool windows: 24.3 vs 23.7-24.0 us)
   constexpr bool PA = ADD && BNR == 0;
   uint4 pad_[PA ? FM : 1][PA ? NP : 1];
@@ -645,31 +548,6 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
         const uint4 pk = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
                                     pack_bf16x2(v[6], v[7]));
         if (ok) *reinterpret_cast<uint4*>(y + (int64_t)m * g.Cout + n) = pk;
-        if constexpr (BNR == 2 || BNR == 3) {
-          if (ok) {
-            const uint4 xv4 = *reinterpret_cast<const uint4*>(br.y + (int64_t)m * g.Cout + n);
-            uint4 mv4 = xv4;
-            unsigned mbits = 0xffu;
-            if constexpr (BNR == 3) {
-              if (br.mb != nullptr) mbits = br.mb[(int64_t)m * (g.Cout >> 3) + (n >> 3)];
-              else mv4 = *reinterpret_cast<const uint4*>(br.ym + (int64_t)m * g.Cout + n);
-            }
-            const float mv[8] = {lo_bf16(mv4.x), hi_bf16(mv4.x), lo_bf16(mv4.y), hi_bf16(mv4.y),
-                                 lo_bf16(mv4.z), hi_bf16(mv4.z), lo_bf16(mv4.w), hi_bf16(mv4.w)};
-            const float gd[8] = {lo_bf16(pk.x), hi_bf16(pk.x), lo_bf16(pk.y), hi_bf16(pk.y),
-                                 lo_bf16(pk.z), hi_bf16(pk.z), lo_bf16(pk.w), hi_bf16(pk.w)};
-            const float xv[8] = {lo_bf16(xv4.x), hi_bf16(xv4.x), lo_bf16(xv4.y), hi_bf16(xv4.y),
-                                 lo_bf16(xv4.z), hi_bf16(xv4.z), lo_bf16(xv4.w), hi_bf16(xv4.w)};
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              const bool pos = BNR == 3 ? (br.mb != nullptr ? ((mbits >> k) & 1u) != 0u : mv[k] > 0.f)
-                                        : fmaf(xv[k], rsc[q][k], rsh[q][k]) > 0.f;
-              const float gk = pos ? gd[k] : 0.f;
-              s1[q][k] += gk;
-              s2[q][k] = fmaf(gk, (xv[k] - rmu[q][k]) * ris[q][k], s2[q][k]);
-            }
-          }
-        }
         if constexpr (BNR == 1) {
           if (ok) {
             // pooled pixel m = (b, oh, ow) of the [B][H][W] dgrad output; its window in y
@@ -728,22 +606,6 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
     for (int q = 0; q < NP; ++q)
 #pragma unroll
       for (int k = 0; k < 8; ++k) { s1[q][k] = row16_sum(s1[q][k]); s2[q][k] = row16_sum(s2[q][k]); }
-    if constexpr (STATS && !BNRED) {
-      if (g.swave) {  // per-wave-row partial rows: lane 15 of each 16-lane group holds 8 channels' sums
-        if ((lane & 15) == 15) {
-          float* r0 = stats + ((int64_t)tm * WM + wm) * 2 * g.Cout + n0 + nl;
-#pragma unroll
-          for (int q = 0; q < NP; ++q) {
-            *reinterpret_cast<float4*>(r0 + 32 * q) = make_float4(s1[q][0], s1[q][1], s1[q][2], s1[q][3]);
-            *reinterpret_cast<float4*>(r0 + 32 * q + 4) = make_float4(s1[q][4], s1[q][5], s1[q][6], s1[q][7]);
-            *reinterpret_cast<float4*>(r0 + g.Cout + 32 * q) = make_float4(s2[q][0], s2[q][1], s2[q][2], s2[q][3]);
-            *reinterpret_cast<float4*>(r0 + g.Cout + 32 * q + 4) =
-                make_float4(s2[q][4], s2[q][5], s2[q][6], s2[q][7]);
-          }
-        }
-        return;
-      }
-    }
     // LDS-only barriers: __syncthreads() would also wait for this wave's output
     // stores (vmcnt(0)) before the tile's statistics, exposing their latency per
     // tile.  No LDS-DMA is in flight (waited above); the ring's reads are lgkm.
@@ -763,10 +625,7 @@ __device__ __forceinline__ void conv_fwd_epilogue_t(const f32x4 (&acc)[FM][FN], 
       float sa = 0.f, sb = 0.f;
 #pragma unroll
       for (int q = 0; q < WM; ++q) { sa += red[(q * 2) * BN + c]; sb += red[(q * 2 + 1) * BN + c]; }
-      if constexpr (BNR >= 2) {  // deterministic partial row per M tile (bn_rows_reduce follows)
-        br.rows[(int64_t)tm * 2 * g.Cout + n0 + c] = sa;
-        br.rows[(int64_t)tm * 2 * g.Cout + g.Cout + n0 + c] = sb;
-      } else if constexpr (BNR == 1) {
+      if constexpr (BNR == 1) {
         // sa = sum dz, sb = sum dz*xhat; atomic rows hold [dgamma; dbeta] (the reduce's layouts)
         if (g_red_atomic) put_stats(br.rows, tm, g.Cout, n0 + c, sb, sa);
         else put_stats(br.rows, tm, g.Cout, n0 + c, sa, sb);
@@ -935,14 +794,13 @@ __device__ __forceinline__ bool splitk_fixup(f32x4 (&acc)[FM][FN], const ConvGeo
 // slices, the reducer of each tile runs the plain (STATS / BNR) epilogue;
 // fixcnt = the launch's per-tile arrival counters.
 template <int BM, int BN, bool STATS, bool SLAB, bool TAPU, int STAGES, int WM = 2, int WN = 2, bool ADD = false,
-          bool TRP = true, int BNR = 0, bool OL = false, bool FIX = false>
+          bool TRP = true, int BNR = 0, bool FIX = false>
 __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                        bf16_t* __restrict__ y, float* __restrict__ stats,
                                                        float* __restrict__ slab, const ConvGeom g, int splits,
                                                        int kt_per_split, unsigned long long* dbg,
                                                        const BnRedArgs br = BnRedArgs{},
                                                        const SgdJob side = SgdJob{},
-                                                       const BnOnLoad ol = BnOnLoad{},
                                                        int* __restrict__ fixcnt = nullptr) {
   // side job (set_conv_side_sgd): the last side.nblk workgroups run part of
   // the step's SGD update on the CUs the convolution's one-workgroup-per-CU
@@ -968,8 +826,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   constexpr bool TR = TRP && FN % 2 == 0;
   static_assert(A_INS >= 1 && B_INS >= 1, "tile too small");
   static_assert(A_INS * NW * 1024 == A_BYTES && B_INS * NW * 1024 == B_BYTES, "DMA split");
-  // (OL: + the on-load scale / shift table past the ring)
-  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES + (OL ? 2 * kOlMaxC * 4 : 0)];
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -979,32 +836,15 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   // swizzle) share one (n-tile, K-split) weight panel and sweep the M tiles,
   // so the panel is fetched into that XCD's L2 once instead of every XCD
   // streaming the whole weight tensor from the Infinity Cache.
-  int tm, tn, split, nsp_b = 0;
-  if (TAPU && g.posm && g.pm_kmax > 0) {
-    // balanced position-major split-K: N tile tn owns pm_P workgroups; pixel
-    // pos gets nbt * nsp(pos) of them, nsp(pos) = ceil(nk(pos) / pm_kmax)
-    const int id = xcd_swizzle(blockIdx.x, conv_grid);
-    const int nbt = g.B / BM;
-    tn = id / g.pm_P;
-    int r = id - tn * g.pm_P, pos = 0, nsp = 1;
-    for (; pos < g.H * g.W - 1; ++pos) {
-      nsp = (posm_nk(g, pos) + g.pm_kmax - 1) / g.pm_kmax;
-      if (r < nbt * nsp) break;
-      r -= nbt * nsp;
-    }
-    if (pos == g.H * g.W - 1) nsp = (posm_nk(g, pos) + g.pm_kmax - 1) / g.pm_kmax;
-    const int bblk = r / nsp;
-    split = r - bblk * nsp;
-    tm = pos * nbt + bblk;
-    nsp_b = nsp;
-  } else {
-    const int npanel = (g.Cout / BN) * splits;
-    const int id = xcd_swizzle(blockIdx.x, ntm * npanel);
-    tm = g.mmajor ? id / npanel : id % ntm;
-    const int panel = g.mmajor ? id - tm * npanel : id / ntm;
-    split = panel % splits;
-    tn = panel / splits;
-  }
+  // (M-tile-major measured 0.8 % slower, r2_fwd_order_ab.txt; per-pixel
+  // balanced position-major split-K no faster, r2_posm_balance_ab.txt: both
+  // removed in round 6)
+  const int npanel = (g.Cout / BN) * splits;
+  const int id = xcd_swizzle(blockIdx.x, ntm * npanel);
+  const int tm = id % ntm;
+  const int panel = id / ntm;
+  const int split = panel % splits;
+  const int tn = panel / splits;
   const int m0 = tm * BM, n0 = tn * BN;
   const int C8 = 1 << g.logC8;
   // Position-major tiles (g.posm, host-enabled for TAPU layers whose output is
@@ -1024,8 +864,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
     kw0 = max(0, g.pad - ow);
     kw1 = min(g.KS, g.W + g.pad - ow);
     nkt_total = (kh1 - kh0) * (kw1 - kw0) * (g.Cin / BK);
-    const int ns = nsp_b > 0 ? nsp_b : splits;
-    ktps = (nkt_total + ns - 1) / ns;
+    ktps = (nkt_total + splits - 1) / splits;
   }
   const int kt_beg = split * ktps;
   const int kt_end = min(nkt_total, kt_beg + ktps);
@@ -1129,33 +968,6 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  float* olt = reinterpret_cast<float*>(smem + STAGES * STAGE_BYTES);  // OL: scale [kOlMaxC], shift [kOlMaxC]
-  if constexpr (OL) {
-    // the BN coefficients (bn_nhwc.hip stats8 + fwd apply arithmetic); visible to
-    // every wave after the first K step's barrier
-    const float invM = 1.f / (float)ol.M;
-    for (int c = tid; c < ol.C; c += 64 * NW) {
-      const float m = ol.acc[c] * invM;
-      const float var = fmaxf(fmaf(-m, m, ol.acc[ol.C + c] * invM), 0.f);  // (as bn_nhwc.hip var_of)
-      const float is = rsqrtf(var + ol.eps);
-      const float sc = ol.w[c] * is;
-      olt[c] = sc;
-      olt[kOlMaxC + c] = fmaf(-m, sc, ol.b[c]);
-      if (blockIdx.x == 0) {
-        ol.save[c] = m;
-        ol.save[ol.C + c] = is;
-        if (ol.rmean != nullptr) {
-          const float unbias = ol.M > 1 ? (float)ol.M / (float)(ol.M - 1) : 1.f;
-          // (explicit fmas, as bn_nhwc.hip bn_coef8)
-          const float keep_m = (1.f - ol.momentum) * ol.rmean[c], keep_v = (1.f - ol.momentum) * ol.rvar[c];
-          ol.rmean[c] = fmaf(ol.momentum, m, keep_m);
-          ol.rvar[c] = fmaf(ol.momentum, var * unbias, keep_v);
-        }
-      }
-    }
-  }
-  const bool ol_store = OL && tn == 0 && wn == 0;  // one writer per activation element
 
   const unsigned long long t_setup = dbg ? stamp() : 0ull;
   // Fragment-prefetch pipeline (g_fwd_pf, STAGES >= 3): every step issues one
@@ -1296,31 +1108,6 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
           bfr[kk][b] = __builtin_bit_cast(bf16x8, Bs[row * CPR + (ch ^ swz_b(row))]);
         }
       }
-      if constexpr (OL) {  // A = relu(scale * y + shift), 8 channels per fragment (1x1: step = 64 channels)
-        const int cstep = (kt_beg + i) * BK;
-#pragma unroll
-        for (int kk = 0; kk < BK / 32; ++kk) {
-          const int c = cstep + (kk * 4 + (lane >> 4)) * 8;
-          const float4 s0 = *reinterpret_cast<const float4*>(olt + c), s1 = *reinterpret_cast<const float4*>(olt + c + 4);
-          const float4 h0 = *reinterpret_cast<const float4*>(olt + kOlMaxC + c);
-          const float4 h1 = *reinterpret_cast<const float4*>(olt + kOlMaxC + c + 4);
-          const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-          const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-#pragma unroll
-          for (int a = 0; a < FM; ++a) {
-            float f[8];
-            unpack8(__builtin_bit_cast(uint4, af[kk][a]), f);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], sc[k], sh[k]), 0.f);
-            const uint4 v = pack8(f);
-            af[kk][a] = __builtin_bit_cast(bf16x8, v);
-            if (ol_store) {
-              const int m = m0 + wm * TM + a * 16 + (lane & 15);
-              if (m < g.M) *reinterpret_cast<uint4*>(ol.out + (int64_t)m * ol.C + c) = v;
-            }
-          }
-        }
-      }
       // the next stage's LDS-DMA issues ride between the MFMAs (their issue cost
       // overlaps matrix-core execution instead of serialising in front of it)
 #pragma unroll
@@ -1362,7 +1149,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   };
   static_assert(BNR == 0 || TR, "the fused BN reduce needs the transposed epilogue");
   if constexpr (FIX) {
-    static_assert(TR && !SLAB && !ADD && !OL, "FIX: transposed plain epilogue after the in-launch combine");
+    static_assert(TR && !SLAB && !ADD, "FIX: transposed plain epilogue after the in-launch combine");
     if (!splitk_fixup<BM, BN, WM, WN, FM, FN>(acc, g, slab, split, splits, m0, n0, pm_b0, pm_pos, fixcnt + tn * ntm + tm,
                                               smem)) {
       dbg_out();
@@ -1408,13 +1195,13 @@ struct RegionGeom {
 };
 
 
-template <int BN, bool STATS, bool SLAB, int STAGES, int WM, int WN, bool BNRED = false, bool PL = false>
+template <int BN, bool STATS, bool SLAB, int STAGES, int WM, int WN, bool BNRED = false>
 __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf16_t* __restrict__ x,
                                                               const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
                                                               float* __restrict__ stats, float* __restrict__ slab,
                                                               const ConvGeom g, const RegionGeom rg, int splits,
                                                               unsigned long long* dbg, int ablate,
-                                                              const BnRedArgs br, const PoolLoad pl = PoolLoad{}) {
+                                                              const BnRedArgs br) {
   const unsigned long long t_start = dbg ? stamp() : 0ull;
   constexpr int BM = 128, BK = 64, CPR = 8, NW = WM * WN, PD = STAGES - 1;
   constexpr int B_BYTES = BN * BK * 2, B_INS = B_BYTES / 1024 / NW, LPS = B_INS;
@@ -1433,8 +1220,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf1
   const int ntm = (g.M + BM - 1) / BM;
   const int npanel = (g.Cout / BN) * splits;
   const int id = xcd_swizzle(blockIdx.x, ntm * npanel);
-  const int tm = g.mmajor ? id / npanel : id % ntm;
-  const int panel = g.mmajor ? id - tm * npanel : id / ntm;
+  const int tm = id % ntm;
+  const int panel = id / ntm;
   const int split = panel % splits, tn = panel / splits;
   const int m0 = tm * BM, n0 = tn * BN;
   const int HW = 1 << g.logHW, Wd = g.W;
@@ -1448,7 +1235,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf1
   const int cbase = split * rg.cpw;  // first 64-channel chunk of this workgroup
 
   // ---- region loads (once per chunk): lane-linear slots -> source pixel/chunk
-  if constexpr (!PL) {
+  {
     const int nq = rg.nslot >> 6;
     // slot -> (region row R, pixel in row, chunk): the region's image rows
     // are consecutive padded rows (rows mode: RH rows of one image; images
@@ -1528,63 +1315,6 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf1
 #pragma unroll
     for (int q = 0; q < LPS; ++q) issue_b(q, ld_k < nk);
     advance_ld();
-  }
-  if constexpr (PL) {
-    // ---- pool-on-load region fill (the weight stages above are in flight).
-    // One 64-channel chunk (cpw == 1, host-checked); every slot of a thread
-    // (<= kPlSlots) has its 4 window loads issued before the coefficient
-    // prologue and the first use: one memory round trip for the whole fill
-    // (a loop with one slot of lookahead paid one per slot).
-    constexpr int NT = 64 * NW;
-    __shared__ __attribute__((aligned(16))) float ssc[64], ssh[64];
-    const int nrows = rg.nimg * rg.RH;
-    const int H2 = 2 * g.H, W2 = 2 * g.W;
-    const bool owner = tn == 0 && split == 0;  // one workgroup per M tile writes pout
-    const int own_lo = rg.rows_mode ? oh0 : 0, own_hi = rg.rows_mode ? oh0 + BM / g.W : g.H;
-    const int rowC = W2 * g.Cin;
-    int src[kPlSlots], dpix[kPlSlots];
-#pragma unroll
-    for (int k = 0; k < kPlSlots; ++k) {
-      // slot -> source element of y (-1: a zero slot) and the pout pixel (-1: none)
-      const int sl = tid + k * NT;
-      src[k] = -1;
-      dpix[k] = -1;
-      const int R = (int)(((float)sl + 0.5f) * rg.inv_RS);
-      const int r2 = sl - R * rg.RS;
-      const int col = (r2 * 6554) >> 16;  // r2 / 10 (S == 10)
-      const int ch = r2 - col * 10;
-      if (sl < rg.nslot && R < nrows && col < rg.RW && ch < 8) {
-        const int pix = start_pix + R * g.Wp + col;  // padded input pixel
-        const int img = pix / HpWp, rem = pix - img * HpWp;
-        const int pr = rem / g.Wp, ih = pr - g.pad, iw = rem - pr * g.Wp - g.pad;
-        if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) {
-          src[k] = ((img * H2 + 2 * ih) * W2 + 2 * iw) * g.Cin + cbase * 64 + ch * 8;
-          if (owner && ih >= own_lo && ih < own_hi) dpix[k] = pix;
-        }
-      }
-    }
-    uint4 v[kPlSlots][4];
-#pragma unroll
-    for (int k = 0; k < kPlSlots; ++k) {
-      const bf16_t* p = pl.y + (src[k] >= 0 ? src[k] : 0);
-      v[k][0] = *reinterpret_cast<const uint4*>(p);
-      v[k][1] = *reinterpret_cast<const uint4*>(p + g.Cin);
-      v[k][2] = *reinterpret_cast<const uint4*>(p + rowC);
-      v[k][3] = *reinterpret_cast<const uint4*>(p + rowC + g.Cin);
-    }
-    bn_fin_block(pl.fin, g.Cin, ssc, ssh);  // (rows summed behind the window loads; ends with a barrier)
-#pragma unroll
-    for (int k = 0; k < kPlSlots; ++k) {
-      const int sl = tid + k * NT;
-      if (sl >= rg.nslot) break;
-      uint4 o = make_uint4(0u, 0u, 0u, 0u);
-      if (src[k] >= 0) {
-        const int cc = src[k] & 63;  // first of the slot's 8 channels (Cin == 64)
-        o = bn_relu_pool8(v[k][0], v[k][1], v[k][2], v[k][3], ssc + cc, ssh + cc);
-        if (dpix[k] >= 0) *reinterpret_cast<uint4*>(pl.pout + (int64_t)dpix[k] * g.Cin + cc) = o;
-      }
-      *reinterpret_cast<uint4*>(sR + sl * 16) = o;
-    }
   }
   const unsigned long long t_issued = dbg ? stamp() : 0ull;
 
@@ -1681,200 +1411,6 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_kernel(const bf1
 constexpr int vmcnt_imm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x70 | 0xF00; }
 
 // --------------------------------------------------------------------------
-// Region kernel with the weight operand loaded straight into registers
-// ("direct B").  The region kernel above streams the weight tile through an
-// LDS ring: per k-step each wave issues LDS-DMA pieces (60-185 issue cycles
-// each among MFMAs, MI355X_MICROARCH.md), waits for the stage, joins a
-// workgroup barrier, and reads both operands back from LDS -- at 8 waves of
-// 32 x 32 (or 64 x 32) wave tiles the LDS traffic per k-step exceeds the
-// MFMA time (fwd2: ~1,700 cycles per k-step vs 512 of MFMA per SIMD).  Here
-// only the activation region lives in LDS (filled once, read-only after one
-// barrier): every wave loads ITS weight fragments (the MFMA A operand of the
-// transposed accumulator) with 16-byte buffer loads into a D-deep register
-// queue, D k-steps ahead, and reads its activation fragments from the region
-// one k-step ahead -- no barrier and no LDS-DMA in the k-loop, wider wave
-// tiles (4 waves: 128 x 32 or 64 x 32) so each LDS byte feeds more MFMAs.
-// Same arithmetic, fragment layouts and epilogue as the region kernel.
-// --------------------------------------------------------------------------
-template <int BN, int WM, int WN, int D, int NK, bool STATS, bool SLAB, bool BNRED = false>
-__global__ void __launch_bounds__(64 * WM * WN) conv_fwd_region_bd_kernel(
-    const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y, float* __restrict__ stats,
-    float* __restrict__ slab, const ConvGeom g, const RegionGeom rg, int splits, unsigned long long* dbg,
-    const BnRedArgs br) {
-  const unsigned long long t_start = dbg ? stamp() : 0ull;
-  constexpr int BM = 128, BK = 64, NW = WM * WN;
-  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
-  constexpr int NB = (BK / 32) * FN;  // weight loads per k-step per lane
-  static_assert(FN % 2 == 0, "the 16-byte epilogue pairs N fragments");
-  static_assert(D * NB < 64, "vmcnt range");
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int region_bytes = rg.nslot * 16;
-  char* sR = smem;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / WN, wn = wid % WN;
-  const int ntm = (g.M + BM - 1) / BM;
-  const int npanel = (g.Cout / BN) * splits;
-  const int id = xcd_swizzle(blockIdx.x, ntm * npanel);
-  const int tm = g.mmajor ? id / npanel : id % ntm;
-  const int panel = g.mmajor ? id - tm * npanel : id / ntm;
-  const int split = panel % splits, tn = panel / splits;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int HW = 1 << g.logHW, Wd = g.W;
-  const int taps = g.KS * g.KS;
-  // NK: the k-step count (cpw x taps) as a compile-time constant -- a static
-  // trip count and tail keep the accumulators in fixed registers
-  constexpr int nk = NK;
-  const int img0 = m0 >> g.logHW, oh0 = (m0 & (HW - 1)) >> g.logW;
-  const int start_pix = img0 * g.Hp * g.Wp + oh0 * g.Wp;
-  const int cbase = split * rg.cpw;
-
-  // ---- region fill (asm LDS-DMA: invisible to the compiler's LDS-DMA alias
-  // waits, which would otherwise drain the weight queue at every fragment read)
-  {
-    const i32x4 xr4 = make_rsrc4(x, (unsigned)((int64_t)g.B * g.Hp * g.Wp * g.Cin * 2));
-    const int nq = rg.nslot >> 6;
-    const int nrows = rg.nimg * rg.RH;
-    for (int q = wid; q < nq; q += NW) {
-      const int sl = q * 64 + lane;
-      const int R = (int)(((float)sl + 0.5f) * rg.inv_RS);
-      const int r2 = sl - R * rg.RS;
-      const int col = (r2 * 6554) >> 16;  // r2 / 10 (exact for r2 < 16384; S == 10)
-      const int ch = r2 - col * 10;
-      const bool ok = R < nrows && col < rg.RW && ch < 8;
-      const int pix = start_pix + R * g.Wp + col;
-      const unsigned voff = ok ? 2u * (unsigned)(pix * g.Cin + ch * 8) : kOOB;
-      for (int c = 0; c < rg.cpw; ++c)
-        blds16_asm(xr4, voff, 2u * (unsigned)((cbase + c) * 64), sR + c * region_bytes + q * 1024);
-    }
-  }
-
-  // ---- weight fragments: lane row n0 + wn*TN + b_frag_row(b, l&15), 8 channels
-  // at k = (step's k offset) + 8 * (4 kk + (l >> 4))
-  const rsrc_t wr = make_rsrc(w, (unsigned)((int64_t)g.Cout * g.K * 2));
-  unsigned bv[BK / 32][FN];
-#pragma unroll
-  for (int kk = 0; kk < BK / 32; ++kk)
-#pragma unroll
-    for (int b = 0; b < FN; ++b) {
-      const int row = n0 + wn * TN + b_frag_row(b, lane & 15);
-      bv[kk][b] = 2u * (unsigned)(row * g.K + (kk * 4 + (lane >> 4)) * 8);
-    }
-  int ld_s = 0, ld_c = 0, ld_t = 0;  // next k-step to load (wave-uniform)
-  bf16x8 bq[D][BK / 32][FN];
-  auto load_b = [&](bf16x8 (&dst)[BK / 32][FN]) {
-    const bool live = ld_s < nk;
-    const int soff = 2 * (ld_t * g.Cin + (cbase + ld_c) * 64);
-#pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk)
-#pragma unroll
-      for (int b = 0; b < FN; ++b)
-        dst[kk][b] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                                    wr, live ? (int)bv[kk][b] : (int)kOOB, soff, 0));
-    ++ld_s;  // branch-free advance
-    ++ld_t;
-    const int wrap = ld_t == taps;
-    ld_t -= wrap * taps;
-    ld_c = min(ld_c + wrap, rg.cpw - 1);
-  };
-#pragma unroll
-  for (int q = 0; q < D; ++q) load_b(bq[q]);
-
-  // ---- activation fragment bases (slot of the tap-(0,0) pixel + lane chunk)
-  int a_base[FM];
-#pragma unroll
-  for (int a = 0; a < FM; ++a) {
-    const int m = min(m0 + wm * TM + a * 16 + (lane & 15), g.M - 1);
-    const int im = (m >> g.logHW) - img0;
-    const int oh = ((m & (HW - 1)) >> g.logW) - oh0;
-    const int ow = m & (Wd - 1);
-    a_base[a] = (im * rg.IS + oh * rg.RS + ow * rg.S + (lane >> 4)) * 16;
-  }
-  int rc = 0, rkh = 0, rkw = 0;  // k-step whose activation fragments are read next
-  auto read_a = [&](bf16x8 (&fa)[BK / 32][FM]) {
-    const char* As = sR + rc * region_bytes + (rkh * rg.RS + rkw * rg.S) * 16;  // wave-uniform tap offset
-#pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk)
-#pragma unroll
-      for (int a = 0; a < FM; ++a) fa[kk][a] = *reinterpret_cast<const bf16x8*>(As + a_base[a] + kk * 64);
-    ++rkw;  // branch-free advance
-    const int ww = rkw == g.KS;
-    rkw -= ww * g.KS;
-    rkh += ww;
-    const int wh = rkh == g.KS;
-    rkh -= wh * g.KS;
-    rc = min(rc + wh, rg.cpw - 1);
-  };
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // the region (older than the D weight stages) landed for this wave, then for all
-  __builtin_amdgcn_s_waitcnt(vmcnt_imm(D * NB));
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-  const unsigned long long t_first = dbg ? stamp() : 0ull;
-  // activation fragments ping-pong between fa0 / fa1 (D is even: the parity
-  // of a step is static in the unrolled body, no register copies)
-  static_assert(D % 2 == 0, "even weight queue depth");
-  constexpr int NRD = (BK / 32) * FM;       // activation fragment reads per step
-  constexpr int NMF = (BK / 32) * FM * FN;  // MFMAs per step
-  bf16x8 fa0[BK / 32][FM], fa1[BK / 32][FM];
-  read_a(fa0);
-  auto step = [&](bf16x8 (&fc)[BK / 32][FM], bf16x8 (&fn)[BK / 32][FM], bf16x8 (&bs)[BK / 32][FN]) {
-    read_a(fn);  // the next k-step's activation fragments while this step's MFMAs run
-#pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk)
-#pragma unroll
-      for (int a = 0; a < FM; ++a)
-#pragma unroll
-        for (int b = 0; b < FN; ++b) acc[a][b] = mfma16(bs[kk][b], fc[kk][a], acc[a][b]);
-    load_b(bs);  // k-step s + D into the slot just consumed
-    // issue order: (MFMA, fragment read) pairs, then (MFMA, weight load) pairs, the rest
-    constexpr int P1 = NRD < NMF ? NRD : NMF;
-    constexpr int P2 = NB < NMF - P1 ? NB : NMF - P1;
-#pragma unroll
-    for (int q = 0; q < P1; ++q) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-    if constexpr (NRD > P1) __builtin_amdgcn_sched_group_barrier(0x100, NRD - P1, 0);
-#pragma unroll
-    for (int q = 0; q < P2; ++q) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-    }
-    if constexpr (NB > P2) __builtin_amdgcn_sched_group_barrier(0x020, NB - P2, 0);
-    if constexpr (NMF - P1 - P2 > 0) __builtin_amdgcn_sched_group_barrier(0x008, NMF - P1 - P2, 0);
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  for (int s0 = 0; s0 + D <= nk; s0 += D) {
-#pragma unroll
-    for (int q = 0; q < D; q += 2) {
-      step(fa0, fa1, bq[q]);
-      step(fa1, fa0, bq[q + 1]);
-    }
-  }
-  // the remaining nk % D steps (their weight stages are the first slots of the queue)
-  constexpr int R = nk % D;
-  if constexpr (R > 0) step(fa0, fa1, bq[0]);
-  if constexpr (R > 1) step(fa1, fa0, bq[1]);
-  if constexpr (R > 2) step(fa0, fa1, bq[2]);
-  static_assert(D <= 4, "the static tail covers up to 3 steps");
-  const unsigned long long t_loop = dbg ? stamp() : 0ull;
-  conv_fwd_epilogue_t<128, BN, STATS, SLAB, WM, WN, FM, FN, false, BNRED ? 1 : 0>(acc, g, y, stats, slab, split, tm,
-                                                                                 m0, n0, smem, 0, 0, br);
-  if (dbg && threadIdx.x == 0) {
-    unsigned long long* d = dbg + (size_t)blockIdx.x * 5;
-    d[0] = t_start; d[1] = t_start; d[2] = t_first; d[3] = t_loop; d[4] = stamp();
-  }
-}
-
-// --------------------------------------------------------------------------
 // First layer (Cin = 8 after the 3 -> 8 channel pad; K = KS*KS*8 = 200): the
 // whole problem of a workgroup fits in LDS at once -- its 128 output pixels'
 // padded input rows (16 B per pixel) and the 64 x K weight panel -- so it is
@@ -1967,124 +1503,11 @@ __global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restri
   }
 }
 
-// --------------------------------------------------------------------------
-// First-layer weight gradient (Cin = 8, K = taps * 8 <= 208) from an LDS-
-// resident input region.  The generic wgrad gathers the im2col rows of x
-// through the L2 for every 64-column K tile: for the reference's layer 1 that
-// is 4 tiles x (8 KB dy + 8 KB im2col) per 64-pixel step, and every conv loop
-// here runs at the L2->CU rate.  A workgroup of this kernel owns a band of R
-// output rows of one image and the WHOLE 64 x 208 weight-gradient tile:
-//   * its padded input rows (R + KS - 1 rows x Wp pixels x 16 B) are DMA'd
-//     into LDS once, and every tap's B fragment is read from there with
-//     ds_read_b64_tr_b16 at the tap's pixel offset (no im2col in memory);
-//   * only dy streams, 64 pixels (8 KB) per step through a 3-stage ring,
-//     read as the other operand with the same transposed reads;
-// so a step moves 8 KB of dy instead of 64 KB, and x is read ~1.25x in total.
-// Waves: wm = wid & 3 owns 16 output channels, wk = wid >> 2 the K fragments
-// wk, wk + 2, ... (fragment j = taps 2j, 2j + 1; taps past KS*KS read a zero
-// slot).  Output: fp32 slab [band][Cout][ldo] (one split per band), the
-// layout of conv_wgrad's slabs.
-// --------------------------------------------------------------------------
-template <int ST>
-__global__ void __launch_bounds__(512) conv_wgrad_c8r_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
-                                                             float* __restrict__ out, const ConvGeom g, int R, int ldo) {
-  constexpr int NW = 8, BK = 64, NKF = 7;  // 13 K fragments over 2 wave columns
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid & 3, wk = wid >> 2;
-  const int taps = g.KS * g.KS, nkf = (taps + 1) / 2;
-  const int bands = g.H / R;
-  const int img = blockIdx.x / bands, R0 = (blockIdx.x - img * bands) * R;
-  const int rrows = R + g.KS - 1;
-  const int rslots = rrows * g.Wp;                   // region pixels (16 B each)
-  const int rslots_p = (rslots + 1 + 63) / 64 * 64;  // + >= 1 zero slot, whole DMA pieces
-  char* sR = smem;
-  char* sD = smem + rslots_p * 16;  // dy ring: ST x [64 px][8 chunks] (swz_tr<8>)
-  // (all LDS-DMA from asm: a builtin one in flight makes hipcc drain vmcnt before every tr read)
-  const i32x4 xr = make_rsrc4(x, (unsigned)((int64_t)g.B * g.Hp * g.Wp * 16));
-  const i32x4 dyr = make_rsrc4(dy, (unsigned)((int64_t)g.B * g.Hp * g.Wp * g.Cout * 2));
-  const int start_pix = (img * g.Hp + R0) * g.Wp;
-  const int npieces = rslots_p / 64;  // region DMA pieces: waves 0 .. npieces % NW - 1 issue one more
-  for (int q = wid; q < npieces; q += NW) {
-    const int sl = q * 64 + lane;
-    blds16_asm(xr, sl < rslots ? 16u * (unsigned)(start_pix + sl) : kOOB, 0u, sR + q * 1024);
-  }
-  // dy lanes: 8 rows (pixels) x 8 chunks per wave instruction, one per wave per step
-  const int drow = 8 * wid + lane / 8;
-  const int dch = swz_tr<8>(drow, lane % 8) - drow * 8;  // logical chunk of this LDS slot (involution)
-  const int nsteps = R * g.W / BK;
-  auto issue = [&](int s, int slot) {
-    const int px = s * BK + drow;  // band-local output pixel
-    const int oh = R0 + (px >> g.logW), ow = px & (g.W - 1);
-    const unsigned v = s < nsteps ? 2u * (unsigned)(((img * g.Hp + oh + g.pad) * g.Wp + ow + g.pad) * g.Cout + dch * 8)
-                                  : kOOB;
-    blds16_asm(dyr, v, 0u, sD + slot * (BK * 128) + wid * 1024);
-  };
-#pragma unroll
-  for (int p = 0; p < ST - 1; ++p) issue(p, p);
-  f32x4 acc[NKF];
-#pragma unroll
-  for (int t = 0; t < NKF; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int gq = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
-  // per K fragment: this lane's tap offset (region slots) and byte offset in the 16-B pixel
-  int toff[NKF], tsub[NKF];
-#pragma unroll
-  for (int t = 0; t < NKF; ++t) {
-    const int jf = wk + 2 * t, k = jf * 16 + 4 * p4, tap = k >> 3;
-    const int kh = tap / g.KS, kw = tap - kh * g.KS;
-    toff[t] = (jf < nkf && tap < taps) ? kh * g.Wp + kw : -1;
-    tsub[t] = (k & 7) * 2;
-  }
-  const int zero_byte = rslots * 16;
-  int slot = 0;
-  for (int s = 0; s < nsteps; ++s) {
-    wait_vmcnt<ST - 2>();  // stage s landed (and, at s = 0, the region: issued before every stage)
-    block_sync_lds();
-    issue(s + ST - 1, (slot + ST - 1) % ST);
-    const char* D = sD + slot * (BK * 128);
-#pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
-      const int r0 = kk * 32 + gq * 8 + q4;
-      const int col = wm * 16 + 4 * p4, ch = col >> 3, sub = (col & 7) * 2;
-      const s16x4 alo = ds_read_tr16(D + swz_tr<8>(r0, ch) * 16 + sub);
-      const s16x4 ahi = ds_read_tr16(D + swz_tr<8>(r0 + 4, ch) * 16 + sub);
-      const bf16x8 fa = bf16x8{alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]};
-      // band-local pixels s*64 + r0 (lo) and + 4 (hi): region slot of tap (0, 0)
-      const int plo = s * BK + r0, phi = plo + 4;
-      const int slo = (plo >> g.logW) * g.Wp + (plo & (g.W - 1)), shi = (phi >> g.logW) * g.Wp + (phi & (g.W - 1));
-#pragma unroll
-      for (int t = 0; t < NKF; ++t) {
-        if (wk + 2 * t >= nkf) break;
-        const int blo = toff[t] >= 0 ? (slo + toff[t]) * 16 + tsub[t] : zero_byte;
-        const int bhi = toff[t] >= 0 ? (shi + toff[t]) * 16 + tsub[t] : zero_byte;
-        const s16x4 lo = ds_read_tr16(sR + blo), hi = ds_read_tr16(sR + bhi);
-        const bf16x8 fb = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        acc[t] = mfma16(fb, fa, acc[t]);  // C^T: lane holds 4 consecutive k of one co
-      }
-    }
-    slot = slot + 1 == ST ? 0 : slot + 1;
-  }
-  wait_vmcnt<0>();  // the trailing zero-fill DMAs target the ring
-  // slab[band][co][k]: lane (rq, col_l) holds k = 16 jf + 4 rq + 0..3 of co = 16 wm + col_l
-  float* o = out + (int64_t)blockIdx.x * g.Cout * ldo;
-  const int col_l = lane & 15, rq = lane >> 4;
-#pragma unroll
-  for (int t = 0; t < NKF; ++t) {
-    const int jf = wk + 2 * t;
-    const int k = jf * 16 + rq * 4, co = wm * 16 + col_l;
-    if (jf < nkf && k < g.K)
-      *reinterpret_cast<float4*>(o + (int64_t)co * ldo + k) = make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
-  }
-}
-
 // split-K combine: y = bf16(sum_s slab[s]) (+ BN partial sums, one row per block)
 template <bool STATS>
 __global__ void __launch_bounds__(256) splitk_combine_kernel(const float* __restrict__ slab, bf16_t* __restrict__ y,
                                                              float* __restrict__ stats, int splits, int M, int N,
                                                              int rows_per_block, const ConvGeom g) {
-  // g.pm_kmax > 0: balanced position-major split-K -- row m (output pixel
-  // m % HW) has nsp = ceil(nk / pm_kmax) written slices, not `splits`
   const int N8 = N >> 3;
   const int tpr = N8;                 // threads per row (one 8-column chunk each)
   const int rpi = 256 / tpr;          // rows per iteration
@@ -2096,7 +1519,7 @@ __global__ void __launch_bounds__(256) splitk_combine_kernel(const float* __rest
   for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
   if (rsub < rpi) {
     for (int m = r0 + rsub; m < r1; m += rpi) {
-      const int splits_m = g.pm_kmax > 0 ? (posm_nk(g, m % (g.H * g.W)) + g.pm_kmax - 1) / g.pm_kmax : splits;
+      const int splits_m = splits;
       float v[8];
       const float* p = slab + (int64_t)m * N + c8 * 8;
       {
@@ -2157,22 +1580,19 @@ __global__ void __launch_bounds__(256) splitk_combine_kernel(const float* __rest
 // Tiles are staged [m][col] (rows = the reduction index) by LDS-DMA and read
 // as MFMA operands with ds_read_b64_tr_b16.  BK = 64 rows of m per stage.
 // --------------------------------------------------------------------------
-// ATOM: split-K partials are atomically added straight into the zeroed fp32
-// weight gradient [Cout][taps][creal] (creal <= Cin drops zero-padded input
-// channels) -- no slab round trip and no slab_reduce launch.
-// wgrad slab stores staged through LDS as whole rows (set_conv_wgrad_stage_store; A/B)
-__constant__ int g_wgrad_stage_store = 1;
-// wgrad main-loop order (set_conv_wgrad_order; A/B): 1 = DMA issued before the fragment reads
-__constant__ int g_wgrad_order = 1;
 // DL_WGRAD_STAMPS builds only (diagnostics): per-workgroup s_memtime phase
 // sums of waves 0 and NW-1 -> [wg][2][6] = start, loop begin, sum of the
 // steps' wait+barrier, sum of the steps' issue work, loop end, end
 __device__ unsigned long long* g_wgrad_stamps = nullptr;
 
-template <int BM, int BN, int STAGES, int WM = 2, int WN = 2, bool PF = true, bool ATOM = false, int BK_ = 64>
+// (Removed in round 6 after losing their A/B: atomic split-K accumulation,
+// r2_mode1_timeline.txt; 256x128 tiles, r3_wgrad_tile256_ab.txt; position-major
+// steps, r5_wgrad_posm_ab.txt; the read-before-DMA loop order and the
+// read-then-compute loop, r3_wgrad_order_ab.txt.)
+template <int BM, int BN, int STAGES, int WM = 2, int WN = 2, int BK_ = 64>
 __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                          float* __restrict__ out, const ConvGeom g, int m_per_split,
-                                                         int ldo, int creal) {
+                                                         int ldo) {
   // dy and x are both spatially zero-padded [B][Hp][Wp][C] (dy: interior at
   // (pad, pad)).  A 64-row M step starts at a multiple of 64 output pixels;
   // with W | 64 and (H*W | 64 or 64 | H*W) the padded position of row r of the
@@ -2202,47 +1622,23 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const int ntm = g.Cout / BM, ntn = (g.Kch * 8 + BN - 1) / BN;
-  // 1-D grid (gridDim.y == 1): split-major XCD-aware order -- the workgroups of
-  // one K split (same dy rows, same x pixels, different taps / channel tiles)
-  // get consecutive ids after the swizzle, i.e. one XCD, so the split's rows
-  // are fetched into that XCD's L2 once instead of once per XCD.  2-D grid
-  // (x = tile, y = split; the earlier layout): a split's tiles land on
-  // (x + y * gridDim.x) % 8, i.e. on every XCD.
-  int tile, split;
-  if (gridDim.y == 1) {
-    const int id = xcd_swizzle(blockIdx.x, gridDim.x);
-    split = id / (ntm * ntn);
-    tile = id - split * (ntm * ntn);
-  } else {
-    tile = xcd_swizzle(blockIdx.x, ntm * ntn);
-    split = blockIdx.y;
-  }
+  // split-major XCD-aware order: the workgroups of one K split (same dy rows,
+  // same x pixels, different taps / channel tiles) get consecutive ids after
+  // the swizzle, i.e. one XCD, so the split's rows are fetched into that XCD's
+  // L2 once instead of once per XCD (wgrad1 15.3 -> 11.0 us, r2_wgrad_xcd_ab.txt)
+  const int id = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int split = id / (ntm * ntn);
+  const int tile = id - split * (ntm * ntn);
   const int tm = tile % ntm, tn = tile / ntm;
   const int co0 = tm * BM, k0 = tn * BN;
   const int mbeg = split * m_per_split;
   const int mend = min(g.M, mbeg + m_per_split);
   const int HW = 1 << g.logHW, Wd = g.W, C8 = 1 << g.logC8;
   const int HpWp = g.Hp * g.Wp;
-  // position-major steps (g.wposm): this tile's steps, balanced over the
-  // ceil(steps / wposm) workgroups it needs; a split past those has no work
-  int pm_beg = 0, pm_nk = 0, pm_ph0 = 0, pm_pw0 = 0, pm_npw = 1;
-  if (g.wposm) {
-    const int ntot = wgrad_posm_steps(g, k0, BN, pm_ph0, pm_pw0, pm_npw);
-    const int st = (ntot + g.wposm - 1) / g.wposm;
-    if (split < st) {
-      pm_beg = split * ntot / st;
-      pm_nk = (split + 1) * ntot / st - pm_beg;
-    } else if (g.wskip) {
-      return;  // nothing issued yet; its slab stays zero from allocation
-    }
-    if (pm_npw == 0) pm_npw = 1;  // (no steps: only the divisor below)
-  }
   // padded pixel offset of row r inside a 64-aligned step (pow2 H, W: the step's
   // pixel decomposes as wave-uniform step base + per-lane row part; otherwise
-  // every lane decomposes its own pixel each step, out_pix); position-major:
-  // row r is image r of the step's chunk
+  // every lane decomposes its own pixel each step, out_pix)
   auto lane_pix = [&](int r) {
-    if (g.wposm) return r * HpWp;
     return g.pow2 ? (r >> g.logHW) * HpWp + ((r & (HW - 1)) >> g.logW) * g.Wp + (r & (Wd - 1)) : 0;
   };
 
@@ -2285,19 +1681,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
     char* sB = sA + A_BYTES;
     const int ms = mbeg + kt * BK;  // 64-aligned first row of the step
     const int left = mend - ms;     // rows left (uniform)
-    if (g.wposm) {
-      // step kt of this workgroup: pixel q, image chunk c (chunk-minor)
-      const bool ok = kt < pm_nk;
-      const int idx = pm_beg + (ok ? kt : 0);
-      const int q = idx >> g.wlognbc, c = idx & ((1 << g.wlognbc) - 1);
-      const int qh = q / pm_npw;
-      const int u = c * BK * HpWp + (pm_ph0 + qh) * g.Wp + pm_pw0 + (q - qh * pm_npw);  // wave-uniform
-      const unsigned ua = 2u * (unsigned)(u * g.Cout), ub = 2u * (unsigned)(u * g.Cin);
-#pragma unroll
-      for (int j = 0; j < A_INS; ++j) blds16_asm(dyr, ok ? a_v[j] : kOOB, ua, sA + (wid * A_INS + j) * 1024);
-#pragma unroll
-      for (int j = 0; j < B_INS; ++j) blds16_asm(xr, ok ? b_v[j] : kOOB, ub, sB + (wid * B_INS + j) * 1024);
-    } else if (g.pow2) {
+    if (g.pow2) {
       const int u = (ms >> g.logHW) * HpWp + ((ms & (HW - 1)) >> g.logW) * g.Wp;  // wave-uniform
       const unsigned ua = 2u * (unsigned)(u * g.Cout), ub = 2u * (unsigned)(u * g.Cin);
 #pragma unroll
@@ -2331,13 +1715,11 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int gq = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
-  const int nk = g.wposm ? pm_nk : max(0, (mend - mbeg + BK - 1) / BK);
-  // PF: (as conv_fwd_region_kernel) every step issues one stage
-  // unconditionally, fragments of step i+1 are read (transposed LDS reads)
-  // while the MFMAs of step i run, interleaved 1:1 -- needs >= 4 stages to
-  // keep DMA lookahead.  !PF: read-then-compute per step, PD-1 stages in
-  // flight beyond the one being read (better at 3 stages / 2 WGs per CU).
-  static_assert(!PF || STAGES >= 3, "fragment prefetch needs >= 3 ring slots");
+  const int nk = max(0, (mend - mbeg + BK - 1) / BK);
+  // (as conv_fwd_region_kernel) every step issues one stage unconditionally,
+  // fragments of step i+1 are read (transposed LDS reads) while the MFMAs of
+  // step i run, interleaved 1:1 -- needs >= 4 stages to keep DMA lookahead
+  static_assert(STAGES >= 3, "fragment prefetch needs >= 3 ring slots");
 #pragma unroll
   for (int p = 0; p < PD; ++p) issue(p, p);
   int rslot = 0, dslot = PD % STAGES;
@@ -2370,30 +1752,15 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
   constexpr int NRD = (BK / 32) * (FM + FN) * 2;  // ds_read_b64_tr_b16 per step
   constexpr int NMF = (BK / 32) * FM * FN;
   bf16x8 fa0[BK / 32][FM], fb0[BK / 32][FN], fa1[BK / 32][FM], fb1[BK / 32][FN];
-  if constexpr (!PF) {
-    for (int i = 0; i < nk; ++i) {
-      wait_vmcnt<(PD - 1) * LPS>();  // stage i landed (loads past nk are zero-fill dummies)
-      block_sync_lds();
-      issue(i + PD, dslot);
-      ++dslot;
-      dslot -= (dslot == STAGES) * STAGES;
-      read_frags(fa0, fb0);
-#pragma unroll
-      for (int kk = 0; kk < BK / 32; ++kk)
-#pragma unroll
-        for (int a = 0; a < FM; ++a)
-#pragma unroll
-          for (int b = 0; b < FN; ++b) acc[a][b] = mfma16(fb0[kk][b], fa0[kk][a], acc[a][b]);
-    }
-  } else {
+  {
   wait_vmcnt<(PD - 1) * LPS>();  // stage 0 landed
   __builtin_amdgcn_s_waitcnt(0xC07F);
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   read_frags(fa0, fb0);
   int kt_next = PD;
-  // DMA_FIRST (g_wgrad_order = 1): the step's LDS-DMA is issued right after
-  // the barrier, BEFORE the fragment reads.  The asm DMA carries a memory
+  // The step's LDS-DMA is issued right after the barrier, BEFORE the
+  // fragment reads.  The asm DMA carries a memory
   // clobber, so reads issued before it cannot move past it: in the old order
   // (reads, DMA, MFMAs) the 24 reads were bunched ahead of all MFMAs and the
   // compiler hoisted the next step's lgkmcnt(0) + barrier to after the 4th
@@ -2401,9 +1768,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
   // with no reads beside them.  DMA first, the reads and MFMAs share one
   // scheduling region and interleave (MFMA, 2 reads) as the group barriers
   // ask, and a closing sched_barrier keeps the next barrier after them.
-  auto step = [&](auto dma_first, bf16x8 (&fca)[BK / 32][FM], bf16x8 (&fcb)[BK / 32][FN],
-                  bf16x8 (&fna)[BK / 32][FM], bf16x8 (&fnb)[BK / 32][FN]) {
-    constexpr bool DF = decltype(dma_first)::value;
+  auto step = [&](bf16x8 (&fca)[BK / 32][FM], bf16x8 (&fcb)[BK / 32][FN], bf16x8 (&fna)[BK / 32][FM],
+                  bf16x8 (&fnb)[BK / 32][FN]) {
 #ifdef DL_WGRAD_STAMPS
     __builtin_amdgcn_sched_barrier(0);
     const unsigned long long sa = stamp();
@@ -2422,20 +1788,12 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
       st_prev = sb;
     }
 #endif
-    if constexpr (DF) {
-      issue(kt_next, dslot);  // into the slot read two steps ago
-      ++kt_next;
-      ++dslot;
-      dslot -= (dslot == STAGES) * STAGES;
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    issue(kt_next, dslot);  // into the slot read two steps ago
+    ++kt_next;
+    ++dslot;
+    dslot -= (dslot == STAGES) * STAGES;
+    __builtin_amdgcn_sched_barrier(0);
     read_frags(fna, fnb);
-    if constexpr (!DF) {
-      issue(kt_next, dslot);  // into the slot read two steps ago
-      ++kt_next;
-      ++dslot;
-      dslot -= (dslot == STAGES) * STAGES;
-    }
     // C^T (k x co): lane holds 4 consecutive k of one co -> 16-byte stores
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk)
@@ -2450,36 +1808,18 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
       __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
     }
     if constexpr (NRD > 2 * P1) __builtin_amdgcn_sched_group_barrier(0x100, NRD - 2 * P1, 0);
-    if constexpr (DF) {
-      if constexpr (NMF > P1) __builtin_amdgcn_sched_group_barrier(0x008, NMF - P1, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    } else if constexpr (NMF > P1) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x020, LPS, 0);
-      if constexpr (NMF > P1 + 1) __builtin_amdgcn_sched_group_barrier(0x008, NMF - P1 - 1, 0);
-    } else {
-      __builtin_amdgcn_sched_group_barrier(0x020, LPS, 0);
-    }
+    if constexpr (NMF > P1) __builtin_amdgcn_sched_group_barrier(0x008, NMF - P1, 0);
+    __builtin_amdgcn_sched_barrier(0);
   };
   int i = 0;
 #ifdef DL_WGRAD_STAMPS
   st_loop = stamp();
 #endif
-  if (g_wgrad_order) {
-    const std::integral_constant<bool, true> df{};
-    for (; i + 1 < nk; i += 2) {
-      step(df, fa0, fb0, fa1, fb1);
-      step(df, fa1, fb1, fa0, fb0);
-    }
-    if (i < nk) step(df, fa0, fb0, fa1, fb1);
-  } else {
-    const std::integral_constant<bool, false> df{};
-    for (; i + 1 < nk; i += 2) {
-      step(df, fa0, fb0, fa1, fb1);
-      step(df, fa1, fb1, fa0, fb0);
-    }
-    if (i < nk) step(df, fa0, fb0, fa1, fb1);
+  for (; i + 1 < nk; i += 2) {
+    step(fa0, fb0, fa1, fb1);
+    step(fa1, fb1, fa0, fb0);
   }
+  if (i < nk) step(fa0, fb0, fa1, fb1);
   }
 
 #ifdef DL_WGRAD_STAMPS
@@ -2497,25 +1837,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
   } stamp_out{g_wgrad_stamps, {st_start, st_loop, st_wait, st_work, st_lend}, wid};
 #endif
   const int col_l = lane & 15, rq = lane >> 4;
-  if constexpr (ATOM) {
-    const int logCin = g.logC8 + 3, taps = g.KH * g.KW;
-#pragma unroll
-    for (int a = 0; a < FM; ++a)
-#pragma unroll
-      for (int b = 0; b < FN; ++b) {
-        const int co = co0 + wm * TM + a * 16 + col_l;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int k = k0 + wn * TN + b * 16 + rq * 4 + r;
-          const int tap = k >> logCin, c = k & ((1 << logCin) - 1);
-          if (co < g.Cout && k < g.K && c < creal)
-            unsafeAtomicAdd(out + ((int64_t)co * taps + tap) * creal + c, acc[a][b][r]);
-        }
-      }
-    return;
-  }
   float* o = out + (int64_t)split * g.Cout * ldo;
-  if (BN >= 128 && g_wgrad_stage_store) {  // (64-wide tiles: measured no gain)
+  if constexpr (BN >= 128) {  // (64-wide tiles: measured no gain)
     // Slab rows through LDS: straight from the accumulators a store
     // instruction writes 16 rows x 64 B; staged, every instruction writes whole
     // BN*4-byte rows (64 lanes x 16 B).  The C^T tile goes into the (drained)
@@ -2798,15 +2121,9 @@ int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile,
 static SgdJob g_side_sgd{};         // set_conv_side_sgd: side SGD job of the next conv_fwd launch
 static uintptr_t g_fwd_addend = 0;  // conv_fwd_add: bf16 [M][Cout] added in the epilogue
 static uintptr_t g_fwd_addend_mask = 0;  // conv_fwd_add: optional uint8 [M][Cout/8] mask bits of the addend
-static int g_fwd_slab_cap = 0;      // split-K slab capacity of the current conv_fwd call (FwdCfg)
 static int g_fwd_keep_slabs = 0;    // FwdCfg bit 20: leave the split-K slabs (the caller combines them)
-static int g_fwd_swave_req = 0;     // FwdCfg bit 21: per-wave-row BN statistics rows (ConvGeom::swave)
-static int g_stat_rows_mult = 1;    // rows per M tile of the last streaming launch (WM when swave)
 static int g_red_atomic_host = 0;   // host mirror of g_red_atomic
 static BnRedArgs g_bnred{};         // conv_fwd_bnred: fused BN backward reduce (region dgrad only)
-static PoolLoad g_pool_load{};      // set_conv_pool_load: the next region conv pools its input on load
-static BnOnLoad g_onload{};         // set_conv_bn_on_load: the next 1x1 GEMM applies a BN + ReLU on load
-static BnRedArgs g_bnred2{};        // set_conv_bn_reduce: NHWC BN backward reduce in the streaming epilogue
 // conv_fwd_fix: the current conv_fwd call combines its split-K slices in-launch
 // (FIX); bnred.rows != nullptr: its epilogue is the BN backward reduce of the
 // block below (BNR 1) instead of the BN statistics
@@ -2816,10 +2133,6 @@ struct FixState {
 };
 static FixState g_fix{};
 static int g_fix_next = 0;  // next free arrival counter (round robin over g_fix_cnt)
-// A/B knob: 0 = the untransposed accumulator layout for the split-K and BN-statistics
-// instances of the streaming kernel (set_conv_fwd_tr)
-static int g_fwd_tr = 1;
-void set_conv_fwd_tr(int on) { g_fwd_tr = on ? 1 : 0; }
 
 // Position-major tiles with padding taps skipped (conv_fwd_kernel, g.posm):
 // for TAPU layers whose output is smaller than the kernel (every output pixel
@@ -2828,47 +2141,12 @@ void set_conv_fwd_tr(int on) { g_fwd_tr = on ? 1 : 0; }
 static int g_posm = 1;
 void set_conv_posm(int on) { g_posm = on ? 1 : 0; }
 
-// Balanced position-major split-K (g.pm_kmax): instead of `splits` equal
-// parts of every tile, pixel pos gets nsp(pos) = ceil(nk(pos) / kmax) parts
-// with kmax the smallest value that keeps the grid within the uniform plan's
-// and nsp within the slab capacity (CIFAR layer 4: 13 instead of 16 K steps
-// on the critical workgroups).  Measured (profiles/r2_posm_balance_ab.txt): no
-// gain -- layer-4 forward / dgrad 15.8 / 15.9 us vs 14.6 / 14.7, the combine
-// 5.9 vs 4.7 us (fill / epilogue, not the K loop, dominate these workgroups),
-// so it is off by default (set_conv_posm_balance).
-static bool g_posm_balance = false;
-void set_conv_posm_balance(int on) { g_posm_balance = on != 0; }
-
-static void plan_posm_balance(ConvGeom& g, int BM, int ntn, int splits, int cap) {
-  g.pm_kmax = g.pm_P = 0;
-  if (!g.posm || !g_posm_balance || splits <= 1 || cap < splits) return;
-  const int HW = g.H * g.W, nbt = g.B / BM, target = (g.M / BM) * splits;  // workgroups per N tile
-  int nkmax = 0;
-  for (int pos = 0; pos < HW; ++pos) nkmax = std::max(nkmax, posm_nk(g, pos));
-  const int k_uniform = (nkmax + splits - 1) / splits;
-  for (int kmax = 1; kmax < k_uniform; ++kmax) {
-    int P = 0, smax = 0;
-    for (int pos = 0; pos < HW; ++pos) {
-      const int ns = (posm_nk(g, pos) + kmax - 1) / kmax;
-      P += nbt * ns;
-      smax = std::max(smax, ns);
-    }
-    if (P <= target && smax <= cap) {
-      g.pm_kmax = kmax;
-      g.pm_P = P;
-      return;
-    }
-  }
-  (void)ntn;
-}
-
 template <int BM, int BN, bool TAPU, int ST, int WM, int WN>
 static void launch_fwd_w(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
                          uintptr_t slab, int splits, hipStream_t s) {
-  g.posm = (g_posm && TAPU && !g_fwd_addend && !g_bnred2.rows && g.B % BM == 0 && (g.H < g.KS || g.W < g.KS) && g.S == 1 && !g.om &&
+  g.posm = (g_posm && TAPU && !g_fwd_addend && g.B % BM == 0 && (g.H < g.KS || g.W < g.KS) && g.S == 1 && !g.om &&
             g.KH == g.KS && g.KW == g.KS && g.Hp == g.H + 2 * g.pad && g.Wp == g.W + 2 * g.pad) ? 1 : 0;
   const int ntm = (g.M + BM - 1) / BM, ntn = (g.Cout + BN - 1) / BN;
-  plan_posm_balance(g, BM, ntn, splits, g_fwd_slab_cap);
   const int nkt = (g.Kch + 7) / 8;
   const int ktps = (nkt + splits - 1) / splits;
   SgdJob side = g_side_sgd;  // one-shot: consumed by this launch
@@ -2876,29 +2154,13 @@ static void launch_fwd_w(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uin
   constexpr int kNT = 64 * WM * WN;
   if (side.nblk < 0)  // auto: one float4 per thread (2048 x 512 measured best of 256..2048 workgroups)
     side.nblk = (int)std::max<int64_t>(1, (side.hi4 - side.lo4 + kNT - 1) / kNT);
-  const int grid = (g.pm_kmax > 0 ? ntn * g.pm_P : ntm * ntn * splits) + side.nblk;
+  const int grid = ntm * ntn * splits + side.nblk;
   constexpr int NT = 64 * WM * WN;
   constexpr bool kTR = (BN / WN / 16) % 2 == 0;
-  g.swave = (g_fwd_swave_req && stats && splits == 1 && !g_red_atomic_host && g_fwd_tr && kTR && !g.posm) ? 1 : 0;
-  g_stat_rows_mult = g.swave ? WM : 1;
-  if (g_onload.y != nullptr) {
-    const BnOnLoad ol = g_onload;  // one-shot
-    g_onload = BnOnLoad{};
-    if constexpr (BM == 128 && BN == 128 && TAPU && WM == 2 && (WN == 2 || WN == 4) && ST <= 3) {
-      if (!stats || splits != 1 || g_fwd_addend || g_bnred2.rows != nullptr || g.posm || g.KS != 1 || g.S != 1 ||
-          g.Cin != ol.C || g.M != ol.M || (const bf16_t*)x != ol.out || side.nblk != 0 || !g_fwd_tr)
-        throw std::runtime_error("conv BN on load: a stride-1 1x1 forward with statistics on the activation's buffer");
-      conv_fwd_kernel<BM, BN, true, false, TAPU, ST, WM, WN, false, true, 0, true><<<grid, NT, 0, s>>>(
-          ol.y, (const bf16_t*)w, (bf16_t*)y, (float*)stats, nullptr, g, 1, ktps, g_conv_dbg, BnRedArgs{}, side, ol);
-      return;
-    } else {
-      throw std::runtime_error("conv BN on load: this tile / ring has no on-load instance (128x128, 4 or 8 waves, <= 3 stages)");
-    }
-  }
   if (g_fix.on) {
     if constexpr (kTR && TAPU && BM == 128 && BN == 64 && WM == 4 && WN == 2) {
-      if (splits < 2 || g.pm_kmax > 0 || g.om || g_fwd_addend || g_bnred2.rows != nullptr)
-        throw std::runtime_error("conv_fwd_fix: split-K without balanced plans / output maps / addends");
+      if (splits < 2 || g.om || g_fwd_addend)
+        throw std::runtime_error("conv_fwd_fix: split-K without output maps / addends");
       const int ntiles = ntm * ntn;
       if (ntiles > kFixCnt) throw std::runtime_error("conv_fwd_fix: too many tiles");
       static int* cnt0 = nullptr;
@@ -2908,17 +2170,17 @@ static void launch_fwd_w(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uin
       g_fix_next += ntiles;
       if (g_fix.bnred.rows != nullptr) {
         if (stats) throw std::runtime_error("conv_fwd_fix: BN reduce epilogue has no statistics");
-        conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, false, true, 1, false, true><<<grid, NT, 0, s>>>(
+        conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, false, true, 1, true><<<grid, NT, 0, s>>>(
             (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, (float*)slab, g, splits, ktps, g_conv_dbg,
-            g_fix.bnred, side, BnOnLoad{}, cnt);
+            g_fix.bnred, side, cnt);
       } else if (stats) {
-        conv_fwd_kernel<BM, BN, true, false, TAPU, ST, WM, WN, false, true, 0, false, true><<<grid, NT, 0, s>>>(
+        conv_fwd_kernel<BM, BN, true, false, TAPU, ST, WM, WN, false, true, 0, true><<<grid, NT, 0, s>>>(
             (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)stats, (float*)slab, g, splits, ktps, g_conv_dbg,
-            BnRedArgs{}, side, BnOnLoad{}, cnt);
+            BnRedArgs{}, side, cnt);
       } else {
-        conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, false, true, 0, false, true><<<grid, NT, 0, s>>>(
+        conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, false, true, 0, true><<<grid, NT, 0, s>>>(
             (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, (float*)slab, g, splits, ktps, g_conv_dbg,
-            BnRedArgs{}, side, BnOnLoad{}, cnt);
+            BnRedArgs{}, side, cnt);
       }
       return;
     } else {
@@ -2926,34 +2188,13 @@ static void launch_fwd_w(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uin
     }
   }
   if (g_fwd_addend && (splits > 1 || stats)) throw std::runtime_error("conv_fwd_add: no split-K / statistics");
-  if (g_bnred2.rows != nullptr) {
-    if (splits > 1 || stats) throw std::runtime_error("conv BN reduce: plain unsplit output only");
-    if ((g_bnred2.ym != nullptr || g_bnred2.mb != nullptr) != (g_fwd_addend != 0))
-      throw std::runtime_error("conv BN reduce: the output-mask form (relu 1) goes with the residual addend");
-    if constexpr ((BN / WN / 16) % 2 == 0) {  // the transposed epilogue (paired N fragments)
-      if (g_fwd_addend)
-        conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, true, true, 3><<<grid, NT, 0, s>>>(
-            (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)g_fwd_addend_mask, (float*)g_fwd_addend, g, 1,
-            ktps, g_conv_dbg, g_bnred2, side);
-      else
-        conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, false, true, 2><<<grid, NT, 0, s>>>(
-            (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, nullptr, nullptr, g, 1, ktps, g_conv_dbg, g_bnred2, side);
-    } else {
-      throw std::runtime_error("conv BN reduce: tile without the transposed epilogue");
-    }
-  } else if (g_fwd_addend)
+  if (g_fwd_addend)
     conv_fwd_kernel<BM, BN, false, false, TAPU, ST, WM, WN, true><<<grid, NT, 0, s>>>(
         (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)g_fwd_addend_mask, (float*)g_fwd_addend, g, 1, ktps,
         g_conv_dbg, BnRedArgs{}, side);
-  else if (splits > 1 && !g_fwd_tr)
-    conv_fwd_kernel<BM, BN, false, true, TAPU, ST, WM, WN, false, false><<<grid, NT, 0, s>>>(
-        (const bf16_t*)x, (const bf16_t*)w, nullptr, nullptr, (float*)slab, g, splits, ktps, g_conv_dbg, BnRedArgs{}, side);
   else if (splits > 1)
     conv_fwd_kernel<BM, BN, false, true, TAPU, ST, WM, WN><<<grid, NT, 0, s>>>(
         (const bf16_t*)x, (const bf16_t*)w, nullptr, nullptr, (float*)slab, g, splits, ktps, g_conv_dbg, BnRedArgs{}, side);
-  else if (stats && !g_fwd_tr)
-    conv_fwd_kernel<BM, BN, true, false, TAPU, ST, WM, WN, false, false><<<grid, NT, 0, s>>>(
-        (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)stats, nullptr, g, 1, ktps, g_conv_dbg, BnRedArgs{}, side);
   else if (stats)
     conv_fwd_kernel<BM, BN, true, false, TAPU, ST, WM, WN><<<grid, NT, 0, s>>>(
         (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)stats, nullptr, g, 1, ktps, g_conv_dbg, BnRedArgs{}, side);
@@ -2963,7 +2204,7 @@ static void launch_fwd_w(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uin
 }
 
 static int g_fwd_waves = 8;
-static int g_fwd_stages = 3, g_wgrad_stages = 0;  // tuning knobs (set_conv_stages); wgrad 0 = per-tile default
+static int g_fwd_stages = 3;  // set_conv_stages (the dgrads of an overlapped step run 2 stages)
 
 // Per-call streaming-kernel configuration packed into the tile id:
 // bits 0-3 tile, bits 4-7 LDS ring stages (0 = the global default), bits 8-11
@@ -2971,9 +2212,6 @@ static int g_fwd_stages = 3, g_wgrad_stages = 0;  // tuning knobs (set_conv_stag
 // (96 -> 64 KiB of LDS: two workgroups per CU, which is what the short-K
 // GEMMs need -- scripts/bench_gemm1x1.py SWEEP=1, ops/conv.py _plan_1x1),
 // while the CIFAR layers keep the tuned global default.
-// bits 12-19: the slab's capacity in K splits (0 = exactly `splits`); a larger
-// capacity lets a position-major layer use the balanced split-K plan
-// (g_fwd_slab_cap, declared with g_fwd_addend).
 // bit 20: keep the split-K slabs -- no combine launch; the consumer sums them
 // (bn_pool.hip combine_bwd_reduce: a dgrad's combine fused with the BN
 // backward reduce of the block below).
@@ -2981,10 +2219,7 @@ struct FwdCfg {
   int saved_st, saved_wv;
   explicit FwdCfg(int& tile) : saved_st(g_fwd_stages), saved_wv(g_fwd_waves) {
     const int st = (tile >> 4) & 15, wv = (tile >> 8) & 15;
-    g_fwd_slab_cap = (tile >> 12) & 255;
     g_fwd_keep_slabs = (tile >> 20) & 1;
-    g_fwd_swave_req = (tile >> 21) & 1;
-    g_stat_rows_mult = 1;
     tile &= 15;
     if (st && (st < 2 || st > 4)) throw std::runtime_error("conv_fwd: packed stages must be 2..4");
     if (wv && wv != 4 && wv != 8) throw std::runtime_error("conv_fwd: packed waves must be 4 or 8");
@@ -2992,7 +2227,7 @@ struct FwdCfg {
     if (wv) g_fwd_waves = wv;
   }
   ~FwdCfg() {
-    g_fwd_stages = saved_st; g_fwd_waves = saved_wv; g_fwd_slab_cap = 0; g_fwd_keep_slabs = 0; g_fwd_swave_req = 0;
+    g_fwd_stages = saved_st; g_fwd_waves = saved_wv; g_fwd_keep_slabs = 0;
   }
 };
 
@@ -3013,19 +2248,9 @@ void set_conv_waves(int waves) {
   g_fwd_waves = waves;
 }
 
-static int g_wgrad_pf = -1;  // wgrad fragment prefetch: -1 = by stage count, 0 off, 1 on
-void set_conv_wgrad_pf(int pf) { g_wgrad_pf = pf; }
-void set_conv_wgrad_stage_store(int on) {
-  const int v = on ? 1 : 0;
-  DL_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_wgrad_stage_store), &v, sizeof(int)));
-}
 void set_conv_fwd_pf(int on) {
   const int v = on ? 1 : 0;
   DL_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_fwd_pf), &v, sizeof(int)));
-}
-void set_conv_wgrad_order(int dma_first) {
-  const int v = dma_first ? 1 : 0;
-  DL_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_wgrad_order), &v, sizeof(int)));
 }
 void set_conv_debug(uintptr_t buf) { g_conv_dbg = (unsigned long long*)buf; }
 void set_conv_wgrad_stamps(uintptr_t buf) {
@@ -3034,10 +2259,9 @@ void set_conv_wgrad_stamps(uintptr_t buf) {
 }
 
 void set_conv_stages(int fwd, int wgrad) {
-  if (fwd < 2 || fwd > 4 || wgrad < 0 || wgrad > 5)
-    throw std::runtime_error("stages must be 2..4 (wgrad 0 = default, 5 = 128x128 tiles only)");
+  if (fwd < 2 || fwd > 4 || wgrad != 0)
+    throw std::runtime_error("stages: fwd 2..4, wgrad 0 (the per-tile default; other rings removed in round 6)");
   g_fwd_stages = fwd;
-  g_wgrad_stages = wgrad;
 }
 
 template <int BM, int BN>
@@ -3140,27 +2364,8 @@ static void launch_fwd_region_st(const ConvGeom& g, const RegionGeom& rg, uintpt
       attr = true;
     }
     kern<<<grid, 64 * WM * WN, lds, s>>>((const bf16_t*)x, (const bf16_t*)w, yy, st, sl, g, rg, splits, g_conv_dbg,
-                                         g_region_ablate, g_bnred, PoolLoad{});
+                                         g_region_ablate, g_bnred);
   };
-  if (g_pool_load.y != nullptr) {
-    // (one instance: the layer-2 forward's tile / wave / ring shape)
-    if constexpr (BN == 128 && WM == 2 && WN == 4 && ST == 6) {
-      if (splits > 1 || !stats || g_bnred.rows != nullptr || g.Cin != 64 || rg.nslot > kPlSlots * 64 * WM * WN)
-        throw std::runtime_error("conv_pool_load: an unsplit forward with statistics, Cin == 64, a small region");
-      auto kern = conv_fwd_region_kernel<BN, true, false, ST, WM, WN, false, true>;
-      static bool attr = false;
-      if (!attr) {
-        DL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024));
-        attr = true;
-      }
-      kern<<<grid, 64 * WM * WN, lds, s>>>((const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)stats, nullptr, g,
-                                           rg, splits, g_conv_dbg, g_region_ablate, g_bnred, g_pool_load);
-      g_pool_load = PoolLoad{};
-      return;
-    } else {
-      throw std::runtime_error("conv_pool_load: this region shape has no pool-on-load instance");
-    }
-  }
   if (g_bnred.rows != nullptr) {
     if (splits > 1 || stats) throw std::runtime_error("conv_fwd_bnred: plain unsplit dgrad only");
     go(conv_fwd_region_kernel<BN, false, false, ST, WM, WN, true>, (bf16_t*)y, nullptr, nullptr);
@@ -3188,81 +2393,12 @@ static void launch_fwd_region(const ConvGeom& g, const RegionGeom& rg, uintptr_t
   else launch_fwd_region_st<BN, WM, WN, 3>(g, rg, x, w, y, stats, slab, splits, s);
 }
 
-// ---- direct-B region kernel (conv_fwd_region_bd_kernel) ---------------------
-// set_conv_region_bd: 0 = off, 1 = row tiles (H*W % 128 == 0), 2 = also
-// whole-image tiles (the 8x8 layer: 2 images per 128-row tile).  Without a
-// weight ring the region may take the whole LDS budget (still leaving room
-// for one RCCL workgroup, kRegionLdsCap).
-static int g_region_bd = 0;
-void set_conv_region_bd(int mode) {
-  if (mode < 0 || mode > 2) throw std::runtime_error("set_conv_region_bd: 0, 1 or 2");
-  g_region_bd = mode;
-}
-
-static bool region_geom_bd(const ConvGeom& g, int splits, RegionGeom& rg) {
-  constexpr int BM = 128;
-  if (!g_region_bd || g.KS != 5 || !g.pow2 || g.Cin % 64 != 0 || g.W > BM || BM % g.W != 0) return false;
-  const int HW = g.H * g.W;
-  const int chunks = g.Cin / 64;
-  if (chunks % splits != 0) return false;
-  rg.cpw = chunks / splits;
-  if (rg.cpw > 2) return false;
-  rg.S = 10;
-  rg.RW = g.Wp;
-  if (HW % BM == 0) {
-    rg.rows_mode = 1;
-    rg.nimg = 1;
-    rg.RH = BM / g.W + g.KS - 1;
-    rg.RS = rg.RW * rg.S;
-  } else if (BM % HW == 0 && g_region_bd >= 2) {
-    rg.rows_mode = 0;
-    rg.nimg = BM / HW;
-    rg.RH = g.Hp;
-    rg.RS = rg.RW * rg.S + 8;
-  } else {
-    return false;
-  }
-  rg.IS = rg.RH * rg.RS;
-  rg.nslot = (rg.nimg * rg.IS + 63) / 64 * 64;
-  if (rg.RS >= 16384 || rg.nslot >= (1 << 16)) return false;
-  rg.inv_S = 1.0f / rg.S;
-  rg.inv_RS = 1.0f / rg.RS;
-  rg.inv_IS = 1.0f / rg.IS;
-  return rg.cpw * rg.nslot * 16 <= kRegionLdsCap;
-}
-
-// either region kernel takes the shape (the streaming kernel otherwise)
+// a region kernel takes the shape (the streaming kernel otherwise).  (The
+// direct-B region kernel -- weights streamed into registers, no LDS ring --
+// measured slower, layer-2 k-loop 24.3 k vs 23.6 k cycles, layer-3 49.9 k vs
+// 34.0 k, README round 5 / scripts/stamp_region.py; removed in round 6.)
 static bool any_region_geom(const ConvGeom& g, int tile, int splits, RegionGeom& rg) {
-  if ((tile == 0 || tile == 2) && region_geom_bd(g, splits, rg)) return true;
   return (tile == 2 && region_geom(g, 64, splits, rg)) || (tile == 0 && region_geom(g, 128, splits, rg));
-}
-
-template <int BN, int WM, int WN, int NK>
-static void launch_fwd_region_bd(const ConvGeom& g, const RegionGeom& rg, uintptr_t x, uintptr_t w, uintptr_t y,
-                                 uintptr_t stats, uintptr_t slab, int splits, hipStream_t s) {
-  constexpr int D = 4;  // weight k-steps in flight per wave
-  const int ntm = (g.M + 127) / 128;
-  const int grid = ntm * (g.Cout / BN) * splits;
-  const size_t lds = std::max<size_t>((size_t)rg.cpw * rg.nslot * 16, (size_t)WM * 2 * BN * 4);
-  auto go = [&](auto kern, bf16_t* yy, float* st, float* sl) {
-    static bool attr = false;  // per instantiation: allow > 64 KiB of dynamic LDS
-    if (!attr) {
-      DL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      attr = true;
-    }
-    kern<<<grid, 64 * WM * WN, lds, s>>>((const bf16_t*)x, (const bf16_t*)w, yy, st, sl, g, rg, splits, g_conv_dbg,
-                                         g_bnred);
-  };
-  if (g_bnred.rows != nullptr) {
-    if (splits > 1 || stats) throw std::runtime_error("conv_fwd_bnred: plain unsplit dgrad only");
-    go(conv_fwd_region_bd_kernel<BN, WM, WN, D, NK, false, false, true>, (bf16_t*)y, nullptr, nullptr);
-  } else if (splits > 1) {
-    go(conv_fwd_region_bd_kernel<BN, WM, WN, D, NK, false, true>, nullptr, nullptr, (float*)slab);
-  } else if (stats) {
-    go(conv_fwd_region_bd_kernel<BN, WM, WN, D, NK, true, false>, (bf16_t*)y, (float*)stats, nullptr);
-  } else {
-    go(conv_fwd_region_bd_kernel<BN, WM, WN, D, NK, false, false>, (bf16_t*)y, nullptr, nullptr);
-  }
 }
 
 // tile: 0 = 128x128, 1 = 64x64, 2 = 128x64 (BM x BN, BK = 64).  splits > 1:
@@ -3281,14 +2417,11 @@ void set_conv_c8_mt(int mt) {
 // fwd/dgrad workgroup order after the XCD swizzle (A/B knob): 0 = panel-major
 // (an XCD's workgroups share a weight panel and sweep M tiles), 1 = M-major
 // (they share M tiles and sweep the panels)
-static int g_fwd_mmajor = 0;
-void set_conv_fwd_order(int mmajor) { g_fwd_mmajor = mmajor ? 1 : 0; }
 
 int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab, int B, int H, int W, int Cin,
              int Cout, int KS, int tile, int splits, uintptr_t stream) {
   const FwdCfg cfg(tile);
   ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
-  g.mmajor = g_fwd_mmajor;
   hipStream_t s = as_stream(stream);
   if (splits < 1) splits = 1;
   if (splits > 1 && !slab) throw std::runtime_error("conv_fwd: split-K needs a slab");
@@ -3310,7 +2443,7 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
   const size_t c8_lds =
       (size_t)((c8_rows * g.Wp + 1 + 63) / 64 * 64 + (64 * KS * KS + 63) / 64 * 64) * 16 + 4 * 2 * 64 * 4;
   // the NHWC BN reduce epilogue and the in-launch split-K combine are on the streaming kernel
-  const bool streaming_only = g_bnred2.rows != nullptr || g_fix.on;
+  const bool streaming_only = g_fix.on;
   if (!streaming_only && tile == 2 && splits == 1 && g_region && g.pow2 && Cin == 8 && W <= 128 && 128 % W == 0 && (H * W) % 128 == 0 &&
       Cout % 64 == 0 && c8_lds <= 160 * 1024) {
     const int grid = (g.M / 128 / c8_mt) * (Cout / 64);
@@ -3325,12 +2458,6 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
     };
     if (stats) go(conv_fwd_c8_kernel<true>);
     else go(conv_fwd_c8_kernel<false>);
-  } else if (!streaming_only && g_pool_load.y == nullptr && (tile == 0 || tile == 2) &&
-             region_geom_bd(g, splits, rg)) {
-    if (tile == 0 && rg.cpw == 1) launch_fwd_region_bd<128, 1, 4, 25>(g, rg, x, w, y, stats, slab, splits, s);
-    else if (tile == 0) launch_fwd_region_bd<128, 1, 4, 50>(g, rg, x, w, y, stats, slab, splits, s);
-    else if (rg.cpw == 1) launch_fwd_region_bd<64, 2, 2, 25>(g, rg, x, w, y, stats, slab, splits, s);
-    else launch_fwd_region_bd<64, 2, 2, 50>(g, rg, x, w, y, stats, slab, splits, s);
   } else if (!streaming_only && tile == 0 && region_geom(g, 128, splits, rg)) {
     if (g_region_waves == 4) launch_fwd_region<128, 2, 2>(g, rg, x, w, y, stats, slab, splits, s);
     else launch_fwd_region<128, 2, 4>(g, rg, x, w, y, stats, slab, splits, s);
@@ -3343,21 +2470,13 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
   else if (tile == 2) launch_fwd<128, 64>(g, x, w, y, stats, slab, splits, s);
   else throw std::runtime_error("conv_fwd: bad tile id");
   DL_HIP_CHECK(hipGetLastError());
-  if (g_onload.y != nullptr) {  // armed, but this call did not take the streaming kernel
-    g_onload = BnOnLoad{};
-    throw std::runtime_error("set_conv_bn_on_load: the next conv_fwd call must be a streaming 1x1 GEMM");
-  }
-  if (g_pool_load.y != nullptr) {  // armed, but this call did not take the region kernel
-    g_pool_load = PoolLoad{};
-    throw std::runtime_error("set_conv_pool_load: the next conv_fwd call must run on the region kernel");
-  }
   if (g_side_sgd.nblk != 0) {  // armed, but this call ran on the region / c8 kernel
     g_side_sgd.nblk = 0;
     throw std::runtime_error("set_conv_side_sgd: the next conv_fwd call must run on the streaming kernel");
   }
-  if (splits == 1 || g_fix.on) return (g.M + fwd_bm(tile) - 1) / fwd_bm(tile) * g_stat_rows_mult;
+  if (splits == 1 || g_fix.on) return (g.M + fwd_bm(tile) - 1) / fwd_bm(tile);
   if (g_fwd_keep_slabs) {
-    if (stats || g.pm_kmax > 0) throw std::runtime_error("conv_fwd keep-slabs: no statistics / balanced split-K");
+    if (stats) throw std::runtime_error("conv_fwd keep-slabs: no statistics");
     return 0;
   }
   if (256 % (Cout / 8) != 0) throw std::runtime_error("conv_fwd split-K combine: Cout/8 must divide 256");
@@ -3398,65 +2517,6 @@ void set_conv_side_reduce(uintptr_t g, int64_t lo, int64_t hi, std::vector<int64
   SgdJob j = make_reduce_job(g, lo, hi, offs, lens, slabs, splits, {}, 0);
   j.nblk = nblk > 0 ? nblk : -1;
   g_side_sgd = j;
-}
-
-// Arm (rows != 0) / disarm (rows == 0) the channels-last BatchNorm backward
-// reduce (BnRedArgs, BNR 2) for the following conv_fwd / conv_fwd_ex calls on
-// the streaming kernel: x = the BN's input [M][C] (the conv output's layout),
-// save = its [mean; invstd], w / b = gamma / beta, rows = [T][2][C] partials;
-// ym != 0: the ReLU mask is ym > 0, mb != 0: the mask is those bits (BN +
-// residual + ReLU, BNR 3; the call must be a conv_fwd_add, whose addend
-// completes the gradient).
-void set_conv_bn_reduce(uintptr_t x, uintptr_t save, uintptr_t w, uintptr_t b, uintptr_t rows, uintptr_t ym,
-                        uintptr_t mb) {
-  if (ym && mb) throw std::runtime_error("set_conv_bn_reduce: ReLU mask from ym or from mask bits, not both");
-  g_bnred2 = rows ? BnRedArgs{(const bf16_t*)x, nullptr, (float*)rows, (const float*)save, (const float*)w,
-                              (const float*)b, (const bf16_t*)ym, (const uint8_t*)mb}
-                  : BnRedArgs{};
-}
-
-// The next conv_fwd call (a region-kernel forward with statistics) takes its
-// input as BN -> ReLU -> 2x2 max-pool of y_prev [B][2H][2W][Cin] on load: the
-// BN coefficients from the accumulated statistics (sums: R = reduce_rows()
-// rows, bn_fin_dev.h; block 0 publishes coef and the running statistics), the
-// pooled activation written into pout [B][H+2p][W+2p][Cin] (interior) for the
-// backward.  Replaces bn_relu_pool_fwd_fin on that edge.  One-shot.
-void set_conv_pool_load(uintptr_t y_prev, uintptr_t sums, int64_t M, uintptr_t gamma, uintptr_t beta, uintptr_t bias,
-                        uintptr_t rmean, uintptr_t rvar, float eps, float momentum, uintptr_t coef, uintptr_t pout) {
-  if (!y_prev || !sums || !gamma || !beta || !coef || !pout) throw std::runtime_error("set_conv_pool_load: null operand");
-  if (reduce_rows() < 1 || reduce_rows() > kMaxRows)
-    throw std::runtime_error("set_conv_pool_load: needs an atomic reduction mode with <= 32 rows");
-  g_pool_load = PoolLoad{(const bf16_t*)y_prev,
-                         make_bn_fin(sums, M, gamma, beta, bias, rmean, rvar, eps, momentum, coef, reduce_rows()),
-                         (bf16_t*)pout};
-}
-
-// The next conv_fwd (a stride-1 1x1 GEMM with statistics whose input buffer
-// is `out`) reads the BatchNorm input y instead and applies that BN + ReLU on
-// load (BnOnLoad); it also writes the activation into `out`, the saved
-// mean / invstd into save and updates the running statistics.  acc: [2C]
-// sum / sum of squares of y.  One-shot.
-void set_conv_bn_on_load(uintptr_t y, uintptr_t acc, uintptr_t w, uintptr_t b, uintptr_t save, uintptr_t rmean,
-                         uintptr_t rvar, int64_t M, int C, double eps, double momentum, uintptr_t out) {
-  if (!y || !acc || !w || !b || !save || !out) throw std::runtime_error("set_conv_bn_on_load: null operand");
-  if (C < 64 || C > kOlMaxC || C % 64 != 0 || M <= 0 || M >= (1ll << 31))
-    throw std::runtime_error("set_conv_bn_on_load: 64 <= C <= 512, C % 64 == 0");
-  g_onload = BnOnLoad{(const bf16_t*)y, (const float*)acc, (const float*)w, (const float*)b, (float*)save,
-                      (float*)rmean, (float*)rvar, (float)eps, (float)momentum, (int)M, C, (bf16_t*)out};
-}
-
-// Whether set_conv_pool_load can serve a conv_fwd of this shape (the
-// region kernel's pool-on-load instance: 128-wide tile, 8 waves, 6 stages).
-int conv_pool_load_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile) {
-  ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
-  RegionGeom rg{};
-  if ((tile & 15) != 0 || g_region_waves != 8 || Cin != 64 || Cout % 128 != 0 || !region_geom(g, 128, 1, rg) ||
-      rg.nslot > kPlSlots * 512)
-    return 0;
-  const int free_b = kRegionLdsCap - rg.cpw * rg.nslot * 16;
-  int st = std::min(8, free_b / (128 * 64 * 2));
-  if (g_region_stages > 0) st = std::min(st, g_region_stages);
-  return st >= 6 && st < 8 ? 1 : 0;  // launch_fwd_region's 6-stage instance
 }
 
 // Whether conv_fwd runs this unsplit shape on the region (tap-reuse) kernel --
@@ -3522,7 +2582,7 @@ int conv_fix_ok(int B, int H, int W, int Cin, int Cout, int KS, int tile, int sp
   (void)B; (void)H; (void)W;
   const int t = tile & 15, wv = (tile >> 8) & 15;
   return (t == 2 && splits >= 2 && Cin >= 64 && Cout % 64 == 0 && KS >= 1 && (wv == 0 ? g_fwd_waves : wv) == 8 &&
-          g_fwd_tr && !g_posm_balance)
+          true)
              ? 1
              : 0;
 }
@@ -3609,7 +2669,7 @@ int conv_fwd_ex(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_
   }
   g_fwd_addend = 0;
   DL_HIP_CHECK(hipGetLastError());
-  if (splits == 1) return (g.M + fwd_bm(tile) - 1) / fwd_bm(tile) * g_stat_rows_mult;
+  if (splits == 1) return (g.M + fwd_bm(tile) - 1) / fwd_bm(tile);
   if (g_fwd_keep_slabs) return 0;
   if (256 % (Cout / 8) != 0) throw std::runtime_error("conv_fwd_ex split-K combine: Cout/8 must divide 256");
   const int rpb = combine_rows_per_block(g.M, Cout);
@@ -3625,19 +2685,14 @@ void conv_wgrad_ex(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int Ho, int 
                    int dpad, int Cin, int Cout, int KH, int KW, int S, int splits, int ldo, int tile,
                    uintptr_t stream);
 
-// out: fp32 [splits][Cout][ldo], ldo >= K (K = KS*KS*Cin); tile 0 = 128x64, 1 = 64x64 (co x k)
-// atomic_creal > 0: every split atomically adds into the ZEROED fp32 gradient
-// out = [Cout][KS*KS][atomic_creal] (no slabs, no slab_reduce).
-// 1 = 1-D split-major XCD-aware wgrad grid (conv_wgrad_kernel), 0 = the 2-D grid (A/B)
-static int g_wgrad_xcd = 1;
-void set_conv_wgrad_xcd(int on) { g_wgrad_xcd = on ? 1 : 0; }
-
+// out: fp32 [splits][Cout][ldo], ldo >= K (K = KS*KS*Cin); tile 1 = 64x64, 2 = 128x128 (co x k)
 static void conv_wgrad_g(const ConvGeom& g, uintptr_t dy, uintptr_t x, uintptr_t out, int splits, int ldo, int tile,
-                         int atomic_creal, uintptr_t stream);
+                         uintptr_t stream);
 
 void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, int Cin, int Cout, int KS, int splits,
                 int ldo, int tile, int atomic_creal, uintptr_t stream) {
-  conv_wgrad_g(make_geom(B, H, W, Cin, Cout, KS), dy, x, out, splits, ldo, tile, atomic_creal, stream);
+  if (atomic_creal != 0) throw std::runtime_error("conv_wgrad: atomic split-K was removed in round 6 (pass 0)");
+  conv_wgrad_g(make_geom(B, H, W, Cin, Cout, KS), dy, x, out, splits, ldo, tile, stream);
 }
 
 void conv_wgrad_ex(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int Ho, int Wo, int Hp, int Wp, int dHp, int dWp,
@@ -3647,162 +2702,34 @@ void conv_wgrad_ex(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int Ho, int 
   g.dsep = 1; g.dHp = dHp; g.dWp = dWp; g.dpad = dpad;
   if (dHp < Ho + dpad || dWp < Wo + dpad) throw std::runtime_error("conv_wgrad_ex: dy buffer too small");
   if ((int64_t)B * dHp * dWp * Cout >= (1ll << 31)) throw std::runtime_error("conv_wgrad_ex: dy too large");
-  conv_wgrad_g(g, dy, x, out, splits, ldo, tile, 0, stream);
+  conv_wgrad_g(g, dy, x, out, splits, ldo, tile, stream);
 }
 
-// Position-major wgrad plan (see ConvGeom::wposm): (max splits a column tile
-// needs, total workgroups with work) at `steps` K steps per workgroup
-static std::pair<int, int> wgrad_posm_need(const ConvGeom& g, int bm, int bn, int steps) {
-  int smax = 0, total = 0, ph0, pw0, npw;
-  for (int k0 = 0; k0 < g.K; k0 += bn) {
-    const int st = (wgrad_posm_steps(g, k0, bn, ph0, pw0, npw) + steps - 1) / steps;
-    smax = std::max(smax, st);
-    total += st;
-  }
-  return {smax, total * (g.Cout / bm)};
-}
-
-std::vector<int> wgrad_posm_plan(int B, int H, int W, int Cin, int Cout, int KS, int tile, int steps) {
-  ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
-  const int bk = tile == 4 ? 32 : 64;
-  if (B % bk != 0 || !is_pow2(B / bk)) return {0, 0};
-  g.wposm = steps;
-  g.wlognbc = ilog2_exact(B / bk, "B/BK");
-  const int bm = tile == 1 ? 64 : (tile >= 3 ? 256 : 128), bn = tile == 1 || tile == 0 ? 64 : 128;
-  const auto r = wgrad_posm_need(g, bm, bn, steps);
-  return {r.first, r.second};
-}
-
-static void conv_wgrad_g(const ConvGeom& g0, uintptr_t dy, uintptr_t x, uintptr_t out, int splits, int ldo, int tile,
-                         int atomic_creal, uintptr_t stream) {
-  ConvGeom g = g0;
-  // tile bits 8-15: position-major steps per workgroup (0 = pixel-major), bit 16: idle splits write nothing
-  const int posm_steps = (tile >> 8) & 255, posm_skip = (tile >> 16) & 1;
-  tile &= 255;
-  if (posm_steps) {
-    const int bk = tile == 4 ? 32 : 64;
-    if (atomic_creal > 0 || g.dsep || !g.pow2 || g.S != 1 || g.B % bk != 0 || !is_pow2(g.B / bk))
-      throw std::runtime_error("conv_wgrad: position-major steps need pow2 H, W, B % BK == 0, B / BK a power of two");
-    g.wposm = posm_steps;
-    g.wlognbc = ilog2_exact(g.B / bk, "B/BK");
-    g.wskip = posm_skip;
-    const int bm = tile == 1 ? 64 : (tile >= 3 ? 256 : 128), bn = tile == 1 || tile == 0 ? 64 : 128;
-    if (wgrad_posm_need(g, bm, bn, posm_steps).first > std::max(1, splits))
-      throw std::runtime_error("conv_wgrad: a column tile needs more position-major splits than given");
-  }
-  const int Cin = g.Cin, Cout = g.Cout, W = g.W;
+static void conv_wgrad_g(const ConvGeom& g, uintptr_t dy, uintptr_t x, uintptr_t out, int splits, int ldo, int tile,
+                         uintptr_t stream) {
+  const int Cout = g.Cout, W = g.W;
+  if (tile != 1 && tile != 2) throw std::runtime_error("conv_wgrad: tile 1 (64x64) or 2 (128x128)");
   if (ldo < g.K) throw std::runtime_error("conv_wgrad: ldo < K");
   if (ldo % 4 != 0) throw std::runtime_error("conv_wgrad: ldo % 4 != 0 (16-byte slab stores)");
   if (Cout % 8 != 0) throw std::runtime_error("conv_wgrad: Cout % 8 != 0");
-  const int bm = tile == 1 ? 64 : (tile >= 3 ? 256 : 128);
+  const int bm = tile == 1 ? 64 : 128;
   if (Cout % bm != 0) throw std::runtime_error("conv_wgrad: Cout must be a multiple of the Cout tile");
-  if (tile >= 3 && g_fwd_waves != 8) throw std::runtime_error("conv_wgrad: the 256x128 tiles need the 8-wave config");
   if (g.pow2 && W > 64) throw std::runtime_error("conv_wgrad: needs W <= 64");
   if (splits < 1) splits = 1;
-  if (atomic_creal > Cin) throw std::runtime_error("conv_wgrad: atomic_creal > Cin");
   int mps = (g.M + splits - 1) / splits;
   mps = (mps + 63) / 64 * 64;  // 64-row aligned M steps (padded-layout addressing)
   hipStream_t s = as_stream(stream);
-  const bool atom = atomic_creal > 0;
-#define DL_WGXK(BM_, BN_, ST_, WM_, WN_, PF_, BK_)                                                         \
-  do {                                                                                                     \
-    const int nt = ((g.Cout + BM_ - 1) / BM_) * ((g.K + BN_ - 1) / BN_);                                  \
-    const dim3 grid = g_wgrad_xcd ? dim3(nt * splits, 1) : dim3(nt, splits);                              \
-    if (atom)                                                                                              \
-      conv_wgrad_kernel<BM_, BN_, ST_, WM_, WN_, PF_, true, BK_><<<grid, 64 * WM_ * WN_, 0, s>>>(          \
-          (const bf16_t*)dy, (const bf16_t*)x, (float*)out, g, mps, ldo, atomic_creal);                     \
-    else                                                                                                   \
-      conv_wgrad_kernel<BM_, BN_, ST_, WM_, WN_, PF_, false, BK_><<<grid, 64 * WM_ * WN_, 0, s>>>(         \
-          (const bf16_t*)dy, (const bf16_t*)x, (float*)out, g, mps, ldo, Cin);                              \
-  } while (0)
-#define DL_WGX(BM_, BN_, ST_, WM_, WN_, PF_) DL_WGXK(BM_, BN_, ST_, WM_, WN_, PF_, 64)
-#define DL_WG(BM_, BN_, ST_, WM_, WN_) DL_WGX(BM_, BN_, ST_, WM_, WN_, true)
-#define DL_WGN(BM_, BN_, ST_, WM_, WN_) DL_WGX(BM_, BN_, ST_, WM_, WN_, false)
-  // the wgrad pipeline keeps >= 2 stages in flight beyond the one being read.
-  // Measured (batch 128): 64x64 tiles want 4 stages (2 WGs/CU still fit:
-  // wgrad1 22.1 -> 16.8 us), 128x64 tiles 3 (4 would drop to 1 WG/CU: +20%),
-  // 128x128 tiles 4 with fragment prefetch (1 WG/CU, 128 KiB LDS, 141 VGPRs:
-  // wgrad2/3/4 31.7/29.7/28.4 us as 128x64 -> 24.7/23.0/21.8 us; the waves
-  // wait on the LDS-DMA ring, so the deeper ring wins over occupancy)
-  const int st = g_wgrad_stages > 0 ? std::max(3, g_wgrad_stages) : (tile == 0 ? 3 : 4);
-  // fragment prefetch (PF): default on for 4 stages, off for 3 (set_conv_wgrad_pf overrides)
-  const bool pf = g_wgrad_pf >= 0 ? g_wgrad_pf != 0 : st >= 4;
-  if (g_fwd_waves == 8) {
-    if (tile == 0) {
-      if (st >= 4) {
-        if (pf) DL_WG(128, 64, 4, 4, 2); else DL_WGN(128, 64, 4, 4, 2);
-      } else {
-        if (pf) DL_WG(128, 64, 3, 4, 2); else DL_WGN(128, 64, 3, 4, 2);
-      }
-    } else if (tile == 2) {
-      if (st >= 5) {
-        DL_WG(128, 128, 5, 2, 4);  // the whole 160 KiB LDS: three stages in flight beyond the one read
-      } else if (st >= 4) {
-        if (pf) DL_WG(128, 128, 4, 2, 4); else DL_WGN(128, 128, 4, 2, 4);
-      } else {
-        if (pf) DL_WG(128, 128, 3, 2, 4); else DL_WGN(128, 128, 3, 2, 4);
-      }
-    } else if (tile == 3) {
-      // 256 (co) x 128 (k): 48 KiB per 64-row stage, 3 stages = 144 KiB (one WG
-      // per CU); half again the MFMAs per DMA'd byte of the 128x128 tile, whose
-      // steps were bound by LDS-DMA issue and L2->LDS bytes, not by the MFMAs
-      // (profiles/r3_wgrad_stamps.txt: ~1240 cycles per step vs 512 of MFMA per SIMD)
-      // no fragment prefetch by default: the double fragment set does not fit the
-      // 256 registers of 2 waves per SIMD (spills: 275 vs 37 us at 100 workgroups)
-      if (g_wgrad_pf == 1) DL_WG(256, 128, 3, 4, 2); else DL_WGN(256, 128, 3, 4, 2);
-    } else if (tile == 4) {
-      // 256x128 with 32-row steps: 24 KiB per stage, a 6-stage ring (144 KiB,
-      // one WG per CU); per step and wave 16 MFMAs (as the 128x128 tile), 16
-      // fragment reads (24) and 3 LDS-DMA pieces (4): the L2->LDS bytes per MFMA
-      // drop by a third and the halved fragment set fits with prefetch
-      if (g.pow2 && W > 32) throw std::runtime_error("conv_wgrad tile 4: needs W <= 32");
-      DL_WGXK(256, 128, 6, 4, 2, true, 32);
-    } else {
-      if (st >= 4) DL_WG(64, 64, 4, 2, 4); else DL_WG(64, 64, 3, 2, 4);
-    }
-  } else {
-    if (tile == 0) {
-      DL_WG(128, 64, 3, 2, 2);
-    } else if (tile == 2) {
-      DL_WG(128, 128, 3, 2, 2);
-    } else {
-      DL_WG(64, 64, 3, 2, 2);
-    }
-  }
-#undef DL_WG
-#undef DL_WGN
-#undef DL_WGX
-#undef DL_WGXK
+  // 4-stage LDS-DMA rings with fragment prefetch: 64x64 tiles (2 WGs per CU:
+  // wgrad1 22.1 -> 16.8 us vs 3 stages), 128x128 tiles (1 WG per CU, 128 KiB
+  // LDS, 141 VGPRs: wgrad2/3/4 31.7/29.7/28.4 us as 128x64 -> 24.7/23.0/21.8 us;
+  // the waves wait on the LDS-DMA ring, so the deeper ring wins over occupancy)
+  auto go = [&](auto kern, int BM_, int BN_, int NT_) {
+    const int nt = ((g.Cout + BM_ - 1) / BM_) * ((g.K + BN_ - 1) / BN_);
+    kern<<<nt * splits, NT_, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (float*)out, g, mps, ldo);
+  };
+  if (tile == 2) go(conv_wgrad_kernel<128, 128, 4, 2, 4>, 128, 128, 512);
+  else go(conv_wgrad_kernel<64, 64, 4, 2, 4>, 64, 64, 512);
   DL_HIP_CHECK(hipGetLastError());
-}
-
-// First-layer weight gradient from an LDS-resident input region
-// (conv_wgrad_c8r_kernel): x = [B][Hp][Wp][8] zero-bordered, dy = [B][Hp][Wp][64]
-// with the output interior at (pad, pad) (conv_wgrad's operands), R output rows
-// per workgroup; out = fp32 slabs [B * H / R][64][ldo].  Returns the split count.
-int conv_wgrad_c8(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, int Cin, int Cout, int KS, int R,
-                  int ldo, uintptr_t stream) {
-  const ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
-  if (Cin != 8 || Cout != 64) throw std::runtime_error("conv_wgrad_c8: Cin = 8, Cout = 64 only");
-  if (KS * KS > 26) throw std::runtime_error("conv_wgrad_c8: at most 26 taps (13 K fragments)");
-  if (!g.pow2 || W % 8 != 0 || 64 % W != 0) throw std::runtime_error("conv_wgrad_c8: W must be 8, 16, 32 or 64");
-  if (R < 1 || H % R != 0 || (R * W) % 64 != 0) throw std::runtime_error("conv_wgrad_c8: R | H and 64 | R * W");
-  if (ldo < g.K || ldo % 4 != 0) throw std::runtime_error("conv_wgrad_c8: ldo >= K, ldo % 4 == 0");
-  constexpr int ST = 3;
-  const int rslots_p = ((R + KS - 1) * g.Wp + 1 + 63) / 64 * 64;
-  const size_t lds = (size_t)rslots_p * 16 + ST * 64 * 128;
-  if (lds > 160 * 1024) throw std::runtime_error("conv_wgrad_c8: region too large for LDS");
-  static bool attr = false;
-  if (!attr) {
-    DL_HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_c8r_kernel<ST>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr = true;
-  }
-  const int grid = B * (H / R);
-  conv_wgrad_c8r_kernel<ST><<<grid, 512, lds, as_stream(stream)>>>((const bf16_t*)dy, (const bf16_t*)x, (float*)out, g,
-                                                                    R, ldo);
-  DL_HIP_CHECK(hipGetLastError());
-  return grid;
 }
 
 void set_reduce_atomic_conv(int rows) {

@@ -30,30 +30,22 @@ def main():
                     help="hold R CUs with RCCL-sized workgroups on a side stream while timing (testing/diag.hip)")
     ap.add_argument("--dtile", type=int, default=-1, help="override the dgrad tile")
     ap.add_argument("--dsplits", type=int, default=-1, help="override the dgrad split count")
-    ap.add_argument("--stages", default="3,0", help="fwd,wgrad LDS ring depth (wgrad 0 = per-tile default)")
-    ap.add_argument("--wtile", type=int, default=-1, help="override the wgrad tile (0 128x64, 1 64x64, 2 128x128)")
-    ap.add_argument("--wpf", type=int, default=-1, help="wgrad fragment prefetch: -1 by stages, 0 off, 1 on")
+    ap.add_argument("--stages", default="3,0", help="fwd,wgrad LDS ring depth (wgrad: 0, the per-tile default)")
+    ap.add_argument("--wtile", type=int, default=-1, help="override the wgrad tile (1 64x64, 2 128x128)")
     ap.add_argument("--waves", type=int, default=8, help="waves per workgroup of the fwd/dgrad kernel (4 or 8)")
     ap.add_argument("--region", type=int, default=1, help="1: tap-reuse (LDS-resident region) fwd/dgrad kernel")
-    ap.add_argument("--region-bd", type=int, default=0,
-                    help="direct-B region kernel (weights into registers): 0 off, 1 row tiles, 2 + whole images")
     ap.add_argument("--rstages", type=int, default=0, help="region kernel B-ring stages (0 = max that fits)")
     ap.add_argument("--rwaves", type=int, default=8, help="region kernel waves per workgroup (4 or 8)")
-    ap.add_argument("--wstage", type=int, default=1, help="wgrad slab stores staged through LDS as whole rows")
-    ap.add_argument("--worder", type=int, default=1, help="wgrad main loop: 1 DMA before the fragment reads, 0 after")
     ap.add_argument("--fpf", type=int, default=1, help="streaming fwd/dgrad fragment prefetch (>= 3 stages)")
     a = ap.parse_args()
     C = _native.native()
     fs, ws = (int(v) for v in a.stages.split(","))
     C.set_conv_stages(fs, ws)
     C.set_conv_waves(a.waves)
-    C.set_conv_wgrad_pf(a.wpf)
     C.set_conv_region(a.region)
-    C.set_conv_region_bd(a.region_bd)
     C.set_conv_region_stages(a.rstages)
     C.set_conv_region_waves(a.rwaves)
-    C.set_conv_wgrad_stage_store(a.wstage)
-    print(f"# stages fwd={fs} wgrad={ws} region={a.region} region_bd={a.region_bd}")
+    print(f"# stages fwd={fs} wgrad={ws} region={a.region}")
     dev = torch.device("cuda")
     def cur():  # current-stream handle at call time (graph capture switches streams)
         return torch.cuda.current_stream().cuda_stream
@@ -91,9 +83,9 @@ def main():
                 cur()),
                 f"tile{dt} split{ds}"))
         wtile, wsp = _wgrad_plan(cout, K, M)
-        if a.wtile >= 0 and cout % (256 if a.wtile >= 3 else 128) == 0:
+        if a.wtile >= 0 and cout % (128 if a.wtile == 2 else 64) == 0:
             wtile = a.wtile
-            bm, bn = {4: (256, 128), 3: (256, 128), 2: (128, 128), 0: (128, 64)}.get(wtile, (64, 64))
+            bm, bn = {2: (128, 128)}.get(wtile, (64, 64))
             tiles = (cout // bm) * ((K + bn - 1) // bn)
             wsp = 1
             while tiles * wsp < 256 and M // (wsp * 2) >= 2048:

@@ -56,17 +56,8 @@ def main():
                                              cout, 1, ft, fs, s)),
             "fwd_stats": timeit(lambda: C.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), rows.data_ptr(),
                                                    slab.data_ptr(), M, 1, 1, cin, cout, 1, ft, fs, s)),
-            "fwd_stats_swave": timeit(lambda: C.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), rows.data_ptr(),
-                                                         slab.data_ptr(), M, 1, 1, cin, cout, 1, ft | (1 << 21), fs, s)),
-            "fwd_stats_rows_reduce": timeit(lambda: C.bn_rows_reduce(rows.data_ptr(), (M + 127) // 128, cout,
-                                                                     gw.data_ptr(), s)),
-            "fwd_stats_swave_rows_reduce": timeit(lambda: C.bn_rows_reduce(rows.data_ptr(), 4 * ((M + 127) // 128), cout,
-                                                                           gw.data_ptr(), s)),
             "dgrad": timeit(lambda: C.conv_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, slab.data_ptr(), M, 1, 1,
                                                cout, cin, 1, dt, ds, s)),
-            "wgrad_atomic": timeit(lambda: (gw.zero_(), C.conv_wgrad(dy.data_ptr(), x.data_ptr(), gw.data_ptr(), M, 1, 1,
-                                                                       cin, cout, 1, wsp, cin, wtile,
-                                                                       cin if wsp > 1 else 0, s))),
             "wgrad": timeit(lambda: (C.conv_wgrad(dy.data_ptr(), x.data_ptr(), wslab.data_ptr(), M, 1, 1, cin, cout, 1,
                                                   wsp, cin, wtile, 0, s),
                                      C.slab_reduce_add(wslab.data_ptr(), gw.data_ptr(), wsp, cout, 1, cin, cin, s))),
@@ -90,17 +81,6 @@ def main():
                                                                            slab.data_ptr(), M, 1, 1, cout, cin, 1, tl, 1, s))
             C.set_conv_stages(3, 0)
             C.set_conv_waves(8)
-            for wst in (0,):
-                C.set_conv_stages(3, wst)
-                for tl in (0, 1, 2):
-                    if cout % (64 if tl == 1 else 128):
-                        continue
-                    for sp in sorted({max(1, wsp // d) for d in (32, 16, 8, 4, 2, 1)}):
-                        if M // sp < 128:
-                            continue
-                        t[f"wgrad_st{wst}_t{tl}_s{sp}"] = timeit(lambda: (gw.zero_(), C.conv_wgrad(
-                            dy.data_ptr(), x.data_ptr(), gw.data_ptr(), M, 1, 1, cin, cout, 1, sp, cin, tl,
-                            cin if sp > 1 else 0, s)))
             C.set_conv_stages(3, 0)
             for tl in (1, 2):
                 if cout % (64 if tl == 1 else 128):

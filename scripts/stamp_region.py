@@ -12,7 +12,6 @@ from torch_distlearn_amd.models.cifar_hip import _fwd_plan
 
 C = _native.native()
 C.set_conv_region(int(os.environ.get("REGION", "1")))  # 2: whole-image tiles too (layers 3-4)
-C.set_conv_region_bd(int(os.environ.get("REGION_BD", "0")))  # the direct-B region kernel
 C.set_conv_region_ablate(int(sys.argv[3]) if len(sys.argv) > 3 else 0)
 C.set_conv_region_stages(int(sys.argv[4]) if len(sys.argv) > 4 else 0)
 C.set_conv_region_waves(int(sys.argv[5]) if len(sys.argv) > 5 else 8)

@@ -94,94 +94,7 @@ def test_conv_fwd_and_stats(C, shape, tile, splits, region):
     torch.testing.assert_close(stats[:, 1].sum(0), (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
 
 
-@pytest.mark.parametrize("B,H,R", [(8, 32, 2), (8, 32, 16), (4, 32, 32), (4, 16, 4), (4, 16, 16), (2, 8, 8)])
-def test_wgrad_first_layer_region(C, B, H, R):
-    """First-layer weight gradient from an LDS-resident input region
-    (conv_wgrad_c8r_kernel: Cin 8, Cout 64, a workgroup per band of R output
-    rows owns the whole 64 x 200 tile, B fragments read per tap from the
-    region with ds_read_b64_tr_b16): one slab per band, whose sum equals an
-    fp64 reference and the generic split-K wgrad."""
-    cin, cout = 8, 64
-    dev = torch.device("cuda")
-    g = torch.Generator(device=dev).manual_seed(41 + B * H + R)
-    x = torch.randn(B, H, H, cin, device=dev, generator=g).to(torch.bfloat16)
-    x[..., 3:] = 0  # the executor's 3 -> 8 channel pad (any values are fine for the kernel)
-    dy = torch.randn(B, H, H, cout, device=dev, generator=g).to(torch.bfloat16)
-    xr = x.double().cpu().permute(0, 3, 1, 2)
-    wr = torch.zeros(cout, cin, 5, 5, dtype=torch.float64, requires_grad=True)
-    F.conv2d(xr, wr, padding=2).backward(dy.double().cpu().permute(0, 3, 1, 2))
-    dw_ref = wr.grad.permute(0, 2, 3, 1).float().to(dev)
-    K = 25 * cin
-    xp, dyp = _pad(x), _pad(dy)
-    nb = B * H // R
-    slabs = torch.full((nb, cout, K), float("nan"), device=dev)
-    assert C.conv_wgrad_c8(dyp.data_ptr(), xp.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, R, K, _s()) == nb
-    dw = torch.empty(cout, 5, 5, cin, device=dev)
-    C.slab_reduce(slabs.data_ptr(), dw.data_ptr(), nb, cout, 25, cin, cin, _s())
-    gen = torch.full((4, cout, K), float("nan"), device=dev)
-    C.conv_wgrad(dyp.data_ptr(), xp.data_ptr(), gen.data_ptr(), B, H, H, cin, cout, 5, 4, K, 1, 0, _s())
-    dwg = torch.empty(cout, 5, 5, cin, device=dev)
-    C.slab_reduce(gen.data_ptr(), dwg.data_ptr(), 4, cout, 25, cin, cin, _s())
-    torch.cuda.synchronize()
-    assert not torch.isnan(slabs).any()
-    assert _rel(dw, dw_ref) < 1e-4, _rel(dw, dw_ref)
-    assert _rel(dw, dwg) < 1e-4
-    # one band alone: slab b is the gradient of the rows it owns
-    b = nb // 2
-    img, r0 = b // (H // R), (b % (H // R)) * R
-    dyb = torch.zeros_like(dy)
-    dyb[img, r0:r0 + R] = dy[img, r0:r0 + R]
-    wr2 = torch.zeros(cout, cin, 5, 5, dtype=torch.float64, requires_grad=True)
-    F.conv2d(xr, wr2, padding=2).backward(dyb.double().cpu().permute(0, 3, 1, 2))
-    ref_b = wr2.grad.permute(0, 2, 3, 1).reshape(cout, K).float().to(dev)
-    assert _rel(slabs[b], ref_b) < 1e-4
-    with pytest.raises(RuntimeError, match="R \\| H"):
-        C.conv_wgrad_c8(dyp.data_ptr(), xp.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, 3, K, _s())
-
-
-# (B, H, Cin, Cout) of the position-major wgrad: the executor's layers 3 / 4 at batch 128
-# and 64 (B / 64 image chunks), plus layer 2's 64-channel taps (a column tile spans two taps)
 WPOSM_SHAPES = [(128, 4, 256, 256), (128, 8, 128, 256), (64, 8, 128, 128), (64, 16, 64, 128)]
-
-
-@pytest.mark.parametrize("shape", WPOSM_SHAPES)
-@pytest.mark.parametrize("tile", [2, 0])
-def test_wgrad_position_major(C, shape, tile):
-    """Position-major weight gradient (ConvGeom::wposm, conv_wgrad tile bits
-    8-16): a K step is 64 images at one output pixel, a column tile visits
-    only the pixels where one of its taps reads inside the image, and its
-    steps are balanced over ceil(steps / L) workgroups.  The slab sum equals
-    an fp64 reference, with idle splits writing zeros (bit 16 off: slabs
-    start as NaN) or nothing (bit 16 on: slabs pre-zeroed), and the plan
-    helper agrees with the kernel (it refuses too few splits)."""
-    B, H, cin, cout = shape
-    dev = torch.device("cuda")
-    g = torch.Generator(device=dev).manual_seed(31 + H + cin)
-    x = torch.randn(B, H, H, cin, device=dev, generator=g).to(torch.bfloat16)
-    dy = torch.randn(B, H, H, cout, device=dev, generator=g).to(torch.bfloat16)
-    xr = x.double().cpu().permute(0, 3, 1, 2)
-    wr = torch.zeros(cout, cin, 5, 5, dtype=torch.float64, requires_grad=True)
-    F.conv2d(xr, wr, padding=2).backward(dy.double().cpu().permute(0, 3, 1, 2))
-    dw_ref = wr.grad.permute(0, 2, 3, 1).float().to(dev)
-    K = 25 * cin
-    xp, dyp = _pad(x), _pad(dy)
-    full = B * H * H // 64
-    for steps in (max(1, full // 4), max(1, full // 2), full):
-        smax, total = C.wgrad_posm_plan(B, H, H, cin, cout, 5, tile, steps)
-        assert 1 <= smax <= (full + steps - 1) // steps and total >= smax
-        for skip in (0, 1):
-            slabs = (torch.zeros if skip else lambda *s, **k: torch.full(s, float("nan"), **k))(
-                smax, cout, K, device=dev)
-            C.conv_wgrad(dyp.data_ptr(), xp.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, smax, K,
-                         tile | (steps << 8) | (skip << 16), 0, _s())
-            dw = torch.empty(cout, 5, 5, cin, device=dev)
-            C.slab_reduce(slabs.data_ptr(), dw.data_ptr(), smax, cout, 25, cin, cin, _s())
-            torch.cuda.synchronize()
-            assert _rel(dw, dw_ref) < 1e-4, (steps, skip, _rel(dw, dw_ref))
-        if smax > 1:
-            with pytest.raises(RuntimeError, match="position-major splits"):
-                C.conv_wgrad(dyp.data_ptr(), xp.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, smax - 1, K,
-                             tile | (steps << 8), 0, _s())
 
 
 @pytest.mark.parametrize("shape", CONV_SHAPES)
@@ -267,8 +180,8 @@ def test_conv_dgrad_wgrad(C, shape):
                 assert _rel(dx, dx_ref) < 8e-3, (tile, splits, region)
     K = 25 * cin
     xp = _pad(x)
-    for tile in (0, 1, 2, 3, 4):
-        if cout % {1: 64, 3: 256, 4: 256}.get(tile, 128) != 0 or (tile == 4 and H > 32):
+    for tile in (1, 2):
+        if cout % {1: 64}.get(tile, 128) != 0:
             continue
         for splits in (1, 3):
             slabs = torch.full((splits, cout, K), float("nan"), device=dev)
@@ -278,24 +191,6 @@ def test_conv_dgrad_wgrad(C, shape):
             C.slab_reduce(slabs.data_ptr(), dw.data_ptr(), splits, cout, 25, cin, cin, _s())
             torch.cuda.synchronize()
             assert _rel(dw, dw_ref) < 1e-4, (tile, splits, _rel(dw, dw_ref))
-    # non-default DMA ring depths / fragment-prefetch modes of the wgrad kernel
-    for tile in (0, 2):
-        if cout % 128 != 0:
-            continue
-        for st, pf in ((3, 1), (3, 0), (4, 0), (4, 1), (5, 1)):
-            C.set_conv_stages(3, st)
-            C.set_conv_wgrad_pf(pf)
-            try:
-                slabs = torch.full((2, cout, K), float("nan"), device=dev)
-                C.conv_wgrad(dyp.data_ptr(), xp.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, 2, K, tile, 0,
-                             _s())
-            finally:
-                C.set_conv_stages(3, 0)
-                C.set_conv_wgrad_pf(-1)
-            dw = torch.empty(cout, 5, 5, cin, device=dev)
-            C.slab_reduce(slabs.data_ptr(), dw.data_ptr(), 2, cout, 25, cin, cin, _s())
-            torch.cuda.synchronize()
-            assert _rel(dw, dw_ref) < 1e-4, (tile, st, pf, _rel(dw, dw_ref))
 
 
 def test_prep_step(C):
@@ -500,14 +395,13 @@ def test_bwd_reduce_head_fused(C):
     assert int(res[1][5][0]) == 1 and float(res[1][4]) == 1.0
 
 
-@pytest.mark.parametrize("atomic", ["2", "1", "0"])
+@pytest.mark.parametrize("atomic", ["2", "0"])
 def test_executor_matches_torch_model(C, atomic, monkeypatch):
     """Whole-model check: HIP executor loss + every gradient vs an fp32 PyTorch
     reference of the same parameters; the error must be within 2x of what
-    PyTorch's own bf16 path shows against the same fp32 reference.  Every
-    reduction mode (2 = striped atomic BN rows + slab weight gradients, 1 =
-    atomic accumulation, no finalize / slab-reduce launches; 0 = deterministic
-    partial rows)."""
+    PyTorch's own bf16 path shows against the same fp32 reference.  Both
+    reduction modes (2 = striped atomic BN rows + slab weight gradients;
+    0 = deterministic partial rows)."""
     monkeypatch.setenv("DISTLEARN_REDUCE_ATOMIC", atomic)
     from torch_distlearn_amd import FlatParams
     from torch_distlearn_amd.models import CifarConvNet
@@ -546,7 +440,6 @@ def test_executor_matches_torch_model(C, atomic, monkeypatch):
     lp_ref = ref(x, compute_dtype=torch.float32)
     lp = ex.predict(x)
     assert _rel(lp, lp_ref) < 2e-2
-
 
 
 @pytest.mark.parametrize("atomic", ["2", "0"])
@@ -734,29 +627,6 @@ def test_head_pool_fused_finalize(C, atomic_mode):
         assert torch.equal(a, b_)
 
 
-@pytest.mark.parametrize("shape", [(8, 32, 8, 64, 3, 1, 128), (8, 16, 64, 128, 64, 2, 8), (8, 8, 128, 256, 128, 2, 5),
-                                   (4, 16, 32, 64, 32, 1, 3)])
-def test_wgrad_atomic_split_k(C, shape):
-    """conv_wgrad with atomic split-K straight into the zeroed gradient
-    (dropping zero-padded input channels) == slabs + slab_reduce."""
-    B, H, cin, cout, creal, tile, splits = shape
-    dev = torch.device("cuda")
-    g = torch.Generator(device=dev).manual_seed(cin * cout + splits)
-    x = torch.randn(B, H, H, cin, device=dev, generator=g)
-    x[..., creal:] = 0
-    xp = _pad(x.to(torch.bfloat16))
-    dyp = _pad(torch.randn(B, H, H, cout, device=dev, generator=g).to(torch.bfloat16))
-    K = 25 * cin
-    slabs = torch.full((splits, cout, K), float("nan"), device=dev)
-    C.conv_wgrad(dyp.data_ptr(), xp.data_ptr(), slabs.data_ptr(), B, H, H, cin, cout, 5, splits, K, tile, 0, _s())
-    ref = torch.empty(cout, 5, 5, creal, device=dev)
-    C.slab_reduce(slabs.data_ptr(), ref.data_ptr(), splits, cout, 25, cin, creal, _s())
-    dw = torch.zeros(cout, 5, 5, creal, device=dev)
-    C.conv_wgrad(dyp.data_ptr(), xp.data_ptr(), dw.data_ptr(), B, H, H, cin, cout, 5, splits, K, tile, creal, _s())
-    torch.cuda.synchronize()
-    assert _rel(dw, ref) < 1e-5
-
-
 def test_prep_zero_ranges(C):
     """The step's prep kernel zeroes the listed accumulator ranges (mode 1)."""
     dev = torch.device("cuda")
@@ -772,35 +642,6 @@ def test_prep_zero_ranges(C):
                 [], [], [], [], [b.data_ptr() for b in bufs], [b.numel() for b in bufs], _s())
     torch.cuda.synchronize()
     assert all(not b.any() for b in bufs) and torch.equal(keep, ref)
-
-
-def test_executor_merged_slab_reduce_bitwise(C, monkeypatch):
-    """The weight-gradient slab reduction launched together with the previous
-    block's BN backward reduce (bwd_reduce_slab_kernel) writes exactly what the
-    stand-alone slab_reduce launches write (deterministic mode 0)."""
-    from torch_distlearn_amd import FlatParams
-    from torch_distlearn_amd.models import CifarConvNet
-    from torch_distlearn_amd.models.cifar_hip import CifarHIPExecutor
-
-    monkeypatch.setenv("DISTLEARN_REDUCE_ATOMIC", "0")
-    monkeypatch.setenv("DISTLEARN_FUSE_COMBINE", "0")  # (merge=1 turns the fused combine off for its layers)
-    dev = torch.device("cuda")
-    g = torch.Generator(device=dev).manual_seed(5)
-    x = torch.randn(64, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)
-    y = torch.randint(0, 10, (64,), device=dev, generator=g)
-    grads = []
-    for merge in ("0", "1"):
-        monkeypatch.setenv("DISTLEARN_MERGE_SLAB", merge)
-        mdl = CifarConvNet(seed=4).to(dev)
-        flat = FlatParams(mdl, grads=True, shadow_bf16=True)
-        flat.grad.fill_(float("nan"))  # every gradient element must be (over)written
-        ex = CifarHIPExecutor(mdl, flat, max_batch=64)
-        assert ex.merge_slab == (merge == "1")
-        ex.forward_backward(x.contiguous(), y)
-        torch.cuda.synchronize()
-        grads.append(torch.cat([v.flatten() for v in flat.views_of(flat.grad)]))
-    assert torch.isfinite(grads[1]).all()
-    assert torch.equal(grads[0], grads[1])
 
 
 @pytest.mark.parametrize("B,atomic", [(128, "0"), (64, "0"), (128, "2")])
@@ -922,14 +763,11 @@ POSM_SHAPES = [(128, 4, 256, 512, 0, 4), (128, 4, 512, 256, 0, 8), (128, 4, 256,
 
 
 @pytest.mark.parametrize("shape", POSM_SHAPES)
-@pytest.mark.parametrize("cap", [0, 2])
-def test_conv_fwd_position_major(C, shape, cap):
+def test_conv_fwd_position_major(C, shape):
     """Streaming conv with position-major M tiles and the zero-border taps
     skipped (g.posm) vs an fp32 reference and vs the pixel-major tiles
     (bitwise without split-K: skipping exact-zero products keeps every fp32
-    partial sum); BN statistics of exactly the stored values.  cap = 2: the
-    slab holds 2 x splits slices (tile-id bits 12-19), so split-K layers use
-    the balanced plan (per-pixel split counts, combine reads each row's own)."""
+    partial sum); BN statistics of exactly the stored values."""
     B, H, cin, cout, tile, splits = shape
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(B + H * cin + cout)
@@ -937,20 +775,17 @@ def test_conv_fwd_position_major(C, shape, cap):
     w = (torch.randn(cout, 5, 5, cin, device=dev, generator=g) * 0.05).to(torch.bfloat16)
     xp = _pad(x)
     rows = C.conv_fwd_stat_rows(B, H, H, cin, cout, 5, tile, splits)
-    ncap = cap * splits if splits > 1 else 0
-    slab = torch.full((max(ncap, splits) * B * H * H * cout,), float("nan"), device=dev)
+    slab = torch.full((splits * B * H * H * cout,), float("nan"), device=dev)
     outs = []
     for posm in (0, 1):
         C.set_conv_posm(posm)
-        C.set_conv_posm_balance(1 if cap else 0)
         try:
             y = torch.full((B, H, H, cout), float("nan"), dtype=torch.bfloat16, device=dev)
             stats = torch.full((max(rows, 400), 2, cout), float("nan"), device=dev)
             T = C.conv_fwd(xp.data_ptr(), w.data_ptr(), y.data_ptr(), stats.data_ptr(), slab.data_ptr(), B, H, H,
-                           cin, cout, 5, tile | (ncap << 12), splits, _s())
+                           cin, cout, 5, tile, splits, _s())
         finally:
             C.set_conv_posm(1)
-            C.set_conv_posm_balance(0)
         torch.cuda.synchronize()
         outs.append((y, stats[:T].sum(0)))
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=2).permute(0, 2, 3, 1)
@@ -994,168 +829,6 @@ def test_conv_c8_tiles_per_workgroup(C, B):
     assert _rel(outs[1][0], ref) < 8e-3
 
 
-def test_pool_on_load_region_conv(C, monkeypatch):
-    """Block 2's region conv takes block 1's BN -> ReLU -> 2x2 pool on load
-    (set_conv_pool_load: coefficients derived in its prologue, the pooled
-    input computed into its LDS region, the pooled copy written for the
-    backward) instead of the bn_relu_pool_fwd_fin launch: the pooled
-    activation is bitwise the stand-alone pool of the same coefficients, the
-    block-2 output bitwise the plain region conv of it, the running
-    statistics updated once, and a step's loss / gradients match the
-    separate launch to the fp32-atomic statistics' noise."""
-    from torch_distlearn_amd import FlatParams
-    from torch_distlearn_amd.models import CifarConvNet
-    from torch_distlearn_amd.models.cifar_convnet import BN_EPS, BN_MOMENTUM
-    from torch_distlearn_amd.models.cifar_hip import KSIZE, SPAD, CifarHIPExecutor
-
-    monkeypatch.setenv("DISTLEARN_REDUCE_ATOMIC", "2")
-    dev = torch.device("cuda")
-    g = torch.Generator(device=dev).manual_seed(11)
-    x = torch.randn(128, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)
-    y = torch.randint(0, 10, (128,), device=dev, generator=g)
-    res = []
-    for pl in ("0", "1", "1"):
-        monkeypatch.setenv("DISTLEARN_POOL_ON_LOAD", pl)
-        mdl = CifarConvNet(seed=4).to(dev)
-        flat = FlatParams(mdl, grads=True, shadow_bf16=True)
-        ex = CifarHIPExecutor(mdl, flat, max_batch=128)
-        assert ex._pool_on_load(1) == (pl == "1")
-        rm0, rv0 = ex.rm[0].clone(), ex.rv[0].clone()
-        # every interior element must be written: NaN inside, the zero border kept
-        interior = ex.p[0][:, SPAD:-SPAD, SPAD:-SPAD]
-        interior.fill_(float("nan"))
-        loss = float(ex.forward_backward(x.contiguous(), y))
-        torch.cuda.synchronize()
-        grads = torch.cat([v.flatten() for v in flat.views_of(flat.grad)])
-        res.append((loss, grads))
-        if pl == "1":
-            h0, c0 = ex.hs[0], ex.couts[0]
-            # the pooled input == the stand-alone pool with the coefficients block 0 published
-            ref = torch.zeros_like(ex.p[0])
-            C.bn_relu_pool_fwd(ex.y[0].data_ptr(), ex.coef[0].data_ptr(), ref.data_ptr(), 128, h0, h0, c0, SPAD,
-                               torch.cuda.current_stream().cuda_stream)
-            torch.cuda.synchronize()
-            assert torch.isfinite(ex.p[0].float()).all()
-            assert torch.equal(ex.p[0], ref)
-            # block 2's output == the plain region conv of that input
-            h1, ci1, co1 = ex.hs[1], ex.cins[1], ex.couts[1]
-            t1, sp1 = ex.fwd_plan[1]
-            y1 = torch.empty_like(ex.y[1])
-            C.conv_fwd(ex.p[0].data_ptr(), ex.p16[ex._leaf(1, 0)].data_ptr(), y1.data_ptr(), 0, 0, 128, h1, h1, ci1,
-                       co1, KSIZE, t1, 1, torch.cuda.current_stream().cuda_stream)
-            torch.cuda.synchronize()
-            assert torch.equal(ex.y[1], y1)
-            # running statistics: one momentum update with the batch statistics
-            coef = ex.coef[0].reshape(-1)  # [4][C]: mean, invstd, scale, shift
-            mean, istd = coef[:c0], coef[c0:2 * c0]
-            var = 1.0 / istd.double() ** 2 - BN_EPS
-            M = 128 * h0 * h0
-            bias = mdl.block_params(0)[1]
-            mo = BN_MOMENTUM
-            torch.testing.assert_close(ex.rm[0], (1 - mo) * rm0 + mo * (mean + bias), rtol=1e-4, atol=1e-5)
-            torch.testing.assert_close(ex.rv[0].double(), (1 - mo) * rv0.double() + mo * var * M / (M - 1), rtol=2e-3,
-                                       atol=1e-4)
-    (l0, g0), (l1, g1), (l2, g2) = res
-    rel = lambda a, b: float((a - b).norm() / b.norm())  # noqa: E731
-    assert abs(l0 - l1) < 1e-3 and abs(l0 - l2) < 1e-3
-    # fp32-atomic statistics make a random-init first step's gradients noisy
-    # (heavy-tailed: 0.036 measured against a 0.009 pair); the pooled input and
-    # the block-2 output above are the bitwise oracle
-    noise = rel(g1, g2)
-    assert min(rel(g1, g0), rel(g2, g0)) < max(3 * noise, 6e-2)
-
-
-@pytest.mark.parametrize("shape", [(8, 16, 64, 128), (8, 8, 128, 256), (3, 16, 64, 128), (3, 8, 128, 64),
-                                   (4, 16, 128, 64), (5, 8, 256, 128)])
-@pytest.mark.parametrize("tile", [0, 2])
-@pytest.mark.parametrize("splits", [1, 2])
-def test_region_direct_b_bitwise(C, shape, tile, splits):
-    """The direct-B region kernel (conv_fwd_region_bd_kernel: weights loaded
-    straight into a register queue, no LDS ring, no barrier in the k-loop)
-    accumulates every output in the region kernel's k order: forward output
-    and split-K slabs are BITWISE those of the LDS-ring region kernel (images
-    mode on both), the BN statistics equal to float rounding, and all within
-    bf16 error of fp32 conv2d."""
-    B, H, cin, cout = shape
-    if cout % _TILE_BN[tile] != 0 or (cin // 64) % splits != 0 or (cin // 64) // splits > 2:
-        pytest.skip("shape outside the region kernels")
-    if splits > 1 and 256 % (cout // 8) != 0:
-        pytest.skip("split-K combine needs Cout/8 | 256")
-    dev = torch.device("cuda")
-    g = torch.Generator(device=dev).manual_seed(101 + B * H + cin + tile)
-    x = torch.randn(B, H, H, cin, device=dev, generator=g).to(torch.bfloat16)
-    w = (torch.randn(cout, 5, 5, cin, device=dev, generator=g) * 0.05).to(torch.bfloat16)
-    xp = _pad(x)
-    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=2).permute(0, 2, 3, 1)
-    rows = C.conv_fwd_stat_rows(B, H, H, cin, cout, 5, tile, splits)
-    C.set_conv_region(2)
-    try:
-        ring_ok = C.conv_region_ok(B, H, H, cin, cout, 5, tile, splits)  # the LDS-ring kernel fits too
-    finally:
-        C.set_conv_region(1)
-    outs = []
-    for bd in ((0, 2) if ring_ok else (2,)):
-        C.set_conv_region(2)
-        C.set_conv_region_bd(bd)
-        try:
-            assert C.conv_region_ok(B, H, H, cin, cout, 5, tile, splits)
-            y = torch.empty(B, H, H, cout, dtype=torch.bfloat16, device=dev)
-            stats = torch.full((rows, 2, cout), float("nan"), device=dev)
-            slab = torch.full((splits * B * H * H * cout,), float("nan"), device=dev)
-            # keep the split-K slabs (FwdCfg bit 20): compare them, not only the combine
-            C.conv_fwd(xp.data_ptr(), w.data_ptr(), y.data_ptr(), stats.data_ptr() if splits == 1 else 0,
-                       slab.data_ptr(), B, H, H, cin, cout, 5, tile | ((1 << 20) if splits > 1 else 0), splits, _s())
-        finally:
-            C.set_conv_region(1)
-            C.set_conv_region_bd(0)
-        torch.cuda.synchronize()
-        if splits == 1:
-            assert _rel(y, ref) < 8e-3, bd
-            outs.append((y, stats))
-        else:
-            part = slab.view(splits, B, H, H, cout).sum(0)
-            assert _rel(part, ref) < 1e-3, bd
-            outs.append((slab,))
-    if len(outs) == 2:
-        # outputs / slabs bitwise; the BN statistics sum the wave rows of a tile in a
-        # different grouping (1 or 2 wave rows vs 2 or 4): equal to float rounding
-        assert torch.equal(outs[0][0], outs[1][0])
-        if splits == 1:
-            torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-3)
-
-
-def test_region_direct_b_dgrad_bn_reduce(C):
-    """The direct-B region kernel as the layer-2 dgrad with the previous
-    block's BN backward reduce in its epilogue (conv_fwd_bnred): dx bitwise
-    the LDS-ring region kernel's, the partial rows to float rounding."""
-    B, H, cin, cout = 8, 16, 64, 128  # the dgrad of block 2: dy [B,16,16,128] -> dP [B,16,16,64]
-    dev = torch.device("cuda")
-    g = torch.Generator(device=dev).manual_seed(5)
-    dy = torch.randn(B, H, H, cout, device=dev, generator=g).to(torch.bfloat16)
-    wt = (torch.randn(cin, 5, 5, cout, device=dev, generator=g) * 0.05).to(torch.bfloat16)
-    yprev = torch.randn(B, 2 * H, 2 * H, cin, device=dev, generator=g).to(torch.bfloat16)
-    coef = torch.stack([torch.randn(cin, device=dev, generator=g) * 0.1, torch.rand(cin, device=dev, generator=g) + 0.5,
-                        torch.rand(cin, device=dev, generator=g) + 0.5, torch.randn(cin, device=dev, generator=g) * 0.1])
-    dyp = _pad(dy)
-    outs = []
-    for bd in (0, 1):
-        C.set_conv_region_bd(bd)
-        try:
-            dx = torch.empty(B, H, H, cin, dtype=torch.bfloat16, device=dev)
-            rows = torch.full(((B * H * H + 127) // 128, 2, cin), float("nan"), device=dev)
-            T = C.conv_fwd_bnred(dyp.data_ptr(), wt.data_ptr(), dx.data_ptr(), B, H, H, cout, cin, 5, 2,
-                                 yprev.data_ptr(), coef.data_ptr(), rows.data_ptr(), _s())
-        finally:
-            C.set_conv_region_bd(0)
-        torch.cuda.synchronize()
-        outs.append((dx, rows[:T]))
-    assert torch.isfinite(outs[0][1]).all()
-    assert torch.equal(outs[0][0], outs[1][0])  # dx bitwise; the rows group the wave rows differently
-    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-3)
-
-
-# (B, H, Cin, Cout, splits): the reference's layer-4 forward (position-major
-# tiles) and dgrad, the layer-3 dgrad, an M tail (80 rows) with 3 slices
 FIX_SHAPES = [(128, 4, 256, 512, 2), (128, 4, 512, 256, 4), (128, 8, 256, 128, 2), (5, 4, 256, 128, 3),
               (32, 8, 128, 256, 4)]
 

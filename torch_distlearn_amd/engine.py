@@ -652,19 +652,79 @@ class DataParallelTrainer:
         self._multi[k] = (g, loss)
         return self._multi[k]
 
-    def comm_profile(self, batch, steps: int = 6) -> dict:
-        """Measure the bucketed all-reduce of ``steps`` eager training steps
-        (``batch``: a DeviceLoader, or a callable i -> (x, y)) with HIP events:
-        communication time, the part of it exposed after the backward, and
-        the overlap fraction (utils/profiling.comm_summary).  Collective:
-        every rank calls it at the same point.  The steps run outside any
-        hipGraph and the training state is restored afterwards, so the
-        measured run continues exactly as if this had not been called."""
+    def comm_profile(self, batch, steps: int = 6, replay: bool = False) -> dict:
+        """Measure the bucketed all-reduce with HIP events: communication time,
+        the part of it exposed after the backward, and the overlap fraction
+        (utils/profiling.comm_summary), over ``steps`` training steps
+        (``batch``: a DeviceLoader, or a callable i -> (x, y)).  Collective:
+        every rank calls it at the same point; the training state is restored
+        afterwards, so the measured run continues as if this had not been
+        called.
+
+        ``replay=True`` (a graph trainer on a DeviceLoader): the events are
+        event-record nodes INSIDE a captured one-step graph, read after each of
+        ``steps`` replays -- the schedule the timed loop runs, fork / join edges
+        of the replayed graph included.  Otherwise (or if
+        this ROCm cannot time graph event nodes) eager steps; the result's
+        ``source`` says which."""
         from .utils.profiling import comm_summary
 
         if self.bucketer is None or self.device.type != "cuda" or self.algo != "sgd":
             return {}
         loader = batch if hasattr(batch, "gather_args") else None
+        err = None
+        if replay and self.graph and loader is not None:
+            try:
+                return self._comm_profile_replay(loader, steps)
+            except RuntimeError as e:
+                err = str(e)[:200]
+                torch.cuda.synchronize()
+        out = self._comm_profile_eager(batch, loader, steps)
+        if out:
+            out["source"] = "eager steps"
+            if err is not None:
+                out["replay_error"] = err
+        return out
+
+    def _comm_profile_replay(self, loader, steps: int) -> dict:
+        from .utils.profiling import comm_summary
+
+        bk = self.bucketer
+        saved = self._snapshot(loader)
+        g = torch.cuda.CUDAGraph()
+        bk.profile, bk.profile_in_capture = [], True
+        try:
+            with _capturing(self.tree.comm), self._seq_record(g), \
+                    torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
+                self._step_body(loader, None)
+            recs = list(bk.profile)
+        finally:
+            bk.profile, bk.profile_in_capture = None, False
+        self.sgd.stepsPerNode[self.tree.nodeIndex - 1] -= 1  # the capture counted a step (not executed)
+        runs = []
+        try:
+            for i in range(steps + 1):  # the first replay is a warm-up
+                self._replay(g)
+                torch.cuda.synchronize()
+                if i:
+                    runs.append(comm_summary(recs, self.tree.numNodes))
+        finally:
+            self._track()
+            self._restore(saved, loader)
+            torch.cuda.synchronize()
+            del g
+        if not runs or not runs[0]:
+            return {}
+        out = dict(runs[0])
+        for k in ("comm_ms", "exposed_comm_ms", "overlap_fraction", "busbw_GBps"):
+            out[k] = round(sum(r[k] for r in runs) / len(runs), 4)
+        out["steps"] = len(runs)
+        out["source"] = "graph replays (event-record nodes in a captured one-step graph)"
+        return out
+
+    def _comm_profile_eager(self, batch, loader, steps: int) -> dict:
+        from .utils.profiling import comm_summary
+
         saved = self._snapshot(loader)
         self.bucketer.profile = []
         try:

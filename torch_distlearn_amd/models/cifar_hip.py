@@ -14,16 +14,11 @@ torch-autograd + cunn).  Per block i:
             -> bn_relu_pool_bwd_apply (dy) -> conv_wgrad (-> slab_reduce)
             -> conv dgrad (= conv_fwd on dy with flipped/transposed weights)
 
-Optional side stream (measured, off by default): the dgrad weight
-flip-transposes only depend on the previous update and could run during the
-forward (``DISTLEARN_PREP_FORK=1``); the weight gradient of block i only
-needs dy_i and the block's input and could run concurrently with the dgrad of
-block i and the BN/pool backward of block i-1 (``DISTLEARN_WGRAD_STREAM=1``).
-On MI355X both are net LOSSES at batch 128 inside the hipGraph (0.531 and
-0.567 vs 0.480 ms/step): every kernel of the step already spans the 256 CUs,
-concurrent kernels thrash each other's L2, and the cross-queue dependencies
-cost more than the overlap wins.  Forks re-join the main stream before
-forward_backward returns (graph-capturable fork/join).
+Side streams (the dgrad weight transposes during the forward, a block's
+weight gradient beside its dgrad) were measured as net losses inside the
+hipGraph (0.531 / 0.567 vs 0.480 ms/step, round 1) and removed in round 6:
+every kernel of the step spans the 256 CUs and a cross-queue edge costs more
+than the overlap wins.
 
 Gradients are written (fp32) straight into the flat gradient buffer; as soon
 as a block's gradients are final its leaves are reported to the
@@ -48,37 +43,19 @@ BF16 = torch.bfloat16
 CIN_PAD = 8  # the 3-channel input layer is zero-padded to 8 channels (one 16-B vector per tap)
 SPAD = KSIZE // 2  # spatial zero border of every convolution input (written once, never touched)
 
-# tile ids of conv_fwd: 0 = 128x128, 1 = 64x64, 2 = 128x64 (BK = 64) ; conv_wgrad: 0 = 128x64, 1 = 64x64, 2 = 128x128
+# tile ids of conv_fwd: 0 = 128x128, 1 = 64x64, 2 = 128x64 (BK = 64) ; conv_wgrad: 1 = 64x64, 2 = 128x128
 _FWD_TILES = {0: (128, 128), 1: (64, 64), 2: (128, 64)}
-_NOSPLIT_128x64 = os.environ.get("DISTLEARN_FWD_NOSPLIT", "1") == "1"
-_NOSPLIT_64 = os.environ.get("DISTLEARN_FWD_NOSPLIT64", "0") == "1"
-# split-K layers on 128x64 tiles with half the splits (fwd4 / dgrad4 at batch 128): half
-# the fp32 slab bytes written and combined, twice the workgroups per split;
-# 0.3306 vs 0.3347 ms/step (profiles/r3_split128x64_ab.txt)
-_SPLIT_128x64 = os.environ.get("DISTLEARN_SPLIT_128x64", "1") == "1"
-# weight gradients of Cout % 256 == 0 layers on 256x128 tiles (csrc conv_wgrad tile 3;
-# A/B, off): without fragment prefetch (the double fragment set spills at 2 waves per
-# SIMD) wgrad3 24.5 vs 22.4 us, end to end 0.358 vs 0.331 ms; tile 4 = 256x128 with 32-row
-# steps (fits with prefetch): wgrad3 25.7 vs 22.2 us, 0.361 vs 0.332 ms (profiles/r3_wgrad_tile256_ab.txt)
-_WGRAD_256 = os.environ.get("DISTLEARN_WGRAD_256", "0") == "1"
-
-
-# The fwd/dgrad split-K slab holds SLAB_CAP x splits slices, announced to
-# conv_fwd in tile-id bits 12-19: a position-major layer (output smaller than
-# the kernel) may then split its K steps per output pixel in proportion to
-# that pixel's valid taps (balanced plan, csrc conv_igemm.hip plan_posm_balance;
-# measured no faster, off: DISTLEARN_POSM_BALANCE=1 with DISTLEARN_SLAB_CAP=2).
-SLAB_CAP = int(os.environ.get("DISTLEARN_SLAB_CAP", "1"))
-
-
-def _slab_cap_bits(splits: int) -> int:
-    return (SLAB_CAP * splits) << 12 if splits > 1 else 0
 
 
 def _fwd_plan(M: int, N: int, K: int):
     """(tile, splits) for a forward/dgrad implicit GEMM: the biggest tile the
     channel count allows, then split-K until the grid covers the 256 CUs
-    (keeping >= 8 K-steps of 64 per split)."""
+    (keeping >= 8 K-steps of 64 per split).  Split-K layers run on 128x64
+    tiles with half the splits (half the fp32 slab bytes written and combined,
+    twice the workgroups per split: fwd4 / dgrad4 at batch 128, 0.3306 vs
+    0.3347 ms/step, profiles/r3_split128x64_ab.txt), and a 128x128 layer whose
+    128x64 tiles already fill the chip takes no split at all (no slab round
+    trip, no combine: fwd3 28.5 -> 24.7 us)."""
     tile = 0 if N % 128 == 0 else 2
     bm, bn = _FWD_TILES[tile]
     tiles = ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
@@ -86,20 +63,14 @@ def _fwd_plan(M: int, N: int, K: int):
     splits = 1
     while tiles * splits < 256 and ksteps // (splits * 2) >= 8:
         splits *= 2
-    if splits > 1 and tile == 0 and ((M + 127) // 128) * (N // 64) >= 256 and _NOSPLIT_128x64:
-        # 128x64 tiles already fill the chip without a K split: no slab round
-        # trip and no combine launch (fwd3 at batch 128: 28.5 -> 24.7 us)
+    if splits > 1 and tile == 0 and ((M + 127) // 128) * (N // 64) >= 256:
         return 2, 1
-    if splits > 1 and tile == 0 and _SPLIT_128x64:
+    if splits > 1 and tile == 0:
         return 2, max(1, splits // 2)
-    if splits > 1 and _NOSPLIT_64 and (M // 64) * (N // 64) >= 256 and M % 64 == 0 and N % 64 == 0:
-        # 64x64 tiles fill the chip without a K split: no fp32 slab round trip
-        # and no combine launch, at twice the LDS traffic per MFMA (A/B knob)
-        return 1, 1
     return tile, splits
 
 
-def _wgrad_plan(cout: int, K: int, M: int, reserve: int = 0, wide: Optional[bool] = None):
+def _wgrad_plan(cout: int, K: int, M: int, reserve: int = 0):
     """(tile, splits) for the weight gradient.  128x128 tiles (tile 2: 4-stage
     DMA ring, fragment prefetch, one workgroup per CU) whenever Cout allows,
     else 64x64 (two per CU).  Every workgroup is one ~20 us "round", so the
@@ -107,67 +78,16 @@ def _wgrad_plan(cout: int, K: int, M: int, reserve: int = 0, wide: Optional[bool
     conv3 50 tiles x 5 splits = 250 workgroups, 26 k-steps each, beats 4 splits
     = 200 workgroups of 32 k-steps by 1.7 us), keeping >= 512 rows per split.
     ``reserve`` CUs are left to a concurrent RCCL collective (its workgroups do
-    not fit beside these: parallel/comm.py)."""
+    not fit beside these: parallel/comm.py).  (Rejected and removed in round 6:
+    256x128 tiles, r3_wgrad_tile256_ab.txt; position-major steps,
+    r5_wgrad_posm_ab.txt; the first layer from an LDS-resident region,
+    r5_wgrad_c8r_ab.txt.)"""
     tile = 2 if cout % 128 == 0 else 1
-    if cout % 256 == 0 and (_WGRAD_256 if wide is None else wide):
-        tile = 3
-    if tile >= 2 and "DISTLEARN_WGRAD_TILE" in os.environ:  # tuning: 0 = 128x64, 2 = 128x128, 3 = 256x128
-        tile = int(os.environ["DISTLEARN_WGRAD_TILE"])
-        if tile >= 3 and cout % 256 != 0:
-            tile = 2
-    bm, bn = {4: (256, 128), 3: (256, 128), 2: (128, 128), 1: (64, 64), 0: (128, 64)}[tile]
+    bm, bn = {2: (128, 128), 1: (64, 64)}[tile]
     slots = 2 * (256 - reserve) if tile == 1 else 256 - reserve
     tiles = (cout // bm) * ((K + bn - 1) // bn)
     splits = max(1, min(slots // tiles, M // 512))
-    if os.environ.get("DISTLEARN_WGRAD_POW2", "0") == "1":  # A/B: the earlier power-of-two rule
-        splits = 1
-        while tiles * splits < 256 and M // (splits * 2) >= 2048:
-            splits *= 2
     return tile, splits
-
-
-# Position-major weight gradients for feature maps of at most this size (0 = off):
-# a K step is 64 images at ONE output pixel, and a column tile (one tap of a
-# 5x5 kernel) skips the pixels where it only reads the zero border -- layer 4
-# (4x4) visits 49 % of the pixel-major steps, layer 3 (8x8) 72 % -- with each
-# tile's steps balanced over as many workgroups as it needs (csrc ConvGeom::wposm).
-# Off: a position-major step gathers 64 rows 32 KB apart (one per image) where a
-# pixel-major step reads 64 adjacent pixels, and costs ~1.8x the time: wgrad3
-# 19.8 -> 27.5 us with 20 instead of 26 steps per workgroup, wgrad4 22.6 -> 26.0,
-# plus the extra slabs' sums; 0.312-0.314 vs 0.298-0.300 ms/step
-# (profiles/r5_wgrad_posm_ab.txt).  Tested option (test_wgrad_position_major).
-_WGRAD_POSM_MAX_HW = int(os.environ.get("DISTLEARN_WGRAD_POSM", "0"))
-
-
-def _wgrad_posm(C, B: int, h: int, cin: int, cout: int, tile: int, splits: int, reserve: int = 0):
-    """(tile id, splits) of a position-major weight gradient, or the pixel-major
-    plan unchanged: the fewest K steps per workgroup whose workgroups still fit
-    one round of the chip, when that beats the pixel-major steps per workgroup.
-    The tile id carries the steps (bits 8-15) and bit 16: splits a column tile
-    does not need write nothing (the executor's slabs are zero from allocation)."""
-    if h > _WGRAD_POSM_MAX_HW or tile not in (0, 2) or B % 64 != 0:
-        return tile, splits
-    slots = 256 - reserve
-    cur = -(-B * h * h // (64 * splits))  # pixel-major steps per workgroup
-    for steps in range(1, cur):
-        smax, total = C.wgrad_posm_plan(B, h, h, cin, cout, KSIZE, tile, steps)
-        if smax <= 1:
-            return tile, splits
-        if total <= slots:
-            return tile | (steps << 8) | (1 << 16), smax
-    return tile, splits
-
-
-# First-layer weight gradient from an LDS-resident input region (csrc
-# conv_wgrad_c8r_kernel): one workgroup per band of this many output rows owns
-# the whole 64 x 200 tile, reads its padded input rows once and streams only dy
-# (8 KB per 64-pixel step instead of 4 K tiles x 16 KB through the L2); one
-# slab per band.  0 = the generic split-K wgrad (default): the region kernel ran
-# 13.2 vs 11.7 us and its 256 slabs cost the update 1 us more -- 0.3052-0.3069 vs
-# 0.3020-0.3038 ms/step at 16 rows, 0.310-0.312 at 32 (profiles/r5_wgrad_c8r_ab.txt):
-# with one workgroup per CU its 16 transposed LDS reads per 7 MFMAs and the barrier
-# per 64-pixel step are exposed latency, so the L2 bytes it saves were not the bound.
-_WGRAD_C8R_ROWS = int(os.environ.get("DISTLEARN_WGRAD_C8R", "0"))
 
 
 class CifarHIPExecutor:
@@ -209,8 +129,7 @@ class CifarHIPExecutor:
         self.bucket_updates_safe = True
         for i in range(self.nb):
             self.g32[self._leaf(i, 1)].zero_()
-        self._wgrad_stages = int(os.environ.get("DISTLEARN_WGRAD_STAGES", "0"))  # tuning (3/4, 0 = per tile)
-        self.C.set_conv_stages(3, self._wgrad_stages)
+        self.C.set_conv_stages(3, 0)
         # The dgrad convolutions run while the bucketed all-reduce is in flight
         # (the first bucket is launched after the last layer's wgrad).  With one
         # CU held by a workgroup of RCCL's footprint (19.7 KiB LDS, ~280
@@ -218,130 +137,68 @@ class CifarHIPExecutor:
         # 256-workgroup streaming dgrad with the 3-stage ring (96 KiB LDS) slows
         # by 14 us (dgrad3/dgrad4 23 -> 37 us), with the 2-stage ring (64 KiB,
         # two workgroups fit a CU) by 1 us; the region dgrad (layer 2) by 1 us.
-        # With a real all-reduce (world > 1) the dgrads use the 2-stage ring.
+        # With a real all-reduce (world > 1) the dgrads use the 2-stage ring
+        # (the measured overlap policy may choose otherwise: select_policy).
         comm = getattr(bucketer, "comm", None)
         overlapped = comm is not None and runs_collectives(comm)
-        # 4 stages switch the streaming kernel to its fragment-prefetch loop (csrc
-        # conv_fwd_kernel, g_fwd_pf; fwd via DISTLEARN_FWD_STAGES=4): measured -1.3 % on one
-        # box and +0.7 % on the next (profiles/r3_fwd_prefetch_ab.txt), so 3 stays.
         self.dgrad_stages = int(os.environ.get("DISTLEARN_DGRAD_STAGES", "2" if overlapped else "3"))
-        # streaming-kernel forward configuration packed into the tile id (csrc conv_fwd
-        # FwdCfg: bits 4-7 ring stages, 8-11 waves; 0 = the global default)
-        self.fwd_cfg = (int(os.environ.get("DISTLEARN_FWD_STAGES", "0")) << 4) | (
-            int(os.environ.get("DISTLEARN_FWD_WAVES", "0")) << 8)
         # CUs held by the concurrent collective's workgroups (wgrad grids leave them free)
         self.cu_reserve = int(os.environ.get("DISTLEARN_CU_RESERVE",
                                              getattr(comm, "cu_reserve", 0) if overlapped else 0))
-        if "DISTLEARN_BN_MINW" in os.environ:  # A/B: "fwd,bwd" register caps of the BN fwd-fin / bwd-apply kernels (1|4)
-            self.C.set_bn_minw(*[int(v) for v in os.environ["DISTLEARN_BN_MINW"].split(",")])
-        if "DISTLEARN_C8_MT" in os.environ:  # tuning: layer-1 M tiles per workgroup (1, 2, 4, 8)
-            self.C.set_conv_c8_mt(int(os.environ["DISTLEARN_C8_MT"]))
-        if "DISTLEARN_FIN_GRID" in os.environ:  # tuning: grid cap of the row-summing BN consumers
-            self.C.set_bn_fin_grid(int(os.environ["DISTLEARN_FIN_GRID"]))
-        if "DISTLEARN_WGRAD_XCD" in os.environ:  # A/B: split-major XCD-aware wgrad grid (1) or the 2-D grid (0)
-            self.C.set_conv_wgrad_xcd(int(os.environ["DISTLEARN_WGRAD_XCD"]))
-        if "DISTLEARN_FWD_MMAJOR" in os.environ:  # A/B: fwd/dgrad tile order after the XCD swizzle
-            self.C.set_conv_fwd_order(int(os.environ["DISTLEARN_FWD_MMAJOR"]))
-        if "DISTLEARN_POSM_BALANCE" in os.environ:  # A/B: balanced (1) or uniform (0) position-major split-K
-            self.C.set_conv_posm_balance(int(os.environ["DISTLEARN_POSM_BALANCE"]))
-        if "DISTLEARN_POSM" in os.environ:  # A/B: position-major conv tiles for the 4x4 layer (1) or not (0)
-            self.C.set_conv_posm(int(os.environ["DISTLEARN_POSM"]))
-        if "DISTLEARN_FWD_TR" in os.environ:  # A/B: transposed-accumulator streaming kernel (1) or not (0)
-            self.C.set_conv_fwd_tr(int(os.environ["DISTLEARN_FWD_TR"]))
-        if "DISTLEARN_FWD_PF" in os.environ:  # A/B: streaming fwd/dgrad fragment prefetch (1) or not (0)
-            self.C.set_conv_fwd_pf(int(os.environ["DISTLEARN_FWD_PF"]))
-        if "DISTLEARN_WGRAD_ORDER" in os.environ:  # A/B: wgrad DMA before (1) or after (0) the fragment reads
-            self.C.set_conv_wgrad_order(int(os.environ["DISTLEARN_WGRAD_ORDER"]))
-        if "DISTLEARN_SGD_TRIM" in os.environ:  # A/B: update grid sized to the range left after the side job's
-            self.C.set_sgd_trim(os.environ["DISTLEARN_SGD_TRIM"] == "1")
-        if "DISTLEARN_WGRAD_PF" in os.environ:  # tuning: wgrad fragment prefetch (-1 auto, 0, 1)
-            self.C.set_conv_wgrad_pf(int(os.environ["DISTLEARN_WGRAD_PF"]))
-        # fuse the last block's BN/ReLU/pool into the head kernel (2048 pooled features)
-        self.head_pool = (os.environ.get("DISTLEARN_HEAD_POOL", "1") == "1"
-                          and (self.hs[-1] // 2) ** 2 * self.couts[-1] == 2048 and self.nclass == 10)
-        self.head_wgrad_fused = os.environ.get("DISTLEARN_HEAD_WGRAD_FUSED", "1") == "1" and self.nclass == 10
-        # (atomic-rows mode 2) the last block's BN backward reduce runs inside the head
-        # kernel and the classifier weight gradient rides the BN backward apply launch:
-        # bwd_reduce_head's launch is gone (DISTLEARN_HEAD_REDUCE=0: A/B)
-        self._region_mode = int(os.environ.get("DISTLEARN_REGION", "1"))
-        if "DISTLEARN_REGION" in os.environ:  # tuning: tap-reuse region conv kernel (0 off, 1 rows, 2 + images)
-            self.C.set_conv_region(self._region_mode)
+        # the last block's BN/ReLU/pool runs inside the head kernel (2048 pooled
+        # features, 10 classes: the reference net), which also computes the
+        # classifier's weight gradient
+        self.head_pool = (self.hs[-1] // 2) ** 2 * self.couts[-1] == 2048 and self.nclass == 10
         # the FORWARD conv of an image smaller than a 128-row tile (layer 3: 8x8, two
         # images per tile) on the region kernel's whole-image tiles: 20.5 vs 24.6 us
         # (scripts/bench_conv.py), 0.2981 vs 0.3021 ms/step (profiles/r5_fwd3_region_ab.txt);
         # the dgrad of that layer stays on the streaming kernel, which hosts the side SGD
-        self.fwd_region_images = (os.environ.get("DISTLEARN_FWD_REGION_IMAGES", "1") == "1"
-                                  and self._region_mode == 1)
-        # direct-B region kernel (weights straight into registers, no LDS ring or
-        # barrier in the k-loop; csrc conv_fwd_region_bd_kernel): 0 off, 1 row
-        # tiles (layer 2 fwd / dgrad), 2 + whole-image tiles (layer 3)
-        self.C.set_conv_region_bd(int(os.environ.get("DISTLEARN_REGION_BD", "0")))
-        if "DISTLEARN_BN_BWD_ITEMS" in os.environ:  # tuning: pooled pixels per thread of the BN backward reduce
-            self.C.set_bn_bwd_items(int(os.environ["DISTLEARN_BN_BWD_ITEMS"]))
-        self.side = torch.cuda.Stream(device=self.dev, priority=int(os.environ.get("DISTLEARN_SIDE_PRIORITY", "0"))) \
-            if self.dev.type == "cuda" else None
-        self.fork_transposes = os.environ.get("DISTLEARN_PREP_FORK", "0") == "1"
+        self.fwd_region_images = True
         # the dgrad weight flip-transposes ride the head launch (blocks past the batch,
         # on the CUs its 128 blocks leave idle) instead of the step's prep launch:
         # prep 9.0 -> 4.8 us (profiles/r3_head_transposes_ab.txt)
-        self.head_transposes = (os.environ.get("DISTLEARN_HEAD_TRANSPOSES", "1") == "1" and self.head_pool
-                                and not self.fork_transposes
-                                and all(self.cins[i] % 64 == 0 and self.couts[i] % 64 == 0 for i in range(1, self.nb)))
-        self.side_wgrad = os.environ.get("DISTLEARN_WGRAD_STREAM", "0") == "1"
-        # (optional) split-K slab reduce of a layer's weight gradient on the side
-        # stream, concurrent with that layer's dgrad; every layer has its own
-        # slab buffer.  Measured inside the hipGraph: 0.459 vs 0.400 ms/step
-        # (the cross-queue edges leave ~150 us of idle gaps per step), so off.
-        self.side_reduce = (not self.side_wgrad and self.side is not None
-                            and os.environ.get("DISTLEARN_REDUCE_STREAM", "0") == "1")
-        # Reduction mode (csrc/kernels/bn_fin_dev.h).  0 = deterministic
-        # partial rows + finalize kernels (bitwise run-to-run reproducible).  1 =
-        # BN statistics, BN parameter gradients and split-K weight gradients are
-        # accumulated with fp32 atomics into buffers the step's prep kernel zeroes
-        # and the consumers derive the BN coefficients themselves: 11 fewer kernel
-        # boundaries per step, but MEASURED SLOWER on MI355X (0.495 vs 0.358 ms/step
-        # at batch 128): same-address fp32 atomics serialise in the L2 -- the layer-1
-        # forward with 1024 workgroups adding into 128 addresses takes 31 us instead
-        # of 11, the 128-way split-K wgrad 56 us instead of 15 + 5 (slab reduce)
-        # (profiles/r2_mode1_timeline.txt).
-        # 2 (default) = the BN part of mode 1 with the atomics striped over R rows
-        # (row = tile / block index mod R, zeroed by the prep kernel, summed by every
-        # consumer block with all row loads in flight at once, overlapped with the
-        # block's first data loads: R-fold less same-address contention) and the
-        # weight gradients on split-K slabs as in mode 0: 7 finalize launches fewer.
-        # Measured interleaved on one box: 0.3466 vs 0.3625 ms/step (mode 0).  Not
-        # bitwise reproducible run to run (fp32 atomics in the BN statistics); the
-        # replicas stay bitwise identical (they apply the same all-reduced gradient).
+        self.head_wgrad_fused = self.nclass == 10  # the classifier wgrad inside the BN backward reduce launch
+        self.head_transposes = (self.head_pool and
+                                all(self.cins[i] % 64 == 0 and self.couts[i] % 64 == 0 for i in range(1, self.nb)))
+        # Reduction mode (csrc/kernels/bn_fin_dev.h).  0 = deterministic partial
+        # rows + finalize kernels (bitwise run-to-run reproducible: the bitwise
+        # graph-vs-eager and resume tests).  2 (default) = BN statistics and BN
+        # parameter gradients accumulated with fp32 atomics striped over R = 16
+        # rows (row = tile / block index mod R, zeroed by the prep kernel, summed
+        # by every consumer block with all row loads in flight, overlapped with
+        # its first data loads: R-fold less same-address contention than one
+        # row), weight gradients on split-K slabs: 7 finalize launches fewer,
+        # 0.3466 vs 0.3625 ms/step (profiles/r2_mode2_ab.txt).  Not bitwise
+        # reproducible run to run (fp32 atomics); the replicas stay bitwise
+        # identical (they apply the same all-reduced gradient).  (Mode 1 -- one
+        # atomic row and atomic split-K weight gradients -- measured 0.495 vs
+        # 0.358 ms/step, profiles/r2_mode1_timeline.txt; removed in round 6.)
         self.mode = int(os.environ.get("DISTLEARN_REDUCE_ATOMIC", "2"))
-        if self.mode not in (0, 1, 2):
-            raise ValueError("DISTLEARN_REDUCE_ATOMIC must be 0, 1 or 2")
-        # (optional, measured slower -> off) the slab reduction of block i's weight
-        # gradient in the same launch as block i-1's BN backward reduce (csrc
-        # bwd_reduce_slab_kernel): 2 launches fewer, but the combined kernels take
-        # 16.0 / 26.4 us vs 6.7 + 5.7 / 8.0 + 7.7 separately (the slab blocks run with
-        # the reduce's LDS / VGPR footprint): 0.3634 vs 0.3506 ms/step
-        # (profiles/r2_merge_slab_ab.txt)
-        self.merge_slab = os.environ.get("DISTLEARN_MERGE_SLAB", "0") == "1"
+        if self.mode not in (0, 2):
+            raise ValueError("DISTLEARN_REDUCE_ATOMIC must be 0 or 2")
         # a split-K dgrad's combine runs inside the BN backward reduce of the block
         # below (csrc bn_pool.hip combine_bwd_reduce): dP is produced, stored and
-        # reduced by one launch (DISTLEARN_FUSE_COMBINE=0: separate kernels, A/B)
+        # reduced by one launch (DISTLEARN_FUSE_COMBINE=0: separate kernels, the
+        # reference the fused path is tested against)
         self.fuse_combine = os.environ.get("DISTLEARN_FUSE_COMBINE", "1") == "1"
         # an unsplit (region-kernel) dgrad runs the BN backward reduce of the block
         # below in its epilogue (csrc conv_fwd_bnred; DISTLEARN_DGRAD_BNRED=0: A/B)
         self.dgrad_bnred = os.environ.get("DISTLEARN_DGRAD_BNRED", "1") == "1"
         # split-K forwards combine their slices in-launch (csrc splitk_fixup): the
-        # splitk_combine launch is gone (layer-4 forward 18.2 + 5.4 -> 22.6 us).
-        # DISTLEARN_FIX=2: the split-K dgrads too, their reducers running the BN
-        # backward reduce of the block below -- measured slower than the
-        # combine_bwd_reduce launch (dgrad4 22.9 -> 27.3, dgrad3 33.5 -> 36.6 us:
-        # the reducer's chain of slice drain, counter, slice loads and pool-window
-        # loads is serial latency at the kernel's tail), 0: off
+        # splitk_combine launch is gone (layer-4 forward 18.2 + 5.4 -> 22.6 us,
+        # profiles/r6_fix_ab.txt).  DISTLEARN_FIX=2: the split-K dgrads too, their
+        # reducers running the BN backward reduce of the block below -- measured
+        # slower than the combine_bwd_reduce launch (dgrad4 22.9 -> 25.9, dgrad3
+        # 33.5 -> 34.9 us: the reducer's chain of slice drain, counter, slice loads
+        # and pool-window loads is serial latency at the kernel's tail), 0: off
         self.fix = int(os.environ.get("DISTLEARN_FIX", "1"))
         self.atomic = self.mode > 0             # BN statistics / gradients by atomics, no finalize kernels
+        # (mode 2) the last block's BN backward reduce runs inside the head kernel and
+        # the classifier weight gradient rides the BN backward apply launch
+        # (DISTLEARN_HEAD_REDUCE=0: bwd_reduce_head's separate launch, the tests' reference)
         self.head_reduce = (os.environ.get("DISTLEARN_HEAD_REDUCE", "1") == "1" and self.mode == 2 and self.head_pool
-                            and self.head_wgrad_fused and self.couts[-1] == 512)
-        self.atomic_wgrad = self.mode == 1      # split-K weight gradients by atomics (else slabs)
-        self.rows = {0: 0, 1: 1, 2: int(os.environ.get("DISTLEARN_REDUCE_ROWS", "16"))}[self.mode]
+                            and self.couts[-1] == 512)
+        self.rows = {0: 0, 2: 16}[self.mode]
         self._alloc(self.B)
         self._deferred = ()  # blocks whose weight-gradient slab reduce the update performs (defer_slab_reduce)
         # multi-node step (fuse_slab_reduces): blocks whose slabs are summed by
@@ -374,11 +231,11 @@ class CifarHIPExecutor:
         self.coef = [torch.empty(4, c, device=d) for c in self.couts]
         self.acoef = [torch.empty(3, c, device=d) for c in self.couts]
         self.fwd_plan, self.stats = [], []
-        # atomic modes: R zeroed [2][C] (sum, sumsq) rows per layer in one arena; mode 2
-        # also R [2][C] (dgamma, dbeta) rows per layer for the backward reduce
+        # mode 2: R zeroed [2][C] (sum, sumsq) rows per layer in one arena, and R
+        # [2][C] (dgamma, dbeta) rows per layer for the backward reduce
         R = self.rows
         per = sum(2 * R * c for c in self.couts)
-        arena = torch.zeros(per * (2 if self.mode == 2 else 1), device=d) if self.atomic else None
+        arena = torch.zeros(2 * per, device=d) if self.atomic else None
         arena_off = 0
         self.bwd_rows = [None] * self.nb
         self.dgrad_plan = [None] * self.nb
@@ -391,12 +248,11 @@ class CifarHIPExecutor:
             K = KSIZE * KSIZE * cin
             tile, splits = _fwd_plan(M, cout, K)
             self.fwd_plan.append((tile, splits))
-            if splits > 1:  # x SLAB_CAP: room for the balanced position-major split-K plan
-                slab_elems = max(slab_elems, SLAB_CAP * splits * M * cout)
+            if splits > 1:
+                slab_elems = max(slab_elems, splits * M * cout)
             if self.atomic:
                 self.stats.append(arena[arena_off:arena_off + 2 * R * cout].view(R, 2, cout))
-                if self.mode == 2:
-                    self.bwd_rows[i] = arena[per + arena_off:per + arena_off + 2 * R * cout].view(R, 2, cout)
+                self.bwd_rows[i] = arena[per + arena_off:per + arena_off + 2 * R * cout].view(R, 2, cout)
                 arena_off += 2 * R * cout
             else:
                 rows = C.conv_fwd_stat_rows(B, h, h, cin, cout, KSIZE, tile, splits)
@@ -412,39 +268,21 @@ class CifarHIPExecutor:
                 if i + 1 < self.nb else g
             self.bwd_part.append(None if self.atomic else torch.empty(gp, 2, cout, device=d))
             tile_w, splits_w = _wgrad_plan(cout, K, M, self.cu_reserve)
-            if not self.atomic_wgrad:
-                tile_w, splits_w = _wgrad_posm(C, B, h, cin, cout, tile_w, splits_w, self.cu_reserve)
-            rb = _WGRAD_C8R_ROWS
-            if (not self.atomic_wgrad and i == 0 and rb > 0 and cin == 8 and cout == 64 and KSIZE * KSIZE <= 26
-                    and h in (8, 16, 32, 64) and h % rb == 0 and (rb * h) % 64 == 0):
-                tile_w, splits_w = -rb, B * h // rb  # tile < 0: conv_wgrad_c8 with -tile output rows per band
             direct = splits_w == 1 and cin == self.cins_real[i]
             self.wplan.append((tile_w, splits_w, direct))
-            if not direct and not self.atomic_wgrad:
+            if not direct:
                 wslab_elems = max(wslab_elems, splits_w * cout * K)
-            # (position-major plans: the slabs of splits a tile does not need stay zero)
-            alloc = torch.zeros if tile_w > 0 and (tile_w >> 16) & 1 else torch.empty
-            self.wslab_l.append(None if (direct or self.atomic_wgrad) else alloc(splits_w * cout * K, device=d))
+            self.wslab_l.append(None if direct else torch.empty(splits_w * cout * K, device=d))
             if i > 0:
                 dt, ds = _fwd_plan(M, cin, KSIZE * KSIZE * cout)
                 self.dgrad_plan[i] = (dt, ds)
                 if ds > 1:
-                    slab_elems = max(slab_elems, SLAB_CAP * ds * M * cin)
+                    slab_elems = max(slab_elems, ds * M * cin)
         self.slabs = torch.empty(max(slab_elems, 1), device=d)    # fwd / dgrad split-K (main stream)
-        # what the step's prep kernel zeroes in the atomic modes: the statistics arena
-        # (mode 2: + the backward rows); mode 1: every layer's [dgamma; dbeta] and the
-        # atomically accumulated weight gradients
+        # what the step's prep kernel zeroes in mode 2: the statistics arena and the backward rows
         self.zero_ranges = []
         if self.atomic:
             self.zero_ranges.append((arena.data_ptr(), arena.numel()))
-            for i in range(self.nb if self.mode == 1 else 0):
-                gw_, gb_ = self.g32[self._leaf(i, 2)], self.g32[self._leaf(i, 3)]
-                if gb_.data_ptr() != gw_.data_ptr() + 4 * gw_.numel():
-                    raise RuntimeError("BN weight/bias gradients must be adjacent in the flat buffer")
-                self.zero_ranges.append((gw_.data_ptr(), 2 * gw_.numel()))
-                if not self.wplan[i][2]:
-                    gw = self.g32[self._leaf(i, 0)]
-                    self.zero_ranges.append((gw.data_ptr(), gw.numel()))
             self._arena = arena
         self.logits = torch.empty(B, self.nclass, device=d)
         self.dlogits = torch.empty(B, self.nclass, device=d)
@@ -496,51 +334,42 @@ class CifarHIPExecutor:
                          self.cins_real[0], CIN_PAD, *tw, *self._zero_args(train), s)
         return B
 
-    def _prep_transposes(self, s: int) -> None:
-        """Flipped/transposed bf16 weights of blocks 2.. for the dgrad (one launch)."""
-        self.C.prep_step(0, 0, 0, self.cins_real[0], CIN_PAD, 0, 0, 0, 0, 0, 0, KSIZE * KSIZE, self.cins_real[0],
-                         CIN_PAD, *self._transpose_args(True), [], [], s)
-
     def _forward(self, B: int, s: int, train: bool, pool_last: bool = True):
         """Conv -> BN finalize -> BN/ReLU/pool per block.  ``pool_last=False``
-        leaves the last block's pool to the head kernel (head_fwd_bwd_pool)."""
+        leaves the last block's pool to the head kernel (head_fwd_bwd_pool).
+        (Block i-1's BN/ReLU/pool applied on load by block i's conv measured a
+        wash -- 25.9 us for the fused conv vs 18.1 + 8.2 us, both bound by the
+        one read of the pre-BN output, profiles/r4_pool_on_load_ab.txt --
+        and was removed in round 6.)"""
         C = self.C
         inp = self.x8
-        pooled = False  # block i-1's BN/ReLU/pool runs inside block i's conv (set_conv_pool_load)
         for i in range(self.nb):
             h, cin, cout = self.hs[i], self.cins[i], self.couts[i]
             M = B * h * h
             w = self.w1p if i == 0 else self.p16[self._leaf(i, 0)]
             t, sp = self.fwd_plan[i]
-            if pooled:
-                hp = self.hs[i - 1]
-                C.set_conv_pool_load(self.y[i - 1].data_ptr(), *self._fin_args(i - 1, B * hp * hp),
-                                     self.p[i - 1].data_ptr())
             img = self.fwd_region_images and h * h < 128 and 128 % (h * h) == 0
             if img:
                 C.set_conv_region(2)
             try:
-                if self._fix_ok(B, h, cin, cout, t | self.fwd_cfg, sp):
+                if self._fix_ok(B, h, cin, cout, t, sp):
                     ntm = C.conv_fwd_fix(inp.data_ptr(), w.data_ptr(), self.y[i].data_ptr(),
                                          self.stats[i].data_ptr() if train else 0, self.slabs.data_ptr(), B, h, h,
-                                         cin, cout, KSIZE, t | self.fwd_cfg, sp, 0, 0, 0, s)
+                                         cin, cout, KSIZE, t, sp, 0, 0, 0, s)
                 else:
                     ntm = C.conv_fwd(inp.data_ptr(), w.data_ptr(), self.y[i].data_ptr(),
                                      self.stats[i].data_ptr() if train else 0, self.slabs.data_ptr(), B, h, h, cin,
-                                     cout, KSIZE, t | self.fwd_cfg | _slab_cap_bits(sp), sp, s)
+                                     cout, KSIZE, t, sp, s)
             finally:
                 if img:
-                    C.set_conv_region(self._region_mode)
+                    C.set_conv_region(1)
             fused = train and self.atomic  # coefficients derived by the consumer kernel
             if not fused:
                 C.bn_finalize(self.stats[i].data_ptr(), ntm, cout, M, self.p32[self._leaf(i, 2)].data_ptr(),
                               self.p32[self._leaf(i, 3)].data_ptr(), self.p32[self._leaf(i, 1)].data_ptr(),
                               self.rm[i].data_ptr(), self.rv[i].data_ptr(), BN_EPS, BN_MOMENTUM, 0 if train else 1,
                               self.coef[i].data_ptr(), s)
-            pooled = fused and i + 1 < self.nb and self._pool_on_load(i + 1)
-            if pooled:
-                pass  # the next conv derives the coefficients and pools on load
-            elif pool_last or i + 1 < self.nb:
+            if pool_last or i + 1 < self.nb:
                 opad = SPAD if i + 1 < self.nb else 0
                 if fused:
                     C.bn_relu_pool_fwd_fin(self.y[i].data_ptr(), *self._fin_args(i, M), self.p[i].data_ptr(), B, h,
@@ -556,27 +385,10 @@ class CifarHIPExecutor:
         runs the epilogue) instead of a combine launch.  DISTLEARN_FIX=0: off."""
         return (self.fix > 0 and splits > 1 and self.C.conv_fix_ok(B, h, h, cin, cout, KSIZE, tile, splits) == 1)
 
-    def _pool_on_load(self, i: int) -> bool:
-        """Whether block i's conv takes block i-1's BN -> ReLU -> 2x2 pool on
-        load (csrc set_conv_pool_load: the region kernel derives the BN
-        coefficients, pools the pre-BN output of block i-1 into its LDS
-        region and writes the pooled copy the backward needs) instead of the
-        separate bn_relu_pool_fwd_fin launch.  Off by default (DISTLEARN_POOL_ON_LOAD=1:
-        on): the fused conv measured 25.9 us against 18.1 + 8.2 us for the two
-        launches, the step 0.3038 vs 0.3025 / 0.3107 vs 0.3107 ms -- both read
-        the pre-BN output once (the fused fill 1.5x with the halo rows), and
-        that read is what bounds them (profiles/r4_pool_on_load_ab.txt)."""
-        if os.environ.get("DISTLEARN_POOL_ON_LOAD", "0") != "1" or i < 1:
-            return False
-        t, sp = self.fwd_plan[i]
-        return (sp == 1 and self.hs[i - 1] == 2 * self.hs[i] and self.cins[i] == self.couts[i - 1]
-                and bool(self.C.conv_pool_load_ok(self.B, self.hs[i], self.hs[i], self.cins[i], self.couts[i], KSIZE,
-                                                  t)))
-
     def _fin_args(self, i: int, M: int):
         """(sums, M, gamma, beta, conv bias, running mean, running var, eps,
         momentum, coef) of block i for the kernels that finalize the BN
-        statistics themselves (mode 1)."""
+        statistics themselves (mode 2)."""
         return (self.stats[i].data_ptr(), M, self.p32[self._leaf(i, 2)].data_ptr(),
                 self.p32[self._leaf(i, 3)].data_ptr(), self.p32[self._leaf(i, 1)].data_ptr(), self.rm[i].data_ptr(),
                 self.rv[i].data_ptr(), BN_EPS, BN_MOMENTUM, self.coef[i].data_ptr())
@@ -588,8 +400,7 @@ class CifarHIPExecutor:
         gradient buffer.  Returns the mean loss (device tensor)."""
         C = self.C
         self._set_mode()
-        main, side = torch.cuda.current_stream(), self.side
-        s, ss = main.cuda_stream, side.cuda_stream
+        s = torch.cuda.current_stream().cuda_stream
         ctr = 0
         if hasattr(x, "gather_args"):
             labels = x.labels_out
@@ -607,13 +418,8 @@ class CifarHIPExecutor:
         else:
             if self.C.sgd_next_prep_armed():  # stale (an update that raised after arm_next_prep): drop it
                 self.C.disarm_sgd_next_prep()
-            B = self._prep(x, s, with_transposes=not (self.fork_transposes or self.head_transposes))
+            B = self._prep(x, s, with_transposes=not self.head_transposes)
         self._last_b = B
-        if self.fork_transposes:  # dgrad weight transposes overlap the forward
-            side.wait_stream(main)
-            self._prep_transposes(ss)
-            wt_ready = torch.cuda.Event()
-            wt_ready.record(side)
         self._forward(B, s, train=True, pool_last=not self.head_pool)
         nfc = 4 * self.nb
         if self.head_pool:  # the last block's BN/ReLU/pool runs inside the head kernel (writes p[-1])
@@ -642,13 +448,6 @@ class CifarHIPExecutor:
             C.head_wgrad(h_, dl_, lb_, F_, B, nc_, dw_, db_, loss_, slot_, ctr_, s)
             self._ready(nfc)
             self._ready(nfc + 1)
-        if self.fork_transposes:
-            main.wait_event(wt_ready)
-        ws = side if self.side_wgrad else main
-        wss = ws.cuda_stream
-        side_pending = False
-        merge = self.merge_slab and not (self.side_wgrad or self.side_reduce)
-        pending = None  # (slab args, block) of a weight gradient whose slab reduce rides the next BN reduce
         dp_splits = 0   # > 0: dP[i] is still in the split-K slabs of block i+1's dgrad (fused combine)
         dp_reduced = 0  # > 0: block i+1's dgrad epilogue already reduced dP[i] (rows written)
         for i in reversed(range(self.nb)):
@@ -657,9 +456,9 @@ class CifarHIPExecutor:
             M = B * h * h
             G = self.bwd_blocks[i]
             dY = self.dYs[i]
-            # mode 1: the reduce accumulates straight into [dgamma; dbeta] of the flat gradient;
-            # mode 2: into R striped rows (the apply kernel writes the totals to the flat gradient)
-            part = {0: self.bwd_part[i], 1: self.g32[self._leaf(i, 2)], 2: self.bwd_rows[i]}[self.mode]
+            # mode 0: deterministic partial rows; mode 2: R striped rows (the apply
+            # kernel writes the totals to the flat gradient)
+            part = self.bwd_rows[i] if self.atomic else self.bwd_part[i]
             if i == self.nb - 1 and self.head_reduce:
                 pass  # reduced inside the head kernel; the classifier wgrad rides the apply launch
             elif dp_reduced:
@@ -677,20 +476,11 @@ class CifarHIPExecutor:
                                          self.y[i].data_ptr(), self.coef[i].data_ptr(), part.data_ptr(), B, h, h, cout,
                                          s)
                 dp_splits = 0
-            elif pending is not None:
-                # one launch: this block's BN backward reduce + block i+1's weight-gradient slab reduce
-                sargs, blk = pending
-                C.bn_bwd_reduce_slab(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
-                                     part.data_ptr(), B, h, h, cout, G, *sargs, s)
-                for j in range(4):
-                    self._ready(self._leaf(blk, j))
-                pending = None
             else:
                 C.bn_relu_pool_bwd_reduce(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
                                           part.data_ptr(), B, h, h, cout, G, s)
             if self.atomic:
-                dgo, dbo = ((self.g32[self._leaf(i, 2)].data_ptr(), self.g32[self._leaf(i, 3)].data_ptr())
-                            if self.mode == 2 else (0, 0))
+                dgo, dbo = self.g32[self._leaf(i, 2)].data_ptr(), self.g32[self._leaf(i, 3)].data_ptr()
                 if i == self.nb - 1 and self.head_reduce:
                     h_, dl_, lb_, F_, nc_, dw_, db_, loss_, slot_, ctr_ = head_args
                     C.bn_bwd_apply_head(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
@@ -709,32 +499,17 @@ class CifarHIPExecutor:
                                   self.g32[self._leaf(i, 3)].data_ptr(), self.acoef[i].data_ptr(), s)
                 C.bn_relu_pool_bwd_apply(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
                                          self.acoef[i].data_ptr(), dY.data_ptr(), B, h, h, cout, SPAD, s)
-            # (optional fork) weight gradient of block i on the side stream
-            if self.side_wgrad:
-                side.wait_stream(main)
             xin = self.x8 if i == 0 else self.p[i - 1]
             K = KSIZE * KSIZE * cin
             tile, splits, direct = self.wplan[i]
             gw = self.g32[self._leaf(i, 0)]
             if direct:
-                C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), gw.data_ptr(), B, h, h, cin, cout, KSIZE, 1, K, tile, 0,
-                             wss)
-            elif self.atomic_wgrad:  # split-K partials atomically added into the zeroed gradient
-                C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), gw.data_ptr(), B, h, h, cin, cout, KSIZE, splits, K, tile,
-                             self.cins_real[i], wss)
-            rs = ws  # the stream that writes this block's weight gradient last
-            if not direct and not self.atomic_wgrad:
+                C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), gw.data_ptr(), B, h, h, cin, cout, KSIZE, 1, K, tile, 0, s)
+            else:
                 slab = self.wslab_l[i]
-                if tile < 0:  # the first layer from an LDS-resident input region, one slab per band
-                    C.conv_wgrad_c8(dY.data_ptr(), xin.data_ptr(), slab.data_ptr(), B, h, h, cin, cout, KSIZE, -tile,
-                                    K, wss)
-                else:
-                    C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), slab.data_ptr(), B, h, h, cin, cout, KSIZE,
-                                 splits, K, tile, 0, wss)
-                sargs = (slab.data_ptr(), gw.data_ptr(), splits, cout, KSIZE * KSIZE, cin, self.cins_real[i])
-                if merge and i > 0:  # reduced by block i-1's BN backward reduce launch
-                    pending = (sargs, i)
-                elif i in self._deferred:
+                C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), slab.data_ptr(), B, h, h, cin, cout, KSIZE, splits, K, tile,
+                             0, s)
+                if i in self._deferred:
                     pass  # summed by the update kernel (defer_slab_reduce)
                 elif i in self._ride:
                     pass  # summed by extra workgroups of this block's dgrad (fuse_slab_reduces)
@@ -742,49 +517,24 @@ class CifarHIPExecutor:
                     if i == self._merged[0]:  # the last merged block's wgrad: one launch sums them all
                         self._reduce_merged(s)
                 else:
-                    if self.side_reduce and i > 0:  # overlaps this block's dgrad (block 1 has none)
-                        side.wait_stream(main)
-                        rs = side
-                    C.slab_reduce(*sargs, rs.cuda_stream)
-            # conv bias grad: exactly 0 under train-mode BN (grad buffer was zero-filled).
-            # Bucket launches issued here are ordered after the stream that wrote the grads;
-            # a bucket readied on the main stream may also hold leaves reduced on the side
-            # stream earlier, so main joins the side stream first.
-            if rs is main and side_pending:
-                main.wait_stream(side)
-                side_pending = False
-            side_pending |= rs is side
+                    C.slab_reduce(slab.data_ptr(), gw.data_ptr(), splits, cout, KSIZE * KSIZE, cin, self.cins_real[i],
+                                  s)
+            # conv bias grad: exactly 0 under train-mode BN (zeroed once at construction)
             if i in self._ride or (i in self._merged and i != self._merged[0]):
                 pass  # ready once the launch that sums its slabs is enqueued
-            elif pending is None or pending[1] != i:
-                with torch.cuda.stream(rs):
-                    for b in (self._merged if i in self._merged else (i,)):
-                        for j in range(4):
-                            self._ready(self._leaf(b, j))
+            else:
+                for b in (self._merged if i in self._merged else (i,)):
+                    for j in range(4):
+                        self._ready(self._leaf(b, j))
             if i > 0:
                 dt, ds = self.dgrad_plan[i]
                 if self.dgrad_stages != 3:
-                    C.set_conv_stages(self.dgrad_stages, self._wgrad_stages)
-                fix = self.fix >= 2 and self._fix_ok(B, h, cout, cin, dt, ds) and not (merge and pending is not None)
-                keep = self.fuse_combine and ds in (2, 4, 8) and not (merge and pending is not None) and not fix
-                bnred = (self.dgrad_bnred and ds == 1 and not keep and self._region_dgrad(i, B)
-                         and not (merge and pending is not None))
-                if fix:
-                    # split-K slices combined inside the launch, whose reducers also
-                    # run block i-1's BN backward reduce (no combine_bwd_reduce launch)
-                    prt = {0: self.bwd_part[i - 1], 1: self.g32[self._leaf(i - 1, 2)], 2: self.bwd_rows[i - 1]}[self.mode]
-                    if self._side is not None and i == self._side["block"]:
-                        self._arm_side()
-                    elif i in self._ride:
-                        C.set_conv_side_reduce(*self._ride[i])
-                    dp_reduced = C.conv_fwd_fix(dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), 0,
-                                                self.slabs.data_ptr(), B, h, h, cout, cin, KSIZE, dt, ds,
-                                                self.y[i - 1].data_ptr(), self.coef[i - 1].data_ptr(), prt.data_ptr(), s)
-                    if i in self._ride:
-                        for j in range(4):
-                            self._ready(self._leaf(i, j))
-                elif bnred:
-                    prt = {0: self.bwd_part[i - 1], 1: self.g32[self._leaf(i - 1, 2)], 2: self.bwd_rows[i - 1]}[self.mode]
+                    C.set_conv_stages(self.dgrad_stages, 0)
+                fix = self.fix >= 2 and self._fix_ok(B, h, cout, cin, dt, ds)
+                keep = self.fuse_combine and ds in (2, 4, 8) and not fix
+                bnred = self.dgrad_bnred and ds == 1 and not keep and self._region_dgrad(i, B)
+                prt = self.bwd_rows[i - 1] if self.atomic else self.bwd_part[i - 1]
+                if bnred:
                     dp_reduced = C.conv_fwd_bnred(dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), B,
                                                   h, h, cout, cin, KSIZE, dt, self.y[i - 1].data_ptr(),
                                                   self.coef[i - 1].data_ptr(), prt.data_ptr(), s)
@@ -793,17 +543,23 @@ class CifarHIPExecutor:
                         self._arm_side()  # this launch also runs the update of blocks >= i
                     elif i in self._ride:
                         C.set_conv_side_reduce(*self._ride[i])  # ... or sums this block's weight-gradient slabs
-                    C.conv_fwd(dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), 0,
-                               self.slabs.data_ptr(), B, h, h, cout, cin, KSIZE,
-                               dt | _slab_cap_bits(ds) | ((1 << 20) if keep else 0), ds, s)
+                    if fix:
+                        # split-K slices combined inside the launch, whose reducers also
+                        # run block i-1's BN backward reduce (no combine_bwd_reduce launch)
+                        dp_reduced = C.conv_fwd_fix(dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(),
+                                                    0, self.slabs.data_ptr(), B, h, h, cout, cin, KSIZE, dt, ds,
+                                                    self.y[i - 1].data_ptr(), self.coef[i - 1].data_ptr(),
+                                                    prt.data_ptr(), s)
+                    else:
+                        C.conv_fwd(dY.data_ptr(), self.wt[i].data_ptr(), self.dP[i - 1].data_ptr(), 0,
+                                   self.slabs.data_ptr(), B, h, h, cout, cin, KSIZE, dt | ((1 << 20) if keep else 0),
+                                   ds, s)
                     if i in self._ride:
                         for j in range(4):
                             self._ready(self._leaf(i, j))
                 dp_splits = ds if keep else 0
                 if self.dgrad_stages != 3:
-                    C.set_conv_stages(3, self._wgrad_stages)
-        if self.side_wgrad or self.side_reduce:
-            main.wait_stream(side)  # join
+                    C.set_conv_stages(3, 0)
         return self.loss[0]
 
     def policies(self) -> dict:
@@ -845,7 +601,7 @@ class CifarHIPExecutor:
         streaming launch."""
         nb = self.nb
         if block is None:
-            block = int(os.environ.get("DISTLEARN_SIDE_SGD_BLOCK", str(nb - 2)))
+            block = nb - 2
         if not (0 < block < nb) or self.flat.shadow is None:
             return None
         if not self._dgrad_hosts_side_job(block):
@@ -895,8 +651,6 @@ class CifarHIPExecutor:
         is enqueued (CIFAR: blocks 1-2 share the last bucket, so merging them
         delays no all-reduce).  Returns {"ride": [...], "merged": [...]}."""
         self._ride, self._merged = {}, ()
-        if self.mode == 1 or self.side_wgrad or self.side_reduce or self.merge_slab:
-            return {}
         f = self.flat
         slab_blocks = [i for i in range(self.nb) if not self.wplan[i][2]]
         unpadded = lambda i: self.cins[i] == self.cins_real[i] and self.wplan[i][1] < 32  # noqa: E731
@@ -933,7 +687,7 @@ class CifarHIPExecutor:
         mo, wd = sd["mw"]
         lo, hi = sd["range"]
         self.C.set_conv_side_sgd(p, g, mom, p16, slot, float(sd["lr"]()), mo, wd, lo, hi, *sd["slabs"],
-                                 int(os.environ.get("DISTLEARN_SIDE_SGD_BLOCKS", "0")))  # 0: sized to the range
+                                 0)  # 0: one float4 per thread over the range
 
     def defer_slab_reduce(self):
         """Leave every split-K weight gradient in its slabs: the slab_reduce
@@ -944,8 +698,6 @@ class CifarHIPExecutor:
         same sums).  Only for a trainer that all-reduces nothing (one node):
         the flat gradient of those weights is then never written.
         Returns [(leaf, slab, splits, Cout, taps, Cp, C)] for the update."""
-        if self.mode == 1 or self.side_wgrad or self.side_reduce or self.merge_slab:
-            return []
         taps = KSIZE * KSIZE
         blocks = [i for i in range(self.nb) if not self.wplan[i][2]]
         padded = [i for i in blocks if not (self.cins[i] == self.cins_real[i] and self.wplan[i][1] < 32)]
@@ -969,7 +721,7 @@ class CifarHIPExecutor:
         update cannot carry it: the first layer's slab reduce not deferred,
         the dgrad transposes in the prep launch, no device loader."""
         if (not hasattr(loader, "gather_args") or self.cins[0] == self.cins_real[0]
-                or self.fork_transposes or not self.head_transposes or loader.batch > self.cap):
+                or not self.head_transposes or loader.batch > self.cap):
             return False
         h = self.hs[0]
         img, order, lab_all, lab_out, ctr, n_order, C, mean, std = loader.gather_args()

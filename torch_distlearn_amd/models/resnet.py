@@ -33,8 +33,8 @@ import torch.nn.functional as F
 # (ops/bn_nhwc.py, csrc/kernels/bn_nhwc.hip; default: 43.7 -> 35.5 ms/step).
 _BN_MODE = os.environ.get("DISTLEARN_RESNET_BN", "hip")
 # eval-mode BatchNorm (predict) on the same HIP apply kernel from the running
-# statistics (0: F.batch_norm on an fp32 copy)
-_BN_EVAL_HIP = os.environ.get("DISTLEARN_RESNET_BN_EVAL", "hip") == "hip"
+# statistics (False: F.batch_norm on an fp32 copy, the tests' reference)
+_BN_EVAL_HIP = True
 
 
 class _BN(nn.Module):
@@ -75,8 +75,7 @@ class _BN(nn.Module):
             residual is None or (residual.dtype == x.dtype and residual.shape == x.shape))
 
     def act(self, x, relu: bool = True, residual=None, acc=None, res_sink=None, have_stats: bool = False,
-            out_pad: int = 0, dx_pad: int = 0, bn_link=None, on_load: bool = False, defer: bool = False,
-            defer_pool: bool = False):
+            out_pad: int = 0, dx_pad: int = 0, defer: bool = False, defer_pool: bool = False):
         """act(BN(x) [+ residual]); one fused HIP kernel pair in "hip" mode
         (``acc`` with ``have_stats``: statistics already accumulated by the
         producing conv; else the step's zeroed arena slice, if any;
@@ -99,7 +98,7 @@ class _BN(nn.Module):
                 acc, have_stats = self.acc, False
             return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual, relu, acc=acc,
                           grads=self.bind, res_sink=res_sink, have_stats=have_stats if acc is not None else None,
-                          out_pad=out_pad, dx_pad=dx_pad, bn_link=bn_link, on_load=on_load,
+                          out_pad=out_pad, dx_pad=dx_pad,
                           defer_apply=defer and not relu and residual is None and have_stats and acc is not None,
                           defer_pool=defer_pool and relu and residual is None and have_stats and acc is not None
                           and not out_pad, pad_key=self.pad_bufs if _PAD_PERSIST else None)
@@ -115,60 +114,49 @@ class _BN(nn.Module):
 # weights (ops/conv.py); "miopen" = every convolution on MIOpen (A/B baseline).
 _CONV_MODE = os.environ.get("DISTLEARN_RESNET_CONV", "hip")
 # BatchNorm statistics from the 1x1 GEMM epilogue (skips the BN statistics pass)
-_FUSE_STATS = os.environ.get("DISTLEARN_RESNET_FUSE_STATS", "1") == "1"
+_FUSE_STATS = True
 # residual gradient added in the c1 dgrad epilogue (ops/conv.py conv_fwd_add).  With
 # the first epilogue (per-element 2-byte addend loads) the dgrad took 308 us instead
 # of 74 us (profiles/r2_resnet50_kernels_fuse_res.txt); the transposed epilogue loads
 # the addend 16 bytes at a time and the fusion now wins: 30.33 -> 29.68 ms/step.
-_FUSE_RES = os.environ.get("DISTLEARN_RESNET_FUSE_RES", "1") == "1"
+_FUSE_RES = True
 # stride-1 3x3 convolutions on the hand-written implicit-GEMM kernels (ops/conv.py
 # Conv3x3) for feature maps of at most this size (0 = off: MIOpen for all 3x3).
 # The 56x56 stage joined once the wgrad ran on the XCD-aware grid with one round
 # of 512 64x64 workgroups (161 vs MIOpen's 167 us; forward 88 vs 117 us:
 # profiles/r2_conv3x3_sweep_v2.jsonl); end to end 25.93 vs 25.94 ms/step with
 # the stage on MIOpen (profiles/r2_resnet_conv3_56_ab.txt).
-_CONV3_MAX_HW = int(os.environ.get("DISTLEARN_RESNET_CONV3_MAX_HW", "56"))
+_CONV3_MAX_HW = 56
 # channels-last copies of the KxK shadows (the HIP 3x3 / stem kernels' KRSC operand and
 # MIOpen's layout in the A/B mode), one launch per step (ops/conv.py)
-_CL_WEIGHTS = os.environ.get("DISTLEARN_RESNET_CL_WEIGHTS", "1") == "1"
+_CL_WEIGHTS = True
 # stem max-pool on the HIP gather-backward kernels (ops/pool.py)
-_POOL_HIP = os.environ.get("DISTLEARN_RESNET_POOL", "hip") == "hip"
+_POOL_HIP = True
 # stride-2 1x1 / 3x3 convolutions and the stem on the generalised MFMA kernels
-# (ops/conv.py Conv1x1S2 / Conv3x3S2 / StemConv; 0 = MIOpen, A/B)
-_STRIDED_HIP = os.environ.get("DISTLEARN_RESNET_STRIDED", "1") == "1"
+# (ops/conv.py Conv1x1S2 / Conv3x3S2 / StemConv; False = MIOpen, A/B)
+_STRIDED_HIP = True
 # classifier (mean + Linear + LogSoftMax + NLL, forward and backward) in one node on the
 # MFMA kernels (ops/head.py; 0 = torch mean / hipBLAS linear / torch log-softmax)
-_HEAD_HIP = os.environ.get("DISTLEARN_RESNET_HEAD", "hip") == "hip"
-# the BatchNorm backward sums (sum g, sum g*xhat) from the epilogue of the dgrad that
-# produces the BN's output gradient (b1 / b2: the c2 / c3 dgrads; b3: the next block's
-# c1 dgrad, which adds the residual gradient) instead of the BN's reduce pass over dz
-# and x (ops/conv.py _bn_reduce_begin); the b3 form reads the ReLU mask bits the forward
-# apply wrote.  Off: the reduce pass goes (-1.64 ms/step) but every fused epilogue
-# re-reads the BN input x, as many bytes as the dgrad writes, and the one-round dgrad
-# grids expose that latency (+2.0 ms): 24.53 vs 24.21 ms/step
-# (profiles/r5_resnet_bn_dgrad_ab.txt; round 3: r3_resnet_bn_dgrad_ab.txt)
-_BN_DGRAD = os.environ.get("DISTLEARN_RESNET_BN_DGRAD", "0") == "1"
-# b2's BatchNorm + ReLU applied by c3's 1x1 GEMM to its A operand on load (csrc
-# set_conv_bn_on_load): the b2 apply launch and its read of c2's output are gone
-# (c3 writes the activation its backward needs).  Off: measured 25.43 vs 24.64
-# ms/step -- the per-fragment transform and the activation stores inside the
-# GEMM cost more than the apply pass they replace
-# (profiles/r4_resnet_bn_on_load_ab.txt).
-_BN_ON_LOAD = os.environ.get("DISTLEARN_RESNET_BN_ON_LOAD", "0") == "1"
+_HEAD_HIP = True
+# (Rejected and removed in round 6: the BatchNorm backward sums in the epilogue
+# of the dgrad that produces the BN's output gradient -- the reduce pass goes,
+# -1.64 ms/step, but every fused epilogue re-reads the BN input, +2.0 ms,
+# profiles/r5_resnet_bn_dgrad_ab.txt; b2's BN + ReLU applied by c3's GEMM on
+# load, 25.43 vs 24.64 ms/step, profiles/r4_resnet_bn_on_load_ab.txt.)
 # the downsample branch's BatchNorm applied on load by the block's b3 apply (csrc
 # bn_nhwc.hip ResBn): b3 reads the downsample conv's output and applies that BN
 # itself, so the downsample BN's apply launch and the write + read of its output
 # go (4 per step, ~0.28 ms at batch 256)
-_DEFER_DOWN_BN = os.environ.get("DISTLEARN_RESNET_DEFER_DOWN_BN", "1") == "1"
+_DEFER_DOWN_BN = True
 # the stem BatchNorm + ReLU applied on load by the stem max-pool (csrc pool_nhwc.hip
 # PoolBn): the apply launch and the write + read of its 112x112x64 output go
-_DEFER_STEM_BN = os.environ.get("DISTLEARN_RESNET_DEFER_STEM_BN", "1") == "1"
+_DEFER_STEM_BN = True
 # the zero-bordered BN outputs / input gradients of the 3x3 convs in buffers that
 # persist per BatchNorm (border zeroed once, not by a zero_border launch per use):
 # 23.66-23.72 vs 23.72-23.92 ms/step (profiles/r5_resnet_pad_persist_ab.txt).  (The
 # first-loss mismatch seen with it was the head's atomic loss sum, which flips the
 # last bit of the mean run to run with or without it.)
-_PAD_PERSIST = os.environ.get("DISTLEARN_RESNET_PAD_PERSIST", "1") == "1"
+_PAD_PERSIST = True
 
 
 class _Conv(nn.Module):
@@ -216,14 +204,12 @@ class _Conv(nn.Module):
 
         return conv3x3_supported(shape, self.weight.shape[0])
 
-    def forward(self, x, stats=None, res_link=None, dx_sink=None, bn_link=None):
+    def forward(self, x, stats=None, res_link=None, dx_sink=None):
         """``stats``: optional fp32 [2*Cout] that receives the output's
         per-channel sum / sum of squares (HIP GEMM path only); ``res_link``:
         a dict through which another branch hands over its gradient of the
         same input (added in the dgrad epilogue); ``dx_sink``: the dict that
-        receives THIS conv's input gradient instead of autograd; ``bn_link``:
-        the dict of the BatchNorm that produced ``x`` (its backward sums come
-        from this conv's dgrad epilogue)."""
+        receives THIS conv's input gradient instead of autograd."""
         b = self.bind
         if b is None or not x.is_cuda or x.dtype != torch.bfloat16:
             return F.conv2d(x, self.weight.to(x.dtype), None, self.stride, self.pad)
@@ -232,19 +218,18 @@ class _Conv(nn.Module):
         # the same HIP kernels in training and in eval / predict (no-grad) mode
         grad = torch.is_grad_enabled()
         if self.hip_gemm(x):
-            return Conv1x1.apply(x, self.weight, b, stats, res_link if grad else None, dx_sink if grad else None,
-                                 bn_link if grad else None)
+            return Conv1x1.apply(x, self.weight, b, stats, res_link if grad else None, dx_sink if grad else None)
         if self.hip_3x3(x) and dx_sink is None:
             from ..ops.conv import Conv3x3
 
-            return Conv3x3.apply(x, self.weight, b, stats, bn_link if grad else None)
+            return Conv3x3.apply(x, self.weight, b, stats)
         if self.hip_strided(x):
             from ..ops.conv import Conv1x1S2, Conv3x3S2, StemConv
 
             if self.k == 7:
                 return StemConv.apply(x, self.weight, b, stats)
             if self.k == 3 and dx_sink is None:
-                return Conv3x3S2.apply(x, self.weight, b, stats, bn_link if grad else None)
+                return Conv3x3S2.apply(x, self.weight, b, stats)
             if self.k == 1:
                 return Conv1x1S2.apply(x, self.weight, b, stats, dx_sink if torch.is_grad_enabled() else None)
         if not torch.is_grad_enabled():
@@ -254,19 +239,15 @@ class _Conv(nn.Module):
 
 
 def _conv_bn(conv: _Conv, bn: "_BN", x, relu: bool = True, residual=None, link=None, res_sink=None, dx_sink=None,
-             out_pad: int = 0, dx_pad: int = 0, in_link=None, out_link=None, into: Optional[_Conv] = None,
-             defer: bool = False, defer_pool: bool = False):
+             out_pad: int = 0, dx_pad: int = 0, defer: bool = False, defer_pool: bool = False):
     """bn.act(conv(x)) with the BatchNorm statistics produced by the conv's
     epilogue when both run on the HIP kernels (one full read of the conv
     output fewer per BatchNorm).  ``out_pad`` / ``dx_pad``: the BatchNorm writes
     its output / input gradient zero-bordered (for a Conv3x3 neighbour).
-    ``in_link``: the bn_link of the BatchNorm that produced ``x`` (the conv's
-    dgrad epilogue computes its backward sums); ``out_link``: this
-    BatchNorm's own bn_link, for the next conv.  ``into``: the 1x1 conv that
-    consumes the output -- with DISTLEARN_RESNET_BN_ON_LOAD=1 it applies this
-    BN + ReLU to its operand on load (no separate apply launch)."""
-    kw = {"res_link": link, "dx_sink": dx_sink, "bn_link": in_link} if conv.bind is not None else {}
-    pads = {"out_pad": out_pad, "dx_pad": dx_pad, "bn_link": out_link}
+    ``defer`` / ``defer_pool``: the BN is applied on load by its consumer (the
+    block's b3, the stem max-pool)."""
+    kw = {"res_link": link, "dx_sink": dx_sink} if conv.bind is not None else {}
+    pads = {"out_pad": out_pad, "dx_pad": dx_pad}
     if _FUSE_STATS and (conv.hip_gemm(x) or conv.hip_3x3(x) or conv.hip_strided(x)) and _BN_MODE == "hip" \
             and bn.training:
         from .._native import native
@@ -276,9 +257,7 @@ def _conv_bn(conv: _Conv, bn: "_BN", x, relu: bool = True, residual=None, link=N
             acc = bn.acc if bn.acc is not None else torch.zeros(4 * cout, device=x.device)
             y = conv(x, stats=acc[:2 * cout], **kw)
             if bn.hip_ok(y, residual):
-                ol = (_BN_ON_LOAD and into is not None and relu and residual is None and not out_pad
-                      and out_link is None and into.hip_gemm(y))
-                return bn.act(y, relu, residual, acc=acc, res_sink=res_sink, have_stats=True, on_load=ol, defer=defer,
+                return bn.act(y, relu, residual, acc=acc, res_sink=res_sink, have_stats=True, defer=defer,
                               defer_pool=defer_pool, **pads)
             return bn.act(y, relu, residual)
     return bn.act(conv(x, **kw), relu, residual, res_sink=res_sink, **pads)
@@ -296,12 +275,6 @@ class _Bottleneck(nn.Module):
             self.down = nn.ModuleList([_Conv(cin, cout, 1, stride, g), _BN(cout)])
 
     def forward(self, x):
-        return self.forward_linked(x)[0]
-
-    def forward_linked(self, x, in_link=None):
-        """(output, bn_link of b3): ``in_link`` is the previous block's b3
-        bn_link -- its backward sums come from this block's c1 dgrad epilogue,
-        which also adds the residual's gradient (identity-residual blocks)."""
         # x feeds c1 (HIP GEMM) and a second branch: the identity residual (its
         # BatchNorm b3 hands the gradient of x over) or the downsample conv (hands
         # its dgrad over); c1's dgrad epilogue adds it -- no separate gradient sum.
@@ -315,17 +288,13 @@ class _Bottleneck(nn.Module):
         n, _, h, w = x.shape  # c1 is 1x1 stride 1: c2's input is [n, width, h, w]
         c2in = (n, self.c2.weight.shape[1], h, w)
         pad = 1 if (self.c2.hip_3x3(x, c2in) or (self.c2.k == 3 and self.c2.hip_strided(x, c2in))) else 0
-        l1 = {} if (_BN_DGRAD and torch.is_grad_enabled()) else None
-        l2 = {} if l1 is not None else None
-        l3 = {} if l1 is not None else None
-        y = _conv_bn(self.c1, self.b1, x, link=link, out_pad=pad, out_link=l1,
-                     in_link=in_link if self.down is None else None)
-        y = _conv_bn(self.c2, self.b2, y, dx_pad=pad, in_link=l1, out_link=l2, into=self.c3)
+        y = _conv_bn(self.c1, self.b1, x, link=link, out_pad=pad)
+        y = _conv_bn(self.c2, self.b2, y, dx_pad=pad)
         if self.down is None:
-            return _conv_bn(self.c3, self.b3, y, residual=x, res_sink=link, in_link=l2, out_link=l3), l3
+            return _conv_bn(self.c3, self.b3, y, residual=x, res_sink=link)
         # (the downsample BN's apply deferred into b3's: csrc ResBn)
         s = _conv_bn(self.down[0], self.down[1], x, relu=False, dx_sink=link, defer=_DEFER_DOWN_BN)
-        return _conv_bn(self.c3, self.b3, y, residual=s, in_link=l2, out_link=l3), l3
+        return _conv_bn(self.c3, self.b3, y, residual=s)
 
 
 class ResNet50(nn.Module):
@@ -359,9 +328,8 @@ class ResNet50(nn.Module):
         from ..ops.pool import max_pool2d_nhwc, supported
 
         h = max_pool2d_nhwc(h, 3, 2, 1) if (_POOL_HIP and supported(h)) else F.max_pool2d(materialize(h), 3, 2, 1)
-        link = None
         for b in self.blocks:
-            h, link = b.forward_linked(h, link)
+            h = b(h)
         return h
 
     def _hip_head(self, h) -> bool:

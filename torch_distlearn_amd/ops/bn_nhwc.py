@@ -12,7 +12,6 @@ op (tests/kernels/test_resnet_gpu.py).
 """
 from __future__ import annotations
 
-import os
 import weakref
 from typing import Optional
 
@@ -20,16 +19,12 @@ import torch
 
 from .._native import native, stream_handle
 
-# "apply_rows,reduce_threads" (csrc bn_nhwc.hip set_bn_tuning): A/B knob of the
-# kernels' rows in flight / reduce block size; empty = the compiled defaults
-_TUNE = os.environ.get("DISTLEARN_BN_TUNE", "")
-_tuned = False
 # BN + residual + ReLU keeps its ReLU mask as bits for the backward (relu mode 3)
-# instead of re-reading the output y in both backward passes; 0 = mode 1 (A/B)
-_MASK_BITS = os.environ.get("DISTLEARN_BN_MASK_BITS", "1") == "1"
+# instead of re-reading the output y in both backward passes; False = mode 1 (A/B)
+_MASK_BITS = True
 # ... and hands (dy, mask bits) to the residual's consumer instead of writing
-# the residual gradient (DISTLEARN_BN_MASKED_ADDEND=0: writes dres, A/B)
-_MASKED_ADDEND = os.environ.get("DISTLEARN_BN_MASKED_ADDEND", "1") == "1"
+# the residual gradient (False: writes dres -- the tests' reference path)
+_MASKED_ADDEND = True
 
 
 def unpack_mask_bits(mbits: torch.Tensor, shape_like: torch.Tensor) -> torch.Tensor:
@@ -42,13 +37,7 @@ def unpack_mask_bits(mbits: torch.Tensor, shape_like: torch.Tensor) -> torch.Ten
 
 
 def _bn():
-    global _tuned
-    C = native()
-    if not _tuned:
-        _tuned = True
-        if _TUNE:
-            C.set_bn_tuning(*[int(v) for v in _TUNE.split(",")])
-    return C
+    return native()
 
 
 def _geom(x: torch.Tensor):
@@ -149,7 +138,7 @@ class _BnAct(torch.autograd.Function):
         # alone does not give.  The apply writes it as bits (one byte per 8
         # channels per row, 1/16 of y) so both backward passes read that instead
         # of y (relu mode 3); y itself is then not kept for the backward (a
-        # consuming dgrad that computes the backward sums, bn_link, reads the bits too).
+        # consuming c1 dgrad adds the residual gradient under the bits too).
         mbits = None
         if relu and residual is not None and _MASK_BITS:
             mbits = torch.empty(M * C // 8, dtype=torch.uint8, device=x.device)
@@ -158,12 +147,7 @@ class _BnAct(torch.autograd.Function):
                  running_mean.data_ptr() if running_mean is not None else 0,
                  running_var.data_ptr() if running_var is not None else 0, M, C, float(eps), float(momentum),
                  int(relu), int(have_stats), H, W, int(out_pad))
-        if on_load and relu and residual is None and have_stats and not out_pad and mbits is None:
-            # y's content comes from the consuming 1x1 GEMM (ops/conv.py Conv1x1):
-            # it applies this BN + ReLU to its A operand on load and writes y, or
-            # runs this apply first when its tile has no on-load instance
-            y._dl_bn_on_load = apply
-        elif defer_pool and relu and residual is None and have_stats and not out_pad and mbits is None:
+        if defer_pool and relu and residual is None and have_stats and not out_pad and mbits is None:
             # y feeds the stem max-pool, which applies this BN + ReLU on load (csrc
             # pool_nhwc.hip PoolBn); the backward needs neither y nor its mask (relu 2)
             y._dl_pool_bn = (apply, (x, acc, weight, bias, save, running_mean, running_var, eps, momentum))
@@ -206,13 +190,6 @@ class _BnAct(torch.autograd.Function):
         # neither saved nor read)
         ctx.relu = (3 if mbits is not None else 1 if ctx.has_res else 2) if relu else 0
         ctx.save_for_backward(x, y if ctx.relu == 1 else mbits, weight, bias, save, acc)
-        ctx.bn_link = bn_link if ctx.relu else None
-        if ctx.bn_link is not None:
-            # what the consuming convolution's dgrad epilogue needs to compute this
-            # BatchNorm's backward sums itself (ops/conv.py _bn_reduce_begin); with a
-            # residual the ReLU mask is the output's sign: its bits (relu mode 3) or y (1)
-            bn_link["fwd"] = (x, save, weight, bias, acc, C, y if ctx.relu == 1 else None,
-                              mbits if ctx.relu == 3 else None)
         return y
 
     @staticmethod
@@ -246,8 +223,7 @@ class _BnAct(torch.autograd.Function):
                 and not ctx.res_sink.get("done"))
         dres = torch.empty_like(x, memory_format=torch.channels_last) if (ctx.has_res and not park) else None
         acc = acc4[2 * C:]
-        # the consumer's dgrad epilogue already reduced sum(g), sum(g*xhat) into acc
-        have_sums = bool(ctx.bn_link is not None and ctx.bn_link.pop("sums", False))
+        have_sums = False  # (the dgrad-epilogue sums of round 5 were removed in round 6)
         if ctx.backwards and not have_sums:  # the kernels accumulate atomically into the zeroed
             acc.zero_()                       # half: a second backward (retain_graph) restarts at 0
         ctx.backwards += 1
@@ -324,8 +300,7 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
            running_var: Optional[torch.Tensor], residual: Optional[torch.Tensor] = None, relu: bool = True,
            eps: float = 1e-5, momentum: float = 0.1, acc: Optional[torch.Tensor] = None,
            grads=None, res_sink: Optional[dict] = None, have_stats: Optional[bool] = None, out_pad: int = 0,
-           dx_pad: int = 0, bn_link: Optional[dict] = None, on_load: bool = False,
-           defer_apply: bool = False, defer_pool: bool = False, pad_key=None) -> torch.Tensor:
+           dx_pad: int = 0, defer_apply: bool = False, defer_pool: bool = False, pad_key=None) -> torch.Tensor:
     """``acc``: optional fp32 [4C] whose last 2C are zero; with ``have_stats``
     (the default when ``acc`` is given) its first 2C already hold the
     per-channel sum / sum of squares of x (see ops/conv.py Conv1x1), else they
@@ -339,16 +314,6 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
     ``out_pad`` / ``dx_pad``: write the output / the input gradient as the
     interior of a zero-bordered buffer (:func:`padded_empty`) for a 3x3
     convolution that reads it directly.
-    ``bn_link``: a dict shared with the convolution that consumes this
-    BatchNorm's output (ReLU only; with a residual, a consumer whose dgrad
-    epilogue adds the residual's gradient): the forward parks what that
-    convolution's dgrad epilogue needs to produce the backward sums
-    sum(g), sum(g*xhat) (ops/conv.py ``fused_bn_reduce``); the backward then
-    skips its own reduce pass over dy and x.
-    ``on_load`` (ReLU, no residual, statistics given, unpadded output): the
-    returned tensor is filled by the 1x1 GEMM that consumes it, which applies
-    this BN + ReLU to its operand on load (ops/conv.py Conv1x1; csrc
-    set_conv_bn_on_load) -- the apply launch and its read of x are skipped.
     ``defer_apply`` (no ReLU, no residual, statistics given, unpadded): the
     returned tensor is only a handle for the BN + residual + ReLU that takes it
     as its residual -- that apply reads this BN's input and applies it on load
@@ -377,4 +342,4 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
         have_stats = acc is not None
     return _BnAct.apply(x, weight.contiguous(), bias.contiguous(), running_mean, running_var, residual, relu, eps,
                         momentum, acc, grads, res_sink, bool(have_stats), int(out_pad), int(dx_pad),
-                        bn_link if relu else None, bool(on_load), bool(defer_apply), bool(defer_pool), pad_key)
+                        None, False, bool(defer_apply), bool(defer_pool), pad_key)

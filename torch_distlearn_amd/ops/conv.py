@@ -37,7 +37,6 @@ Reference parity: these are the ResNet-50 stress config of BASELINE.json
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn.functional as F
@@ -45,22 +44,6 @@ import torch.nn.functional as F
 from .._native import native, stream_handle
 
 BF16 = torch.bfloat16
-
-# BN statistics of the forward convs as one partial row per (M tile, wave row), written
-# straight from the epilogue lanes (conv_igemm.hip ConvGeom::swave, tile-id bit 21):
-# no LDS round trip and no barriers in the epilogue; up to 4x the rows for bn_rows_reduce.
-# Off: 25.62 vs 25.58 ms/step (profiles/r3_resnet_stats_wave_ab.txt) -- the epilogue's
-# barriers are not what the statistics cost
-_STATS_WAVE = os.environ.get("DISTLEARN_RESNET_STATS_WAVE", "0") == "1"
-_SWAVE_BIT = 1 << 21
-
-
-def _stats_cfg(tile: int, nrows: int):
-    """(tile id, row capacity) of a forward conv that emits BN statistics."""
-    if _STATS_WAVE:
-        return tile | _SWAVE_BIT, 4 * nrows
-    return tile, nrows
-
 
 class ShadowBinding:
     """What a conv module needs from the trainer: its bf16 shadow weight view,
@@ -130,63 +113,10 @@ def _plan_1x1(M: int, N: int, K: int):
     return tile | (stages << 4) | (waves << 8), 1
 
 
-# ResNet-50 1x1 weight gradients on the 256x128 tile where Cout allows (A/B, default off)
-_WGRAD_256 = os.environ.get("DISTLEARN_RESNET_WGRAD_256", "0") == "1"
-
-
 def _wgrad_plan(cout: int, K: int, M: int):
     from ..models.cifar_hip import _wgrad_plan as plan
 
-    return plan(cout, K, M, 0, wide=_WGRAD_256)
-
-
-def _bn_reduce_begin(C, link, M: int, cin: int, nrows: int, residual_add: bool = False):
-    """Arm the dgrad epilogue's BatchNorm backward reduce: ``link`` is the dict
-    the BatchNorm that produced this conv's input filled in its forward
-    (ops/bn_nhwc.py ``bn_link``: its input x, [mean; invstd], gamma, beta and
-    its [4C] sums buffer).  The dgrad output IS that BatchNorm's output
-    gradient dz, so the epilogue computes g = dz * (x*scale + shift > 0) and
-    per-M-tile partial rows of sum(g), sum(g*xhat) while dz is still in
-    registers (csrc conv_igemm.hip set_conv_bn_reduce, BnRedArgs BNR 2): the
-    BatchNorm backward's reduce pass -- a full read of dz and x -- goes away.
-    A BatchNorm + residual + ReLU (the bottleneck's b3) takes its mask from
-    its saved output; its output gradient is only complete in the epilogue of
-    the next block's c1 dgrad that adds the residual's gradient
-    (``residual_add``).  Returns the state for :func:`_bn_reduce_end`, or
-    None (not linked / not applicable)."""
-    f = link.get("fwd") if link is not None else None
-    if f is None:
-        return None
-    x, save, w, b, acc4, cc, ym, mb = f
-    if (ym is not None or mb is not None) != residual_add:
-        return None
-    if cc != cin or x.numel() != M * cin or not x.is_contiguous(memory_format=torch.channels_last):
-        return None
-    if ym is not None and (ym.numel() != M * cin or not ym.is_contiguous(memory_format=torch.channels_last)):
-        return None
-    if mb is not None and mb.numel() * 8 != M * cin:
-        return None
-    rows = torch.empty(max(1, nrows), 2, cc, device=x.device)
-    C.set_conv_bn_reduce(x.data_ptr(), save.data_ptr(), w.data_ptr(), b.data_ptr(), rows.data_ptr(),
-                         0 if ym is None else ym.data_ptr(), 0 if mb is None else mb.data_ptr())
-    return rows, f
-
-
-def _bn_reduce_end(C, link, st, T: int, s) -> None:
-    """Disarm, then column-sum the partial rows into the BatchNorm's backward
-    half of its sums buffer and tell its backward (``link["sums"]``)."""
-    C.set_conv_bn_reduce(0, 0, 0, 0, 0)
-    rows, (x, save, w, b, acc4, cc, _, _) = st
-    accb = acc4[2 * cc:]
-    if link.get("nbwd", 0):  # a second backward (retain_graph): start from 0 again
-        accb.zero_()
-    link["nbwd"] = link.get("nbwd", 0) + 1
-    C.bn_rows_reduce(rows.data_ptr(), T, cc, accb.data_ptr(), s)
-    link["sums"] = True
-
-
-def _bn_disarm(C):
-    C.set_conv_bn_reduce(0, 0, 0, 0, 0)
+    return plan(cout, K, M, 0)
 
 
 def conv1x1_supported(x: torch.Tensor, cout: int) -> bool:
@@ -224,33 +154,16 @@ class ChannelsLastWeights:
         native().weights_to_cl(self.table.data_ptr(), self.n, stream_handle())
 
 
-def _on_load_ok(tile: int, splits: int, cin: int, stats: bool) -> bool:
-    """Whether the 1x1 GEMM of this packed tile id has a BN-on-load instance
-    (csrc set_conv_bn_on_load): 128x128 tile, 4 or 8 waves, a 2- or 3-stage
-    ring (0: the global default, 3), one split, statistics, Cin % 64 == 0,
-    Cin <= 512."""
-    st, wv = (tile >> 4) & 15, (tile >> 8) & 15
-    return ((tile & 15) == 0 and splits == 1 and stats and st in (0, 2, 3) and wv in (0, 4, 8)
-            and cin % 64 == 0 and cin <= 512)
-
-
 class Conv1x1(torch.autograd.Function):
     """y = conv1x1(x, W) on the MFMA kernels; x channels-last bf16 [N, Cin, H, W]."""
 
     @staticmethod
-    def forward(ctx, x, weight, bind: ShadowBinding, stats, res_link=None, dx_sink=None, bn_link=None):
+    def forward(ctx, x, weight, bind: ShadowBinding, stats, res_link=None, dx_sink=None):
         C = native()
         ctx.res_link = res_link
-        ctx.bn_link = bn_link
         ctx.dx_sink = dx_sink
         if dx_sink is not None:
             dx_sink["expect"] = True  # dx goes to the sink's consumer, not to autograd
-        ol = getattr(x, "_dl_bn_on_load", None)  # x: a BatchNorm output still to be computed (bn_act on_load)
-        if ol is not None:
-            del x._dl_bn_on_load
-            if not x.is_contiguous(memory_format=torch.channels_last):
-                native().bn_nhwc_fwd_pad(*ol, stream_handle(), 0)
-                ol = None
         x = x.contiguous(memory_format=torch.channels_last)
         N, cin, H, W = x.shape
         cout = weight.shape[0]
@@ -265,16 +178,7 @@ class Conv1x1(torch.autograd.Function):
             if C.reduce_atomic() != 0:
                 raise RuntimeError("Conv1x1 statistics need reduction mode 0 (partial rows)")
             nrows = C.conv_fwd_stat_rows(M, 1, 1, cin, cout, 1, tile, splits)
-            if splits == 1:
-                tile, nrows = _stats_cfg(tile, nrows)
             rows = torch.empty(max(nrows, 400 if splits > 1 else 1), 2, cout, device=x.device)
-        if ol is not None:
-            if _on_load_ok(tile, splits, cin, rows is not None):
-                # this GEMM reads the BN input, applies BN + ReLU on load and writes x
-                (xin, _, _, acc, w, b, save, rm, rv, Mx, Cx, eps, mom) = ol[:13]
-                C.set_conv_bn_on_load(xin, acc, w, b, save, rm, rv, Mx, Cx, eps, mom, x.data_ptr())
-            else:
-                C.bn_nhwc_fwd_pad(*ol, s, 0)
         T = C.conv_fwd(x.data_ptr(), bind.w16.data_ptr(), y.data_ptr(), 0 if rows is None else rows.data_ptr(),
                        0 if slab is None else slab.data_ptr(), M, 1, 1, cin, cout, 1, tile, splits, s)
         if rows is not None:  # ... -> sum / sum of squares per channel for the BatchNorm
@@ -319,31 +223,13 @@ class Conv1x1(torch.autograd.Function):
             dx = torch.empty_like(x, memory_format=torch.channels_last)
             tile, splits = _plan_1x1(M, cin, cout)
             if add is not None and splits == 1:
-                # the previous block's b3 (BN + residual + ReLU) backward sums in this epilogue
-                bst = _bn_reduce_begin(C, ctx.bn_link, M, cin, (M + 127) // 128, residual_add=True) \
-                    if s2 is None else None
-                try:
-                    C.conv_fwd_add(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), add.data_ptr(), M, 1, 1, cout, cin,
-                                   1, tile, s, 0 if add_mask is None else add_mask.data_ptr())
-                finally:
-                    if bst is not None:
-                        _bn_disarm(C)
-                if bst is not None:
-                    _bn_reduce_end(C, ctx.bn_link, bst, (M + 127) // 128, s)
+                C.conv_fwd_add(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), add.data_ptr(), M, 1, 1, cout, cin,
+                               1, tile, s, 0 if add_mask is None else add_mask.data_ptr())
                 add = None
             else:
                 slab = torch.empty(splits * M * cin, device=x.device) if splits > 1 else None
-                bst = None
-                if splits == 1 and add is None and s2 is None:
-                    bst = _bn_reduce_begin(C, ctx.bn_link, M, cin, (M + 127) // 128)
-                try:
-                    T = C.conv_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0,
-                                   0 if slab is None else slab.data_ptr(), M, 1, 1, cout, cin, 1, tile, splits, s)
-                finally:
-                    if bst is not None:
-                        _bn_disarm(C)
-                if bst is not None:
-                    _bn_reduce_end(C, ctx.bn_link, bst, T, s)
+                C.conv_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, 0 if slab is None else slab.data_ptr(), M,
+                           1, 1, cout, cin, 1, tile, splits, s)
             if add is not None:
                 if add_mask is not None:  # (split-K dgrad: the masked residual gradient the slow way)
                     from .bn_nhwc import unpack_mask_bits
@@ -370,7 +256,7 @@ class Conv1x1(torch.autograd.Function):
         if ctx.dx_sink is not None and dx is not None:
             ctx.dx_sink["g"] = dx
             dx = None
-        return dx, None, None, None, None, None, None
+        return dx, None, None, None, None, None
 
 
 PAD_COPIES = [0]  # Conv3x3 inputs / gradients that had to be padded by a copy (tests)
@@ -409,7 +295,7 @@ def _plan_3x3(M: int, N: int, K: int):
     return tile | (2 << 4) | (waves << 8), 1
 
 
-_W4_C64 = os.environ.get("DISTLEARN_RESNET_3X3_W4", "1") == "1"
+_W4_C64 = True  # (r5_conv3x3_sweep.jsonl)
 
 
 def _wgrad_plan_3x3(cout: int, K: int, M: int):
@@ -438,12 +324,11 @@ class Conv3x3(torch.autograd.Function):
     (GEMM epilogue rows, as Conv1x1)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bind: ShadowBinding, stats, bn_link=None):
+    def forward(ctx, x, weight, bind: ShadowBinding, stats):
         C = native()
         N, cin, H, W = x.shape
         cout = weight.shape[0]
         keep, xbase = _padded_base(x, 1)
-        ctx.bn_link = bn_link
         M, K = N * H * W, 9 * cin
         y = torch.empty((N, cout, H, W), dtype=BF16, device=x.device, memory_format=torch.channels_last)
         tile, splits = _plan_3x3(M, cout, K)
@@ -454,8 +339,6 @@ class Conv3x3(torch.autograd.Function):
             if C.reduce_atomic() != 0:
                 raise RuntimeError("Conv3x3 statistics need reduction mode 0 (partial rows)")
             nrows = C.conv_fwd_stat_rows(N, H, W, cin, cout, 3, tile, splits)
-            if splits == 1:
-                tile, nrows = _stats_cfg(tile, nrows)
             rows = torch.empty(max(nrows, 400 if splits > 1 else 1), 2, cout, device=x.device)
         T = C.conv_fwd(xbase, bind.wcl.data_ptr(), y.data_ptr(), 0 if rows is None else rows.data_ptr(),
                        0 if slab is None else slab.data_ptr(), N, H, W, cin, cout, 3, tile, splits, s)
@@ -480,22 +363,15 @@ class Conv3x3(torch.autograd.Function):
             dx = torch.empty((N, cin, H, W), dtype=BF16, device=dy.device, memory_format=torch.channels_last)
             dt, ds = _plan_3x3(M, cin, 9 * cout)
             slab = torch.empty(ds * M * cin, device=dy.device) if ds > 1 else None
-            bst = _bn_reduce_begin(C, ctx.bn_link, M, cin, (M + 127) // 128) if ds == 1 else None
-            try:
-                T = C.conv_fwd(dybase, wt.data_ptr(), dx.data_ptr(), 0, 0 if slab is None else slab.data_ptr(), N, H,
-                               W, cout, cin, 3, dt, ds, s)
-            finally:
-                if bst is not None:
-                    _bn_disarm(C)
-            if bst is not None:
-                _bn_reduce_end(C, ctx.bn_link, bst, T, s)
+            C.conv_fwd(dybase, wt.data_ptr(), dx.data_ptr(), 0, 0 if slab is None else slab.data_ptr(), N, H, W,
+                       cout, cin, 3, dt, ds, s)
         tile, splits = _wgrad_plan_3x3(cout, K, M)
         ws = torch.empty(splits * cout * K, device=dy.device)
         C.conv_wgrad(dybase, ctx.xbase, ws.data_ptr(), N, H, W, cin, cout, 3, splits, K, tile, 0, s)
         C.slab_reduce_add_oihw(ws.data_ptr(), bind.g32.data_ptr(), splits, cout, 9, cin, cin, s)
         bind.ready()
         del keep_dy
-        return dx, None, None, None, None
+        return dx, None, None, None
 
 
 class ShadowConv(torch.autograd.Function):
@@ -569,8 +445,7 @@ class StemConv(torch.autograd.Function):
         if stats is not None:
             if C.reduce_atomic() != 0:
                 raise RuntimeError("StemConv statistics need reduction mode 0 (partial rows)")
-            tile, nrows = _stats_cfg(tile, (N * Ho * Wo + 127) // 128)
-            rows = torch.empty(nrows, 2, cout, device=x.device)
+            rows = torch.empty((N * Ho * Wo + 127) // 128, 2, cout, device=x.device)
         T = C.conv_fwd_ex(S.data_ptr(), w4.data_ptr(), y.data_ptr(), 0 if rows is None else rows.data_ptr(), 0, N, Ho,
                           Wo, Hs, Ws, 16, cout, 4, 4, 1, 0, 0, 0, 0, 0, 0, tile, 1, s)
         if rows is not None:
@@ -624,8 +499,7 @@ class Conv1x1S2(torch.autograd.Function):
         if stats is not None:
             if C.reduce_atomic() != 0:
                 raise RuntimeError("Conv1x1S2 statistics need reduction mode 0 (partial rows)")
-            tile, nrows = _stats_cfg(tile, (N * Ho * Wo + 127) // 128)
-            rows = torch.empty(nrows, 2, cout, device=x.device)
+            rows = torch.empty((N * Ho * Wo + 127) // 128, 2, cout, device=x.device)
         T = C.conv_fwd_ex(x.data_ptr(), bind.w16.data_ptr(), y.data_ptr(), 0 if rows is None else rows.data_ptr(), 0,
                           N, Ho, Wo, H, W, cin, cout, 1, 1, 2, 0, 0, 0, 0, 0, 0, tile, 1, s)
         if rows is not None:
@@ -684,13 +558,12 @@ class Conv3x3S2(torch.autograd.Function):
     zero-stuffed upsampling."""
 
     @staticmethod
-    def forward(ctx, x, weight, bind: ShadowBinding, stats, bn_link=None):
+    def forward(ctx, x, weight, bind: ShadowBinding, stats):
         C = native()
         N, cin, H, W = x.shape
         cout = weight.shape[0]
         Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
         keep, xbase = _padded_base(x, 1)
-        ctx.bn_link = bn_link
         y = torch.empty((N, cout, Ho, Wo), dtype=BF16, device=x.device, memory_format=torch.channels_last)
         tile = 0 if cout % 128 == 0 else 2
         s = _stream()
@@ -698,8 +571,7 @@ class Conv3x3S2(torch.autograd.Function):
         if stats is not None:
             if C.reduce_atomic() != 0:
                 raise RuntimeError("Conv3x3S2 statistics need reduction mode 0 (partial rows)")
-            tile, nrows = _stats_cfg(tile, (N * Ho * Wo + 127) // 128)
-            rows = torch.empty(nrows, 2, cout, device=x.device)
+            rows = torch.empty((N * Ho * Wo + 127) // 128, 2, cout, device=x.device)
         T = C.conv_fwd_ex(xbase, bind.wcl.data_ptr(), y.data_ptr(), 0 if rows is None else rows.data_ptr(), 0, N, Ho,
                           Wo, H + 2, W + 2, cin, cout, 3, 3, 2, 0, 0, 0, 0, 0, 0, tile, 1, s)
         if rows is not None:
@@ -727,23 +599,13 @@ class Conv3x3S2(torch.autograd.Function):
             dx = torch.empty((N, cin, H, W), dtype=BF16, device=dy.device, memory_format=torch.channels_last)
             interior = dybase + (Wq + 1) * cout * 2  # dy[0][0]: tap t of phase pixel q reads dy[q + t]
             tile = 0 if cin % 128 == 0 else 2
-            tp = (N * Ho * Wo + 127) // 128  # M tiles (partial BN rows) per phase conv
-            bst = _bn_reduce_begin(C, ctx.bn_link, N * H * W, cin, 4 * tp)
-            off = T = 0
-            try:
-                for rh in (0, 1):
-                    for rw in (0, 1):
-                        kh, kw = 1 + rh, 1 + rw
-                        if bst is not None:  # each phase conv writes its own block of rows
-                            C.set_conv_bn_reduce(*[t.data_ptr() for t in bst[1][:4]], bst[0][T:].data_ptr())
-                        T += C.conv_fwd_ex(interior, ph[off * cin * cout:].data_ptr(), dx.data_ptr(), 0, 0, N, Ho,
-                                           Wo, Hq, Wq, cout, cin, kh, kw, 1, 2, rh, rw, W, H * W, 0, tile, 1, s)
-                        off += kh * kw
-            finally:
-                if bst is not None:
-                    _bn_disarm(C)
-            if bst is not None:
-                _bn_reduce_end(C, ctx.bn_link, bst, T, s)
+            off = 0
+            for rh in (0, 1):
+                for rw in (0, 1):
+                    kh, kw = 1 + rh, 1 + rw
+                    C.conv_fwd_ex(interior, ph[off * cin * cout:].data_ptr(), dx.data_ptr(), 0, 0, N, Ho, Wo, Hq, Wq,
+                                  cout, cin, kh, kw, 1, 2, rh, rw, W, H * W, 0, tile, 1, s)
+                    off += kh * kw
         K = 9 * cin
         tile_w, splits = _wgrad_plan_3x3(cout, K, N * Ho * Wo)
         ws = torch.empty(splits * cout * K, device=dy.device)
@@ -752,4 +614,4 @@ class Conv3x3S2(torch.autograd.Function):
         C.slab_reduce_add_oihw(ws.data_ptr(), bind.g32.data_ptr(), splits, cout, 9, cin, cin, s)
         bind.ready()
         del keep_dy
-        return dx, None, None, None, None
+        return dx, None, None, None

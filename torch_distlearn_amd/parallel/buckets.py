@@ -87,8 +87,11 @@ class GradBucketer:
             self.need[b] += 1
         self.cuda = flat.data.is_cuda
         # communication profile (utils/profiling.py): a list while enabled; eager
-        # steps only -- nothing is recorded while a hipGraph is being captured
+        # steps, or -- profile_in_capture -- a hipGraph capture, whose event-record
+        # nodes re-record the same events at every replay
+        # (DataParallelTrainer.comm_profile(replay=True))
         self.profile = None
+        self.profile_in_capture = False
         self._rec = None
         self.stream = stream if stream is not None else (
             torch.cuda.Stream(device=flat.device, priority=-1) if self.cuda else None)
@@ -116,7 +119,8 @@ class GradBucketer:
 
     # ---------------------------------------------------------------- launch
     def _profiling(self) -> bool:
-        return self.profile is not None and self.cuda and not torch.cuda.is_current_stream_capturing()
+        return (self.profile is not None and self.cuda
+                and (self.profile_in_capture or not torch.cuda.is_current_stream_capturing()))
 
     def _event(self, stream):
         ev = torch.cuda.Event(enable_timing=True)
