@@ -395,13 +395,14 @@ def test_bwd_reduce_head_fused(C):
     assert int(res[1][5][0]) == 1 and float(res[1][4]) == 1.0
 
 
-@pytest.mark.parametrize("atomic", ["2", "0"])
-def test_executor_matches_torch_model(C, atomic, monkeypatch):
+@pytest.mark.parametrize("atomic,B", [("2", 16), ("0", 16), ("2", 4), ("0", 4)])
+def test_executor_matches_torch_model(C, atomic, B, monkeypatch):
     """Whole-model check: HIP executor loss + every gradient vs an fp32 PyTorch
     reference of the same parameters; the error must be within 2x of what
     PyTorch's own bf16 path shows against the same fp32 reference.  Both
     reduction modes (2 = striped atomic BN rows + slab weight gradients;
-    0 = deterministic partial rows)."""
+    0 = deterministic partial rows); batch 16 and 4 run the batch-aware plans
+    (64x64 tiles, up to 16 K-splits: cifar_hip._fwd_plan)."""
     monkeypatch.setenv("DISTLEARN_REDUCE_ATOMIC", atomic)
     from torch_distlearn_amd import FlatParams
     from torch_distlearn_amd.models import CifarConvNet
@@ -409,8 +410,8 @@ def test_executor_matches_torch_model(C, atomic, monkeypatch):
 
     dev = torch.device("cuda")
     torch.manual_seed(0)
-    x = torch.randn(16, 32, 32, 3, device=dev).to(torch.bfloat16)
-    y = torch.randint(0, 10, (16,), device=dev)
+    x = torch.randn(B, 32, 32, 3, device=dev).to(torch.bfloat16)
+    y = torch.randint(0, 10, (B,), device=dev)
     refs = {}
     for dt in (torch.float32, torch.bfloat16):
         m = CifarConvNet(seed=3).to(dev)
@@ -421,7 +422,8 @@ def test_executor_matches_torch_model(C, atomic, monkeypatch):
     rbf, Lbf = refs[torch.bfloat16]
     mdl = CifarConvNet(seed=3).to(dev)
     flat = FlatParams(mdl, grads=True, shadow_bf16=True)
-    ex = CifarHIPExecutor(mdl, flat, max_batch=16)
+    ex = CifarHIPExecutor(mdl, flat, max_batch=B)
+    assert any(p is not None and p[0] == 1 and p[1] > 1 for p in ex.fwd_plan + ex.dgrad_plan)
     flat.grad.zero_()
     loss = ex.forward_backward(x.contiguous(), y)
     torch.cuda.synchronize()

@@ -299,6 +299,34 @@ def test_comm_profile_is_side_effect_free(dev, monkeypatch):
     assert torch.equal(outs[0][0], outs[1][0])
 
 
+def test_comm_profile_from_graph_replays(dev, monkeypatch):
+    """comm_profile(replay=True) reads the bucket events from event-record
+    nodes of a captured one-step graph after each replay (the timed
+    schedule): labelled as such, side-effect free like the eager profile, and
+    within noise of the eager calibration (same buckets, same bytes, comm time
+    within 3x -- a world-1 RCCL all-reduce is a few microseconds either way)."""
+    monkeypatch.setenv("DISTLEARN_RCCL_WORLD1", "1")
+    outs = []
+    for prof in (False, True):
+        tr = _trainer(dev, "hip", True, 29706)
+        ld = _loader(dev, batch=16)
+        tr.run(ld, 3)
+        if prof:
+            ev = tr.comm_profile(ld, steps=4)
+            rp = tr.comm_profile(ld, steps=4, replay=True)
+            assert "replay_error" not in ev
+            assert rp["source"].startswith("graph replays"), rp
+            assert rp["steps"] == 4 and rp["buckets"] == ev["buckets"] == len(tr.bucketer.ranges)
+            assert rp["bytes_per_step"] == ev["bytes_per_step"] == tr.flat.total * 4
+            assert rp["comm_ms"] > 0 and 0.0 <= rp["overlap_fraction"] <= 1.0
+            assert ev["comm_ms"] / 3 <= rp["comm_ms"] <= 3 * ev["comm_ms"], (ev, rp)
+        tr.run(ld, 5)
+        torch.cuda.synchronize()
+        outs.append((tr.flat.data.clone(), int(ld.ctr[0]), int(tr.sgd.stepsPerNode.sum())))
+    assert outs[0][1:] == outs[1][1:]
+    assert torch.equal(outs[0][0], outs[1][0])
+
+
 @pytest.mark.parametrize("mode", ["2"])
 def test_atomic_modes_train_and_graph_tracks_eager(dev, monkeypatch, mode):
     """Reduction mode 2 (fp32 atomics: not bitwise reproducible run to

@@ -47,8 +47,20 @@ SPAD = KSIZE // 2  # spatial zero border of every convolution input (written onc
 _FWD_TILES = {0: (128, 128), 1: (64, 64), 2: (128, 64)}
 
 
-def _fwd_plan(M: int, N: int, K: int):
-    """(tile, splits) for a forward/dgrad implicit GEMM: the biggest tile the
+def _fwd_plan(M: int, N: int, K: int, batch_aware: bool = False):
+    """(tile, splits) for a forward/dgrad implicit GEMM.
+
+    ``batch_aware`` (the CIFAR executor's 5x5 layers): a layer that splits K,
+    or has <= 1024 output rows (batch <= 4 at 16x16), is latency-bound -- a
+    few microseconds of DMA-ring fill per workgroup, whatever the work -- so it
+    takes 64x64 tiles when M <= 1024 (128x64 otherwise) and doubles the splits
+    while the grid is under 256 workgroups, each split keeps >= 6 K-steps of
+    64 and splits <= 16.  Measured per layer at batch 4 / 32 / 128
+    (scripts/sweep_small_batch.py, profiles/r6_sweep_small_batch.txt): batch 4
+    dgrad3 15.9 -> 10.9 us, fwd4 16.4 -> 11.9 us; batch 32 fwd3 18.7 -> 16.5 us;
+    every batch-128 plan unchanged.
+
+    Otherwise the batch-128 rule: the biggest tile the
     channel count allows, then split-K until the grid covers the 256 CUs
     (keeping >= 8 K-steps of 64 per split).  Split-K layers run on 128x64
     tiles with half the splits (half the fp32 slab bytes written and combined,
@@ -56,6 +68,20 @@ def _fwd_plan(M: int, N: int, K: int):
     0.3347 ms/step, profiles/r3_split128x64_ab.txt), and a 128x128 layer whose
     128x64 tiles already fill the chip takes no split at all (no slab round
     trip, no combine: fwd3 28.5 -> 24.7 us)."""
+    tile, splits = _fwd_plan_b128(M, N, K)
+    if not batch_aware or (splits == 1 and M > 1024):
+        return tile, splits
+    tile = 1 if M <= 1024 else 2
+    bm, bn = _FWD_TILES[tile]
+    tiles = ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
+    ksteps = (K + 63) // 64
+    splits = 1
+    while tiles * splits < 256 and splits < 16 and ksteps // (splits * 2) >= 6:
+        splits *= 2
+    return tile, splits
+
+
+def _fwd_plan_b128(M: int, N: int, K: int):
     tile = 0 if N % 128 == 0 else 2
     bm, bn = _FWD_TILES[tile]
     tiles = ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
@@ -246,7 +272,7 @@ class CifarHIPExecutor:
             h, cin, cout = self.hs[i], self.cins[i], self.couts[i]
             M = B * h * h
             K = KSIZE * KSIZE * cin
-            tile, splits = _fwd_plan(M, cout, K)
+            tile, splits = _fwd_plan(M, cout, K, batch_aware=True)
             self.fwd_plan.append((tile, splits))
             if splits > 1:
                 slab_elems = max(slab_elems, splits * M * cout)
@@ -274,7 +300,7 @@ class CifarHIPExecutor:
                 wslab_elems = max(wslab_elems, splits_w * cout * K)
             self.wslab_l.append(None if direct else torch.empty(splits_w * cout * K, device=d))
             if i > 0:
-                dt, ds = _fwd_plan(M, cin, KSIZE * KSIZE * cout)
+                dt, ds = _fwd_plan(M, cin, KSIZE * KSIZE * cout, batch_aware=True)
                 self.dgrad_plan[i] = (dt, ds)
                 if ds > 1:
                     slab_elems = max(slab_elems, ds * M * cin)

@@ -123,7 +123,9 @@ class GradBucketer:
                 and (self.profile_in_capture or not torch.cuda.is_current_stream_capturing()))
 
     def _event(self, stream):
-        ev = torch.cuda.Event(enable_timing=True)
+        # external: inside a capture this is an event-RECORD node (re-timestamped at
+        # every replay), not the internal fork/join dependency a plain record becomes
+        ev = torch.cuda.Event(enable_timing=True, external=self.profile_in_capture)
         ev.record(stream)
         return ev
 
