@@ -67,7 +67,8 @@ def parse():
     ap.add_argument("--overlap", type=int, default=1, help="bucketed all-reduce overlapped with backward")
     ap.add_argument("--grad-comm-dtype", default=os.environ.get("DISTLEARN_GRAD_COMM_DTYPE", "fp32"),
                     choices=["fp32", "bf16"],
-                    help="gradient all-reduce wire dtype (bf16: half the xGMI bytes, count in an fp32 side slot)")
+                    help="gradient all-reduce wire dtype (bf16: half the xGMI bytes, count in an fp32 side slot); "
+                         "with --algo async: the AsyncEA delta push")
     ap.add_argument("--nworld-path", type=int, default=0,
                     help="1 = run the MULTI-NODE step configuration on one GPU (diagnostic, not the headline): the "
                          "bucket all-reduces go through RCCL at world 1 (DISTLEARN_RCCL_WORLD1=1), so the trainer "
@@ -258,7 +259,8 @@ def main():
         from torch_distlearn_amd import AsyncEA, FlatParams
 
         flat = FlatParams(model, grads=False, shadow_bf16=not cpu)
-        server = AsyncEA(tree, None, None, None, None, None, world - 1, 0, a.tau, a.alpha)
+        server = AsyncEA(tree, None, None, None, None, None, world - 1, 0, a.tau, a.alpha,
+                         delta_wire=a.grad_comm_dtype)
         server.initServer(flat)
         while server.syncServer(flat):
             pass
@@ -266,7 +268,7 @@ def main():
         tr = DataParallelTrainer(model, tree, lr=a.lr, algo=a.algo, tau=a.tau, alpha=a.alpha, backend=backend,
                                  compute_dtype=cdt, bucket_bytes=int(a.bucket_mb * (1 << 20)), overlap=bool(a.overlap),
                                  graph=bool(a.graph) and not cpu, max_batch=batch,
-                                 grad_comm_dtype=a.grad_comm_dtype if a.algo == "sgd" else "fp32")
+                                 grad_comm_dtype=a.grad_comm_dtype if a.algo in ("sgd", "async") else "fp32")
         tr.synchronize_parameters()
         if a.model == "cifar10":
             # synthetic CIFAR-10-shaped uint8 dataset resident in HBM (this rank's
@@ -391,6 +393,7 @@ def main():
         "dgrad_stages": getattr(ex, "dgrad_stages", None),
         # the wire dtype actually used (world 1: no collective, fp32)
         "grad_comm_dtype": getattr(tr, "grad_comm_dtype", "fp32") if not is_server else "fp32",
+        "delta_wire": a.grad_comm_dtype if a.algo == "async" else None,
         # world > 1: the overlap policy measured on this machine during warm-up
         # (engine.py select_policy: both candidates' ms per step, max over ranks)
         "policy": getattr(tr, "policy", None) if not is_server else None,
@@ -428,7 +431,7 @@ def main():
             "final_loss": round(lval, 4),
         }
         if comm:
-            out["comm"] = {**comm, "method": f"rank-0 HIP events, {comm.get('source', 'eager steps')}, "
+            out["comm"] = {**comm, "method": f"rank 0, {comm.get('source', 'eager steps')}, "
                                              "6 calibration steps outside the timed region"}
         print(json.dumps(out), flush=True)
     tree.comm.barrier()

@@ -18,9 +18,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("lr"), py::arg("momentum"), py::arg("wd"), py::arg("n"), py::arg("stream"));
   m.def("scale_by_count", &scale_by_count);
   m.def("elastic_step", &elastic_step);
+  m.def("elastic_step_wire16", &elastic_step_wire16);
   m.def("add_inplace", &add_inplace);
   m.def("fill_f32", &fill_f32);
   m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("stamp_time", &stamp_time);
+  m.def("wall_clock_khz", &wall_clock_khz);
   m.def("cast_bf16_f32", &cast_bf16_f32);
   m.def("sgd_update_g16", &sgd_update_g16);
   m.def("sgd_update_slabs", &sgd_update_slabs);

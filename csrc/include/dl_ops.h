@@ -16,6 +16,10 @@ void elastic_step(uintptr_t p, uintptr_t c, uintptr_t pending, uintptr_t out, ui
                   uintptr_t stream);
 void add_inplace(uintptr_t y, uintptr_t x, int64_t n, uintptr_t stream);
 void fill_f32(uintptr_t x, float v, int64_t n, int64_t slot_index, float slot_value, uintptr_t stream);
+void elastic_step_wire16(uintptr_t p, uintptr_t c, uintptr_t out, uintptr_t out16, uintptr_t p16, float alpha,
+                         int64_t n, uintptr_t stream);
+void stamp_time(uintptr_t slot, uintptr_t stream);
+int wall_clock_khz();
 void cast_f32_bf16(uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream);
 void cast_bf16_f32(uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream);
 // the next streaming conv_fwd launch also runs the SGD of flat elements [lo, hi)

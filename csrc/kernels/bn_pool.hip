@@ -830,7 +830,8 @@ int combine_bwd_reduce(uintptr_t slab, int splits, uintptr_t dP, uintptr_t y, ui
     case 2: combine_bwd_reduce_kernel<2><<<nb, 256, 0, s>>>(S, D, Y, K, P, B, H, W, C, rpb); break;
     case 4: combine_bwd_reduce_kernel<4><<<nb, 256, 0, s>>>(S, D, Y, K, P, B, H, W, C, rpb); break;
     case 8: combine_bwd_reduce_kernel<8><<<nb, 256, 0, s>>>(S, D, Y, K, P, B, H, W, C, rpb); break;
-    default: throw std::runtime_error("combine_bwd_reduce: splits must be 2, 4 or 8");
+    case 16: combine_bwd_reduce_kernel<16><<<nb, 256, 0, s>>>(S, D, Y, K, P, B, H, W, C, rpb); break;
+    default: throw std::runtime_error("combine_bwd_reduce: splits must be 2, 4, 8 or 16");
   }
   DL_HIP_CHECK(hipGetLastError());
   return nb;

@@ -136,6 +136,35 @@ __global__ void __launch_bounds__(256) elastic_kernel(float* __restrict__ p, flo
   }
 }
 
+// Elastic step for AsyncEA's bf16 delta wire: delta = alpha * (p - c) rounded
+// to bf16 (the wire copy out16), and p moves by the ROUNDED delta, so p + c is
+// conserved exactly as with the fp32 wire; out = the rounded delta in fp32
+// (what the server adds), p16 = the bf16 shadow.  One pass instead of the
+// elastic step + cast + correction + shadow passes.
+__global__ void __launch_bounds__(256) elastic_wire16_kernel(float* __restrict__ p, const float* __restrict__ c,
+                                                             float* __restrict__ out, bf16_t* __restrict__ out16,
+                                                             bf16_t* __restrict__ p16, float alpha, int64_t n4) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pv = reinterpret_cast<float4*>(p)[i];
+    const float4 cv = reinterpret_cast<const float4*>(c)[i];
+    uint2 w;
+    w.x = pack_bf16x2(alpha * (pv.x - cv.x), alpha * (pv.y - cv.y));
+    w.y = pack_bf16x2(alpha * (pv.z - cv.z), alpha * (pv.w - cv.w));
+    const float4 d = make_float4(lo_bf16(w.x), hi_bf16(w.x), lo_bf16(w.y), hi_bf16(w.y));
+    pv.x -= d.x; pv.y -= d.y; pv.z -= d.z; pv.w -= d.w;
+    reinterpret_cast<float4*>(p)[i] = pv;
+    reinterpret_cast<float4*>(out)[i] = d;
+    reinterpret_cast<uint2*>(out16)[i] = w;
+    if (p16) {
+      uint2 packed;
+      packed.x = pack_bf16x2(pv.x, pv.y);
+      packed.y = pack_bf16x2(pv.z, pv.w);
+      reinterpret_cast<uint2*>(p16)[i] = packed;
+    }
+  }
+}
+
 // y += x
 __global__ void __launch_bounds__(256) add_inplace_kernel(float* __restrict__ y, const float* __restrict__ x, int64_t n4) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -184,6 +213,18 @@ __global__ void __launch_bounds__(256) cast_bf16_f32_kernel(const bf16_t* __rest
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride)
     reinterpret_cast<float4*>(y)[i] = load_grad4(x, i);
+}
+
+// Device timestamp (the constant-rate wall clock, hipDeviceAttributeWallClockRate)
+// written by one lane with a vector store.  A captured graph re-runs it at every
+// replay, so bucket timings read after a replay time the replayed schedule
+// (engine.comm_profile(replay=True); HIP refuses external event-record nodes
+// in a capture, scripts/probe_graph_events.py).
+__global__ void __launch_bounds__(64) stamp_kernel(long long* __restrict__ slot) {
+  if (threadIdx.x == 0) {
+    const long long t = wall_clock64();
+    __builtin_nontemporal_store(t, slot);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -363,6 +404,16 @@ void elastic_step(uintptr_t p, uintptr_t c, uintptr_t pending, uintptr_t out, ui
   DL_HIP_CHECK(hipGetLastError());
 }
 
+void elastic_step_wire16(uintptr_t p, uintptr_t c, uintptr_t out, uintptr_t out16, uintptr_t p16, float alpha,
+                         int64_t n, uintptr_t stream) {
+  check_vec4(n, "elastic_step_wire16");
+  const int64_t n4 = n / 4;
+  if (n4 == 0) return;
+  elastic_wire16_kernel<<<stream_grid(n4), 256, 0, as_stream(stream)>>>((float*)p, (const float*)c, (float*)out,
+                                                                         (bf16_t*)out16, (bf16_t*)p16, alpha, n4);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
 void add_inplace(uintptr_t y, uintptr_t x, int64_t n, uintptr_t stream) {
   check_vec4(n, "add_inplace");
   const int64_t n4 = n / 4;
@@ -385,6 +436,18 @@ void cast_f32_bf16(uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream) {
   if (n4 == 0) return;
   cast_f32_bf16_kernel<<<stream_grid(n4), 256, 0, as_stream(stream)>>>((const float*)x, (bf16_t*)y, n4);
   DL_HIP_CHECK(hipGetLastError());
+}
+
+void stamp_time(uintptr_t slot, uintptr_t stream) {
+  stamp_kernel<<<1, 64, 0, as_stream(stream)>>>((long long*)slot);
+  DL_HIP_CHECK(hipGetLastError());
+}
+
+int wall_clock_khz() {
+  int dev = 0, khz = 0;
+  DL_HIP_CHECK(hipGetDevice(&dev));
+  DL_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+  return khz;
 }
 
 }  // namespace dl

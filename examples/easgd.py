@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--maxSteps", type=int, default=0)
     ap.add_argument("--communicationTime", type=int, default=10, help="tau")
     ap.add_argument("--alpha", type=float, default=0.2)
+    ap.add_argument("--deltaWire", default="fp32", choices=["fp32", "bf16"],
+                    help="dtype of the client's delta push (bf16: half the bytes; every role must agree)")
     ap.add_argument("--testTime", type=int, default=100)
     ap.add_argument("--save", default="log")
     ap.add_argument("--resultsRoot", default="Results")
@@ -118,7 +120,8 @@ def run(opt):
 
     torch.manual_seed(0)
     model = (CifarConvNet(seed=0) if opt.dataset == "cifar10" else MnistConvNet(seed=0)).to(dev)
-    ea = AsyncEA(tree, None, None, None, None, None, N, rank, opt.communicationTime, opt.alpha)
+    ea = AsyncEA(tree, None, None, None, None, None, N, rank, opt.communicationTime, opt.alpha,
+                 delta_wire=opt.deltaWire)
     cd = torch.bfloat16 if dev.type == "cuda" else torch.float32
     hip = opt.backend == "hip" or (opt.backend == "auto" and dev.type == "cuda" and opt.dataset == "cifar10")
     if hip and (dev.type != "cuda" or opt.dataset != "cifar10"):

@@ -15,7 +15,10 @@ Modelled (no second GPU here): the xGMI transfer of the 17.3 MB payload each
 way over the single link between the server and that client.
 
 The server handles one client at a time; its per-sync service time is
-  T_s = ctrl + 2 * max(p2p, bytes / link_bw) + apply
+  T_s = ctrl + max(p2p, bytes / link_bw) + max(p2p_push, push_bytes / link_bw) + apply
+(the center pull is fp32; the delta push is fp32 or, with AsyncEA
+delta_wire="bf16", half the bytes -- the client then rounds its delta and
+moves by the rounded one, the server casts it back: both measured here)
 (the payload stream serialises the pull and the push; the host loop moves on
 to the next ENTER while the GPU still applies the delta, so apply only counts
 when the GPU is the bottleneck).  A client syncs every tau steps; alone it
@@ -85,7 +88,7 @@ def main():
         p.join(timeout=60)
 
     os.environ["DISTLEARN_RCCL_WORLD1"] = "1"
-    from torch_distlearn_amd.ops.flat import add_, cast_, elastic_step_
+    from torch_distlearn_amd.ops.flat import add_, cast_, elastic_step_, elastic_step_wire16_
     from torch_distlearn_amd.parallel.comm import RcclCommunicator
 
     dev = torch.device("cuda", 0)
@@ -95,6 +98,8 @@ def main():
     params = torch.randn(n, device=dev)
     delta = torch.empty(n, device=dev)
     recv = torch.empty(n, device=dev)
+    d16 = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    recv16 = torch.empty(n, device=dev, dtype=torch.bfloat16)
     shadow = torch.empty(n, device=dev, dtype=torch.bfloat16)
     pstream = torch.cuda.Stream(device=dev)
 
@@ -118,36 +123,61 @@ def main():
                 comm.recv(recv, 0, stream=pstream)
         torch.cuda.current_stream().wait_stream(pstream)
 
+    def p2p16():  # the bf16 delta push
+        pstream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(pstream):
+            with comm.group():
+                comm.send(d16, 0, stream=pstream)
+                comm.recv(recv16, 0, stream=pstream)
+        torch.cuda.current_stream().wait_stream(pstream)
+
     def apply():
         add_(center, recv)
         params.copy_(center)
         cast_(shadow, params)
 
+    def apply16():  # serverGetUpdateDiff with the bf16 wire (async_ea.syncServer)
+        cast_(recv, recv16)
+        apply()
+
     def elastic():
         elastic_step_(params, center, delta, 0.2, shadow=shadow)
 
+    def elastic16():  # async_ea.syncClient with the bf16 wire: one fused kernel
+        elastic_step_wire16_(params, center, delta, d16, 0.2, shadow=shadow)
+
     p2p_us = timed(p2p, a.reps)
+    p2p16_us = timed(p2p16, a.reps)
     apply_us = timed(apply, a.reps)
+    apply16_us = timed(apply16, a.reps)
     elastic_us = timed(elastic, a.reps)
+    elastic16_us = timed(elastic16, a.reps)
     comm.close()
 
     nbytes = n * 4
     t_step_us = a.step_ms * 1e3
     rows = []
-    for bw in a.link_GBps:
-        xfer = nbytes / (bw * 1e9) * 1e6
-        t_s = ctrl_us + 2 * max(p2p_us, xfer) + apply_us
-        t_c = a.tau * t_step_us + t_s + elastic_us
-        rho = a.clients * t_s / t_c
-        # clients alone: k * tau * B / T_c; server-bound: tau * B / T_s
-        ips_free = a.clients * a.tau * a.batch / (t_c * 1e-6)
-        ips_cap = a.tau * a.batch / (t_s * 1e-6)
-        rows.append({"link_GBps": bw, "xfer_us_each_way": round(xfer, 1), "server_us_per_sync": round(t_s, 1),
-                     "client_cycle_us": round(t_c, 1), "server_utilisation": round(rho, 3),
-                     "node_img_per_s": round(min(ips_free, ips_cap), 0), "bound": "server" if rho >= 1 else "clients",
-                     "clients_for_saturation": round(t_c / t_s, 2)})
+    for wire in ("fp32", "bf16"):
+        push_bytes, push_us = (nbytes, p2p_us) if wire == "fp32" else (nbytes // 2, p2p16_us)
+        app_us, el_us = (apply_us, elastic_us) if wire == "fp32" else (apply16_us, elastic16_us)
+        for bw in a.link_GBps:
+            xfer = nbytes / (bw * 1e9) * 1e6
+            xpush = push_bytes / (bw * 1e9) * 1e6
+            t_s = ctrl_us + max(p2p_us, xfer) + max(push_us, xpush) + app_us
+            t_c = a.tau * t_step_us + t_s + el_us
+            rho = a.clients * t_s / t_c
+            # clients alone: k * tau * B / T_c; server-bound: tau * B / T_s
+            ips_free = a.clients * a.tau * a.batch / (t_c * 1e-6)
+            ips_cap = a.tau * a.batch / (t_s * 1e-6)
+            rows.append({"delta_wire": wire, "link_GBps": bw, "xfer_us_pull": round(xfer, 1),
+                         "xfer_us_push": round(xpush, 1), "server_us_per_sync": round(t_s, 1),
+                         "client_cycle_us": round(t_c, 1), "server_utilisation": round(rho, 3),
+                         "node_img_per_s": round(min(ips_free, ips_cap), 0),
+                         "bound": "server" if rho >= 1 else "clients", "clients_for_saturation": round(t_c / t_s, 2)})
     out = {"measured_world1": {"ctrl_roundtrip_us": round(ctrl_us, 1), "p2p_self_us": round(p2p_us, 1),
-                               "server_apply_us": round(apply_us, 1), "client_elastic_us": round(elastic_us, 1),
+                               "p2p_self_bf16_us": round(p2p16_us, 1), "server_apply_us": round(apply_us, 1),
+                               "server_apply_bf16_us": round(apply16_us, 1), "client_elastic_us": round(elastic_us, 1),
+                               "client_elastic_bf16_us": round(elastic16_us, 1),
                                "payload_MB": round(nbytes / 1e6, 2)},
            "tau": a.tau, "clients": a.clients, "batch": a.batch, "client_step_ms": a.step_ms, "model": rows}
     txt = json.dumps(out, indent=1)

@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out; export TMPDIR=/tmp
 S=scripts/gpu_step.sh
-$S 400 gpurun_out/plans_tests.log python -u -m pytest tests/kernels/test_convnet_gpu.py tests/kernels/test_engine_gpu.py -m gpu -x -v --timeout 200 --timeout-method thread -p no:cacheprovider -k "matches_torch_model or comm_profile or in_launch or fused_combine or dgrad_bn_reduce" || exit 1
+$S 400 gpurun_out/plans_tests.log python -u -m pytest tests/kernels/test_convnet_gpu.py tests/kernels/test_engine_gpu.py -m gpu -x -v --timeout 200 --timeout-method thread -p no:cacheprovider -k "matches_torch_model or comm_profile or in_launch or fused_combine or dgrad_bn_reduce or device_loader or resume or unrolled or graph" || exit 1
 for B in 128 32 4; do
   $S 200 gpurun_out/plans_b$B.log python bench.py --batch $B || exit 1
 done

@@ -646,7 +646,7 @@ def test_prep_zero_ranges(C):
     assert all(not b.any() for b in bufs) and torch.equal(keep, ref)
 
 
-@pytest.mark.parametrize("B,atomic", [(128, "0"), (64, "0"), (128, "2")])
+@pytest.mark.parametrize("B,atomic", [(128, "0"), (64, "0"), (128, "2"), (4, "0")])
 def test_executor_fused_combine_bwd_reduce(C, monkeypatch, B, atomic):
     """A split-K dgrad's combine fused into the next BN backward reduce
     (combine_bwd_reduce: one launch writes dP and the reduce's partial rows)
@@ -669,7 +669,9 @@ def test_executor_fused_combine_bwd_reduce(C, monkeypatch, B, atomic):
         flat.grad.fill_(float("nan"))
         ex = CifarHIPExecutor(mdl, flat, max_batch=B)
         assert ex.fuse_combine == (fuse == "1")
-        assert any(p is not None and p[1] in (2, 4, 8) for p in ex.dgrad_plan)  # the fused path is exercised
+        assert any(p is not None and p[1] in (2, 4, 8, 16) for p in ex.dgrad_plan)  # the fused path is exercised
+        if B == 4:
+            assert any(p is not None and p[1] == 16 for p in ex.dgrad_plan)
         ex.forward_backward(x.contiguous(), y)
         torch.cuda.synchronize()
         grads.append(torch.cat([v.flatten() for v in flat.views_of(flat.grad)]))

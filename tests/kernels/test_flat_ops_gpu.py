@@ -70,6 +70,30 @@ def test_elastic_step(dev, n, pending):
 
 
 @pytest.mark.parametrize("n", SIZES)
+def test_elastic_step_wire16(dev, n):
+    """AsyncEA bf16 delta wire kernel vs the fp32 reference: the wire copy is
+    bf16(alpha (p - c)) (round to nearest even, like torch), the fp32 delta is
+    exactly that bf16 value, p moved by exactly it, shadow = bf16(p)."""
+    from torch_distlearn_amd.ops.flat import elastic_step_wire16_
+
+    g0 = torch.Generator(device=dev).manual_seed(11 + n)
+    p = torch.randn(n, device=dev, generator=g0)
+    c = torch.randn(n, device=dev, generator=g0)
+    p0, c0 = p.clone(), c.clone()
+    out = torch.empty(n, device=dev)
+    out16 = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    sh = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    elastic_step_wire16_(p, c, out, out16, 0.2, shadow=sh)
+    torch.cuda.synchronize()
+    d16 = (0.2 * (p0 - c0)).to(torch.bfloat16)
+    assert torch.equal(out16, d16)
+    assert torch.equal(out, d16.float())
+    assert torch.equal(p, p0 - d16.float())
+    assert torch.equal(c, c0)
+    assert torch.equal(sh, p.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("n", SIZES)
 def test_fill_scale_add(dev, n):
     from torch_distlearn_amd.ops.flat import add_, fill_, scale_by_count_
 

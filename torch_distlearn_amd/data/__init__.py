@@ -198,16 +198,19 @@ class Batcher:
 class DeviceLoader:
     """Device-side batching for graph-captured training steps.
 
-    The epoch's sample order (from the same native sampler as
-    :class:`Batcher`) is uploaded ONCE per epoch as an int32 vector in HBM;
-    a step's batch is then selected by a device-resident step counter and
-    gathered + normalised + padded by the native executor's first kernel
+    The sample order (from the same native sampler as :class:`Batcher`) lives
+    in HBM as an int32 ring of TWO epochs; a step's batch is selected by a
+    device-resident step counter -- step s reads ``order[(s*B + b) mod 2n]`` --
+    and gathered + normalised + padded by the native executor's first kernel
     (``prep_step_gather``); a later kernel of the same step advances the
-    counter.  A captured
-    hipGraph therefore replays consecutive batches with no per-step host
-    work and no host->device copies.  :meth:`step_done` keeps the host's
-    count so that a new epoch's order is uploaded (outside the graph, in
-    place) when the current one is used up.
+    counter.  A captured hipGraph therefore replays consecutive batches with
+    no per-step host work and no host->device copies, across an epoch
+    boundary too.  :meth:`step_done` keeps the host's count; when an epoch is
+    used up the host generates the order two epochs ahead into a pinned
+    buffer and uploads it, asynchronously and stream-ordered behind the steps
+    already queued, into the half the finished epoch occupied -- no pageable
+    copy, no host stall inside the training loop (at N=8
+    an epoch is 48 steps, so every timed window used to contain one).
 
     Paths without the native executor call :meth:`getBatch` (eager gather of
     the same batch sequence).
@@ -220,22 +223,42 @@ class DeviceLoader:
                                     ds.num_classes, ds.partition, ds.partitions, kind, seed)
         self.steps_per_epoch = max(1, int(self.sampler.size()) // self.batch)
         n = self.steps_per_epoch * self.batch
-        self.order = torch.empty(n, dtype=torch.int32, device=ds.device)
+        self.order = torch.empty(2 * n, dtype=torch.int32, device=ds.device)  # epochs e, e+1 (halves e % 2)
         self.ctr = torch.zeros(2, dtype=torch.int64, device=ds.device)  # [step, reserved]
         self.labels_out = torch.empty(self.batch, dtype=torch.int64, device=ds.device)
         self._host_steps = 0
         self.epoch = 0
         self._idx = torch.empty(self.batch, dtype=torch.int64)
-        self._fill_epoch()
+        cuda = self.order.is_cuda
+        self._pinned = [torch.empty(n, dtype=torch.int32, pin_memory=cuda) for _ in range(2)]
+        self._upload_ev = [None, None]
+        self._upload(0)
+        self._upload(1)
 
-    def _fill_epoch(self) -> None:
+    def _upload(self, half: int) -> None:
+        """Generate the sampler's next epoch and upload it into ``half`` of the
+        ring (stream-ordered on the current stream)."""
         self.sampler.reset_epoch()
         rows = []
         for _ in range(self.steps_per_epoch):
             _next_indices(self.sampler, self.batch, self._idx)
             rows.append(self._idx.clone())
-        self.order.copy_(torch.cat(rows).to(torch.int32))
-        self.ctr.zero_()
+        n = self.steps_per_epoch * self.batch
+        src = self._pinned[half]
+        ev = self._upload_ev[half]
+        if ev is not None:
+            ev.synchronize()  # this pinned buffer's previous upload (an epoch ago) has run
+        src.copy_(torch.cat(rows))
+        self.order[half * n:(half + 1) * n].copy_(src, non_blocking=True)
+        if self.order.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+            self._upload_ev[half] = ev
+
+    def _next_epoch(self) -> None:
+        # the finished epoch's half takes the epoch after the next one
+        self._upload(self.epoch % 2)
+        self.epoch += 1
         self._host_steps = 0
 
     def numBatches(self) -> int:  # noqa: N802
@@ -253,10 +276,9 @@ class DeviceLoader:
         n = int(nbatches)
         while n >= self.steps_per_epoch - self._host_steps:
             n -= self.steps_per_epoch - self._host_steps
-            self.epoch += 1
-            self._fill_epoch()
+            self._next_epoch()
         self._host_steps += n
-        self.ctr[0] = self._host_steps
+        self.ctr[0] = (self.epoch % 2) * self.steps_per_epoch + self._host_steps
 
     def gather_args(self):
         ds = self.ds
@@ -265,17 +287,17 @@ class DeviceLoader:
                 [float(v) for v in ds.std[:ds.C]])
 
     def step_done(self) -> None:
-        """Host bookkeeping after a step consumed a batch: start a new epoch
-        (new order, counter reset) once this one is used up."""
+        """Host bookkeeping after a step consumed a batch: once an epoch is
+        used up, refill its half of the ring (the device counter runs on into
+        the next half, already uploaded)."""
         self._host_steps += 1
         if self._host_steps >= self.steps_per_epoch:
-            self.epoch += 1
-            self._fill_epoch()
+            self._next_epoch()
 
     def getBatch(self) -> Tuple[torch.Tensor, torch.Tensor]:  # noqa: N802
         """Eager equivalent (the same batch the device path would use):
         (x NHWC normalised, y int64); advances the counter."""
-        k = int(self.ctr[0].item()) % self.steps_per_epoch
+        k = int(self.ctr[0].item()) % (2 * self.steps_per_epoch)
         idx = self.order[k * self.batch:(k + 1) * self.batch].to(torch.int64)
         ds = self.ds
         x = ds.images.index_select(0, idx).float().div_(255.0)

@@ -557,7 +557,7 @@ class CifarHIPExecutor:
                 if self.dgrad_stages != 3:
                     C.set_conv_stages(self.dgrad_stages, 0)
                 fix = self.fix >= 2 and self._fix_ok(B, h, cout, cin, dt, ds)
-                keep = self.fuse_combine and ds in (2, 4, 8) and not fix
+                keep = self.fuse_combine and ds in (2, 4, 8, 16) and not fix
                 bnred = self.dgrad_bnred and ds == 1 and not keep and self._region_dgrad(i, B)
                 prt = self.bwd_rows[i - 1] if self.atomic else self.bwd_part[i - 1]
                 if bnred:
@@ -659,7 +659,7 @@ class CifarHIPExecutor:
         h, cout, cin = self.hs[block], self.couts[block], self.cins[block]
         if self.C.conv_region_ok(self.B, h, h, cout, cin, KSIZE, dt, ds):
             return False
-        keep = self.fuse_combine and ds in (2, 4, 8)
+        keep = self.fuse_combine and ds in (2, 4, 8, 16)
         return not (self.dgrad_bnred and ds == 1 and not keep)
 
     def fuse_slab_reduces(self) -> dict:

@@ -295,6 +295,24 @@ def elastic_step_(p: torch.Tensor, c: torch.Tensor, out: torch.Tensor, alpha: fl
             shadow.copy_(p)
 
 
+def elastic_step_wire16_(p: torch.Tensor, c: torch.Tensor, out: torch.Tensor, out16: torch.Tensor,
+                         alpha: float, shadow: torch.Tensor | None = None) -> None:
+    """AsyncEA bf16 delta wire: out16 = bf16(alpha*(p - c)); out = float(out16);
+    p -= out (the ROUNDED delta: p + c conserved); [shadow = bf16(p)]."""
+    if p.is_cuda and p.numel() % 4 == 0:
+        native().elastic_step_wire16(p.data_ptr(), c.data_ptr(), out.data_ptr(), out16.data_ptr(), _ptr(shadow),
+                                     float(alpha), p.numel(), stream_handle())
+        return
+    with torch.no_grad():
+        torch.sub(p, c, out=out)
+        out.mul_(alpha)
+        out16.copy_(out)
+        out.copy_(out16)
+        p.sub_(out)
+        if shadow is not None:
+            shadow.copy_(p)
+
+
 def cast_(dst: torch.Tensor, src: torch.Tensor) -> None:
     """dst = src between fp32 and bf16 (same length, multiple of 4 on GPU)."""
     if dst.is_cuda and dst.numel() % 4 == 0:

@@ -60,7 +60,7 @@ from typing import Any, Optional
 import torch
 import torch.distributed as dist
 
-from ..ops.flat import HEADER, FlatParams, add_, elastic_step_
+from ..ops.flat import HEADER, FlatParams, add_, cast_, elastic_step_, elastic_step_wire16_
 from ..utils.color_print import printClient, printServer
 from .allreduce_ea import _FlatState
 from .comm import MSG_LEN, CommError, Communicator, comm_timeout
@@ -86,7 +86,7 @@ class AsyncEA:
     def __init__(self, server=None, serverBroadcast=None, client=None, clientBroadcast=None,  # noqa: N803
                  serverTest=None, clientTest=None, numNodes: int = 1, node: int = 0, tau: int = 10,  # noqa: N803
                  alpha: float = 0.2, comm: Optional[Communicator] = None, timeout: Optional[float] = None,
-                 idle_timeout: Optional[float] = None):
+                 idle_timeout: Optional[float] = None, delta_wire: str = "fp32"):
         if comm is None:
             for c in (server, serverBroadcast, client, clientBroadcast, serverTest, clientTest):
                 if isinstance(c, Tree):
@@ -119,6 +119,15 @@ class AsyncEA:
         self.idle_timeout = None if idle_timeout is None else float(idle_timeout)
         self._ps = None        # payload stream (GPU)
         self._done = set()     # clients that said BYE (server)
+        # the delta push on the wire: "fp32", or "bf16" (half the bytes of the
+        # transfer that bounds a server's client count, README "AsyncEA server
+        # throughput"); the client applies the ROUNDED delta to itself, so
+        # p + center is conserved exactly as with the fp32 wire.  Every role of
+        # a job must use the same wire.
+        if delta_wire not in ("fp32", "bf16"):
+            raise ValueError(f"delta_wire must be 'fp32' or 'bf16', not {delta_wire!r}")
+        self.delta_wire = delta_wire
+        self.delta16 = None
 
     # ------------------------------------------------------------- helpers
     def _one_time_init(self, params: Any):  # (:18-29)
@@ -126,6 +135,8 @@ class AsyncEA:
             self.state = _FlatState(params)
             self.center = self.state.flat.data.clone()
             self.delta = self.state.flat.data.clone()
+            if self.delta_wire == "bf16":
+                self.delta16 = torch.zeros_like(self.delta, dtype=torch.bfloat16)
         else:
             self.state.sync_in(params)
 
@@ -202,9 +213,16 @@ class AsyncEA:
         printClient(self.node, "Received center")
         f = self.flat                                            # calculateUpdateDiff (:109-119)
         H = HEADER  # (the header stays out of the elastic math, like AllReduceEA)
-        elastic_step_(f.data[H:], self.center[H:], self.delta[H:], self.alpha,
-                      shadow=None if f.shadow is None else f.shadow[H:])
-        self._send_payload(self.delta, SERVER_RANK)              # clientSendDiff (:122-132)
+        shadow = None if f.shadow is None else f.shadow[H:]
+        if self.delta16 is not None:
+            # bf16 wire: one kernel rounds the delta and moves p by the ROUNDED
+            # delta (`delta` = what the server adds)
+            elastic_step_wire16_(f.data[H:], self.center[H:], self.delta[H:], self.delta16[H:], self.alpha,
+                                 shadow=shadow)
+            self._send_payload(self.delta16, SERVER_RANK)        # clientSendDiff (:122-132)
+        else:
+            elastic_step_(f.data[H:], self.center[H:], self.delta[H:], self.alpha, shadow=shadow)
+            self._send_payload(self.delta, SERVER_RANK)
         self.syncs += 1
         return True
 
@@ -239,7 +257,11 @@ class AsyncEA:
         printServer(f"Current client is #{sender}")
         self._msg(GRANT, sender, TAG_GRANT)
         self._send_payload(self.center, sender)                   # serverSendCenter (:180-196)
-        self._recv_payload(self.delta, sender)                    # serverGetUpdateDiff (:198-228)
+        if self.delta16 is not None:                              # serverGetUpdateDiff (:198-228)
+            self._recv_payload(self.delta16, sender)
+            cast_(self.delta, self.delta16)
+        else:
+            self._recv_payload(self.delta, sender)
         add_(self.center, self.delta)                            # (compute stream, after the delta landed)
         self.flat.data.copy_(self.center)
         self.flat.refresh_shadow()

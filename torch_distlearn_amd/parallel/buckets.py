@@ -61,6 +61,35 @@ def _nullctx():
     return contextlib.nullcontext()
 
 
+class _Stamp:
+    """A device timestamp (native ``stamp_time``: the constant-rate wall clock)
+    with the ``elapsed_time`` interface of a HIP event, read after the work that
+    wrote it has finished."""
+
+    _khz = None
+
+    def __init__(self, buf, i):
+        self.buf, self.i = buf, i
+
+    @classmethod
+    def record(cls, stamps, stream):
+        from .._native import native
+
+        buf, i = stamps
+        if i >= buf.numel():
+            raise RuntimeError("capture profile: out of timestamp slots")
+        stamps[1] = i + 1
+        native().stamp_time(buf.data_ptr() + 8 * i, stream.cuda_stream)
+        return cls(buf, i)
+
+    def elapsed_time(self, end) -> float:
+        if _Stamp._khz is None:
+            from .._native import native
+
+            _Stamp._khz = native().wall_clock_khz()
+        return float(int(end.buf[end.i]) - int(self.buf[self.i])) / _Stamp._khz  # ms
+
+
 class GradBucketer:
     def __init__(self, comm, flat: FlatParams, bucket_bytes: int = 4 << 20, hooks: bool = True,
                  stream: Optional["torch.cuda.Stream"] = None, wire: str = "fp32"):
@@ -123,11 +152,23 @@ class GradBucketer:
                 and (self.profile_in_capture or not torch.cuda.is_current_stream_capturing()))
 
     def _event(self, stream):
-        # external: inside a capture this is an event-RECORD node (re-timestamped at
-        # every replay), not the internal fork/join dependency a plain record becomes
-        ev = torch.cuda.Event(enable_timing=True, external=self.profile_in_capture)
+        if self.profile_in_capture:
+            # inside a capture: a device-timestamp kernel node (re-run at every
+            # replay); a plain event record would become a fork/join edge, and HIP
+            # refuses external event-record nodes (scripts/probe_graph_events.py)
+            return _Stamp.record(self._stamps, stream)
+        ev = torch.cuda.Event(enable_timing=True)
         ev.record(stream)
         return ev
+
+    def start_capture_profile(self, slots: int = 512) -> None:
+        """Profile the next capture with device timestamps (``profile`` := [])."""
+        self.profile, self.profile_in_capture = [], True
+        self._stamps = [torch.zeros(slots, dtype=torch.int64, device="cuda"), 0]
+
+    def stop_capture_profile(self) -> list:
+        recs, self.profile, self.profile_in_capture = self.profile, None, False
+        return recs
 
     def set_early_update(self, fn) -> None:
         """``fn(start, end, grad)`` updates parameters [start, end) from the
