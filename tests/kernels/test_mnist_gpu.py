@@ -61,7 +61,13 @@ def test_mnist_trainer_hip_vs_torch(dev):
         tr = DataParallelTrainer(m, tree, lr=0.05, backend=backend, compute_dtype=torch.float32, graph=graph,
                                  max_batch=4)
         tr.synchronize_parameters()
-        res[backend] = ([float(tr.step(xs[i], ys[i])) for i in range(20)], tr.flat.data.clone())
-    (lh, ph), (lt, pt) = res["hip"], res["torch"]
+        losses = [float(tr.step(xs[i], ys[i])) for i in range(20)]
+        # the public predict (the trainer passes batch_stats to every
+        # executor; the MNIST net has no BatchNorm, so both modes agree)
+        lps = [tr.predict(xs[0], batch_stats=bs) for bs in (False, True)]
+        res[backend] = (losses, tr.flat.data.clone(), lps)
+    (lh, ph, lph), (lt, pt, lpt) = res["hip"], res["torch"]
     assert max(abs(a - b) for a, b in zip(lh, lt)) < 1e-3
     assert float((ph - pt).abs().max()) < 1e-4
+    assert torch.equal(lph[0], lph[1])
+    torch.testing.assert_close(lph[0], lpt[0], rtol=1e-3, atol=1e-3)
