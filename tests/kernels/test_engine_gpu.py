@@ -320,12 +320,55 @@ def test_comm_profile_from_graph_replays(dev, monkeypatch):
             assert rp["steps"] == 4 and rp["buckets"] == ev["buckets"] == len(tr.bucketer.ranges)
             assert rp["bytes_per_step"] == ev["bytes_per_step"] == tr.flat.total * 4
             assert rp["comm_ms"] > 0 and 0.0 <= rp["overlap_fraction"] <= 1.0
-            assert ev["comm_ms"] / 3 <= rp["comm_ms"] <= 3 * ev["comm_ms"], (ev, rp)
+            # the eager calibration also times the host issuing each collective into
+            # an idle comm stream (0.01-0.12 ms measured at world 1), the replay
+            # does not: never more than eager plus noise
+            assert rp["comm_ms"] <= ev["comm_ms"] + 0.02, (ev, rp)
         tr.run(ld, 5)
         torch.cuda.synchronize()
         outs.append((tr.flat.data.clone(), int(ld.ctr[0]), int(tr.sgd.stepsPerNode.sum())))
     assert outs[0][1:] == outs[1][1:]
     assert torch.equal(outs[0][0], outs[1][0])
+
+
+def test_capture_timestamps_match_hip_events(dev):
+    """The timestamp nodes comm_profile(replay=True) uses time a fixed GPU
+    workload like HIP events do: 8 copies of 64 MB between two stamps in a
+    replayed graph vs the same copies between two events, eagerly, within 10 %."""
+    from torch_distlearn_amd.parallel.buckets import _Stamp
+
+    a = torch.empty(16 << 20, device=dev)
+    b = torch.ones(16 << 20, device=dev)
+    stamps = [torch.zeros(4, dtype=torch.int64, device=dev), 0]
+    s = torch.cuda.Stream()
+
+    def work():
+        for _ in range(8):
+            a.copy_(b)
+
+    with torch.cuda.stream(s):
+        work()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        t0 = _Stamp.record(stamps, torch.cuda.current_stream())
+        work()
+        t1 = _Stamp.record(stamps, torch.cuda.current_stream())
+    ev = []
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        work()
+        e1.record()
+        torch.cuda.synchronize()
+        ev.append(e0.elapsed_time(e1))
+    st = []
+    for _ in range(5):
+        g.replay()
+        torch.cuda.synchronize()
+        st.append(t0.elapsed_time(t1))
+    ev_ms, st_ms = sorted(ev)[2], sorted(st)[2]
+    assert ev_ms > 0.05 and abs(st_ms - ev_ms) <= 0.1 * ev_ms, (ev, st)
 
 
 @pytest.mark.parametrize("mode", ["2"])

@@ -365,7 +365,9 @@ class DataParallelTrainer:
             self.prepare(loader, unroll)
         while nsteps > 0:
             # a graph may run into the next epoch (its order is already in the
-            # loader's two-epoch ring) but not past it
+            # loader's two-epoch ring) but not past it.  (Replaying the smallest
+            # graph of the decomposition first measured within noise of largest
+            # first, profiles/r6_replay_order_ab.txt.)
             left = 2 * loader.steps_per_epoch - loader._host_steps
             cap = min(nsteps, left)
             key = None
