@@ -273,6 +273,12 @@ class CifarHIPExecutor:
             M = B * h * h
             K = KSIZE * KSIZE * cin
             tile, splits = _fwd_plan(M, cout, K, batch_aware=True)
+            if tile == 2 and splits == 2 and self._fix_ok(B, h, cin, cout, 2, 4):
+                # combined in-launch, a 2-split forward takes 4 (two rounds of the
+                # 128x64 grid; the reducer's 3 extra slice loads are all in flight):
+                # batch-128 layer-4 forward 22.7 -> 20.9 us, step 0.2946 -> 0.2935 ms
+                # median of 10 interleaved runs (profiles/r6_fwd4_splits_ab.txt)
+                splits = 4
             self.fwd_plan.append((tile, splits))
             if splits > 1:
                 slab_elems = max(slab_elems, splits * M * cout)

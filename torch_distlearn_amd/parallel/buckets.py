@@ -164,7 +164,7 @@ class GradBucketer:
     def start_capture_profile(self, slots: int = 512) -> None:
         """Profile the next capture with device timestamps (``profile`` := [])."""
         self.profile, self.profile_in_capture = [], True
-        self._stamps = [torch.zeros(slots, dtype=torch.int64, device="cuda"), 0]
+        self._stamps = [torch.zeros(slots, dtype=torch.int64, device=self.flat.grad.device), 0]
 
     def stop_capture_profile(self) -> list:
         recs, self.profile, self.profile_in_capture = self.profile, None, False
