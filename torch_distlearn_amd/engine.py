@@ -365,9 +365,10 @@ class DataParallelTrainer:
             self.prepare(loader, unroll)
         while nsteps > 0:
             # a graph may run into the next epoch (its order is already in the
-            # loader's two-epoch ring) but not past it.  (Replaying the smallest
-            # graph of the decomposition first measured within noise of largest
-            # first, profiles/r6_replay_order_ab.txt.)
+            # loader's two-epoch ring) but not past it.  (Replaying a small graph
+            # first -- the device starts before the big graph's submission ends --
+            # measured within noise or slower: the extra graph boundary costs
+            # more, profiles/r6_replay_order_ab.txt.)
             left = 2 * loader.steps_per_epoch - loader._host_steps
             cap = min(nsteps, left)
             key = None
