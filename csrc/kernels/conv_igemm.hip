@@ -816,7 +816,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   // (host-checked); rows of an M tail load a valid pixel and are masked out
   // of the stores and BN statistics.
   const unsigned long long t_start = dbg ? stamp() : 0ull;
-  constexpr int BK = 64, CPR = 8, NW = WM * WN, NT = 64 * NW, PD = STAGES - 1;
+  constexpr int BK = 64, CPR = 8, NW = WM * WN, PD = STAGES - 1;
   static_assert(STAGES >= 2 && STAGES <= 4, "2..4 stages");
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE_BYTES = A_BYTES + B_BYTES;
   constexpr int A_INS = A_BYTES / 1024 / NW, B_INS = B_BYTES / 1024 / NW;  // glds per wave per stage
