@@ -1424,7 +1424,8 @@ constexpr int vmcnt_imm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x70 | 0xF
 template <bool STATS>
 __global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                           bf16_t* __restrict__ y, float* __restrict__ stats,
-                                                          const ConvGeom g, int region_rows, int mt) {
+                                                          const ConvGeom g, int region_rows, int mt,
+                                                          unsigned long long* dbg) {
   // mt consecutive 128-pixel M tiles per workgroup (whole output rows of one
   // image): the weight panel (BN x taps x 16 B = 25.6 KiB for the reference's
   // layer 1) is DMA'd once per workgroup instead of once per tile, the region
@@ -1432,11 +1433,16 @@ __global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restri
   // one after the other from LDS (epilogue scratch after the region).
   constexpr int BM = 128, BN = 64, WM = 4, WN = 2, NW = 8, TM = 32, TN = 32, FM = 2, FN = 2;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const unsigned long long t_start = dbg ? stamp() : 0;  // (set_conv_debug: phase stamps)
   const int taps = g.KS * g.KS;                      // K = taps * 8
   const int nsteps = (taps + 3) / 4;                 // 32-deep k-steps (4 taps each)
   const int rslots = region_rows * g.Wp;             // region pixels (16 B each)
   const int rslots_p = (rslots + 1 + 63) / 64 * 64;  // + >= 1 zero slot, whole DMA pieces
-  const int wslots = BN * taps;                      // weight panel: BN rows x taps 16-B chunks
+  // weight panel: BN rows x taps 16-B chunks.  (Its B-fragment reads put rows
+  // r and r+16 on the same banks; spreading them with 4 empty chunks per 16
+  // rows measured no change -- the k loop is not LDS-bound, 12.96 vs 13.24 us,
+  // profiles/r6_c8_stamps.txt.)
+  const int wslots = BN * taps;
   const int wslots_p = (wslots + 63) / 64 * 64;
   char* sR = smem;
   char* sW = smem + rslots_p * 16;
@@ -1469,6 +1475,8 @@ __global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restri
   for (int b = 0; b < FN; ++b) b_row[b] = wn * TN + 8 * (i >> 2) + 4 * b + (i & 3);
   wait_vmcnt<0>();
   block_sync_lds();
+  const unsigned long long t_dma = dbg ? stamp() : 0;
+  unsigned long long t_mfma = 0;
   const int zero_slot = rslots;  // loaded from an out-of-range offset: zeros
   for (int t_ = 0; t_ < mt; ++t_) {
   const int tm = tg * mt + t_, m0 = tm * BM;
@@ -1499,7 +1507,12 @@ __global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restri
 #pragma unroll
       for (int b = 0; b < FN; ++b) acc[a][b] = mfma16(fb[b], fa[a], acc[a][b]);
   }
+  if (dbg) t_mfma = stamp();
   conv_fwd_epilogue_t<128, BN, STATS, false, WM, WN, FM, FN>(acc, g, y, stats, nullptr, 0, tm, m0, n0, sX);
+  }
+  if (dbg && threadIdx.x == 0) {
+    unsigned long long* d = dbg + (size_t)blockIdx.x * 4;
+    d[0] = t_start; d[1] = t_dma; d[2] = t_mfma; d[3] = stamp();
   }
 }
 
@@ -2454,7 +2467,7 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
         attr = true;
       }
       kern<<<grid, 512, c8_lds, s>>>((const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)stats, g, c8_rows,
-                                     c8_mt);
+                                     c8_mt, g_conv_dbg);
     };
     if (stats) go(conv_fwd_c8_kernel<true>);
     else go(conv_fwd_c8_kernel<false>);
