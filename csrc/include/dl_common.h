@@ -49,6 +49,21 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
 __device__ __forceinline__ float lo_bf16(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float hi_bf16(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
+// First-layer packed weight index of element e of a [Cout][taps][C] weight.
+// cp > 0: channel-padded [Cout][taps][cp].  cp = -KW (square KW x KW kernel,
+// C <= 4): two horizontally adjacent taps per 16-byte chunk,
+// [Cout][KW][ceil(KW/2)][2][4] -- the layout of the pair-packed first-layer
+// forward (conv_fwd_c8_kernel<.., PAIR>); pads are never written.
+__device__ __forceinline__ int64_t pack1_index(int64_t e, int C, int cp) {
+  const int64_t px = e / C;
+  const int c = (int)(e - px * C);
+  if (cp > 0) return px * cp + c;
+  const int kw = -cp, taps = kw * kw, cpr = (kw + 1) >> 1;
+  const int64_t co = px / taps;
+  const int tap = (int)(px - co * taps), kh = tap / kw, kx = tap - kh * kw;
+  return ((co * kw + kh) * cpr + (kx >> 1)) * 8 + (kx & 1) * 4 + c;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -1421,7 +1421,7 @@ constexpr int vmcnt_imm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x70 | 0xF
 // Output: transposed accumulator -> conv_fwd_epilogue_t (16-byte stores, BN
 // statistics per M tile).
 // --------------------------------------------------------------------------
-template <bool STATS>
+template <bool STATS, bool PAIR = false>
 __global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                           bf16_t* __restrict__ y, float* __restrict__ stats,
                                                           const ConvGeom g, int region_rows, int mt,
@@ -1434,10 +1434,18 @@ __global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restri
   constexpr int BM = 128, BN = 64, WM = 4, WN = 2, NW = 8, TM = 32, TN = 32, FM = 2, FN = 2;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const unsigned long long t_start = dbg ? stamp() : 0;  // (set_conv_debug: phase stamps)
-  const int taps = g.KS * g.KS;                      // K = taps * 8
-  const int nsteps = (taps + 3) / 4;                 // 32-deep k-steps (4 taps each)
+  // PAIR: the input has <= 4 real channels and the weights are pair-packed
+  // (pack1_index, cp = -KS): one 16-byte K chunk = channels 0-3 of two
+  // horizontally adjacent taps, read as the first 8 bytes of two adjacent
+  // region pixels -- K = KS * ceil(KS/2) * 8 (120 for 5x5) instead of
+  // KS * KS * 8 (200), 4 k-steps instead of 7 and a 15.4 instead of a 25.6 KiB
+  // weight panel.  (The odd last tap's partner is a zero weight; the pixel it
+  // reads is the next padded row's zero border, or a zero slot.)
+  const int cpr = (g.KS + 1) >> 1;
+  const int taps = PAIR ? g.KS * cpr : g.KS * g.KS;  // K chunks (16 B) per output channel
+  const int nsteps = (taps + 3) / 4;                 // 32-deep k-steps (4 chunks each)
   const int rslots = region_rows * g.Wp;             // region pixels (16 B each)
-  const int rslots_p = (rslots + 1 + 63) / 64 * 64;  // + >= 1 zero slot, whole DMA pieces
+  const int rslots_p = (rslots + 2 + 63) / 64 * 64;  // + >= 2 zero slots, whole DMA pieces
   // weight panel: BN rows x taps 16-B chunks.  (Its B-fragment reads put rows
   // r and r+16 on the same banks; spreading them with 4 empty chunks per 16
   // rows measured no change -- the k loop is not LDS-bound, 12.96 vs 13.24 us,
@@ -1492,13 +1500,21 @@ __global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restri
 #pragma unroll
     for (int b = 0; b < FN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int st = 0; st < nsteps; ++st) {
-    const int t = 4 * st + qg;  // this lane group's tap
-    const int kh = t / g.KS, kw = t - (t / g.KS) * g.KS;
+    const int t = 4 * st + qg;  // this lane group's tap (PAIR: tap pair)
+    const int kh = PAIR ? t / cpr : t / g.KS, kw = PAIR ? 2 * (t - kh * cpr) : t - kh * g.KS;
     const int toff = kh * g.Wp + kw;
     bf16x8 fa[FM], fb[FN];
 #pragma unroll
-    for (int a = 0; a < FM; ++a)
-      fa[a] = *reinterpret_cast<const bf16x8*>(sR + (t < taps ? a_pix[a] + toff : zero_slot) * 16);
+    for (int a = 0; a < FM; ++a) {
+      const int q = t < taps ? a_pix[a] + toff : zero_slot;
+      if constexpr (PAIR) {
+        const uint2 lo = *reinterpret_cast<const uint2*>(sR + q * 16);
+        const uint2 hi = *reinterpret_cast<const uint2*>(sR + (q + 1) * 16);
+        fa[a] = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      } else {
+        fa[a] = *reinterpret_cast<const bf16x8*>(sR + q * 16);
+      }
+    }
 #pragma unroll
     for (int b = 0; b < FN; ++b)
       fb[b] = *reinterpret_cast<const bf16x8*>(sW + (b_row[b] * taps + min(t, taps - 1)) * 16);
@@ -2014,6 +2030,12 @@ __global__ void __launch_bounds__(256) prep_step_kernel(const PrepArgs a) {
   }
   blk -= a.nb_pad;
   if (blk < a.nb_pack) {
+    if (a.w1_cp < 0) {  // pair-packed (pack1_index): scatter the real elements, pads stay zero
+      const int total = a.w1_cout * a.taps * a.w1_c;
+      for (int e = blk * 256 + threadIdx.x; e < total; e += a.nb_pack * 256)
+        a.w1p[pack1_index(e, a.w1_c, a.w1_cp)] = f32_to_bf16(a.w1[e]);
+      return;
+    }
     const int total = a.w1_cout * a.taps * a.w1_cp;
     for (int i = blk * 256 + threadIdx.x; i < total; i += a.nb_pack * 256) {
       const int c = i % a.w1_cp;
@@ -2068,7 +2090,8 @@ static void launch_prep(PrepArgs& a, int64_t P, uintptr_t w1, uintptr_t w1p, int
   a.nt = (int)tw.size();
   if (a.nt > 4 || twt.size() != tw.size() || tcout.size() != tw.size() || tcin.size() != tw.size())
     throw std::runtime_error("prep_step: up to 4 consistent transposes");
-  a.nb_pack = (int)std::min<int64_t>(((int64_t)w1_cout * taps * w1_cp + 255) / 256, 256);
+  if (w1_cp < 0 && (w1_c > 4 || taps != w1_cp * w1_cp)) throw std::runtime_error("prep_step: pair pack needs C <= 4, a square kernel");
+  a.nb_pack = (int)std::min<int64_t>(((int64_t)w1_cout * taps * (w1_cp > 0 ? w1_cp : w1_c) + 255) / 256, 256);
   int total = a.nb_pad + a.nb_pack + a.nb_zero;
   for (int j = 0; j < a.nt; ++j) {
     a.tw[j] = (const bf16_t*)tw[j]; a.twt[j] = (bf16_t*)twt[j];
@@ -2135,6 +2158,7 @@ static SgdJob g_side_sgd{};         // set_conv_side_sgd: side SGD job of the ne
 static uintptr_t g_fwd_addend = 0;  // conv_fwd_add: bf16 [M][Cout] added in the epilogue
 static uintptr_t g_fwd_addend_mask = 0;  // conv_fwd_add: optional uint8 [M][Cout/8] mask bits of the addend
 static int g_fwd_keep_slabs = 0;    // FwdCfg bit 20: leave the split-K slabs (the caller combines them)
+static int g_c8_pair = 0;           // FwdCfg bit 24: pair-packed first-layer weights (conv_fwd_c8_kernel PAIR)
 static int g_red_atomic_host = 0;   // host mirror of g_red_atomic
 static BnRedArgs g_bnred{};         // conv_fwd_bnred: fused BN backward reduce (region dgrad only)
 // conv_fwd_fix: the current conv_fwd call combines its split-K slices in-launch
@@ -2233,6 +2257,7 @@ struct FwdCfg {
   explicit FwdCfg(int& tile) : saved_st(g_fwd_stages), saved_wv(g_fwd_waves) {
     const int st = (tile >> 4) & 15, wv = (tile >> 8) & 15;
     g_fwd_keep_slabs = (tile >> 20) & 1;
+    g_c8_pair = (tile >> 24) & 1;
     tile &= 15;
     if (st && (st < 2 || st > 4)) throw std::runtime_error("conv_fwd: packed stages must be 2..4");
     if (wv && wv != 4 && wv != 8) throw std::runtime_error("conv_fwd: packed waves must be 4 or 8");
@@ -2240,7 +2265,7 @@ struct FwdCfg {
     if (wv) g_fwd_waves = wv;
   }
   ~FwdCfg() {
-    g_fwd_stages = saved_st; g_fwd_waves = saved_wv; g_fwd_keep_slabs = 0;
+    g_fwd_stages = saved_st; g_fwd_waves = saved_wv; g_fwd_keep_slabs = 0; g_c8_pair = 0;
   }
 };
 
@@ -2453,8 +2478,9 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
     }
   }
   const int c8_rows = c8_mt * 128 / std::max(1, W) + KS - 1;
+  const int c8_chunks = g_c8_pair ? KS * ((KS + 1) / 2) : KS * KS;  // weight chunks per output channel
   const size_t c8_lds =
-      (size_t)((c8_rows * g.Wp + 1 + 63) / 64 * 64 + (64 * KS * KS + 63) / 64 * 64) * 16 + 4 * 2 * 64 * 4;
+      (size_t)((c8_rows * g.Wp + 2 + 63) / 64 * 64 + (64 * c8_chunks + 63) / 64 * 64) * 16 + 4 * 2 * 64 * 4;
   // the NHWC BN reduce epilogue and the in-launch split-K combine are on the streaming kernel
   const bool streaming_only = g_fix.on;
   if (!streaming_only && tile == 2 && splits == 1 && g_region && g.pow2 && Cin == 8 && W <= 128 && 128 % W == 0 && (H * W) % 128 == 0 &&
@@ -2469,8 +2495,16 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
       kern<<<grid, 512, c8_lds, s>>>((const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)stats, g, c8_rows,
                                      c8_mt, g_conv_dbg);
     };
-    if (stats) go(conv_fwd_c8_kernel<true>);
-    else go(conv_fwd_c8_kernel<false>);
+    if (g_c8_pair) {
+      if (stats) go(conv_fwd_c8_kernel<true, true>);
+      else go(conv_fwd_c8_kernel<false, true>);
+    } else if (stats) {
+      go(conv_fwd_c8_kernel<true>);
+    } else {
+      go(conv_fwd_c8_kernel<false>);
+    }
+  } else if (g_c8_pair) {
+    throw std::runtime_error("conv_fwd: pair-packed weights need the first-layer kernel (Cin 8, tile 2, no split)");
   } else if (!streaming_only && tile == 0 && region_geom(g, 128, splits, rg)) {
     if (g_region_waves == 4) launch_fwd_region<128, 2, 2>(g, rg, x, w, y, stats, slab, splits, s);
     else launch_fwd_region<128, 2, 4>(g, rg, x, w, y, stats, slab, splits, s);

@@ -271,7 +271,7 @@ void arm_sgd_next_prep(uintptr_t img, uintptr_t order, uintptr_t lab_all, uintpt
                        int Cp, int H, int W, int sp, std::vector<uintptr_t> zp, std::vector<int64_t> zn,
                        uintptr_t w1p, int w1_cp, int64_t pack_off, int64_t pack_len) {
   if (g_next_armed) throw std::runtime_error("arm_sgd_next_prep: already armed (no sgd_update_slabs consumed it)");
-  if (!xp || !w1p || w1_cp < C) throw std::runtime_error("arm_sgd_next_prep: input buffer / packed weights");
+  if (!xp || !w1p || (w1_cp > 0 ? w1_cp < C : C > 4)) throw std::runtime_error("arm_sgd_next_prep: input buffer / packed weights");
   if (pack_off % 4 || pack_len % 4 || pack_off < 0 || pack_len <= 0 || pack_len % C)
     throw std::runtime_error("arm_sgd_next_prep: the first layer's element range must be 16-byte aligned");
   PrepArgs a{};

@@ -151,8 +151,8 @@ struct SgdJob {
   int64_t skip_lo4, skip_hi4;  // updated elsewhere (another launch's side job); empty: -1, -1
   SlabRanges r;
   int nblk;             // side job: workgroups of the host launch that run it (0: none)
-  // the tail's updated weights also go to this channel-padded bf16 copy
-  // ([Cout][taps][pack_cp], pads untouched): the first conv layer's operand,
+  // the tail's updated weights also go to this packed bf16 copy (pack1_index:
+  // channel-padded, or pair-packed for cp < 0; pads untouched): the first conv layer's operand,
   // when the launch prepares the next step (flat_ops.hip, prep_dev.h)
   bf16_t* tail_pack;
   int tail_pack_cp;
@@ -176,7 +176,7 @@ __device__ __forceinline__ void pack_range4(const SgdJob& j, int64_t i, const fl
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int64_t e = e0 + k;
-    j.tail_pack[(e / j.pack_c) * j.tail_pack_cp + e % j.pack_c] = f32_to_bf16(v[k]);
+    j.tail_pack[pack1_index(e, j.pack_c, j.tail_pack_cp)] = f32_to_bf16(v[k]);
   }
 }
 
@@ -279,7 +279,7 @@ __device__ __forceinline__ void sgd_tail_block(const SgdJob& j, int bid) {
     if constexpr (kMomentum) j.mom[e] = mv;
     j.p[e] = pv;
     if constexpr (kShadow) j.p16[e] = f32_to_bf16(pv);
-    if (j.tail_pack) j.tail_pack[(i / r.tail_c) * j.tail_pack_cp + i % r.tail_c] = f32_to_bf16(pv);
+    if (j.tail_pack) j.tail_pack[pack1_index(i, r.tail_c, j.tail_pack_cp)] = f32_to_bf16(pv);
   };
   if (r.tail_tpo == 32)
     slab_reduce_each<32>(r.tail_slab, r.tail_splits, r.tail_cout, r.tail_taps, r.tail_cp, r.tail_c, bid, r.tail_nblk,

@@ -802,6 +802,64 @@ def test_conv_fwd_position_major(C, shape):
     torch.testing.assert_close(st[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
 
 
+def _pair_pack(w):  # [Cout][5][5][3] fp32 -> [Cout][5][3][2][4] bf16 (csrc dl_common.h pack1_index, cp = -5)
+    co = w.shape[0]
+    q = torch.zeros(co, 5, 3, 2, 4, dtype=torch.bfloat16, device=w.device)
+    for kx in range(5):
+        q[:, :, kx // 2, kx % 2, :3] = w[:, :, kx, :].to(torch.bfloat16)
+    return q
+
+
+def test_prep_step_pair_pack(C):
+    """prep_step with w1_cp = -KS packs the first-layer weights two taps per
+    16-byte chunk (3 channels + a zero each) and leaves the pads alone."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(3)
+    B = 2
+    x3 = torch.randn(B, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)
+    x8 = torch.zeros(B, 36, 36, 8, dtype=torch.bfloat16, device=dev)
+    w1 = torch.randn(64, 5, 5, 3, device=dev, generator=g)
+    w1q = torch.zeros(64, 5, 3, 2, 4, dtype=torch.bfloat16, device=dev)
+    C.prep_step(x3.data_ptr(), x8.data_ptr(), B * 1024, 3, 8, 32, 32, 2, w1.data_ptr(), w1q.data_ptr(), 64, 25, 3, -5,
+                [], [], [], [], [], [], _s())
+    torch.cuda.synchronize()
+    assert torch.equal(w1q, _pair_pack(w1))
+
+
+@pytest.mark.parametrize("B", [128, 4])
+def test_conv_c8_pair_packed_weights(C, B):
+    """First-layer forward on pair-packed weights (tile bit 24: 120 instead of
+    200 K values per output channel) == the channel-padded kernel to bf16
+    rounding of a reordered fp32 sum, BN sums likewise, and vs fp32."""
+    dev = torch.device("cuda")
+    H, cout = 32, 64
+    g = torch.Generator(device=dev).manual_seed(B + 1)
+    x = torch.randn(B, H, H, 3, device=dev, generator=g).to(torch.bfloat16)
+    w = torch.randn(cout, 5, 5, 3, device=dev, generator=g) * 0.2
+    x8 = torch.zeros(B, H + 4, H + 4, 8, dtype=torch.bfloat16, device=dev)
+    x8[:, 2:H + 2, 2:H + 2, :3] = x
+    w8 = torch.zeros(cout, 5, 5, 8, dtype=torch.bfloat16, device=dev)
+    w8[..., :3] = w.to(torch.bfloat16)
+    wq = _pair_pack(w)
+    rows = C.conv_fwd_stat_rows(B, H, H, 8, cout, 5, 2, 1)
+    outs = []
+    for wt, tile in ((w8, 2), (wq, 2 | (1 << 24))):
+        y = torch.full((B, H, H, cout), float("nan"), dtype=torch.bfloat16, device=dev)
+        st = torch.zeros(max(rows, 4096), 2, cout, device=dev)
+        T = C.conv_fwd(x8.data_ptr(), wt.data_ptr(), y.data_ptr(), st.data_ptr(), 0, B, H, H, 8, cout, 5, tile, 1, _s())
+        torch.cuda.synchronize()
+        outs.append((y, st[:T].sum(0)))
+    (y0, s0), (y1, s1) = outs
+    assert torch.isfinite(y1.float()).all()
+    assert _rel(y1, y0.float()) < 4e-3
+    torch.testing.assert_close(s1, s0, rtol=1e-3, atol=1e-2)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.to(torch.bfloat16).float().permute(0, 3, 1, 2),
+                   padding=2).permute(0, 2, 3, 1)
+    assert _rel(y1, ref) < 8e-3
+    with pytest.raises(RuntimeError):  # pair-packed weights on a plan the first-layer kernel does not serve
+        C.conv_fwd(x8.data_ptr(), wq.data_ptr(), y1.data_ptr(), 0, 0, B, H, H, 8, cout, 5, 0 | (1 << 24), 1, _s())
+
+
 @pytest.mark.parametrize("B", [128, 64])
 def test_conv_c8_tiles_per_workgroup(C, B):
     """First-layer (Cin = 8) kernel with several M tiles per workgroup sharing

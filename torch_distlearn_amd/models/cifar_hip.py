@@ -218,6 +218,10 @@ class CifarHIPExecutor:
         # 33.5 -> 34.9 us: the reducer's chain of slice drain, counter, slice loads
         # and pool-window loads is serial latency at the kernel's tail), 0: off
         self.fix = int(os.environ.get("DISTLEARN_FIX", "1"))
+        # layer 1's forward on pair-packed weights (csrc conv_fwd_c8_kernel PAIR):
+        # 12.3 -> 11.1 us, step 0.2946 -> 0.2929 ms median of 10 interleaved runs
+        # (profiles/r6_pair1_ab.txt)
+        self.pair1 = True
         self.atomic = self.mode > 0             # BN statistics / gradients by atomics, no finalize kernels
         # (mode 2) the last block's BN backward reduce runs inside the head kernel and
         # the classifier weight gradient rides the BN backward apply launch
@@ -245,7 +249,13 @@ class CifarHIPExecutor:
         # producers write the interior, the kernels never bounds-test a tap
         P2 = 2 * SPAD
         self.x8 = torch.zeros(B, H0 + P2, H0 + P2, CIN_PAD, dtype=BF16, device=d)
-        self.w1p = torch.zeros(self.couts[0], KSIZE * KSIZE * CIN_PAD, dtype=BF16, device=d)
+        # layer-1 weights for its forward: pair-packed (two adjacent taps' 3 channels
+        # per 16-byte chunk, csrc dl_common.h pack1_index with cp = -KSIZE: 120
+        # instead of 200 K values per output channel, conv_fwd_c8_kernel PAIR);
+        # the packers (prep, the update's tail) never write the zero pads
+        self.w1_cp = -KSIZE if self.pair1 else CIN_PAD
+        self.w1p = torch.zeros(self.couts[0], KSIZE * ((KSIZE + 1) // 2) * 8 if self.pair1
+                               else KSIZE * KSIZE * CIN_PAD, dtype=BF16, device=d)
         self.wt = [None] + [e(self.cins[i], KSIZE, KSIZE, self.couts[i]) for i in range(1, self.nb)]
         self.y = [e(B, h, h, c) for h, c in zip(self.hs, self.couts)]
         self.p = [torch.zeros(B, h // 2 + P2, h // 2 + P2, c, dtype=BF16, device=d) if i + 1 < self.nb
@@ -354,7 +364,7 @@ class CifarHIPExecutor:
                 raise ValueError("DeviceLoader images do not match the model input")
             self.C.prep_step_gather(img, order, lab_all, lab_out, ctr, n_order, B, C, mean, std, self.x8.data_ptr(),
                                     CIN_PAD, h, h, SPAD, self.p32[0].data_ptr(), self.w1p.data_ptr(), self.couts[0],
-                                    KSIZE * KSIZE, self.cins_real[0], CIN_PAD, *tw, *self._zero_args(train), s)
+                                    KSIZE * KSIZE, self.cins_real[0], self.w1_cp, *tw, *self._zero_args(train), s)
             return B
         B = x.shape[0]
         if B > self.cap:
@@ -363,7 +373,7 @@ class CifarHIPExecutor:
             raise ValueError("CifarHIPExecutor expects contiguous NHWC bf16 input [B, H, W, 3]")
         self.C.prep_step(x.data_ptr(), self.x8.data_ptr(), B * h * h, self.cins_real[0], CIN_PAD, h, h, SPAD,
                          self.p32[0].data_ptr(), self.w1p.data_ptr(), self.couts[0], KSIZE * KSIZE,
-                         self.cins_real[0], CIN_PAD, *tw, *self._zero_args(train), s)
+                         self.cins_real[0], self.w1_cp, *tw, *self._zero_args(train), s)
         return B
 
     def _forward(self, B: int, s: int, train: bool, pool_last: bool = True):
@@ -380,6 +390,8 @@ class CifarHIPExecutor:
             M = B * h * h
             w = self.w1p if i == 0 else self.p16[self._leaf(i, 0)]
             t, sp = self.fwd_plan[i]
+            if i == 0 and self.pair1:
+                t |= 1 << 24  # pair-packed weights (csrc FwdCfg bit 24)
             img = self.fwd_region_images and h * h < 128 and 128 % (h * h) == 0
             if img:
                 C.set_conv_region(2)
@@ -762,7 +774,7 @@ class CifarHIPExecutor:
         lf = self._leaf(0, 0)
         self.C.arm_sgd_next_prep(img, order, lab_all, lab_out, ctr, n_order, loader.batch, C, mean, std,
                                  self.x8.data_ptr(), CIN_PAD, h, h, SPAD, *self._zero_args(True),
-                                 self.w1p.data_ptr(), CIN_PAD, self.flat.offsets[lf] - HEADER, self.flat.numels[lf])
+                                 self.w1p.data_ptr(), self.w1_cp, self.flat.offsets[lf] - HEADER, self.flat.numels[lf])
         self._prefetched = True
         self.prepared_ahead += 1
         return True
