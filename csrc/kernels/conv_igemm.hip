@@ -98,6 +98,7 @@ struct ConvGeom {
   // reads padded input pixel (S*oh + kh, S*ow + kw) of the [B][Hp][Wp][Cin]
   // buffer; kernels may be KH x KW (K = KH*KW*Cin, taps row-major).
   int S, KH, KW;
+  int kwstep;  // wgrad B chunks: tap column kw * kwstep (2: the pair-packed first layer, make_geom_pair)
   int dsep, dHp, dWp, dpad;  // wgrad: dy has its own buffer geometry [B][dHp][dWp][Cout], interior at dpad
   // epilogue output-row map (om != 0): output pixel (b, oh, ow) is stored at
   // row b*omHW + (omS*oh + omH0)*omW + omS*ow + omW0 (the phases of a strided
@@ -170,7 +171,7 @@ static ConvGeom make_geom(int B, int H, int W, int Cin, int Cout, int KS) {
   if (Cin < 8) throw std::runtime_error("conv: Cin must be >= 8 (pad the input channels)");
   g.pow2 = is_pow2(W) && is_pow2(H) ? 1 : 0;
   g.posm = 0;
-  g.S = 1; g.KH = KS; g.KW = KS;
+  g.S = 1; g.KH = KS; g.KW = KS; g.kwstep = 1;
   g.dsep = 0; g.dHp = g.Hp; g.dWp = g.Wp; g.dpad = g.pad;
   g.om = 0; g.omS = 1; g.omH0 = 0; g.omW0 = 0; g.omW = W; g.omHW = H * W;
   g.logW = g.pow2 ? ilog2_exact(W, "W") : 0;
@@ -185,6 +186,20 @@ static ConvGeom make_geom(int B, int H, int W, int Cin, int Cout, int KS) {
   g.Kch = g.K / 8;
   if ((int64_t)B * g.Hp * g.Wp * std::max(Cin, Cout) >= (1ll << 31) || (int64_t)Cout * g.K >= (1ll << 31))
     throw std::runtime_error("conv: operand too large for 32-bit offsets");
+  return g;
+}
+
+// The pair-packed first layer (4-channel padded input, <= 4 real channels):
+// one 16-byte K chunk = channels 0-3 of two horizontally adjacent taps
+// (dl_common.h pack1_index, cp = -KS), K = KS * ceil(KS/2) * 8.  For the
+// wgrad kernel's B operand the chunk is 2 adjacent pixels of the [.][Wp][4]
+// buffer: KW = ceil(KS/2) chunk columns at tap column 2 * kw.
+static ConvGeom make_geom_pair(int B, int H, int W, int Cout, int KS) {
+  ConvGeom g = make_geom(B, H, W, 8, Cout, KS);
+  const int cpr = (KS + 1) / 2;
+  g.Cin = 4; g.logC8 = 0;
+  g.KW = cpr; g.kwstep = 2;
+  g.Kch = KS * cpr; g.K = g.Kch * 8;
   return g;
 }
 
@@ -1444,7 +1459,8 @@ __global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restri
   const int cpr = (g.KS + 1) >> 1;
   const int taps = PAIR ? g.KS * cpr : g.KS * g.KS;  // K chunks (16 B) per output channel
   const int nsteps = (taps + 3) / 4;                 // 32-deep k-steps (4 chunks each)
-  const int rslots = region_rows * g.Wp;             // region pixels (16 B each)
+  const int rpix = region_rows * g.Wp;               // region pixels (PAIR: 8 B each, else 16 B)
+  const int rslots = PAIR ? (rpix + 1) / 2 : rpix;   // 16-byte region slots
   const int rslots_p = (rslots + 2 + 63) / 64 * 64;  // + >= 2 zero slots, whole DMA pieces
   // weight panel: BN rows x taps 16-B chunks.  (Its B-fragment reads put rows
   // r and r+16 on the same banks; spreading them with 4 empty chunks per 16
@@ -1466,12 +1482,13 @@ __global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restri
   const int HW = 1 << g.logHW;
   const int img0 = mg0 >> g.logHW, oh0 = (mg0 & (HW - 1)) >> g.logW;
   const int start_pix = (img0 * g.Hp + oh0) * g.Wp;
-  const rsrc_t xr = make_rsrc(x, (unsigned)((int64_t)g.B * g.Hp * g.Wp * 16));
+  const rsrc_t xr = make_rsrc(x, (unsigned)((int64_t)g.B * g.Hp * g.Wp * (PAIR ? 8 : 16)));
   const rsrc_t wr = make_rsrc(w, (unsigned)((int64_t)g.Cout * taps * 16));
   // one DMA burst: region pixels (contiguous padded rows) then the weight panel
   for (int q = wid; q < rslots_p / 64; q += NW) {
     const int sl = q * 64 + lane;
-    blds16(xr, sl < rslots ? 16u * (unsigned)(start_pix + sl) : kOOB, 0u, sR + q * 1024);
+    blds16(xr, sl < rslots ? (PAIR ? 8u * (unsigned)start_pix + 16u * (unsigned)sl : 16u * (unsigned)(start_pix + sl))
+                           : kOOB, 0u, sR + q * 1024);
   }
   for (int q = wid; q < wslots_p / 64; q += NW) {
     const int sl = q * 64 + lane;
@@ -1506,13 +1523,14 @@ __global__ void __launch_bounds__(512) conv_fwd_c8_kernel(const bf16_t* __restri
     bf16x8 fa[FM], fb[FN];
 #pragma unroll
     for (int a = 0; a < FM; ++a) {
-      const int q = t < taps ? a_pix[a] + toff : zero_slot;
-      if constexpr (PAIR) {
-        const uint2 lo = *reinterpret_cast<const uint2*>(sR + q * 16);
-        const uint2 hi = *reinterpret_cast<const uint2*>(sR + (q + 1) * 16);
-        fa[a] = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      if constexpr (PAIR) {  // 8-byte pixels: the chunk is pixels q, q+1 (two 8-byte-aligned reads)
+        const int q = a_pix[a] + (t < taps ? toff : 0);
+        const uint2 lo = *reinterpret_cast<const uint2*>(sR + q * 8);
+        const uint2 hi = *reinterpret_cast<const uint2*>(sR + q * 8 + 8);
+        const bool ok = t < taps;  // past the last chunk: zeros (the weights there are clamped, not zero)
+        fa[a] = __builtin_bit_cast(bf16x8, make_uint4(ok ? lo.x : 0u, ok ? lo.y : 0u, ok ? hi.x : 0u, ok ? hi.y : 0u));
       } else {
-        fa[a] = *reinterpret_cast<const bf16x8*>(sR + q * 16);
+        fa[a] = *reinterpret_cast<const bf16x8*>(sR + (t < taps ? a_pix[a] + toff : zero_slot) * 16);
       }
     }
 #pragma unroll
@@ -1691,7 +1709,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
     const int kc = k0 / 8 + ch;
     b_kok[j] = kc < g.Kch;
     const int kpos = kc >> g.logC8;
-    const int kh = kpos / g.KW, kw = kpos - kh * g.KW;
+    const int kh = kpos / g.KW, kw = (kpos - kh * g.KW) * g.kwstep;
     b_off[j] = (lane_pix(row) + kh * g.Wp + kw) * g.Cin + ((kc & (C8 - 1)) << 3);
   }
   const i32x4 dyr = make_rsrc4(dy, (unsigned)((int64_t)g.B * g.dHp * g.dWp * g.Cout * 2));
@@ -2459,7 +2477,8 @@ void set_conv_c8_mt(int mt) {
 int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t slab, int B, int H, int W, int Cin,
              int Cout, int KS, int tile, int splits, uintptr_t stream) {
   const FwdCfg cfg(tile);
-  ConvGeom g = make_geom(B, H, W, Cin, Cout, KS);
+  if (g_c8_pair && Cin != 4) throw std::runtime_error("conv_fwd: pair-packed weights need the 4-channel input");
+  ConvGeom g = g_c8_pair ? make_geom_pair(B, H, W, Cout, KS) : make_geom(B, H, W, Cin, Cout, KS);
   hipStream_t s = as_stream(stream);
   if (splits < 1) splits = 1;
   if (splits > 1 && !slab) throw std::runtime_error("conv_fwd: split-K needs a slab");
@@ -2479,11 +2498,12 @@ int conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t s
   }
   const int c8_rows = c8_mt * 128 / std::max(1, W) + KS - 1;
   const int c8_chunks = g_c8_pair ? KS * ((KS + 1) / 2) : KS * KS;  // weight chunks per output channel
+  const int c8_rslots = g_c8_pair ? (c8_rows * g.Wp + 1) / 2 : c8_rows * g.Wp;  // 16-B region slots (pair: 2 pixels)
   const size_t c8_lds =
-      (size_t)((c8_rows * g.Wp + 2 + 63) / 64 * 64 + (64 * c8_chunks + 63) / 64 * 64) * 16 + 4 * 2 * 64 * 4;
+      (size_t)((c8_rslots + 2 + 63) / 64 * 64 + (64 * c8_chunks + 63) / 64 * 64) * 16 + 4 * 2 * 64 * 4;
   // the NHWC BN reduce epilogue and the in-launch split-K combine are on the streaming kernel
   const bool streaming_only = g_fix.on;
-  if (!streaming_only && tile == 2 && splits == 1 && g_region && g.pow2 && Cin == 8 && W <= 128 && 128 % W == 0 && (H * W) % 128 == 0 &&
+  if (!streaming_only && tile == 2 && splits == 1 && g_region && g.pow2 && (Cin == 8 || g_c8_pair) && W <= 128 && 128 % W == 0 && (H * W) % 128 == 0 &&
       Cout % 64 == 0 && c8_lds <= 160 * 1024) {
     const int grid = (g.M / 128 / c8_mt) * (Cout / 64);
     auto go = [&](auto kern) {
@@ -2739,6 +2759,11 @@ static void conv_wgrad_g(const ConvGeom& g, uintptr_t dy, uintptr_t x, uintptr_t
 void conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t out, int B, int H, int W, int Cin, int Cout, int KS, int splits,
                 int ldo, int tile, int atomic_creal, uintptr_t stream) {
   if (atomic_creal != 0) throw std::runtime_error("conv_wgrad: atomic split-K was removed in round 6 (pass 0)");
+  if ((tile >> 24) & 1) {  // pair-packed first layer (make_geom_pair): x is [B][Hp][Wp][4]
+    if (Cin != 4) throw std::runtime_error("conv_wgrad: the pair-packed layout needs a 4-channel input");
+    conv_wgrad_g(make_geom_pair(B, H, W, Cout, KS), dy, x, out, splits, ldo, tile & 15, stream);
+    return;
+  }
   conv_wgrad_g(make_geom(B, H, W, Cin, Cout, KS), dy, x, out, splits, ldo, tile, stream);
 }
 

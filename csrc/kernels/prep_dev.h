@@ -68,10 +68,17 @@ __device__ __forceinline__ void prep_pad_block(const PrepArgs& a, int blk) {
 #pragma unroll
         for (int k = 0; k < 12; ++k) f[k] = (k & 1) ? hi_bf16(d[k >> 1]) : lo_bf16(d[k >> 1]);
       }
-      uint4* dst = reinterpret_cast<uint4*>(a.xp + (((int64_t)b * Hp + h + a.sp) * Wp + w + a.sp) * 8);
+      if (a.Cp == 4) {  // 8-byte pixels (the pair-packed first layer: csrc conv_fwd_c8_kernel PAIR)
+        uint2* dst = reinterpret_cast<uint2*>(a.xp + (((int64_t)b * Hp + h + a.sp) * Wp + w + a.sp) * 4);
 #pragma unroll
-      for (int px = 0; px < 4; ++px)
-        dst[px] = make_uint4(pack_bf16x2(f[3 * px], f[3 * px + 1]), pack_bf16x2(f[3 * px + 2], 0.f), 0u, 0u);
+        for (int px = 0; px < 4; ++px)
+          dst[px] = make_uint2(pack_bf16x2(f[3 * px], f[3 * px + 1]), pack_bf16x2(f[3 * px + 2], 0.f));
+      } else {
+        uint4* dst = reinterpret_cast<uint4*>(a.xp + (((int64_t)b * Hp + h + a.sp) * Wp + w + a.sp) * 8);
+#pragma unroll
+        for (int px = 0; px < 4; ++px)
+          dst[px] = make_uint4(pack_bf16x2(f[3 * px], f[3 * px + 1]), pack_bf16x2(f[3 * px + 2], 0.f), 0u, 0u);
+      }
     }
     return;
   }
@@ -95,8 +102,12 @@ __device__ __forceinline__ void prep_pad_block(const PrepArgs& a, int blk) {
       for (int c = 0; c < a.C; ++c) v[c] = a.x[(int64_t)p * a.C + c];
     }
     const int64_t q = ((int64_t)b * Hp + h + a.sp) * Wp + w + a.sp;  // interior of the zero-bordered buffer
-    for (int c = 0; c < a.Cp; c += 8)
-      *reinterpret_cast<uint4*>(a.xp + q * a.Cp + c) = *reinterpret_cast<const uint4*>(v + c);
+    if (a.Cp == 4) {
+      *reinterpret_cast<uint2*>(a.xp + q * 4) = *reinterpret_cast<const uint2*>(v);
+    } else {
+      for (int c = 0; c < a.Cp; c += 8)
+        *reinterpret_cast<uint4*>(a.xp + q * a.Cp + c) = *reinterpret_cast<const uint4*>(v + c);
+    }
   }
 }
 
@@ -129,11 +140,12 @@ inline void prep_set_zero(PrepArgs& a, const std::vector<uintptr_t>& zp, const s
 
 // Host: the pad/gather job over P = B*H*W pixels (sets P, quad, nb_pad).
 inline void prep_set_pad(PrepArgs& a, int64_t P) {
-  if (a.C > 16 || a.Cp > 16 || a.Cp % 8 != 0) throw std::runtime_error("prep_step: input channels must pad to 8 or 16");
+  if (a.C > 16 || a.Cp > 16 || (a.Cp % 8 != 0 && a.Cp != 4) || a.C > a.Cp)
+    throw std::runtime_error("prep_step: input channels must pad to 4, 8 or 16");
   if (P >= (1ll << 31)) throw std::runtime_error("prep_step: too many pixels");
   if (P > 0 && (a.H <= 0 || a.W <= 0 || P % ((int64_t)a.H * a.W) != 0)) throw std::runtime_error("prep_step: P != B*H*W");
   a.P = (int)P;
-  a.quad = (a.C == 3 && a.Cp == 8 && P > 0 && a.W % 4 == 0) ? 1 : 0;
+  a.quad = (a.C == 3 && (a.Cp == 8 || a.Cp == 4) && P > 0 && a.W % 4 == 0) ? 1 : 0;
   a.nb_pad = a.quad ? (int)(P / ((int64_t)a.H * a.W)) : (int)std::min<int64_t>((P + 255) / 256, 1024);
 }
 

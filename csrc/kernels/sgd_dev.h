@@ -330,7 +330,8 @@ inline SgdJob make_sgd_job(uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t p1
     r.tail_splits = (int)tail[2]; r.tail_cout = (int)tail[3]; r.tail_taps = (int)tail[4];
     r.tail_cp = (int)tail[5]; r.tail_c = (int)tail[6];
     if (off % 4 || len % 4 || off < lo || off + len > hi || len != (int64_t)r.tail_cout * r.tail_taps * r.tail_c ||
-        r.tail_c > r.tail_cp || r.tail_splits < 1 || tail_slab == 0)
+        (r.tail_cp > 0 ? r.tail_c > r.tail_cp : (r.tail_c > 4 || r.tail_taps != r.tail_cp * r.tail_cp)) ||
+        r.tail_splits < 1 || tail_slab == 0)
       throw std::runtime_error("sgd job: inconsistent tail range");
     for (size_t q = 0; q < k; ++q)
       if (offs[q] < off + len && off < offs[q] + lens[q]) throw std::runtime_error("sgd job: tail overlaps");

@@ -19,13 +19,14 @@ template <int TPO, class F>
 __device__ __forceinline__ void slab_reduce_each(const float* __restrict__ slabs, int splits, int Cout, int taps,
                                                  int Cp, int C, int bid, int nblk, F&& f) {
   const int64_t total = (int64_t)Cout * taps * C;
-  const int64_t slab = (int64_t)Cout * taps * Cp;
+  // Cp < 0: the pair-packed first layer (dl_common.h pack1_index, -Cp = kernel width)
+  const int64_t slab = Cp > 0 ? (int64_t)Cout * taps * Cp : (int64_t)Cout * (-Cp) * ((1 - Cp) / 2) * 8;
   const int sub = threadIdx.x % TPO;
   const int64_t opb = 256 / TPO;  // outputs per block iteration
   for (int64_t i = (int64_t)bid * opb + threadIdx.x / TPO; i < total; i += (int64_t)nblk * opb) {
     const int c = (int)(i % C);
     const int64_t rest = i / C;  // co*taps + tap
-    const int64_t src = rest * Cp + c;
+    const int64_t src = Cp > 0 ? rest * Cp + c : pack1_index(i, C, Cp);
     // splits in batches of 4 loads in flight before the adds (a load->add chain
     // per split was latency-bound); the adds keep the split order
     float s = 0.f;

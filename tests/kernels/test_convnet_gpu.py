@@ -817,19 +817,24 @@ def test_prep_step_pair_pack(C):
     g = torch.Generator(device=dev).manual_seed(3)
     B = 2
     x3 = torch.randn(B, 32, 32, 3, device=dev, generator=g).to(torch.bfloat16)
-    x8 = torch.zeros(B, 36, 36, 8, dtype=torch.bfloat16, device=dev)
     w1 = torch.randn(64, 5, 5, 3, device=dev, generator=g)
-    w1q = torch.zeros(64, 5, 3, 2, 4, dtype=torch.bfloat16, device=dev)
-    C.prep_step(x3.data_ptr(), x8.data_ptr(), B * 1024, 3, 8, 32, 32, 2, w1.data_ptr(), w1q.data_ptr(), 64, 25, 3, -5,
-                [], [], [], [], [], [], _s())
-    torch.cuda.synchronize()
-    assert torch.equal(w1q, _pair_pack(w1))
+    for cp in (8, 4):  # the input into the 8- or the 4-channel layer-1 buffer
+        xb = torch.full((B, 36, 36, cp), float("nan"), dtype=torch.bfloat16, device=dev)
+        xb[:, :2] = 0; xb[:, -2:] = 0; xb[:, :, :2] = 0; xb[:, :, -2:] = 0  # noqa: E702 (the executor's zero border)
+        w1q = torch.zeros(64, 5, 3, 2, 4, dtype=torch.bfloat16, device=dev)
+        C.prep_step(x3.data_ptr(), xb.data_ptr(), B * 1024, 3, cp, 32, 32, 2, w1.data_ptr(), w1q.data_ptr(), 64, 25, 3,
+                    -5, [], [], [], [], [], [], _s())
+        torch.cuda.synchronize()
+        assert torch.equal(w1q, _pair_pack(w1))
+        assert torch.equal(xb[:, 2:34, 2:34, :3], x3) and not xb[:, 2:34, 2:34, 3:].any()
+        assert not xb[:, :2].any() and not xb[:, :, -2:].any()
 
 
 @pytest.mark.parametrize("B", [128, 4])
 def test_conv_c8_pair_packed_weights(C, B):
-    """First-layer forward on pair-packed weights (tile bit 24: 120 instead of
-    200 K values per output channel) == the channel-padded kernel to bf16
+    """First-layer forward on pair-packed weights over the 4-channel input
+    (tile bit 24: 120 instead of 200 K values per output channel, 8-byte
+    pixels) == the channel-padded kernel on the 8-channel input to bf16
     rounding of a reordered fp32 sum, BN sums likewise, and vs fp32."""
     dev = torch.device("cuda")
     H, cout = 32, 64
@@ -838,15 +843,17 @@ def test_conv_c8_pair_packed_weights(C, B):
     w = torch.randn(cout, 5, 5, 3, device=dev, generator=g) * 0.2
     x8 = torch.zeros(B, H + 4, H + 4, 8, dtype=torch.bfloat16, device=dev)
     x8[:, 2:H + 2, 2:H + 2, :3] = x
+    x4 = x8[..., :4].contiguous()
     w8 = torch.zeros(cout, 5, 5, 8, dtype=torch.bfloat16, device=dev)
     w8[..., :3] = w.to(torch.bfloat16)
     wq = _pair_pack(w)
     rows = C.conv_fwd_stat_rows(B, H, H, 8, cout, 5, 2, 1)
     outs = []
-    for wt, tile in ((w8, 2), (wq, 2 | (1 << 24))):
+    for xin, wt, cin, tile in ((x8, w8, 8, 2), (x4, wq, 4, 2 | (1 << 24))):
         y = torch.full((B, H, H, cout), float("nan"), dtype=torch.bfloat16, device=dev)
         st = torch.zeros(max(rows, 4096), 2, cout, device=dev)
-        T = C.conv_fwd(x8.data_ptr(), wt.data_ptr(), y.data_ptr(), st.data_ptr(), 0, B, H, H, 8, cout, 5, tile, 1, _s())
+        T = C.conv_fwd(xin.data_ptr(), wt.data_ptr(), y.data_ptr(), st.data_ptr(), 0, B, H, H, cin, cout, 5, tile, 1,
+                       _s())
         torch.cuda.synchronize()
         outs.append((y, st[:T].sum(0)))
     (y0, s0), (y1, s1) = outs
@@ -857,7 +864,42 @@ def test_conv_c8_pair_packed_weights(C, B):
                    padding=2).permute(0, 2, 3, 1)
     assert _rel(y1, ref) < 8e-3
     with pytest.raises(RuntimeError):  # pair-packed weights on a plan the first-layer kernel does not serve
-        C.conv_fwd(x8.data_ptr(), wq.data_ptr(), y1.data_ptr(), 0, 0, B, H, H, 8, cout, 5, 0 | (1 << 24), 1, _s())
+        C.conv_fwd(x4.data_ptr(), wq.data_ptr(), y1.data_ptr(), 0, 0, B, H, H, 4, cout, 5, 0 | (1 << 24), 1, _s())
+    with pytest.raises(RuntimeError):  # ... or on the 8-channel input
+        C.conv_fwd(x8.data_ptr(), wq.data_ptr(), y1.data_ptr(), 0, 0, B, H, H, 8, cout, 5, 2 | (1 << 24), 1, _s())
+
+
+@pytest.mark.parametrize("splits", [1, 4])
+def test_conv_wgrad_pair_packed(C, splits):
+    """First-layer weight gradient in the pair-packed layout (tile bit 24: the
+    B chunk = two adjacent pixels of the 4-channel input, K = 120) vs an fp32
+    reference, and slab_reduce with Cp = -5 == the leaf's [Cout][5][5][3]."""
+    dev = torch.device("cuda")
+    B, H, cout = 8, 32, 64
+    g = torch.Generator(device=dev).manual_seed(11 + splits)
+    x = torch.randn(B, H, H, 3, device=dev, generator=g).to(torch.bfloat16)
+    dy = torch.randn(B, H, H, cout, device=dev, generator=g).to(torch.bfloat16)
+    x4 = torch.zeros(B, H + 4, H + 4, 4, dtype=torch.bfloat16, device=dev)
+    x4[:, 2:H + 2, 2:H + 2, :3] = x
+    dyp = _pad(dy)
+    slabs = torch.full((splits, cout, 120), float("nan"), device=dev)
+    C.conv_wgrad(dyp.data_ptr(), x4.data_ptr(), slabs.data_ptr(), B, H, H, 4, cout, 5, splits, 120, 1 | (1 << 24), 0,
+                 _s())
+    dw = torch.full((cout, 5, 5, 3), float("nan"), device=dev)
+    C.slab_reduce(slabs.data_ptr(), dw.data_ptr(), splits, cout, 25, -5, 3, _s())
+    wr = torch.zeros(cout, 3, 5, 5, device=dev, requires_grad=True)
+    F.conv2d(x.float().permute(0, 3, 1, 2), wr, padding=2).backward(dy.float().permute(0, 3, 1, 2))
+    torch.cuda.synchronize()
+    ref = wr.grad.permute(0, 2, 3, 1)
+    assert _rel(dw, ref) < 1e-4
+    # the packed slab itself: chunk (kh, kw // 2), half kw % 2, channel c (the pad channel's sums are 0)
+    packed = slabs.sum(0).view(cout, 5, 3, 2, 4)
+    for kx in range(5):
+        assert _rel(packed[:, :, kx // 2, kx % 2, :3], ref[:, :, kx, :]) < 1e-4
+    assert not packed[..., 3].any()
+    with pytest.raises(RuntimeError):
+        C.conv_wgrad(dyp.data_ptr(), x4.data_ptr(), slabs.data_ptr(), B, H, H, 8, cout, 5, 1, 120, 1 | (1 << 24), 0,
+                     _s())
 
 
 @pytest.mark.parametrize("B", [128, 64])

@@ -112,7 +112,11 @@ def _wgrad_plan(cout: int, K: int, M: int, reserve: int = 0):
     bm, bn = {2: (128, 128), 1: (64, 64)}[tile]
     slots = 2 * (256 - reserve) if tile == 1 else 256 - reserve
     tiles = (cout // bm) * ((K + bn - 1) // bn)
-    splits = max(1, min(slots // tiles, M // 512))
+    # at most 128 splits: the reducer (a 32-lane group per weight) then keeps
+    # its 4 loads per lane in flight at once -- the pair-packed layer 1 (2
+    # tiles) at 256 splits: wgrad 8.6 us but its reduce 11.1 vs 8.8 us at 128
+    # (profiles/r6_pair1_x4_ab.txt)
+    splits = max(1, min(slots // tiles, M // 512, 128))
     return tile, splits
 
 
@@ -218,9 +222,12 @@ class CifarHIPExecutor:
         # 33.5 -> 34.9 us: the reducer's chain of slice drain, counter, slice loads
         # and pool-window loads is serial latency at the kernel's tail), 0: off
         self.fix = int(os.environ.get("DISTLEARN_FIX", "1"))
-        # layer 1's forward on pair-packed weights (csrc conv_fwd_c8_kernel PAIR):
-        # 12.3 -> 11.1 us, step 0.2946 -> 0.2929 ms median of 10 interleaved runs
-        # (profiles/r6_pair1_ab.txt)
+        # layer 1 on pair-packed weights over a 4-channel input (csrc
+        # conv_fwd_c8_kernel PAIR, make_geom_pair): forward 12.3 -> 11.1 us, step
+        # 0.2946 -> 0.2929 ms (profiles/r6_pair1_ab.txt); the weight gradient in
+        # the same layout (K 200 -> 120) 12.2 -> 8.8 us, step 0.2981 -> 0.2949 ms
+        # median of 10 interleaved runs against the channel-padded layer 1
+        # (profiles/r6_pair1_x4_ab.txt)
         self.pair1 = True
         self.atomic = self.mode > 0             # BN statistics / gradients by atomics, no finalize kernels
         # (mode 2) the last block's BN backward reduce runs inside the head kernel and
@@ -248,7 +255,11 @@ class CifarHIPExecutor:
         # convolution inputs live in zero-bordered buffers [B, H+4, W+4, C]: the
         # producers write the interior, the kernels never bounds-test a tap
         P2 = 2 * SPAD
-        self.x8 = torch.zeros(B, H0 + P2, H0 + P2, CIN_PAD, dtype=BF16, device=d)
+        # layer 1 on pair-packed weights reads a 4-channel input (8-byte pixels; the
+        # wgrad's B chunk = two adjacent pixels), else the 8-channel one
+        self.kin0 = 4 if self.pair1 else CIN_PAD
+        self.k1 = KSIZE * ((KSIZE + 1) // 2) * 8 if self.pair1 else KSIZE * KSIZE * CIN_PAD  # layer-1 K
+        self.x8 = torch.zeros(B, H0 + P2, H0 + P2, self.kin0, dtype=BF16, device=d)
         # layer-1 weights for its forward: pair-packed (two adjacent taps' 3 channels
         # per 16-byte chunk, csrc dl_common.h pack1_index with cp = -KSIZE: 120
         # instead of 200 K values per output channel, conv_fwd_c8_kernel PAIR);
@@ -282,6 +293,7 @@ class CifarHIPExecutor:
             h, cin, cout = self.hs[i], self.cins[i], self.couts[i]
             M = B * h * h
             K = KSIZE * KSIZE * cin
+            Kw = self.k1 if i == 0 else K  # the weight gradient's K (layer 1: its packed layout)
             tile, splits = _fwd_plan(M, cout, K, batch_aware=True)
             if tile == 2 and splits == 2 and self._fix_ok(B, h, cin, cout, 2, 4):
                 # combined in-launch, a 2-split forward takes 4 (two rounds of the
@@ -309,12 +321,12 @@ class CifarHIPExecutor:
             gp = max(g, C.combine_bwd_reduce_blocks(B, h, h, cout), (B * (h // 2) * (h // 2) + 127) // 128) \
                 if i + 1 < self.nb else g
             self.bwd_part.append(None if self.atomic else torch.empty(gp, 2, cout, device=d))
-            tile_w, splits_w = _wgrad_plan(cout, K, M, self.cu_reserve)
+            tile_w, splits_w = _wgrad_plan(cout, Kw, M, self.cu_reserve)
             direct = splits_w == 1 and cin == self.cins_real[i]
             self.wplan.append((tile_w, splits_w, direct))
             if not direct:
-                wslab_elems = max(wslab_elems, splits_w * cout * K)
-            self.wslab_l.append(None if direct else torch.empty(splits_w * cout * K, device=d))
+                wslab_elems = max(wslab_elems, splits_w * cout * Kw)
+            self.wslab_l.append(None if direct else torch.empty(splits_w * cout * Kw, device=d))
             if i > 0:
                 dt, ds = _fwd_plan(M, cin, KSIZE * KSIZE * cout, batch_aware=True)
                 self.dgrad_plan[i] = (dt, ds)
@@ -363,7 +375,7 @@ class CifarHIPExecutor:
             if (x.H, x.W, C) != (h, h, self.cins_real[0]):
                 raise ValueError("DeviceLoader images do not match the model input")
             self.C.prep_step_gather(img, order, lab_all, lab_out, ctr, n_order, B, C, mean, std, self.x8.data_ptr(),
-                                    CIN_PAD, h, h, SPAD, self.p32[0].data_ptr(), self.w1p.data_ptr(), self.couts[0],
+                                    self.kin0, h, h, SPAD, self.p32[0].data_ptr(), self.w1p.data_ptr(), self.couts[0],
                                     KSIZE * KSIZE, self.cins_real[0], self.w1_cp, *tw, *self._zero_args(train), s)
             return B
         B = x.shape[0]
@@ -371,7 +383,7 @@ class CifarHIPExecutor:
             raise ValueError(f"batch {B} > executor capacity {self.cap}")
         if x.dim() != 4 or x.shape[-1] != self.cins_real[0] or x.dtype != BF16 or not x.is_contiguous():
             raise ValueError("CifarHIPExecutor expects contiguous NHWC bf16 input [B, H, W, 3]")
-        self.C.prep_step(x.data_ptr(), self.x8.data_ptr(), B * h * h, self.cins_real[0], CIN_PAD, h, h, SPAD,
+        self.C.prep_step(x.data_ptr(), self.x8.data_ptr(), B * h * h, self.cins_real[0], self.kin0, h, h, SPAD,
                          self.p32[0].data_ptr(), self.w1p.data_ptr(), self.couts[0], KSIZE * KSIZE,
                          self.cins_real[0], self.w1_cp, *tw, *self._zero_args(train), s)
         return B
@@ -402,8 +414,8 @@ class CifarHIPExecutor:
                                          cin, cout, KSIZE, t, sp, 0, 0, 0, s)
                 else:
                     ntm = C.conv_fwd(inp.data_ptr(), w.data_ptr(), self.y[i].data_ptr(),
-                                     self.stats[i].data_ptr() if train else 0, self.slabs.data_ptr(), B, h, h, cin,
-                                     cout, KSIZE, t, sp, s)
+                                     self.stats[i].data_ptr() if train else 0, self.slabs.data_ptr(), B, h, h,
+                                     self.kin0 if i == 0 else cin, cout, KSIZE, t, sp, s)
             finally:
                 if img:
                     C.set_conv_region(1)
@@ -428,6 +440,12 @@ class CifarHIPExecutor:
         launch (csrc conv_fwd_fix: the tile's last-arriving slice sums them and
         runs the epilogue) instead of a combine launch.  DISTLEARN_FIX=0: off."""
         return (self.fix > 0 and splits > 1 and self.C.conv_fix_ok(B, h, h, cin, cout, KSIZE, tile, splits) == 1)
+
+    def _slab_cp(self, i: int) -> int:
+        """The weight-gradient slab layout of block i for the reducers (csrc
+        slab_reduce_each Cp): the padded channel count, or -KSIZE for the
+        pair-packed first layer (dl_common.h pack1_index)."""
+        return self.w1_cp if i == 0 else self.cins[i]
 
     def _fin_args(self, i: int, M: int):
         """(sums, M, gamma, beta, conv bias, running mean, running var, eps,
@@ -544,15 +562,17 @@ class CifarHIPExecutor:
                 C.bn_relu_pool_bwd_apply(self.y[i].data_ptr(), self.dP[i].data_ptr(), self.coef[i].data_ptr(),
                                          self.acoef[i].data_ptr(), dY.data_ptr(), B, h, h, cout, SPAD, s)
             xin = self.x8 if i == 0 else self.p[i - 1]
-            K = KSIZE * KSIZE * cin
+            K = self.k1 if i == 0 else KSIZE * KSIZE * cin
+            kcin = self.kin0 if i == 0 else cin
             tile, splits, direct = self.wplan[i]
+            wtile = tile | (1 << 24) if i == 0 and self.pair1 else tile  # pair-packed layer 1 (csrc make_geom_pair)
             gw = self.g32[self._leaf(i, 0)]
             if direct:
-                C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), gw.data_ptr(), B, h, h, cin, cout, KSIZE, 1, K, tile, 0, s)
+                C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), gw.data_ptr(), B, h, h, kcin, cout, KSIZE, 1, K, wtile, 0, s)
             else:
                 slab = self.wslab_l[i]
-                C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), slab.data_ptr(), B, h, h, cin, cout, KSIZE, splits, K, tile,
-                             0, s)
+                C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), slab.data_ptr(), B, h, h, kcin, cout, KSIZE, splits, K,
+                             wtile, 0, s)
                 if i in self._deferred:
                     pass  # summed by the update kernel (defer_slab_reduce)
                 elif i in self._ride:
@@ -561,8 +581,8 @@ class CifarHIPExecutor:
                     if i == self._merged[0]:  # the last merged block's wgrad: one launch sums them all
                         self._reduce_merged(s)
                 else:
-                    C.slab_reduce(slab.data_ptr(), gw.data_ptr(), splits, cout, KSIZE * KSIZE, cin, self.cins_real[i],
-                                  s)
+                    C.slab_reduce(slab.data_ptr(), gw.data_ptr(), splits, cout, KSIZE * KSIZE, self._slab_cp(i),
+                                  self.cins_real[i], s)
             # conv bias grad: exactly 0 under train-mode BN (zeroed once at construction)
             if i in self._ride or (i in self._merged and i != self._merged[0]):
                 pass  # ready once the launch that sums its slabs is enqueued
@@ -714,7 +734,7 @@ class CifarHIPExecutor:
             if padded:
                 i = padded[0]
                 tail = [f.offsets[lfs[i]], f.numels[lfs[i]], self.wplan[i][1], self.couts[i], KSIZE * KSIZE,
-                        self.cins[i], self.cins_real[i]]
+                        self._slab_cp(i), self.cins_real[i]]
                 tslab = self.wslab_l[i].data_ptr()
             self._merged_args = (f.grad.data_ptr(), f.total, [f.offsets[lfs[i]] for i in inplace],
                                  [f.numels[lfs[i]] for i in inplace], [self.wslab_l[i].data_ptr() for i in inplace],
@@ -750,7 +770,7 @@ class CifarHIPExecutor:
         # reduces one padded tail; any further block keeps its stand-alone slab_reduce
         blocks = sorted(inplace[:4] + padded[:1])
         self._deferred = tuple(blocks)
-        return [(self._leaf(i, 0), self.wslab_l[i], self.wplan[i][1], self.couts[i], taps, self.cins[i],
+        return [(self._leaf(i, 0), self.wslab_l[i], self.wplan[i][1], self.couts[i], taps, self._slab_cp(i),
                  self.cins_real[i]) for i in blocks]
 
     def arm_next_prep(self, loader) -> bool:
@@ -773,7 +793,7 @@ class CifarHIPExecutor:
             return False
         lf = self._leaf(0, 0)
         self.C.arm_sgd_next_prep(img, order, lab_all, lab_out, ctr, n_order, loader.batch, C, mean, std,
-                                 self.x8.data_ptr(), CIN_PAD, h, h, SPAD, *self._zero_args(True),
+                                 self.x8.data_ptr(), self.kin0, h, h, SPAD, *self._zero_args(True),
                                  self.w1p.data_ptr(), self.w1_cp, self.flat.offsets[lf] - HEADER, self.flat.numels[lf])
         self._prefetched = True
         self.prepared_ahead += 1
