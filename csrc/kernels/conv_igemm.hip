@@ -863,7 +863,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_fwd_kernel(const bf16_t* __
   const int m0 = tm * BM, n0 = tn * BN;
   const int C8 = 1 << g.logC8;
   // Position-major tiles (g.posm, host-enabled for TAPU layers whose output is
-  // smaller than the kernel, B % BM == 0): M tile tm holds images b0..b0+BM-1
+  // smaller than twice the kernel, B % BM == 0): M tile tm holds images b0..b0+BM-1
   // at ONE output pixel, so every row of the tile has the same valid taps and
   // the taps that only read the zero border are skipped (4x4 output, 5x5
   // kernel: 9-16 of 25 taps per pixel).  K steps are split evenly per tile.
@@ -2190,8 +2190,11 @@ static FixState g_fix{};
 static int g_fix_next = 0;  // next free arrival counter (round robin over g_fix_cnt)
 
 // Position-major tiles with padding taps skipped (conv_fwd_kernel, g.posm):
-// for TAPU layers whose output is smaller than the kernel (every output pixel
-// then has padding-only taps), the batch a multiple of BM and no addend.
+// for TAPU layers whose output is smaller than twice the kernel (most output
+// pixels then have padding-only taps), the batch a multiple of BM and no
+// addend.  (8x8 outputs added in round 6: CIFAR layer-3 dgrad 27.2 -> 25.7 us,
+// 28 % of its taps read only the border; the per-tile work is then uneven, and
+// 4 splits to even it out lost, profiles/r6_posm8_ab.txt.)
 // set_conv_posm(0) = the pixel-major tiles (A/B).
 static int g_posm = 1;
 void set_conv_posm(int on) { g_posm = on ? 1 : 0; }
@@ -2199,7 +2202,7 @@ void set_conv_posm(int on) { g_posm = on ? 1 : 0; }
 template <int BM, int BN, bool TAPU, int ST, int WM, int WN>
 static void launch_fwd_w(ConvGeom& g, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
                          uintptr_t slab, int splits, hipStream_t s) {
-  g.posm = (g_posm && TAPU && !g_fwd_addend && g.B % BM == 0 && (g.H < g.KS || g.W < g.KS) && g.S == 1 && !g.om &&
+  g.posm = (g_posm && TAPU && !g_fwd_addend && g.B % BM == 0 && (g.H < 2 * g.KS || g.W < 2 * g.KS) && g.S == 1 && !g.om &&
             g.KH == g.KS && g.KW == g.KS && g.Hp == g.H + 2 * g.pad && g.Wp == g.W + 2 * g.pad) ? 1 : 0;
   const int ntm = (g.M + BM - 1) / BM, ntn = (g.Cout + BN - 1) / BN;
   const int nkt = (g.Kch + 7) / 8;

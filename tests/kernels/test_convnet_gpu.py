@@ -759,11 +759,11 @@ def test_executor_dgrad_bn_reduce_epilogue(C, monkeypatch, B, atomic):
 
 
 # (B, H, Cin, Cout, tile, splits): position-major tiles (batch a multiple of the
-# 128-row tile, output smaller than the 5x5 kernel): the reference's layer 4
+# 128-row tile, output smaller than twice the 5x5 kernel): the reference's layer 4
 # forward (4x4, 256 -> 512, split 4) and dgrad (512 -> 256, split 8), a 2x2
-# map, a 3x3 map (odd W), 128x64 tiles
+# map, a 3x3 map (odd W), 128x64 tiles, the layer-3 dgrad (8x8, 256 -> 128, split 2)
 POSM_SHAPES = [(128, 4, 256, 512, 0, 4), (128, 4, 512, 256, 0, 8), (128, 4, 256, 512, 0, 1), (256, 2, 128, 128, 0, 2),
-               (128, 3, 64, 128, 2, 3), (256, 4, 128, 64, 2, 1)]
+               (128, 3, 64, 128, 2, 3), (256, 4, 128, 64, 2, 1), (128, 8, 256, 128, 0, 2), (128, 8, 128, 256, 0, 1)]
 
 
 @pytest.mark.parametrize("shape", POSM_SHAPES)
