@@ -1639,7 +1639,14 @@ __device__ unsigned long long* g_wgrad_stamps = nullptr;
 template <int BM, int BN, int STAGES, int WM = 2, int WN = 2, int BK_ = 64>
 __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                          float* __restrict__ out, const ConvGeom g, int m_per_split,
-                                                         int ldo) {
+                                                         int ldo, const SgdJob side = SgdJob{}) {
+  // side job (set_conv_side_sgd, as conv_fwd_kernel): the last side.nblk
+  // workgroups run part of the step's SGD update beside the weight gradient
+  const int wg_grid = (int)gridDim.x - side.nblk;
+  if ((int)blockIdx.x >= wg_grid) {
+    sgd_side_block(side, (int)blockIdx.x - wg_grid);
+    return;
+  }
   // dy and x are both spatially zero-padded [B][Hp][Wp][C] (dy: interior at
   // (pad, pad)).  A 64-row M step starts at a multiple of 64 output pixels;
   // with W | 64 and (H*W | 64 or 64 | H*W) the padded position of row r of the
@@ -1673,7 +1680,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const bf16_t* 
   // same x pixels, different taps / channel tiles) get consecutive ids after
   // the swizzle, i.e. one XCD, so the split's rows are fetched into that XCD's
   // L2 once instead of once per XCD (wgrad1 15.3 -> 11.0 us, r2_wgrad_xcd_ab.txt)
-  const int id = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int id = xcd_swizzle(blockIdx.x, wg_grid);
   const int split = id / (ntm * ntn);
   const int tile = id - split * (ntm * ntn);
   const int tm = tile % ntm, tn = tile / ntm;
@@ -2172,7 +2179,7 @@ int conv_fwd_stat_rows(int B, int H, int W, int Cin, int Cout, int KS, int tile,
   return (g.M + rpb - 1) / rpb;
 }
 
-static SgdJob g_side_sgd{};         // set_conv_side_sgd: side SGD job of the next conv_fwd launch
+static SgdJob g_side_sgd{};         // set_conv_side_sgd: side SGD job of the next conv_fwd / conv_wgrad launch
 static uintptr_t g_fwd_addend = 0;  // conv_fwd_add: bf16 [M][Cout] added in the epilogue
 static uintptr_t g_fwd_addend_mask = 0;  // conv_fwd_add: optional uint8 [M][Cout/8] mask bits of the addend
 static int g_fwd_keep_slabs = 0;    // FwdCfg bit 20: leave the split-K slabs (the caller combines them)
@@ -2798,9 +2805,12 @@ static void conv_wgrad_g(const ConvGeom& g, uintptr_t dy, uintptr_t x, uintptr_t
   // wgrad1 22.1 -> 16.8 us vs 3 stages), 128x128 tiles (1 WG per CU, 128 KiB
   // LDS, 141 VGPRs: wgrad2/3/4 31.7/29.7/28.4 us as 128x64 -> 24.7/23.0/21.8 us;
   // the waves wait on the LDS-DMA ring, so the deeper ring wins over occupancy)
+  SgdJob side = g_side_sgd;  // one-shot: consumed by this launch
+  g_side_sgd.nblk = 0;
   auto go = [&](auto kern, int BM_, int BN_, int NT_) {
     const int nt = ((g.Cout + BM_ - 1) / BM_) * ((g.K + BN_ - 1) / BN_);
-    kern<<<nt * splits, NT_, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (float*)out, g, mps, ldo);
+    if (side.nblk < 0) side.nblk = (int)std::max<int64_t>(1, (side.hi4 - side.lo4 + NT_ - 1) / NT_);
+    kern<<<nt * splits + side.nblk, NT_, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (float*)out, g, mps, ldo, side);
   };
   if (tile == 2) go(conv_wgrad_kernel<128, 128, 4, 2, 4>, 128, 128, 512);
   else go(conv_wgrad_kernel<64, 64, 4, 2, 4>, 64, 64, 512);

@@ -466,8 +466,9 @@ def test_deferred_slab_reduce_is_bitwise(dev, monkeypatch, momentum):
     the stand-alone reduce (deterministic reduction mode; batch 128: 19 splits
     summed on 8 lanes + a shuffle tree, 5 sequentially, and the first layer's
     channel-padded 128 splits on 32 lanes in extra blocks of the launch);
-    with the side job, blocks 3-4 and the classifier are updated by extra
-    workgroups of block 3's dgrad launch -- still bitwise the same; and with
+    with the side jobs, blocks 3-4 and the classifier are updated by extra
+    workgroups of block 3's dgrad launch and block 2 by extra workgroups of
+    the first layer's weight-gradient launch -- still bitwise the same; and with
     the update launch preparing the next step of the unrolled graph (its
     batch gathered, accumulators zeroed, first-layer operand packed: the
     executor's arm_next_prep) -- still bitwise, across an epoch boundary."""
@@ -493,10 +494,12 @@ def test_deferred_slab_reduce_is_bitwise(dev, monkeypatch, momentum):
             assert blocks in ([0, 1, 2], [0, 1, 2, 3]), blocks
             ks = {e[0] // 4: e[2] for e in tr._slabs}
             assert ks[2] < 8 <= ks[1] < 32 <= ks[0], ks  # sequential, 8 lanes + tree, 32 lanes (padded tail)
-            # side == "1": blocks 3-4 + classifier updated inside block 3's dgrad launch
+            # side == "1": blocks 3-4 + classifier updated inside block 3's dgrad launch,
+            # block 2 inside the first layer's weight-gradient launch
             assert (tr._side is not None) == (side == "1")
             if side == "1":
-                assert tr._side == (tr.flat.offsets[8], tr.flat.total)
+                assert tr._side == (tr.flat.offsets[4], tr.flat.total)
+                assert tr.executor._side["w"]["range"] == (tr.flat.offsets[4], tr.flat.offsets[8])
         else:
             assert tr._slabs is None and tr._side is None
         assert tr.grads_materialized == (defer == "0")  # flat.grad is not written for deferred slabs

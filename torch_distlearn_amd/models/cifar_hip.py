@@ -229,6 +229,9 @@ class CifarHIPExecutor:
         # median of 10 interleaved runs against the channel-padded layer 1
         # (profiles/r6_pair1_x4_ab.txt)
         self.pair1 = True
+        # the update of blocks 1 .. side block - 1 rides the first layer's weight
+        # gradient launch (side_update); DISTLEARN_SIDE_WGRAD1=0: off
+        self.side_wgrad1 = os.environ.get("DISTLEARN_SIDE_WGRAD1", "1") == "1"
         self.atomic = self.mode > 0             # BN statistics / gradients by atomics, no finalize kernels
         # (mode 2) the last block's BN backward reduce runs inside the head kernel and
         # the classifier weight gradient rides the BN backward apply launch
@@ -567,6 +570,8 @@ class CifarHIPExecutor:
             tile, splits, direct = self.wplan[i]
             wtile = tile | (1 << 24) if i == 0 and self.pair1 else tile  # pair-packed layer 1 (csrc make_geom_pair)
             gw = self.g32[self._leaf(i, 0)]
+            if i == 0 and self._side is not None and self._side["w"] is not None:
+                self._arm_side(self._side["w"])  # this launch also updates blocks 1 .. side block - 1
             if direct:
                 C.conv_wgrad(dY.data_ptr(), xin.data_ptr(), gw.data_ptr(), B, h, h, kcin, cout, KSIZE, 1, K, wtile, 0, s)
             else:
@@ -678,12 +683,24 @@ class CifarHIPExecutor:
         if any(self.cins[i] != self.cins_real[i] for i in self._deferred if i >= block):
             return None
         slabs.sort()
-        self._side = {"block": block, "lr": lr_fn,
-                      "args": (base, f.grad.data_ptr(), 0 if mom is None else mom.data_ptr(), f.shadow.data_ptr(),
-                               0 if slot is None else slot.data_ptr()),
-                      "mw": (float(momentum), float(weight_decay)), "range": (lo, hi),
-                      "slabs": ([o for o, _, _, _ in slabs], [n for _, n, _, _ in slabs],
-                                [t for _, _, t, _ in slabs], [k for _, _, _, k in slabs])}
+        args = (base, f.grad.data_ptr(), 0 if mom is None else mom.data_ptr(), f.shadow.data_ptr(),
+                0 if slot is None else slot.data_ptr())
+        pack = lambda sl: ([o for o, _, _, _ in sl], [n for _, n, _, _ in sl],  # noqa: E731
+                           [t for _, _, t, _ in sl], [k for _, _, _, k in sl])
+        self._side = {"block": block, "lr": lr_fn, "args": args, "mw": (float(momentum), float(weight_decay)),
+                      "range": (lo, hi), "slabs": pack(slabs), "w": None}
+        # ... and the blocks before it down to block 1 ride the first layer's
+        # weight-gradient launch (the last launch before the update: every one of
+        # their gradients is final by then, csrc conv_wgrad_g side job), so the
+        # final update is left with block 0 and its slab tail
+        # (profiles/r6_side_wgrad1_ab.txt)
+        lo1 = f.offsets[self._leaf(1, 0)]
+        sl1 = [(f.offsets[self._leaf(i, 0)], f.numels[self._leaf(i, 0)], self.wslab_l[i].data_ptr(),
+                self.wplan[i][1]) for i in self._deferred if 1 <= i < block]
+        if block > 1 and self.side_wgrad1 and all(self.cins[i] == self.cins_real[i] for i in self._deferred
+                                                  if 1 <= i < block):
+            self._side["w"] = {"range": (lo1, lo), "slabs": pack(sorted(sl1))}
+            return lo1, hi
         return lo, hi
 
     def _dgrad_hosts_side_job(self, block: int) -> bool:
@@ -745,12 +762,13 @@ class CifarHIPExecutor:
     def _reduce_merged(self, s: int) -> None:
         self.C.slab_reduce_multi(*self._merged_args, s)
 
-    def _arm_side(self) -> None:
+    def _arm_side(self, job: Optional[dict] = None) -> None:
         sd = self._side
+        job = job or sd
         p, g, mom, p16, slot = sd["args"]
         mo, wd = sd["mw"]
-        lo, hi = sd["range"]
-        self.C.set_conv_side_sgd(p, g, mom, p16, slot, float(sd["lr"]()), mo, wd, lo, hi, *sd["slabs"],
+        lo, hi = job["range"]
+        self.C.set_conv_side_sgd(p, g, mom, p16, slot, float(sd["lr"]()), mo, wd, lo, hi, *job["slabs"],
                                  0)  # 0: one float4 per thread over the range
 
     def defer_slab_reduce(self):
