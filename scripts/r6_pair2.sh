@@ -1,4 +1,5 @@
 #!/bin/bash
+# (record of a finished A/B: its DISTLEARN_AB_* toggles were removed when the result was adopted)
 # Pair-packed first layer on the 4-channel input (forward + weight gradient):
 # GPU tests, a kernel profile and an interleaved step A/B against the
 # channel-padded layer 1 (DISTLEARN_AB_PAIR1=0).

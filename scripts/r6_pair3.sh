@@ -1,4 +1,5 @@
 #!/bin/bash
+# (record of a finished A/B: its DISTLEARN_AB_* toggles were removed when the result was adopted)
 # Layer-1 weight-gradient split count on the pair-packed layout (256 = the
 # plan, 128) vs the channel-padded layer 1, with 8-deep slab-reduce batches.
 set -o pipefail

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (record of a finished A/B: its DISTLEARN_AB_* toggles were removed when the result was adopted)
 # Position-major tiles (padding taps skipped) extended to the 8x8 layer-3
 # dgrad: correctness check, kernel profile and interleaved step A/B.
 set -o pipefail

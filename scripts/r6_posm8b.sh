@@ -1,4 +1,5 @@
 #!/bin/bash
+# (record of a finished A/B: its DISTLEARN_AB_* toggles were removed when the result was adopted)
 # Layer-3 dgrad on position-major tiles: 2 vs 4 splits (posm=2), vs pixel-major 2 splits.
 set -o pipefail
 mkdir -p gpurun_out; export TMPDIR=/tmp
