@@ -40,7 +40,8 @@ from ..parallel.comm import runs_collectives
 from .cifar_convnet import BN_EPS, BN_MOMENTUM, KSIZE, CifarConvNet
 
 BF16 = torch.bfloat16
-CIN_PAD = 8  # the 3-channel input layer is zero-padded to 8 channels (one 16-B vector per tap)
+CIN_PAD = 8  # the 3-channel input layer zero-padded to 8 channels (one 16-B vector per tap); the default
+#              pair-packed layer 1 reads a 4-channel input instead (CifarHIPExecutor.kin0, pair1)
 SPAD = KSIZE // 2  # spatial zero border of every convolution input (written once, never touched)
 
 # tile ids of conv_fwd: 0 = 128x128, 1 = 64x64, 2 = 128x64 (BK = 64) ; conv_wgrad: 1 = 64x64, 2 = 128x128
