@@ -73,7 +73,7 @@ def parse():
                     help="1 = run the MULTI-NODE step configuration on one GPU (diagnostic, not the headline): the "
                          "bucket all-reduces go through RCCL at world 1 (DISTLEARN_RCCL_WORLD1=1), so the trainer "
                          "materialises every gradient for them (no one-node slab deferral / side SGD), the executor "
-                         "takes its overlap policy (both candidates timed and reported unless DISTLEARN_POLICY "
+                         "takes its overlap policy (every candidate timed and reported unless DISTLEARN_POLICY "
                          "forces one)")
     ap.add_argument("--hold-cus", type=int, default=0,
                     help="with --nworld-path: hold R CUs during the timed region with workgroups of RCCL's "
@@ -395,7 +395,7 @@ def main():
         "grad_comm_dtype": getattr(tr, "grad_comm_dtype", "fp32") if not is_server else "fp32",
         "delta_wire": a.grad_comm_dtype if a.algo == "async" else None,
         # world > 1: the overlap policy measured on this machine during warm-up
-        # (engine.py select_policy: both candidates' ms per step, max over ranks)
+        # (engine.py select_policy: every candidate's ms per step, max over ranks)
         "policy": getattr(tr, "policy", None) if not is_server else None,
     }
     if a.nworld_path:

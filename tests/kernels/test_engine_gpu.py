@@ -526,7 +526,7 @@ def test_policy_selected_on_the_machine(dev, monkeypatch):
     tr.prepare(ld, 4)
     torch.cuda.synchronize()
     pol = tr.policy
-    names = {f"{p}@{c}" for p in ("full", "reserve") for c in (16, 32)}  # x the measured channel caps
+    names = {f"{p}@{c}" for p in ("full", "reserve", "wreserve") for c in (16, 32)}  # x the measured channel caps
     assert pol is not None and pol["chosen"] in names, pol
     assert set(pol["ms_per_step"]) == names and all(v > 0 for v in pol["ms_per_step"].values())
     assert pol["chosen"] == min(pol["ms_per_step"], key=pol["ms_per_step"].get)

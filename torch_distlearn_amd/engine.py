@@ -458,14 +458,14 @@ class DataParallelTrainer:
         graph is captured (README "Compute / all-reduce co-residency").  With
         world > 1 the bucketed all-reduce runs beside the backward convs and
         RCCL's workgroups hold CUs; the candidates are the executor's
-        ``policies()`` -- full-chip grids with 3-stage dgrads vs wgrad grids
-        that leave the channel cap of CUs free with 2-stage dgrads.  Each is
+        ``policies()`` -- full-chip grids with 3-stage dgrads, wgrad grids
+        that leave the channel cap of CUs free with 2- or 3-stage dgrads.  Each is
         captured as a one-step graph and replayed ``reps`` times, timed with
         HIP events, training state restored; every rank takes the policy
         whose slowest rank is fastest (:func:`agree_on_policy`).  Runs once;
         ``DISTLEARN_POLICY=<name>`` forces a candidate, one node keeps the
         executor default unless ``DISTLEARN_POLICY_SELECT=1``.  The choice
-        and both timings land in :attr:`policy` (bench.py's JSON config).
+        and every timing lands in :attr:`policy` (bench.py's JSON config).
 
         With an RCCL communicator whose collectives run, the candidates are
         also crossed with the channel caps of

@@ -637,7 +637,8 @@ class CifarHIPExecutor:
         (world > 1): "full" = full-chip grids and 3-stage dgrads (fastest when
         nothing else holds a CU), "reserve" = 2-stage dgrads and wgrad grids
         that leave the RCCL channel cap of CUs free (what the single-CU
-        emulation favoured).  Empty when DISTLEARN_DGRAD_STAGES /
+        emulation favoured), "wreserve" = those wgrad grids with 3-stage
+        dgrads.  Empty when DISTLEARN_DGRAD_STAGES /
         DISTLEARN_CU_RESERVE pin the policy."""
         if "DISTLEARN_DGRAD_STAGES" in os.environ or "DISTLEARN_CU_RESERVE" in os.environ:
             return {}
@@ -645,7 +646,11 @@ class CifarHIPExecutor:
 
         comm = getattr(self.bucketer, "comm", None)
         cap = getattr(comm, "cu_reserve", 0) or rccl_channel_cap()
-        return {"full": {"dgrad_stages": 3, "cu_reserve": 0}, "reserve": {"dgrad_stages": 2, "cu_reserve": int(cap)}}
+        # "wreserve": the wgrad grids leave the cap free, the dgrads keep 3 stages -- with
+        # 32 CUs held on one GPU 0.3297-0.3300 ms/step vs full 0.3543-0.3619 and reserve
+        # 0.3362-0.3380 (profiles/r6_nworld_policy_hold.txt)
+        return {"full": {"dgrad_stages": 3, "cu_reserve": 0}, "reserve": {"dgrad_stages": 2, "cu_reserve": int(cap)},
+                "wreserve": {"dgrad_stages": 3, "cu_reserve": int(cap)}}
 
     def set_policy(self, dgrad_stages: int, cu_reserve: int) -> None:
         """Switch the overlap policy (re-plans the weight-gradient grids and
