@@ -60,7 +60,7 @@ def test_ranks_agree_on_the_fastest_slowest_rank(world):
         assert pol["chosen"] == want and pol["ms_per_step"] == pytest.approx(want_table)
         assert r["again"]
         # both candidates measured (sorted order), then the winner set for good
-        assert r["seen"] == [(3, 0), (2, 32)] and r["calls"][-1] == (2, 32)
+        assert r["seen"] == [(3, 0), (2, 32), (2, 32), (3, 0)] and r["calls"][-1] == (2, 32)  # 2 passes
 
 
 def _forced_worker(rank, world, port):
@@ -134,7 +134,8 @@ def test_channel_cap_is_measured_with_the_policy(world):
         assert set(pol["ms_per_step"]) == {"full@16", "reserve@16", "full@32", "reserve@32"}
         assert pol["chosen"] == "reserve@16" and pol["channel_cap"] == 16 and r["cap"] == 16
         assert r["final"] == (2, 16)
-        assert r["seen"] == [(3, 0, 16), (2, 16, 16), (3, 0, 32), (2, 32, 32)]
+        fwd = [(3, 0, 16), (2, 16, 16), (3, 0, 32), (2, 32, 32)]
+        assert r["seen"] == fwd + fwd[::-1]  # two passes, the second reversed
         assert r["rebuilt"] == [16, 32, 16]  # one rebuild per cap, then back to the winner's
         assert pol["candidates"]["reserve@32"] == {"dgrad_stages": 2, "cu_reserve": 32, "channel_cap": 32}
 

@@ -497,13 +497,20 @@ class DataParallelTrainer:
                 self._apply_candidate(*next(iter(cands.values())))
             return self.policy
         local = {}
-        # caps outermost: the communicator is rebuilt once per cap
-        for name, (kw, cap) in sorted(cands.items(), key=lambda it: (it[1][1] or 0, it[0])):
+        # caps outermost: the communicator is rebuilt once per cap; a second pass in
+        # reverse order, each candidate keeping its faster pass, so the clock warm-up
+        # of the first candidates does not favour the last ones (one GPU, no CU held:
+        # one pass chose wreserve@32, timed last, in 3 of 3 runs although full ran
+        # 0.5-1 % faster, profiles/r6_nworld_policy_hold.txt)
+        order = sorted(cands.items(), key=lambda it: (it[1][1] or 0, it[0]))
+        for name, (kw, cap) in order + order[::-1]:
             self._apply_candidate(kw, cap)
-            local[name] = self._time_step_graph(loader, reps)
+            ms = self._time_step_graph(loader, reps)
+            local[name] = min(ms, local.get(name, ms))
         name, table = agree_on_policy(self.tree.comm, local)
         self._apply_candidate(*cands[name])
-        self.policy = {"chosen": name, "ms_per_step": table, "how": f"measured ({reps} graph replays per policy)",
+        self.policy = {"chosen": name, "ms_per_step": table,
+                       "how": f"measured (2 passes x {reps} graph replays per policy)",
                        "candidates": {n: dict(kw, **({"channel_cap": cap} if cap else {}))
                                       for n, (kw, cap) in cands.items()}, **self._cap_record()}
         return self.policy
